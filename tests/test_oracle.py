@@ -1,0 +1,110 @@
+"""Pins the CPU restatement (oracle/) against the reference's own known answers.
+
+Every expected value below is read from tests/golden/reference_known_answers.json, which
+transcribes the reference's gtest assertions (file:line in that JSON).
+"""
+import numpy as np
+
+from oracle import oracle as O
+
+
+def _rev(a):
+    return np.array([O.reverse_bytes(int(x)) for x in a], dtype=np.uint64)
+
+
+def test_reverse_bytes_involution():
+    # tests/cpp/localizer_test.cc:56-63
+    mx = (1 << 64) - 1
+    n = 1000
+    for i in range(n):
+        j = (mx // n) * i
+        assert O.reverse_bytes(O.reverse_bytes(j)) == j
+
+
+def test_localizer_base(rcv1, known):
+    k = known["localizer_base"]
+    uniq, cnt, col = O.localize(rcv1.offs, rcv1.ids)
+    assert int(_rev(uniq).sum()) == k["sum_uidx"]
+    assert float(cnt.sum()) == k["sum_freq"]
+    assert np.all(np.diff(uniq.astype(np.float64)) >= 0) and np.all(uniq[1:] != uniq[:-1])
+    # compacted block keeps every nnz: the remapped column points at its own key
+    assert np.array_equal(uniq[col], _rev_keys(rcv1.ids))
+
+
+def _rev_keys(ids, max_index=(1 << 64) - 1):
+    return np.array([O.reverse_bytes(int(i) % max_index) for i in ids], dtype=np.uint64)
+
+
+def test_localizer_hash(rcv1, known):
+    k = known["localizer_hash1000"]
+    uniq, cnt, col = O.localize(rcv1.offs, rcv1.ids, max_index=k["max_index"])
+    assert int(_rev(uniq).sum()) == k["sum_uidx"]
+    assert float(cnt.sum()) == k["sum_freq"]
+
+
+def _fm_weights(uidx, d):
+    U = len(uidx)
+    W = np.zeros(U * (d + 1), np.float32)
+    wp = (np.arange(U) * (d + 1)).astype(np.int32)
+    for i in range(U):
+        W[i * (d + 1)] = uidx[i] / 5e4
+        for j in range(1, d + 1):
+            W[i * (d + 1) + j] = uidx[i] * j / 5e5
+    return W, wp, wp + 1
+
+
+def test_fmloss_nov(rcv1, known):
+    k = known["fmloss_nov"]
+    uniq, _, col = O.localize(rcv1.offs, rcv1.ids)
+    w = (_rev(uniq) / 5e4).astype(np.float32)
+    pred = O.fm_predict(rcv1.offs, col, rcv1.vals, w, None, None, 0)
+    assert abs(O.evaluate(rcv1.labels, pred) - k["objv"]) < k["objv_tol"]
+    g = O.fm_calcgrad(rcv1.offs, col, rcv1.vals, rcv1.labels, None, w, None, None, len(uniq), 0,
+                      pred)
+    assert abs(float((g.astype(np.float64) ** 2).sum()) - k["grad_norm2"]) < k["grad_tol"]
+
+
+def test_fmloss_hasv(rcv1, known):
+    k = known["fmloss_hasv"]
+    d = k["V_dim"]
+    uniq, _, col = O.localize(rcv1.offs, rcv1.ids)
+    W, wp, vp = _fm_weights(_rev(uniq), d)
+    pred = O.fm_predict(rcv1.offs, col, rcv1.vals, W, wp, vp, d)
+    assert abs(O.evaluate(rcv1.labels, pred) - k["objv"]) < k["objv_tol"]
+    g = O.fm_calcgrad(rcv1.offs, col, rcv1.vals, rcv1.labels, None, W, wp, vp, len(uniq), d, pred)
+    assert abs(float((g.astype(np.float64) ** 2).sum()) - k["grad_norm2"]) < k["grad_tol"]
+
+
+def test_sgd_learner_basic(rcv1, known):
+    k = known["sgd_learner_basic"]
+    kw = k["kwargs"]
+    up = O.Updater(V_dim=kw["V_dim"], l2=kw["l2"], l1=kw["l1"], lr=kw["lr"])
+    for ep, want in enumerate(k["objv"]):
+        loss, _ = up.train_step(rcv1.offs, rcv1.ids, rcv1.vals, rcv1.labels)
+        assert abs(loss - want) < k["tol"], (ep, loss, want)
+
+
+def test_rand_r_is_glibc_lcg():
+    """InitV's rand_r (sgd_updater.cc:148): 3 LCG steps per call, a=1103515245, c=12345."""
+    seq, _ = O.rand_r_seq(0, 50)
+    s = 0
+    for want in seq:
+        r = 0
+        for shift, mod in ((0, 2048), (10, 1024), (10, 1024)):
+            s = (s * 1103515245 + 12345) & 0xFFFFFFFF
+            r = (r << shift) ^ ((s >> 16) % mod)
+        assert r == want
+
+
+def test_save_load_roundtrip(rcv1, tmp_path):
+    up = O.Updater(V_dim=4, V_threshold=2, lr=.1, V_lr=.01, l1=.1)
+    for ep in range(3):
+        up.train_step(rcv1.offs, rcv1.ids, rcv1.vals, rcv1.labels, push_cnt=(ep == 0))
+    path = str(tmp_path / "model")
+    up.save(path, True)
+    up2 = O.Updater(V_dim=4)
+    up2.load(path)
+    uniq, _, _ = O.localize(rcv1.offs, rcv1.ids)
+    a, la = up.get(uniq)
+    b, lb = up2.get(uniq)
+    assert np.array_equal(a, b) and np.array_equal(la, lb)
