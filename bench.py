@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — train examples/sec of DiFacto's FM (V_dim=16) hot path on MI355X.
+
+Workload (BASELINE.json configs[2]): Criteo-shaped synthetic data,
+39 binary nnz per row, feature ids ~ U[0, 2^24), labels +1 w.p. 0.25; FM V_dim=16 with the
+throughput settings l1=0, V_threshold=0 (every key carries V once touched), lr=.1,
+V_lr=.01; B=100,000 rows per GPU per step.
+
+A "step" is one minibatch through the whole per-batch hot path of SGDLearner::IterateData
+(sgd_learner.cc:201-317): Localizer (sort/unique/remap) -> pull -> FM forward -> Evaluate
+-> AUC -> FM backward -> FTRL/AdaGrad push (+ InitV), as ONE dfx_train_step on device-resident
+input.  Before timing, one untimed "epoch 0" pass over the key space pushes feature counts
+(kFeaCount) so the model is in its steady state (every key has V); then W warmup steps and K
+timed steps run on fresh batches (epoch >= 1, no count push), as in the reference.
+
+Prints one JSON line (driver contract) with a roofline object for the dominant kernel and a
+cpu_baseline (the oracle restatement timed on this host on a bounded sample).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=100_000, help="rows per GPU per step")
+    ap.add_argument("--nnz", type=int, default=39)
+    ap.add_argument("--key-bits", type=int, default=24)
+    ap.add_argument("--vdim", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=200_000)
+    ap.add_argument("--cpu-batch", type=int, default=10_000)
+    return ap.parse_args()
+
+
+class DevBatch:
+    """A synthetic RowBlock generated directly in HBM (torch is only the allocator/RNG)."""
+
+    def __init__(self, torch, dev, B, k, key_bits, seed):
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed)
+        self.size = B
+        self.nnz = B * k
+        self.ids = torch.randint(0, 1 << key_bits, (self.nnz,), device=dev, generator=g,
+                                 dtype=torch.int64)
+        self.offs = torch.arange(0, self.nnz + 1, k, device=dev, dtype=torch.int64)
+        r = torch.rand(B, device=dev, generator=g)
+        self.labels = torch.where(r < 0.25, 1.0, -1.0).to(torch.float32)
+        self.vals = None
+        self.weights = None
+
+    def as_batch(self):
+        from difacto_amd import _lib
+        import ctypes
+        return _lib.Batch(self.size, self.nnz, ctypes.c_void_p(self.offs.data_ptr()),
+                          ctypes.c_void_p(self.ids.data_ptr()), None,
+                          ctypes.c_void_p(self.labels.data_ptr()), None)
+
+
+def algorithmic_bytes(B, nnz, U, d):
+    """Essential HBM bytes per launch, binary data, all V live."""
+    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (4 + 8 + 4 * d)
+    bwd = U * (8 + 4 + 8 + 32 + 16 * d + 4) + nnz * (4 + 4 + 4 + 4 * d)
+    return {"forward": fwd, "backward_update": bwd}
+
+
+def cpu_baseline(args):
+    """The oracle (scalar C++ restatement, 1 thread) on a bounded sample of the same workload:
+    epoch 0 (count push, untimed) then a timed epoch over the same rows (steady state)."""
+    from difacto_amd import data as D
+    from oracle import oracle as O
+    O.build()
+    up = O.Updater(V_dim=args.vdim, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    nb = max(1, args.cpu_rows // args.cpu_batch)
+    blocks = [D.synthetic(args.cpu_batch, args.nnz, 1 << args.key_bits, seed=1000 + i)
+              for i in range(nb)]
+    for b in blocks:
+        up.train_step(b.offs, b.ids, b.vals, b.labels, push_cnt=True)
+    t0 = time.perf_counter()
+    for b in blocks:
+        up.train_step(b.offs, b.ids, b.vals, b.labels, push_cnt=False)
+    dt = time.perf_counter() - t0
+    return {"value": round(nb * args.cpu_batch / dt, 1), "unit": "train examples/sec",
+            "cores": 1, "kind": "port",
+            "sample": "%d rows (%d batches of %d), Criteo-shaped C3, steady-state epoch 2 after a "
+                      "count-push epoch; oracle/oracle.cc full hot path incl. Localizer/AUC, "
+                      "1 thread" % (nb * args.cpu_batch, nb, args.cpu_batch)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from difacto_amd import hotpath as H
+    import ctypes
+
+    B, k, kb, d = args.batch, args.nnz, args.key_bits, args.vdim
+    keyspace = 1 << kb
+    ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
+                    max_keys=keyspace, max_vrows=keyspace)
+    ctx.reserve(B, B * k)
+    lib = H._lib.lib()
+
+    def step(batch, push_cnt):
+        b = batch.as_batch()
+        H.check(lib.dfx_train_step(ctx.h, ctypes.byref(b), H.kTraining, int(push_cnt),
+                                   ctypes.c_uint64(H.MAX_INDEX), None))
+
+    # untimed epoch 0: touch the key space with count pushes (all keys end up with V)
+    n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (B * k)))
+    for i in range(n_warm_epoch):
+        step(DevBatch(torch, dev, B, k, kb, seed=1_000_000 * (rank + 1) + i), True)
+    torch.cuda.synchronize()
+    H.progress(ctx)
+    for i in range(args.warmup):
+        step(DevBatch(torch, dev, B, k, kb, seed=2_000_000 * (rank + 1) + i), False)
+    batches = [DevBatch(torch, dev, B, k, kb, seed=3_000_000 * (rank + 1) + i)
+               for i in range(args.steps)]
+    torch.cuda.synchronize()
+    H.prof_read(ctx)
+    H.progress(ctx)
+    H.prof_enable(ctx, args.steps)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for bt in batches:
+        step(bt, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    phases, nrec, mean_u = H.prof_read(ctx)
+    prog = H.progress(ctx)
+    ctx.sync()
+    st = H.Store(ctx).stats()
+
+    value = world * B * args.steps / elapsed
+    per_launch_ms = {p: phases[p] / max(nrec, 1) for p in phases}
+    ab = algorithmic_bytes(B, B * k, mean_u, d)
+    dom = max(ab, key=lambda p: per_launch_ms[p])
+    achieved = ab[dom] / (per_launch_ms[dom] * 1e-3) / 1e9
+    out = {
+        "metric": "train examples/sec (FM V_dim=16) at 1/8 GPU + achieved HBM GB/s",
+        "value": round(value, 1),
+        "unit": "train examples/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (device-generated, resident in HBM before timing)",
+        "config": {"workload": "C3 Criteo-shaped FM V_dim=%d, %d binary nnz/row, 2^%d keys, "
+                               "l1=0 V_threshold=0, fused dfx_train_step" % (d, k, kb),
+                   "rows_per_gpu_step": B, "global_batch": B * world,
+                   "parallelism": "dp%d replicas" % world if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None,
+                     "algorithmic_bytes_per_launch": int(ab[dom]),
+                     "launch_ms": round(per_launch_ms[dom], 4)},
+        "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
+        "mean_unique_keys": round(mean_u, 1),
+        "train_loss_per_row": round(prog["loss"] / max(prog["nrows"], 1), 6),
+        "train_auc": round(prog["auc"] / max(prog["nrows"], 1), 6),
+        "model_keys": st["n_keys"], "model_vrows": st["n_vrows"],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,96 @@
+"""ctypes binding of libdifacto_amd.so (the C-ABI declared in include/difacto_amd.h).
+
+torch is imported BEFORE the library is opened: libdifacto_amd.so needs
+``libamdhip64.so.7`` and, with torch already loaded, the dynamic loader resolves it to
+torch's copy, so the library, torch tensors and torch streams share one HIP runtime.
+There is no fallback: a missing library raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede CDLL, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdifacto_amd.so")
+
+_lib = None
+
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+vp = ctypes.c_void_p
+i64p = ctypes.POINTER(ctypes.c_int64)
+f64p = ctypes.POINTER(ctypes.c_double)
+
+
+class DfxError(RuntimeError):
+    pass
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("size", c_i64), ("nnz", c_i64), ("offset", vp), ("index", vp), ("value", vp),
+                ("label", vp), ("weight", vp)]
+
+
+class Progress(ctypes.Structure):
+    _fields_ = [("nrows", ctypes.c_double), ("loss", ctypes.c_double), ("auc", ctypes.c_double),
+                ("penalty", ctypes.c_double), ("nnz_w", ctypes.c_double)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "dfx_last_error": (ctypes.c_char_p, []),
+    "dfx_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(vp)]),
+    "dfx_ctx_destroy": (ctypes.c_int, [vp]),
+    "dfx_ctx_set_stream": (ctypes.c_int, [vp, vp]),
+    "dfx_ctx_vdim": (ctypes.c_int, [vp]),
+    "dfx_sync": (ctypes.c_int, [vp]),
+    "dfx_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
+    "dfx_free": (ctypes.c_int, [vp, vp]),
+    "dfx_memcpy": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, ctypes.c_int]),
+    "dfx_reserve": (ctypes.c_int, [vp, c_i64, c_i64]),
+    "dfx_localize": (ctypes.c_int, [vp, c_i64, c_i64, vp, vp, c_u64, vp, vp, vp, i64p]),
+    "dfx_fm_predict": (ctypes.c_int, [vp, c_i64, c_i64, vp, vp, vp, vp, vp, vp, c_i64,
+                                      ctypes.c_int, vp]),
+    "dfx_fm_calcgrad": (ctypes.c_int, [vp, c_i64, c_i64, vp, vp, vp, vp, vp, vp, vp, vp, c_i64,
+                                       ctypes.c_int, vp, vp]),
+    "dfx_get_pos": (ctypes.c_int, [vp, c_i64, vp, vp, vp]),
+    "dfx_evaluate": (ctypes.c_int, [vp, c_i64, vp, vp, f64p]),
+    "dfx_auc": (ctypes.c_int, [vp, c_i64, vp, vp, f64p]),
+    "dfx_store_pull": (ctypes.c_int, [vp, vp, c_i64, vp, vp, i64p]),
+    "dfx_store_push": (ctypes.c_int, [vp, vp, c_i64, ctypes.c_int, vp, c_i64, vp]),
+    "dfx_store_save": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int]),
+    "dfx_store_load": (ctypes.c_int, [vp, ctypes.c_char_p]),
+    "dfx_store_dump": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
+    "dfx_store_stats": (ctypes.c_int, [vp, i64p, i64p, f64p, ctypes.POINTER(ctypes.c_uint32)]),
+    "dfx_store_evaluate": (ctypes.c_int, [vp, f64p, i64p]),
+    "dfx_store_reserve": (ctypes.c_int, [vp, c_i64, c_i64]),
+    "dfx_store_entry": (ctypes.c_int, [vp, c_u64, vp, vp, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)]),
+    "dfx_train_step": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.c_int, ctypes.c_int,
+                                      c_u64, vp]),
+    "dfx_progress_read": (ctypes.c_int, [vp, ctypes.POINTER(Progress), ctypes.c_int]),
+    "dfx_prof_enable": (ctypes.c_int, [vp, ctypes.c_int]),
+    "dfx_prof_read": (ctypes.c_int, [vp, f64p, ctypes.POINTER(ctypes.c_int), f64p]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DfxError("libdifacto_amd.so is not built (%s); run `make` at the repo root"
+                           % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().dfx_last_error()
+        raise DfxError("libdifacto_amd: status %d: %s" % (rc, msg.decode() if msg else "?"))

@@ -1,0 +1,200 @@
+// Device helpers shared by the gfx950 kernels: wave64 scans, key scrambling, the device
+// hash table view, glibc rand_r restated as an LCG with jump-ahead.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dfx {
+
+constexpr int kWave = 64;
+constexpr uint64_t kEmptyKey = ~0ull;  // never produced by the Localizer
+
+// include/difacto/base.h:39-51 — nibble reversal (involution).
+__host__ __device__ inline uint64_t reverse_bytes(uint64_t x) {
+  x = x << 32 | x >> 32;
+  x = (x & 0x0000FFFF0000FFFFull) << 16 | (x & 0xFFFF0000FFFF0000ull) >> 16;
+  x = (x & 0x00FF00FF00FF00FFull) << 8 | (x & 0xFF00FF00FF00FF00ull) >> 8;
+  x = (x & 0x0F0F0F0F0F0F0F0Full) << 4 | (x & 0xF0F0F0F0F0F0F0F0ull) >> 4;
+  return x;
+}
+
+__device__ inline int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ inline uint64_t lanemask_lt() {
+  const int l = lane_id();
+  return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// inclusive scan over the 64 lanes of a wave
+__device__ inline uint32_t wave_incl_scan(uint32_t v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    uint32_t t = __shfl_up(v, off, kWave);
+    if (l >= off) v += t;
+  }
+  return v;
+}
+
+// exclusive scan over a block of NT threads; lds needs NT/64 + 1 words.
+template <int NT>
+__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
+  constexpr int NW = NT / kWave;
+  const int w = threadIdx.x / kWave;
+  uint32_t inc = wave_incl_scan(v);
+  if (lane_id() == kWave - 1) lds[w] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int i = 0; i < NW; ++i) { uint32_t t = lds[i]; lds[i] = run; run += t; }
+    lds[NW] = run;
+  }
+  __syncthreads();
+  uint32_t r = lds[w] + inc - v;
+  if (total) *total = lds[NW];
+  __syncthreads();
+  return r;
+}
+
+// ---- glibc rand_r (stdlib/rand_r.c): three LCG steps per call ------------------------
+constexpr uint32_t kLcgA = 1103515245u, kLcgC = 12345u;
+
+// (A, C) such that stepping the LCG m times maps s -> A*s + C (mod 2^32).
+__host__ __device__ inline void lcg_jump(uint64_t m, uint32_t* A, uint32_t* C) {
+  uint32_t ra = 1, rc = 0, ca = kLcgA, cc = kLcgC;
+  while (m) {
+    if (m & 1) { ra = ca * ra; rc = ca * rc + cc; }
+    cc = ca * cc + cc;
+    ca = ca * ca;
+    m >>= 1;
+  }
+  *A = ra; *C = rc;
+}
+
+__host__ __device__ inline uint32_t lcg_advance(uint32_t s, uint64_t steps) {
+  uint32_t A, C;
+  lcg_jump(steps, &A, &C);
+  return A * s + C;
+}
+
+__host__ __device__ inline int rand_r_dev(uint32_t* seed) {
+  uint32_t next = *seed;
+  int result;
+  next = next * kLcgA + kLcgC;
+  result = (int)((next >> 16) % 2048u);
+  next = next * kLcgA + kLcgC;
+  result = (int)(((uint32_t)result << 10) ^ ((next >> 16) % 1024u));
+  next = next * kLcgA + kLcgC;
+  result = (int)(((uint32_t)result << 10) ^ ((next >> 16) % 1024u));
+  *seed = next;
+  return result;
+}
+
+// InitV's draw (sgd_updater.cc:148): (float)(((float)r / (float)RAND_MAX - 0.5) * scale)
+__host__ __device__ inline float initv_value(int r, float scale) {
+  float q = (float)r / 2147483648.0f;  // (real_t)RAND_MAX == 2^31 in float
+  return (float)(((double)q - 0.5) * (double)scale);
+}
+
+// ---- device hash table view (open addressing, linear probing) ------------------------
+struct Table {
+  uint64_t* keys;   // cap, kEmptyKey == free
+  float4* st;       // cap: {w, sqrt_g, z, fea_cnt}
+  int32_t* vrow;    // cap: V pool row or -1
+  float* V;         // vcap * d
+  float* Vaux;      // vcap * d (AdaGrad accumulators)
+  uint64_t mask;    // cap - 1
+  int logcap;
+  int d;
+  int64_t vcap;
+};
+
+__device__ inline uint64_t tbl_hash(uint64_t k, int logcap) {
+  return (k * 0x9E3779B97F4A7C15ull) >> (64 - logcap);
+}
+
+__device__ inline int64_t tbl_find(const Table& t, uint64_t k) {
+  uint64_t h = tbl_hash(k, t.logcap);
+  for (uint64_t probe = 0; probe <= t.mask; ++probe) {
+    uint64_t kk = t.keys[h];
+    if (kk == k) return (int64_t)h;
+    if (kk == kEmptyKey) return -1;
+    h = (h + 1) & t.mask;
+  }
+  return -1;
+}
+
+// find-or-insert; -1 when the table is full.  Keys of one launch must be distinct.
+// Fresh slots already hold zero state and vrow -1 (the table is never compacted), which is
+// what `model_[key]` default-constructs (sgd_updater.h:20-34).
+__device__ inline int64_t tbl_insert(const Table& t, uint64_t k, bool* inserted) {
+  uint64_t h = tbl_hash(k, t.logcap);
+  *inserted = false;
+  for (uint64_t probe = 0; probe <= t.mask; ++probe) {
+    uint64_t kk = t.keys[h];
+    if (kk == k) return (int64_t)h;
+    if (kk == kEmptyKey) {
+      unsigned long long old = atomicCAS((unsigned long long*)&t.keys[h],
+                                         (unsigned long long)kEmptyKey, (unsigned long long)k);
+      if (old == kEmptyKey) { *inserted = true; return (int64_t)h; }
+      if (old == k) return (int64_t)h;
+    }
+    h = (h + 1) & t.mask;
+  }
+  return -1;
+}
+
+// device-side error word bits (checked at dfx_sync)
+enum : int {
+  kErrTableFull = 1,
+  kErrPoolFull = 2,
+  kErrLens = 4,
+  kErrNoV = 8,
+};
+
+struct Params {
+  float l1, l2, V_l2, lr, lr_beta, V_lr, V_lr_beta, V_init_scale;
+  int V_dim, V_threshold;
+  int l1_shrk;
+};
+
+// SGDUpdater::UpdateW (sgd_updater.cc:105-131), exact float expression order.
+// Returns +1 / -1 / 0 for the new_w statistic; *transition is set on a 0 -> nonzero move.
+__device__ inline int ftrl_update(const Params& P, float gw, float4* e, bool* transition) {
+  float sg = e->y;
+  float w = e->x;
+  gw += w * P.l2;
+  float nsg = sqrtf(sg * sg + gw * gw);
+  e->y = nsg;
+  e->z -= gw - (nsg - sg) / P.lr * w;
+  float z = e->z;
+  float l1 = P.l1;
+  if (z <= l1 && z >= -l1) {
+    e->x = 0;
+  } else {
+    float eta = (P.lr_beta + nsg) / P.lr;
+    e->x = (z > 0 ? z - l1 : z + l1) / eta;
+  }
+  *transition = false;
+  if (w == 0 && e->x != 0) { *transition = true; return 1; }
+  if (w != 0 && e->x == 0) return -1;
+  return 0;
+}
+
+// SGDUpdater::UpdateV (sgd_updater.cc:133-142) for one coordinate.
+__device__ inline void adagrad_update(const Params& P, float gV, float* v, float* cg) {
+  float g = gV + P.V_l2 * (*v);
+  float c = *cg;
+  float nc = sqrtf(c * c + g * g);
+  *cg = nc;
+  float eta = P.V_lr / (nc + P.V_lr_beta);
+  *v -= eta * g;
+}
+
+__host__ __device__ inline int next_pow2_lanes(int d) {
+  int g = 1;
+  while (g < d && g < 64) g <<= 1;
+  return g;
+}
+
+}  // namespace dfx

@@ -1,0 +1,235 @@
+// Context lifecycle, .conf-key parsing, device memory helpers and error plumbing.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+#include "internal.h"
+
+namespace dfx {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int DevBuf::ensure(size_t n) {
+  if (n == 0) n = 16;
+  if (n <= bytes) return DFX_OK;
+  if (p) {
+    DFX_HIP(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+  }
+  size_t want = n + n / 4;  // headroom so ragged batches do not reallocate each step
+  DFX_HIP(hipMalloc(&p, want));
+  bytes = want;
+  return DFX_OK;
+}
+
+void DevBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+// SGDUpdaterParam / FMLossParam defaults (sgd_param.h:109-122, fm_loss.h:25)
+static void default_params(Params* P) {
+  P->l1 = 1; P->l2 = 0; P->V_l2 = .01f; P->lr = .01f; P->lr_beta = 1; P->V_lr = .01f;
+  P->V_lr_beta = 1; P->V_init_scale = .01f; P->V_dim = 0; P->V_threshold = 10; P->l1_shrk = 1;
+}
+
+struct Kw {
+  Params P;
+  unsigned seed = 0;
+  long long max_keys = 1ll << 22;
+  long long max_vrows = -1;
+  int loss_fm = 1;
+};
+
+static int parse_kwargs(const char* kwargs, Kw* kw) {
+  default_params(&kw->P);
+  if (!kwargs) return DFX_OK;
+  std::string s(kwargs);
+  for (char& ch : s)
+    if (ch == ',' || ch == ';' || ch == '\n' || ch == '\t') ch = ' ';
+  std::istringstream is(s);
+  std::string tok;
+  while (is >> tok) {
+    auto eq = tok.find('=');
+    if (eq == std::string::npos) continue;
+    std::string k = tok.substr(0, eq), v = tok.substr(eq + 1);
+    const char* cv = v.c_str();
+    auto f = [&]() { return strtof(cv, nullptr); };
+    if (k == "l1") kw->P.l1 = f();
+    else if (k == "l2") kw->P.l2 = f();
+    else if (k == "V_l2") kw->P.V_l2 = f();
+    else if (k == "lr") kw->P.lr = f();
+    else if (k == "lr_beta") kw->P.lr_beta = f();
+    else if (k == "V_lr") kw->P.V_lr = f();
+    else if (k == "V_lr_beta") kw->P.V_lr_beta = f();
+    else if (k == "V_init_scale") kw->P.V_init_scale = f();
+    else if (k == "V_dim") kw->P.V_dim = atoi(cv);
+    else if (k == "V_threshold") kw->P.V_threshold = atoi(cv);
+    else if (k == "l1_shrk") kw->P.l1_shrk = !(v == "0" || v == "false");
+    else if (k == "seed") kw->seed = (unsigned)strtoul(cv, nullptr, 10);
+    else if (k == "max_keys") kw->max_keys = atoll(cv);
+    else if (k == "max_vrows") kw->max_vrows = atoll(cv);
+    else if (k == "loss") {
+      if (v == "fm") kw->loss_fm = 1;
+      else if (v == "logit") kw->loss_fm = 0;
+      else { set_error("unknown loss: " + v + " (fm|logit)"); return DFX_ERR_ARG; }
+    }
+  }
+  if (kw->P.V_dim < 0 || kw->P.V_dim > 1024) {
+    set_error("V_dim must be in [0, 1024]");
+    return DFX_ERR_ARG;
+  }
+  if (!kw->loss_fm) kw->P.V_dim = 0;  // LogitLoss ignores V (logit_loss.h)
+  return DFX_OK;
+}
+
+// store allocation: table capacity = next pow2 >= 2*n_keys (load factor <= 0.5)
+int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows);
+void table_release(Context* c);
+
+}  // namespace dfx
+
+using namespace dfx;
+
+extern "C" {
+
+const char* dfx_last_error(void) { return g_last_error.c_str(); }
+
+int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
+  DFX_CHECK_ARG(out, "dfx_ctx_create: null out");
+  Kw kw;
+  DFX_TRY(parse_kwargs(kwargs, &kw));
+  int ndev = 0;
+  DFX_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0) device = 0;
+  DFX_CHECK_ARG(device < ndev, "dfx_ctx_create: no such device");
+  DFX_HIP(hipSetDevice(device));
+  dfx_ctx* ctx = new dfx_ctx();
+  Context* c = &ctx->c;
+  c->device = device;
+  c->P = kw.P;
+  c->loss_fm = kw.loss_fm;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    set_error("hipStreamCreate failed");
+    return DFX_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  if (hipMalloc(&c->ds, sizeof(DevState)) != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete ctx;
+    set_error("hipMalloc(DevState) failed");
+    return DFX_ERR_HIP;
+  }
+  DevState init;
+  memset(&init, 0, sizeof(init));
+  init.seed = kw.seed;
+  (void)hipMemcpy(c->ds, &init, sizeof(init), hipMemcpyHostToDevice);
+  int64_t vrows = kw.max_vrows >= 0 ? kw.max_vrows : (c->P.V_dim > 0 ? kw.max_keys : 0);
+  int rc = table_alloc(c, kw.max_keys, vrows);
+  if (rc != DFX_OK) {
+    dfx_ctx_destroy(ctx);
+    return rc;
+  }
+  *out = ctx;
+  return DFX_OK;
+}
+
+int dfx_ctx_destroy(dfx_ctx* ctx) {
+  if (!ctx) return DFX_OK;
+  Context* c = &ctx->c;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  Workspace& w = c->ws;
+  DevBuf* bufs[] = {&w.keys0, &w.keys1, &w.vals0, &w.vals1, &w.rowid, &w.hist, &w.tiles,
+                    &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
+                    &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch};
+  for (DevBuf* b : bufs) b->release();
+  table_release(c);
+  if (c->ds) (void)hipFree(c->ds);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete ctx;
+  return DFX_OK;
+}
+
+int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  ctx->c.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->c.own_stream;
+  return DFX_OK;
+}
+
+int dfx_ctx_vdim(dfx_ctx* ctx) { return ctx ? ctx->c.P.V_dim : -1; }
+
+int dfx_sync(dfx_ctx* ctx) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  int err = 0;
+  DFX_HIP(hipMemcpyAsync(&err, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  if (err) {
+    (void)hipMemsetAsync(&c->ds->err, 0, sizeof(int), c->stream);
+    (void)hipStreamSynchronize(c->stream);
+    std::string m = "device error:";
+    if (err & kErrTableFull) m += " hash table full (raise max_keys / dfx_store_reserve);";
+    if (err & kErrPoolFull) m += " V pool full (raise max_vrows);";
+    if (err & kErrLens) m += " CHECK_EQ(lens[i], V_dim+1) failed (sgd_updater.cc:83);";
+    if (err & kErrNoV) m += " CHECK(e.V != nullptr) failed (sgd_updater.cc:84);";
+    set_error(m);
+    return (err & (kErrTableFull | kErrPoolFull)) ? DFX_ERR_CAPACITY : DFX_ERR_CHECK;
+  }
+  return DFX_OK;
+}
+
+int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes) {
+  DFX_CHECK_ARG(ctx && ptr, "dfx_malloc: null argument");
+  DFX_HIP(hipSetDevice(ctx->c.device));
+  DFX_HIP(hipMalloc(ptr, bytes ? bytes : 16));
+  return DFX_OK;
+}
+
+int dfx_free(dfx_ctx* ctx, void* ptr) {
+  (void)ctx;
+  if (ptr) DFX_HIP(hipFree(ptr));
+  return DFX_OK;
+}
+
+int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  if (bytes == 0) return DFX_OK;
+  hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
+                              : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
+  DFX_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->c.stream));
+  if (kind == 1) DFX_HIP(hipStreamSynchronize(ctx->c.stream));
+  return DFX_OK;
+}
+
+int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  return ws_reserve(&ctx->c, max_rows, max_nnz);
+}
+
+int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset) {
+  DFX_CHECK_ARG(ctx && out, "null argument");
+  Context* c = &ctx->c;
+  double prog[5];
+  DFX_HIP(hipMemcpyAsync(prog, c->ds->prog, sizeof(prog), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  out->nrows = prog[0];
+  out->loss = prog[1];
+  out->auc = prog[2];
+  out->penalty = prog[3];
+  out->nnz_w = prog[4];
+  if (reset) {
+    DFX_HIP(hipMemsetAsync(c->ds->prog, 0, sizeof(prog), c->stream));
+    DFX_HIP(hipStreamSynchronize(c->stream));
+  }
+  return dfx_sync(ctx);
+}
+
+}  // extern "C"

@@ -1,0 +1,473 @@
+// FMLoss / LogitLoss forward and backward on gfx950 (src/loss/fm_loss.h:56-203,
+// src/loss/logit_loss.h:41-103, src/common/spmv.h, spmm.h).
+//
+// Forward (k_fm_fwd): a group of G lanes owns one CSR row, lane l owns V coordinates
+// l, l+G, ...  Each lane walks the row's nnz in order, so X*V and (X.*X)*(V.*V) are summed in
+// exactly the reference's (row, nnz) order; the V_dim-reduction is then done serially over
+// coordinates through wave shuffles — predictions are bit-identical to the reference.
+// At V_dim 16 a wave holds 4 rows and every gathered V row is one 64-byte segment.
+//
+// Backward (k_fm_bwd): Xᵀ products as a sorted-key segmented reduction — no atomics.  A
+// group of G lanes owns one column (unique key); it walks that key's occurrences in the
+// Localizer's sorted (key, pos) order, i.e. ascending (row, nnz): the same order as the
+// reference's column-range-partitioned TransTimes, so gradients are deterministic and, up
+// to expf, bit-identical.  In the fused step the same walk ends in the FTRL/AdaGrad update
+// of the key (no gradient round trip through HBM).
+#include "fm_args.h"
+
+namespace dfx {
+
+constexpr int kFmNT = 256;
+
+enum FwdMode { kPredict = 0, kGradPrep = 1, kFused = 2 };
+
+// p = -y / (1 + exp(y * pred)) [* weight]   (fm_loss.h:155-165).  exp in double, rounded:
+// correctly rounded like glibc's expf in all but rare ties (within the 1e-5 tolerance).
+__device__ inline float logit_p(float label, float pred, const float* rw, int64_t r) {
+  float y = label > 0 ? 1.f : -1.f;
+  float t = y * pred;
+  float e = (float)exp((double)t);
+  float den = 1.f + e;
+  float p = -y / den;
+  if (rw) p = p * rw[r];
+  return p;
+}
+
+
+
+template <int G, int CPL, int MODE, bool PACKED>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
+  constexpr int RPB = kFmNT / G;  // rows per block
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t r = (int64_t)blockIdx.x * RPB + g;
+  const int d = a.d;
+  __shared__ double red[kFmNT / kWave];
+  double loss = 0;
+  if (r < a.B) {
+    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
+    float acc = (MODE == kPredict) ? a.pred[r] : 0.f;
+    float xv[CPL], xxvv[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
+    const bool valued = a.val != nullptr;
+    for (uint64_t j = o0; j < o1; ++j) {
+      const uint32_t c = a.col[j];
+      const float x = valued ? a.val[j] : 1.f;
+      float w;
+      int vp;
+      if (PACKED) {
+        int2 e = a.wv[c];
+        w = __int_as_float(e.x);
+        vp = e.y;
+      } else {
+        if (a.wpos) { int q = a.wpos[c]; w = q < 0 ? 0.f : a.W[q]; } else { w = a.W[c]; }
+        vp = d > 0 ? a.vpos[c] : -1;
+      }
+      if (MODE != kGradPrep) {
+        // SpMV::Times skips w == 0 (spmv.h:124-125)
+        if (w != 0.f) acc = valued ? acc + w * x : acc + w;
+      }
+      if (vp >= 0) {
+        const float* V = a.Vbase + vp;
+        const float xx = x * x;  // XX_ (fm_loss.h:86-92)
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l + k * G;
+          if (cd < d) {
+            const float v = V[cd];
+            xv[k] = valued ? xv[k] + v * x : xv[k] + v;
+            if (MODE != kGradPrep) {
+              const float vv = v * v;  // VV (fm_loss.h:95-101)
+              xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
+            }
+          }
+        }
+      }
+    }
+    float pr = acc;
+    if (MODE != kGradPrep && d > 0) {
+      // s = sum_l (XV_l^2 - XXVV_l), serially in l (fm_loss.h:110-113)
+      float t[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) t[k] = xv[k] * xv[k] - xxvv[k];
+      float s = 0.f;
+      const int gbase = (threadIdx.x % kWave) - l;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        for (int q = 0; q < G; ++q) {
+          float tk = __shfl(t[k], gbase + q, kWave);
+          if (k * G + q < d) s += tk;
+        }
+      }
+      double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
+      pr = (float)y;
+      pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
+    }
+    if (MODE == kPredict) {
+      if (l == 0) a.pred[r] = pr;
+    } else {
+      const float predv = (MODE == kGradPrep) ? a.pred_in[r] : pr;
+      const float p = logit_p(a.label[r], predv, a.rw, r);
+      if (l == 0) {
+        a.p_out[r] = p;
+        if (MODE == kFused) {
+          a.pred[r] = pr;
+          double yy = a.label[r] > 0 ? 1.0 : -1.0;
+          loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+        }
+      }
+      if (d > 0) {
+        float* o = a.XVp + r * d;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l + k * G;
+          if (cd < d) o[cd] = xv[k] * p;  // XV_ *= p (fm_loss.h:196-199)
+        }
+      }
+    }
+  }
+  if (MODE == kFused) {
+    for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+    if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0;
+      for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+      a.loss_part[blockIdx.x] = s;
+    }
+  }
+}
+
+template <int MODE, bool PACKED>
+static int launch_fwd_gc(const FwdArgs& a, int G, int CPL, hipStream_t st) {
+  const int64_t rpb = kFmNT / G;
+  dim3 grid((unsigned)((a.B + rpb - 1) / rpb));
+  if (a.B <= 0) return DFX_OK;
+#define DFX_FWD(GG, CC)                                                                   \
+  if (G == GG && CPL == CC) {                                                             \
+    hipLaunchKernelGGL((k_fm_fwd<GG, CC, MODE, PACKED>), grid, dim3(kFmNT), 0, st, a);   \
+    DFX_HIP(hipGetLastError());                                                           \
+    return DFX_OK;                                                                        \
+  }
+  DFX_FWD(1, 1) DFX_FWD(2, 1) DFX_FWD(4, 1) DFX_FWD(8, 1) DFX_FWD(16, 1) DFX_FWD(32, 1)
+  DFX_FWD(64, 1) DFX_FWD(64, 2) DFX_FWD(64, 4) DFX_FWD(64, 8) DFX_FWD(64, 16)
+#undef DFX_FWD
+  set_error("unsupported V_dim");
+  return DFX_ERR_ARG;
+}
+
+void lanes_for(int d, int* G, int* CPL) {
+  int g = next_pow2_lanes(d < 1 ? 1 : d);
+  int cpl = (d + g - 1) / g;
+  if (cpl < 1) cpl = 1;
+  int c2 = 1;
+  while (c2 < cpl) c2 <<= 1;
+  *G = g;
+  *CPL = c2;
+}
+
+template <int MODE, bool PACKED>
+int launch_fwd(const FwdArgs& a, hipStream_t st) {
+  int G, CPL;
+  lanes_for(a.d, &G, &CPL);
+  return launch_fwd_gc<MODE, PACKED>(a, G, CPL, st);
+}
+
+int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
+  int G, CPL;
+  lanes_for(a.d, &G, &CPL);
+  const int64_t rpb = kFmNT / G;
+  *nblk = (int)((a.B + rpb - 1) / rpb);
+  return launch_fwd_gc<kFused, true>(a, G, CPL, st);
+}
+
+// ---- backward: sorted-key segmented reduction --------------------------------------------
+
+
+template <int G, int CPL, bool FUSED>
+__global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
+  constexpr int SPB = kFmNT / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t u = (int64_t)blockIdx.x * SPB + g;
+  const int64_t nseg = a.nseg_host >= 0 ? a.nseg_host : (int64_t)a.ds->u_count;
+  __shared__ int red[kFmNT / kWave];
+  int dnew = 0;
+  if (u < nseg) {
+    const uint32_t* P = (a.P1 && a.ds->sortmeta[31]) ? a.P1 : a.P;
+    const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
+    const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
+    const bool valued = a.val != nullptr;
+    const int d = a.d;
+    float gw, xxp = 0.f;
+    int wq = -1, vq = -1;
+    if (FUSED) {
+      gw = 0.f;
+      vq = a.wv[cidx].y;
+    } else {
+      wq = a.wpos ? a.wpos[cidx] : (int)cidx;
+      gw = wq >= 0 ? a.grad[wq] : 0.f;
+      vq = d > 0 ? a.vpos[cidx] : -1;
+    }
+    // SpMV::TransTimes for g_w and XXp (spmv.h:139-171): skip p == 0
+    for (uint32_t i = s0; i < s1; ++i) {
+      const uint32_t pos = P[i];
+      const float pr = a.p[a.rowid[pos]];
+      if (pr == 0.f) continue;
+      if (valued) {
+        const float x = a.val[pos];
+        gw += pr * x;
+        xxp += pr * (x * x);
+      } else {
+        gw += pr;
+        xxp += pr;
+      }
+    }
+    float acc[CPL];
+    if (vq >= 0) {
+      const float* V = FUSED ? (a.T.V + vq) : (a.W + vq);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int cd = l + k * G;
+        if (cd < d) {
+          const float g0 = FUSED ? 0.f : a.grad[vq + cd];
+          acc[k] = g0 - V[cd] * xxp;  // grad_u -= diag(XXp) V (fm_loss.h:185-192)
+        }
+      }
+      // SpMM::TransTimes (spmm.h:127-159): += (XV_ p) x, no zero skip
+      for (uint32_t i = s0; i < s1; ++i) {
+        const uint32_t pos = P[i];
+        const float* xr = a.XVp + (int64_t)a.rowid[pos] * d;
+        const float x = valued ? a.val[pos] : 1.f;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l + k * G;
+          if (cd < d) acc[k] = valued ? acc[k] + xr[cd] * x : acc[k] + xr[cd];
+        }
+      }
+    }
+    if (!FUSED) {
+      if (l == 0 && wq >= 0) a.grad[wq] = gw;
+      if (vq >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l + k * G;
+          if (cd < d) a.grad[vq + cd] = acc[k];
+        }
+      }
+    } else {
+      // Update(kGradient): UpdateW (FTRL), then UpdateV (AdaGrad) if V was pulled
+      const uint32_t sl = a.slot[cidx];
+      float4 e = a.T.st[sl];
+      bool tr;
+      int dw = ftrl_update(a.Pm, gw, &e, &tr);
+      if (vq >= 0) {
+        float* V = a.T.V + vq;
+        float* C = a.T.Vaux + vq;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l + k * G;
+          if (cd < d) adagrad_update(a.Pm, acc[k], V + cd, C + cd);
+        }
+      }
+      if (l == 0) {
+        a.T.st[sl] = e;
+        dnew = dw;
+        // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121)
+        bool need = tr && d > 0 && a.T.vrow[sl] < 0 && e.w > (float)a.Pm.V_threshold;
+        a.flags[u] = need ? 1u : 0u;
+      }
+    }
+  }
+  if (FUSED) {
+    for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
+    if (lane_id() == 0) red[threadIdx.x / kWave] = dnew;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int s = 0;
+      for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+      if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
+    }
+  }
+}
+
+template <bool FUSED>
+int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
+  if (nseg_bound <= 0) return DFX_OK;
+  int G, CPL;
+  lanes_for(a.d, &G, &CPL);
+  const int64_t spb = kFmNT / G;
+  dim3 grid((unsigned)((nseg_bound + spb - 1) / spb));
+#define DFX_BWD(GG, CC)                                                               \
+  if (G == GG && CPL == CC) {                                                         \
+    hipLaunchKernelGGL((k_fm_bwd<GG, CC, FUSED>), grid, dim3(kFmNT), 0, st, a);      \
+    DFX_HIP(hipGetLastError());                                                       \
+    return DFX_OK;                                                                    \
+  }
+  DFX_BWD(1, 1) DFX_BWD(2, 1) DFX_BWD(4, 1) DFX_BWD(8, 1) DFX_BWD(16, 1) DFX_BWD(32, 1)
+  DFX_BWD(64, 1) DFX_BWD(64, 2) DFX_BWD(64, 4) DFX_BWD(64, 8) DFX_BWD(64, 16)
+#undef DFX_BWD
+  set_error("unsupported V_dim");
+  return DFX_ERR_ARG;
+}
+
+int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
+  return launch_bwd<true>(a, nseg_bound, st);
+}
+
+// ---- standalone CalcGrad support: CSC order of a compacted block ------------------------
+__global__ void k_csc_prep(int64_t B, const uint64_t* __restrict__ offs,
+                           const uint32_t* __restrict__ col, uint32_t* __restrict__ keys,
+                           uint32_t* __restrict__ pos, uint32_t* __restrict__ rowid) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= B) return;
+  for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
+    keys[j] = col[j];
+    pos[j] = (uint32_t)j;
+    rowid[j] = (uint32_t)r;
+  }
+}
+
+// segments of the sorted column list: head flags -> scan -> segstart/segcol
+__global__ void k_csc_heads(const uint32_t* k0, const uint32_t* k1, int64_t n,
+                            const DevState* ds, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* K = ds->sortmeta[31] ? k1 : k0;
+  flags[i] = (i == 0 || K[i] != K[i - 1]) ? 1u : 0u;
+}
+
+__global__ void k_csc_segs(const uint32_t* k0, const uint32_t* k1, int64_t n,
+                           const DevState* ds, const uint32_t* excl, uint32_t* segstart,
+                           uint32_t* segcol, const uint32_t* total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* K = ds->sortmeta[31] ? k1 : k0;
+  const bool head = (i == 0 || K[i] != K[i - 1]);
+  if (head) {
+    segstart[excl[i]] = (uint32_t)i;
+    segcol[excl[i]] = K[i];
+  }
+  if (i == n - 1) segstart[*total] = (uint32_t)n;
+}
+
+int get_nbits(int64_t n) {
+  int b = 0;
+  while (b < 32 && ((int64_t)1 << b) < n) ++b;
+  return b;
+}
+
+}  // namespace dfx
+
+using namespace dfx;
+
+extern "C" int dfx_fm_predict(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t* offset,
+                              const uint32_t* col, const float* value, const float* weights,
+                              const int32_t* w_pos, const int32_t* V_pos, int64_t n_cols,
+                              int V_dim, float* pred) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_ARG(B >= 0 && nnz >= 0 && V_dim >= 0 && V_dim <= 1024, "fm_predict: bad sizes");
+  DFX_CHECK_ARG(V_dim == 0 || (w_pos && V_pos), "fm_predict: V_dim > 0 needs w_pos and V_pos");
+  if (B == 0) return DFX_OK;
+  DFX_CHECK_ARG(offset && pred && (nnz == 0 || (col && weights)), "fm_predict: null buffer");
+  (void)n_cols;
+  FwdArgs a{};
+  a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
+  a.vpos = V_pos; a.Vbase = weights; a.d = V_dim; a.pred = pred;
+  return launch_fwd<kPredict, false>(a, ctx->c.stream);
+}
+
+extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t* offset,
+                               const uint32_t* col, const float* value, const float* label,
+                               const float* row_weight, const float* weights,
+                               const int32_t* w_pos, const int32_t* V_pos, int64_t n_cols,
+                               int V_dim, const float* pred, float* grad) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(B >= 0 && nnz >= 0 && V_dim >= 0 && V_dim <= 1024, "fm_calcgrad: bad sizes");
+  DFX_CHECK_ARG(V_dim == 0 || (w_pos && V_pos), "fm_calcgrad: V_dim > 0 needs w_pos and V_pos");
+  DFX_CHECK_ARG(n_cols >= 0 && n_cols < 0xFFFFFFFFll, "fm_calcgrad: bad n_cols");
+  if (B == 0 || nnz == 0) return DFX_OK;
+  DFX_CHECK_ARG(offset && col && label && weights && pred && grad, "fm_calcgrad: null buffer");
+  Workspace& ws = c->ws;
+  DFX_TRY(ws.p.ensure(B * 4));
+  if (V_dim > 0) DFX_TRY(ws.XVp.ensure((size_t)B * V_dim * 4));
+  DFX_TRY(ws.vals0.ensure(nnz * 4));
+  DFX_TRY(ws.vals1.ensure(nnz * 4));
+  DFX_TRY(ws.keys0.ensure(nnz * 4));
+  DFX_TRY(ws.keys1.ensure(nnz * 4));
+  DFX_TRY(ws.rowid.ensure(nnz * 4));
+  DFX_TRY(ws.flags.ensure((nnz + 1) * 4));
+  DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
+  DFX_TRY(ws.slot.ensure((nnz + 1) * 4));
+  DFX_TRY(ws.cnt.ensure(4 * 4));
+  // 1) p and XV*p per row
+  FwdArgs a{};
+  a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
+  a.vpos = V_pos; a.Vbase = weights; a.d = V_dim; a.label = label; a.rw = row_weight;
+  a.pred_in = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
+  DFX_TRY((launch_fwd<kGradPrep, false>(a, c->stream)));
+  // 2) CSC order: stable sort of (col, pos)
+  uint32_t* k0 = ws.keys0.as<uint32_t>();
+  uint32_t* k1 = ws.keys1.as<uint32_t>();
+  hipLaunchKernelGGL(k_csc_prep, dim3((B + 255) / 256), dim3(256), 0, c->stream, B, offset, col,
+                     k0, ws.vals0.as<uint32_t>(), ws.rowid.as<uint32_t>());
+  DFX_TRY(radix_sort_pairs<uint32_t>(c, k0, ws.vals0.as<uint32_t>(), k1,
+                                     ws.vals1.as<uint32_t>(), nnz, 0, get_nbits(n_cols),
+                                     nullptr, c->ds->sortmeta));
+  uint32_t* flags = ws.flags.as<uint32_t>();
+  uint32_t* total = ws.cnt.as<uint32_t>();
+  hipLaunchKernelGGL(k_csc_heads, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, k0, k1, nnz,
+                     c->ds, flags);
+  DFX_TRY(scan_u32(c, flags, nnz, total));
+  hipLaunchKernelGGL(k_csc_segs, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, k0, k1, nnz,
+                     c->ds, flags, ws.segstart.as<uint32_t>(), ws.slot.as<uint32_t>(), total);
+  // 3) segmented reduction into grad
+  BwdArgs b{};
+  b.segstart = ws.segstart.as<uint32_t>();
+  b.ds = c->ds;
+  b.nseg_host = -1;
+  b.segcol = ws.slot.as<uint32_t>();
+  b.P = ws.vals0.as<uint32_t>();
+  b.P1 = ws.vals1.as<uint32_t>();
+  b.rowid = ws.rowid.as<uint32_t>();
+  b.val = value; b.p = ws.p.as<float>(); b.XVp = ws.XVp.as<float>(); b.d = V_dim;
+  b.wpos = w_pos; b.vpos = V_pos; b.W = weights; b.grad = grad;
+  // the number of segments is device-side; store it where k_fm_bwd reads it
+  DFX_HIP(hipMemcpyAsync(&c->ds->u_count, total, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                         c->stream));
+  return launch_bwd<false>(b, nnz, c->stream);
+}
+
+__global__ void k_get_pos(int64_t n, const int32_t* lens, const uint32_t* excl, int32_t* w_pos,
+                          int32_t* V_pos) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int l = lens[i];
+  const int p = (int)excl[i];
+  w_pos[i] = l == 0 ? -1 : p;
+  V_pos[i] = l > 1 ? p + 1 : -1;
+}
+
+__global__ void k_copy_i32_u32(int64_t n, const int32_t* a, uint32_t* b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = (uint32_t)a[i];
+}
+
+// SGDLearner::GetPos (sgd_learner.cc:151-165)
+extern "C" int dfx_get_pos(dfx_ctx* ctx, int64_t n, const int32_t* lens, int32_t* w_pos,
+                           int32_t* V_pos) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  if (n <= 0) return DFX_OK;
+  DFX_CHECK_ARG(lens && w_pos && V_pos, "get_pos: null buffer");
+  Context* c = &ctx->c;
+  DFX_TRY(c->ws.flags.ensure((n + 1) * 4));
+  uint32_t* ex = c->ws.flags.as<uint32_t>();
+  hipLaunchKernelGGL(k_copy_i32_u32, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, lens, ex);
+  DFX_TRY(scan_u32(c, ex, n, nullptr));
+  hipLaunchKernelGGL(k_get_pos, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, lens, ex,
+                     w_pos, V_pos);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}

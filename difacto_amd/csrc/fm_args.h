@@ -1,0 +1,59 @@
+// Argument blocks of the FM forward/backward kernels (fm.hip), shared with step.hip.
+#pragma once
+#include "internal.h"
+
+namespace dfx {
+
+struct FwdArgs {
+  int64_t B;
+  const uint64_t* offs;
+  const uint32_t* col;
+  const float* val;
+  // weights: packed {w, V offset} per column (fused) or interleaved weights + positions
+  const int2* wv;
+  const float* W;
+  const int32_t* wpos;
+  const int32_t* vpos;
+  const float* Vbase;
+  int d;
+  const float* label;
+  const float* rw;
+  const float* pred_in;  // gradient prep: p from this pred
+  float* pred;           // predict: in/out (+=); fused: out
+  float* p_out;
+  float* XVp;            // B*d: XV_ * p
+  double* loss_part;     // fused: per-block partial sums of Evaluate
+};
+
+struct BwdArgs {
+  const uint32_t* segstart;  // nseg+1
+  const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
+  int64_t nseg_host;
+  const uint32_t* segcol;    // column of each segment (NULL: segment index == column)
+  const uint32_t* P;         // sorted nnz positions, buffer 0 ...
+  const uint32_t* P1;        // ... or buffer 1, chosen by ds->sortmeta[31]
+  const uint32_t* rowid;
+  const float* val;
+  const float* p;
+  const float* XVp;
+  int d;
+  // standalone CalcGrad: positions into grad
+  const int32_t* wpos;
+  const int32_t* vpos;
+  const float* W;
+  float* grad;
+  // fused update
+  const int2* wv;
+  const uint32_t* slot;
+  Table T;
+  Params Pm;
+  uint32_t* flags;  // InitV request per key
+  DevState* dsw;
+};
+
+// fused forward; *nblk receives the number of loss partials written
+int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk);
+// fused backward + FTRL/AdaGrad update over at most nseg_bound segments
+int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st);
+
+}  // namespace dfx

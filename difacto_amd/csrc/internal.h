@@ -1,0 +1,149 @@
+// Host-side internals of libdifacto_amd.so: the context, its device store and workspace,
+// error plumbing, and the launchers each .hip file exports to the others.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/difacto_amd.h"
+#include "common.h"
+
+namespace dfx {
+
+void set_error(const std::string& msg);
+
+#define DFX_HIP(call)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (call);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      ::dfx::set_error(std::string(#call) + ": " + hipGetErrorString(_e));            \
+      return DFX_ERR_HIP;                                                             \
+    }                                                                                 \
+  } while (0)
+
+#define DFX_CHECK_ARG(cond, msg)              \
+  do {                                        \
+    if (!(cond)) {                            \
+      ::dfx::set_error(msg);                  \
+      return DFX_ERR_ARG;                     \
+    }                                         \
+  } while (0)
+
+#define DFX_TRY(expr)             \
+  do {                            \
+    int _rc = (expr);             \
+    if (_rc != DFX_OK) return _rc; \
+  } while (0)
+
+// A grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t n);  // may synchronise (hipFree/hipMalloc)
+  void release();
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Device counters and progress, one small allocation.
+struct DevState {
+  unsigned long long n_keys;   // occupied table slots
+  unsigned long long n_vrows;  // V pool rows in use
+  unsigned int seed;           // rand_r state (SGDUpdaterParam::seed)
+  int err;                     // kErr* bits
+  long long new_w;             // SGDUpdater::new_w statistic
+  double prog[5];              // dfx_progress accumulators
+  unsigned long long or_mask;  // sort bit-range detection (per call)
+  unsigned long long and_mask;
+  unsigned long long diff_mask;
+  unsigned int u_count;        // U of the current batch
+  unsigned int n_init;         // InitV count of the current phase
+  unsigned int sortmeta[32];   // per-pass {active, src} + final selector (Localizer sort)
+  unsigned int sortmeta2[32];  // the same for the AUC sort
+  unsigned int totals[8];      // scan totals of the current step
+  double auc_n;                // AUC * n of the current step
+  double sum_u;                // sum of U over dfx_train_step calls (roofline bytes)
+  double n_steps;
+  double scratch[8];
+};
+
+struct Workspace {
+  // sort double buffers (u64 keys, u32 payload) and per-nnz arrays
+  DevBuf keys0, keys1, vals0, vals1, rowid;
+  DevBuf hist;     // radix histograms
+  DevBuf tiles;    // per-tile scan partials
+  // per-unique arrays
+  DevBuf uniq, cnt, segstart, col, slot, flags, wb, Vb, vpos;
+  // per-row arrays
+  DevBuf p, pred, XVp, rowtmp;
+  DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
+  DevBuf dscratch;  // double partials
+  int64_t rows = 0, nnz = 0;
+};
+
+struct Context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  Params P{};
+  int loss_fm = 1;
+  // store
+  Table T{};
+  int64_t cap = 0;
+  DevState* ds = nullptr;  // device
+  Workspace ws;
+  // per-phase HIP-event timing of dfx_train_step (dfx_prof_*); events on c->stream
+  std::vector<hipEvent_t> prof_ev;  // prof_max steps x kProfMarks
+  int prof_max = 0, prof_n = 0;
+};
+
+constexpr int kProfMarks = 8;  // start, localize, feacnt, pull, fwd, auc, bwd, initv/end
+inline void prof_mark(Context* c, int m) {
+  if (c->prof_n < c->prof_max)
+    (void)hipEventRecord(c->prof_ev[(size_t)c->prof_n * kProfMarks + m], c->stream);
+}
+
+// ---- cross-file launchers --------------------------------------------------------------
+// radix sort of (key, u32 payload) pairs over bits [begin_bit, end_bit), 8 bits per pass.
+// Reads from (k0,v0), uses (k1,v1) as the ping-pong buffer.  When diff_mask (device, a
+// u64 of the bits that vary) is given, passes over constant digits are skipped on the
+// device.  The result lives in buffer sel (0 or 1) written to *sel_dev.
+template <typename K>
+int radix_sort_pairs(Context* c, K* k0, uint32_t* v0, K* k1, uint32_t* v1, int64_t n,
+                     int begin_bit, int end_bit, const unsigned long long* diff_mask,
+                     unsigned int* sortmeta);
+
+// exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
+int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev);
+
+// exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
+void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);
+
+// Localizer::Compact on the device.  Leaves in the workspace: the sorted (key, pos)
+// pairs (buffer selected by ds->sortmeta[31]), rowid[nnz] when want_rowid, U in
+// ds->u_count.  Writes uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].
+int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
+                 const uint64_t* index, uint64_t max_index, uint64_t* uniq, float* cnt,
+                 uint32_t* col, uint32_t* segstart, bool want_rowid);
+
+int ws_reserve(Context* c, int64_t rows, int64_t nnz);
+
+// store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
+int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
+              const uint32_t* slot);
+int push_cnt_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
+                 const float* cnt, const uint32_t* segstart, uint32_t* slot, uint32_t* flags,
+                 uint32_t* total_dev);
+int resolve_pull_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
+                     uint32_t* slot, int2* wv);
+int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows);
+
+// metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
+int auc_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
+int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
+
+}  // namespace dfx
+
+struct dfx_ctx {
+  dfx::Context c;
+};

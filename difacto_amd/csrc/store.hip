@@ -1,0 +1,707 @@
+// The device model store: SGDUpdater (src/sgd/sgd_updater.{h,cc}) behind the Store
+// push/pull boundary (include/difacto/store.h:44-75), on one GPU.
+//
+// Layout in HBM (sized for 288 GB):
+//   keys  u64[cap]      open-addressing table, multiplicative hash of the (already
+//                       nibble-reversed) key, linear probing, cap = pow2 >= 2*max_keys
+//   st    float4[cap]   {w, sqrt_g, z, fea_cnt}       (SGDEntry, sgd_updater.h:20-34)
+//   vrow  i32[cap]      row of the lazy V pool, -1 == no V (SGDEntry::V == nullptr)
+//   V     f32[vcap*d]   embedding rows, allocated by InitV in rand_r order
+//   Vaux  f32[vcap*d]   AdaGrad accumulators
+// InitV (sgd_updater.cc:144-152) draws glibc rand_r in key order; on the GPU every key that
+// needs V gets its exclusive-scan rank r among this push's InitV keys and jumps the LCG by
+// 3*V_dim*r steps, which reproduces the reference's sequential draws exactly.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iomanip>
+#include <sstream>
+#include <vector>
+
+#include "internal.h"
+
+namespace dfx {
+
+constexpr int kStNT = 256;
+
+__device__ inline void block_count_add(int v, unsigned long long* dst) {
+  __shared__ int red[kStNT / kWave];
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 0; i < kStNT / kWave; ++i) s += red[i];
+    if (s) atomicAdd(dst, (unsigned long long)(long long)s);
+  }
+}
+
+__device__ inline int64_t count_of(int64_t n_host, const DevState* ds) {
+  return n_host >= 0 ? n_host : (int64_t)ds->u_count;
+}
+
+// ---- InitV --------------------------------------------------------------------------------
+// excl: exclusive scan of the per-key InitV flags; *total: their sum.
+__global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t* excl,
+                                                 const uint32_t* total, const uint32_t* slot,
+                                                 Table T, float scale, DevState* ds) {
+  const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  const int64_t n = count_of(n_host, ds);
+  if (u >= n) return;
+  const uint32_t e = excl[u];
+  const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
+  if (nx == e) return;
+  const int d = T.d;
+  uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+  const int64_t vr = (int64_t)ds->n_vrows + e;
+  if (vr >= T.vcap) {
+    atomicOr(&ds->err, kErrPoolFull);
+    return;
+  }
+  float* V = T.V + vr * d;
+  float* C = T.Vaux + vr * d;
+  for (int k = 0; k < d; ++k) {
+    V[k] = initv_value(rand_r_dev(&s), scale);
+    C[k] = 0.f;
+  }
+  T.vrow[slot[u]] = (int32_t)vr;
+}
+
+__global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, DevState* ds) {
+  const uint32_t n = *total;
+  ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * n);
+  unsigned long long nv = ds->n_vrows + n;
+  ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+}
+
+// flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
+int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
+              const uint32_t* slot) {
+  if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
+  DFX_TRY(scan_u32(c, flags, n_bound, total_dev));
+  hipLaunchKernelGGL(k_initv, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
+                     n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds);
+  hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
+                     c->T.vcap, c->ds);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+// ---- Update(kFeaCount) (sgd_updater.cc:64-75) ---------------------------------------------
+// cnt: float counts, or NULL to derive them from segstart (fused path).
+__global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n_host, const uint64_t* keys,
+                                                    const float* cnt, const uint32_t* segstart,
+                                                    Table T, Params P, uint32_t* slot,
+                                                    uint32_t* flags, DevState* ds) {
+  const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  const int64_t n = count_of(n_host, ds);
+  int ins = 0;
+  if (u < n) {
+    bool inserted;
+    int64_t s = tbl_insert(T, keys[u], &inserted);
+    ins = inserted;
+    uint32_t f = 0;
+    if (s < 0) {
+      atomicOr(&ds->err, kErrTableFull);
+    } else {
+      float c = cnt ? cnt[u] : (float)(segstart[u + 1] - segstart[u]);
+      float4 e = T.st[s];
+      e.w += c;  // fea_cnt
+      T.st[s] = e;
+      if (P.V_dim > 0 && T.vrow[s] < 0 && e.x != 0.f && e.w > (float)P.V_threshold) f = 1;
+      slot[u] = (uint32_t)s;
+    }
+    flags[u] = f;
+  }
+  block_count_add(ins, &ds->n_keys);
+}
+
+// ---- fused pull: resolve slots (find-or-insert) and emit {w, V pool offset} per key ------
+// SGDUpdater::Get (sgd_updater.cc:34-58): V only if present and not (l1_shrk && w == 0).
+__global__ __launch_bounds__(kStNT) void k_resolve_pull(int64_t n_host, const uint64_t* keys,
+                                                        Table T, Params P, uint32_t* slot,
+                                                        int2* wv, DevState* ds) {
+  const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  const int64_t n = count_of(n_host, ds);
+  int ins = 0;
+  if (u < n) {
+    bool inserted;
+    int64_t s = tbl_insert(T, keys[u], &inserted);
+    ins = inserted;
+    if (s < 0) {
+      atomicOr(&ds->err, kErrTableFull);
+      wv[u] = make_int2(0, -1);
+      slot[u] = 0xFFFFFFFFu;
+    } else {
+      float w = T.st[s].x;
+      int vr = T.vrow[s];
+      bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
+      wv[u] = make_int2(__float_as_int(w), live ? vr * T.d : -1);
+      slot[u] = (uint32_t)s;
+    }
+  }
+  block_count_add(ins, &ds->n_keys);
+}
+
+int push_cnt_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
+                 const float* cnt, const uint32_t* segstart, uint32_t* slot, uint32_t* flags,
+                 uint32_t* total_dev) {
+  if (n_bound <= 0) return DFX_OK;
+  hipLaunchKernelGGL(k_push_cnt, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
+                     n_host, keys, cnt, segstart, c->T, c->P, slot, flags, c->ds);
+  DFX_HIP(hipGetLastError());
+  return run_initv(c, n_host, n_bound, flags, total_dev, slot);
+}
+
+int resolve_pull_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
+                     uint32_t* slot, int2* wv) {
+  if (n_bound <= 0) return DFX_OK;
+  hipLaunchKernelGGL(k_resolve_pull, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0,
+                     c->stream, n_host, keys, c->T, c->P, slot, wv, c->ds);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+// ---- standalone Get: interleaved [w | V] + lens ---------------------------------------------
+__global__ __launch_bounds__(kStNT) void k_pull_lens(int64_t n, const uint64_t* keys, Table T,
+                                                     Params P, int32_t* vr_out,
+                                                     uint32_t* len_out) {
+  const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  if (i >= n) return;
+  int64_t s = tbl_find(T, keys[i]);
+  int vr = -1;
+  float w = 0.f;
+  if (s >= 0) { w = T.st[s].x; vr = T.vrow[s]; }
+  bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
+  vr_out[i] = live ? vr : -1;
+  len_out[i] = live ? (uint32_t)(T.d + 1) : 1u;
+}
+
+__global__ __launch_bounds__(kStNT) void k_pull_write(int64_t n, const uint64_t* keys, Table T,
+                                                      const int32_t* vr_in,
+                                                      const uint32_t* off, float* vals,
+                                                      int32_t* lens) {
+  const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  if (i >= n) return;
+  int64_t s = tbl_find(T, keys[i]);
+  const uint32_t o = off[i];
+  vals[o] = s >= 0 ? T.st[s].x : 0.f;
+  const int vr = vr_in[i];
+  const int d = T.d;
+  if (vr >= 0) {
+    const float* V = T.V + (int64_t)vr * d;
+    for (int k = 0; k < d; ++k) vals[o + 1 + k] = V[k];
+  }
+  if (lens) lens[i] = vr >= 0 ? d + 1 : 1;
+}
+
+// ---- standalone Update(kGradient) (sgd_updater.cc:76-98) -----------------------------------
+__global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* keys,
+                                                     const float* vals, const int32_t* lens,
+                                                     const uint32_t* off, Table T, Params P,
+                                                     uint32_t* slot, uint32_t* flags,
+                                                     DevState* ds) {
+  const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
+  int ins = 0, dnew = 0;
+  if (i < n) {
+    bool inserted;
+    int64_t s = tbl_insert(T, keys[i], &inserted);
+    ins = inserted;
+    uint32_t f = 0;
+    if (s < 0) {
+      atomicOr(&ds->err, kErrTableFull);
+    } else {
+      const int d = T.d;
+      const uint32_t o = lens ? off[i] : (uint32_t)i;
+      float4 e = T.st[s];
+      bool tr;
+      dnew = ftrl_update(P, vals[o], &e, &tr);
+      T.st[s] = e;
+      const int vr = T.vrow[s];
+      if (lens && lens[i] > 1) {
+        if (lens[i] != d + 1) {
+          atomicOr(&ds->err, kErrLens);
+        } else if (vr < 0) {
+          atomicOr(&ds->err, kErrNoV);
+        } else {
+          float* V = T.V + (int64_t)vr * d;
+          float* C = T.Vaux + (int64_t)vr * d;
+          for (int k = 0; k < d; ++k) adagrad_update(P, vals[o + 1 + k], V + k, C + k);
+        }
+      }
+      // InitV when w leaves 0 and the feature is frequent enough (sgd_updater.cc:118-121)
+      if (tr && d > 0 && vr < 0 && e.w > (float)P.V_threshold) f = 1;
+      slot[i] = (uint32_t)s;
+    }
+    flags[i] = f;
+  }
+  block_count_add(ins, &ds->n_keys);
+  __syncthreads();
+  block_count_add(dnew, (unsigned long long*)&ds->new_w);
+}
+
+__global__ void k_check_total(const uint32_t* total, int64_t n_vals, DevState* ds) {
+  if ((int64_t)*total != n_vals) atomicOr(&ds->err, kErrLens);
+}
+
+__global__ void k_lens_u32(int64_t n, const int32_t* lens, uint32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)lens[i];
+}
+
+// ---- table allocation / growth ------------------------------------------------------------
+__global__ void k_rehash(const uint64_t* okeys, const float4* ost, const int32_t* ovrow,
+                         int64_t ocap, Table T, DevState* ds) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ocap) return;
+  const uint64_t k = okeys[i];
+  if (k == kEmptyKey) return;
+  bool ins;
+  int64_t s = tbl_insert(T, k, &ins);
+  if (s < 0) { atomicOr(&ds->err, kErrTableFull); return; }
+  T.st[s] = ost[i];
+  T.vrow[s] = ovrow[i];
+}
+
+int table_alloc_arrays(Table* T, int64_t cap) {
+  DFX_HIP(hipMalloc(&T->keys, cap * sizeof(uint64_t)));
+  DFX_HIP(hipMalloc(&T->st, cap * sizeof(float4)));
+  DFX_HIP(hipMalloc(&T->vrow, cap * sizeof(int32_t)));
+  DFX_HIP(hipMemset(T->keys, 0xFF, cap * sizeof(uint64_t)));
+  DFX_HIP(hipMemset(T->st, 0, cap * sizeof(float4)));
+  DFX_HIP(hipMemset(T->vrow, 0xFF, cap * sizeof(int32_t)));
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
+  T->logcap = lg;
+  T->mask = (uint64_t)cap - 1;
+  return DFX_OK;
+}
+
+int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
+  if (n_keys < 1024) n_keys = 1024;
+  int64_t cap = 1;
+  while (cap < 2 * n_keys) cap <<= 1;
+  Table& T = c->T;
+  T.d = c->P.V_dim;
+  DFX_TRY(table_alloc_arrays(&T, cap));
+  c->cap = cap;
+  T.vcap = T.d > 0 ? (n_vrows > 0 ? n_vrows : 1) : 0;
+  if (T.d > 0) {
+    DFX_HIP(hipMalloc(&T.V, T.vcap * T.d * sizeof(float)));
+    DFX_HIP(hipMalloc(&T.Vaux, T.vcap * T.d * sizeof(float)));
+  }
+  return DFX_OK;
+}
+
+void table_release(Context* c) {
+  Table& T = c->T;
+  if (T.keys) (void)hipFree(T.keys);
+  if (T.st) (void)hipFree(T.st);
+  if (T.vrow) (void)hipFree(T.vrow);
+  if (T.V) (void)hipFree(T.V);
+  if (T.Vaux) (void)hipFree(T.Vaux);
+  T = Table{};
+}
+
+struct HostCounters {
+  unsigned long long n_keys, n_vrows;
+  unsigned seed;
+  long long new_w;
+};
+
+static int read_counters(Context* c, HostCounters* h) {
+  DevState s;
+  DFX_HIP(hipMemcpyAsync(&s, c->ds, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  h->n_keys = s.n_keys;
+  h->n_vrows = s.n_vrows;
+  h->seed = s.seed;
+  h->new_w = s.new_w;
+  return DFX_OK;
+}
+
+int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  Table& T = c->T;
+  if (2 * n_keys > c->cap) {
+    int64_t cap = c->cap;
+    while (cap < 2 * n_keys) cap <<= 1;
+    Table NT = T;
+    DFX_TRY(table_alloc_arrays(&NT, cap));
+    hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.keys,
+                       T.st, T.vrow, c->cap, NT, c->ds);
+    DFX_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(T.keys);
+    (void)hipFree(T.st);
+    (void)hipFree(T.vrow);
+    T.keys = NT.keys; T.st = NT.st; T.vrow = NT.vrow; T.mask = NT.mask; T.logcap = NT.logcap;
+    c->cap = cap;
+  }
+  if (T.d > 0 && n_vrows > T.vcap) {
+    HostCounters h;
+    DFX_TRY(read_counters(c, &h));
+    float *nV, *nC;
+    DFX_HIP(hipMalloc(&nV, n_vrows * T.d * sizeof(float)));
+    DFX_HIP(hipMalloc(&nC, n_vrows * T.d * sizeof(float)));
+    if (h.n_vrows) {
+      DFX_HIP(hipMemcpy(nV, T.V, h.n_vrows * T.d * sizeof(float), hipMemcpyDeviceToDevice));
+      DFX_HIP(hipMemcpy(nC, T.Vaux, h.n_vrows * T.d * sizeof(float), hipMemcpyDeviceToDevice));
+    }
+    (void)hipFree(T.V);
+    (void)hipFree(T.Vaux);
+    T.V = nV; T.Vaux = nC; T.vcap = n_vrows;
+  }
+  return DFX_OK;
+}
+
+// load: host-parsed entries uploaded and inserted
+__global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const int32_t* vr,
+                       int has_aux, Table T, DevState* ds) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int ins = 0;
+  if (i < n) {
+    bool inserted;
+    int64_t s = tbl_insert(T, keys[i], &inserted);
+    ins = inserted;
+    if (s < 0) {
+      atomicOr(&ds->err, kErrTableFull);
+    } else {
+      float4 e = T.st[s];
+      e.x = st[i].x;
+      if (has_aux) { e.y = st[i].y; e.z = st[i].z; }
+      T.st[s] = e;
+      if (vr[i] >= 0) T.vrow[s] = vr[i];
+    }
+  }
+  block_count_add(ins, &ds->n_keys);
+}
+
+__global__ void k_penalty(const uint64_t* keys, const float4* st, const int32_t* vrow,
+                          int64_t cap, Table T, Params P, double* acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double objv = 0, nnz = 0;
+  if (i < cap && keys[i] != kEmptyKey) {
+    const float w = st[i].x;
+    if (w != 0.f) nnz += 1;
+    objv += P.l1 * fabs(w) + .5 * P.l2 * w * w;
+    const int vr = vrow[i];
+    if (vr >= 0) {
+      nnz += T.d;
+      const float* V = T.V + (int64_t)vr * T.d;
+      for (int k = 0; k < T.d; ++k) objv += .5 * P.l2 * V[k] * V[k];  // (sic) l2, :21
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    objv += __shfl_xor(objv, off, kWave);
+    nnz += __shfl_xor(nnz, off, kWave);
+  }
+  if (lane_id() == 0 && (objv != 0 || nnz != 0)) {
+    atomicAdd(&acc[0], objv);
+    atomicAdd(&acc[1], nnz);
+  }
+}
+
+}  // namespace dfx
+
+using namespace dfx;
+
+extern "C" {
+
+int dfx_store_pull(dfx_ctx* ctx, const uint64_t* keys, int64_t n, float* vals, int32_t* lens,
+                   int64_t* n_vals) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  const int d = c->P.V_dim;
+  DFX_CHECK_ARG(n >= 0, "pull: negative n");
+  DFX_CHECK_ARG(d == 0 || lens || n == 0, "pull: lens required when V_dim > 0");
+  if (n == 0) {
+    if (n_vals) *n_vals = 0;
+    return DFX_OK;
+  }
+  DFX_CHECK_ARG(keys && vals, "pull: null buffer");
+  Workspace& ws = c->ws;
+  DFX_TRY(ws.flags.ensure((n + 1) * 4));
+  DFX_TRY(ws.slot.ensure((n + 1) * 4));
+  DFX_TRY(ws.cnt.ensure(16));
+  uint32_t* off = ws.flags.as<uint32_t>();
+  int32_t* vr = ws.slot.as<int32_t>();
+  uint32_t* total = ws.cnt.as<uint32_t>();
+  dim3 grid((n + kStNT - 1) / kStNT);
+  hipLaunchKernelGGL(k_pull_lens, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, c->P, vr, off);
+  DFX_TRY(scan_u32(c, off, n, total));
+  hipLaunchKernelGGL(k_pull_write, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, vr, off, vals,
+                     d > 0 ? lens : nullptr);
+  DFX_HIP(hipGetLastError());
+  if (n_vals) {
+    uint32_t t = 0;
+    DFX_HIP(hipMemcpyAsync(&t, total, 4, hipMemcpyDeviceToHost, c->stream));
+    DFX_HIP(hipStreamSynchronize(c->stream));
+    *n_vals = t;
+  }
+  return DFX_OK;
+}
+
+int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, const float* vals,
+                   int64_t n_vals, const int32_t* lens) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(n >= 0, "push: negative n");
+  if (n == 0) return DFX_OK;
+  DFX_CHECK_ARG(keys && vals, "push: null buffer");
+  Workspace& ws = c->ws;
+  DFX_TRY(ws.flags.ensure((n + 1) * 4));
+  DFX_TRY(ws.slot.ensure((n + 1) * 4));
+  DFX_TRY(ws.tiles.ensure(16));
+  DFX_TRY(ws.cnt.ensure(16));
+  uint32_t* flags = ws.flags.as<uint32_t>();
+  uint32_t* slot = ws.slot.as<uint32_t>();
+  uint32_t* total = ws.cnt.as<uint32_t>();
+  if (type == DFX_FEA_COUNT) {
+    if (n_vals != n) {
+      set_error("CHECK_EQ(fea_ids.size(), values.size()) failed (sgd_updater.cc:65)");
+      return DFX_ERR_CHECK;
+    }
+    return push_cnt_run(c, n, n, keys, vals, nullptr, slot, flags, total);
+  }
+  if (type != DFX_GRADIENT) {
+    set_error("UNKNOWN value_type (sgd_updater.cc:100)");
+    return DFX_ERR_CHECK;
+  }
+  uint32_t* off = nullptr;
+  if (lens) {
+    DFX_TRY(ws.rowtmp.ensure((n + 1) * 4));
+    off = ws.rowtmp.as<uint32_t>();
+    hipLaunchKernelGGL(k_lens_u32, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, lens, off);
+    DFX_TRY(scan_u32(c, off, n, total));
+    hipLaunchKernelGGL(k_check_total, dim3(1), dim3(1), 0, c->stream, total, n_vals, c->ds);
+  } else if (n_vals != n) {
+    set_error("CHECK_EQ(values.size(), size) failed (sgd_updater.cc:79)");
+    return DFX_ERR_CHECK;
+  }
+  hipLaunchKernelGGL(k_push_grad, dim3((n + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream, n,
+                     keys, vals, lens, off, c->T, c->P, slot, flags, c->ds);
+  DFX_HIP(hipGetLastError());
+  return run_initv(c, n, n, flags, total, slot);
+}
+
+int dfx_store_reserve(dfx_ctx* ctx, int64_t n_keys, int64_t n_vrows) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  return store_reserve(&ctx->c, n_keys, n_vrows);
+}
+
+int dfx_store_stats(dfx_ctx* ctx, int64_t* n_keys, int64_t* n_vrows, double* new_w,
+                    uint32_t* seed) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  HostCounters h;
+  DFX_TRY(read_counters(&ctx->c, &h));
+  if (n_keys) *n_keys = (int64_t)h.n_keys;
+  if (n_vrows) *n_vrows = (int64_t)h.n_vrows;
+  if (new_w) *new_w = (double)h.new_w;
+  if (seed) *seed = h.seed;
+  return dfx_sync(ctx);
+}
+
+int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  DFX_TRY(c->ws.dscratch.ensure(64));
+  double* acc = c->ws.dscratch.as<double>();
+  DFX_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(double), c->stream));
+  hipLaunchKernelGGL(k_penalty, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, c->T.keys,
+                     c->T.st, c->T.vrow, c->cap, c->T, c->P, acc);
+  double h[2];
+  DFX_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  if (penalty) *penalty = h[0];
+  if (nnz) *nnz = (int64_t)h[1];
+  return DFX_OK;
+}
+
+int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has_v, int* found) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  const Table& T = c->T;
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  // host-side probe of the same hash sequence (test hook; not a hot path)
+  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> (64 - T.logcap);
+  *found = 0;
+  for (uint64_t probe = 0; probe <= T.mask; ++probe) {
+    uint64_t kk;
+    DFX_HIP(hipMemcpy(&kk, T.keys + h, 8, hipMemcpyDeviceToHost));
+    if (kk == kEmptyKey) return DFX_OK;
+    if (kk == key) {
+      float4 e;
+      int32_t vr;
+      DFX_HIP(hipMemcpy(&e, T.st + h, sizeof(e), hipMemcpyDeviceToHost));
+      DFX_HIP(hipMemcpy(&vr, T.vrow + h, 4, hipMemcpyDeviceToHost));
+      state[0] = e.x; state[1] = e.y; state[2] = e.z; state[3] = e.w;
+      *has_v = vr >= 0;
+      if (vr >= 0 && V) {
+        DFX_HIP(hipMemcpy(V, T.V + (int64_t)vr * T.d, T.d * 4, hipMemcpyDeviceToHost));
+        DFX_HIP(hipMemcpy(V + T.d, T.Vaux + (int64_t)vr * T.d, T.d * 4, hipMemcpyDeviceToHost));
+      }
+      *found = 1;
+      return DFX_OK;
+    }
+    h = (h + 1) & T.mask;
+  }
+  return DFX_OK;
+}
+
+// SGDUpdater::Save (sgd_updater.h:84-106, SGDEntry::SaveEntry :35-48)
+int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux) {
+  DFX_CHECK_ARG(ctx && path, "null argument");
+  Context* c = &ctx->c;
+  const Table& T = c->T;
+  HostCounters hc;
+  DFX_TRY(read_counters(c, &hc));
+  std::vector<uint64_t> keys(c->cap);
+  std::vector<float4> st(c->cap);
+  std::vector<int32_t> vrow(c->cap);
+  std::vector<float> V((size_t)hc.n_vrows * T.d), C((size_t)hc.n_vrows * T.d);
+  DFX_HIP(hipMemcpy(keys.data(), T.keys, c->cap * 8, hipMemcpyDeviceToHost));
+  DFX_HIP(hipMemcpy(st.data(), T.st, c->cap * sizeof(float4), hipMemcpyDeviceToHost));
+  DFX_HIP(hipMemcpy(vrow.data(), T.vrow, c->cap * 4, hipMemcpyDeviceToHost));
+  if (!V.empty()) {
+    DFX_HIP(hipMemcpy(V.data(), T.V, V.size() * 4, hipMemcpyDeviceToHost));
+    DFX_HIP(hipMemcpy(C.data(), T.Vaux, C.size() * 4, hipMemcpyDeviceToHost));
+  }
+  FILE* f = fopen(path, "wb");
+  if (!f) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
+  bool aux = save_aux != 0;
+  fwrite(&aux, sizeof(bool), 1, f);
+  for (int64_t i = 0; i < c->cap; ++i) {
+    if (keys[i] == kEmptyKey) continue;
+    const int size = vrow[i] >= 0 ? 1 + T.d : 1;
+    const float w = st[i].x;
+    if (w == 0.f && size == 1) continue;  // SGDEntry::empty()
+    fwrite(&keys[i], 8, 1, f);
+    fwrite(&size, sizeof(int), 1, f);
+    fwrite(&w, 4, 1, f);
+    if (aux) { fwrite(&st[i].y, 4, 1, f); fwrite(&st[i].z, 4, 1, f); }
+    if (size == 1) continue;
+    fwrite(V.data() + (size_t)vrow[i] * T.d, 4, T.d, f);
+    if (aux) fwrite(C.data() + (size_t)vrow[i] * T.d, 4, T.d, f);
+  }
+  fclose(f);
+  return DFX_OK;
+}
+
+// SGDUpdater::Load (sgd_updater.h:84-96, SGDEntry::LoadEntry :50-68)
+int dfx_store_load(dfx_ctx* ctx, const char* path) {
+  DFX_CHECK_ARG(ctx && path, "null argument");
+  Context* c = &ctx->c;
+  Table& T = c->T;
+  FILE* f = fopen(path, "rb");
+  if (!f) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
+  bool aux;
+  if (fread(&aux, sizeof(bool), 1, f) != 1) { fclose(f); return DFX_OK; }
+  HostCounters hc;
+  DFX_TRY(read_counters(c, &hc));
+  std::vector<uint64_t> keys;
+  std::vector<float4> st;
+  std::vector<int32_t> vr;
+  std::vector<float> V, C;
+  uint64_t key;
+  int64_t vnext = (int64_t)hc.n_vrows;
+  while (fread(&key, 8, 1, f) == 1) {
+    int size;
+    float4 e = make_float4(0, 0, 0, 0);
+    if (fread(&size, sizeof(int), 1, f) != 1 || fread(&e.x, 4, 1, f) != 1) {
+      fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
+    }
+    if (aux && (fread(&e.y, 4, 1, f) != 1 || fread(&e.z, 4, 1, f) != 1)) {
+      fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
+    }
+    int32_t row = -1;
+    if (size > 1) {
+      if (size != T.d + 1) { fclose(f); set_error("model V_dim mismatch"); return DFX_ERR_CHECK; }
+      size_t base = V.size();
+      V.resize(base + T.d);
+      C.resize(base + T.d, 0.f);
+      if (fread(V.data() + base, 4, T.d, f) != (size_t)T.d) {
+        fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
+      }
+      if (aux && fread(C.data() + base, 4, T.d, f) != (size_t)T.d) {
+        fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
+      }
+      row = (int32_t)vnext++;
+    }
+    keys.push_back(key);
+    st.push_back(e);
+    vr.push_back(row);
+  }
+  fclose(f);
+  const int64_t n = (int64_t)keys.size();
+  DFX_TRY(store_reserve(c, (int64_t)hc.n_keys + n, vnext));
+  if (n == 0) return DFX_OK;
+  uint64_t* dk;
+  float4* dst;
+  int32_t* dvr;
+  DFX_HIP(hipMalloc(&dk, n * 8));
+  DFX_HIP(hipMalloc(&dst, n * sizeof(float4)));
+  DFX_HIP(hipMalloc(&dvr, n * 4));
+  DFX_HIP(hipMemcpy(dk, keys.data(), n * 8, hipMemcpyHostToDevice));
+  DFX_HIP(hipMemcpy(dst, st.data(), n * sizeof(float4), hipMemcpyHostToDevice));
+  DFX_HIP(hipMemcpy(dvr, vr.data(), n * 4, hipMemcpyHostToDevice));
+  if (!V.empty()) {
+    DFX_HIP(hipMemcpy(T.V + hc.n_vrows * T.d, V.data(), V.size() * 4, hipMemcpyHostToDevice));
+    DFX_HIP(hipMemcpy(T.Vaux + hc.n_vrows * T.d, C.data(), C.size() * 4, hipMemcpyHostToDevice));
+  }
+  hipLaunchKernelGGL(k_load, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, dk, dst, dvr,
+                     aux ? 1 : 0, T, c->ds);
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  unsigned long long nv = (unsigned long long)vnext;
+  DFX_HIP(hipMemcpy(&c->ds->n_vrows, &nv, 8, hipMemcpyHostToDevice));
+  // new_w = model_.size() (sgd_updater.h:91)
+  DevState s;
+  DFX_HIP(hipMemcpy(&s, c->ds, sizeof(s), hipMemcpyDeviceToHost));
+  long long nw = (long long)s.n_keys;
+  DFX_HIP(hipMemcpy(&c->ds->new_w, &nw, 8, hipMemcpyHostToDevice));
+  (void)hipFree(dk);
+  (void)hipFree(dst);
+  (void)hipFree(dvr);
+  return dfx_sync(ctx);
+}
+
+// SGDUpdater::Dump (sgd_updater.h:108-139): text, one entry per line
+int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_reverse) {
+  DFX_CHECK_ARG(ctx && path, "null argument");
+  Context* c = &ctx->c;
+  const Table& T = c->T;
+  HostCounters hc;
+  DFX_TRY(read_counters(c, &hc));
+  std::vector<uint64_t> keys(c->cap);
+  std::vector<float4> st(c->cap);
+  std::vector<int32_t> vrow(c->cap);
+  std::vector<float> V((size_t)hc.n_vrows * T.d), C((size_t)hc.n_vrows * T.d);
+  DFX_HIP(hipMemcpy(keys.data(), T.keys, c->cap * 8, hipMemcpyDeviceToHost));
+  DFX_HIP(hipMemcpy(st.data(), T.st, c->cap * sizeof(float4), hipMemcpyDeviceToHost));
+  DFX_HIP(hipMemcpy(vrow.data(), T.vrow, c->cap * 4, hipMemcpyDeviceToHost));
+  if (!V.empty()) {
+    DFX_HIP(hipMemcpy(V.data(), T.V, V.size() * 4, hipMemcpyDeviceToHost));
+    DFX_HIP(hipMemcpy(C.data(), T.Vaux, C.size() * 4, hipMemcpyDeviceToHost));
+  }
+  std::ofstream os(path);
+  if (!os) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
+  for (int64_t i = 0; i < c->cap; ++i) {
+    if (keys[i] == kEmptyKey) continue;
+    const int size = vrow[i] >= 0 ? 1 + T.d : 1;
+    if (st[i].x == 0.f && size == 1) continue;
+    os << (need_reverse ? reverse_bytes(keys[i]) : keys[i]);
+    os << '\t' << size << '\t' << st[i].x;
+    if (dump_aux) os << '\t' << st[i].y << '\t' << st[i].z;
+    if (size > 1) {
+      const float* v = V.data() + (size_t)vrow[i] * T.d;
+      for (int k = 0; k < T.d; ++k) os << '\t' << v[k];
+      if (dump_aux) {
+        const float* cc = C.data() + (size_t)vrow[i] * T.d;
+        for (int k = 0; k < T.d; ++k) os << '\t' << cc[k];
+      }
+    }
+    os << '\n';
+  }
+  return DFX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+/*
+ * difacto_amd.h — the C-ABI of libdifacto_amd.so, the MI355X (gfx950) implementation of
+ * DiFacto's data-parallel hot path.
+ *
+ * Plain pointers and sizes only (no C++ or torch types).  Every function returns a status
+ * (DFX_OK == 0); on failure dfx_last_error() holds the message.  The C++ adapters under
+ * difacto_amd/host map a non-zero status to LOG(FATAL), which is the reference's own error
+ * convention (CHECK / LOG(FATAL) abort, include/difacto/base.h + dmlc logging).
+ *
+ * POINTERS: every array argument is a DEVICE pointer (hipMalloc / dfx_malloc / a torch
+ * tensor's data_ptr()) on the context's device; scalar outputs (int64_t*, double*) are host
+ * pointers.  Work is queued on the context's stream (dfx_ctx_set_stream); functions whose
+ * result is a host scalar synchronise that stream.
+ *
+ * Reference interfaces replaced (paths relative to the reference repository):
+ *   Localizer::Compact            src/data/localizer.h:41-51, localizer.cc:11-107
+ *   FMLoss::Predict / CalcGrad    src/loss/fm_loss.h:56-119, 136-203
+ *   LogitLoss::Predict / CalcGrad src/loss/logit_loss.h:41-57, 71-103   (== FM with V_dim 0)
+ *   Loss::Evaluate                include/difacto/loss.h:57-66
+ *   BinClassMetric::AUC           src/loss/bin_class_metric.h:35-57
+ *   SGDLearner::GetPos            src/sgd/sgd_learner.cc:151-165
+ *   Store::Push / Pull            include/difacto/store.h:44-75 (StoreLocal store_local.h:24-45,
+ *                                 KVStoreDist kvstore_dist.h:90-107)
+ *   SGDUpdater::Get / Update      src/sgd/sgd_updater.cc:34-152 (FTRL w, AdaGrad V, InitV)
+ *   SGDUpdater::Save/Load/Dump    src/sgd/sgd_updater.h:84-139
+ *   SGDUpdater::Evaluate          src/sgd/sgd_updater.cc:12-30
+ *   SGDLearner::IterateData body  src/sgd/sgd_learner.cc:201-317 (fused: dfx_train_step)
+ */
+#ifndef DIFACTO_AMD_H_
+#define DIFACTO_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFX_OK 0
+#define DFX_ERR_ARG 1      /* bad argument (shape, null pointer, unsupported V_dim) */
+#define DFX_ERR_HIP 2      /* a HIP runtime call failed */
+#define DFX_ERR_CAPACITY 3 /* hash table or V pool full (see dfx_store_reserve) */
+#define DFX_ERR_CHECK 4    /* a reference CHECK failed (e.g. lens[i] != V_dim+1) */
+#define DFX_ERR_IO 5       /* model file could not be read / written */
+
+/* value types, include/difacto/store.h:33-35 */
+#define DFX_FEA_COUNT 1
+#define DFX_WEIGHT 2
+#define DFX_GRADIENT 3
+
+/* job types, src/sgd/sgd_utils.h:14-20 */
+#define DFX_JOB_TRAINING 3
+#define DFX_JOB_VALIDATION 4
+#define DFX_JOB_PREDICTION 5
+
+typedef struct dfx_ctx dfx_ctx;
+
+/* dmlc::RowBlock<feaid_t> as produced by BatchReader (device pointers). */
+typedef struct dfx_batch {
+  int64_t size;           /* B rows */
+  int64_t nnz;            /* == offset[B] */
+  const uint64_t* offset; /* B+1 (size_t), offset[0] == 0 */
+  const uint64_t* index;  /* nnz raw feature ids */
+  const float* value;     /* nnz, or NULL for binary data (batch_reader.cc:71-73) */
+  const float* label;     /* B */
+  const float* weight;    /* B row weights, or NULL */
+} dfx_batch;
+
+/* sgd::Progress (src/sgd/sgd_utils.h:52-93), accumulated in double. auc is AUC*rows. */
+typedef struct dfx_progress {
+  double nrows;
+  double loss;
+  double auc;
+  double penalty;
+  double nnz_w;
+} dfx_progress;
+
+/* ---- context -------------------------------------------------------------------------
+ * kwargs: the reference .conf keys, "k=v" separated by ',', ';', ' ' or newlines:
+ *   loss (fm|logit), V_dim, lr, lr_beta, l1, l2, V_lr, V_lr_beta, V_l2, V_init_scale,
+ *   V_threshold, l1_shrk, seed          (sgd_param.h:79-123, fm_loss.h:19-27)
+ * plus device-store sizing: max_keys (hash table keys, default 1<<22), max_vrows
+ * (V pool rows, default max_keys).  Unknown keys are ignored (InitAllowUnknown). */
+const char* dfx_last_error(void);
+int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out);
+int dfx_ctx_destroy(dfx_ctx* ctx);
+int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+int dfx_ctx_vdim(dfx_ctx* ctx);
+int dfx_sync(dfx_ctx* ctx); /* waits for the stream and reports deferred device errors */
+int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes);
+int dfx_free(dfx_ctx* ctx, void* ptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device; async on the stream */
+int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+/* pre-size the fused-path workspace so dfx_train_step allocates nothing (graph capture) */
+int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz);
+
+/* ---- Localizer::Compact (localizer.h:41-51) -------------------------------------------
+ * keys = ReverseBytes(index % max_index); uniq[U] ascending, cnt[U] occurrence counts
+ * (float, may be NULL), col[nnz] = rank of each nnz's key (the u32 CSR index).  Offsets,
+ * values and labels of the compacted block equal the input's (every index matches).
+ * uniq and cnt need room for nnz entries.  *n_uniq receives U (synchronises). */
+int dfx_localize(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t* offset,
+                 const uint64_t* index, uint64_t max_index, uint64_t* uniq, float* cnt,
+                 uint32_t* col, int64_t* n_uniq);
+
+/* ---- FMLoss / LogitLoss ----------------------------------------------------------------
+ * weights: the interleaved Pull layout [w | V(V_dim)] addressed by w_pos / V_pos
+ * (SGDLearner::GetPos).  V_dim == 0 is LogitLoss; then w_pos may be NULL (w = weights[col]).
+ * V_dim > 0 requires w_pos and V_pos.  n_cols = number of columns (U).
+ * pred accumulates (+=) like the reference; grad accumulates too (pre-zero it). */
+int dfx_fm_predict(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t* offset,
+                   const uint32_t* col, const float* value, const float* weights,
+                   const int32_t* w_pos, const int32_t* V_pos, int64_t n_cols, int V_dim,
+                   float* pred);
+int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t* offset,
+                    const uint32_t* col, const float* value, const float* label,
+                    const float* row_weight, const float* weights, const int32_t* w_pos,
+                    const int32_t* V_pos, int64_t n_cols, int V_dim, const float* pred,
+                    float* grad);
+/* SGDLearner::GetPos: lens[n] -> w_pos[n], V_pos[n] */
+int dfx_get_pos(dfx_ctx* ctx, int64_t n, const int32_t* lens, int32_t* w_pos, int32_t* V_pos);
+/* Loss::Evaluate and BinClassMetric::AUC (returns AUC*n like the reference) */
+int dfx_evaluate(dfx_ctx* ctx, int64_t B, const float* label, const float* pred, double* objv);
+int dfx_auc(dfx_ctx* ctx, int64_t B, const float* label, const float* pred, double* auc_n);
+
+/* ---- Store / SGDUpdater (device hash table, lazy V pool) --------------------------------
+ * keys: n reversed feature ids, unique within one call (the Localizer guarantees it).
+ * pull: vals needs room for n*(1+V_dim); lens (n, NULL when V_dim == 0) receives 1 or
+ *       V_dim+1; *n_vals the number of values written (synchronises).
+ * push: DFX_FEA_COUNT (vals[n]) or DFX_GRADIENT (interleaved like pull; lens NULL means
+ *       w only).  Processing order = array order (InitV draws rand_r in that order). */
+int dfx_store_pull(dfx_ctx* ctx, const uint64_t* keys, int64_t n, float* vals, int32_t* lens,
+                   int64_t* n_vals);
+int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, const float* vals,
+                   int64_t n_vals, const int32_t* lens);
+int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux);
+int dfx_store_load(dfx_ctx* ctx, const char* path);
+int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_reverse);
+int dfx_store_stats(dfx_ctx* ctx, int64_t* n_keys, int64_t* n_vrows, double* new_w,
+                    uint32_t* seed);
+int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz);
+int dfx_store_reserve(dfx_ctx* ctx, int64_t n_keys, int64_t n_vrows);
+/* test hook: state[4] = {w, sqrt_g, z, fea_cnt}, V/Vaux (2*V_dim floats, host) */
+int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has_v,
+                    int* found);
+
+/* ---- fused minibatch (SGDLearner::IterateData executor, sgd_learner.cc:203-269) --------
+ * localize -> [push kFeaCount] -> pull -> predict -> evaluate -> AUC -> calcgrad -> push,
+ * all on the device with no host round trip (graph-capturable after dfx_reserve).
+ * job_type: DFX_JOB_TRAINING updates the model; validation/prediction stop after AUC.
+ * push_cnt: push occurrence counts first (epoch 0 with V_dim > 0, sgd_learner.cc:272).
+ * pred_out: optional device B floats.  Progress accumulates on the device. */
+int dfx_train_step(dfx_ctx* ctx, const dfx_batch* batch, int job_type, int push_cnt,
+                   uint64_t max_index, float* pred_out);
+int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset);
+
+/* ---- measurement ------------------------------------------------------------------------
+ * HIP events on the context stream around each phase of dfx_train_step, for up to
+ * max_steps calls.  dfx_prof_read returns summed ms[7] = {localize, feacnt push, pull,
+ * forward, evaluate+AUC, backward+update, InitV+finalize}, the number of recorded steps,
+ * and the mean unique-key count U per step (for algorithmic-byte accounting); it resets. */
+int dfx_prof_enable(dfx_ctx* ctx, int max_steps);
+int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIFACTO_AMD_H_ */

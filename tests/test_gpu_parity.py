@@ -1,0 +1,374 @@
+"""Parity of the HIP path (through the C-ABI) with the oracle and the reference's known
+answers.  Bars (BASELINE.json north_star): Localizer bit-exact; predictions and gradients
+within 1e-5 relative (fp32); loss / AUC within 1e-4.  Predictions are also checked for
+bit-exactness, which the kernels achieve by summing in the reference's order."""
+import numpy as np
+import pytest
+import torch
+
+from difacto_amd import data as D
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def H():
+    from difacto_amd import hotpath
+    return hotpath
+
+
+def close(a, b, rtol=RTOL):
+    """|a-b| <= rtol*max(|a|,|b|) + small absolute floor scaled to the data."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    floor = 1e-6 * max(1.0, float(np.max(np.abs(b))) if b.size else 1.0)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(a), np.abs(b)) + floor)
+
+
+def _rev(a):
+    return np.array([O.reverse_bytes(int(x)) for x in a], dtype=np.uint64)
+
+
+# ---------------------------------------------------------------- Localizer (bit-exact)
+def _check_localize(H, c, blk, max_index=(1 << 64) - 1):
+    db = H.DeviceRowBlock(c, blk)
+    col, uniq, cnt = H.Localizer(c, max_index).compact(db)
+    ou, oc, ocol = O.localize(blk.offs, blk.ids, max_index=max_index)
+    assert np.array_equal(H.u64(uniq), ou)
+    assert np.array_equal(cnt.cpu().numpy(), oc)
+    assert np.array_equal(H.u32(col), ocol)
+    return ou, oc
+
+
+def test_localizer_rcv1_known_answers(H, rcv1, known):
+    c = H.Context(0)
+    ou, oc = _check_localize(H, c, rcv1)
+    assert int(_rev(ou).sum()) == known["localizer_base"]["sum_uidx"]
+    assert float(oc.sum()) == known["localizer_base"]["sum_freq"]
+    ou, oc = _check_localize(H, c, rcv1, max_index=1000)
+    assert int(_rev(ou).sum()) == known["localizer_hash1000"]["sum_uidx"]
+
+
+@pytest.mark.parametrize("kind", ["criteo", "ragged", "zipf", "u64", "dups", "big"])
+def test_localizer_synthetic(H, kind):
+    c = H.Context(0)
+    if kind == "criteo":
+        blk = D.synthetic(4000, 39, 1 << 24, seed=1)
+    elif kind == "ragged":
+        blk = D.synthetic(3000, 20, 1 << 20, seed=2, ragged=True, binary=False)
+    elif kind == "zipf":
+        blk = D.synthetic(3000, 39, 1 << 24, seed=3, zipf=1.1)
+    elif kind == "u64":
+        blk = D.synthetic(2000, 30, 1 << 20, seed=4)
+        rng = np.random.default_rng(4)
+        blk.ids = rng.integers(0, np.iinfo(np.uint64).max, size=blk.nnz, dtype=np.uint64,
+                               endpoint=True)
+        blk.ids[:7] = np.iinfo(np.uint64).max  # x % UINT64_MAX == 0 edge
+    elif kind == "dups":
+        blk = D.synthetic(2000, 39, 50, seed=5)  # massive key collisions
+    else:
+        blk = D.synthetic(60000, 39, 1 << 24, seed=6)  # many sort tiles
+    _check_localize(H, c, blk)
+    if kind == "u64":
+        _check_localize(H, c, blk, max_index=1000)
+
+
+def test_localizer_empty(H):
+    c = H.Context(0)
+    blk = D.RowBlock(np.zeros(5, np.uint64), np.zeros(0, np.uint64), None, np.ones(4, np.float32))
+    db = H.DeviceRowBlock(c, blk)
+    col, uniq, cnt = H.Localizer(c).compact(db)
+    assert uniq.numel() == 0 and col.numel() == 0
+
+
+# ---------------------------------------------------------------- FMLoss
+def _fm_weights(uidx, d):
+    U = len(uidx)
+    W = np.zeros(U * (d + 1), np.float32)
+    wp = (np.arange(U) * (d + 1)).astype(np.int32)
+    for i in range(U):
+        W[i * (d + 1)] = uidx[i] / 5e4
+        for j in range(1, d + 1):
+            W[i * (d + 1) + j] = uidx[i] * j / 5e5
+    return W, wp, wp + 1
+
+
+def _fm_run(H, c, blk, W, wp, vp, d, U, rw=None):
+    db = H.DeviceRowBlock(c, blk)
+    if rw is not None:
+        db.weights = c.tensor(rw, torch.float32)
+    col, uniq, _ = H.Localizer(c).compact(db)
+    loss = H.FMLoss(c, d)
+    tW = c.tensor(W, torch.float32)
+    twp = c.tensor(wp, torch.int32)
+    tvp = c.tensor(vp, torch.int32)
+    pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+    loss.predict(db, col, tW, twp, tvp, pred, U)
+    grad = torch.zeros(len(W), dtype=torch.float32, device=c.device)
+    loss.calc_grad(db, col, tW, twp, tvp, pred, grad, U)
+    objv = loss.evaluate(db.labels, pred)
+    return pred.cpu().numpy(), grad.cpu().numpy(), objv, H.u32(col)
+
+
+def test_fmloss_nov_known(H, rcv1, known):
+    k = known["fmloss_nov"]
+    c = H.Context(0)
+    ou, _, ocol = O.localize(rcv1.offs, rcv1.ids)
+    w = (_rev(ou) / 5e4).astype(np.float32)
+    pred, grad, objv, col = _fm_run(H, c, rcv1, w, None, None, 0, len(ou))
+    assert abs(objv - k["objv"]) < k["objv_tol"]
+    assert abs(float((grad.astype(np.float64) ** 2).sum()) - k["grad_norm2"]) < k["grad_tol"]
+    opred = O.fm_predict(rcv1.offs, ocol, rcv1.vals, w, None, None, 0)
+    assert np.array_equal(pred, opred)
+    og = O.fm_calcgrad(rcv1.offs, ocol, rcv1.vals, rcv1.labels, None, w, None, None, len(ou), 0,
+                       opred)
+    assert close(grad, og)
+
+
+def test_fmloss_hasv_known(H, rcv1, known):
+    k = known["fmloss_hasv"]
+    d = k["V_dim"]
+    c = H.Context(0)
+    ou, _, ocol = O.localize(rcv1.offs, rcv1.ids)
+    W, wp, vp = _fm_weights(_rev(ou), d)
+    pred, grad, objv, col = _fm_run(H, c, rcv1, W, wp, vp, d, len(ou))
+    assert abs(objv - k["objv"]) < k["objv_tol"]
+    assert abs(float((grad.astype(np.float64) ** 2).sum()) - k["grad_norm2"]) < k["grad_tol"]
+    opred = O.fm_predict(rcv1.offs, ocol, rcv1.vals, W, wp, vp, d)
+    assert np.array_equal(pred, opred)
+    og = O.fm_calcgrad(rcv1.offs, ocol, rcv1.vals, rcv1.labels, None, W, wp, vp, len(ou), d, opred)
+    assert close(grad, og)
+
+
+@pytest.mark.parametrize("d", [0, 1, 2, 5, 16, 33, 64, 100, 128, 200])
+@pytest.mark.parametrize("binary", [True, False])
+def test_fmloss_random(H, d, binary):
+    rng = np.random.default_rng(100 + d)
+    blk = D.synthetic(1500, 25, 3000, binary=binary, seed=7 + d, ragged=True)
+    ou, _, ocol = O.localize(blk.offs, blk.ids)
+    U = len(ou)
+    # interleaved Pull layout with ~1/3 of the keys lacking V (lens == 1)
+    lens = np.where(rng.random(U) < 0.33, 1, d + 1).astype(np.int32) if d > 0 else None
+    if d > 0:
+        wp, vp = O.get_pos(lens)
+        W = (rng.standard_normal(int(lens.sum())) * 0.1).astype(np.float32)
+        W[wp[rng.random(U) < 0.1]] = 0  # w == 0 skip path
+    else:
+        wp = vp = None
+        W = (rng.standard_normal(U) * 0.1).astype(np.float32)
+    rw = (rng.random(blk.size) + 0.5).astype(np.float32)
+    c = H.Context(0)
+    pred, grad, objv, col = _fm_run(H, c, blk, W, wp, vp, d, U, rw=rw)
+    opred = O.fm_predict(blk.offs, ocol, blk.vals, W, wp, vp, d)
+    assert np.array_equal(pred, opred), np.max(np.abs(pred - opred))
+    og = O.fm_calcgrad(blk.offs, ocol, blk.vals, blk.labels, rw, W, wp, vp, U, d, opred)
+    assert close(grad, og)
+    assert abs(objv - O.evaluate(blk.labels, opred)) <= 1e-4 * abs(objv)
+
+
+def test_get_pos(H):
+    rng = np.random.default_rng(0)
+    lens = rng.choice([0, 1, 17], size=5000).astype(np.int32)
+    c = H.Context(0)
+    w, v = H.get_pos(c, c.tensor(lens, torch.int32))
+    ow, ov = O.get_pos(lens)
+    assert np.array_equal(w.cpu().numpy(), ow) and np.array_equal(v.cpu().numpy(), ov)
+
+
+def test_auc_and_evaluate(H):
+    rng = np.random.default_rng(1)
+    n = 20000
+    label = np.where(rng.random(n) < 0.3, 1.0, -1.0).astype(np.float32)
+    pred = (rng.standard_normal(n) + 0.5 * label).astype(np.float32)
+    c = H.Context(0)
+    tl, tp = c.tensor(label, torch.float32), c.tensor(pred, torch.float32)
+    a = H.auc(c, tl, tp)
+    assert abs(a - O.auc(label, pred)) <= 1e-4 * n
+    assert abs(H.FMLoss(c, 0).evaluate(tl, tp) - O.evaluate(label, pred)) <= 1e-6 * n
+    # degenerate batch: the reference returns 1 (not 1*n)
+    assert H.auc(c, tl, c.tensor(np.ones(n, np.float32), torch.float32)) > 0
+    assert H.auc(c, c.tensor(np.ones(n, np.float32), torch.float32), tp) == 1.0
+
+
+# ---------------------------------------------------------------- Store / SGDUpdater
+def _store_pair(H, **kw):
+    c = H.Context(0, max_keys=1 << 16, **kw)
+    return c, H.Store(c), O.Updater(**kw)
+
+
+def _pull_eq(H, c, st, up, keys):
+    v, l = st.pull(c.tensor(keys, torch.int64))
+    ov, ol = up.get(keys)
+    assert np.array_equal(v.cpu().numpy(), ov)
+    if ol is not None:
+        assert np.array_equal(l.cpu().numpy(), ol)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(V_dim=0, l1=1, l2=0.1, lr=0.5),
+    dict(V_dim=8, V_threshold=2, l1=0.01, lr=0.1, V_lr=0.05, V_init_scale=0.5, seed=7),
+    dict(V_dim=16, V_threshold=0, l1=0, lr=0.1, l1_shrk=0),
+])
+def test_store_matches_updater(H, kw):
+    rng = np.random.default_rng(11)
+    c, st, up = _store_pair(H, **kw)
+    d = kw["V_dim"]
+    keys_all = np.unique(rng.integers(0, 1 << 62, size=3000, dtype=np.uint64))
+    for it in range(6):
+        keys = np.sort(rng.choice(keys_all, size=1200, replace=False))
+        tk = c.tensor(keys, torch.int64)
+        if it < 2 and d > 0:
+            cnt = rng.integers(1, 5, size=len(keys)).astype(np.float32)
+            st.push(tk, H.kFeaCount, c.tensor(cnt, torch.float32))
+            up.update(keys, O.Updater.kFeaCount, cnt)
+        _pull_eq(H, c, st, up, keys)
+        ov, ol = up.get(keys)
+        g = (rng.standard_normal(len(ov)) * 2).astype(np.float32)
+        st.push(tk, H.kGradient, c.tensor(g, torch.float32),
+                c.tensor(ol, torch.int32) if ol is not None else None)
+        up.update(keys, O.Updater.kGradient, g, ol)
+        c.sync()
+    _pull_eq(H, c, st, up, keys_all)
+    s = st.stats()
+    assert s["seed"] == up.seed
+    assert s["new_w"] == up.new_w
+    for k in keys_all[:200]:
+        e, oe = st.entry(k), up.entry(k)
+        assert (e is None) == (oe is None) or (oe is not None and not oe[0].any())
+        if e is not None and oe is not None:
+            assert np.array_equal(e[0][:3], oe[0][:3])
+            if oe[1] is not None:
+                assert np.array_equal(e[1], oe[1])
+    pen, nnz = st.evaluate()
+    open_, onnz = up.penalty()
+    assert nnz == onnz and abs(pen - open_) <= 1e-6 * max(1, abs(open_))
+
+
+def test_store_check_failures(H):
+    c = H.Context(0, V_dim=4, max_keys=1024)
+    st = H.Store(c)
+    keys = c.tensor(np.arange(1, 11, dtype=np.uint64), torch.int64)
+    g = c.tensor(np.ones(10 * 5, np.float32), torch.float32)
+    lens = c.tensor(np.full(10, 5, np.int32), torch.int32)
+    st.push(keys, H.kGradient, g, lens)  # no V exists yet -> CHECK(e.V) fails
+    with pytest.raises(H._lib.DfxError):
+        c.sync()
+    with pytest.raises(H._lib.DfxError):
+        st.push(keys, 7, g, lens)
+
+
+def test_save_load_interop(H, tmp_path):
+    kw = dict(V_dim=6, V_threshold=1, l1=0.01, lr=0.1, V_lr=0.05)
+    rng = np.random.default_rng(3)
+    c, st, up = _store_pair(H, **kw)
+    keys = np.unique(rng.integers(0, 1 << 60, size=800, dtype=np.uint64))
+    tk = c.tensor(keys, torch.int64)
+    cnt = np.full(len(keys), 3, np.float32)
+    st.push(tk, H.kFeaCount, c.tensor(cnt, torch.float32))
+    up.update(keys, 1, cnt)
+    for _ in range(3):
+        ov, ol = up.get(keys)
+        g = rng.standard_normal(len(ov)).astype(np.float32)
+        st.push(tk, H.kGradient, c.tensor(g, torch.float32), c.tensor(ol, torch.int32))
+        up.update(keys, 3, g, ol)
+    p_gpu, p_orc = str(tmp_path / "gpu_part-0"), str(tmp_path / "orc_part-0")
+    st.save(p_gpu, True)
+    up.save(p_orc, True)
+    # reference-format files load into the other implementation
+    up2 = O.Updater(**kw)
+    up2.load(p_gpu)
+    c2 = H.Context(0, max_keys=1 << 12, **kw)
+    st2 = H.Store(c2)
+    st2.load(p_orc)
+    _pull_eq(H, c2, st2, up2, keys)
+    assert st2.stats()["n_keys"] == up2.size()
+    st.dump(str(tmp_path / "dump.txt"), True, True)
+    assert sum(1 for _ in open(tmp_path / "dump.txt")) == up2.size()
+
+
+# ---------------------------------------------------------------- fused minibatch
+def test_fused_sgd_learner_basic(H, rcv1, known):
+    """SGDLearner.Basic (tests/cpp/sgd_learner_test.cc:9-49) through dfx_train_step."""
+    k = known["sgd_learner_basic"]
+    kw = k["kwargs"]
+    c = H.Context(0, V_dim=kw["V_dim"], l2=kw["l2"], l1=kw["l1"], lr=kw["lr"], max_keys=1 << 14)
+    db = H.DeviceRowBlock(c, rcv1)
+    for ep, want in enumerate(k["objv"]):
+        H.train_step(c, db, H.kTraining, push_cnt=False)
+        p = H.progress(c)
+        assert abs(p["loss"] - want) < k["tol"], (ep, p["loss"], want)
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(V_dim=4, V_threshold=2, lr=.1, V_lr=.01, l1=.1),
+    dict(V_dim=2, lr=.02, V_lr=.001, V_threshold=1, l1=0.05),    # C1-like (FM d=2)
+    dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01),          # C3-like, all keys get V
+])
+def test_fused_matches_oracle_rcv1(H, rcv1, cfg):
+    c = H.Context(0, max_keys=1 << 14, **cfg)
+    up = O.Updater(**cfg)
+    db = H.DeviceRowBlock(c, rcv1)
+    halves = [rcv1.slice(0, 50), rcv1.slice(50, 100)]
+    dhalves = [H.DeviceRowBlock(c, h) for h in halves]
+    for ep in range(6):
+        for hb, dh in zip(halves, dhalves):
+            loss, auc = up.train_step(hb.offs, hb.ids, hb.vals, hb.labels, push_cnt=(ep == 0))
+            H.train_step(c, dh, H.kTraining, push_cnt=(ep == 0))
+            p = H.progress(c)
+            assert abs(p["loss"] - loss) <= 1e-4 * max(1, abs(loss)), (ep, p["loss"], loss)
+            assert abs(p["auc"] - auc) <= 1e-4 * hb.size, (ep, p["auc"], auc)
+    st = H.Store(c)
+    uniq, _, _ = O.localize(rcv1.offs, rcv1.ids)
+    v, l = st.pull(c.tensor(uniq, torch.int64))
+    ov, ol = up.get(uniq)
+    assert np.array_equal(l.cpu().numpy(), ol)
+    assert close(v.cpu().numpy(), ov, rtol=1e-4)
+    assert st.stats()["seed"] == up.seed
+
+
+def test_fused_criteo_like_vs_oracle(H):
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    c = H.Context(0, max_keys=1 << 18, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(3000, 39, 1 << 16, seed=50 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        db = H.DeviceRowBlock(c, blk)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, db, H.kTraining, push_cnt=(step < 2), pred=pred)
+        p = H.progress(c)
+        assert close(pred.cpu().numpy(), opred, rtol=1e-4)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss)
+        assert abs(p["auc"] - auc) <= 1e-4 * blk.size
+    s = H.Store(c).stats()
+    assert s["seed"] == up.seed and s["n_keys"] == up.size()
+
+
+def test_fused_validation_does_not_update(H, rcv1):
+    c = H.Context(0, V_dim=4, V_threshold=0, l1=0, lr=.1, max_keys=1 << 14)
+    db = H.DeviceRowBlock(c, rcv1)
+    H.train_step(c, db, H.kTraining, push_cnt=True)
+    H.progress(c)
+    st = H.Store(c)
+    uniq, _, _ = O.localize(rcv1.offs, rcv1.ids)
+    before = st.pull(c.tensor(uniq, torch.int64))[0].cpu().numpy()
+    H.train_step(c, db, H.kValidation)
+    p = H.progress(c)
+    after = st.pull(c.tensor(uniq, torch.int64))[0].cpu().numpy()
+    assert np.array_equal(before, after) and p["nrows"] == 100
+
+
+def test_fused_empty_and_tiny(H):
+    c = H.Context(0, V_dim=8, V_threshold=0, l1=0, max_keys=1 << 12)
+    blk = D.RowBlock(np.array([0, 0, 3, 3], np.uint64), np.array([5, 9, 5], np.uint64), None,
+                     np.array([1, -1, 1], np.float32))
+    up = O.Updater(V_dim=8, V_threshold=0, l1=0)
+    for ep in range(3):
+        loss, auc = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels, push_cnt=(ep == 0))
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(ep == 0))
+        p = H.progress(c)
+        assert abs(p["loss"] - loss) <= 1e-5 * abs(loss) and p["auc"] == pytest.approx(auc)
