@@ -41,6 +41,7 @@ _SIGS = {
     "dfx_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(vp)]),
     "dfx_ctx_destroy": (ctypes.c_int, [vp]),
     "dfx_ctx_set_stream": (ctypes.c_int, [vp, vp]),
+    "dfx_ctx_use_own_stream": (ctypes.c_int, [vp]),
     "dfx_ctx_vdim": (ctypes.c_int, [vp]),
     "dfx_sync": (ctypes.c_int, [vp]),
     "dfx_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),

@@ -160,7 +160,14 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
 
 int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream) {
   DFX_CHECK_ARG(ctx, "null ctx");
-  ctx->c.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->c.own_stream;
+  // NULL is HIP's null (legacy default) stream, which is also torch's default stream
+  ctx->c.stream = static_cast<hipStream_t>(hip_stream);
+  return DFX_OK;
+}
+
+int dfx_ctx_use_own_stream(dfx_ctx* ctx) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  ctx->c.stream = ctx->c.own_stream;
   return DFX_OK;
 }
 

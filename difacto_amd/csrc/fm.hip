@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         if (w != 0.f) acc = valued ? acc + w * x : acc + w;
       }
       if (vp >= 0) {
-        const float* V = a.Vbase + vp;
+        const float* V = PACKED ? a.Vbase + (int64_t)vp * d : a.Vbase + vp;
         const float xx = x * x;  // XX_ (fm_loss.h:86-92)
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     }
     float acc[CPL];
     if (vq >= 0) {
-      const float* V = FUSED ? (a.T.V + vq) : (a.W + vq);
+      const float* V = FUSED ? (a.T.V + (int64_t)vq * d) : (a.W + vq);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int cd = l + k * G;
@@ -263,8 +263,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       bool tr;
       int dw = ftrl_update(a.Pm, gw, &e, &tr);
       if (vq >= 0) {
-        float* V = a.T.V + vq;
-        float* C = a.T.Vaux + vq;
+        float* V = a.T.V + (int64_t)vq * d;
+        float* C = a.T.Vaux + (int64_t)vq * d;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
           const int cd = l + k * G;

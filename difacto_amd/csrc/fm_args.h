@@ -9,7 +9,7 @@ struct FwdArgs {
   const uint64_t* offs;
   const uint32_t* col;
   const float* val;
-  // weights: packed {w, V offset} per column (fused) or interleaved weights + positions
+  // weights: packed {w, V pool row} per column (fused) or interleaved weights + positions
   const int2* wv;
   const float* W;
   const int32_t* wpos;

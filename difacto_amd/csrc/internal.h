@@ -114,7 +114,9 @@ int radix_sort_pairs(Context* c, K* k0, uint32_t* v0, K* k1, uint32_t* v1, int64
                      unsigned int* sortmeta);
 
 // exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
-int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev);
+// n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.
+int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
+             const uint32_t* n_dev = nullptr);
 
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
 void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);

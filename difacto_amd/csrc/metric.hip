@@ -18,7 +18,7 @@ __global__ void k_auc_keys(int64_t B, const float* label, const float* pred, uin
                            uint32_t* v) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
-  uint32_t u = __float_as_uint(pred[i]);
+  uint32_t u = __float_as_uint(pred[i] + 0.0f);  // -0 == +0, as operator< sees them
   u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
   k[i] = u;
   v[i] = label[i] > 0 ? 1u : 0u;

@@ -211,9 +211,19 @@ constexpr int kScanNT = 256;
 constexpr int kScanItems = 8;
 constexpr int kScanTile = kScanNT * kScanItems;
 
-__global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, int64_t n,
+// Entries at index >= *n_dev (when n_dev is given) count as zero: callers size the grid by a
+// host-known bound while the live count (U) stays on the device.
+__device__ inline int64_t scan_limit(int64_t n, const uint32_t* n_dev) {
+  if (!n_dev) return n;
+  const int64_t m = (int64_t)*n_dev;
+  return m < n ? m : n;
+}
+
+__global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, int64_t n0,
+                                                         const uint32_t* n_dev,
                                                          uint32_t* tilesum) {
   __shared__ uint32_t lds[kScanNT / kWave + 1];
+  const int64_t n = scan_limit(n0, n_dev);
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   uint32_t s = 0;
 #pragma unroll
@@ -238,9 +248,11 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint32_t* tilesum, int64_t nt
   if (threadIdx.x == 0 && total) *total = run;
 }
 
-__global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t n,
+__global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t n0,
+                                                        const uint32_t* n_dev,
                                                         const uint32_t* tilesum) {
   __shared__ uint32_t lds[kScanNT / kWave + 1];
+  const int64_t n = scan_limit(n0, n_dev);
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
   uint32_t v[kScanItems];
   uint32_t s = 0;
@@ -261,7 +273,8 @@ void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* tot
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, tilesum, ntiles, total_dev);
 }
 
-int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev) {
+int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
+             const uint32_t* n_dev) {
   if (n <= 0) {
     if (total_dev) DFX_HIP(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), c->stream));
     return DFX_OK;
@@ -269,9 +282,11 @@ int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev) {
   const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
   DFX_TRY(c->ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = c->ws.tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, ts);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, n_dev,
+                     ts);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, ts, ntiles, total_dev);
-  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, ts);
+  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, n_dev,
+                     ts);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -78,7 +78,7 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
               const uint32_t* slot) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
-  DFX_TRY(scan_u32(c, flags, n_bound, total_dev));
+  DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &c->ds->u_count));
   hipLaunchKernelGGL(k_initv, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
                      n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds);
   hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kStNT) void k_resolve_pull(int64_t n_host, const ui
       float w = T.st[s].x;
       int vr = T.vrow[s];
       bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
-      wv[u] = make_int2(__float_as_int(w), live ? vr * T.d : -1);
+      wv[u] = make_int2(__float_as_int(w), live ? vr : -1);  // V row index
       slot[u] = (uint32_t)s;
     }
   }

@@ -84,7 +84,10 @@ typedef struct dfx_progress {
 const char* dfx_last_error(void);
 int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out);
 int dfx_ctx_destroy(dfx_ctx* ctx);
-int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+/* A new context queues work on its own non-blocking stream.  set_stream switches to the given
+ * hipStream_t (NULL = the null stream, torch's default); use_own_stream switches back. */
+int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream);
+int dfx_ctx_use_own_stream(dfx_ctx* ctx);
 int dfx_ctx_vdim(dfx_ctx* ctx);
 int dfx_sync(dfx_ctx* ctx); /* waits for the stream and reports deferred device errors */
 int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes);

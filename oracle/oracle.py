@@ -154,6 +154,29 @@ def auc(label, pred):
     return lib().orc_auc(len(pred), _p(label, f32p), _p(pred, f32p))
 
 
+def auc_stable_ties(label, pred):
+    """BinClassMetric::AUC (bin_class_metric.h:35-57) with ties between equal predictions
+    kept in input order.  The reference sorts with the unstable std::sort, so its value on
+    tied predictions (e.g. the all-zero first batch, or clipped +-20) is unspecified; the
+    device path breaks ties by input order, and tie-heavy checks compare against this."""
+    label = np.asarray(label, np.float32)
+    pred = np.asarray(pred, np.float32) + np.float32(0.0)
+    n = len(pred)
+    lab = (label[np.argsort(pred, kind="stable")] > 0).astype(np.float64)
+    before = np.cumsum(lab) - lab
+    area = float(before[lab == 0].sum())
+    P = float(lab.sum())
+    if P == 0 or P == n:
+        return 1.0
+    area /= P * (n - P)
+    return (1 - area if area < 0.5 else area) * n
+
+
+def has_ties(pred):
+    p = np.asarray(pred, np.float32) + np.float32(0.0)
+    return len(np.unique(p)) != len(p)
+
+
 def get_pos(lens):
     lens = _c(lens, np.int32)
     n = len(lens)

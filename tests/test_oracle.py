@@ -108,3 +108,12 @@ def test_save_load_roundtrip(rcv1, tmp_path):
     a, la = up.get(uniq)
     b, lb = up2.get(uniq)
     assert np.array_equal(a, b) and np.array_equal(la, lb)
+
+
+def test_auc_tie_convention_agrees_without_ties():
+    rng = np.random.default_rng(5)
+    for n in (10, 100, 5000):
+        label = np.where(rng.random(n) < 0.3, 1.0, -1.0).astype(np.float32)
+        pred = rng.permutation(np.linspace(-3, 3, n)).astype(np.float32)
+        assert not O.has_ties(pred)
+        assert abs(O.auc_stable_ties(label, pred) - O.auc(label, pred)) <= 1e-4 * n
