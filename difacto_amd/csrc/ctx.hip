@@ -127,6 +127,12 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
     set_error("hipMalloc(DevState) failed");
     return DFX_ERR_HIP;
   }
+  if (hipMalloc(&c->zpad, 1024 * sizeof(float)) != hipSuccess ||
+      hipMemset(c->zpad, 0, 1024 * sizeof(float)) != hipSuccess) {
+    set_error("hipMalloc(zpad) failed");
+    dfx_ctx_destroy(ctx);
+    return DFX_ERR_HIP;
+  }
   DevState init;
   memset(&init, 0, sizeof(init));
   init.seed = kw.seed;
@@ -151,7 +157,16 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
                     &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch};
   for (DevBuf* b : bufs) b->release();
+  w.occ_row.release();
+  w.occ_x.release();
+  w.ak0.release();
+  w.ak1.release();
+  w.av0.release();
+  w.av1.release();
+  w.atiles.release();
+  for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   table_release(c);
+  if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete ctx;

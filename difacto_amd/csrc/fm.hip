@@ -6,13 +6,18 @@
 // exactly the reference's (row, nnz) order; the V_dim-reduction is then done serially over
 // coordinates through wave shuffles — predictions are bit-identical to the reference.
 // At V_dim 16 a wave holds 4 rows and every gathered V row is one 64-byte segment.
+// The walk is latency-bound (col -> {w, V row} -> V), so each iteration first issues the
+// loads of UNR nnz (clamped, unconditional addresses) and only then accumulates them in
+// order: UNR independent gathers in flight per group instead of one.
 //
 // Backward (k_fm_bwd): Xᵀ products as a sorted-key segmented reduction — no atomics.  A
 // group of G lanes owns one column (unique key); it walks that key's occurrences in the
 // Localizer's sorted (key, pos) order, i.e. ascending (row, nnz): the same order as the
 // reference's column-range-partitioned TransTimes, so gradients are deterministic and, up
-// to expf, bit-identical.  In the fused step the same walk ends in the FTRL/AdaGrad update
-// of the key (no gradient round trip through HBM).
+// to expf, bit-identical.  The Localizer already wrote each occurrence's row (and value) in
+// sorted order, so the walk is occ_row -> {p, XV*p row}; the key's own state is loaded up
+// front, independent of the walk.  In the fused step the walk ends in the FTRL/AdaGrad
+// update of the key (no gradient round trip through HBM).
 #include "fm_args.h"
 
 namespace dfx {
@@ -33,11 +38,10 @@ __device__ inline float logit_p(float label, float pred, const float* rw, int64_
   return p;
 }
 
-
-
 template <int G, int CPL, int MODE, bool PACKED>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   constexpr int RPB = kFmNT / G;  // rows per block
+  constexpr int UNR = CPL <= 2 ? 8 : (CPL <= 4 ? 4 : 2);
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t r = (int64_t)blockIdx.x * RPB + g;
@@ -51,35 +55,67 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 #pragma unroll
     for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
     const bool valued = a.val != nullptr;
-    for (uint64_t j = o0; j < o1; ++j) {
-      const uint32_t c = a.col[j];
-      const float x = valued ? a.val[j] : 1.f;
-      float w;
-      int vp;
-      if (PACKED) {
-        int2 e = a.wv[c];
-        w = __int_as_float(e.x);
-        vp = e.y;
-      } else {
-        if (a.wpos) { int q = a.wpos[c]; w = q < 0 ? 0.f : a.W[q]; } else { w = a.W[c]; }
-        vp = d > 0 ? a.vpos[c] : -1;
+    for (uint64_t j0 = o0; j0 < o1; j0 += UNR) {
+      uint32_t c[UNR];
+      float x[UNR];
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        const uint64_t jj = (j0 + t < o1) ? j0 + t : o1 - 1;
+        c[t] = a.col[jj];
+        x[t] = valued ? a.val[jj] : 1.f;
       }
-      if (MODE != kGradPrep) {
-        // SpMV::Times skips w == 0 (spmv.h:124-125)
-        if (w != 0.f) acc = valued ? acc + w * x : acc + w;
+      float w[UNR];
+      int vp[UNR];
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        if (PACKED) {
+          const int2 e = a.wv[c[t]];
+          w[t] = __int_as_float(e.x);
+          vp[t] = e.y;
+        } else {
+          if (a.wpos) {
+            const int q = a.wpos[c[t]];
+            w[t] = a.W[q < 0 ? 0 : q];
+            if (q < 0) w[t] = 0.f;
+          } else {
+            w[t] = a.W[c[t]];
+          }
+          vp[t] = d > 0 ? a.vpos[c[t]] : -1;
+        }
       }
-      if (vp >= 0) {
-        const float* V = PACKED ? a.Vbase + (int64_t)vp * d : a.Vbase + vp;
-        const float xx = x * x;  // XX_ (fm_loss.h:86-92)
+      float v[UNR][CPL];
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        const float* Vr = vp[t] < 0 ? a.zpad
+                                    : (PACKED ? a.Vbase + (int64_t)vp[t] * d : a.Vbase + vp[t]);
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
           const int cd = l + k * G;
-          if (cd < d) {
-            const float v = V[cd];
-            xv[k] = valued ? xv[k] + v * x : xv[k] + v;
-            if (MODE != kGradPrep) {
-              const float vv = v * v;  // VV (fm_loss.h:95-101)
-              xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
+          v[t][k] = Vr[cd < d ? cd : 0];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        if (j0 + t >= o1) {  // past the row: a no-op item (w == 0 is skipped, no V)
+          w[t] = 0.f;
+          vp[t] = -1;
+        }
+        if (MODE != kGradPrep) {
+          // SpMV::Times skips w == 0 (spmv.h:124-125)
+          if (w[t] != 0.f) acc = valued ? acc + w[t] * x[t] : acc + w[t];
+        }
+        if (vp[t] >= 0) {
+          const float xx = x[t] * x[t];  // XX_ (fm_loss.h:86-92)
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const int cd = l + k * G;
+            if (cd < d) {
+              const float vk = v[t][k];
+              xv[k] = valued ? xv[k] + vk * x[t] : xv[k] + vk;
+              if (MODE != kGradPrep) {
+                const float vv = vk * vk;  // VV (fm_loss.h:95-101)
+                xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
+              }
             }
           }
         }
@@ -183,11 +219,10 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
 }
 
 // ---- backward: sorted-key segmented reduction --------------------------------------------
-
-
 template <int G, int CPL, bool FUSED>
 __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   constexpr int SPB = kFmNT / G;
+  constexpr int UNR = CPL <= 2 ? 4 : 2;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t u = (int64_t)blockIdx.x * SPB + g;
@@ -195,55 +230,149 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   __shared__ int red[kFmNT / kWave];
   int dnew = 0;
   if (u < nseg) {
-    const uint32_t* P = (a.P1 && a.ds->sortmeta[31]) ? a.P1 : a.P;
     const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
-    const bool valued = a.val != nullptr;
+    const bool valued = a.occ_x != nullptr;
     const int d = a.d;
-    float gw, xxp = 0.f;
-    int wq = -1, vq = -1;
+    // ---- the key's own operands first: they do not depend on the walk
+    int wq = -1, vq = -1, vrow = -1;
+    uint32_t sl = 0;
+    float gw = 0.f;
+    float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+    float vcur[CPL], ccur[CPL], g0[CPL];
     if (FUSED) {
-      gw = 0.f;
       vq = a.wv[cidx].y;
-    } else {
-      wq = a.wpos ? a.wpos[cidx] : (int)cidx;
-      gw = wq >= 0 ? a.grad[wq] : 0.f;
-      vq = d > 0 ? a.vpos[cidx] : -1;
-    }
-    // SpMV::TransTimes for g_w and XXp (spmv.h:139-171): skip p == 0
-    for (uint32_t i = s0; i < s1; ++i) {
-      const uint32_t pos = P[i];
-      const float pr = a.p[a.rowid[pos]];
-      if (pr == 0.f) continue;
-      if (valued) {
-        const float x = a.val[pos];
-        gw += pr * x;
-        xxp += pr * (x * x);
-      } else {
-        gw += pr;
-        xxp += pr;
-      }
-    }
-    float acc[CPL];
-    if (vq >= 0) {
-      const float* V = FUSED ? (a.T.V + (int64_t)vq * d) : (a.W + vq);
+      sl = a.slot[cidx];
+      e = a.T.st[sl];
+      vrow = a.T.vrow[sl];
+      const float* Vr = vq >= 0 ? a.T.V + (int64_t)vq * d : a.zpad;
+      const float* Cr = vq >= 0 ? a.T.Vaux + (int64_t)vq * d : a.zpad;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int cd = l + k * G;
-        if (cd < d) {
-          const float g0 = FUSED ? 0.f : a.grad[vq + cd];
-          acc[k] = g0 - V[cd] * xxp;  // grad_u -= diag(XXp) V (fm_loss.h:185-192)
-        }
+        vcur[k] = Vr[cd < d ? cd : 0];
+        ccur[k] = Cr[cd < d ? cd : 0];
+        g0[k] = 0.f;
       }
-      // SpMM::TransTimes (spmm.h:127-159): += (XV_ p) x, no zero skip
-      for (uint32_t i = s0; i < s1; ++i) {
-        const uint32_t pos = P[i];
-        const float* xr = a.XVp + (int64_t)a.rowid[pos] * d;
-        const float x = valued ? a.val[pos] : 1.f;
+    } else {
+      wq = a.wpos ? a.wpos[cidx] : (int)cidx;
+      vq = d > 0 ? a.vpos[cidx] : -1;
+      gw = a.grad[wq < 0 ? 0 : wq];
+      if (wq < 0) gw = 0.f;
+      const float* Vr = vq >= 0 ? a.W + vq : a.zpad;
+      const float* Gr = vq >= 0 ? a.grad + vq : a.zpad;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int cd = l + k * G;
+        vcur[k] = Vr[cd < d ? cd : 0];
+        g0[k] = Gr[cd < d ? cd : 0];
+        ccur[k] = 0.f;
+      }
+    }
+    float xxp = 0.f;
+    float acc[CPL];
+    // ---- pass 1: g_w and XXp (SpMV::TransTimes, spmv.h:139-171: skip p == 0)
+    // ---- pass 2: grad_u = (g0 - V*XXp) + sum (XV_ p) x (fm_loss.h:185-202, spmm.h:127-159)
+    // Both sums run in occurrence order; a segment of <= UNR occurrences (the common case)
+    // issues every load of both passes at once.
+    const uint32_t len = s1 - s0;
+    if (len <= (uint32_t)UNR) {
+      uint32_t row[UNR];
+      float x[UNR], pr[UNR], xr[UNR][CPL];
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        const uint32_t i = s0 + ((uint32_t)t < len ? (uint32_t)t : 0u);
+        row[t] = a.occ_row[i];
+        x[t] = valued ? a.occ_x[i] : 1.f;
+      }
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        pr[t] = a.p[row[t]];
+        const float* xrow = d > 0 ? a.XVp + (int64_t)row[t] * d : a.zpad;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
           const int cd = l + k * G;
-          if (cd < d) acc[k] = valued ? acc[k] + xr[cd] * x : acc[k] + xr[cd];
+          xr[t][k] = xrow[cd < d ? cd : 0];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < UNR; ++t) {
+        if ((uint32_t)t < len && pr[t] != 0.f) {
+          if (valued) {
+            gw += pr[t] * x[t];
+            xxp += pr[t] * (x[t] * x[t]);
+          } else {
+            gw += pr[t];
+            xxp += pr[t];
+          }
+        }
+      }
+      if (vq >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          if ((uint32_t)t < len) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+              acc[k] = valued ? acc[k] + xr[t][k] * x[t] : acc[k] + xr[t][k];
+          }
+        }
+      }
+    } else {
+      for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+        uint32_t row[UNR];
+        float x[UNR], pr[UNR];
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
+          row[t] = a.occ_row[i];
+          x[t] = valued ? a.occ_x[i] : 1.f;
+        }
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) pr[t] = a.p[row[t]];
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          if (i0 + t < s1 && pr[t] != 0.f) {
+            if (valued) {
+              gw += pr[t] * x[t];
+              xxp += pr[t] * (x[t] * x[t]);
+            } else {
+              gw += pr[t];
+              xxp += pr[t];
+            }
+          }
+        }
+      }
+      if (vq >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
+        for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+          uint32_t row[UNR];
+          float x[UNR], xr[UNR][CPL];
+#pragma unroll
+          for (int t = 0; t < UNR; ++t) {
+            const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
+            row[t] = a.occ_row[i];
+            x[t] = valued ? a.occ_x[i] : 1.f;
+          }
+#pragma unroll
+          for (int t = 0; t < UNR; ++t) {
+            const float* xrow = a.XVp + (int64_t)row[t] * d;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+              const int cd = l + k * G;
+              xr[t][k] = xrow[cd < d ? cd : 0];
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < UNR; ++t) {
+            if (i0 + t < s1) {
+#pragma unroll
+              for (int k = 0; k < CPL; ++k)
+                acc[k] = valued ? acc[k] + xr[t][k] * x[t] : acc[k] + xr[t][k];
+            }
+          }
         }
       }
     }
@@ -258,24 +387,26 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       }
     } else {
       // Update(kGradient): UpdateW (FTRL), then UpdateV (AdaGrad) if V was pulled
-      const uint32_t sl = a.slot[cidx];
-      float4 e = a.T.st[sl];
       bool tr;
-      int dw = ftrl_update(a.Pm, gw, &e, &tr);
+      const int dw = ftrl_update(a.Pm, gw, &e, &tr);
       if (vq >= 0) {
         float* V = a.T.V + (int64_t)vq * d;
         float* C = a.T.Vaux + (int64_t)vq * d;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
           const int cd = l + k * G;
-          if (cd < d) adagrad_update(a.Pm, acc[k], V + cd, C + cd);
+          if (cd < d) {
+            adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
+            V[cd] = vcur[k];
+            C[cd] = ccur[k];
+          }
         }
       }
       if (l == 0) {
         a.T.st[sl] = e;
         dnew = dw;
-        // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121)
-        bool need = tr && d > 0 && a.T.vrow[sl] < 0 && e.w > (float)a.Pm.V_threshold;
+        // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
+        const bool need = tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
         a.flags[u] = need ? 1u : 0u;
       }
     }
@@ -338,12 +469,18 @@ __global__ void k_csc_heads(const uint32_t* k0, const uint32_t* k1, int64_t n,
   flags[i] = (i == 0 || K[i] != K[i - 1]) ? 1u : 0u;
 }
 
-__global__ void k_csc_segs(const uint32_t* k0, const uint32_t* k1, int64_t n,
-                           const DevState* ds, const uint32_t* excl, uint32_t* segstart,
-                           uint32_t* segcol, const uint32_t* total) {
+__global__ void k_csc_segs(const uint32_t* k0, const uint32_t* k1, const uint32_t* p0,
+                           const uint32_t* p1, int64_t n, const DevState* ds,
+                           const uint32_t* excl, uint32_t* segstart, uint32_t* segcol,
+                           const uint32_t* total, const uint32_t* rowid, const float* val,
+                           uint32_t* occ_row, float* occ_x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t* K = ds->sortmeta[31] ? k1 : k0;
+  const uint32_t* P = ds->sortmeta[31] ? p1 : p0;
+  const uint32_t pos = P[i];
+  occ_row[i] = rowid[pos];
+  if (val) occ_x[i] = val[pos];
   const bool head = (i == 0 || K[i] != K[i - 1]);
   if (head) {
     segstart[excl[i]] = (uint32_t)i;
@@ -374,7 +511,7 @@ extern "C" int dfx_fm_predict(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64
   (void)n_cols;
   FwdArgs a{};
   a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
-  a.vpos = V_pos; a.Vbase = weights; a.d = V_dim; a.pred = pred;
+  a.vpos = V_pos; a.Vbase = weights; a.zpad = ctx->c.zpad; a.d = V_dim; a.pred = pred;
   return launch_fwd<kPredict, false>(a, ctx->c.stream);
 }
 
@@ -401,14 +538,16 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   DFX_TRY(ws.flags.ensure((nnz + 1) * 4));
   DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(ws.slot.ensure((nnz + 1) * 4));
+  DFX_TRY(ws.occ_row.ensure(nnz * 4));
+  DFX_TRY(ws.occ_x.ensure(nnz * 4));
   DFX_TRY(ws.cnt.ensure(4 * 4));
   // 1) p and XV*p per row
   FwdArgs a{};
   a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
-  a.vpos = V_pos; a.Vbase = weights; a.d = V_dim; a.label = label; a.rw = row_weight;
-  a.pred_in = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
+  a.vpos = V_pos; a.Vbase = weights; a.zpad = c->zpad; a.d = V_dim; a.label = label;
+  a.rw = row_weight; a.pred_in = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
   DFX_TRY((launch_fwd<kGradPrep, false>(a, c->stream)));
-  // 2) CSC order: stable sort of (col, pos)
+  // 2) CSC order: stable sort of (col, pos); occurrences' rows/values in that order
   uint32_t* k0 = ws.keys0.as<uint32_t>();
   uint32_t* k1 = ws.keys1.as<uint32_t>();
   hipLaunchKernelGGL(k_csc_prep, dim3((B + 255) / 256), dim3(256), 0, c->stream, B, offset, col,
@@ -421,18 +560,21 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   hipLaunchKernelGGL(k_csc_heads, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, k0, k1, nnz,
                      c->ds, flags);
   DFX_TRY(scan_u32(c, flags, nnz, total));
-  hipLaunchKernelGGL(k_csc_segs, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, k0, k1, nnz,
-                     c->ds, flags, ws.segstart.as<uint32_t>(), ws.slot.as<uint32_t>(), total);
+  hipLaunchKernelGGL(k_csc_segs, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, k0, k1,
+                     ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>(), nnz, c->ds, flags,
+                     ws.segstart.as<uint32_t>(), ws.slot.as<uint32_t>(), total,
+                     ws.rowid.as<uint32_t>(), value, ws.occ_row.as<uint32_t>(),
+                     ws.occ_x.as<float>());
   // 3) segmented reduction into grad
   BwdArgs b{};
   b.segstart = ws.segstart.as<uint32_t>();
   b.ds = c->ds;
   b.nseg_host = -1;
   b.segcol = ws.slot.as<uint32_t>();
-  b.P = ws.vals0.as<uint32_t>();
-  b.P1 = ws.vals1.as<uint32_t>();
-  b.rowid = ws.rowid.as<uint32_t>();
-  b.val = value; b.p = ws.p.as<float>(); b.XVp = ws.XVp.as<float>(); b.d = V_dim;
+  b.occ_row = ws.occ_row.as<uint32_t>();
+  b.occ_x = value ? ws.occ_x.as<float>() : nullptr;
+  b.zpad = c->zpad;
+  b.p = ws.p.as<float>(); b.XVp = ws.XVp.as<float>(); b.d = V_dim;
   b.wpos = w_pos; b.vpos = V_pos; b.W = weights; b.grad = grad;
   // the number of segments is device-side; store it where k_fm_bwd reads it
   DFX_HIP(hipMemcpyAsync(&c->ds->u_count, total, sizeof(uint32_t), hipMemcpyDeviceToDevice,

@@ -15,6 +15,7 @@ struct FwdArgs {
   const int32_t* wpos;
   const int32_t* vpos;
   const float* Vbase;
+  const float* zpad;     // >= 1024 device zeros: target of masked (clamped) gathers
   int d;
   const float* label;
   const float* rw;
@@ -30,10 +31,9 @@ struct BwdArgs {
   const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
   int64_t nseg_host;
   const uint32_t* segcol;    // column of each segment (NULL: segment index == column)
-  const uint32_t* P;         // sorted nnz positions, buffer 0 ...
-  const uint32_t* P1;        // ... or buffer 1, chosen by ds->sortmeta[31]
-  const uint32_t* rowid;
-  const float* val;
+  const uint32_t* occ_row;   // row of every occurrence, in sorted (key, pos) order
+  const float* occ_x;        // its value (NULL: binary data)
+  const float* zpad;
   const float* p;
   const float* XVp;
   int d;

@@ -74,6 +74,7 @@ struct Workspace {
   DevBuf tiles;    // per-tile scan partials
   // per-unique arrays
   DevBuf uniq, cnt, segstart, col, slot, flags, wb, Vb, vpos;
+  DevBuf occ_row, occ_x;  // per occurrence in sorted order (backward walk)
   // per-row arrays
   DevBuf p, pred, XVp, rowtmp;
   DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
@@ -91,6 +92,7 @@ struct Context {
   Table T{};
   int64_t cap = 0;
   DevState* ds = nullptr;  // device
+  float* zpad = nullptr;   // 1024 device zeros (masked-gather target)
   Workspace ws;
   // per-phase HIP-event timing of dfx_train_step (dfx_prof_*); events on c->stream
   std::vector<hipEvent_t> prof_ev;  // prof_max steps x kProfMarks
@@ -124,9 +126,12 @@ void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* tot
 // Localizer::Compact on the device.  Leaves in the workspace: the sorted (key, pos)
 // pairs (buffer selected by ds->sortmeta[31]), rowid[nnz] when want_rowid, U in
 // ds->u_count.  Writes uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].
+// With occ_row (and occ_x when value != NULL) it also writes every occurrence's row (and
+// value) in sorted order, for the backward walk.
 int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, uint64_t* uniq, float* cnt,
-                 uint32_t* col, uint32_t* segstart, bool want_rowid);
+                 uint32_t* col, uint32_t* segstart, const float* value, uint32_t* occ_row,
+                 float* occ_x);
 
 int ws_reserve(Context* c, int64_t rows, int64_t nnz);
 

@@ -90,7 +90,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const 
 __global__ __launch_bounds__(kLocNT) void k_loc_write(
     const uint64_t* k0, const uint64_t* k1, const uint32_t* p0, const uint32_t* p1, int64_t n,
     DevState* ds, const uint32_t* tilebase, uint64_t* __restrict__ uniq,
-    uint32_t* __restrict__ col, uint32_t* __restrict__ segstart) {
+    uint32_t* __restrict__ col, uint32_t* __restrict__ segstart, const uint32_t* rowid,
+    const float* value, uint32_t* __restrict__ occ_row, float* __restrict__ occ_x) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   const bool s1 = ds->sortmeta[31] != 0;
   const uint64_t* K = s1 ? k1 : k0;
@@ -120,7 +121,10 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(
       uniq[rank] = k[i];
       if (segstart) segstart[rank] = (uint32_t)idx;
     }
-    col[P[idx]] = rank;
+    const uint32_t pos = P[idx];
+    col[pos] = rank;
+    if (occ_row) occ_row[idx] = rowid[pos];
+    if (occ_x) occ_x[idx] = value[pos];
     if (idx == n - 1) {
       ds->u_count = rank + 1;
       if (segstart) segstart[rank + 1] = (uint32_t)n;
@@ -138,7 +142,8 @@ __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, uint64_t* uniq, float* cnt,
-                 uint32_t* col, uint32_t* segstart, bool want_rowid) {
+                 uint32_t* col, uint32_t* segstart, const float* value, uint32_t* occ_row,
+                 float* occ_x) {
   Workspace& ws = c->ws;
   DFX_CHECK_ARG(max_index != 0, "localize: max_index must be > 0");
   DFX_CHECK_ARG(nnz < (int64_t)0xFFFFFFFFll, "localize: nnz must fit u32 (localizer.cc:16)");
@@ -148,6 +153,7 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
+  const bool want_rowid = occ_row != nullptr;
   DFX_TRY(ws.keys0.ensure(nnz * 8));
   DFX_TRY(ws.keys1.ensure(nnz * 8));
   DFX_TRY(ws.vals0.ensure(nnz * 4));
@@ -176,7 +182,9 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
   scan_tiles_top(c, ts, ntiles, nullptr);
   hipLaunchKernelGGL(k_loc_write, dim3(ntiles), dim3(kLocNT), 0, c->stream,
                      ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>(), ws.vals0.as<uint32_t>(),
-                     ws.vals1.as<uint32_t>(), nnz, c->ds, ts, uniq, col, segs);
+                     ws.vals1.as<uint32_t>(), nnz, c->ds, ts, uniq, col, segs,
+                     want_rowid ? ws.rowid.as<uint32_t>() : nullptr, value, occ_row,
+                     (occ_row && value) ? occ_x : nullptr);
   if (cnt) {
     hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, c->ds, segs,
                        cnt, nnz);
@@ -196,7 +204,8 @@ extern "C" int dfx_localize(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t
   Context* c = &ctx->c;
   DFX_CHECK_ARG(B >= 0 && nnz >= 0, "localize: negative sizes");
   DFX_CHECK_ARG(nnz == 0 || (offset && index && uniq && col), "localize: null buffer");
-  DFX_TRY(localize_run(c, B, nnz, offset, index, max_index, uniq, cnt, col, nullptr, false));
+  DFX_TRY(localize_run(c, B, nnz, offset, index, max_index, uniq, cnt, col, nullptr, nullptr,
+                       nullptr, nullptr));
   if (n_uniq) {
     unsigned u = 0;
     DFX_HIP(hipMemcpyAsync(&u, &c->ds->u_count, sizeof(unsigned), hipMemcpyDeviceToHost,

@@ -42,6 +42,8 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(ws.slot.ensure((nnz + 1) * 4));
   DFX_TRY(ws.flags.ensure((nnz + 1) * 4));
   DFX_TRY(ws.wb.ensure(nnz * 8));
+  DFX_TRY(ws.occ_row.ensure(nnz * 4));
+  DFX_TRY(ws.occ_x.ensure(nnz * 4));
   DFX_TRY(ws.p.ensure(rows * 4));
   DFX_TRY(ws.pred.ensure(rows * 4));
   if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * d * 4));
@@ -83,8 +85,10 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   float* pred = pred_out ? pred_out : ws.pred.as<float>();
 
   prof_mark(c, 0);
+  uint32_t* occ_row = ws.occ_row.as<uint32_t>();
+  float* occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
   DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, uniq, nullptr, col, segstart,
-                       true));
+                       b->value, occ_row, occ_x));
   prof_mark(c, 1);
   if (push_cnt && d > 0) DFX_TRY(push_cnt_run(c, -1, nnz, uniq, nullptr, segstart, slot, flags,
                                               total));
@@ -94,6 +98,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
 
   FwdArgs a{};
   a.B = B; a.offs = b->offset; a.col = col; a.val = b->value; a.wv = wv; a.Vbase = c->T.V;
+  a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>();
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -107,8 +112,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
     BwdArgs g{};
     g.segstart = segstart; g.ds = c->ds; g.nseg_host = -1; g.segcol = nullptr;
-    g.P = ws.vals0.as<uint32_t>(); g.P1 = ws.vals1.as<uint32_t>();
-    g.rowid = ws.rowid.as<uint32_t>(); g.val = b->value; g.p = ws.p.as<float>();
+    g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.d = d; g.wv = wv; g.slot = slot; g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
