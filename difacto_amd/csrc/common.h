@@ -96,11 +96,19 @@ __host__ __device__ inline float initv_value(int r, float scale) {
   return (float)(((double)q - 0.5) * (double)scale);
 }
 
-// ---- device hash table view (open addressing, linear probing) ------------------------
+// ---- device hash table (open addressing, linear probing) -----------------------------
+// One 32-byte entry per key (SGDEntry, sgd_updater.h:20-34): the probe that finds the key
+// brings the FTRL state and the V-pool row in the same cache line.
+struct __attribute__((aligned(32))) Entry {
+  float w, sqrt_g, z, fea_cnt;  // float4-aligned
+  unsigned long long key;       // kEmptyKey == free slot
+  int32_t vrow;                 // V pool row, -1 == no V (SGDEntry::V == nullptr)
+  uint32_t pad;
+};
+static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
+
 struct Table {
-  uint64_t* keys;   // cap, kEmptyKey == free
-  float4* st;       // cap: {w, sqrt_g, z, fea_cnt}
-  int32_t* vrow;    // cap: V pool row or -1
+  Entry* ent;       // cap entries
   float* V;         // vcap * d
   float* Vaux;      // vcap * d (AdaGrad accumulators)
   uint64_t mask;    // cap - 1
@@ -109,14 +117,17 @@ struct Table {
   int64_t vcap;
 };
 
-__device__ inline uint64_t tbl_hash(uint64_t k, int logcap) {
+__device__ inline float4 ent_state(const Entry* e) { return *reinterpret_cast<const float4*>(e); }
+__device__ inline void ent_set_state(Entry* e, float4 s) { *reinterpret_cast<float4*>(e) = s; }
+
+__host__ __device__ inline uint64_t tbl_hash(uint64_t k, int logcap) {
   return (k * 0x9E3779B97F4A7C15ull) >> (64 - logcap);
 }
 
 __device__ inline int64_t tbl_find(const Table& t, uint64_t k) {
   uint64_t h = tbl_hash(k, t.logcap);
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-    uint64_t kk = t.keys[h];
+    uint64_t kk = t.ent[h].key;
     if (kk == k) return (int64_t)h;
     if (kk == kEmptyKey) return -1;
     h = (h + 1) & t.mask;
@@ -131,11 +142,11 @@ __device__ inline int64_t tbl_insert(const Table& t, uint64_t k, bool* inserted)
   uint64_t h = tbl_hash(k, t.logcap);
   *inserted = false;
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-    uint64_t kk = t.keys[h];
+    uint64_t kk = t.ent[h].key;
     if (kk == k) return (int64_t)h;
     if (kk == kEmptyKey) {
-      unsigned long long old = atomicCAS((unsigned long long*)&t.keys[h],
-                                         (unsigned long long)kEmptyKey, (unsigned long long)k);
+      unsigned long long old = atomicCAS(&t.ent[h].key, (unsigned long long)kEmptyKey,
+                                         (unsigned long long)k);
       if (old == kEmptyKey) { *inserted = true; return (int64_t)h; }
       if (old == k) return (int64_t)h;
     }

@@ -69,9 +69,12 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         if (PACKED) {
-          const int2 e = a.wv[c[t]];
-          w[t] = __int_as_float(e.x);
-          vp[t] = e.y;
+          // the key's table entry: w and its V row share one cache line; V is visible
+          // only if present and not (l1_shrk && w == 0)  (SGDUpdater::Get, :40-43)
+          const Entry* en = a.T.ent + c[t];
+          w[t] = en->w;
+          const int vr = en->vrow;
+          vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
         } else {
           if (a.wpos) {
             const int q = a.wpos[c[t]];
@@ -241,10 +244,12 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
     float vcur[CPL], ccur[CPL], g0[CPL];
     if (FUSED) {
-      vq = a.wv[cidx].y;
       sl = a.slot[cidx];
-      e = a.T.st[sl];
-      vrow = a.T.vrow[sl];
+      const Entry* en = a.T.ent + sl;
+      e = ent_state(en);
+      vrow = en->vrow;
+      // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
+      vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
       const float* Vr = vq >= 0 ? a.T.V + (int64_t)vq * d : a.zpad;
       const float* Cr = vq >= 0 ? a.T.Vaux + (int64_t)vq * d : a.zpad;
 #pragma unroll
@@ -403,7 +408,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         }
       }
       if (l == 0) {
-        a.T.st[sl] = e;
+        ent_set_state(a.T.ent + sl, e);
         dnew = dw;
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
         const bool need = tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;

@@ -7,10 +7,12 @@ namespace dfx {
 struct FwdArgs {
   int64_t B;
   const uint64_t* offs;
-  const uint32_t* col;
+  const uint32_t* col;   // remapped column, or (fused) the nnz's model-table slot
   const float* val;
-  // weights: packed {w, V pool row} per column (fused) or interleaved weights + positions
-  const int2* wv;
+  // fused: the model table itself (SGDUpdater::Get semantics, l1_shrk from P);
+  // standalone: interleaved weights addressed by positions
+  Table T;
+  int l1_shrk;
   const float* W;
   const int32_t* wpos;
   const int32_t* vpos;
@@ -43,8 +45,7 @@ struct BwdArgs {
   const float* W;
   float* grad;
   // fused update
-  const int2* wv;
-  const uint32_t* slot;
+  const uint32_t* slot;      // model-table slot of each segment's key
   Table T;
   Params Pm;
   uint32_t* flags;  // InitV request per key

@@ -127,22 +127,31 @@ void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* tot
 // pairs (buffer selected by ds->sortmeta[31]), rowid[nnz] when want_rowid, U in
 // ds->u_count.  Writes uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].
 // With occ_row (and occ_x when value != NULL) it also writes every occurrence's row (and
-// value) in sorted order, for the backward walk.
+// value) in sorted order, for the backward walk.  With nslot (fused step) every nnz's key is
+// found-or-inserted in the model table (nslot[nnz] = its slot) and segslot[U] receives each
+// unique key's slot; uniq / col may then be NULL.
+struct LocOut {
+  uint64_t* uniq = nullptr;
+  float* cnt = nullptr;
+  uint32_t* col = nullptr;
+  uint32_t* segstart = nullptr;
+  const float* value = nullptr;
+  uint32_t* occ_row = nullptr;
+  float* occ_x = nullptr;
+  uint32_t* nslot = nullptr;
+  uint32_t* segslot = nullptr;
+};
 int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
-                 const uint64_t* index, uint64_t max_index, uint64_t* uniq, float* cnt,
-                 uint32_t* col, uint32_t* segstart, const float* value, uint32_t* occ_row,
-                 float* occ_x);
+                 const uint64_t* index, uint64_t max_index, const LocOut& o);
 
 int ws_reserve(Context* c, int64_t rows, int64_t nnz);
 
 // store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
               const uint32_t* slot);
-int push_cnt_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
-                 const float* cnt, const uint32_t* segstart, uint32_t* slot, uint32_t* flags,
-                 uint32_t* total_dev);
-int resolve_pull_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
-                     uint32_t* slot, int2* wv);
+// fused Update(kFeaCount): one segment per unique key (count = segment length)
+int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
+                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev);
 int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles

@@ -36,12 +36,10 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(ws.hist.ensure(sizeof(uint32_t) * (256 * (ntiles > (rows + 2047) / 2048
                                                         ? ntiles : (rows + 2047) / 2048) + 256)));
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
-  DFX_TRY(ws.uniq.ensure(nnz * 8));
   DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(ws.col.ensure(nnz * 4));
   DFX_TRY(ws.slot.ensure((nnz + 1) * 4));
   DFX_TRY(ws.flags.ensure((nnz + 1) * 4));
-  DFX_TRY(ws.wb.ensure(nnz * 8));
   DFX_TRY(ws.occ_row.ensure(nnz * 4));
   DFX_TRY(ws.occ_x.ensure(nnz * 4));
   DFX_TRY(ws.p.ensure(rows * 4));
@@ -75,30 +73,36 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   const int d = c->P.V_dim;
   Workspace& ws = c->ws;
   DFX_TRY(ws_reserve(c, B, nnz));
-  uint64_t* uniq = ws.uniq.as<uint64_t>();
   uint32_t* segstart = ws.segstart.as<uint32_t>();
-  uint32_t* col = ws.col.as<uint32_t>();
-  uint32_t* slot = ws.slot.as<uint32_t>();
+  uint32_t* nslot = ws.col.as<uint32_t>();   // per nnz: model-table slot of its key
+  uint32_t* segslot = ws.slot.as<uint32_t>();  // per unique key (sorted): its slot
   uint32_t* flags = ws.flags.as<uint32_t>();
-  int2* wv = ws.wb.as<int2>();
   uint32_t* total = &c->ds->totals[0];
   float* pred = pred_out ? pred_out : ws.pred.as<float>();
-
-  prof_mark(c, 0);
   uint32_t* occ_row = ws.occ_row.as<uint32_t>();
   float* occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
-  DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, uniq, nullptr, col, segstart,
-                       b->value, occ_row, occ_x));
+
+  prof_mark(c, 0);
+  // Localizer::Compact + the pull's key resolution: each nnz's key is found-or-inserted in
+  // the model table (Get's model_[key], sgd_updater.cc:37); segments come out in sorted key
+  // order, which is the order Update walks keys in (InitV draws) and the (row, nnz) order of
+  // every key's gradient sum.
+  LocOut o;
+  o.segstart = segstart;
+  o.value = b->value;
+  o.occ_row = occ_row;
+  o.occ_x = occ_x;
+  o.nslot = nslot;
+  o.segslot = segslot;
+  DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, o));
   prof_mark(c, 1);
-  if (push_cnt && d > 0) DFX_TRY(push_cnt_run(c, -1, nnz, uniq, nullptr, segstart, slot, flags,
-                                              total));
+  if (push_cnt && d > 0) DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total));
   prof_mark(c, 2);
-  DFX_TRY(resolve_pull_run(c, -1, nnz, uniq, slot, wv));
-  prof_mark(c, 3);
+  prof_mark(c, 3);  // the pull is the forward's direct read of each key's table entry
 
   FwdArgs a{};
-  a.B = B; a.offs = b->offset; a.col = col; a.val = b->value; a.wv = wv; a.Vbase = c->T.V;
-  a.zpad = c->zpad;
+  a.B = B; a.offs = b->offset; a.col = nslot; a.val = b->value; a.T = c->T;
+  a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>();
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -113,11 +117,11 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     BwdArgs g{};
     g.segstart = segstart; g.ds = c->ds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
-    g.XVp = ws.XVp.as<float>(); g.d = d; g.wv = wv; g.slot = slot; g.T = c->T; g.Pm = c->P;
+    g.XVp = ws.XVp.as<float>(); g.d = d; g.slot = segslot; g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
     prof_mark(c, 6);
-    DFX_TRY(run_initv(c, -1, nnz, flags, total, slot));
+    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot));
   } else {
     prof_mark(c, 6);
   }

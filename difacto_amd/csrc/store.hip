@@ -2,10 +2,11 @@
 // push/pull boundary (include/difacto/store.h:44-75), on one GPU.
 //
 // Layout in HBM (sized for 288 GB):
-//   keys  u64[cap]      open-addressing table, multiplicative hash of the (already
-//                       nibble-reversed) key, linear probing, cap = pow2 >= 2*max_keys
-//   st    float4[cap]   {w, sqrt_g, z, fea_cnt}       (SGDEntry, sgd_updater.h:20-34)
-//   vrow  i32[cap]      row of the lazy V pool, -1 == no V (SGDEntry::V == nullptr)
+//   ent   Entry[cap]    32-byte records {w, sqrt_g, z, fea_cnt | key | vrow}: SGDEntry
+//                       (sgd_updater.h:20-34) + its key, open addressing with a
+//                       multiplicative hash of the (already nibble-reversed) key and linear
+//                       probing, cap = pow2 >= 2*max_keys.  A probe's cache line carries the
+//                       key's whole scalar state.
 //   V     f32[vcap*d]   embedding rows, allocated by InitV in rand_r order
 //   Vaux  f32[vcap*d]   AdaGrad accumulators
 // InitV (sgd_updater.cc:144-152) draws glibc rand_r in key order; on the GPU every key that
@@ -34,6 +35,7 @@ __device__ inline void block_count_add(int v, unsigned long long* dst) {
     for (int i = 0; i < kStNT / kWave; ++i) s += red[i];
     if (s) atomicAdd(dst, (unsigned long long)(long long)s);
   }
+  __syncthreads();
 }
 
 __device__ inline int64_t count_of(int64_t n_host, const DevState* ds) {
@@ -41,7 +43,8 @@ __device__ inline int64_t count_of(int64_t n_host, const DevState* ds) {
 }
 
 // ---- InitV --------------------------------------------------------------------------------
-// excl: exclusive scan of the per-key InitV flags; *total: their sum.
+// excl: exclusive scan of the per-key InitV flags; *total: their sum; slot: table slot of
+// each flagged key.
 __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t* excl,
                                                  const uint32_t* total, const uint32_t* slot,
                                                  Table T, float scale, DevState* ds) {
@@ -64,7 +67,7 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
     V[k] = initv_value(rand_r_dev(&s), scale);
     C[k] = 0.f;
   }
-  T.vrow[slot[u]] = (int32_t)vr;
+  T.ent[slot[u]].vrow = (int32_t)vr;
 }
 
 __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, DevState* ds) {
@@ -88,13 +91,20 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
 }
 
 // ---- Update(kFeaCount) (sgd_updater.cc:64-75) ---------------------------------------------
-// cnt: float counts, or NULL to derive them from segstart (fused path).
-__global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n_host, const uint64_t* keys,
-                                                    const float* cnt, const uint32_t* segstart,
-                                                    Table T, Params P, uint32_t* slot,
-                                                    uint32_t* flags, DevState* ds) {
+__device__ inline uint32_t feacnt_apply(const Table& T, const Params& P, int64_t s, float c) {
+  Entry* e = &T.ent[s];
+  float4 st = ent_state(e);
+  st.w += c;  // fea_cnt
+  ent_set_state(e, st);
+  return (P.V_dim > 0 && e->vrow < 0 && st.x != 0.f && st.w > (float)P.V_threshold) ? 1u : 0u;
+}
+
+// standalone: keys + float counts (find-or-insert)
+__global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n, const uint64_t* keys,
+                                                    const float* cnt, Table T, Params P,
+                                                    uint32_t* slot, uint32_t* flags,
+                                                    DevState* ds) {
   const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
-  const int64_t n = count_of(n_host, ds);
   int ins = 0;
   if (u < n) {
     bool inserted;
@@ -104,11 +114,7 @@ __global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n_host, const uint64
     if (s < 0) {
       atomicOr(&ds->err, kErrTableFull);
     } else {
-      float c = cnt ? cnt[u] : (float)(segstart[u + 1] - segstart[u]);
-      float4 e = T.st[s];
-      e.w += c;  // fea_cnt
-      T.st[s] = e;
-      if (P.V_dim > 0 && T.vrow[s] < 0 && e.x != 0.f && e.w > (float)P.V_threshold) f = 1;
+      f = feacnt_apply(T, P, s, cnt[u]);
       slot[u] = (uint32_t)s;
     }
     flags[u] = f;
@@ -116,83 +122,61 @@ __global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n_host, const uint64
   block_count_add(ins, &ds->n_keys);
 }
 
-// ---- fused pull: resolve slots (find-or-insert) and emit {w, V pool offset} per key ------
-// SGDUpdater::Get (sgd_updater.cc:34-58): V only if present and not (l1_shrk && w == 0).
-__global__ __launch_bounds__(kStNT) void k_resolve_pull(int64_t n_host, const uint64_t* keys,
-                                                        Table T, Params P, uint32_t* slot,
-                                                        int2* wv, DevState* ds) {
+// fused: one segment per unique key, already resolved to a slot; count = segment length
+__global__ __launch_bounds__(kStNT) void k_push_cnt_seg(const uint32_t* segstart,
+                                                        const uint32_t* segslot, Table T,
+                                                        Params P, uint32_t* flags,
+                                                        const DevState* ds) {
   const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
-  const int64_t n = count_of(n_host, ds);
-  int ins = 0;
-  if (u < n) {
-    bool inserted;
-    int64_t s = tbl_insert(T, keys[u], &inserted);
-    ins = inserted;
-    if (s < 0) {
-      atomicOr(&ds->err, kErrTableFull);
-      wv[u] = make_int2(0, -1);
-      slot[u] = 0xFFFFFFFFu;
-    } else {
-      float w = T.st[s].x;
-      int vr = T.vrow[s];
-      bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
-      wv[u] = make_int2(__float_as_int(w), live ? vr : -1);  // V row index
-      slot[u] = (uint32_t)s;
-    }
-  }
-  block_count_add(ins, &ds->n_keys);
+  if (u >= (int64_t)ds->u_count) return;
+  const float c = (float)(segstart[u + 1] - segstart[u]);
+  flags[u] = feacnt_apply(T, P, segslot[u], c);
 }
 
-int push_cnt_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
-                 const float* cnt, const uint32_t* segstart, uint32_t* slot, uint32_t* flags,
-                 uint32_t* total_dev) {
+int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
+                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev) {
   if (n_bound <= 0) return DFX_OK;
-  hipLaunchKernelGGL(k_push_cnt, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
-                     n_host, keys, cnt, segstart, c->T, c->P, slot, flags, c->ds);
+  hipLaunchKernelGGL(k_push_cnt_seg, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0,
+                     c->stream, segstart, segslot, c->T, c->P, flags, c->ds);
   DFX_HIP(hipGetLastError());
-  return run_initv(c, n_host, n_bound, flags, total_dev, slot);
-}
-
-int resolve_pull_run(Context* c, int64_t n_host, int64_t n_bound, const uint64_t* keys,
-                     uint32_t* slot, int2* wv) {
-  if (n_bound <= 0) return DFX_OK;
-  hipLaunchKernelGGL(k_resolve_pull, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0,
-                     c->stream, n_host, keys, c->T, c->P, slot, wv, c->ds);
-  DFX_HIP(hipGetLastError());
-  return DFX_OK;
+  return run_initv(c, -1, n_bound, flags, total_dev, segslot);
 }
 
 // ---- standalone Get: interleaved [w | V] + lens ---------------------------------------------
+// SGDUpdater::Get (sgd_updater.cc:34-58): V only if present and not (l1_shrk && w == 0).
+// Missing keys read as w = 0 without V; Get's insertion of empty entries is not observable.
 __global__ __launch_bounds__(kStNT) void k_pull_lens(int64_t n, const uint64_t* keys, Table T,
-                                                     Params P, int32_t* vr_out,
+                                                     Params P, int32_t* slot_out,
                                                      uint32_t* len_out) {
   const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   if (i >= n) return;
   int64_t s = tbl_find(T, keys[i]);
   int vr = -1;
   float w = 0.f;
-  if (s >= 0) { w = T.st[s].x; vr = T.vrow[s]; }
+  if (s >= 0) { w = T.ent[s].w; vr = T.ent[s].vrow; }
   bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
-  vr_out[i] = live ? vr : -1;
+  slot_out[i] = (int32_t)s;
   len_out[i] = live ? (uint32_t)(T.d + 1) : 1u;
 }
 
-__global__ __launch_bounds__(kStNT) void k_pull_write(int64_t n, const uint64_t* keys, Table T,
-                                                      const int32_t* vr_in,
+__global__ __launch_bounds__(kStNT) void k_pull_write(int64_t n, Table T, Params P,
+                                                      const int32_t* slot_in,
                                                       const uint32_t* off, float* vals,
                                                       int32_t* lens) {
   const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   if (i >= n) return;
-  int64_t s = tbl_find(T, keys[i]);
+  const int32_t s = slot_in[i];
   const uint32_t o = off[i];
-  vals[o] = s >= 0 ? T.st[s].x : 0.f;
-  const int vr = vr_in[i];
+  const float w = s >= 0 ? T.ent[s].w : 0.f;
+  const int vr = s >= 0 ? T.ent[s].vrow : -1;
+  const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
+  vals[o] = w;
   const int d = T.d;
-  if (vr >= 0) {
+  if (live) {
     const float* V = T.V + (int64_t)vr * d;
     for (int k = 0; k < d; ++k) vals[o + 1 + k] = V[k];
   }
-  if (lens) lens[i] = vr >= 0 ? d + 1 : 1;
+  if (lens) lens[i] = live ? d + 1 : 1;
 }
 
 // ---- standalone Update(kGradient) (sgd_updater.cc:76-98) -----------------------------------
@@ -213,11 +197,12 @@ __global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* 
     } else {
       const int d = T.d;
       const uint32_t o = lens ? off[i] : (uint32_t)i;
-      float4 e = T.st[s];
+      Entry* en = &T.ent[s];
+      float4 e = ent_state(en);
       bool tr;
       dnew = ftrl_update(P, vals[o], &e, &tr);
-      T.st[s] = e;
-      const int vr = T.vrow[s];
+      ent_set_state(en, e);
+      const int vr = en->vrow;
       if (lens && lens[i] > 1) {
         if (lens[i] != d + 1) {
           atomicOr(&ds->err, kErrLens);
@@ -236,7 +221,6 @@ __global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* 
     flags[i] = f;
   }
   block_count_add(ins, &ds->n_keys);
-  __syncthreads();
   block_count_add(dnew, (unsigned long long*)&ds->new_w);
 }
 
@@ -250,26 +234,32 @@ __global__ void k_lens_u32(int64_t n, const int32_t* lens, uint32_t* out) {
 }
 
 // ---- table allocation / growth ------------------------------------------------------------
-__global__ void k_rehash(const uint64_t* okeys, const float4* ost, const int32_t* ovrow,
-                         int64_t ocap, Table T, DevState* ds) {
+__global__ void k_tbl_init(Entry* ent, int64_t cap) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ocap) return;
-  const uint64_t k = okeys[i];
-  if (k == kEmptyKey) return;
-  bool ins;
-  int64_t s = tbl_insert(T, k, &ins);
-  if (s < 0) { atomicOr(&ds->err, kErrTableFull); return; }
-  T.st[s] = ost[i];
-  T.vrow[s] = ovrow[i];
+  if (i >= cap) return;
+  Entry e;
+  e.w = e.sqrt_g = e.z = e.fea_cnt = 0.f;
+  e.key = kEmptyKey;
+  e.vrow = -1;
+  e.pad = 0;
+  ent[i] = e;
 }
 
-int table_alloc_arrays(Table* T, int64_t cap) {
-  DFX_HIP(hipMalloc(&T->keys, cap * sizeof(uint64_t)));
-  DFX_HIP(hipMalloc(&T->st, cap * sizeof(float4)));
-  DFX_HIP(hipMalloc(&T->vrow, cap * sizeof(int32_t)));
-  DFX_HIP(hipMemset(T->keys, 0xFF, cap * sizeof(uint64_t)));
-  DFX_HIP(hipMemset(T->st, 0, cap * sizeof(float4)));
-  DFX_HIP(hipMemset(T->vrow, 0xFF, cap * sizeof(int32_t)));
+__global__ void k_rehash(const Entry* old, int64_t ocap, Table T, DevState* ds) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ocap) return;
+  const Entry e = old[i];
+  if (e.key == kEmptyKey) return;
+  bool ins;
+  int64_t s = tbl_insert(T, e.key, &ins);
+  if (s < 0) { atomicOr(&ds->err, kErrTableFull); return; }
+  T.ent[s] = e;
+}
+
+static int table_alloc_entries(Table* T, int64_t cap, hipStream_t st) {
+  DFX_HIP(hipMalloc(&T->ent, cap * sizeof(Entry)));
+  hipLaunchKernelGGL(k_tbl_init, dim3((cap + 255) / 256), dim3(256), 0, st, T->ent, cap);
+  DFX_HIP(hipGetLastError());
   int lg = 0;
   while ((1ll << lg) < cap) ++lg;
   T->logcap = lg;
@@ -283,7 +273,8 @@ int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
   while (cap < 2 * n_keys) cap <<= 1;
   Table& T = c->T;
   T.d = c->P.V_dim;
-  DFX_TRY(table_alloc_arrays(&T, cap));
+  DFX_TRY(table_alloc_entries(&T, cap, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
   c->cap = cap;
   T.vcap = T.d > 0 ? (n_vrows > 0 ? n_vrows : 1) : 0;
   if (T.d > 0) {
@@ -295,9 +286,7 @@ int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
 
 void table_release(Context* c) {
   Table& T = c->T;
-  if (T.keys) (void)hipFree(T.keys);
-  if (T.st) (void)hipFree(T.st);
-  if (T.vrow) (void)hipFree(T.vrow);
+  if (T.ent) (void)hipFree(T.ent);
   if (T.V) (void)hipFree(T.V);
   if (T.Vaux) (void)hipFree(T.Vaux);
   T = Table{};
@@ -327,14 +316,12 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
     int64_t cap = c->cap;
     while (cap < 2 * n_keys) cap <<= 1;
     Table NT = T;
-    DFX_TRY(table_alloc_arrays(&NT, cap));
-    hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.keys,
-                       T.st, T.vrow, c->cap, NT, c->ds);
+    DFX_TRY(table_alloc_entries(&NT, cap, c->stream));
+    hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
+                       c->cap, NT, c->ds);
     DFX_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(T.keys);
-    (void)hipFree(T.st);
-    (void)hipFree(T.vrow);
-    T.keys = NT.keys; T.st = NT.st; T.vrow = NT.vrow; T.mask = NT.mask; T.logcap = NT.logcap;
+    (void)hipFree(T.ent);
+    T.ent = NT.ent; T.mask = NT.mask; T.logcap = NT.logcap;
     c->cap = cap;
   }
   if (T.d > 0 && n_vrows > T.vcap) {
@@ -354,7 +341,8 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
   return DFX_OK;
 }
 
-// load: host-parsed entries uploaded and inserted
+// load: host-parsed entries uploaded and inserted (SGDEntry::LoadEntry keeps fea_cnt, and
+// keeps sqrt_g/z when the file has no aux data)
 __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const int32_t* vr,
                        int has_aux, Table T, DevState* ds) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -366,25 +354,25 @@ __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const 
     if (s < 0) {
       atomicOr(&ds->err, kErrTableFull);
     } else {
-      float4 e = T.st[s];
+      Entry* en = &T.ent[s];
+      float4 e = ent_state(en);
       e.x = st[i].x;
       if (has_aux) { e.y = st[i].y; e.z = st[i].z; }
-      T.st[s] = e;
-      if (vr[i] >= 0) T.vrow[s] = vr[i];
+      ent_set_state(en, e);
+      if (vr[i] >= 0) en->vrow = vr[i];
     }
   }
   block_count_add(ins, &ds->n_keys);
 }
 
-__global__ void k_penalty(const uint64_t* keys, const float4* st, const int32_t* vrow,
-                          int64_t cap, Table T, Params P, double* acc) {
+__global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double objv = 0, nnz = 0;
-  if (i < cap && keys[i] != kEmptyKey) {
-    const float w = st[i].x;
+  if (i < cap && T.ent[i].key != kEmptyKey) {
+    const float w = T.ent[i].w;
     if (w != 0.f) nnz += 1;
     objv += P.l1 * fabs(w) + .5 * P.l2 * w * w;
-    const int vr = vrow[i];
+    const int vr = T.ent[i].vrow;
     if (vr >= 0) {
       nnz += T.d;
       const float* V = T.V + (int64_t)vr * T.d;
@@ -399,6 +387,27 @@ __global__ void k_penalty(const uint64_t* keys, const float4* st, const int32_t*
     atomicAdd(&acc[0], objv);
     atomicAdd(&acc[1], nnz);
   }
+}
+
+// host copy of the table for save / dump
+struct HostTable {
+  std::vector<Entry> ent;
+  std::vector<float> V, C;
+};
+
+static int copy_table_to_host(Context* c, HostTable* h) {
+  const Table& T = c->T;
+  HostCounters hc;
+  DFX_TRY(read_counters(c, &hc));
+  h->ent.resize(c->cap);
+  h->V.resize((size_t)hc.n_vrows * T.d);
+  h->C.resize((size_t)hc.n_vrows * T.d);
+  DFX_HIP(hipMemcpy(h->ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
+  if (!h->V.empty()) {
+    DFX_HIP(hipMemcpy(h->V.data(), T.V, h->V.size() * 4, hipMemcpyDeviceToHost));
+    DFX_HIP(hipMemcpy(h->C.data(), T.Vaux, h->C.size() * 4, hipMemcpyDeviceToHost));
+  }
+  return DFX_OK;
 }
 
 }  // namespace dfx
@@ -424,12 +433,12 @@ int dfx_store_pull(dfx_ctx* ctx, const uint64_t* keys, int64_t n, float* vals, i
   DFX_TRY(ws.slot.ensure((n + 1) * 4));
   DFX_TRY(ws.cnt.ensure(16));
   uint32_t* off = ws.flags.as<uint32_t>();
-  int32_t* vr = ws.slot.as<int32_t>();
+  int32_t* sl = ws.slot.as<int32_t>();
   uint32_t* total = ws.cnt.as<uint32_t>();
   dim3 grid((n + kStNT - 1) / kStNT);
-  hipLaunchKernelGGL(k_pull_lens, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, c->P, vr, off);
+  hipLaunchKernelGGL(k_pull_lens, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, c->P, sl, off);
   DFX_TRY(scan_u32(c, off, n, total));
-  hipLaunchKernelGGL(k_pull_write, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, vr, off, vals,
+  hipLaunchKernelGGL(k_pull_write, grid, dim3(kStNT), 0, c->stream, n, c->T, c->P, sl, off, vals,
                      d > 0 ? lens : nullptr);
   DFX_HIP(hipGetLastError());
   if (n_vals) {
@@ -451,7 +460,6 @@ int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, cons
   Workspace& ws = c->ws;
   DFX_TRY(ws.flags.ensure((n + 1) * 4));
   DFX_TRY(ws.slot.ensure((n + 1) * 4));
-  DFX_TRY(ws.tiles.ensure(16));
   DFX_TRY(ws.cnt.ensure(16));
   uint32_t* flags = ws.flags.as<uint32_t>();
   uint32_t* slot = ws.slot.as<uint32_t>();
@@ -461,7 +469,10 @@ int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, cons
       set_error("CHECK_EQ(fea_ids.size(), values.size()) failed (sgd_updater.cc:65)");
       return DFX_ERR_CHECK;
     }
-    return push_cnt_run(c, n, n, keys, vals, nullptr, slot, flags, total);
+    hipLaunchKernelGGL(k_push_cnt, dim3((n + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream, n,
+                       keys, vals, c->T, c->P, slot, flags, c->ds);
+    DFX_HIP(hipGetLastError());
+    return run_initv(c, n, n, flags, total, slot);
   }
   if (type != DFX_GRADIENT) {
     set_error("UNKNOWN value_type (sgd_updater.cc:100)");
@@ -507,8 +518,8 @@ int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz) {
   DFX_TRY(c->ws.dscratch.ensure(64));
   double* acc = c->ws.dscratch.as<double>();
   DFX_HIP(hipMemsetAsync(acc, 0, 2 * sizeof(double), c->stream));
-  hipLaunchKernelGGL(k_penalty, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, c->T.keys,
-                     c->T.st, c->T.vrow, c->cap, c->T, c->P, acc);
+  hipLaunchKernelGGL(k_penalty, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, c->T, c->cap,
+                     c->P, acc);
   double h[2];
   DFX_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
@@ -518,27 +529,24 @@ int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz) {
 }
 
 int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has_v, int* found) {
-  DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_ARG(ctx && state && has_v && found, "null argument");
   Context* c = &ctx->c;
   const Table& T = c->T;
   DFX_HIP(hipStreamSynchronize(c->stream));
   // host-side probe of the same hash sequence (test hook; not a hot path)
-  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> (64 - T.logcap);
+  uint64_t h = tbl_hash(key, T.logcap);
   *found = 0;
   for (uint64_t probe = 0; probe <= T.mask; ++probe) {
-    uint64_t kk;
-    DFX_HIP(hipMemcpy(&kk, T.keys + h, 8, hipMemcpyDeviceToHost));
-    if (kk == kEmptyKey) return DFX_OK;
-    if (kk == key) {
-      float4 e;
-      int32_t vr;
-      DFX_HIP(hipMemcpy(&e, T.st + h, sizeof(e), hipMemcpyDeviceToHost));
-      DFX_HIP(hipMemcpy(&vr, T.vrow + h, 4, hipMemcpyDeviceToHost));
-      state[0] = e.x; state[1] = e.y; state[2] = e.z; state[3] = e.w;
-      *has_v = vr >= 0;
-      if (vr >= 0 && V) {
-        DFX_HIP(hipMemcpy(V, T.V + (int64_t)vr * T.d, T.d * 4, hipMemcpyDeviceToHost));
-        DFX_HIP(hipMemcpy(V + T.d, T.Vaux + (int64_t)vr * T.d, T.d * 4, hipMemcpyDeviceToHost));
+    Entry e;
+    DFX_HIP(hipMemcpy(&e, T.ent + h, sizeof(Entry), hipMemcpyDeviceToHost));
+    if (e.key == kEmptyKey) return DFX_OK;
+    if (e.key == key) {
+      state[0] = e.w; state[1] = e.sqrt_g; state[2] = e.z; state[3] = e.fea_cnt;
+      *has_v = e.vrow >= 0;
+      if (e.vrow >= 0 && V) {
+        DFX_HIP(hipMemcpy(V, T.V + (int64_t)e.vrow * T.d, T.d * 4, hipMemcpyDeviceToHost));
+        DFX_HIP(hipMemcpy(V + T.d, T.Vaux + (int64_t)e.vrow * T.d, T.d * 4,
+                          hipMemcpyDeviceToHost));
       }
       *found = 1;
       return DFX_OK;
@@ -552,36 +560,25 @@ int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has
 int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux) {
   DFX_CHECK_ARG(ctx && path, "null argument");
   Context* c = &ctx->c;
-  const Table& T = c->T;
-  HostCounters hc;
-  DFX_TRY(read_counters(c, &hc));
-  std::vector<uint64_t> keys(c->cap);
-  std::vector<float4> st(c->cap);
-  std::vector<int32_t> vrow(c->cap);
-  std::vector<float> V((size_t)hc.n_vrows * T.d), C((size_t)hc.n_vrows * T.d);
-  DFX_HIP(hipMemcpy(keys.data(), T.keys, c->cap * 8, hipMemcpyDeviceToHost));
-  DFX_HIP(hipMemcpy(st.data(), T.st, c->cap * sizeof(float4), hipMemcpyDeviceToHost));
-  DFX_HIP(hipMemcpy(vrow.data(), T.vrow, c->cap * 4, hipMemcpyDeviceToHost));
-  if (!V.empty()) {
-    DFX_HIP(hipMemcpy(V.data(), T.V, V.size() * 4, hipMemcpyDeviceToHost));
-    DFX_HIP(hipMemcpy(C.data(), T.Vaux, C.size() * 4, hipMemcpyDeviceToHost));
-  }
+  const int d = c->T.d;
+  HostTable ht;
+  DFX_TRY(copy_table_to_host(c, &ht));
   FILE* f = fopen(path, "wb");
   if (!f) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
   bool aux = save_aux != 0;
   fwrite(&aux, sizeof(bool), 1, f);
-  for (int64_t i = 0; i < c->cap; ++i) {
-    if (keys[i] == kEmptyKey) continue;
-    const int size = vrow[i] >= 0 ? 1 + T.d : 1;
-    const float w = st[i].x;
-    if (w == 0.f && size == 1) continue;  // SGDEntry::empty()
-    fwrite(&keys[i], 8, 1, f);
+  for (const Entry& e : ht.ent) {
+    if (e.key == kEmptyKey) continue;
+    const int size = e.vrow >= 0 ? 1 + d : 1;
+    if (e.w == 0.f && size == 1) continue;  // SGDEntry::empty()
+    const uint64_t key = e.key;
+    fwrite(&key, 8, 1, f);
     fwrite(&size, sizeof(int), 1, f);
-    fwrite(&w, 4, 1, f);
-    if (aux) { fwrite(&st[i].y, 4, 1, f); fwrite(&st[i].z, 4, 1, f); }
+    fwrite(&e.w, 4, 1, f);
+    if (aux) { fwrite(&e.sqrt_g, 4, 1, f); fwrite(&e.z, 4, 1, f); }
     if (size == 1) continue;
-    fwrite(V.data() + (size_t)vrow[i] * T.d, 4, T.d, f);
-    if (aux) fwrite(C.data() + (size_t)vrow[i] * T.d, 4, T.d, f);
+    fwrite(ht.V.data() + (size_t)e.vrow * d, 4, d, f);
+    if (aux) fwrite(ht.C.data() + (size_t)e.vrow * d, 4, d, f);
   }
   fclose(f);
   return DFX_OK;
@@ -668,35 +665,24 @@ int dfx_store_load(dfx_ctx* ctx, const char* path) {
 int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_reverse) {
   DFX_CHECK_ARG(ctx && path, "null argument");
   Context* c = &ctx->c;
-  const Table& T = c->T;
-  HostCounters hc;
-  DFX_TRY(read_counters(c, &hc));
-  std::vector<uint64_t> keys(c->cap);
-  std::vector<float4> st(c->cap);
-  std::vector<int32_t> vrow(c->cap);
-  std::vector<float> V((size_t)hc.n_vrows * T.d), C((size_t)hc.n_vrows * T.d);
-  DFX_HIP(hipMemcpy(keys.data(), T.keys, c->cap * 8, hipMemcpyDeviceToHost));
-  DFX_HIP(hipMemcpy(st.data(), T.st, c->cap * sizeof(float4), hipMemcpyDeviceToHost));
-  DFX_HIP(hipMemcpy(vrow.data(), T.vrow, c->cap * 4, hipMemcpyDeviceToHost));
-  if (!V.empty()) {
-    DFX_HIP(hipMemcpy(V.data(), T.V, V.size() * 4, hipMemcpyDeviceToHost));
-    DFX_HIP(hipMemcpy(C.data(), T.Vaux, C.size() * 4, hipMemcpyDeviceToHost));
-  }
+  const int d = c->T.d;
+  HostTable ht;
+  DFX_TRY(copy_table_to_host(c, &ht));
   std::ofstream os(path);
   if (!os) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
-  for (int64_t i = 0; i < c->cap; ++i) {
-    if (keys[i] == kEmptyKey) continue;
-    const int size = vrow[i] >= 0 ? 1 + T.d : 1;
-    if (st[i].x == 0.f && size == 1) continue;
-    os << (need_reverse ? reverse_bytes(keys[i]) : keys[i]);
-    os << '\t' << size << '\t' << st[i].x;
-    if (dump_aux) os << '\t' << st[i].y << '\t' << st[i].z;
+  for (const Entry& e : ht.ent) {
+    if (e.key == kEmptyKey) continue;
+    const int size = e.vrow >= 0 ? 1 + d : 1;
+    if (e.w == 0.f && size == 1) continue;
+    os << (need_reverse ? reverse_bytes(e.key) : (uint64_t)e.key);
+    os << '\t' << size << '\t' << e.w;
+    if (dump_aux) os << '\t' << e.sqrt_g << '\t' << e.z;
     if (size > 1) {
-      const float* v = V.data() + (size_t)vrow[i] * T.d;
-      for (int k = 0; k < T.d; ++k) os << '\t' << v[k];
+      const float* v = ht.V.data() + (size_t)e.vrow * d;
+      for (int k = 0; k < d; ++k) os << '\t' << v[k];
       if (dump_aux) {
-        const float* cc = C.data() + (size_t)vrow[i] * T.d;
-        for (int k = 0; k < T.d; ++k) os << '\t' << cc[k];
+        const float* cc = ht.C.data() + (size_t)e.vrow * d;
+        for (int k = 0; k < d; ++k) os << '\t' << cc[k];
       }
     }
     os << '\n';
