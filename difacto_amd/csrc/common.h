@@ -99,11 +99,14 @@ __host__ __device__ inline float initv_value(int r, float scale) {
 // ---- device hash table (open addressing, linear probing) -----------------------------
 // One 32-byte entry per key (SGDEntry, sgd_updater.h:20-34): the probe that finds the key
 // brings the FTRL state and the V-pool row in the same cache line.
+// {w, vrow} lead so the forward pass reads both with one 8-byte load.
 struct __attribute__((aligned(32))) Entry {
-  float w, sqrt_g, z, fea_cnt;  // float4-aligned
-  unsigned long long key;       // kEmptyKey == free slot
+  float w;
   int32_t vrow;                 // V pool row, -1 == no V (SGDEntry::V == nullptr)
+  float sqrt_g, z;
+  float fea_cnt;
   uint32_t pad;
+  unsigned long long key;       // kEmptyKey == free slot
 };
 static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
 
@@ -117,8 +120,17 @@ struct Table {
   int64_t vcap;
 };
 
-__device__ inline float4 ent_state(const Entry* e) { return *reinterpret_cast<const float4*>(e); }
-__device__ inline void ent_set_state(Entry* e, float4 s) { *reinterpret_cast<float4*>(e) = s; }
+__device__ inline float4 ent_state(const Entry* e) {
+  const float4 a = *reinterpret_cast<const float4*>(e);  // w, vrow, sqrt_g, z
+  return make_float4(a.x, a.z, a.w, e->fea_cnt);          // {w, sqrt_g, z, fea_cnt}
+}
+// writes back {w, sqrt_g, z, fea_cnt}; vrow is untouched
+__device__ inline void ent_set_state(Entry* e, float4 s) {
+  e->w = s.x;
+  e->sqrt_g = s.y;
+  e->z = s.z;
+  e->fea_cnt = s.w;
+}
 
 __host__ __device__ inline uint64_t tbl_hash(uint64_t k, int logcap) {
   return (k * 0x9E3779B97F4A7C15ull) >> (64 - logcap);

@@ -127,8 +127,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
     set_error("hipMalloc(DevState) failed");
     return DFX_ERR_HIP;
   }
-  if (hipMalloc(&c->zpad, 1024 * sizeof(float)) != hipSuccess ||
-      hipMemset(c->zpad, 0, 1024 * sizeof(float)) != hipSuccess) {
+  if (hipMalloc(&c->zpad, kZpadFloats * sizeof(float)) != hipSuccess ||
+      hipMemset(c->zpad, 0, kZpadFloats * sizeof(float)) != hipSuccess) {
     set_error("hipMalloc(zpad) failed");
     dfx_ctx_destroy(ctx);
     return DFX_ERR_HIP;

@@ -71,9 +71,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         if (PACKED) {
           // the key's table entry: w and its V row share one cache line; V is visible
           // only if present and not (l1_shrk && w == 0)  (SGDUpdater::Get, :40-43)
-          const Entry* en = a.T.ent + c[t];
-          w[t] = en->w;
-          const int vr = en->vrow;
+          const int2 wr = *reinterpret_cast<const int2*>(a.T.ent + c[t]);  // {w, vrow}
+          w[t] = __int_as_float(wr.x);
+          const int vr = wr.y;
           vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
         } else {
           if (a.wpos) {
@@ -89,7 +89,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       float v[UNR][CPL];
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
-        const float* Vr = vp[t] < 0 ? a.zpad
+        // masked items read zeros from one of 256 spread lines (one shared line would be a
+        // single-L2-channel hotspot when many keys have no V)
+        const float* Vr = vp[t] < 0 ? a.zpad + ((c[t] & 255u) << 4)
                                     : (PACKED ? a.Vbase + (int64_t)vp[t] * d : a.Vbase + vp[t]);
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
@@ -237,21 +239,41 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
     const bool valued = a.occ_x != nullptr;
     const int d = a.d;
-    // ---- the key's own operands first: they do not depend on the walk
+    const uint32_t len = s1 - s0;
+    // ---- level-2 loads, mutually independent: the key's table entry (or its positions in
+    // the pulled layout) and the first UNR occurrences of its segment
     int wq = -1, vq = -1, vrow = -1;
     uint32_t sl = 0;
+    float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+    float fc = 0.f;
+    if (FUSED) {
+      sl = a.slot[cidx];
+      const Entry* en = a.T.ent + sl;
+      h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
+      fc = en->fea_cnt;
+    } else {
+      wq = a.wpos ? a.wpos[cidx] : (int)cidx;
+      vq = d > 0 ? a.vpos[cidx] : -1;
+    }
+    uint32_t row[UNR];
+    float x[UNR];
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      const uint32_t i = s0 + ((uint32_t)t < len ? (uint32_t)t : 0u);
+      row[t] = a.occ_row[i];
+      x[t] = valued ? a.occ_x[i] : 1.f;
+    }
+    // ---- level 3: V / Vaux (or grad / W) of the key, p and XV*p of the occurrences' rows
     float gw = 0.f;
     float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
     float vcur[CPL], ccur[CPL], g0[CPL];
     if (FUSED) {
-      sl = a.slot[cidx];
-      const Entry* en = a.T.ent + sl;
-      e = ent_state(en);
-      vrow = en->vrow;
+      e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
+      vrow = __float_as_int(h.y);
       // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
       vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
-      const float* Vr = vq >= 0 ? a.T.V + (int64_t)vq * d : a.zpad;
-      const float* Cr = vq >= 0 ? a.T.Vaux + (int64_t)vq * d : a.zpad;
+      const float* Vr = vq >= 0 ? a.T.V + (int64_t)vq * d : a.zpad + ((cidx & 255u) << 4);
+      const float* Cr = vq >= 0 ? a.T.Vaux + (int64_t)vq * d : a.zpad + ((cidx & 255u) << 4);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int cd = l + k * G;
@@ -260,12 +282,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         g0[k] = 0.f;
       }
     } else {
-      wq = a.wpos ? a.wpos[cidx] : (int)cidx;
-      vq = d > 0 ? a.vpos[cidx] : -1;
       gw = a.grad[wq < 0 ? 0 : wq];
       if (wq < 0) gw = 0.f;
-      const float* Vr = vq >= 0 ? a.W + vq : a.zpad;
-      const float* Gr = vq >= 0 ? a.grad + vq : a.zpad;
+      const float* Vr = vq >= 0 ? a.W + vq : a.zpad + ((cidx & 255u) << 4);
+      const float* Gr = vq >= 0 ? a.grad + vq : a.zpad + ((cidx & 255u) << 4);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int cd = l + k * G;
@@ -274,32 +294,24 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         ccur[k] = 0.f;
       }
     }
+    float pr[UNR], xr[UNR][CPL];
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      pr[t] = a.p[row[t]];
+      const float* xrow = d > 0 ? a.XVp + (int64_t)row[t] * d : a.zpad;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int cd = l + k * G;
+        xr[t][k] = xrow[cd < d ? cd : 0];
+      }
+    }
     float xxp = 0.f;
     float acc[CPL];
     // ---- pass 1: g_w and XXp (SpMV::TransTimes, spmv.h:139-171: skip p == 0)
     // ---- pass 2: grad_u = (g0 - V*XXp) + sum (XV_ p) x (fm_loss.h:185-202, spmm.h:127-159)
     // Both sums run in occurrence order; a segment of <= UNR occurrences (the common case)
-    // issues every load of both passes at once.
-    const uint32_t len = s1 - s0;
+    // is computed from the registers loaded above.
     if (len <= (uint32_t)UNR) {
-      uint32_t row[UNR];
-      float x[UNR], pr[UNR], xr[UNR][CPL];
-#pragma unroll
-      for (int t = 0; t < UNR; ++t) {
-        const uint32_t i = s0 + ((uint32_t)t < len ? (uint32_t)t : 0u);
-        row[t] = a.occ_row[i];
-        x[t] = valued ? a.occ_x[i] : 1.f;
-      }
-#pragma unroll
-      for (int t = 0; t < UNR; ++t) {
-        pr[t] = a.p[row[t]];
-        const float* xrow = d > 0 ? a.XVp + (int64_t)row[t] * d : a.zpad;
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int cd = l + k * G;
-          xr[t][k] = xrow[cd < d ? cd : 0];
-        }
-      }
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         if ((uint32_t)t < len && pr[t] != 0.f) {

@@ -17,7 +17,7 @@ struct FwdArgs {
   const int32_t* wpos;
   const int32_t* vpos;
   const float* Vbase;
-  const float* zpad;     // >= 1024 device zeros: target of masked (clamped) gathers
+  const float* zpad;     // kZpadFloats device zeros: targets of masked (clamped) gathers
   int d;
   const float* label;
   const float* rw;

@@ -92,12 +92,15 @@ struct Context {
   Table T{};
   int64_t cap = 0;
   DevState* ds = nullptr;  // device
-  float* zpad = nullptr;   // 1024 device zeros (masked-gather target)
+  float* zpad = nullptr;   // kZpadFloats device zeros (masked-gather targets)
   Workspace ws;
   // per-phase HIP-event timing of dfx_train_step (dfx_prof_*); events on c->stream
   std::vector<hipEvent_t> prof_ev;  // prof_max steps x kProfMarks
   int prof_max = 0, prof_n = 0;
 };
+
+// masked gathers read zpad + ((index & 255) << 4) + [0, 1024): 256 spread 64-byte lines
+constexpr int kZpadFloats = 256 * 16 + 1024;
 
 constexpr int kProfMarks = 8;  // start, localize, feacnt, pull, fwd, auc, bwd, initv/end
 inline void prof_mark(Context* c, int m) {

@@ -166,11 +166,22 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
         if (a.segslot) a.segslot[rank] = a.nslot[pos];
       }
       if (a.col) a.col[pos] = rank;
-      if (a.occ_row) a.occ_row[idx] = a.rowid[pos];
-      if (a.occ_x) a.occ_x[idx] = a.value[pos];
       if (idx == n - 1) {
         a.ds->u_count = rank + 1;
         if (a.segstart) a.segstart[rank + 1] = (uint32_t)n;
+      }
+    }
+  }
+  // per-occurrence outputs need no rank: write them striped (coalesced stores)
+  if (a.occ_row) {
+    const int64_t tb = (int64_t)blockIdx.x * kLocTile;
+#pragma unroll
+    for (int i = 0; i < kLocItems; ++i) {
+      const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
+      if (idx < n) {
+        const uint32_t pos = P[idx];
+        a.occ_row[idx] = a.rowid[pos];
+        if (a.occ_x) a.occ_x[idx] = a.value[pos];
       }
     }
   }
