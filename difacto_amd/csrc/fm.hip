@@ -1,23 +1,23 @@
 // FMLoss / LogitLoss forward and backward on gfx950 (src/loss/fm_loss.h:56-203,
 // src/loss/logit_loss.h:41-103, src/common/spmv.h, spmm.h).
 //
-// Forward (k_fm_fwd): a group of G lanes owns one CSR row, lane l owns V coordinates
-// l, l+G, ...  Each lane walks the row's nnz in order, so X*V and (X.*X)*(V.*V) are summed in
-// exactly the reference's (row, nnz) order; the V_dim-reduction is then done serially over
-// coordinates through wave shuffles — predictions are bit-identical to the reference.
-// At V_dim 16 a wave holds 4 rows and every gathered V row is one 64-byte segment.
-// The walk is latency-bound (col -> {w, V row} -> V), so each iteration first issues the
+// Forward (k_fm_fwd): a group of G lanes owns one CSR row; lane l owns the contiguous V
+// coordinates [l*CPL, l*CPL+CPL).  Every lane walks the row's nnz in order, so X*V and
+// (X.*X)*(V.*V) are summed in exactly the reference's (row, nnz) order; the V_dim reduction
+// then runs serially over coordinates 0..d-1 through wave shuffles — predictions are
+// bit-identical to the reference.  At V_dim 16 a group is 4 lanes x float4, so a wave holds
+// 16 rows and every gathered V row is one 64-byte segment read by 4 vector loads.
+// The walk is latency-bound (slot -> {w, V row} -> V), so each iteration first issues the
 // loads of UNR nnz (clamped, unconditional addresses) and only then accumulates them in
-// order: UNR independent gathers in flight per group instead of one.
+// order.
 //
 // Backward (k_fm_bwd): Xᵀ products as a sorted-key segmented reduction — no atomics.  A
-// group of G lanes owns one column (unique key); it walks that key's occurrences in the
-// Localizer's sorted (key, pos) order, i.e. ascending (row, nnz): the same order as the
-// reference's column-range-partitioned TransTimes, so gradients are deterministic and, up
-// to expf, bit-identical.  The Localizer already wrote each occurrence's row (and value) in
-// sorted order, so the walk is occ_row -> {p, XV*p row}; the key's own state is loaded up
-// front, independent of the walk.  In the fused step the walk ends in the FTRL/AdaGrad
-// update of the key (no gradient round trip through HBM).
+// group owns one unique key and walks its occurrences in the Localizer's sorted (key, pos)
+// order, i.e. ascending (row, nnz): the order of the reference's column-range-partitioned
+// TransTimes, so gradients are deterministic and, up to expf, bit-identical.  The key's
+// table entry and the first occurrences are loaded first, then V / Vaux and the rows' p and
+// XV*p; in the fused step the walk ends in the FTRL/AdaGrad update of the key (no gradient
+// round trip through HBM).
 #include "fm_args.h"
 
 namespace dfx {
@@ -38,10 +38,48 @@ __device__ inline float logit_p(float label, float pred, const float* rw, int64_
   return p;
 }
 
-template <int G, int CPL, int MODE, bool PACKED>
+// Coordinates [l*CPL, l*CPL+CPL) of a length-d row.  VEC: d is a multiple of the vector
+// width and the row 16-byte aligned, so a lane's chunk is wholly inside or wholly outside
+// the row (outside chunks read chunk 0 and are ignored).
+template <int CPL, bool VEC>
+__device__ inline void load_coords(const float* row, int l, int d, float (&v)[CPL]) {
+  const int base = l * CPL;
+  if constexpr (VEC && CPL % 4 == 0) {
+    const int b = base < d ? base : 0;
+#pragma unroll
+    for (int m = 0; m < CPL / 4; ++m) {
+      const float4 f = *reinterpret_cast<const float4*>(row + b + 4 * m);
+      v[4 * m] = f.x; v[4 * m + 1] = f.y; v[4 * m + 2] = f.z; v[4 * m + 3] = f.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int cd = base + k;
+      v[k] = row[cd < d ? cd : 0];
+    }
+  }
+}
+
+template <int CPL, bool VEC>
+__device__ inline void store_coords(float* row, int l, int d, const float (&v)[CPL]) {
+  const int base = l * CPL;
+  if (base >= d) return;
+  if constexpr (VEC && CPL % 4 == 0) {
+#pragma unroll
+    for (int m = 0; m < CPL / 4; ++m)
+      *reinterpret_cast<float4*>(row + base + 4 * m) =
+          make_float4(v[4 * m], v[4 * m + 1], v[4 * m + 2], v[4 * m + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+      if (base + k < d) row[base + k] = v[k];
+  }
+}
+
+template <int G, int CPL, int MODE, bool PACKED, bool VEC>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   constexpr int RPB = kFmNT / G;  // rows per block
-  constexpr int UNR = CPL <= 2 ? 8 : (CPL <= 4 ? 4 : 2);
+  constexpr int UNR = CPL <= 4 ? 8 : (CPL <= 8 ? 4 : 2);
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t r = (int64_t)blockIdx.x * RPB + g;
@@ -69,9 +107,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         if (PACKED) {
-          // the key's table entry: w and its V row share one cache line; V is visible
-          // only if present and not (l1_shrk && w == 0)  (SGDUpdater::Get, :40-43)
-          const int2 wr = *reinterpret_cast<const int2*>(a.T.ent + c[t]);  // {w, vrow}
+          // the key's table entry: {w, vrow} in one 8-byte load; V is visible only if
+          // present and not (l1_shrk && w == 0)  (SGDUpdater::Get, sgd_updater.cc:40-43)
+          const int2 wr = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
           w[t] = __int_as_float(wr.x);
           const int vr = wr.y;
           vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
@@ -93,11 +131,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         // single-L2-channel hotspot when many keys have no V)
         const float* Vr = vp[t] < 0 ? a.zpad + ((c[t] & 255u) << 4)
                                     : (PACKED ? a.Vbase + (int64_t)vp[t] * d : a.Vbase + vp[t]);
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int cd = l + k * G;
-          v[t][k] = Vr[cd < d ? cd : 0];
-        }
+        load_coords<CPL, VEC>(Vr, l, d, v[t]);
       }
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
@@ -113,14 +147,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           const float xx = x[t] * x[t];  // XX_ (fm_loss.h:86-92)
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
-            const int cd = l + k * G;
-            if (cd < d) {
-              const float vk = v[t][k];
-              xv[k] = valued ? xv[k] + vk * x[t] : xv[k] + vk;
-              if (MODE != kGradPrep) {
-                const float vv = vk * vk;  // VV (fm_loss.h:95-101)
-                xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
-              }
+            const float vk = v[t][k];
+            xv[k] = valued ? xv[k] + vk * x[t] : xv[k] + vk;
+            if (MODE != kGradPrep) {
+              const float vv = vk * vk;  // VV (fm_loss.h:95-101)
+              xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
             }
           }
         }
@@ -128,17 +159,17 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
     }
     float pr = acc;
     if (MODE != kGradPrep && d > 0) {
-      // s = sum_l (XV_l^2 - XXVV_l), serially in l (fm_loss.h:110-113)
+      // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
       float t[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) t[k] = xv[k] * xv[k] - xxvv[k];
       float s = 0.f;
       const int gbase = (threadIdx.x % kWave) - l;
+      for (int q = 0; q < G; ++q) {
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        for (int q = 0; q < G; ++q) {
-          float tk = __shfl(t[k], gbase + q, kWave);
-          if (k * G + q < d) s += tk;
+        for (int k = 0; k < CPL; ++k) {
+          const float tk = __shfl(t[k], gbase + q, kWave);
+          if (q * CPL + k < d) s += tk;
         }
       }
       double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
@@ -159,12 +190,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         }
       }
       if (d > 0) {
-        float* o = a.XVp + r * d;
+        float o[CPL];
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int cd = l + k * G;
-          if (cd < d) o[cd] = xv[k] * p;  // XV_ *= p (fm_loss.h:196-199)
-        }
+        for (int k = 0; k < CPL; ++k) o[k] = xv[k] * p;  // XV_ *= p (fm_loss.h:196-199)
+        store_coords<CPL, VEC>(a.XVp + r * d, l, d, o);
       }
     }
   }
@@ -180,54 +209,73 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   }
 }
 
+// Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
+// multiple of 4); otherwise scalar coordinates (the pulled interleaved layout is unaligned).
+void lanes_for(int d, bool vec, int* G, int* CPL, bool* use_vec) {
+  if (d <= 0) {
+    *G = 1; *CPL = 1; *use_vec = false;
+    return;
+  }
+  if (vec && d % 4 == 0) {
+    int cpl = 4;
+    while (d / cpl > 64) cpl *= 2;
+    int n = (d + cpl - 1) / cpl, g = 1;
+    while (g < n) g <<= 1;
+    *G = g; *CPL = cpl; *use_vec = true;
+    return;
+  }
+  int g = next_pow2_lanes(d);
+  int cpl = (d + g - 1) / g, c2 = 1;
+  while (c2 < cpl) c2 <<= 1;
+  *G = g; *CPL = c2; *use_vec = false;
+}
+
+#define DFX_SCALAR_SET(X) X(1, 1, false) X(2, 1, false) X(4, 1, false) X(8, 1, false) \
+  X(16, 1, false) X(32, 1, false) X(64, 1, false) X(64, 2, false) X(64, 4, false)     \
+  X(64, 8, false) X(64, 16, false)
+#define DFX_VEC_SET(X) X(1, 4, true) X(2, 4, true) X(4, 4, true) X(8, 4, true) X(16, 4, true) \
+  X(32, 4, true) X(64, 4, true) X(64, 8, true) X(64, 16, true)
+
 template <int MODE, bool PACKED>
-static int launch_fwd_gc(const FwdArgs& a, int G, int CPL, hipStream_t st) {
+static int launch_fwd_gc(const FwdArgs& a, int G, int CPL, bool vec, hipStream_t st) {
   const int64_t rpb = kFmNT / G;
   dim3 grid((unsigned)((a.B + rpb - 1) / rpb));
   if (a.B <= 0) return DFX_OK;
-#define DFX_FWD(GG, CC)                                                                   \
-  if (G == GG && CPL == CC) {                                                             \
-    hipLaunchKernelGGL((k_fm_fwd<GG, CC, MODE, PACKED>), grid, dim3(kFmNT), 0, st, a);   \
-    DFX_HIP(hipGetLastError());                                                           \
-    return DFX_OK;                                                                        \
+#define DFX_FWD(GG, CC, VV)                                                                  \
+  if (G == GG && CPL == CC && vec == VV) {                                                   \
+    hipLaunchKernelGGL((k_fm_fwd<GG, CC, MODE, PACKED, VV>), grid, dim3(kFmNT), 0, st, a);  \
+    DFX_HIP(hipGetLastError());                                                              \
+    return DFX_OK;                                                                           \
   }
-  DFX_FWD(1, 1) DFX_FWD(2, 1) DFX_FWD(4, 1) DFX_FWD(8, 1) DFX_FWD(16, 1) DFX_FWD(32, 1)
-  DFX_FWD(64, 1) DFX_FWD(64, 2) DFX_FWD(64, 4) DFX_FWD(64, 8) DFX_FWD(64, 16)
+  DFX_SCALAR_SET(DFX_FWD)
+  if constexpr (PACKED) { DFX_VEC_SET(DFX_FWD) }
 #undef DFX_FWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
 }
 
-void lanes_for(int d, int* G, int* CPL) {
-  int g = next_pow2_lanes(d < 1 ? 1 : d);
-  int cpl = (d + g - 1) / g;
-  if (cpl < 1) cpl = 1;
-  int c2 = 1;
-  while (c2 < cpl) c2 <<= 1;
-  *G = g;
-  *CPL = c2;
-}
-
 template <int MODE, bool PACKED>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   int G, CPL;
-  lanes_for(a.d, &G, &CPL);
-  return launch_fwd_gc<MODE, PACKED>(a, G, CPL, st);
+  bool vec;
+  lanes_for(a.d, PACKED, &G, &CPL, &vec);
+  return launch_fwd_gc<MODE, PACKED>(a, G, CPL, vec, st);
 }
 
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
   int G, CPL;
-  lanes_for(a.d, &G, &CPL);
+  bool vec;
+  lanes_for(a.d, true, &G, &CPL, &vec);
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
-  return launch_fwd_gc<kFused, true>(a, G, CPL, st);
+  return launch_fwd_gc<kFused, true>(a, G, CPL, vec, st);
 }
 
 // ---- backward: sorted-key segmented reduction --------------------------------------------
-template <int G, int CPL, bool FUSED>
+template <int G, int CPL, bool FUSED, bool VEC>
 __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   constexpr int SPB = kFmNT / G;
-  constexpr int UNR = CPL <= 2 ? 4 : 2;
+  constexpr int UNR = CPL <= 4 ? 4 : 2;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t u = (int64_t)blockIdx.x * SPB + g;
@@ -267,43 +315,29 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float gw = 0.f;
     float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
     float vcur[CPL], ccur[CPL], g0[CPL];
+    const float* zp = a.zpad + ((cidx & 255u) << 4);
     if (FUSED) {
       e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
       vrow = __float_as_int(h.y);
       // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
       vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
-      const float* Vr = vq >= 0 ? a.T.V + (int64_t)vq * d : a.zpad + ((cidx & 255u) << 4);
-      const float* Cr = vq >= 0 ? a.T.Vaux + (int64_t)vq * d : a.zpad + ((cidx & 255u) << 4);
+      load_coords<CPL, VEC>(vq >= 0 ? a.T.V + (int64_t)vq * d : zp, l, d, vcur);
+      load_coords<CPL, VEC>(vq >= 0 ? a.T.Vaux + (int64_t)vq * d : zp, l, d, ccur);
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const int cd = l + k * G;
-        vcur[k] = Vr[cd < d ? cd : 0];
-        ccur[k] = Cr[cd < d ? cd : 0];
-        g0[k] = 0.f;
-      }
+      for (int k = 0; k < CPL; ++k) g0[k] = 0.f;
     } else {
       gw = a.grad[wq < 0 ? 0 : wq];
       if (wq < 0) gw = 0.f;
-      const float* Vr = vq >= 0 ? a.W + vq : a.zpad + ((cidx & 255u) << 4);
-      const float* Gr = vq >= 0 ? a.grad + vq : a.zpad + ((cidx & 255u) << 4);
+      load_coords<CPL, VEC>(vq >= 0 ? a.W + vq : zp, l, d, vcur);
+      load_coords<CPL, VEC>(vq >= 0 ? a.grad + vq : zp, l, d, g0);
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const int cd = l + k * G;
-        vcur[k] = Vr[cd < d ? cd : 0];
-        g0[k] = Gr[cd < d ? cd : 0];
-        ccur[k] = 0.f;
-      }
+      for (int k = 0; k < CPL; ++k) ccur[k] = 0.f;
     }
     float pr[UNR], xr[UNR][CPL];
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
       pr[t] = a.p[row[t]];
-      const float* xrow = d > 0 ? a.XVp + (int64_t)row[t] * d : a.zpad;
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) {
-        const int cd = l + k * G;
-        xr[t][k] = xrow[cd < d ? cd : 0];
-      }
+      load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)row[t] * d : zp, l, d, xr[t]);
     }
     float xxp = 0.f;
     float acc[CPL];
@@ -338,25 +372,25 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       }
     } else {
       for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
-        uint32_t row[UNR];
-        float x[UNR], pr[UNR];
+        uint32_t rw[UNR];
+        float xw[UNR], pw[UNR];
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
           const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-          row[t] = a.occ_row[i];
-          x[t] = valued ? a.occ_x[i] : 1.f;
+          rw[t] = a.occ_row[i];
+          xw[t] = valued ? a.occ_x[i] : 1.f;
         }
 #pragma unroll
-        for (int t = 0; t < UNR; ++t) pr[t] = a.p[row[t]];
+        for (int t = 0; t < UNR; ++t) pw[t] = a.p[rw[t]];
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
-          if (i0 + t < s1 && pr[t] != 0.f) {
+          if (i0 + t < s1 && pw[t] != 0.f) {
             if (valued) {
-              gw += pr[t] * x[t];
-              xxp += pr[t] * (x[t] * x[t]);
+              gw += pw[t] * xw[t];
+              xxp += pw[t] * (xw[t] * xw[t]);
             } else {
-              gw += pr[t];
-              xxp += pr[t];
+              gw += pw[t];
+              xxp += pw[t];
             }
           }
         }
@@ -365,29 +399,23 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
         for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
-          uint32_t row[UNR];
-          float x[UNR], xr[UNR][CPL];
+          uint32_t rw[UNR];
+          float xw[UNR], xrw[UNR][CPL];
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
             const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-            row[t] = a.occ_row[i];
-            x[t] = valued ? a.occ_x[i] : 1.f;
+            rw[t] = a.occ_row[i];
+            xw[t] = valued ? a.occ_x[i] : 1.f;
           }
 #pragma unroll
-          for (int t = 0; t < UNR; ++t) {
-            const float* xrow = a.XVp + (int64_t)row[t] * d;
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-              const int cd = l + k * G;
-              xr[t][k] = xrow[cd < d ? cd : 0];
-            }
-          }
+          for (int t = 0; t < UNR; ++t)
+            load_coords<CPL, VEC>(a.XVp + (int64_t)rw[t] * d, l, d, xrw[t]);
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
             if (i0 + t < s1) {
 #pragma unroll
               for (int k = 0; k < CPL; ++k)
-                acc[k] = valued ? acc[k] + xr[t][k] * x[t] : acc[k] + xr[t][k];
+                acc[k] = valued ? acc[k] + xrw[t][k] * xw[t] : acc[k] + xrw[t][k];
             }
           }
         }
@@ -395,29 +423,16 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     }
     if (!FUSED) {
       if (l == 0 && wq >= 0) a.grad[wq] = gw;
-      if (vq >= 0) {
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int cd = l + k * G;
-          if (cd < d) a.grad[vq + cd] = acc[k];
-        }
-      }
+      if (vq >= 0) store_coords<CPL, VEC>(a.grad + vq, l, d, acc);
     } else {
       // Update(kGradient): UpdateW (FTRL), then UpdateV (AdaGrad) if V was pulled
       bool tr;
       const int dw = ftrl_update(a.Pm, gw, &e, &tr);
       if (vq >= 0) {
-        float* V = a.T.V + (int64_t)vq * d;
-        float* C = a.T.Vaux + (int64_t)vq * d;
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const int cd = l + k * G;
-          if (cd < d) {
-            adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
-            V[cd] = vcur[k];
-            C[cd] = ccur[k];
-          }
-        }
+        for (int k = 0; k < CPL; ++k) adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
+        store_coords<CPL, VEC>(a.T.V + (int64_t)vq * d, l, d, vcur);
+        store_coords<CPL, VEC>(a.T.Vaux + (int64_t)vq * d, l, d, ccur);
       }
       if (l == 0) {
         ent_set_state(a.T.ent + sl, e);
@@ -444,17 +459,18 @@ template <bool FUSED>
 int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;
-  lanes_for(a.d, &G, &CPL);
+  bool vec;
+  lanes_for(a.d, FUSED, &G, &CPL, &vec);
   const int64_t spb = kFmNT / G;
   dim3 grid((unsigned)((nseg_bound + spb - 1) / spb));
-#define DFX_BWD(GG, CC)                                                               \
-  if (G == GG && CPL == CC) {                                                         \
-    hipLaunchKernelGGL((k_fm_bwd<GG, CC, FUSED>), grid, dim3(kFmNT), 0, st, a);      \
-    DFX_HIP(hipGetLastError());                                                       \
-    return DFX_OK;                                                                    \
+#define DFX_BWD(GG, CC, VV)                                                              \
+  if (G == GG && CPL == CC && vec == VV) {                                               \
+    hipLaunchKernelGGL((k_fm_bwd<GG, CC, FUSED, VV>), grid, dim3(kFmNT), 0, st, a);     \
+    DFX_HIP(hipGetLastError());                                                          \
+    return DFX_OK;                                                                       \
   }
-  DFX_BWD(1, 1) DFX_BWD(2, 1) DFX_BWD(4, 1) DFX_BWD(8, 1) DFX_BWD(16, 1) DFX_BWD(32, 1)
-  DFX_BWD(64, 1) DFX_BWD(64, 2) DFX_BWD(64, 4) DFX_BWD(64, 8) DFX_BWD(64, 16)
+  DFX_SCALAR_SET(DFX_BWD)
+  if constexpr (FUSED) { DFX_VEC_SET(DFX_BWD) }
 #undef DFX_BWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
