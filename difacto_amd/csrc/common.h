@@ -112,13 +112,20 @@ static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
 
 struct Table {
   Entry* ent;       // cap entries
-  float* V;         // vcap * d
-  float* Vaux;      // vcap * d (AdaGrad accumulators)
+  float* V;         // vcap rows of [V(d) | Vaux(d)]: a key's embedding and its AdaGrad
+                    // accumulators share one 2*d*4-byte row (one 128-byte line at d = 16)
   uint64_t mask;    // cap - 1
   int logcap;
   int d;
   int64_t vcap;
 };
+
+__host__ __device__ inline float* row_V(const Table& t, int64_t vr) {
+  return t.V + vr * 2 * (int64_t)t.d;
+}
+__host__ __device__ inline float* row_C(const Table& t, int64_t vr) {
+  return t.V + vr * 2 * (int64_t)t.d + t.d;
+}
 
 __device__ inline float4 ent_state(const Entry* e) {
   const float4 a = *reinterpret_cast<const float4*>(e);  // w, vrow, sqrt_g, z

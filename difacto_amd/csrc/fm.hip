@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         // masked items read zeros from one of 256 spread lines (one shared line would be a
         // single-L2-channel hotspot when many keys have no V)
         const float* Vr = vp[t] < 0 ? a.zpad + ((c[t] & 255u) << 4)
-                                    : (PACKED ? a.Vbase + (int64_t)vp[t] * d : a.Vbase + vp[t]);
+                                    : (PACKED ? row_V(a.T, vp[t]) : a.Vbase + vp[t]);
         load_coords<CPL, VEC>(Vr, l, d, v[t]);
       }
 #pragma unroll
@@ -321,8 +321,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       vrow = __float_as_int(h.y);
       // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
       vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
-      load_coords<CPL, VEC>(vq >= 0 ? a.T.V + (int64_t)vq * d : zp, l, d, vcur);
-      load_coords<CPL, VEC>(vq >= 0 ? a.T.Vaux + (int64_t)vq * d : zp, l, d, ccur);
+      load_coords<CPL, VEC>(vq >= 0 ? row_V(a.T, vq) : zp, l, d, vcur);
+      load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) g0[k] = 0.f;
     } else {
@@ -431,8 +431,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (vq >= 0) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
-        store_coords<CPL, VEC>(a.T.V + (int64_t)vq * d, l, d, vcur);
-        store_coords<CPL, VEC>(a.T.Vaux + (int64_t)vq * d, l, d, ccur);
+        store_coords<CPL, VEC>(row_V(a.T, vq), l, d, vcur);
+        store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur);
       }
       if (l == 0) {
         ent_set_state(a.T.ent + sl, e);

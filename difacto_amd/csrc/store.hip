@@ -7,8 +7,8 @@
 //                       multiplicative hash of the (already nibble-reversed) key and linear
 //                       probing, cap = pow2 >= 2*max_keys.  A probe's cache line carries the
 //                       key's whole scalar state.
-//   V     f32[vcap*d]   embedding rows, allocated by InitV in rand_r order
-//   Vaux  f32[vcap*d]   AdaGrad accumulators
+//   V     f32[vcap*2d]  rows of [V(d) | Vaux(d)] (embedding + AdaGrad accumulators in one
+//                       row: one 128-byte line per key at V_dim 16), allocated by InitV
 // InitV (sgd_updater.cc:144-152) draws glibc rand_r in key order; on the GPU every key that
 // needs V gets its exclusive-scan rank r among this push's InitV keys and jumps the LCG by
 // 3*V_dim*r steps, which reproduces the reference's sequential draws exactly.
@@ -61,8 +61,8 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
     atomicOr(&ds->err, kErrPoolFull);
     return;
   }
-  float* V = T.V + vr * d;
-  float* C = T.Vaux + vr * d;
+  float* V = row_V(T, vr);
+  float* C = row_C(T, vr);
   for (int k = 0; k < d; ++k) {
     V[k] = initv_value(rand_r_dev(&s), scale);
     C[k] = 0.f;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(kStNT) void k_pull_write(int64_t n, Table T, Params
   vals[o] = w;
   const int d = T.d;
   if (live) {
-    const float* V = T.V + (int64_t)vr * d;
+    const float* V = row_V(T, vr);
     for (int k = 0; k < d; ++k) vals[o + 1 + k] = V[k];
   }
   if (lens) lens[i] = live ? d + 1 : 1;
@@ -209,8 +209,8 @@ __global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* 
         } else if (vr < 0) {
           atomicOr(&ds->err, kErrNoV);
         } else {
-          float* V = T.V + (int64_t)vr * d;
-          float* C = T.Vaux + (int64_t)vr * d;
+          float* V = row_V(T, vr);
+          float* C = row_C(T, vr);
           for (int k = 0; k < d; ++k) adagrad_update(P, vals[o + 1 + k], V + k, C + k);
         }
       }
@@ -277,10 +277,7 @@ int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
   DFX_HIP(hipStreamSynchronize(c->stream));
   c->cap = cap;
   T.vcap = T.d > 0 ? (n_vrows > 0 ? n_vrows : 1) : 0;
-  if (T.d > 0) {
-    DFX_HIP(hipMalloc(&T.V, T.vcap * T.d * sizeof(float)));
-    DFX_HIP(hipMalloc(&T.Vaux, T.vcap * T.d * sizeof(float)));
-  }
+  if (T.d > 0) DFX_HIP(hipMalloc(&T.V, T.vcap * 2 * T.d * sizeof(float)));
   return DFX_OK;
 }
 
@@ -288,7 +285,6 @@ void table_release(Context* c) {
   Table& T = c->T;
   if (T.ent) (void)hipFree(T.ent);
   if (T.V) (void)hipFree(T.V);
-  if (T.Vaux) (void)hipFree(T.Vaux);
   T = Table{};
 }
 
@@ -327,16 +323,14 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
   if (T.d > 0 && n_vrows > T.vcap) {
     HostCounters h;
     DFX_TRY(read_counters(c, &h));
-    float *nV, *nC;
-    DFX_HIP(hipMalloc(&nV, n_vrows * T.d * sizeof(float)));
-    DFX_HIP(hipMalloc(&nC, n_vrows * T.d * sizeof(float)));
+    float* nV;
+    DFX_HIP(hipMalloc(&nV, n_vrows * 2 * T.d * sizeof(float)));
     if (h.n_vrows) {
-      DFX_HIP(hipMemcpy(nV, T.V, h.n_vrows * T.d * sizeof(float), hipMemcpyDeviceToDevice));
-      DFX_HIP(hipMemcpy(nC, T.Vaux, h.n_vrows * T.d * sizeof(float), hipMemcpyDeviceToDevice));
+      DFX_HIP(hipMemcpy(nV, T.V, h.n_vrows * 2 * T.d * sizeof(float), hipMemcpyDeviceToDevice));
     }
     (void)hipFree(T.V);
-    (void)hipFree(T.Vaux);
-    T.V = nV; T.Vaux = nC; T.vcap = n_vrows;
+    T.V = nV;
+    T.vcap = n_vrows;
   }
   return DFX_OK;
 }
@@ -375,7 +369,7 @@ __global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
     const int vr = T.ent[i].vrow;
     if (vr >= 0) {
       nnz += T.d;
-      const float* V = T.V + (int64_t)vr * T.d;
+      const float* V = row_V(T, vr);
       for (int k = 0; k < T.d; ++k) objv += .5 * P.l2 * V[k] * V[k];  // (sic) l2, :21
     }
   }
@@ -392,21 +386,22 @@ __global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
 // host copy of the table for save / dump
 struct HostTable {
   std::vector<Entry> ent;
-  std::vector<float> V, C;
+  std::vector<float> VV;  // n_vrows rows of [V(d) | Vaux(d)]
+  int d = 0;
+  const float* V(int vr) const { return VV.data() + (size_t)vr * 2 * d; }
+  const float* C(int vr) const { return VV.data() + (size_t)vr * 2 * d + d; }
 };
 
 static int copy_table_to_host(Context* c, HostTable* h) {
   const Table& T = c->T;
   HostCounters hc;
   DFX_TRY(read_counters(c, &hc));
+  h->d = T.d;
   h->ent.resize(c->cap);
-  h->V.resize((size_t)hc.n_vrows * T.d);
-  h->C.resize((size_t)hc.n_vrows * T.d);
+  h->VV.resize((size_t)hc.n_vrows * 2 * T.d);
   DFX_HIP(hipMemcpy(h->ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
-  if (!h->V.empty()) {
-    DFX_HIP(hipMemcpy(h->V.data(), T.V, h->V.size() * 4, hipMemcpyDeviceToHost));
-    DFX_HIP(hipMemcpy(h->C.data(), T.Vaux, h->C.size() * 4, hipMemcpyDeviceToHost));
-  }
+  if (!h->VV.empty())
+    DFX_HIP(hipMemcpy(h->VV.data(), T.V, h->VV.size() * 4, hipMemcpyDeviceToHost));
   return DFX_OK;
 }
 
@@ -544,8 +539,8 @@ int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has
       state[0] = e.w; state[1] = e.sqrt_g; state[2] = e.z; state[3] = e.fea_cnt;
       *has_v = e.vrow >= 0;
       if (e.vrow >= 0 && V) {
-        DFX_HIP(hipMemcpy(V, T.V + (int64_t)e.vrow * T.d, T.d * 4, hipMemcpyDeviceToHost));
-        DFX_HIP(hipMemcpy(V + T.d, T.Vaux + (int64_t)e.vrow * T.d, T.d * 4,
+        DFX_HIP(hipMemcpy(V, row_V(T, e.vrow), T.d * 4, hipMemcpyDeviceToHost));
+        DFX_HIP(hipMemcpy(V + T.d, row_C(T, e.vrow), T.d * 4,
                           hipMemcpyDeviceToHost));
       }
       *found = 1;
@@ -577,8 +572,8 @@ int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux) {
     fwrite(&e.w, 4, 1, f);
     if (aux) { fwrite(&e.sqrt_g, 4, 1, f); fwrite(&e.z, 4, 1, f); }
     if (size == 1) continue;
-    fwrite(ht.V.data() + (size_t)e.vrow * d, 4, d, f);
-    if (aux) fwrite(ht.C.data() + (size_t)e.vrow * d, 4, d, f);
+    fwrite(ht.V(e.vrow), 4, d, f);
+    if (aux) fwrite(ht.C(e.vrow), 4, d, f);
   }
   fclose(f);
   return DFX_OK;
@@ -598,7 +593,7 @@ int dfx_store_load(dfx_ctx* ctx, const char* path) {
   std::vector<uint64_t> keys;
   std::vector<float4> st;
   std::vector<int32_t> vr;
-  std::vector<float> V, C;
+  std::vector<float> VV;  // rows of [V(d) | Vaux(d)]
   uint64_t key;
   int64_t vnext = (int64_t)hc.n_vrows;
   while (fread(&key, 8, 1, f) == 1) {
@@ -613,13 +608,12 @@ int dfx_store_load(dfx_ctx* ctx, const char* path) {
     int32_t row = -1;
     if (size > 1) {
       if (size != T.d + 1) { fclose(f); set_error("model V_dim mismatch"); return DFX_ERR_CHECK; }
-      size_t base = V.size();
-      V.resize(base + T.d);
-      C.resize(base + T.d, 0.f);
-      if (fread(V.data() + base, 4, T.d, f) != (size_t)T.d) {
+      size_t base = VV.size();
+      VV.resize(base + 2 * T.d, 0.f);
+      if (fread(VV.data() + base, 4, T.d, f) != (size_t)T.d) {
         fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
       }
-      if (aux && fread(C.data() + base, 4, T.d, f) != (size_t)T.d) {
+      if (aux && fread(VV.data() + base + T.d, 4, T.d, f) != (size_t)T.d) {
         fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
       }
       row = (int32_t)vnext++;
@@ -641,10 +635,8 @@ int dfx_store_load(dfx_ctx* ctx, const char* path) {
   DFX_HIP(hipMemcpy(dk, keys.data(), n * 8, hipMemcpyHostToDevice));
   DFX_HIP(hipMemcpy(dst, st.data(), n * sizeof(float4), hipMemcpyHostToDevice));
   DFX_HIP(hipMemcpy(dvr, vr.data(), n * 4, hipMemcpyHostToDevice));
-  if (!V.empty()) {
-    DFX_HIP(hipMemcpy(T.V + hc.n_vrows * T.d, V.data(), V.size() * 4, hipMemcpyHostToDevice));
-    DFX_HIP(hipMemcpy(T.Vaux + hc.n_vrows * T.d, C.data(), C.size() * 4, hipMemcpyHostToDevice));
-  }
+  if (!VV.empty())
+    DFX_HIP(hipMemcpy(row_V(T, hc.n_vrows), VV.data(), VV.size() * 4, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_load, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, dk, dst, dvr,
                      aux ? 1 : 0, T, c->ds);
   DFX_HIP(hipStreamSynchronize(c->stream));
@@ -678,10 +670,10 @@ int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_revers
     os << '\t' << size << '\t' << e.w;
     if (dump_aux) os << '\t' << e.sqrt_g << '\t' << e.z;
     if (size > 1) {
-      const float* v = ht.V.data() + (size_t)e.vrow * d;
+      const float* v = ht.V(e.vrow);
       for (int k = 0; k < d; ++k) os << '\t' << v[k];
       if (dump_aux) {
-        const float* cc = ht.C.data() + (size_t)e.vrow * d;
+        const float* cc = ht.C(e.vrow);
         for (int k = 0; k < d; ++k) os << '\t' << cc[k];
       }
     }
