@@ -71,6 +71,13 @@ _SIGS = {
     "dfx_progress_read": (ctypes.c_int, [vp, ctypes.POINTER(Progress), ctypes.c_int]),
     "dfx_prof_enable": (ctypes.c_int, [vp, ctypes.c_int]),
     "dfx_prof_read": (ctypes.c_int, [vp, f64p, ctypes.POINTER(ctypes.c_int), f64p]),
+    "dfx_dist_record_floats": (ctypes.c_int, [vp]),
+    "dfx_dist_localize": (ctypes.c_int, [vp, ctypes.POINTER(Batch), c_u64, ctypes.c_int, vp, vp,
+                                         i64p, i64p]),
+    "dfx_dist_owner_begin": (ctypes.c_int, [vp, vp, i64p, ctypes.c_int, vp]),
+    "dfx_dist_owner_pull": (ctypes.c_int, [vp, vp]),
+    "dfx_dist_fwd_bwd": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, ctypes.c_int, vp, vp]),
+    "dfx_dist_owner_push": (ctypes.c_int, [vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -164,6 +164,8 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   w.av0.release();
   w.av1.release();
   w.atiles.release();
+  for (DevBuf* b : {&w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted})
+    b->release();
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   table_release(c);
   if (c->zpad) (void)hipFree(c->zpad);

@@ -1,0 +1,522 @@
+// Key-range-sharded multi-GPU store: the device phases of one synchronous data-parallel step.
+//
+// The reference's distributed store (src/store/kvstore_dist.h) shards the model over ps-lite
+// servers by key range; a worker ZPushes / ZPulls its sorted keys (:90-108) and each server
+// answers a pull with updater_->Get (:167-175) and applies every push as one
+// updater_->Update call (:158-165), each server holding its own SGDUpdater (own rand_r seed,
+// own new_w).  Here every GPU is both a worker (its own minibatch) and the server of one
+// contiguous range of the nibble-reversed (hence uniform) key space:
+//   owner(k) = floor(k * N / 2^64).
+// The reference's sync_mode is a TODO (kvstore_dist.h:137-147); this is its bulk-synchronous
+// (max_delay 0) schedule, made deterministic by applying pushes in worker-rank order:
+//
+//   worker  dist_localize     Localizer::Compact of its batch; sorted keys split by owner
+//   --- alltoallv keys (+ occurrence counts in epoch 0) ---
+//   owner   dist_owner_begin  sort+dedupe the received keys (stable: rank order within a key),
+//                             find-or-insert their table slots; with counts, the ranks'
+//                             Update(kFeaCount) pushes in rank order, then their InitV draws
+//   owner   dist_owner_pull   SGDUpdater::Get per received key: record [V(d) | w | live | 0 0]
+//   --- alltoallv records back ---
+//   worker  dist_fwd_bwd      FMLoss Predict/Evaluate/AUC on its batch, CalcGrad into per-key
+//                             gradient records [gV(d) | gw | 0 | 0 | 0]
+//   --- alltoallv gradient records to the owners ---
+//   owner   dist_owner_push   the ranks' Update(kGradient) pushes in rank order: per key,
+//                             FTRL (+ AdaGrad if V was pulled) once per pushing rank; InitV
+//                             draws in (rank, key) order, the order one server would meet them
+//
+// Every per-key result therefore equals what N reference servers produce when worker r's push
+// reaches them r-th, with every pull of the step answered before any push.
+#include "fm_args.h"
+
+namespace dfx {
+
+constexpr int kDNT = 256;
+constexpr int kMaxRanks = 64;
+
+// launchers shared with fm.hip / metric.hip
+int launch_fwd_records(const FwdArgs& a, hipStream_t st, int* nblk);
+int launch_bwd_positions(const BwdArgs& a, int64_t nseg_bound, hipStream_t st);
+void sum_parts(Context* c, const double* part, int64_t n, double* out, bool accumulate);
+
+__host__ __device__ inline int rec_floats(int d) { return d + 4; }
+
+__device__ inline uint32_t owner_of(uint64_t k, uint32_t n) {
+  return (uint32_t)__umul64hi(k, (uint64_t)n);
+}
+
+// offsets of each source rank's keys in the owner's receive buffer (kernel argument)
+struct RankOffs {
+  int n;
+  int64_t off[kMaxRanks + 1];
+};
+
+__device__ inline int rank_of(const RankOffs& ro, int64_t i) {
+  int lo = 0, hi = ro.n;  // off[lo] <= i < off[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (ro.off[mid] <= i) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// ---- worker: split sorted unique keys by owner --------------------------------------------
+__global__ void k_owner_counts(const uint64_t* uniq, int64_t U, uint32_t nranks,
+                               unsigned long long* counts) {
+  __shared__ unsigned int c[kMaxRanks];
+  if (threadIdx.x < kMaxRanks) c[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < U) atomicAdd(&c[owner_of(uniq[u], nranks)], 1u);
+  __syncthreads();
+  if (threadIdx.x < nranks && c[threadIdx.x]) atomicAdd(&counts[threadIdx.x], c[threadIdx.x]);
+}
+
+// ---- worker: positions of the pulled records -----------------------------------------------
+__global__ void k_record_pos(const float* rec, int64_t U, int d, int32_t* wpos, int32_t* vpos) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const int64_t S = rec_floats(d);
+  wpos[u] = (int32_t)(u * S + d);
+  vpos[u] = (d > 0 && rec[u * S + d + 1] != 0.f) ? (int32_t)(u * S) : -1;
+}
+
+__global__ void k_dist_worker_finalize(DevState* ds, int64_t B) {
+  ds->prog[0] += (double)B;  // sgd::Progress of this worker (sgd_learner.cc:213-229)
+  ds->prog[1] += ds->scratch[3];
+  ds->prog[2] += ds->auc_n;
+}
+
+// ---- owner: received keys -> unique segments -----------------------------------------------
+__global__ void k_dist_init_masks(DevState* ds) {
+  ds->or_mask = 0;
+  ds->and_mask = ~0ull;
+}
+
+__global__ __launch_bounds__(kDNT) void k_dist_recv_prep(const uint64_t* keys, int64_t R,
+                                                         uint64_t* k0, uint32_t* p0,
+                                                         DevState* ds) {
+  __shared__ unsigned long long ro[kDNT / kWave], ra[kDNT / kWave];
+  const int64_t i = (int64_t)blockIdx.x * kDNT + threadIdx.x;
+  unsigned long long vor = 0, vand = ~0ull;
+  if (i < R) {
+    const uint64_t k = keys[i];
+    k0[i] = k;
+    p0[i] = (uint32_t)i;
+    vor = k;
+    vand = k;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    vor |= __shfl_xor(vor, off, kWave);
+    vand &= __shfl_xor(vand, off, kWave);
+  }
+  if (lane_id() == 0) { ro[threadIdx.x / kWave] = vor; ra[threadIdx.x / kWave] = vand; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    vor = ro[0];
+    vand = ra[0];
+    for (int w = 1; w < kDNT / kWave; ++w) { vor |= ro[w]; vand &= ra[w]; }
+    atomicOr(&ds->or_mask, vor);
+    atomicAnd(&ds->and_mask, vand);
+  }
+}
+
+__global__ void k_dist_diff(DevState* ds) { ds->diff_mask = ds->or_mask ^ ds->and_mask; }
+
+__global__ void k_dist_heads(const uint64_t* k0, const uint64_t* k1, int64_t R,
+                             const DevState* ds, uint32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R) return;
+  const uint64_t* K = ds->sortmeta[31] ? k1 : k0;
+  flags[i] = (i == 0 || K[i] != K[i - 1]) ? 1u : 0u;
+}
+
+// segstart[seg], segslot[seg] (find-or-insert), seg_of[received index], sorted_idx[sorted
+// position] = received index.  *total = number of unique keys.
+__global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* k0, const uint64_t* k1,
+                                                    const uint32_t* p0, const uint32_t* p1,
+                                                    int64_t R, DevState* ds,
+                                                    const uint32_t* excl, const uint32_t* total,
+                                                    Table T, uint32_t* segstart,
+                                                    uint32_t* segslot, uint32_t* seg_of,
+                                                    uint32_t* sorted_idx) {
+  const int64_t i = (int64_t)blockIdx.x * kDNT + threadIdx.x;
+  int ins = 0;
+  if (i < R) {
+    const bool s1 = ds->sortmeta[31] != 0;
+    const uint64_t* K = s1 ? k1 : k0;
+    const uint32_t* P = s1 ? p1 : p0;
+    const bool head = (i == 0 || K[i] != K[i - 1]);
+    const uint32_t seg = head ? excl[i] : excl[i] - 1u;  // excl[i] = heads before i
+    sorted_idx[i] = P[i];
+    seg_of[P[i]] = seg;
+    if (head) {
+      segstart[seg] = (uint32_t)i;
+      bool inserted;
+      int64_t s = tbl_insert(T, K[i], &inserted);
+      if (s < 0) {
+        atomicOr(&ds->err, kErrTableFull);
+        s = 0;
+      }
+      ins = inserted;
+      segslot[seg] = (uint32_t)s;
+    }
+    if (i == R - 1) segstart[*total] = (uint32_t)R;
+  }
+  for (int off = 32; off > 0; off >>= 1) ins += __shfl_xor(ins, off, kWave);
+  if (lane_id() == 0 && ins) atomicAdd(&ds->n_keys, (unsigned long long)ins);
+}
+
+// The ranks' Update(kFeaCount) pushes in rank order (sgd_updater.cc:64-75), per owned key:
+// fea_cnt += count; InitV once V is absent, w != 0 and fea_cnt > V_threshold.  frank[u] = the
+// pushing rank whose Update draws the key's InitV.
+__global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
+                              const uint32_t* sorted_idx, const float* recv_cnt, RankOffs ro,
+                              Table T, Params P, const uint32_t* nuniq, uint32_t* flags,
+                              uint32_t* frank) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= (int64_t)*nuniq) return;
+  Entry* e = &T.ent[segslot[u]];
+  float4 st = ent_state(e);  // {w, sqrt_g, z, fea_cnt}
+  bool has_v = e->vrow >= 0;
+  uint32_t f = 0, fr = 0;
+  for (uint32_t i = segstart[u]; i < segstart[u + 1]; ++i) {
+    const uint32_t src = sorted_idx[i];
+    st.w += recv_cnt[src];
+    if (P.V_dim > 0 && !has_v && st.x != 0.f && st.w > (float)P.V_threshold) {
+      has_v = true;
+      f = 1;
+      fr = (uint32_t)rank_of(ro, src);
+    }
+  }
+  e->fea_cnt = st.w;
+  flags[u] = f;
+  frank[u] = fr;
+}
+
+// The ranks' Update(kGradient) pushes in rank order (sgd_updater.cc:76-100): per pushing rank,
+// UpdateW (FTRL) and, when the rank pulled V (lens > 1), UpdateV (AdaGrad).  V was pulled iff
+// present and not (l1_shrk && w == 0) when the step's pulls were answered, before any push.
+__global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
+                            const uint32_t* sorted_idx, const float* g, RankOffs ro, Table T,
+                            Params P, const uint32_t* nuniq, uint32_t* flags, uint32_t* frank,
+                            DevState* ds) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int dnew = 0;
+  if (u < (int64_t)*nuniq) {
+    const int d = T.d;
+    const int64_t S = rec_floats(d);
+    Entry* en = &T.ent[segslot[u]];
+    float4 e = ent_state(en);
+    const int vr = en->vrow;
+    const bool pulled_v = vr >= 0 && !(P.l1_shrk && e.x == 0.f);
+    bool has_v = vr >= 0;
+    float* V = pulled_v ? row_V(T, vr) : nullptr;
+    float* C = pulled_v ? row_C(T, vr) : nullptr;
+    uint32_t f = 0, fr = 0;
+    for (uint32_t i = segstart[u]; i < segstart[u + 1]; ++i) {
+      const uint32_t src = sorted_idx[i];
+      const float* gr = g + (int64_t)src * S;
+      bool tr;
+      dnew += ftrl_update(P, gr[d], &e, &tr);
+      if (tr && d > 0 && !has_v && e.w > (float)P.V_threshold) {  // :118-121
+        has_v = true;
+        f = 1;
+        fr = (uint32_t)rank_of(ro, src);
+      }
+      if (pulled_v)
+        for (int k = 0; k < d; ++k) adagrad_update(P, gr[k], V + k, C + k);
+    }
+    ent_set_state(en, e);
+    flags[u] = f;
+    frank[u] = fr;
+  }
+  for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
+  if (lane_id() == 0 && dnew)
+    atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+}
+
+// flagged keys (key order) -> (rank, key) order: rank keys, segment payloads; the unused tail
+// sorts last
+__global__ void k_dist_initv_list(const uint32_t* flags_excl, const uint32_t* ftotal,
+                                  const uint32_t* frank, const uint32_t* nuniq, int64_t bound,
+                                  uint32_t* rk, uint32_t* rv) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= bound) return;
+  const int64_t n = *nuniq;
+  const uint32_t F = *ftotal;
+  if (u < n) {
+    const uint32_t e = flags_excl[u];
+    const uint32_t nx = (u + 1 < n) ? flags_excl[u + 1] : F;
+    if (nx != e) {
+      rk[e] = frank[u];
+      rv[e] = (uint32_t)u;
+    }
+  }
+  if (u >= F) rk[u] = 0xFFu;
+}
+
+// InitV (sgd_updater.cc:144-152) of the q-th draw: seed jumped 3*d*q steps, pool row n_vrows+q
+__global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uint32_t* ftotal,
+                             const uint32_t* segslot, Table T, float scale, DevState* ds) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (int64_t)*ftotal) return;
+  const uint32_t* rv = ds->sortmeta[31] ? rv1 : rv0;
+  const int d = T.d;
+  uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)q);
+  const int64_t vr = (int64_t)ds->n_vrows + q;
+  if (vr >= T.vcap) {
+    atomicOr(&ds->err, kErrPoolFull);
+    return;
+  }
+  float* V = row_V(T, vr);
+  float* C = row_C(T, vr);
+  for (int k = 0; k < d; ++k) {
+    V[k] = initv_value(rand_r_dev(&s), scale);
+    C[k] = 0.f;
+  }
+  T.ent[segslot[rv[q]]].vrow = (int32_t)vr;
+}
+
+__global__ void k_dist_initv_finalize(const uint32_t* ftotal, int d, int64_t vcap,
+                                      DevState* ds) {
+  const uint32_t F = *ftotal;
+  ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * F);
+  const unsigned long long nv = ds->n_vrows + F;
+  ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+}
+
+// SGDUpdater::Get (sgd_updater.cc:34-58) per received key, in received order
+__global__ void k_dist_pull(int64_t R, const uint32_t* seg_of, const uint32_t* segslot,
+                            Table T, Params P, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R) return;
+  const int d = T.d;
+  const Entry* e = &T.ent[segslot[seg_of[i]]];
+  const float w = e->w;
+  const int vr = e->vrow;
+  const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
+  float* o = out + i * rec_floats(d);
+  const float* V = live ? row_V(T, vr) : nullptr;
+  for (int k = 0; k < d; ++k) o[k] = live ? V[k] : 0.f;
+  o[d] = w;
+  o[d + 1] = live ? 1.f : 0.f;
+  o[d + 2] = 0.f;
+  o[d + 3] = 0.f;
+}
+
+// InitV of the flagged keys in (pushing rank, key) order, all on the device
+static int owner_initv(Context* c, int nranks) {
+  Workspace& ws = c->ws;
+  const int64_t R = c->dist_R;
+  uint32_t* flags = ws.oflags.as<uint32_t>();
+  uint32_t* nuniq = &c->ds->totals[1];
+  uint32_t* ftotal = &c->ds->totals[2];
+  DFX_TRY(scan_u32(c, flags, R, ftotal, nuniq));
+  uint32_t* rk0 = ws.vals0.as<uint32_t>();
+  uint32_t* rv0 = ws.vals1.as<uint32_t>();
+  uint32_t* rk1 = reinterpret_cast<uint32_t*>(ws.keys0.as<uint64_t>());
+  uint32_t* rv1 = reinterpret_cast<uint32_t*>(ws.keys1.as<uint64_t>());
+  const dim3 grid((R + kDNT - 1) / kDNT);
+  hipLaunchKernelGGL(k_dist_initv_list, grid, dim3(kDNT), 0, c->stream, flags, ftotal,
+                     ws.ofrank.as<uint32_t>(), nuniq, R, rk0, rv0);
+  int bits = 0;
+  while ((1 << bits) < nranks) ++bits;
+  // stable by rank; the tail (0xFF) sorts last and is never read
+  DFX_TRY(radix_sort_pairs<uint32_t>(c, rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
+                                     c->ds->sortmeta));
+  hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, c->stream, rv0, rv1, ftotal,
+                     ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds);
+  hipLaunchKernelGGL(k_dist_initv_finalize, dim3(1), dim3(1), 0, c->stream, ftotal, c->P.V_dim,
+                     c->T.vcap, c->ds);
+  return DFX_OK;
+}
+
+static RankOffs rank_offs(const Context* c) {
+  RankOffs ro{};
+  ro.n = (int)c->dist_offs.size() - 1;
+  for (int r = 0; r <= ro.n; ++r) ro.off[r] = c->dist_offs[r];
+  return ro;
+}
+
+}  // namespace dfx
+
+using namespace dfx;
+
+extern "C" {
+
+int dfx_dist_record_floats(dfx_ctx* ctx) { return ctx ? rec_floats(ctx->c.P.V_dim) : -1; }
+
+int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* b, uint64_t max_index, int nranks,
+                      uint64_t* keys_out, float* cnt_out, int64_t* split_counts,
+                      int64_t* n_uniq) {
+  DFX_CHECK_ARG(ctx && b && split_counts && n_uniq, "null argument");
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
+  DFX_CHECK_ARG(b->size >= 0 && b->nnz >= 0, "dist_localize: negative sizes");
+  DFX_CHECK_ARG(b->size == 0 || b->offset, "dist_localize: null offset");
+  DFX_CHECK_ARG(b->nnz == 0 || (b->index && keys_out), "dist_localize: null buffer");
+  Context* c = &ctx->c;
+  Workspace& ws = c->ws;
+  const int64_t B = b->size, nnz = b->nnz;
+  DFX_TRY(ws_reserve(c, B, nnz));
+  DFX_TRY(ws.oflags.ensure(kMaxRanks * 8));
+  LocOut o;
+  o.uniq = keys_out;
+  o.cnt = cnt_out;
+  o.col = ws.col.as<uint32_t>();
+  o.segstart = ws.segstart.as<uint32_t>();
+  o.value = b->value;
+  o.occ_row = ws.occ_row.as<uint32_t>();
+  o.occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
+  DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, o));
+  uint32_t u = 0;
+  DFX_HIP(hipMemcpyAsync(&u, &c->ds->u_count, 4, hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  unsigned long long* counts = reinterpret_cast<unsigned long long*>(ws.oflags.p);
+  DFX_HIP(hipMemsetAsync(counts, 0, kMaxRanks * 8, c->stream));
+  if (u > 0)
+    hipLaunchKernelGGL(k_owner_counts, dim3((u + 255) / 256), dim3(256), 0, c->stream, keys_out,
+                       (int64_t)u, (uint32_t)nranks, counts);
+  unsigned long long h[kMaxRanks];
+  DFX_HIP(hipMemcpyAsync(h, counts, kMaxRanks * 8, hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  for (int r = 0; r < nranks; ++r) split_counts[r] = (int64_t)h[r];
+  *n_uniq = u;
+  c->dist_U = u;
+  c->dist_rows = B;
+  return DFX_OK;
+}
+
+int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* b, const float* pulled, int job_type,
+                     float* grads_out, float* pred_out) {
+  DFX_CHECK_ARG(ctx && b, "null argument");
+  DFX_CHECK_ARG(job_type == DFX_JOB_TRAINING || job_type == DFX_JOB_VALIDATION ||
+                    job_type == DFX_JOB_PREDICTION,
+                "dist_fwd_bwd: bad job type");
+  Context* c = &ctx->c;
+  Workspace& ws = c->ws;
+  const int d = c->P.V_dim;
+  const int64_t B = b->size;
+  DFX_CHECK_ARG(B == c->dist_rows,"dist_fwd_bwd: batch differs from dist_localize's");
+  DFX_CHECK_ARG(B == 0 || b->label, "dist_fwd_bwd: null label");
+  const int64_t U = c->dist_U;
+  DFX_CHECK_ARG(U == 0 || pulled, "dist_fwd_bwd: null pulled records");
+  const bool train = job_type == DFX_JOB_TRAINING && U > 0;
+  DFX_CHECK_ARG(!train || grads_out, "dist_fwd_bwd: grads_out required for training");
+  const int64_t S = rec_floats(d);
+  DFX_TRY(ws.vpos.ensure((U + 1) * 4));
+  DFX_TRY(ws.wb.ensure((U + 1) * 4));
+  int32_t* wpos = ws.wb.as<int32_t>();
+  int32_t* vpos = ws.vpos.as<int32_t>();
+  float* pred = pred_out ? pred_out : ws.pred.as<float>();
+  if (U > 0)
+    hipLaunchKernelGGL(k_record_pos, dim3((U + 255) / 256), dim3(256), 0, c->stream, pulled, U,
+                       d, wpos, vpos);
+  FwdArgs a{};
+  a.B = B; a.offs = b->offset; a.col = ws.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
+  a.wpos = wpos; a.vpos = vpos; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
+  a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
+  a.loss_part = ws.dscratch.as<double>() + 8;
+  int nblk = 0;
+  DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
+  sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
+  DFX_TRY(auc_run(c, B, b->label, pred, &c->ds->auc_n));
+  hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
+  if (train) {
+    DFX_HIP(hipMemsetAsync(grads_out, 0, (size_t)U * S * 4, c->stream));
+    BwdArgs g{};
+    g.segstart = ws.segstart.as<uint32_t>(); g.ds = c->ds; g.nseg_host = U; g.segcol = nullptr;
+    g.occ_row = ws.occ_row.as<uint32_t>();
+    g.occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
+    g.zpad = c->zpad; g.p = ws.p.as<float>(); g.XVp = ws.XVp.as<float>(); g.d = d;
+    g.wpos = wpos; g.vpos = vpos; g.W = pulled; g.grad = grads_out;
+    DFX_TRY(launch_bwd_positions(g, U, c->stream));
+  }
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t* recv_offsets,
+                         int nranks, const float* recv_cnt) {
+  DFX_CHECK_ARG(ctx && recv_offsets, "null argument");
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
+  Context* c = &ctx->c;
+  Workspace& ws = c->ws;
+  DFX_CHECK_ARG(recv_offsets[0] == 0, "dist_owner_begin: recv_offsets[0] must be 0");
+  for (int r = 0; r < nranks; ++r)
+    DFX_CHECK_ARG(recv_offsets[r + 1] >= recv_offsets[r], "dist_owner_begin: bad offsets");
+  const int64_t R = recv_offsets[nranks];
+  DFX_CHECK_ARG(R < 0x7FFFFFFFll, "dist_owner_begin: too many keys");
+  DFX_CHECK_ARG(R == 0 || recv_keys, "dist_owner_begin: null keys");
+  c->dist_R = R;
+  c->dist_offs.assign(recv_offsets, recv_offsets + nranks + 1);
+  DFX_HIP(hipMemsetAsync(&c->ds->totals[1], 0, 8, c->stream));
+  if (R == 0) return DFX_OK;
+  DFX_TRY(ws.keys0.ensure(R * 8));
+  DFX_TRY(ws.keys1.ensure(R * 8));
+  DFX_TRY(ws.vals0.ensure(R * 4));
+  DFX_TRY(ws.vals1.ensure(R * 4));
+  DFX_TRY(ws.oflags.ensure((R + kMaxRanks) * 8));
+  DFX_TRY(ws.ofrank.ensure((R + 1) * 4));
+  DFX_TRY(ws.osegstart.ensure((R + 1) * 4));
+  DFX_TRY(ws.osegslot.ensure((R + 1) * 4));
+  DFX_TRY(ws.oseg_of.ensure((R + 1) * 4));
+  DFX_TRY(ws.osorted.ensure((R + 1) * 4));
+  uint64_t* k0 = ws.keys0.as<uint64_t>();
+  uint32_t* p0 = ws.vals0.as<uint32_t>();
+  uint32_t* flags = ws.oflags.as<uint32_t>();
+  uint32_t* nuniq = &c->ds->totals[1];
+  const dim3 grid((R + kDNT - 1) / kDNT);
+  hipLaunchKernelGGL(k_dist_init_masks, dim3(1), dim3(1), 0, c->stream, c->ds);
+  hipLaunchKernelGGL(k_dist_recv_prep, grid, dim3(kDNT), 0, c->stream, recv_keys, R, k0, p0,
+                     c->ds);
+  hipLaunchKernelGGL(k_dist_diff, dim3(1), dim3(1), 0, c->stream, c->ds);
+  DFX_TRY(radix_sort_pairs<uint64_t>(c, k0, p0, ws.keys1.as<uint64_t>(), ws.vals1.as<uint32_t>(),
+                                     R, 0, 64, &c->ds->diff_mask, c->ds->sortmeta));
+  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, c->stream, k0, ws.keys1.as<uint64_t>(),
+                     R, c->ds, flags);
+  DFX_TRY(scan_u32(c, flags, R, nuniq));
+  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, c->stream, k0, ws.keys1.as<uint64_t>(),
+                     p0, ws.vals1.as<uint32_t>(), R, c->ds, flags, nuniq, c->T,
+                     ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
+                     ws.oseg_of.as<uint32_t>(), ws.osorted.as<uint32_t>());
+  if (recv_cnt) {
+    hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, c->stream,
+                       ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
+                       ws.osorted.as<uint32_t>(), recv_cnt, rank_offs(c), c->T, c->P, nuniq,
+                       flags, ws.ofrank.as<uint32_t>());
+    if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, nranks));
+  }
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_dist_owner_pull(dfx_ctx* ctx, float* vals_out) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  const int64_t R = c->dist_R;
+  if (R == 0) return DFX_OK;
+  DFX_CHECK_ARG(vals_out, "dist_owner_pull: null buffer");
+  hipLaunchKernelGGL(k_dist_pull, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream, R,
+                     c->ws.oseg_of.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(), c->T, c->P,
+                     vals_out);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_dist_owner_push(dfx_ctx* ctx, const float* recv_grads) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  const int64_t R = c->dist_R;
+  if (R == 0) return DFX_OK;
+  DFX_CHECK_ARG(recv_grads, "dist_owner_push: null buffer");
+  const dim3 grid((R + kDNT - 1) / kDNT);
+  hipLaunchKernelGGL(k_dist_push, grid, dim3(kDNT), 0, c->stream, c->ws.osegstart.as<uint32_t>(),
+                     c->ws.osegslot.as<uint32_t>(), c->ws.osorted.as<uint32_t>(), recv_grads,
+                     rank_offs(c), c->T, c->P, &c->ds->totals[1], c->ws.oflags.as<uint32_t>(),
+                     c->ws.ofrank.as<uint32_t>(), c->ds);
+  if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, (int)c->dist_offs.size() - 1));
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+}  // extern "C"

@@ -248,7 +248,7 @@ static int launch_fwd_gc(const FwdArgs& a, int G, int CPL, bool vec, hipStream_t
     return DFX_OK;                                                                           \
   }
   DFX_SCALAR_SET(DFX_FWD)
-  if constexpr (PACKED) { DFX_VEC_SET(DFX_FWD) }
+  if constexpr (PACKED || MODE == kFused) { DFX_VEC_SET(DFX_FWD) }
 #undef DFX_FWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -269,6 +269,17 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
   return launch_fwd_gc<kFused, true>(a, G, CPL, vec, st);
+}
+
+// sharded store: forward over pulled records [V(d) | w | live | 0 | 0] (16-byte aligned rows
+// when d % 4 == 0), addressed through wpos / vpos
+int launch_fwd_records(const FwdArgs& a, hipStream_t st, int* nblk) {
+  int G, CPL;
+  bool vec;
+  lanes_for(a.d, true, &G, &CPL, &vec);
+  const int64_t rpb = kFmNT / G;
+  *nblk = (int)((a.B + rpb - 1) / rpb);
+  return launch_fwd_gc<kFused, false>(a, G, CPL, vec, st);
 }
 
 // ---- backward: sorted-key segmented reduction --------------------------------------------
@@ -456,11 +467,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 }
 
 template <bool FUSED>
-int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
+int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligned = FUSED) {
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;
   bool vec;
-  lanes_for(a.d, FUSED, &G, &CPL, &vec);
+  lanes_for(a.d, aligned, &G, &CPL, &vec);
   const int64_t spb = kFmNT / G;
   dim3 grid((unsigned)((nseg_bound + spb - 1) / spb));
 #define DFX_BWD(GG, CC, VV)                                                              \
@@ -470,7 +481,7 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
     return DFX_OK;                                                                       \
   }
   DFX_SCALAR_SET(DFX_BWD)
-  if constexpr (FUSED) { DFX_VEC_SET(DFX_BWD) }
+  DFX_VEC_SET(DFX_BWD)
 #undef DFX_BWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -478,6 +489,11 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
 
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
   return launch_bwd<true>(a, nseg_bound, st);
+}
+
+// sharded store: per-key gradient records in the pulled-record layout (aligned rows)
+int launch_bwd_positions(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
+  return launch_bwd<false>(a, nseg_bound, st, true);
 }
 
 // ---- standalone CalcGrad support: CSC order of a compacted block ------------------------

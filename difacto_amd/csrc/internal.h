@@ -79,6 +79,8 @@ struct Workspace {
   DevBuf p, pred, XVp, rowtmp;
   DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
   DevBuf dscratch;  // double partials
+  // sharded store, owner side (dist.hip): per received key / per owned unique key
+  DevBuf oflags, ofrank, osegstart, osegslot, oseg_of, osorted;
   int64_t rows = 0, nnz = 0;
 };
 
@@ -97,6 +99,10 @@ struct Context {
   // per-phase HIP-event timing of dfx_train_step (dfx_prof_*); events on c->stream
   std::vector<hipEvent_t> prof_ev;  // prof_max steps x kProfMarks
   int prof_max = 0, prof_n = 0;
+  // sharded store (dist.hip): keys received by this owner in the current step and each
+  // source rank's offset among them; rows and unique keys of this worker's batch
+  int64_t dist_R = 0, dist_rows = 0, dist_U = 0;
+  std::vector<int64_t> dist_offs;
 };
 
 // masked gathers read zpad + ((index & 255) << 4) + [0, 1024): 256 spread 64-byte lines

@@ -1,0 +1,137 @@
+"""The key-range-sharded store's device phases (dfx_dist_*, through the C-ABI) against the
+sharded oracle (oracle/dist_oracle.py: N restated SGDUpdater servers).  N shards live on the
+one GPU of the test box and exchange through LoopbackComm (device copies); the
+torch.distributed exchange itself is covered by tests/test_dist.py (gloo, world_size 2).
+Bars as in test_gpu_parity.py: predictions / state within 1e-5 relative, loss within 1e-4;
+InitV seeds, V-row counts and new_w exact."""
+import numpy as np
+import pytest
+import torch
+
+from difacto_amd import data as D
+from oracle import dist_oracle as DO
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def close(a, b, rtol=RTOL):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    floor = 1e-6 * max(1.0, float(np.max(np.abs(b))) if b.size else 1.0)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(a), np.abs(b)) + floor)
+
+
+CFGS = {
+    "fm_v4": (3, dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.5, l2=0.01, seed=7)),
+    "fm_v16": (2, dict(V_dim=16, V_threshold=0, lr=0.1, V_lr=0.01, l1=0.0, seed=3)),
+    "fm_v5_odd": (4, dict(V_dim=5, V_threshold=2, lr=0.05, l1=0.1, seed=11)),
+    "logit": (2, dict(V_dim=0, lr=0.2, l1=0.05)),
+}
+
+
+def _batches(nranks, steps, rows=300, nnz=8, key_space=3000, seed=0):
+    return [[D.synthetic(rows, nnz, key_space, binary=(r % 2 == 0), seed=seed + 131 * s + r,
+                         ragged=(s == 2)) for r in range(nranks)] for s in range(steps)]
+
+
+@pytest.mark.parametrize("name", list(CFGS))
+def test_sharded_loopback_matches_sharded_oracle(name):
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS[name]
+    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.ShardedOracle(N, **kw)
+    batches = _batches(N, 5)
+    for s, step in enumerate(batches):
+        push = s < 3
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        preds = [torch.zeros(step[r].size, dtype=torch.float32, device=ctxs[r].device)
+                 for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=push, preds=preds)
+        out = so.step(step, push_cnt=push)
+        for r in range(N):
+            p = preds[r].cpu().numpy()
+            assert close(p, out[r][2]), (name, s, r)
+            pr = H.progress(ctxs[r])
+            assert pr["nrows"] == step[r].size
+            assert pr["loss"] == pytest.approx(out[r][0], rel=1e-4)
+            want_auc = (O.auc_stable_ties(step[r].labels, out[r][2])
+                        if O.has_ties(out[r][2]) else out[r][1])
+            assert pr["auc"] == pytest.approx(want_auc, rel=1e-4, abs=1e-6)
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
+                                     for step in batches for b in step]))
+    n_v = 0
+    for g in range(N):
+        st = H.Store(ctxs[g]).stats()
+        assert st["seed"] == so.up[g].seed, (name, g)
+        assert st["n_keys"] == so.up[g].size(), (name, g)
+        assert st["new_w"] == so.up[g].new_w, (name, g)
+        own = keys[DO.owner_of(keys, N) == g]
+        for k in own[:: max(1, len(own) // 150)]:
+            e = so.up[g].entry(k)
+            got = H.Store(ctxs[g]).entry(k)
+            assert (got is None) == (e is None)
+            if e is None:
+                continue
+            assert close(got[0], e[0]), (name, g, k)
+            assert (got[1] is None) == (e[1] is None), (name, g, k)
+            if e[1] is not None:
+                n_v += 1
+                assert close(got[1], e[1]), (name, g, k)
+    if kw.get("V_dim", 0) > 0:
+        assert n_v > 0
+    for c in ctxs:
+        c.sync()
+        c.close()
+
+
+def test_sharded_validation_does_not_update():
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS["fm_v4"]
+    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    step = _batches(N, 1)[0]
+    dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+    DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=True)
+    before = [H.Store(c).stats() for c in ctxs]
+    DI.sharded_step(shards, dbs, comm, H.kValidation)
+    after = [H.Store(c).stats() for c in ctxs]
+    assert before == after
+    for c in ctxs:
+        c.sync()
+        c.close()
+
+
+def test_sharded_empty_shard_and_batch():
+    """a rank with an empty batch, and ranks that own none of the step's keys"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = 4, dict(V_dim=4, V_threshold=0, lr=0.1, l1=0.0)
+    ctxs = [H.Context(0, max_keys=1 << 12, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.ShardedOracle(N, **kw)
+    empty = D.RowBlock(np.zeros(1, np.uint64), np.zeros(0, np.uint64), None,
+                       np.zeros(0, np.float32))
+    # two keys only: most owners receive nothing
+    tiny = D.RowBlock(np.array([0, 2, 3], np.uint64), np.array([5, 9, 5], np.uint64), None,
+                      np.array([1, -1], np.float32))
+    steps = [[tiny, empty, tiny, empty], [empty, empty, empty, tiny]]
+    for s, step in enumerate(steps):
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=True)
+        so.step(step, push_cnt=True)
+    for g in range(N):
+        st = H.Store(ctxs[g]).stats()
+        assert st["seed"] == so.up[g].seed
+        assert st["n_keys"] == so.up[g].size()
+    for c in ctxs:
+        c.sync()
+        c.close()
