@@ -12,7 +12,7 @@
 //
 //   worker  dist_localize     Localizer::Compact of its batch; sorted keys split by owner
 //   --- alltoallv keys (+ occurrence counts in epoch 0) ---
-//   owner   dist_owner_begin  sort+dedupe the received keys (stable: rank order within a key),
+//   owner   dist_owner_begin  merge the ranks' sorted key runs (stable: rank order within a key),
 //                             find-or-insert their table slots; with counts, the ranks'
 //                             Update(kFeaCount) pushes in rank order, then their InitV draws
 //   owner   dist_owner_pull   SGDUpdater::Get per received key: record [V(d) | w | live | 0 0]
@@ -26,6 +26,8 @@
 //
 // Every per-key result therefore equals what N reference servers produce when worker r's push
 // reaches them r-th, with every pull of the step answered before any push.
+#include <algorithm>
+
 #include "fm_args.h"
 
 namespace dfx {
@@ -87,53 +89,64 @@ __global__ void k_dist_worker_finalize(DevState* ds, int64_t B) {
 }
 
 // ---- owner: received keys -> unique segments -----------------------------------------------
-__global__ void k_dist_init_masks(DevState* ds) {
-  ds->or_mask = 0;
-  ds->and_mask = ~0ull;
+// The receive buffer is N sorted runs (one per source rank, in rank order), so the owner's
+// key order is a stable merge of the runs: ceil(log2 N) rounds of pairwise merge-path merges
+// (run 2p before run 2p+1 on equal keys = rank order).  Payload = received index.
+constexpr int kMergeK = 8;  // outputs per thread
+constexpr int kMaxPairs = kMaxRanks / 2 + 1;
+
+struct PairList {
+  int n;
+  int64_t lo[kMaxPairs], mid[kMaxPairs], hi[kMaxPairs];  // pair p: A = [lo, mid), B = [mid, hi)
+};
+
+__global__ __launch_bounds__(kDNT) void k_merge_pairs(const uint64_t* __restrict__ kin,
+                                                      const uint32_t* __restrict__ vin,
+                                                      uint64_t* __restrict__ kout,
+                                                      uint32_t* __restrict__ vout, int64_t R,
+                                                      PairList pl) {
+  int64_t t = ((int64_t)blockIdx.x * kDNT + threadIdx.x) * kMergeK;
+  if (t >= R) return;
+  const int64_t tend = t + kMergeK < R ? t + kMergeK : R;
+  int p = 0;
+  {
+    int lo = 0, hi = pl.n;  // pl.lo[lo] <= t < pl.lo[hi]
+    while (hi - lo > 1) {
+      const int m = (lo + hi) >> 1;
+      if (pl.lo[m] <= t) lo = m; else hi = m;
+    }
+    p = lo;
+  }
+  while (t < tend) {
+    while (t >= pl.hi[p]) ++p;
+    const int64_t a0 = pl.lo[p], a1 = pl.mid[p], b1 = pl.hi[p];
+    const int64_t na = a1 - a0, nb = b1 - a1, k = t - a0;
+    // merge path: how many of the first k outputs come from A (A wins ties)
+    int64_t lo = k - nb > 0 ? k - nb : 0, hi = k < na ? k : na;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (kin[a0 + m] <= kin[a1 + k - 1 - m]) lo = m + 1; else hi = m;
+    }
+    int64_t i = a0 + lo, j = a1 + (k - lo);
+    const int64_t stop = tend < b1 ? tend : b1;
+    for (; t < stop; ++t) {
+      const bool takeA = i < a1 && (j >= b1 || kin[i] <= kin[j]);
+      const int64_t src = takeA ? i++ : j++;
+      kout[t] = kin[src];
+      vout[t] = vin ? vin[src] : (uint32_t)src;
+    }
+  }
 }
 
-__global__ __launch_bounds__(kDNT) void k_dist_recv_prep(const uint64_t* keys, int64_t R,
-                                                         uint64_t* k0, uint32_t* p0,
-                                                         DevState* ds) {
-  __shared__ unsigned long long ro[kDNT / kWave], ra[kDNT / kWave];
-  const int64_t i = (int64_t)blockIdx.x * kDNT + threadIdx.x;
-  unsigned long long vor = 0, vand = ~0ull;
-  if (i < R) {
-    const uint64_t k = keys[i];
-    k0[i] = k;
-    p0[i] = (uint32_t)i;
-    vor = k;
-    vand = k;
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    vor |= __shfl_xor(vor, off, kWave);
-    vand &= __shfl_xor(vand, off, kWave);
-  }
-  if (lane_id() == 0) { ro[threadIdx.x / kWave] = vor; ra[threadIdx.x / kWave] = vand; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    vor = ro[0];
-    vand = ra[0];
-    for (int w = 1; w < kDNT / kWave; ++w) { vor |= ro[w]; vand &= ra[w]; }
-    atomicOr(&ds->or_mask, vor);
-    atomicAnd(&ds->and_mask, vand);
-  }
-}
-
-__global__ void k_dist_diff(DevState* ds) { ds->diff_mask = ds->or_mask ^ ds->and_mask; }
-
-__global__ void k_dist_heads(const uint64_t* k0, const uint64_t* k1, int64_t R,
-                             const DevState* ds, uint32_t* flags) {
+__global__ void k_dist_heads(const uint64_t* K, int64_t R, uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R) return;
-  const uint64_t* K = ds->sortmeta[31] ? k1 : k0;
   flags[i] = (i == 0 || K[i] != K[i - 1]) ? 1u : 0u;
 }
 
 // segstart[seg], segslot[seg] (find-or-insert), seg_of[received index], sorted_idx[sorted
-// position] = received index.  *total = number of unique keys.
-__global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* k0, const uint64_t* k1,
-                                                    const uint32_t* p0, const uint32_t* p1,
+// position] = received index (P == NULL: identity).  *total = number of unique keys.
+__global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* K, const uint32_t* P,
                                                     int64_t R, DevState* ds,
                                                     const uint32_t* excl, const uint32_t* total,
                                                     Table T, uint32_t* segstart,
@@ -142,13 +155,11 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* k0, const ui
   const int64_t i = (int64_t)blockIdx.x * kDNT + threadIdx.x;
   int ins = 0;
   if (i < R) {
-    const bool s1 = ds->sortmeta[31] != 0;
-    const uint64_t* K = s1 ? k1 : k0;
-    const uint32_t* P = s1 ? p1 : p0;
     const bool head = (i == 0 || K[i] != K[i - 1]);
     const uint32_t seg = head ? excl[i] : excl[i] - 1u;  // excl[i] = heads before i
-    sorted_idx[i] = P[i];
-    seg_of[P[i]] = seg;
+    const uint32_t src = P ? P[i] : (uint32_t)i;
+    sorted_idx[i] = src;
+    seg_of[src] = seg;
     if (head) {
       segstart[seg] = (uint32_t)i;
       bool inserted;
@@ -303,6 +314,96 @@ __global__ void k_dist_pull(int64_t R, const uint32_t* seg_of, const uint32_t* s
   o[d + 2] = 0.f;
   o[d + 3] = 0.f;
 }
+
+// d % 4 == 0: a group of G lanes per key, float4 chunks of V / Vaux / records
+template <int G>
+__global__ __launch_bounds__(kDNT) void k_dist_pull_vec(int64_t R, const uint32_t* seg_of,
+                                                        const uint32_t* segslot, Table T,
+                                                        Params P, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  if (i >= R) return;
+  const int d = T.d, nc = d >> 2;
+  const Entry* e = &T.ent[segslot[seg_of[i]]];
+  const int2 wr = *reinterpret_cast<const int2*>(e);  // {w, vrow}
+  const float w = __int_as_float(wr.x);
+  const int vr = wr.y;
+  const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
+  float4* o = reinterpret_cast<float4*>(out + i * (int64_t)rec_floats(d));
+  const float4* V = reinterpret_cast<const float4*>(live ? row_V(T, vr) : T.V);
+  for (int c = l; c < nc; c += G) o[c] = live ? V[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (l == 0) o[nc] = make_float4(w, live ? 1.f : 0.f, 0.f, 0.f);
+}
+
+template <int G>
+__global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart,
+                                                        const uint32_t* segslot,
+                                                        const uint32_t* sorted_idx,
+                                                        const float* g, RankOffs ro, Table T,
+                                                        Params P, const uint32_t* nuniq,
+                                                        uint32_t* flags, uint32_t* frank,
+                                                        DevState* ds) {
+  const int64_t u = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  int dnew = 0;
+  if (u < (int64_t)*nuniq) {
+    const int d = T.d, nc = d >> 2;
+    const int64_t S = rec_floats(d);
+    Entry* en = &T.ent[segslot[u]];
+    float4 e = ent_state(en);
+    const int vr = en->vrow;
+    const bool pulled_v = vr >= 0 && !(P.l1_shrk && e.x == 0.f);
+    bool has_v = vr >= 0;
+    const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
+    // UpdateW per pushing rank; every lane of the group runs the same sequence
+    uint32_t f = 0, fr = 0;
+    for (uint32_t i = s0; i < s1; ++i) {
+      const uint32_t src = sorted_idx[i];
+      bool tr;
+      const int dw = ftrl_update(P, g[(int64_t)src * S + d], &e, &tr);
+      if (l == 0) dnew += dw;
+      if (tr && d > 0 && !has_v && e.w > (float)P.V_threshold) {  // :118-121
+        has_v = true;
+        f = 1;
+        fr = (uint32_t)rank_of(ro, src);
+      }
+    }
+    if (l == 0) {
+      ent_set_state(en, e);
+      flags[u] = f;
+      frank[u] = fr;
+    }
+    // UpdateV per pushing rank (each coordinate independent)
+    if (pulled_v) {
+      float4* V4 = reinterpret_cast<float4*>(row_V(T, vr));
+      float4* C4 = reinterpret_cast<float4*>(row_C(T, vr));
+      for (int c = l; c < nc; c += G) {
+        float4 v = V4[c], cg = C4[c];
+        for (uint32_t i = s0; i < s1; ++i) {
+          const float4 gv = reinterpret_cast<const float4*>(g + (int64_t)sorted_idx[i] * S)[c];
+          adagrad_update(P, gv.x, &v.x, &cg.x);
+          adagrad_update(P, gv.y, &v.y, &cg.y);
+          adagrad_update(P, gv.z, &v.z, &cg.z);
+          adagrad_update(P, gv.w, &v.w, &cg.w);
+        }
+        V4[c] = v;
+        C4[c] = cg;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
+  if (lane_id() == 0 && dnew)
+    atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+}
+
+static int vec_group(int d) {
+  if (d <= 0 || d % 4 != 0) return 0;
+  int g = 1;
+  while (g < d / 4 && g < 64) g <<= 1;
+  return g;
+}
+
+#define DFX_DIST_GROUPS(X) X(1) X(2) X(4) X(8) X(16) X(32) X(64)
 
 // InitV of the flagged keys in (pushing rank, key) order, all on the device
 static int owner_initv(Context* c, int nranks) {
@@ -461,23 +562,42 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t*
   DFX_TRY(ws.osegslot.ensure((R + 1) * 4));
   DFX_TRY(ws.oseg_of.ensure((R + 1) * 4));
   DFX_TRY(ws.osorted.ensure((R + 1) * 4));
-  uint64_t* k0 = ws.keys0.as<uint64_t>();
-  uint32_t* p0 = ws.vals0.as<uint32_t>();
   uint32_t* flags = ws.oflags.as<uint32_t>();
   uint32_t* nuniq = &c->ds->totals[1];
   const dim3 grid((R + kDNT - 1) / kDNT);
-  hipLaunchKernelGGL(k_dist_init_masks, dim3(1), dim3(1), 0, c->stream, c->ds);
-  hipLaunchKernelGGL(k_dist_recv_prep, grid, dim3(kDNT), 0, c->stream, recv_keys, R, k0, p0,
-                     c->ds);
-  hipLaunchKernelGGL(k_dist_diff, dim3(1), dim3(1), 0, c->stream, c->ds);
-  DFX_TRY(radix_sort_pairs<uint64_t>(c, k0, p0, ws.keys1.as<uint64_t>(), ws.vals1.as<uint32_t>(),
-                                     R, 0, 64, &c->ds->diff_mask, c->ds->sortmeta));
-  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, c->stream, k0, ws.keys1.as<uint64_t>(),
-                     R, c->ds, flags);
+  // stable merge of the N sorted runs (none for one run)
+  const uint64_t* K = recv_keys;
+  const uint32_t* Pm = nullptr;
+  {
+    std::vector<int64_t> runs(recv_offsets, recv_offsets + nranks + 1);
+    uint64_t* kb[2] = {ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>()};
+    uint32_t* vb[2] = {ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>()};
+    int sel = 0;
+    const dim3 mgrid((R + (int64_t)kDNT * kMergeK - 1) / ((int64_t)kDNT * kMergeK));
+    while (runs.size() > 2) {
+      const int m = (int)runs.size() - 1;
+      PairList pl{};
+      std::vector<int64_t> next;
+      for (int p = 0; 2 * p < m; ++p) {
+        pl.lo[p] = runs[2 * p];
+        pl.mid[p] = runs[std::min(2 * p + 1, m)];
+        pl.hi[p] = runs[std::min(2 * p + 2, m)];
+        next.push_back(runs[2 * p]);
+        pl.n = p + 1;
+      }
+      next.push_back(runs[m]);
+      hipLaunchKernelGGL(k_merge_pairs, mgrid, dim3(kDNT), 0, c->stream, K, Pm, kb[sel],
+                         vb[sel], R, pl);
+      K = kb[sel];
+      Pm = vb[sel];
+      sel ^= 1;
+      runs.swap(next);
+    }
+  }
+  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, c->stream, K, R, flags);
   DFX_TRY(scan_u32(c, flags, R, nuniq));
-  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, c->stream, k0, ws.keys1.as<uint64_t>(),
-                     p0, ws.vals1.as<uint32_t>(), R, c->ds, flags, nuniq, c->T,
-                     ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
+  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, c->stream, K, Pm, R, c->ds, flags, nuniq,
+                     c->T, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
                      ws.oseg_of.as<uint32_t>(), ws.osorted.as<uint32_t>());
   if (recv_cnt) {
     hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, c->stream,
@@ -496,9 +616,20 @@ int dfx_dist_owner_pull(dfx_ctx* ctx, float* vals_out) {
   const int64_t R = c->dist_R;
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(vals_out, "dist_owner_pull: null buffer");
-  hipLaunchKernelGGL(k_dist_pull, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream, R,
-                     c->ws.oseg_of.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(), c->T, c->P,
-                     vals_out);
+  const int G = vec_group(c->P.V_dim);
+#define DFX_PULL(GG)                                                                         \
+  if (G == GG) {                                                                             \
+    const int64_t per = kDNT / GG;                                                           \
+    hipLaunchKernelGGL(k_dist_pull_vec<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0,        \
+                       c->stream, R, c->ws.oseg_of.as<uint32_t>(),                           \
+                       c->ws.osegslot.as<uint32_t>(), c->T, c->P, vals_out);                \
+  }
+  DFX_DIST_GROUPS(DFX_PULL)
+#undef DFX_PULL
+  if (G == 0)
+    hipLaunchKernelGGL(k_dist_pull, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream, R,
+                       c->ws.oseg_of.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(), c->T, c->P,
+                       vals_out);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -509,11 +640,25 @@ int dfx_dist_owner_push(dfx_ctx* ctx, const float* recv_grads) {
   const int64_t R = c->dist_R;
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(recv_grads, "dist_owner_push: null buffer");
-  const dim3 grid((R + kDNT - 1) / kDNT);
-  hipLaunchKernelGGL(k_dist_push, grid, dim3(kDNT), 0, c->stream, c->ws.osegstart.as<uint32_t>(),
-                     c->ws.osegslot.as<uint32_t>(), c->ws.osorted.as<uint32_t>(), recv_grads,
-                     rank_offs(c), c->T, c->P, &c->ds->totals[1], c->ws.oflags.as<uint32_t>(),
-                     c->ws.ofrank.as<uint32_t>(), c->ds);
+  const int G = vec_group(c->P.V_dim);
+  const RankOffs ro = rank_offs(c);
+#define DFX_PUSH(GG)                                                                         \
+  if (G == GG) {                                                                             \
+    const int64_t per = kDNT / GG;                                                           \
+    hipLaunchKernelGGL(k_dist_push_vec<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0,        \
+                       c->stream, c->ws.osegstart.as<uint32_t>(),                            \
+                       c->ws.osegslot.as<uint32_t>(), c->ws.osorted.as<uint32_t>(),          \
+                       recv_grads, ro, c->T, c->P, &c->ds->totals[1],                       \
+                       c->ws.oflags.as<uint32_t>(), c->ws.ofrank.as<uint32_t>(), c->ds);     \
+  }
+  DFX_DIST_GROUPS(DFX_PUSH)
+#undef DFX_PUSH
+  if (G == 0)
+    hipLaunchKernelGGL(k_dist_push, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream,
+                       c->ws.osegstart.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(),
+                       c->ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,
+                       &c->ds->totals[1], c->ws.oflags.as<uint32_t>(),
+                       c->ws.ofrank.as<uint32_t>(), c->ds);
   if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, (int)c->dist_offs.size() - 1));
   DFX_HIP(hipGetLastError());
   return DFX_OK;

@@ -89,15 +89,20 @@ class Shard:
 
 
 class TorchComm:
-    """Exchange over torch.distributed; this process holds one shard (its rank)."""
+    """Exchange over torch.distributed; this process holds one shard (its rank).
 
-    def __init__(self, group=None, device=None):
+    device: where the count exchange lives (the GPU for nccl/RCCL, cpu for gloo).
+    stage_cpu: route device tensors through host memory (gloo between processes that share
+    one GPU — the single-GPU test box; RCCL needs one GPU per rank)."""
+
+    def __init__(self, group=None, device=None, stage_cpu=False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        self.device = device  # where the count exchange lives (cuda for nccl, cpu for gloo)
+        self.device = device
+        self.stage_cpu = stage_cpu
 
     def exchange_counts(self, send_splits):
         (s,) = send_splits
@@ -108,12 +113,16 @@ class TorchComm:
 
     def alltoallv(self, tensors, send_splits, recv_splits, row=1):
         (x,), (ss,), (rs,) = tensors, send_splits, recv_splits
+        home = x.device
+        x = x[:sum(ss) * row]
+        if self.stage_cpu:
+            x = x.cpu()
         out = torch.empty(sum(rs) * row, dtype=x.dtype, device=x.device)
-        self.dist.all_to_all_single(out, x[:sum(ss) * row].contiguous(),
+        self.dist.all_to_all_single(out, x.contiguous(),
                                     output_split_sizes=[int(r) * row for r in rs],
                                     input_split_sizes=[int(s) * row for s in ss],
                                     group=self.group)
-        return [out]
+        return [out.to(home) if self.stage_cpu else out]
 
     def allreduce_sum(self, values):
         (v,) = values
@@ -149,28 +158,45 @@ class LoopbackComm:
         return [list(tot) for _ in values]
 
 
+PHASES = ("localize", "xchg_keys", "owner_begin", "owner_pull", "xchg_pull", "fwd_bwd",
+          "xchg_grads", "owner_push")
+
+
 def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index=MAX_INDEX,
-                 preds=None):
+                 preds=None, mark=None):
     """One synchronous step of the sharded store.  shards / dblks (/ preds): this process's
     shards and their batches (one each under torch.distributed, N under LoopbackComm).
     push_cnt: epoch-0 Update(kFeaCount) (sgd_learner.cc:272, 304-307); ignored when V_dim == 0
-    like the reference's do_embedding_."""
+    like the reference's do_embedding_.  mark(i): called after phase PHASES[i] is issued
+    (and with -1 first), e.g. to record stream events."""
+    mark = mark or (lambda i: None)
+    mark(-1)
     n = len(shards)
     want_cnt = bool(push_cnt) and shards[0].ctx.V_dim > 0
     loc = [shards[i].localize(dblks[i], want_cnt, max_index) for i in range(n)]
+    mark(0)
     send = [l[2] for l in loc]
     recv = comm.exchange_counts(send)
     rkeys = comm.alltoallv([l[0] for l in loc], send, recv)
     rcnt = comm.alltoallv([l[1] for l in loc], send, recv) if want_cnt else [None] * n
+    mark(1)
     for i in range(n):
         shards[i].owner_begin(rkeys[i], recv[i], rcnt[i])
+    mark(2)
     S = shards[0].S
     vals = [s.owner_pull() for s in shards]
+    mark(3)
     pulled = comm.alltoallv(vals, recv, send, S)
+    mark(4)
     grads = [shards[i].fwd_bwd(dblks[i], pulled[i], job_type, preds[i] if preds else None)
              for i in range(n)]
+    mark(5)
     if job_type == kTraining:
         rgrads = comm.alltoallv(grads, send, recv, S)
+        mark(6)
         for i in range(n):
             shards[i].owner_push(rgrads[i])
+    else:
+        mark(6)
+    mark(7)
     return [sum(s) for s in recv]  # keys served per shard (for accounting)

@@ -29,6 +29,7 @@ CFGS = {
     "fm_v16": (2, dict(V_dim=16, V_threshold=0, lr=0.1, V_lr=0.01, l1=0.0, seed=3)),
     "fm_v5_odd": (4, dict(V_dim=5, V_threshold=2, lr=0.05, l1=0.1, seed=11)),
     "logit": (2, dict(V_dim=0, lr=0.2, l1=0.05)),
+    "fm_v8_n6": (6, dict(V_dim=8, V_threshold=1, lr=0.1, V_lr=0.02, l1=0.2, seed=5)),
 }
 
 
@@ -135,3 +136,65 @@ def test_sharded_empty_shard_and_batch():
     for c in ctxs:
         c.sync()
         c.close()
+
+
+def _mp_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from difacto_amd import dist as DI
+        from difacto_amd import hotpath as H
+        _, kw = CFGS["fm_v4"]
+        ctx = H.Context(0, max_keys=1 << 15, **kw)
+        shard = DI.Shard(ctx, world)
+        comm = DI.TorchComm(device="cpu", stage_cpu=True)
+        preds = []
+        for s, step in enumerate(_batches(world, 4)):
+            db = H.DeviceRowBlock(ctx, step[rank])
+            pred = torch.zeros(step[rank].size, dtype=torch.float32, device=ctx.device)
+            DI.sharded_step([shard], [db], comm, H.kTraining, push_cnt=s < 2, preds=[pred])
+            preds.append(pred.cpu().numpy())
+        ctx.sync()
+        q.put((rank, preds, H.Store(ctx).stats()))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_two_processes_one_gpu():
+    """world_size 2 through torch.distributed with each process's shard on the GPU (the
+    exchange staged through host memory over gloo, since RCCL needs a GPU per rank)"""
+    import socket
+    import torch.multiprocessing as mp
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, preds, st = q.get(timeout=100)
+            res[r] = (preds, st)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs)
+    _, kw = CFGS["fm_v4"]
+    so = DO.ShardedOracle(world, **kw)
+    outs = [so.step(step, push_cnt=s < 2) for s, step in enumerate(_batches(world, 4))]
+    for r in range(world):
+        preds, st = res[r]
+        for s in range(4):
+            assert close(preds[s], outs[s][r][2]), (r, s)
+        assert st["seed"] == so.up[r].seed
+        assert st["n_keys"] == so.up[r].size()
+        assert st["new_w"] == so.up[r].new_w
