@@ -11,7 +11,18 @@ OBJS = $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS))
 HDRS = $(wildcard $(CSRC)/*.h) include/difacto_amd.h
 LIB = difacto_amd/libdifacto_amd.so
 
-all: $(LIB) oracle
+HOSTBIN = build/host_tests
+HOSTSRC = difacto_amd/host/gpu_adapters.cc tests/host/host_tests.cc
+HOSTHDR = difacto_amd/host/iface.h difacto_amd/host/gpu_adapters.h include/difacto_amd.h
+
+all: $(LIB) oracle $(HOSTBIN)
+
+# C++ host adapters (the reference's Loss/Updater/Store over the C-ABI) + their test driver;
+# plain g++ against the C-ABI, no HIP headers
+$(HOSTBIN): $(HOSTSRC) $(HOSTHDR) $(LIB)
+	@mkdir -p build
+	g++ -std=c++14 -O2 -Wall -o $@ $(HOSTSRC) -Ldifacto_amd -ldifacto_amd \
+	  -Wl,-rpath,'$$ORIGIN/../difacto_amd'
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

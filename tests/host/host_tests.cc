@@ -1,0 +1,196 @@
+// host_tests.cc — the reference's own hot-path gtests, restated against the C++ adapters
+// (difacto_amd/host/gpu_adapters.h) so they run through the same plugin interfaces the
+// reference's SGDLearner uses.  Needs a GPU; run by tests/test_host_cpp.py (-m gpu).
+//
+//   Localizer.Base / BaseHash   tests/cpp/localizer_test.cc:12-63
+//   FMLoss.NoV / HasV           tests/cpp/fm_loss_test.cc:12-83
+//   SGDLearner.Basic            tests/cpp/sgd_learner_test.cc:9-49 (interface and fused drivers)
+//   + the two drivers agree on an FM V_dim=8 run, and Save/Load round-trips through a Stream
+//
+// Usage: host_tests <path to tests/golden/rcv1_100.libsvm>.  Exit status 0 == all passed.
+#include <cstdio>
+#include <string>
+
+#include "../../difacto_amd/host/gpu_adapters.h"
+
+using namespace difacto;
+
+static int g_fail = 0;
+#define EXPECT(cond, ...)                                                     \
+  do {                                                                        \
+    if (!(cond)) {                                                            \
+      std::printf("  FAIL %s:%d: %s: ", __FILE__, __LINE__, #cond);           \
+      std::printf(__VA_ARGS__);                                               \
+      std::printf("\n");                                                      \
+      ++g_fail;                                                               \
+    }                                                                         \
+  } while (0)
+
+static feaid_t ReverseBytes(feaid_t x) {  // include/difacto/base.h:39-51 (test-side)
+  x = x << 32 | x >> 32;
+  x = (x & 0x0000FFFF0000FFFFULL) << 16 | (x & 0xFFFF0000FFFF0000ULL) >> 16;
+  x = (x & 0x00FF00FF00FF00FFULL) << 8 | (x & 0xFF00FF00FF00FF00ULL) >> 8;
+  x = (x & 0x0F0F0F0F0F0F0F0FULL) << 4 | (x & 0xF0F0F0F0F0F0F0F0ULL) >> 4;
+  return x;
+}
+
+static void TestLocalizer(const RowBlockContainer<feaid_t>& data) {
+  std::printf("Localizer.Base / BaseHash\n");
+  auto ctx = std::make_shared<GpuContext>(0, KWArgs{{"max_keys", "16"}});
+  for (feaid_t max_index : {~(feaid_t)0, (feaid_t)1000}) {
+    GpuLocalizer lc(ctx, max_index);
+    RowBlockContainer<unsigned> compacted;
+    std::vector<feaid_t> uidx;
+    std::vector<real_t> cnt;
+    lc.Compact(data.GetBlock(), &compacted, &uidx, &cnt);
+    uint64_t su = 0;
+    double sc = 0;
+    for (size_t i = 0; i < uidx.size(); ++i) {
+      su += ReverseBytes(uidx[i]);
+      sc += cnt[i];
+      if (i) EXPECT(uidx[i - 1] < uidx[i], "uniq not ascending at %zu", i);
+    }
+    const uint64_t want = max_index == ~(feaid_t)0 ? 65111856ull : 478817ull;
+    EXPECT(su == want, "sum uidx %llu want %llu", (unsigned long long)su,
+           (unsigned long long)want);
+    EXPECT(sc == 9648, "sum cnt %f", sc);
+    EXPECT(compacted.index.size() == data.index.size(), "nnz kept");
+    EXPECT(compacted.max_index + 1 == uidx.size(), "max_index");
+    // the remap is a bijection onto the ranks: keys of equal ids share a column
+    for (size_t j = 0; j < data.index.size(); ++j) {
+      const feaid_t id = max_index == ~(feaid_t)0 ? data.index[j] : data.index[j] % max_index;
+      if (ReverseBytes(uidx[compacted.index[j]]) != id) {
+        EXPECT(false, "remap mismatch at nnz %zu", j);
+        break;
+      }
+    }
+  }
+}
+
+// FMLoss known answers: w[i] = id/5e4, V[i][j] = id*j/5e5 (fm_loss_test.cc:20-33,50-70)
+static void TestFMLoss(const RowBlockContainer<feaid_t>& data, int d, double objv_want,
+                       double objv_tol, double g2_want, double g2_tol) {
+  std::printf("FMLoss.%s\n", d ? "HasV" : "NoV");
+  auto ctx = std::make_shared<GpuContext>(0, KWArgs{{"max_keys", "16"}});
+  GpuLocalizer lc(ctx);
+  RowBlockContainer<unsigned> compacted;
+  std::vector<feaid_t> uidx;
+  lc.Compact(data.GetBlock(), &compacted, &uidx);
+  const size_t U = uidx.size();
+  SArray<real_t> w(U * (d + 1));
+  SArray<int> w_pos, V_pos;
+  for (size_t i = 0; i < U; ++i) {
+    const double id = (double)ReverseBytes(uidx[i]);
+    w[i * (d + 1)] = (real_t)(id / 5e4);
+    for (int j = 1; j <= d; ++j) w[i * (d + 1) + j] = (real_t)(id * j / 5e5);
+  }
+  if (d) {
+    SArray<int> lens(U, d + 1);
+    GetPos(lens, &w_pos, &V_pos);
+  }
+  GpuFMLoss loss(d == 0);
+  loss.Init({{"V_dim", std::to_string(d)}});
+  auto blk = compacted.GetBlock();
+  SArray<real_t> pred(blk.size);
+  std::vector<SArray<char>> param = {SArray<char>(w), SArray<char>(w_pos), SArray<char>(V_pos)};
+  loss.Predict(blk, param, &pred);
+  const double objv = loss.Evaluate(blk.label, pred);
+  EXPECT(std::fabs(objv - objv_want) < objv_tol, "objv %.6f want %.6f", objv, objv_want);
+  SArray<real_t> grad(w.size());
+  param.push_back(SArray<char>(pred));
+  loss.CalcGrad(blk, param, &grad);
+  double g2 = 0;
+  for (real_t g : grad) g2 += (double)g * g;
+  EXPECT(std::fabs(g2 - g2_want) < g2_tol, "|g|^2 %.6f want %.6f", g2, g2_want);
+}
+
+// SGDLearner.Basic: V_dim 0, l1 = l2 = lr = 1, one 100-row batch per epoch, 20 epochs
+static void TestSGDLearnerBasic(const RowBlockContainer<feaid_t>& data, bool fused) {
+  std::printf("SGDLearner.Basic (%s)\n", fused ? "fused dfx_train_step" : "interfaces");
+  static const double objv[] = {69.314718, 69.314718, 67.151912, 61.414778, 56.244989,
+                                53.218700, 51.248737, 49.846688, 48.650164, 47.698351,
+                                46.924038, 46.388223, 45.970721, 45.499307, 45.102245,
+                                44.798413, 44.565211, 44.386417, 44.240657, 44.109764};
+  GpuSGDLearner learner({{"V_dim", "0"}, {"l2", "1"}, {"l1", "1"}, {"lr", "1"},
+                         {"fused", fused ? "1" : "0"}, {"max_keys", "16384"}});
+  for (int ep = 0; ep < 20; ++ep) {
+    Progress prog;
+    learner.ProcessBatch(data.GetBlock(), GpuSGDLearner::kTraining, ep == 0, &prog);
+    EXPECT(std::fabs(prog.loss - objv[ep]) < 5e-5, "epoch %d objv %.6f want %.6f", ep, prog.loss,
+           objv[ep]);
+    EXPECT(prog.nrows == 100, "nrows");
+  }
+}
+
+// the interface driver and the fused step are two routes through the same kernels
+static void TestDriversAgree(const RowBlockContainer<feaid_t>& data) {
+  std::printf("FM V_dim=8: interface driver == fused step; Save/Load round trip\n");
+  KWArgs kw = {{"V_dim", "8"}, {"V_threshold", "1"}, {"l1", "0.05"}, {"lr", "0.1"},
+               {"V_lr", "0.01"}, {"max_keys", "16384"}};
+  KWArgs kf = kw, ki = kw;
+  kf.push_back({"fused", "1"});
+  ki.push_back({"fused", "0"});
+  GpuSGDLearner a(ki), b(kf);
+  RowSlice h0 = Slice(data, 0, 50), h1 = Slice(data, 50, 100);
+  for (int ep = 0; ep < 5; ++ep) {
+    for (RowSlice* h : {&h0, &h1}) {
+      Progress pa, pb;
+      a.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0, &pa);
+      b.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0, &pb);
+      EXPECT(std::fabs(pa.loss - pb.loss) <= 1e-4 * std::fabs(pb.loss), "epoch %d loss %.7f vs %.7f",
+             ep, pa.loss, pb.loss);
+      EXPECT(std::fabs(pa.auc - pb.auc) <= 1e-4 * 50, "epoch %d auc %.7f vs %.7f", ep, pa.auc,
+             pb.auc);
+    }
+  }
+  // Save (with aux) -> Load into a fresh updater -> identical pulls
+  const char* path = "/tmp/difacto_amd_host_test_model";
+  {
+    FileStream fo(path, "w");
+    b.updater()->Save(true, &fo);
+  }
+  GpuSGDUpdater fresh;
+  fresh.Init(kw);
+  {
+    FileStream fi(path, "r");
+    fresh.Load(&fi);
+  }
+  auto ctx = std::make_shared<GpuContext>(0, KWArgs{{"max_keys", "16"}});
+  GpuLocalizer lc(ctx);
+  RowBlockContainer<unsigned> compacted;
+  auto uidx = std::make_shared<std::vector<feaid_t>>();
+  lc.Compact(data.GetBlock(), &compacted, uidx.get());
+  SArray<feaid_t> keys(uidx);
+  SArray<real_t> v0, v1;
+  SArray<int> l0, l1;
+  b.updater()->Get(keys, Store::kWeight, &v0, &l0);
+  fresh.Get(keys, Store::kWeight, &v1, &l1);
+  EXPECT(v0.size() == v1.size() && l0.size() == l1.size(), "pull sizes %zu %zu", v0.size(),
+         v1.size());
+  bool same = v0.size() == v1.size();
+  for (size_t i = 0; same && i < v0.size(); ++i) same = v0[i] == v1[i];
+  for (size_t i = 0; same && i < l0.size(); ++i) same = l0[i] == l1[i];
+  EXPECT(same, "loaded model differs");
+  std::remove(path);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s rcv1_100.libsvm\n", argv[0]);
+    return 2;
+  }
+  RowBlockContainer<feaid_t> data;
+  if (!ReadLibSVM(argv[1], &data)) {
+    std::fprintf(stderr, "cannot read %s\n", argv[1]);
+    return 2;
+  }
+  std::printf("rcv1-100: %zu rows, %zu nnz\n", data.Size(), data.index.size());
+  TestLocalizer(data);
+  TestFMLoss(data, 0, 147.4672, 1e-3, 90.5817, 1e-3);
+  TestFMLoss(data, 5, 330.628, 1e-3, 1237.8, 0.1);
+  TestSGDLearnerBasic(data, false);
+  TestSGDLearnerBasic(data, true);
+  TestDriversAgree(data);
+  std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+  return g_fail ? 1 : 0;
+}
