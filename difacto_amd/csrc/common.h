@@ -180,6 +180,7 @@ enum : int {
   kErrPoolFull = 2,
   kErrLens = 4,
   kErrNoV = 8,
+  kErrSort = 16,
 };
 
 struct Params {

@@ -155,7 +155,7 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   Workspace& w = c->ws;
   DevBuf* bufs[] = {&w.keys0, &w.keys1, &w.vals0, &w.vals1, &w.rowid, &w.hist, &w.tiles,
                     &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
-                    &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch};
+                    &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv};
   for (DevBuf* b : bufs) b->release();
   w.occ_row.release();
   w.occ_x.release();
@@ -204,6 +204,7 @@ int dfx_sync(dfx_ctx* ctx) {
     if (err & kErrPoolFull) m += " V pool full (raise max_vrows);";
     if (err & kErrLens) m += " CHECK_EQ(lens[i], V_dim+1) failed (sgd_updater.cc:83);";
     if (err & kErrNoV) m += " CHECK(e.V != nullptr) failed (sgd_updater.cc:84);";
+    if (err & kErrSort) m += " radix sort look-back never completed;";
     set_error(m);
     return (err & (kErrTableFull | kErrPoolFull)) ? DFX_ERR_CAPACITY : DFX_ERR_CHECK;
   }

@@ -96,10 +96,16 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
     for (uint64_t j0 = o0; j0 < o1; j0 += UNR) {
       uint32_t c[UNR];
       float x[UNR];
+      int2 wr[UNR];
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         const uint64_t jj = (j0 + t < o1) ? j0 + t : o1 - 1;
-        c[t] = a.col[jj];
+        if (PACKED && a.wv) {
+          wr[t] = a.wv[jj];
+          c[t] = (uint32_t)jj;
+        } else {
+          c[t] = a.col[jj];
+        }
         x[t] = valued ? a.val[jj] : 1.f;
       }
       float w[UNR];
@@ -107,11 +113,12 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         if (PACKED) {
-          // the key's table entry: {w, vrow} in one 8-byte load; V is visible only if
-          // present and not (l1_shrk && w == 0)  (SGDUpdater::Get, sgd_updater.cc:40-43)
-          const int2 wr = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
-          w[t] = __int_as_float(wr.x);
-          const int vr = wr.y;
+          // the key's table entry: {w, vrow} in one 8-byte load (or handed over by the
+          // Localizer's probe); V is visible only if present and not (l1_shrk && w == 0)
+          // (SGDUpdater::Get, sgd_updater.cc:40-43)
+          if (!a.wv) wr[t] = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
+          w[t] = __int_as_float(wr[t].x);
+          const int vr = wr[t].y;
           vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
         } else {
           if (a.wpos) {

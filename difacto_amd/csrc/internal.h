@@ -61,6 +61,7 @@ struct DevState {
   unsigned int sortmeta[32];   // per-pass {active, src} + final selector (Localizer sort)
   unsigned int sortmeta2[32];  // the same for the AUC sort
   unsigned int totals[8];      // scan totals of the current step
+  unsigned int sort_epoch;     // radix sorts launched (tags their look-back words)
   double auc_n;                // AUC * n of the current step
   double sum_u;                // sum of U over dfx_train_step calls (roofline bytes)
   double n_steps;
@@ -75,10 +76,19 @@ struct Workspace {
   // per-unique arrays
   DevBuf uniq, cnt, segstart, col, slot, flags, wb, Vb, vpos;
   DevBuf occ_row, occ_x;  // per occurrence in sorted order (backward walk)
+  DevBuf wv;              // per nnz: {w, vrow} of its key (fused forward)
   // per-row arrays
   DevBuf p, pred, XVp, rowtmp;
   DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
   DevBuf dscratch;  // double partials
+  DevBuf os;        // radix sort: digit counts [8][256] u32, then look-back words [tiles][256]
+  int64_t os_tiles = 0;
+  int os_reserve(int64_t ntiles);
+  uint32_t* os_counts() const { return os.as<uint32_t>(); }
+  unsigned long long* os_status() const {
+    return reinterpret_cast<unsigned long long*>(os.as<char>() + kOsCountBytes);
+  }
+  static constexpr size_t kOsCountBytes = 8 * 256 * sizeof(uint32_t);
   // sharded store, owner side (dist.hip): per received key / per owned unique key
   DevBuf oflags, ofrank, osegstart, osegslot, oseg_of, osorted;
   int64_t rows = 0, nnz = 0;
@@ -115,14 +125,16 @@ inline void prof_mark(Context* c, int m) {
 }
 
 // ---- cross-file launchers --------------------------------------------------------------
-// radix sort of (key, u32 payload) pairs over bits [begin_bit, end_bit), 8 bits per pass.
-// Reads from (k0,v0), uses (k1,v1) as the ping-pong buffer.  When diff_mask (device, a
-// u64 of the bits that vary) is given, passes over constant digits are skipped on the
-// device.  The result lives in buffer sel (0 or 1) written to *sel_dev.
-template <typename K>
-int radix_sort_pairs(Context* c, K* k0, uint32_t* v0, K* k1, uint32_t* v1, int64_t n,
-                     int begin_bit, int end_bit, const unsigned long long* diff_mask,
-                     unsigned int* sortmeta);
+// radix sort of (key, payload) pairs over bits [begin_bit, end_bit), 8 bits per pass
+// (sort.hip).  Reads from (k0,v0), uses (k1,v1) as the ping-pong buffer.  When diff_mask
+// (device, a u64 of the bits that vary) is given, passes over constant digits are skipped on
+// the device.  The result lives in buffer sortmeta[31] (0 or 1, device).  n_dev (optional):
+// a device-side item count <= n.
+constexpr int kOsSortTile = 4096;
+template <typename K, typename P>
+int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
+                     int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
+                     const uint32_t* n_dev = nullptr);
 
 // exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
 // n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.
@@ -132,13 +144,14 @@ int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
 void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);
 
-// Localizer::Compact on the device.  Leaves in the workspace: the sorted (key, pos)
-// pairs (buffer selected by ds->sortmeta[31]), rowid[nnz] when want_rowid, U in
-// ds->u_count.  Writes uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].
-// With occ_row (and occ_x when value != NULL) it also writes every occurrence's row (and
-// value) in sorted order, for the backward walk.  With nslot (fused step) every nnz's key is
-// found-or-inserted in the model table (nslot[nnz] = its slot) and segslot[U] receives each
-// unique key's slot; uniq / col may then be NULL.
+// Localizer::Compact on the device (localize.hip).  Leaves in the workspace the sorted
+// (key, payload) pairs (buffer selected by ds->sortmeta[31]) and U in ds->u_count.  Writes
+// uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].  With occ_row (and occ_x when
+// value != NULL) it also writes every occurrence's row (and value) in sorted order, for the
+// backward walk.  With segslot (fused step) every nnz's key is found-or-inserted in the model
+// table and segslot[U] receives each unique key's slot (uniq / col may then be NULL); per nnz
+// in input order it hands the forward either wv[nnz] = the key's {w, vrow} (no count push
+// before the forward) or nslot[nnz] = its slot.
 struct LocOut {
   uint64_t* uniq = nullptr;
   float* cnt = nullptr;
@@ -147,8 +160,9 @@ struct LocOut {
   const float* value = nullptr;
   uint32_t* occ_row = nullptr;
   float* occ_x = nullptr;
-  uint32_t* nslot = nullptr;
   uint32_t* segslot = nullptr;
+  int2* wv = nullptr;
+  uint32_t* nslot = nullptr;
 };
 int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o);

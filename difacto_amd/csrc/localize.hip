@@ -1,13 +1,17 @@
 // Localizer::Compact on gfx950 (src/data/localizer.cc:11-107).
 //
-//   1. k_loc_transform: key = ReverseBytes(id % max_index), payload = nnz position, and the
-//      row of every nnz (rowid, used by the transposed gradient); OR/AND of all keys so the
-//      radix sort skips digits that never vary (uniform 2^24 ids reverse into 24 high bits).
-//      In the fused step it also finds-or-inserts every nnz's key in the model table, so the
-//      forward pass reads each key's state by slot (no remapped column, no separate pull).
-//   2. stable LSD radix sort of (key, pos)                              (localizer.cc:26-27)
-//   3. run heads -> tile counts -> scan -> uniq[rank], segstart[rank], col[pos] = rank
-//      (CountUniqIndex's run-length pass + RemapIndex's merge-join, localizer.cc:31-107)
+//   1. k_loc_transform: key = ReverseBytes(id % max_index) and a 64-bit payload per nnz, plus
+//      the OR/AND of all keys so the radix sort skips digits that never vary (uniform 2^24 ids
+//      reverse into 24 high bits).  In the fused step it also finds-or-inserts every nnz's key
+//      in the model table (SGDUpdater::Get's model_[key]) and hands the forward pass the key's
+//      {w, V row} directly — the entry line the probe brought in — or, when a count push must
+//      run first, the slot.  Probes of several nnz are issued together (latency-bound loop).
+//   2. stable LSD radix sort of (key, payload)                          (localizer.cc:26-27)
+//   3. run heads -> tile counts -> scan -> per unique key (rank): uniq, segment start, slot;
+//      per nnz: col[pos] = rank (CountUniqIndex's run-length pass + RemapIndex's merge-join,
+//      localizer.cc:31-107); per occurrence in sorted order: its row (and value), which the
+//      backward pass walks.  What a consumer needs travels in the payload, so the write pass
+//      reads sorted data only (no random gathers on binary data).
 // Every index of the block is in its own dictionary, so the compacted block keeps all nnz:
 // its offsets/values/labels are the input's and only `col` is new.  Bit-exact by
 // construction (ranks depend only on keys).
@@ -16,50 +20,106 @@
 namespace dfx {
 
 constexpr int kLocNT = 256;
+constexpr int kLocRows = 64;   // rows per transform block
+constexpr int kLocUnr = 4;     // probes in flight per thread
 constexpr int kLocItems = 8;
 constexpr int kLocTile = kLocNT * kLocItems;
 
-__global__ __launch_bounds__(kLocNT) void k_loc_transform(
-    int64_t B, const uint64_t* __restrict__ offset, const uint64_t* __restrict__ index,
-    uint64_t max_index, uint64_t* __restrict__ keys, uint32_t* __restrict__ pos,
-    uint32_t* __restrict__ rowid, Table T, uint32_t* __restrict__ nslot, DevState* ds) {
-  __shared__ uint64_t offs[kLocNT + 1];
+// payload layouts (lo32 | hi32 << 32)
+enum LocMode : int {
+  kLocPlain = 0,     // lo = pos, hi = row               (dfx_localize, sharded worker)
+  kLocFusedBin = 1,  // lo = row, hi = table slot        (binary data: no value to fetch)
+  kLocFusedVal = 2,  // lo = pos, hi = table slot        (+ rowid[pos], value[pos] gathers)
+};
+
+struct TransformArgs {
+  int64_t B;
+  const uint64_t* offset;
+  const uint64_t* index;
+  uint64_t max_index;
+  uint64_t* keys;
+  uint64_t* pay;
+  uint32_t* rowid;  // fused valued: row of each nnz
+  Table T;
+  int2* wv;         // fused, no count push: {w, vrow} of each nnz's key
+  uint32_t* nslot;  // fused with a count push: each nnz's slot
+  DevState* ds;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
+  __shared__ uint64_t offs[kLocRows + 1];
   __shared__ unsigned long long red_or[kLocNT / kWave], red_and[kLocNT / kWave];
   __shared__ int red_ins[kLocNT / kWave];
-  const int64_t r0 = (int64_t)blockIdx.x * kLocNT;
-  const int64_t nr = (B - r0) < kLocNT ? (B - r0) : kLocNT;
-  for (int i = threadIdx.x; i <= nr; i += kLocNT) offs[i] = offset[r0 + i];
+  const int64_t r0 = (int64_t)blockIdx.x * kLocRows;
+  const int nr = (int)((a.B - r0) < kLocRows ? (a.B - r0) : kLocRows);
+  for (int i = threadIdx.x; i <= nr; i += kLocNT) offs[i] = a.offset[r0 + i];
   __syncthreads();
   const uint64_t j0 = offs[0], j1 = offs[nr];
   unsigned long long vor = 0, vand = ~0ull;
   int ins = 0;
-  for (uint64_t j = j0 + threadIdx.x; j < j1; j += kLocNT) {
-    uint64_t id = index[j];
-    uint64_t m = max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % max_index;
-    uint64_t k = reverse_bytes(m);
-    keys[j] = k;
-    pos[j] = (uint32_t)j;
-    vor |= k;
-    vand &= k;
-    if (rowid) {
-      // upper_bound(j) - 1 over the block's offsets (empty rows skipped)
-      int lo = 0, hi = (int)nr;
+  for (uint64_t jb = j0 + threadIdx.x; jb < j1; jb += (uint64_t)kLocNT * kLocUnr) {
+    uint64_t key[kLocUnr], h[kLocUnr];
+    bool ok[kLocUnr];
+#pragma unroll
+    for (int u = 0; u < kLocUnr; ++u) {
+      const uint64_t j = jb + (uint64_t)u * kLocNT;
+      ok[u] = j < j1;
+      const uint64_t id = ok[u] ? a.index[j] : 0ull;
+      const uint64_t m =
+          a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+      key[u] = reverse_bytes(m);
+    }
+    // probe the home slots of all items at once: key and {w, vrow} share the entry's line
+    unsigned long long kk[kLocUnr];
+    int2 wr[kLocUnr];
+    if (MODE != kLocPlain) {
+#pragma unroll
+      for (int u = 0; u < kLocUnr; ++u) {
+        h[u] = tbl_hash(key[u], a.T.logcap);
+        kk[u] = a.T.ent[h[u]].key;
+        wr[u] = *reinterpret_cast<const int2*>(a.T.ent + h[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kLocUnr; ++u) {
+      if (!ok[u]) continue;
+      const uint64_t j = jb + (uint64_t)u * kLocNT;
+      const uint64_t k = key[u];
+      vor |= k;
+      vand &= k;
+      // row = upper_bound(j) - 1 over the block's offsets (empty rows skipped)
+      int lo = 0, hi = nr;
       while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
+        const int mid = (lo + hi) >> 1;
         if (offs[mid] <= j) lo = mid; else hi = mid;
       }
-      rowid[j] = (uint32_t)(r0 + lo);
-    }
-    if (nslot) {
-      // model_[key] (sgd_updater.cc:37): duplicates of one key resolve to one slot via CAS
-      bool inserted;
-      int64_t s = tbl_insert(T, k, &inserted);
-      if (s < 0) {
-        atomicOr(&ds->err, kErrTableFull);
-        s = 0;
+      const int row = (int)(r0 + lo);
+      if (MODE == kLocPlain) {
+        a.keys[j] = k;
+        a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)row << 32);
+        continue;
       }
-      nslot[j] = (uint32_t)s;
-      ins += inserted ? 1 : 0;
+      int64_t s;
+      if (kk[u] == k) {
+        s = (int64_t)h[u];
+      } else {
+        // model_[key] (sgd_updater.cc:37): duplicates of one key resolve to one slot via CAS
+        bool inserted;
+        s = tbl_insert(a.T, k, &inserted);
+        if (s < 0) {
+          atomicOr(&a.ds->err, kErrTableFull);
+          s = 0;
+        }
+        ins += inserted ? 1 : 0;
+        wr[u] = *reinterpret_cast<const int2*>(a.T.ent + s);
+      }
+      a.keys[j] = k;
+      const uint32_t lo32 = MODE == kLocFusedBin ? (uint32_t)row : (uint32_t)j;
+      a.pay[j] = (uint64_t)lo32 | ((uint64_t)(uint32_t)s << 32);
+      if (MODE == kLocFusedVal) a.rowid[j] = (uint32_t)row;
+      if (a.wv) a.wv[j] = wr[u];
+      if (a.nslot) a.nslot[j] = (uint32_t)s;
     }
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -82,9 +142,9 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(
       vand &= red_and[w];
       ins += red_ins[w];
     }
-    atomicOr(&ds->or_mask, vor);
-    atomicAnd(&ds->and_mask, vand);
-    if (ins) atomicAdd(&ds->n_keys, (unsigned long long)ins);
+    atomicOr(&a.ds->or_mask, vor);
+    atomicAnd(&a.ds->and_mask, vand);
+    if (ins) atomicAdd(&a.ds->n_keys, (unsigned long long)ins);
   }
 }
 
@@ -116,8 +176,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const 
 struct LocWriteArgs {
   const uint64_t* k0;
   const uint64_t* k1;
-  const uint32_t* p0;
-  const uint32_t* p1;
+  const uint64_t* p0;
+  const uint64_t* p1;
   int64_t n;
   DevState* ds;
   const uint32_t* tilebase;
@@ -128,15 +188,15 @@ struct LocWriteArgs {
   const float* value;
   uint32_t* occ_row;
   float* occ_x;
-  const uint32_t* nslot;
   uint32_t* segslot;
 };
 
+template <int MODE>
 __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   const bool s1 = a.ds->sortmeta[31] != 0;
   const uint64_t* K = s1 ? a.k1 : a.k0;
-  const uint32_t* P = s1 ? a.p1 : a.p0;
+  const uint64_t* P = s1 ? a.p1 : a.p0;
   const int64_t n = a.n;
   const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint64_t k[kLocItems];
@@ -159,13 +219,12 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     if (idx < n) {
       incl += h[i];
       const uint32_t rank = incl - 1;
-      const uint32_t pos = P[idx];
       if (h[i]) {
         if (a.uniq) a.uniq[rank] = k[i];
         if (a.segstart) a.segstart[rank] = (uint32_t)idx;
-        if (a.segslot) a.segslot[rank] = a.nslot[pos];
+        if (MODE != kLocPlain) a.segslot[rank] = (uint32_t)(P[idx] >> 32);
       }
-      if (a.col) a.col[pos] = rank;
+      if (MODE == kLocPlain && a.col) a.col[(uint32_t)P[idx]] = rank;
       if (idx == n - 1) {
         a.ds->u_count = rank + 1;
         if (a.segstart) a.segstart[rank + 1] = (uint32_t)n;
@@ -179,9 +238,16 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     for (int i = 0; i < kLocItems; ++i) {
       const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
       if (idx < n) {
-        const uint32_t pos = P[idx];
-        a.occ_row[idx] = a.rowid[pos];
-        if (a.occ_x) a.occ_x[idx] = a.value[pos];
+        const uint64_t p = P[idx];
+        const uint32_t lo = (uint32_t)p;
+        if (MODE == kLocPlain) {
+          a.occ_row[idx] = (uint32_t)(p >> 32);
+        } else if (MODE == kLocFusedBin) {
+          a.occ_row[idx] = lo;
+        } else {
+          a.occ_row[idx] = a.rowid[lo];
+        }
+        if (MODE != kLocFusedBin && a.occ_x) a.occ_x[idx] = a.value[lo];
       }
     }
   }
@@ -206,42 +272,59 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
-  const bool want_rowid = o.occ_row != nullptr;
+  const bool fused = o.segslot != nullptr;
+  const int mode = !fused ? kLocPlain : (o.value ? kLocFusedVal : kLocFusedBin);
   DFX_TRY(ws.keys0.ensure(nnz * 8));
   DFX_TRY(ws.keys1.ensure(nnz * 8));
-  DFX_TRY(ws.vals0.ensure(nnz * 4));
-  DFX_TRY(ws.vals1.ensure(nnz * 4));
-  if (want_rowid) DFX_TRY(ws.rowid.ensure(nnz * 4));
+  DFX_TRY(ws.vals0.ensure(nnz * 8));
+  DFX_TRY(ws.vals1.ensure(nnz * 8));
+  if (mode == kLocFusedVal) DFX_TRY(ws.rowid.ensure(nnz * 4));
   uint32_t* segs = o.segstart;
   if (o.cnt && !segs) {
     DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
     segs = ws.segstart.as<uint32_t>();
   }
-  const int64_t ntile_rows = (B + kLocNT - 1) / kLocNT;
+  uint64_t* k0 = ws.keys0.as<uint64_t>();
+  uint64_t* k1 = ws.keys1.as<uint64_t>();
+  uint64_t* p0 = ws.vals0.as<uint64_t>();
+  uint64_t* p1 = ws.vals1.as<uint64_t>();
   hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, c->stream, c->ds);
-  hipLaunchKernelGGL(k_loc_transform, dim3(ntile_rows), dim3(kLocNT), 0, c->stream, B, offset,
-                     index, max_index, ws.keys0.as<uint64_t>(), ws.vals0.as<uint32_t>(),
-                     want_rowid ? ws.rowid.as<uint32_t>() : nullptr, c->T, o.nslot, c->ds);
+  TransformArgs t{};
+  t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
+  t.keys = k0; t.pay = p0; t.rowid = ws.rowid.as<uint32_t>(); t.T = c->T;
+  t.wv = o.wv; t.nslot = o.nslot; t.ds = c->ds;
+  const dim3 tg((unsigned)((B + kLocRows - 1) / kLocRows));
+  if (mode == kLocPlain) {
+    hipLaunchKernelGGL(k_loc_transform<kLocPlain>, tg, dim3(kLocNT), 0, c->stream, t);
+  } else if (mode == kLocFusedBin) {
+    hipLaunchKernelGGL(k_loc_transform<kLocFusedBin>, tg, dim3(kLocNT), 0, c->stream, t);
+  } else {
+    hipLaunchKernelGGL(k_loc_transform<kLocFusedVal>, tg, dim3(kLocNT), 0, c->stream, t);
+  }
   hipLaunchKernelGGL(k_loc_diff, dim3(1), dim3(1), 0, c->stream, c->ds);
-  DFX_TRY(radix_sort_pairs<uint64_t>(
-      c, ws.keys0.as<uint64_t>(), ws.vals0.as<uint32_t>(), ws.keys1.as<uint64_t>(),
-      ws.vals1.as<uint32_t>(), nnz, 0, 64, &c->ds->diff_mask, c->ds->sortmeta));
+  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(c, k0, p0, k1, p1, nnz, 0, 64,
+                                                &c->ds->diff_mask, c->ds->sortmeta)));
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = ws.tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, c->stream,
-                     ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>(), nnz, c->ds, ts);
+  hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, c->stream, k0, k1, nnz, c->ds,
+                     ts);
   scan_tiles_top(c, ts, ntiles, nullptr);
   LocWriteArgs a{};
-  a.k0 = ws.keys0.as<uint64_t>(); a.k1 = ws.keys1.as<uint64_t>();
-  a.p0 = ws.vals0.as<uint32_t>(); a.p1 = ws.vals1.as<uint32_t>();
+  a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1;
   a.n = nnz; a.ds = c->ds; a.tilebase = ts;
   a.uniq = o.uniq; a.col = o.col; a.segstart = segs;
-  a.rowid = want_rowid ? ws.rowid.as<uint32_t>() : nullptr;
+  a.rowid = ws.rowid.as<uint32_t>();
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
-  a.nslot = o.nslot; a.segslot = o.nslot ? o.segslot : nullptr;
-  hipLaunchKernelGGL(k_loc_write, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
+  a.segslot = o.segslot;
+  if (mode == kLocPlain) {
+    hipLaunchKernelGGL(k_loc_write<kLocPlain>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
+  } else if (mode == kLocFusedBin) {
+    hipLaunchKernelGGL(k_loc_write<kLocFusedBin>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
+  } else {
+    hipLaunchKernelGGL(k_loc_write<kLocFusedVal>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
+  }
   if (o.cnt) {
     hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, c->ds, segs,
                        o.cnt, nnz);

@@ -1,145 +1,159 @@
-// LSD radix sort of (key, u32 payload) pairs and a device-wide exclusive scan, written for
-// gfx950 wave64.  Stable: within a digit, items keep input order, so sorting (key, pos)
-// pairs whose pos ascends leaves every key's positions ascending — the (row, nnz) order
-// the reference's column sums use.
+// LSD radix sort of (key, payload) pairs — "onesweep" form — and a device-wide exclusive scan,
+// written for gfx950 wave64.  Stable: within a digit, items keep input order, so sorting
+// (key, pos) pairs whose pos ascends leaves every key's positions ascending — the (row, nnz)
+// order the reference's column sums use.
 //
-// One pass = 3 launches: per-tile digit histogram -> per-digit scan over tiles (one block
-// per digit) -> stable scatter.  The scatter ranks items inside a wave with 8 ballots per
-// 64-item chunk (a match-any on the digit), so the rank is exact and order preserving.
-// Passes whose digit is constant over all keys (detected by an OR/AND reduction the
-// caller provides) exit on the device: no host round trip, graph-capturable.
+// Launches per sort: k_os_plan (1 block: zero the digit counts, pick the active digits) ->
+// k_os_hist (one read of the keys: the global digit counts of EVERY pass) -> one k_os_scatter
+// per pass.  A scatter block takes its tile id from a counter (so tiles start in order), ranks
+// its 4096 items with wave ballots (exact and order preserving), publishes its per-digit counts
+// and finds its global offsets by decoupled look-back over the preceding tiles' published
+// words, then writes the tile through LDS in digit order, so stores leave in runs of
+// consecutive addresses.  Digits that are constant over all keys (an OR/AND reduction the
+// caller provides) get no pass: the active digits run first and the trailing launches exit on
+// the device — no host round trip, graph-capturable.  An optional device-side count (n_dev)
+// bounds the items when only the device knows it.
 #include "internal.h"
 
 namespace dfx {
 
-constexpr int kSortNT = 256;
-constexpr int kSortItems = 8;
-constexpr int kSortWaves = kSortNT / kWave;
-constexpr int kSortTile = kSortNT * kSortItems;  // 2048 items per tile
+constexpr int kOsNT = 256;
+constexpr int kOsWaves = kOsNT / kWave;
+constexpr int kOsItems = 16;
+constexpr int kOsTile = kOsNT * kOsItems;  // 4096 items per tile
+static_assert(kOsTile == kOsSortTile, "tile size");
+constexpr int kOsMaxPasses = 8;
+constexpr unsigned kOsNone = 0xFFFFFFFFu;
+// sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
+// buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
+// The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
+constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = 24;
 
-__global__ void k_sort_meta(const unsigned long long* diff_mask, int npasses, int begin_bit,
-                            int end_bit, unsigned int* meta) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  unsigned src = 0;
+__global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff_mask,
+                                                   int npasses, int begin_bit, int end_bit,
+                                                   unsigned int* meta, uint32_t* counts,
+                                                   DevState* ds) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < kOsMaxPasses; ++q) counts[q * 256 + t] = 0;
+  if (t != 0) return;
+  // one epoch counter for every sort of the context: tags never repeat across sorts
+  meta[kMetaEpoch] = ++ds->sort_epoch;
+  int q = 0;
   for (int p = 0; p < npasses; ++p) {
-    int shift = begin_bit + 8 * p;
-    int bits = end_bit - shift < 8 ? end_bit - shift : 8;
-    unsigned long long dmask = (1ull << bits) - 1;
-    unsigned active = diff_mask ? (((*diff_mask >> shift) & dmask) != 0) : 1u;
-    meta[2 * p] = active;
-    meta[2 * p + 1] = src;
-    if (active) src ^= 1u;
+    const int shift = begin_bit + 8 * p;
+    const int bits = end_bit - shift < 8 ? end_bit - shift : 8;
+    const unsigned long long dmask = (1ull << bits) - 1;
+    const bool active = diff_mask ? (((*diff_mask >> shift) & dmask) != 0) : true;
+    if (active) meta[q++] = (unsigned)shift | ((unsigned)bits << 16);
   }
-  meta[31] = src;
+  for (int r = q; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
+  for (int r = 0; r < kOsMaxPasses; ++r) {
+    meta[kMetaSrc + r] = (unsigned)(r & 1);
+    meta[kMetaTile + r] = 0;
+  }
+  meta[31] = (unsigned)(q & 1);
+}
+
+__device__ inline int64_t os_count(int64_t n, const uint32_t* n_dev) {
+  if (!n_dev) return n;
+  const int64_t m = (int64_t)*n_dev;
+  return m < n ? m : n;
 }
 
 template <typename K>
-__global__ __launch_bounds__(kSortNT) void k_sort_hist(const K* __restrict__ k0,
-                                                       const K* __restrict__ k1, int64_t n,
-                                                       int shift, uint32_t dmask,
-                                                       const unsigned int* meta, int pass,
-                                                       uint32_t* hist, int64_t ntiles) {
-  if (!meta[2 * pass]) return;
-  const K* keys = meta[2 * pass + 1] ? k1 : k0;
-  __shared__ uint32_t cnt[256];
-  cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+__global__ __launch_bounds__(kOsNT) void k_os_hist(const K* __restrict__ keys, int64_t n0,
+                                                   const uint32_t* n_dev,
+                                                   const unsigned int* meta, uint32_t* counts) {
+  __shared__ uint32_t lc[kOsMaxPasses][256];
+  __shared__ unsigned sm[kOsMaxPasses];
+  const int t = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < kSortItems; ++i) {
-    int64_t idx = base + (int64_t)i * kSortNT + threadIdx.x;
-    if (idx < n) atomicAdd(&cnt[(uint32_t)(keys[idx] >> shift) & dmask], 1u);
+  for (int q = 0; q < kOsMaxPasses; ++q) lc[q][t] = 0;
+  if (t < kOsMaxPasses) sm[t] = meta[t];
+  __syncthreads();
+  int nq = 0;
+  while (nq < kOsMaxPasses && sm[nq] != kOsNone) ++nq;
+  const int64_t n = os_count(n0, n_dev);
+  for (int64_t i = (int64_t)blockIdx.x * kOsNT + t; i < n; i += (int64_t)gridDim.x * kOsNT) {
+    const K k = keys[i];
+    for (int q = 0; q < nq; ++q) {
+      const unsigned m = sm[q];
+      const uint32_t d = (uint32_t)(k >> (m & 0xFFFFu)) & ((1u << (m >> 16)) - 1u);
+      atomicAdd(&lc[q][d], 1u);
+    }
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+  for (int q = 0; q < nq; ++q)
+    if (lc[q][t]) atomicAdd(&counts[q * 256 + t], lc[q][t]);
 }
 
-// one block per digit: exclusive scan of that digit's per-tile counts, total -> rowtot
-__global__ __launch_bounds__(kSortNT) void k_sort_rowscan(uint32_t* hist, int64_t ntiles,
-                                                          uint32_t* rowtot,
-                                                          const unsigned int* meta, int pass) {
-  if (!meta[2 * pass]) return;
-  __shared__ uint32_t lds[kSortNT / kWave + 1];
-  uint32_t* row = hist + (int64_t)blockIdx.x * ntiles;
-  uint32_t run = 0;
-  for (int64_t s = 0; s < ntiles; s += kSortNT * 4) {
-    uint32_t v[4];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int64_t idx = s + (int64_t)threadIdx.x * 4 + j;
-      v[j] = idx < ntiles ? row[idx] : 0;
-      sum += v[j];
-    }
-    uint32_t tot;
-    uint32_t ex = block_excl_scan<kSortNT>(sum, lds, &tot);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int64_t idx = s + (int64_t)threadIdx.x * 4 + j;
-      if (idx < ntiles) row[idx] = run + ex;
-      ex += v[j];
-    }
-    run += tot;
-  }
-  if (threadIdx.x == 0) rowtot[blockIdx.x] = run;
+__device__ inline unsigned long long os_word(uint32_t tag, uint32_t flag, uint32_t v) {
+  return ((unsigned long long)((tag << 2) | flag) << 32) | v;
 }
 
-template <typename K>
-__global__ __launch_bounds__(kSortNT) void k_sort_scatter(K* k0, uint32_t* v0, K* k1,
-                                                          uint32_t* v1, int64_t n, int shift,
-                                                          int bits, const unsigned int* meta,
-                                                          int pass, const uint32_t* hist,
-                                                          const uint32_t* rowtot,
-                                                          int64_t ntiles) {
-  if (!meta[2 * pass]) return;
-  const bool from1 = meta[2 * pass + 1] != 0;
+template <typename K, typename P>
+__global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1, int64_t n0,
+                                                      const uint32_t* n_dev, unsigned int* meta,
+                                                      int q, const uint32_t* counts,
+                                                      unsigned long long* status,
+                                                      DevState* ds) {
+  const unsigned m = meta[q];
+  if (m == kOsNone) return;
+  const int shift = (int)(m & 0xFFFFu);
+  const uint32_t dmask = (1u << (m >> 16)) - 1u;
+  const int bits = (int)(m >> 16);
+  const bool from1 = meta[kMetaSrc + q] != 0;
   const K* kin = from1 ? k1 : k0;
-  const uint32_t* vin = from1 ? v1 : v0;
+  const P* vin = from1 ? v1 : v0;
   K* kout = from1 ? k0 : k1;
-  uint32_t* vout = from1 ? v0 : v1;
-  const uint32_t dmask = (1u << bits) - 1;
+  P* vout = from1 ? v0 : v1;
+  const uint32_t tag = (meta[kMetaEpoch] * kOsMaxPasses + (unsigned)q) & 0x3FFFFFFFu;
 
-  __shared__ uint32_t wcnt[kSortWaves][256];
-  __shared__ uint32_t dbase[256];
-  __shared__ uint32_t lds[kSortNT / kWave + 1];
+  __shared__ K lk[kOsTile];
+  __shared__ P lv[kOsTile];
+  __shared__ uint32_t wcnt[kOsWaves][256];
+  __shared__ uint32_t gdig[256], lstart[256];
+  __shared__ uint32_t lds[kOsNT / kWave + 1];
+  __shared__ int64_t s_tile;
   const int t = threadIdx.x;
   const int w = t / kWave;
   const int l = lane_id();
-  {
-    uint32_t tot = rowtot[t];
-    uint32_t ex = block_excl_scan<kSortNT>(tot, lds, nullptr);
-    dbase[t] = ex + hist[(int64_t)t * ntiles + blockIdx.x];
-  }
+  if (t == 0) s_tile = (int64_t)atomicAdd(&meta[kMetaTile + q], 1u);
 #pragma unroll
-  for (int i = 0; i < kSortWaves; ++i) wcnt[i][t] = 0;
+  for (int i = 0; i < kOsWaves; ++i) wcnt[i][t] = 0;
   __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t n = os_count(n0, n_dev);
+  const int64_t tbase = tile * kOsTile;
+  if (tbase >= n) return;  // every later tile exits too: no waiter is left behind
 
-  K key[kSortItems];
-  uint32_t val[kSortItems];
-  uint32_t rank[kSortItems];
-  uint32_t dig[kSortItems];
-  const int64_t wbase = (int64_t)blockIdx.x * kSortTile + (int64_t)w * kWave * kSortItems;
+  // ---- load (wave w owns a contiguous 64*kOsItems run) and rank with ballots
+  K key[kOsItems];
+  P val[kOsItems];
+  uint32_t rank[kOsItems], dig[kOsItems];
+  const int64_t wbase = tbase + (int64_t)w * kWave * kOsItems;
 #pragma unroll
-  for (int c = 0; c < kSortItems; ++c) {
-    int64_t idx = wbase + c * kWave + l;
-    bool valid = idx < n;
+  for (int c = 0; c < kOsItems; ++c) {
+    const int64_t idx = wbase + c * kWave + l;
+    const bool valid = idx < n;
     key[c] = valid ? kin[idx] : (K)0;
-    val[c] = (valid && vin) ? vin[idx] : 0u;
+    val[c] = valid ? vin[idx] : (P)0;
   }
 #pragma unroll
-  for (int c = 0; c < kSortItems; ++c) {
-    int64_t idx = wbase + c * kWave + l;
-    bool valid = idx < n;
-    uint32_t d = valid ? ((uint32_t)(key[c] >> shift) & dmask) : 0u;
+  for (int c = 0; c < kOsItems; ++c) {
+    const int64_t idx = wbase + c * kWave + l;
+    const bool valid = idx < n;
+    const uint32_t d = valid ? ((uint32_t)(key[c] >> shift) & dmask) : 0u;
     uint64_t peers = __ballot(valid);
     for (int b = 0; b < bits; ++b) {
-      bool bit = (d >> b) & 1u;
-      uint64_t m = __ballot(valid && bit);
-      peers &= bit ? m : ~m;
+      const bool bit = (d >> b) & 1u;
+      const uint64_t mb = __ballot(valid && bit);
+      peers &= bit ? mb : ~mb;
     }
     if (!valid) peers = 0;
-    uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
-    uint32_t old = valid ? wcnt[w][d] : 0u;
+    const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
+    const uint32_t old = valid ? wcnt[w][d] : 0u;
     __builtin_amdgcn_wave_barrier();
     if (valid && r == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
     __builtin_amdgcn_wave_barrier();
@@ -147,64 +161,118 @@ __global__ __launch_bounds__(kSortNT) void k_sort_scatter(K* k0, uint32_t* v0, K
     dig[c] = d;
   }
   __syncthreads();
-  {
-    uint32_t run = 0;
+  // ---- per-digit tile count; waves' exclusive offsets within the digit
+  uint32_t cnt = 0;
 #pragma unroll
-    for (int i = 0; i < kSortWaves; ++i) {
-      uint32_t x = wcnt[i][t];
-      wcnt[i][t] = run;
-      run += x;
+  for (int i = 0; i < kOsWaves; ++i) {
+    const uint32_t x = wcnt[i][t];
+    wcnt[i][t] = cnt;
+    cnt += x;
+  }
+  // ---- decoupled look-back: this digit's items in all preceding tiles
+  unsigned long long* st = status + tile * 256 + t;
+  uint32_t pre = 0;
+  if (tile == 0) {
+    __hip_atomic_store(st, os_word(tag, 2u, cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(st, os_word(tag, 1u, cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t k = tile - 1;
+    uint32_t spins = 0;
+    while (k >= 0) {
+      const unsigned long long v = __hip_atomic_load(status + k * 256 + t, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t hi = (uint32_t)(v >> 32);
+      if ((hi >> 2) != tag || (hi & 3u) == 0) {
+        if (++spins > (1u << 26)) {  // a predecessor never published: give up loudly
+          atomicOr(&ds->err, kErrSort);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      pre += (uint32_t)v;
+      if ((hi & 3u) == 2u) break;
+      --k;
+    }
+    __hip_atomic_store(st, os_word(tag, 2u, pre + cnt), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // global start of this digit's items in this tile; tile-local start of the digit
+  const uint32_t gb = block_excl_scan<kOsNT>(counts[q * 256 + t], lds, nullptr);
+  gdig[t] = gb + pre;
+  lstart[t] = block_excl_scan<kOsNT>(cnt, lds, nullptr);
+  __syncthreads();
+  // ---- tile-local stable sort through LDS, then stores in digit runs
+#pragma unroll
+  for (int c = 0; c < kOsItems; ++c) {
+    const int64_t idx = wbase + c * kWave + l;
+    if (idx < n) {
+      const uint32_t li = lstart[dig[c]] + wcnt[w][dig[c]] + rank[c];
+      lk[li] = key[c];
+      lv[li] = val[c];
     }
   }
   __syncthreads();
+  const int64_t nvalid = (n - tbase) < kOsTile ? (n - tbase) : kOsTile;
 #pragma unroll
-  for (int c = 0; c < kSortItems; ++c) {
-    int64_t idx = wbase + c * kWave + l;
-    if (idx < n) {
-      uint32_t pos = dbase[dig[c]] + wcnt[w][dig[c]] + rank[c];
-      kout[pos] = key[c];
-      if (vout) vout[pos] = val[c];
+  for (int i = 0; i < kOsItems; ++i) {
+    const int qi = i * kOsNT + t;
+    if (qi < nvalid) {
+      const K kk = lk[qi];
+      const uint32_t d = (uint32_t)(kk >> shift) & dmask;
+      const uint32_t pos = gdig[d] + ((uint32_t)qi - lstart[d]);
+      kout[pos] = kk;
+      vout[pos] = lv[qi];
     }
   }
 }
 
-template <typename K>
-int radix_sort_pairs(Context* c, K* k0, uint32_t* v0, K* k1, uint32_t* v1, int64_t n,
-                     int begin_bit, int end_bit, const unsigned long long* diff_mask,
-                     unsigned int* sortmeta) {
+int Workspace::os_reserve(int64_t ntiles) {
+  if (ntiles < 1) ntiles = 1;
+  void* before = os.p;
+  const size_t want = kOsCountBytes + (size_t)ntiles * 256 * sizeof(unsigned long long);
+  DFX_TRY(os.ensure(want));
+  if (os.p != before) DFX_HIP(hipMemset(os.p, 0, os.bytes));  // no stale look-back words
+  os_tiles = ntiles;
+  return DFX_OK;
+}
+
+template <typename K, typename P>
+int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
+                     int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
+                     const uint32_t* n_dev) {
   if (n <= 0 || end_bit <= begin_bit) {
-    hipLaunchKernelGGL(k_sort_meta, dim3(1), dim3(1), 0, c->stream, diff_mask, 0, begin_bit,
-                       end_bit, sortmeta);
+    DFX_TRY(c->ws.os_reserve(1));
+    hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, 0, begin_bit,
+                       end_bit, sortmeta, c->ws.os_counts(), c->ds);
+    DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
   const int npasses = (end_bit - begin_bit + 7) / 8;
-  const int64_t ntiles = (n + kSortTile - 1) / kSortTile;
-  DFX_TRY(c->ws.hist.ensure(sizeof(uint32_t) * (256 * ntiles + 256)));
-  uint32_t* hist = c->ws.hist.as<uint32_t>();
-  uint32_t* rowtot = hist + 256 * ntiles;
-  hipLaunchKernelGGL(k_sort_meta, dim3(1), dim3(1), 0, c->stream, diff_mask, npasses,
-                     begin_bit, end_bit, sortmeta);
-  for (int p = 0; p < npasses; ++p) {
-    int shift = begin_bit + 8 * p;
-    int bits = end_bit - shift < 8 ? end_bit - shift : 8;
-    uint32_t dmask = (1u << bits) - 1;
-    hipLaunchKernelGGL(k_sort_hist<K>, dim3(ntiles), dim3(kSortNT), 0, c->stream, k0, k1, n,
-                       shift, dmask, sortmeta, p, hist, ntiles);
-    hipLaunchKernelGGL(k_sort_rowscan, dim3(256), dim3(kSortNT), 0, c->stream, hist, ntiles,
-                       rowtot, sortmeta, p);
-    hipLaunchKernelGGL(k_sort_scatter<K>, dim3(ntiles), dim3(kSortNT), 0, c->stream, k0, v0,
-                       k1, v1, n, shift, bits, sortmeta, p, hist, rowtot, ntiles);
+  const int64_t ntiles = (n + kOsTile - 1) / kOsTile;
+  DFX_TRY(c->ws.os_reserve(ntiles));
+  uint32_t* counts = c->ws.os_counts();
+  unsigned long long* status = c->ws.os_status();
+  hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, npasses,
+                     begin_bit, end_bit, sortmeta, counts, c->ds);
+  const int64_t hblocks = ntiles < 1024 ? ntiles : 1024;
+  hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)hblocks), dim3(kOsNT), 0, c->stream, k0, n,
+                     n_dev, sortmeta, counts);
+  for (int q = 0; q < npasses; ++q) {
+    hipLaunchKernelGGL((k_os_scatter<K, P>), dim3((unsigned)ntiles), dim3(kOsNT), 0, c->stream,
+                       k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, c->ds);
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-template int radix_sort_pairs<uint64_t>(Context*, uint64_t*, uint32_t*, uint64_t*, uint32_t*,
-                                        int64_t, int, int, const unsigned long long*,
-                                        unsigned int*);
-template int radix_sort_pairs<uint32_t>(Context*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                                        int64_t, int, int, const unsigned long long*,
-                                        unsigned int*);
+#define DFX_SORT_INST(K, P)                                                                  \
+  template int radix_sort_pairs<K, P>(Context*, K*, P*, K*, P*, int64_t, int, int,           \
+                                      const unsigned long long*, unsigned int*, const uint32_t*);
+DFX_SORT_INST(uint64_t, uint32_t)
+DFX_SORT_INST(uint64_t, uint64_t)
+DFX_SORT_INST(uint32_t, uint32_t)
+#undef DFX_SORT_INST
 
 // ---- device-wide exclusive scan (reduce -> scan tile sums -> scan + apply) -------------
 constexpr int kScanNT = 256;

@@ -30,11 +30,11 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   const int64_t ntiles = (nnz + 2047) / 2048;
   DFX_TRY(ws.keys0.ensure(nnz * 8));
   DFX_TRY(ws.keys1.ensure(nnz * 8));
-  DFX_TRY(ws.vals0.ensure(nnz * 4));
-  DFX_TRY(ws.vals1.ensure(nnz * 4));
+  DFX_TRY(ws.vals0.ensure(nnz * 8));
+  DFX_TRY(ws.vals1.ensure(nnz * 8));
+  DFX_TRY(ws.wv.ensure(nnz * 8));
+  DFX_TRY(ws.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
   DFX_TRY(ws.rowid.ensure(nnz * 4));
-  DFX_TRY(ws.hist.ensure(sizeof(uint32_t) * (256 * (ntiles > (rows + 2047) / 2048
-                                                        ? ntiles : (rows + 2047) / 2048) + 256)));
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(ws.col.ensure(nnz * 4));
@@ -87,21 +87,30 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   // the model table (Get's model_[key], sgd_updater.cc:37); segments come out in sorted key
   // order, which is the order Update walks keys in (InitV draws) and the (row, nnz) order of
   // every key's gradient sum.
+  // Without a count push nothing changes the table between this probe and the forward, so
+  // the probe hands each nnz's {w, vrow} straight to it; a count push (epoch 0) may InitV
+  // first, so the forward then re-reads the entry by slot.
+  const bool cnt_first = push_cnt && d > 0;
   LocOut o;
   o.segstart = segstart;
   o.value = b->value;
   o.occ_row = occ_row;
   o.occ_x = occ_x;
-  o.nslot = nslot;
   o.segslot = segslot;
+  if (cnt_first) {
+    o.nslot = nslot;
+  } else {
+    o.wv = ws.wv.as<int2>();
+  }
   DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, o));
   prof_mark(c, 1);
-  if (push_cnt && d > 0) DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total));
+  if (cnt_first) DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total));
   prof_mark(c, 2);
   prof_mark(c, 3);  // the pull is the forward's direct read of each key's table entry
 
   FwdArgs a{};
-  a.B = B; a.offs = b->offset; a.col = nslot; a.val = b->value; a.T = c->T;
+  a.B = B; a.offs = b->offset; a.col = nslot; a.wv = cnt_first ? nullptr : ws.wv.as<int2>();
+  a.val = b->value; a.T = c->T;
   a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>();

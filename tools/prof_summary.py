@@ -1,16 +1,19 @@
-"""Summarise a rocprofv3 kernel trace (+ optional FETCH/WRITE PMC passes) per kernel over
-the LAST n dispatches of each kernel (the bench's timed steps), as markdown."""
-import csv
+"""Summarise a rocprofv3 kernel trace (+ optional FETCH/WRITE PMC passes) over the bench's
+timed steps, as markdown.
+
+The timed window is the last N steps: it starts where the (N+1)-th-from-last step's
+`k_step_finalize` ended and stops where the last one ended.  Per kernel: dispatches per step,
+average duration, microseconds per step, and the busy fraction of the window.
+usage: prof_summary.py trace.csv N [fetch_pmc.csv write_pmc.csv]
+"""
 import collections
+import csv
 import sys
 
 
-def load_trace(path):
-    rows = list(csv.DictReader(open(path)))
-    per = collections.defaultdict(list)
-    for r in rows:
-        per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    return per
+def short(name):
+    s = name.split("(")[0]
+    return s.replace("void ", "").replace("dfx::", "")[:56]
 
 
 def load_pmc(path):
@@ -20,31 +23,40 @@ def load_pmc(path):
     return per
 
 
-def short(name):
-    s = name.split("(")[0]
-    return s.replace("void ", "").replace("dfx::", "")[:48]
-
-
 def main():
-    trace, last = sys.argv[1], int(sys.argv[2])
+    trace, nsteps = sys.argv[1], int(sys.argv[2])
     fetch = load_pmc(sys.argv[3]) if len(sys.argv) > 3 else {}
     write = load_pmc(sys.argv[4]) if len(sys.argv) > 4 else {}
-    per = load_trace(trace)
-    rows = []
-    for k, v in per.items():
-        calls_per_step = max(1, round(len(v) / max(1, len(per.get(next(
-            n for n in per if "k_step_finalize" in n or "k_sum_parts" in n), [1])))))
-        tail = v[-last * calls_per_step:]
-        rows.append((sum(tail) / last, k, len(v), sum(tail) / len(tail), calls_per_step))
-    rows.sort(reverse=True)
-    print("| kernel | calls/step | avg us/dispatch (last %d steps) | us/step | FETCH_SIZE MB/dispatch | WRITE_SIZE MB/dispatch |" % last)
-    print("|---|---|---|---|---|---|")
-    for per_step, k, n, avg, cps in rows:
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        fm = "%.1f" % (sum(f[-cps:]) / max(1, len(f[-cps:])) / 1024) if f else ""
-        wm = "%.1f" % (sum(w[-cps:]) / max(1, len(w[-cps:])) / 1024) if w else ""
-        print("| %s | %d | %.1f | %.1f | %s | %s |" % (short(k), cps, avg, per_step, fm, wm))
+    rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+            for r in csv.DictReader(open(trace))]
+    rows.sort()
+    fin = [e for s, e, k in rows if "k_step_finalize" in k]
+    if len(fin) < nsteps + 1:
+        raise SystemExit("trace holds %d steps, need %d" % (len(fin), nsteps + 1))
+    t0, t1 = fin[-nsteps - 1], fin[-1]
+    per = collections.defaultdict(list)
+    busy = 0
+    for s, e, k in rows:
+        if s >= t0 and e <= t1:
+            per[k].append((e - s) / 1e3)
+            busy += e - s
+    wall_us = (t1 - t0) / 1e3
+    out = sorted(((sum(v) / nsteps, k, v) for k, v in per.items()), reverse=True)
+    print("window: %d steps, %.1f us/step wall, %.1f us/step inside kernels, %d dispatches/step"
+          % (nsteps, wall_us / nsteps, busy / 1e3 / nsteps,
+             sum(len(v) for v in per.values()) // nsteps))
+    print()
+    print("| kernel | calls/step | avg us/dispatch | us/step | % of step | FETCH_SIZE MB/dispatch "
+          "| WRITE_SIZE MB/dispatch |")
+    print("|---|---|---|---|---|---|---|")
+    for us, k, v in out:
+        cps = len(v) / nsteps
+        f, w = fetch.get(k, []), write.get(k, [])
+        n = max(1, int(round(cps)))
+        fm = "%.1f" % (sum(f[-n:]) / len(f[-n:]) / 1024) if f else ""
+        wm = "%.1f" % (sum(w[-n:]) / len(w[-n:]) / 1024) if w else ""
+        print("| %s | %.2g | %.1f | %.1f | %.1f | %s | %s |" % (
+            short(k), cps, sum(v) / len(v), us, 100 * us * nsteps / wall_us, fm, wm))
 
 
 if __name__ == "__main__":
