@@ -68,6 +68,10 @@ struct DevState {
   double scratch[8];
 };
 
+constexpr int kOsSortTile = 4096;  // radix sort tile (sort.hip)
+constexpr int kOsDigits = 8;       // 8-bit digit positions of a u64 key
+constexpr int kOsParts = 16;       // partial digit-count copies (spread the atomics)
+
 struct Workspace {
   // sort double buffers (u64 keys, u32 payload) and per-nnz arrays
   DevBuf keys0, keys1, vals0, vals1, rowid;
@@ -81,14 +85,17 @@ struct Workspace {
   DevBuf p, pred, XVp, rowtmp;
   DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
   DevBuf dscratch;  // double partials
-  DevBuf os;        // radix sort: digit counts [8][256] u32, then look-back words [tiles][256]
+  // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
+  // look-back words [tiles][256] (u64)
+  DevBuf os;
   int64_t os_tiles = 0;
   int os_reserve(int64_t ntiles);
-  uint32_t* os_counts() const { return os.as<uint32_t>(); }
+  uint32_t* os_parts() const { return os.as<uint32_t>(); }
+  uint32_t* os_counts() const { return os.as<uint32_t>() + kOsParts * kOsDigits * 256; }
   unsigned long long* os_status() const {
     return reinterpret_cast<unsigned long long*>(os.as<char>() + kOsCountBytes);
   }
-  static constexpr size_t kOsCountBytes = 8 * 256 * sizeof(uint32_t);
+  static constexpr size_t kOsCountBytes = (kOsParts + 1) * kOsDigits * 256 * sizeof(uint32_t);
   // sharded store, owner side (dist.hip): per received key / per owned unique key
   DevBuf oflags, ofrank, osegstart, osegslot, oseg_of, osorted;
   int64_t rows = 0, nnz = 0;
@@ -130,11 +137,14 @@ inline void prof_mark(Context* c, int m) {
 // (device, a u64 of the bits that vary) is given, passes over constant digits are skipped on
 // the device.  The result lives in buffer sortmeta[31] (0 or 1, device).  n_dev (optional):
 // a device-side item count <= n.
-constexpr int kOsSortTile = 4096;
+// flags: kSortDiffIsOrAnd — diff_mask points at {OR, AND} of the keys (the varying bits are
+// their XOR); kSortCountsReady — the producer of the keys already added the counts of every
+// 8-bit digit position into ws.os_parts()[block % kOsParts] (begin_bit must be 0).
+constexpr int kSortDiffIsOrAnd = 1, kSortCountsReady = 2;
 template <typename K, typename P>
 int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
-                     const uint32_t* n_dev = nullptr);
+                     const uint32_t* n_dev = nullptr, int flags = 0);
 
 // exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
 // n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.

@@ -33,6 +33,7 @@ enum LocMode : int {
 };
 
 struct TransformArgs {
+  uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
   int64_t B;
   const uint64_t* offset;
   const uint64_t* index;
@@ -51,6 +52,9 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
   __shared__ uint64_t offs[kLocRows + 1];
   __shared__ unsigned long long red_or[kLocNT / kWave], red_and[kLocNT / kWave];
   __shared__ int red_ins[kLocNT / kWave];
+  __shared__ uint32_t hist[kOsDigits][256];  // digit counts for the sort (no extra key read)
+#pragma unroll
+  for (int p = 0; p < kOsDigits; ++p) hist[p][threadIdx.x] = 0;
   const int64_t r0 = (int64_t)blockIdx.x * kLocRows;
   const int nr = (int)((a.B - r0) < kLocRows ? (a.B - r0) : kLocRows);
   for (int i = threadIdx.x; i <= nr; i += kLocNT) offs[i] = a.offset[r0 + i];
@@ -88,6 +92,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
       const uint64_t k = key[u];
       vor |= k;
       vand &= k;
+#pragma unroll
+      for (int p = 0; p < kOsDigits; ++p) atomicAdd(&hist[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
       // row = upper_bound(j) - 1 over the block's offsets (empty rows skipped)
       int lo = 0, hi = nr;
       while (hi - lo > 1) {
@@ -146,14 +152,16 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
     atomicAnd(&a.ds->and_mask, vand);
     if (ins) atomicAdd(&a.ds->n_keys, (unsigned long long)ins);
   }
+  uint32_t* dst = a.parts + (size_t)(blockIdx.x % kOsParts) * kOsDigits * 256;
+#pragma unroll
+  for (int p = 0; p < kOsDigits; ++p)
+    if (hist[p][threadIdx.x]) atomicAdd(&dst[p * 256 + threadIdx.x], hist[p][threadIdx.x]);
 }
 
 __global__ void k_loc_init(DevState* ds) {
   ds->or_mask = 0;
   ds->and_mask = ~0ull;
 }
-
-__global__ void k_loc_diff(DevState* ds) { ds->diff_mask = ds->or_mask ^ ds->and_mask; }
 
 // heads per tile
 __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const uint64_t* k1,
@@ -288,8 +296,10 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
   uint64_t* k1 = ws.keys1.as<uint64_t>();
   uint64_t* p0 = ws.vals0.as<uint64_t>();
   uint64_t* p1 = ws.vals1.as<uint64_t>();
+  DFX_TRY(ws.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
   hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, c->stream, c->ds);
   TransformArgs t{};
+  t.parts = ws.os_parts();
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
   t.keys = k0; t.pay = p0; t.rowid = ws.rowid.as<uint32_t>(); t.T = c->T;
   t.wv = o.wv; t.nslot = o.nslot; t.ds = c->ds;
@@ -301,9 +311,10 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
   } else {
     hipLaunchKernelGGL(k_loc_transform<kLocFusedVal>, tg, dim3(kLocNT), 0, c->stream, t);
   }
-  hipLaunchKernelGGL(k_loc_diff, dim3(1), dim3(1), 0, c->stream, c->ds);
-  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(c, k0, p0, k1, p1, nnz, 0, 64,
-                                                &c->ds->diff_mask, c->ds->sortmeta)));
+  // the varying bits are OR ^ AND of the keys; the transform already counted the digits
+  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(c, k0, p0, k1, p1, nnz, 0, 64, &c->ds->or_mask,
+                                                c->ds->sortmeta, nullptr,
+                                                kSortDiffIsOrAnd | kSortCountsReady)));
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = ws.tiles.as<uint32_t>();

@@ -3,16 +3,18 @@
 // (key, pos) pairs whose pos ascends leaves every key's positions ascending — the (row, nnz)
 // order the reference's column sums use.
 //
-// Launches per sort: k_os_plan (1 block: zero the digit counts, pick the active digits) ->
-// k_os_hist (one read of the keys: the global digit counts of EVERY pass) -> one k_os_scatter
-// per pass.  A scatter block takes its tile id from a counter (so tiles start in order), ranks
-// its 4096 items with wave ballots (exact and order preserving), publishes its per-digit counts
-// and finds its global offsets by decoupled look-back over the preceding tiles' published
-// words, then writes the tile through LDS in digit order, so stores leave in runs of
-// consecutive addresses.  Digits that are constant over all keys (an OR/AND reduction the
-// caller provides) get no pass: the active digits run first and the trailing launches exit on
-// the device — no host round trip, graph-capturable.  An optional device-side count (n_dev)
-// bounds the items when only the device knows it.
+// Launches per sort: [k_os_hist: one read of the keys, the digit counts of EVERY pass — or the
+// producer of the keys accumulates them itself, as the Localizer's transform does] ->
+// k_os_plan (1 block: reduce the counts, pick the digits that vary) -> one k_os_scatter per
+// pass.  A scatter block takes its tile id from a counter (so tiles start in order), ranks its
+// 4096 items with wave ballots (exact and order preserving), publishes its per-digit counts and
+// finds its global offsets by decoupled look-back over the preceding tiles' published words
+// (several predecessors read per step), then writes the tile through LDS in digit order, so
+// stores leave in runs of consecutive addresses: keys first, then the payloads through the same
+// LDS buffer (half the LDS, more blocks per CU).  Digits that are constant over all keys (an
+// OR/AND reduction of the keys) get no pass: the active digits run first and the trailing
+// launches exit on the device — no host round trip, graph-capturable.  An optional
+// device-side count (n_dev) bounds the items when only the device knows it.
 #include "internal.h"
 
 namespace dfx {
@@ -22,37 +24,59 @@ constexpr int kOsWaves = kOsNT / kWave;
 constexpr int kOsItems = 16;
 constexpr int kOsTile = kOsNT * kOsItems;  // 4096 items per tile
 static_assert(kOsTile == kOsSortTile, "tile size");
-constexpr int kOsMaxPasses = 8;
+static_assert(kOsTile <= 4096, "rank packing below assumes < 2^12 items per wave");
+constexpr int kOsMaxPasses = kOsDigits;
+constexpr int kOsLookback = 4;  // predecessor words read per look-back step
 constexpr unsigned kOsNone = 0xFFFFFFFFu;
 // sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
 // The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
 constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = 24;
 
-__global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff_mask,
+// Reduce the partial digit counts (parts[kOsParts][8][256], digit position p = bits
+// [begin + 8p, +8)) into counts[q] for the active passes q, zero the parts for the next sort,
+// and write the plan.  diff: the bits that vary, or (or_and) a pointer to {OR, AND} of the keys.
+__global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff, int or_and,
                                                    int npasses, int begin_bit, int end_bit,
-                                                   unsigned int* meta, uint32_t* counts,
-                                                   DevState* ds) {
+                                                   unsigned int* meta, uint32_t* parts,
+                                                   uint32_t* counts, DevState* ds) {
+  __shared__ int s_pos[kOsMaxPasses];
+  __shared__ int s_nq;
   const int t = threadIdx.x;
+  if (t == 0) {
+    // one epoch counter for every sort of the context: tags never repeat across sorts
+    meta[kMetaEpoch] = ++ds->sort_epoch;
+    unsigned long long dm = ~0ull;
+    if (diff) dm = or_and ? (diff[0] ^ diff[1]) : diff[0];
+    int q = 0;
+    for (int p = 0; p < npasses; ++p) {
+      const int shift = begin_bit + 8 * p;
+      const int bits = end_bit - shift < 8 ? end_bit - shift : 8;
+      const unsigned long long dmask = (1ull << bits) - 1;
+      if (((dm >> shift) & dmask) != 0) {
+        s_pos[q] = p;
+        meta[q++] = (unsigned)shift | ((unsigned)bits << 16);
+      }
+    }
+    for (int r = q; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
+    for (int r = 0; r < kOsMaxPasses; ++r) {
+      meta[kMetaSrc + r] = (unsigned)(r & 1);
+      meta[kMetaTile + r] = 0;
+    }
+    meta[31] = (unsigned)(q & 1);
+    s_nq = q;
+  }
+  __syncthreads();
+  const int nq = s_nq;
+  for (int q = 0; q < nq; ++q) {
+    const int p = s_pos[q];
+    uint32_t sum = 0;
 #pragma unroll
-  for (int q = 0; q < kOsMaxPasses; ++q) counts[q * 256 + t] = 0;
-  if (t != 0) return;
-  // one epoch counter for every sort of the context: tags never repeat across sorts
-  meta[kMetaEpoch] = ++ds->sort_epoch;
-  int q = 0;
-  for (int p = 0; p < npasses; ++p) {
-    const int shift = begin_bit + 8 * p;
-    const int bits = end_bit - shift < 8 ? end_bit - shift : 8;
-    const unsigned long long dmask = (1ull << bits) - 1;
-    const bool active = diff_mask ? (((*diff_mask >> shift) & dmask) != 0) : true;
-    if (active) meta[q++] = (unsigned)shift | ((unsigned)bits << 16);
+    for (int c = 0; c < kOsParts; ++c) sum += parts[(c * kOsDigits + p) * 256 + t];
+    counts[q * 256 + t] = sum;
   }
-  for (int r = q; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
-  for (int r = 0; r < kOsMaxPasses; ++r) {
-    meta[kMetaSrc + r] = (unsigned)(r & 1);
-    meta[kMetaTile + r] = 0;
-  }
-  meta[31] = (unsigned)(q & 1);
+  for (int c = 0; c < kOsParts; ++c)
+    for (int p = 0; p < kOsDigits; ++p) parts[(c * kOsDigits + p) * 256 + t] = 0;
 }
 
 __device__ inline int64_t os_count(int64_t n, const uint32_t* n_dev) {
@@ -61,31 +85,35 @@ __device__ inline int64_t os_count(int64_t n, const uint32_t* n_dev) {
   return m < n ? m : n;
 }
 
+// digit counts of every 8-bit position of the keys into parts[blockIdx % kOsParts]
 template <typename K>
 __global__ __launch_bounds__(kOsNT) void k_os_hist(const K* __restrict__ keys, int64_t n0,
-                                                   const uint32_t* n_dev,
-                                                   const unsigned int* meta, uint32_t* counts) {
-  __shared__ uint32_t lc[kOsMaxPasses][256];
-  __shared__ unsigned sm[kOsMaxPasses];
+                                                   const uint32_t* n_dev, int begin_bit,
+                                                   int npasses, uint32_t* parts) {
+  __shared__ uint32_t lc[kOsDigits][256];
   const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < kOsMaxPasses; ++q) lc[q][t] = 0;
-  if (t < kOsMaxPasses) sm[t] = meta[t];
+  for (int p = 0; p < kOsDigits; ++p) lc[p][t] = 0;
   __syncthreads();
-  int nq = 0;
-  while (nq < kOsMaxPasses && sm[nq] != kOsNone) ++nq;
   const int64_t n = os_count(n0, n_dev);
-  for (int64_t i = (int64_t)blockIdx.x * kOsNT + t; i < n; i += (int64_t)gridDim.x * kOsNT) {
-    const K k = keys[i];
-    for (int q = 0; q < nq; ++q) {
-      const unsigned m = sm[q];
-      const uint32_t d = (uint32_t)(k >> (m & 0xFFFFu)) & ((1u << (m >> 16)) - 1u);
-      atomicAdd(&lc[q][d], 1u);
+  const int64_t base = (int64_t)blockIdx.x * kOsTile;
+  K k[kOsItems];
+#pragma unroll
+  for (int i = 0; i < kOsItems; ++i) {
+    const int64_t idx = base + (int64_t)i * kOsNT + t;
+    k[i] = idx < n ? keys[idx] : (K)0;
+  }
+#pragma unroll
+  for (int i = 0; i < kOsItems; ++i) {
+    if (base + (int64_t)i * kOsNT + t < n) {
+      for (int p = 0; p < npasses; ++p)
+        atomicAdd(&lc[p][(uint32_t)(k[i] >> (begin_bit + 8 * p)) & 255u], 1u);
     }
   }
   __syncthreads();
-  for (int q = 0; q < nq; ++q)
-    if (lc[q][t]) atomicAdd(&counts[q * 256 + t], lc[q][t]);
+  uint32_t* dst = parts + (size_t)(blockIdx.x % kOsParts) * kOsDigits * 256;
+  for (int p = 0; p < npasses; ++p)
+    if (lc[p][t]) atomicAdd(&dst[p * 256 + t], lc[p][t]);
 }
 
 __device__ inline unsigned long long os_word(uint32_t tag, uint32_t flag, uint32_t v) {
@@ -101,8 +129,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   const unsigned m = meta[q];
   if (m == kOsNone) return;
   const int shift = (int)(m & 0xFFFFu);
-  const uint32_t dmask = (1u << (m >> 16)) - 1u;
   const int bits = (int)(m >> 16);
+  const uint32_t dmask = (1u << bits) - 1u;
   const bool from1 = meta[kMetaSrc + q] != 0;
   const K* kin = from1 ? k1 : k0;
   const P* vin = from1 ? v1 : v0;
@@ -110,8 +138,10 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   P* vout = from1 ? v0 : v1;
   const uint32_t tag = (meta[kMetaEpoch] * kOsMaxPasses + (unsigned)q) & 0x3FFFFFFFu;
 
-  __shared__ K lk[kOsTile];
-  __shared__ P lv[kOsTile];
+  constexpr int kBuf = sizeof(K) > sizeof(P) ? sizeof(K) : sizeof(P);
+  __shared__ __attribute__((aligned(16))) unsigned char lbuf[kOsTile * kBuf];
+  K* lk = reinterpret_cast<K*>(lbuf);
+  P* lv = reinterpret_cast<P*>(lbuf);
   __shared__ uint32_t wcnt[kOsWaves][256];
   __shared__ uint32_t gdig[256], lstart[256];
   __shared__ uint32_t lds[kOsNT / kWave + 1];
@@ -128,17 +158,15 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   const int64_t tbase = tile * kOsTile;
   if (tbase >= n) return;  // every later tile exits too: no waiter is left behind
 
-  // ---- load (wave w owns a contiguous 64*kOsItems run) and rank with ballots
+  // ---- keys (wave w owns a contiguous 64*kOsItems run); rank with ballots.  dr packs the
+  // digit (bits 0-7) and the rank among the wave's items of that digit (bits 8-19).
   K key[kOsItems];
-  P val[kOsItems];
-  uint32_t rank[kOsItems], dig[kOsItems];
+  uint32_t dr[kOsItems];
   const int64_t wbase = tbase + (int64_t)w * kWave * kOsItems;
 #pragma unroll
   for (int c = 0; c < kOsItems; ++c) {
     const int64_t idx = wbase + c * kWave + l;
-    const bool valid = idx < n;
-    key[c] = valid ? kin[idx] : (K)0;
-    val[c] = valid ? vin[idx] : (P)0;
+    key[c] = idx < n ? kin[idx] : (K)0;
   }
 #pragma unroll
   for (int c = 0; c < kOsItems; ++c) {
@@ -157,8 +185,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
     __builtin_amdgcn_wave_barrier();
     if (valid && r == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
     __builtin_amdgcn_wave_barrier();
-    rank[c] = old + r;
-    dig[c] = d;
+    dr[c] = d | ((old + r) << 8);
   }
   __syncthreads();
   // ---- per-digit tile count; waves' exclusive offsets within the digit
@@ -178,21 +205,35 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
     __hip_atomic_store(st, os_word(tag, 1u, cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int64_t k = tile - 1;
     uint32_t spins = 0;
-    while (k >= 0) {
-      const unsigned long long v = __hip_atomic_load(status + k * 256 + t, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t hi = (uint32_t)(v >> 32);
-      if ((hi >> 2) != tag || (hi & 3u) == 0) {
-        if (++spins > (1u << 26)) {  // a predecessor never published: give up loudly
+    bool done = false;
+    while (!done) {
+      unsigned long long v[kOsLookback];
+#pragma unroll
+      for (int i = 0; i < kOsLookback; ++i)
+        v[i] = (k - i >= 0) ? __hip_atomic_load(status + (k - i) * 256 + t, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : 0ull;
+      bool stalled = false;
+#pragma unroll
+      for (int i = 0; i < kOsLookback; ++i) {
+        if (done || stalled || k < 0) continue;
+        const uint32_t hi = (uint32_t)(v[i] >> 32);
+        if ((hi >> 2) != tag || (hi & 3u) == 0) {
+          stalled = true;  // not published yet: retry from tile k
+          continue;
+        }
+        pre += (uint32_t)v[i];
+        --k;
+        if ((hi & 3u) == 2u) done = true;
+      }
+      if (k < 0) done = true;
+      if (stalled && !done) {
+        if (++spins > (1u << 24)) {  // a predecessor never published: give up loudly
           atomicOr(&ds->err, kErrSort);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        continue;
       }
-      pre += (uint32_t)v;
-      if ((hi & 3u) == 2u) break;
-      --k;
     }
     __hip_atomic_store(st, os_word(tag, 2u, pre + cnt), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -202,28 +243,41 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   gdig[t] = gb + pre;
   lstart[t] = block_excl_scan<kOsNT>(cnt, lds, nullptr);
   __syncthreads();
-  // ---- tile-local stable sort through LDS, then stores in digit runs
+  // ---- keys: tile-local stable order through LDS, then stores in digit runs
+  const int64_t nvalid = (n - tbase) < kOsTile ? (n - tbase) : kOsTile;
 #pragma unroll
   for (int c = 0; c < kOsItems; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     if (idx < n) {
-      const uint32_t li = lstart[dig[c]] + wcnt[w][dig[c]] + rank[c];
-      lk[li] = key[c];
-      lv[li] = val[c];
+      const uint32_t d = dr[c] & 255u;
+      dr[c] = lstart[d] + wcnt[w][d] + (dr[c] >> 8);  // now the tile-local sorted index
+      lk[dr[c]] = key[c];
     }
   }
   __syncthreads();
-  const int64_t nvalid = (n - tbase) < kOsTile ? (n - tbase) : kOsTile;
+  uint32_t opos[kOsItems];
 #pragma unroll
   for (int i = 0; i < kOsItems; ++i) {
     const int qi = i * kOsNT + t;
     if (qi < nvalid) {
       const K kk = lk[qi];
       const uint32_t d = (uint32_t)(kk >> shift) & dmask;
-      const uint32_t pos = gdig[d] + ((uint32_t)qi - lstart[d]);
-      kout[pos] = kk;
-      vout[pos] = lv[qi];
+      opos[i] = gdig[d] + ((uint32_t)qi - lstart[d]);
+      kout[opos[i]] = kk;
     }
+  }
+  __syncthreads();
+  // ---- payloads: the same permutation through the same LDS buffer
+#pragma unroll
+  for (int c = 0; c < kOsItems; ++c) {
+    const int64_t idx = wbase + c * kWave + l;
+    if (idx < n) lv[dr[c]] = vin[idx];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kOsItems; ++i) {
+    const int qi = i * kOsNT + t;
+    if (qi < nvalid) vout[opos[i]] = lv[qi];
   }
 }
 
@@ -232,7 +286,7 @@ int Workspace::os_reserve(int64_t ntiles) {
   void* before = os.p;
   const size_t want = kOsCountBytes + (size_t)ntiles * 256 * sizeof(unsigned long long);
   DFX_TRY(os.ensure(want));
-  if (os.p != before) DFX_HIP(hipMemset(os.p, 0, os.bytes));  // no stale look-back words
+  if (os.p != before) DFX_HIP(hipMemset(os.p, 0, os.bytes));  // zero parts, no stale words
   os_tiles = ntiles;
   return DFX_OK;
 }
@@ -240,24 +294,26 @@ int Workspace::os_reserve(int64_t ntiles) {
 template <typename K, typename P>
 int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
-                     const uint32_t* n_dev) {
+                     const uint32_t* n_dev, int flags) {
+  const int64_t ntiles = n > 0 ? (n + kOsTile - 1) / kOsTile : 1;
+  DFX_TRY(c->ws.os_reserve(ntiles));
+  uint32_t* parts = c->ws.os_parts();
+  uint32_t* counts = c->ws.os_counts();
+  const int or_and = (flags & kSortDiffIsOrAnd) ? 1 : 0;
   if (n <= 0 || end_bit <= begin_bit) {
-    DFX_TRY(c->ws.os_reserve(1));
-    hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, 0, begin_bit,
-                       end_bit, sortmeta, c->ws.os_counts(), c->ds);
+    hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, or_and, 0,
+                       begin_bit, end_bit, sortmeta, parts, counts, c->ds);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
   const int npasses = (end_bit - begin_bit + 7) / 8;
-  const int64_t ntiles = (n + kOsTile - 1) / kOsTile;
-  DFX_TRY(c->ws.os_reserve(ntiles));
-  uint32_t* counts = c->ws.os_counts();
   unsigned long long* status = c->ws.os_status();
-  hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, npasses,
-                     begin_bit, end_bit, sortmeta, counts, c->ds);
-  const int64_t hblocks = ntiles < 1024 ? ntiles : 1024;
-  hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)hblocks), dim3(kOsNT), 0, c->stream, k0, n,
-                     n_dev, sortmeta, counts);
+  if (!(flags & kSortCountsReady)) {
+    hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)ntiles), dim3(kOsNT), 0, c->stream, k0, n,
+                       n_dev, begin_bit, npasses, parts);
+  }
+  hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, or_and, npasses,
+                     begin_bit, end_bit, sortmeta, parts, counts, c->ds);
   for (int q = 0; q < npasses; ++q) {
     hipLaunchKernelGGL((k_os_scatter<K, P>), dim3((unsigned)ntiles), dim3(kOsNT), 0, c->stream,
                        k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, c->ds);
@@ -266,9 +322,10 @@ int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begi
   return DFX_OK;
 }
 
-#define DFX_SORT_INST(K, P)                                                                  \
-  template int radix_sort_pairs<K, P>(Context*, K*, P*, K*, P*, int64_t, int, int,           \
-                                      const unsigned long long*, unsigned int*, const uint32_t*);
+#define DFX_SORT_INST(K, P)                                                                 \
+  template int radix_sort_pairs<K, P>(Context*, K*, P*, K*, P*, int64_t, int, int,          \
+                                      const unsigned long long*, unsigned int*,             \
+                                      const uint32_t*, int);
 DFX_SORT_INST(uint64_t, uint32_t)
 DFX_SORT_INST(uint64_t, uint64_t)
 DFX_SORT_INST(uint32_t, uint32_t)
