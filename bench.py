@@ -151,17 +151,32 @@ def main():
         H.check(lib.dfx_train_step(ctx.h, ctypes.byref(b), H.kTraining, int(push_cnt),
                                    ctypes.c_uint64(H.MAX_INDEX), None))
 
+    # Batches come from a loader stream (as a reader's host->device copies would): the
+    # library's Localizer lane waits only for that stream, so it overlaps the previous batch's
+    # forward / backward on the context stream.  Batches stay referenced until a sync point.
+    loader = torch.cuda.Stream(device=dev)
+    if not os.environ.get("DFX_SERIAL"):
+        ctx.set_input_stream(loader)
+
+    def make(seed):
+        with torch.cuda.stream(loader):
+            return DevBatch(torch, dev, B, k, kb, seed=seed)
+
     # untimed epoch 0: touch the key space with count pushes (all keys end up with V)
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (B * k)))
+    live = []
     for i in range(n_warm_epoch):
-        step(DevBatch(torch, dev, B, k, kb, seed=1_000_000 * (rank + 1) + i), True)
+        live.append(make(1_000_000 * (rank + 1) + i))
+        step(live[-1], True)
     torch.cuda.synchronize()
+    live.clear()
     H.progress(ctx)
     for i in range(args.warmup):
-        step(DevBatch(torch, dev, B, k, kb, seed=2_000_000 * (rank + 1) + i), False)
-    batches = [DevBatch(torch, dev, B, k, kb, seed=3_000_000 * (rank + 1) + i)
-               for i in range(args.steps)]
+        live.append(make(2_000_000 * (rank + 1) + i))
+        step(live[-1], False)
+    batches = [make(3_000_000 * (rank + 1) + i) for i in range(args.steps)]
     torch.cuda.synchronize()
+    live.clear()
     H.prof_read(ctx)
     H.progress(ctx)
     H.prof_enable(ctx, args.steps)
@@ -172,6 +187,7 @@ def main():
     t0 = time.perf_counter()
     for bt in batches:
         step(bt, False)
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -182,6 +198,7 @@ def main():
         elapsed = float(t.item())
 
     phases, nrec, mean_u = H.prof_read(ctx)
+    lanes = H.prof_lanes(ctx)
     prog = H.progress(ctx)
     ctx.sync()
     st = H.Store(ctx).stats()
@@ -215,6 +232,8 @@ def main():
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
+        "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+        "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
         "train_loss_per_row": round(prog["loss"] / max(prog["nrows"], 1), 6),
         "train_auc": round(prog["auc"] / max(prog["nrows"], 1), 6),

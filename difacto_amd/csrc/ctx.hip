@@ -45,6 +45,7 @@ struct Kw {
   long long max_keys = 1ll << 22;
   long long max_vrows = -1;
   int loss_fm = 1;
+  int ordered = 1;
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -75,6 +76,11 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "seed") kw->seed = (unsigned)strtoul(cv, nullptr, 10);
     else if (k == "max_keys") kw->max_keys = atoll(cv);
     else if (k == "max_vrows") kw->max_vrows = atoll(cv);
+    else if (k == "hash") {
+      if (v == "ordered") kw->ordered = 1;
+      else if (v == "mixed") kw->ordered = 0;
+      else { set_error("unknown hash: " + v + " (ordered|mixed)"); return DFX_ERR_ARG; }
+    }
     else if (k == "loss") {
       if (v == "fm") kw->loss_fm = 1;
       else if (v == "logit") kw->loss_fm = 0;
@@ -92,6 +98,38 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
 // store allocation: table capacity = next pow2 >= 2*n_keys (load factor <= 0.5)
 int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows);
 void table_release(Context* c);
+
+static void release_ws(Workspace& w) {
+  DevBuf* bufs[] = {&w.keys0, &w.keys1, &w.vals0, &w.vals1, &w.rowid, &w.hist, &w.tiles,
+                    &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
+                    &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
+                    &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1, &w.atiles,
+                    &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted};
+  for (DevBuf* b : bufs) b->release();
+}
+
+// streams, events and lane states of the fused step's pipeline, created on first use
+int pipeline_init(Context* c) {
+  if (c->loc_stream) return DFX_OK;
+  // the side lanes run latency-bound chains of small launches beside a full-occupancy
+  // backward: give them priority so their workgroups are not queued behind its tail
+  int lo = 0, hi = 0;
+  DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  const char* lp = getenv("DFX_LOC_PRIO");  // experiment: 0 low, 1 high, else normal
+  int locp = lp ? (atoi(lp) == 0 ? lo : (atoi(lp) == 1 ? hi : 0)) : hi;
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, locp));
+  const char* ap = getenv("DFX_AUX_PRIO");  // experiment: 0 low, 1 high, else normal
+  int auxp = ap ? (atoi(ap) == 0 ? lo : (atoi(ap) == 1 ? hi : 0)) : hi;
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, auxp));
+  for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
+                        &c->ev_free[0], &c->ev_free[1]})
+    DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads}) {
+    DFX_HIP(hipMalloc(d, sizeof(DevState)));
+    DFX_HIP(hipMemset(*d, 0, sizeof(DevState)));
+  }
+  return DFX_OK;
+}
 
 }  // namespace dfx
 
@@ -138,6 +176,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   init.seed = kw.seed;
   (void)hipMemcpy(c->ds, &init, sizeof(init), hipMemcpyHostToDevice);
   int64_t vrows = kw.max_vrows >= 0 ? kw.max_vrows : (c->P.V_dim > 0 ? kw.max_keys : 0);
+  c->T.ordered = kw.ordered;
+  c->T.probe_flag = &c->ds->probe_flag;
   int rc = table_alloc(c, kw.max_keys, vrows);
   if (rc != DFX_OK) {
     dfx_ctx_destroy(ctx);
@@ -152,21 +192,19 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   Context* c = &ctx->c;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
-  Workspace& w = c->ws;
-  DevBuf* bufs[] = {&w.keys0, &w.keys1, &w.vals0, &w.vals1, &w.rowid, &w.hist, &w.tiles,
-                    &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
-                    &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv};
-  for (DevBuf* b : bufs) b->release();
-  w.occ_row.release();
-  w.occ_x.release();
-  w.ak0.release();
-  w.ak1.release();
-  w.av0.release();
-  w.av1.release();
-  w.atiles.release();
-  for (DevBuf* b : {&w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted})
-    b->release();
+  release_ws(c->ws);
+  release_ws(c->bws[0]);
+  release_ws(c->bws[1]);
+  release_ws(c->aws);
+  for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_loc[0], c->ev_loc[1],
+                       c->ev_free[0], c->ev_free[1]})
+    if (e) (void)hipEventDestroy(e);
+  for (DevState* d : {c->bds[0], c->bds[1], c->ads})
+    if (d) (void)hipFree(d);
+  if (c->loc_stream) (void)hipStreamDestroy(c->loc_stream);
+  if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
   table_release(c);
   if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
@@ -182,6 +220,13 @@ int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream) {
   return DFX_OK;
 }
 
+int dfx_ctx_set_input_stream(dfx_ctx* ctx, void* hip_stream) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  ctx->c.in_stream = static_cast<hipStream_t>(hip_stream);
+  ctx->c.has_in_stream = hip_stream != nullptr;
+  return DFX_OK;
+}
+
 int dfx_ctx_use_own_stream(dfx_ctx* ctx) {
   DFX_CHECK_ARG(ctx, "null ctx");
   ctx->c.stream = ctx->c.own_stream;
@@ -193,9 +238,12 @@ int dfx_ctx_vdim(dfx_ctx* ctx) { return ctx ? ctx->c.P.V_dim : -1; }
 int dfx_sync(dfx_ctx* ctx) {
   DFX_CHECK_ARG(ctx, "null ctx");
   Context* c = &ctx->c;
+  // the AUC lane runs behind the context stream: join it first
+  if (c->ev_auc) DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   int err = 0;
   DFX_HIP(hipMemcpyAsync(&err, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
+  if (!err) DFX_TRY(table_unclump(c));
   if (err) {
     (void)hipMemsetAsync(&c->ds->err, 0, sizeof(int), c->stream);
     (void)hipStreamSynchronize(c->stream);
@@ -236,13 +284,14 @@ int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind)
 
 int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz) {
   DFX_CHECK_ARG(ctx, "null ctx");
-  return ws_reserve(&ctx->c, max_rows, max_nnz);
+  return step_reserve(&ctx->c, max_rows, max_nnz);
 }
 
 int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset) {
   DFX_CHECK_ARG(ctx && out, "null argument");
   Context* c = &ctx->c;
   double prog[5];
+  if (c->ev_auc) DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   DFX_HIP(hipMemcpyAsync(prog, c->ds->prog, sizeof(prog), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   out->nrows = prog[0];

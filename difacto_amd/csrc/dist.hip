@@ -423,7 +423,7 @@ static int owner_initv(Context* c, int nranks) {
   int bits = 0;
   while ((1 << bits) < nranks) ++bits;
   // stable by rank; the tail (0xFF) sorts last and is never read
-  DFX_TRY(radix_sort_pairs<uint32_t>(c, rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
+  DFX_TRY(radix_sort_pairs<uint32_t>(main_lane(c), rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
                                      c->ds->sortmeta));
   hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, c->stream, rv0, rv1, ftotal,
                      ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds);
@@ -459,6 +459,7 @@ int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* b, uint64_t max_index, int 
   Workspace& ws = c->ws;
   const int64_t B = b->size, nnz = b->nnz;
   DFX_TRY(ws_reserve(c, B, nnz));
+  DFX_TRY(loc_reserve(ws, nnz));
   DFX_TRY(ws.oflags.ensure(kMaxRanks * 8));
   LocOut o;
   o.uniq = keys_out;
@@ -468,7 +469,7 @@ int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* b, uint64_t max_index, int 
   o.value = b->value;
   o.occ_row = ws.occ_row.as<uint32_t>();
   o.occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
-  DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, o));
+  DFX_TRY(localize_run(c, main_lane(c), B, nnz, b->offset, b->index, max_index, o));
   uint32_t u = 0;
   DFX_HIP(hipMemcpyAsync(&u, &c->ds->u_count, 4, hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
@@ -520,7 +521,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* b, const float* pulled, int 
   int nblk = 0;
   DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
-  DFX_TRY(auc_run(c, B, b->label, pred, &c->ds->auc_n));
+  DFX_TRY(auc_run(main_lane(c), B, b->label, pred, &c->ds->auc_n));
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {
     DFX_HIP(hipMemsetAsync(grads_out, 0, (size_t)U * S * 4, c->stream));

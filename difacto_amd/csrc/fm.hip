@@ -116,7 +116,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           // the key's table entry: {w, vrow} in one 8-byte load (or handed over by the
           // Localizer's probe); V is visible only if present and not (l1_shrk && w == 0)
           // (SGDUpdater::Get, sgd_updater.cc:40-43)
-          if (!a.wv) wr[t] = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
+          if (a.wv_rank) {
+            wr[t] = a.wv_rank[c[t]];
+          } else if (!a.wv) {
+            wr[t] = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
+          }
           w[t] = __int_as_float(wr[t].x);
           const int vr = wr[t].y;
           vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
@@ -608,7 +612,7 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   uint32_t* k1 = ws.keys1.as<uint32_t>();
   hipLaunchKernelGGL(k_csc_prep, dim3((B + 255) / 256), dim3(256), 0, c->stream, B, offset, col,
                      k0, ws.vals0.as<uint32_t>(), ws.rowid.as<uint32_t>());
-  DFX_TRY(radix_sort_pairs<uint32_t>(c, k0, ws.vals0.as<uint32_t>(), k1,
+  DFX_TRY(radix_sort_pairs<uint32_t>(main_lane(c), k0, ws.vals0.as<uint32_t>(), k1,
                                      ws.vals1.as<uint32_t>(), nnz, 0, get_nbits(n_cols),
                                      nullptr, c->ds->sortmeta));
   uint32_t* flags = ws.flags.as<uint32_t>();

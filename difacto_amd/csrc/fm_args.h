@@ -8,7 +8,8 @@ struct FwdArgs {
   int64_t B;
   const uint64_t* offs;
   const uint32_t* col;   // remapped column, or (fused) the nnz's model-table slot
-  const int2* wv;        // fused without a count push: the nnz's {w, vrow} (col unused)
+  const int2* wv;        // the nnz's {w, vrow} (col unused)
+  const int2* wv_rank;   // {w, vrow} per key rank, reached through col (the Pull's output)
   const float* val;
   // fused: the model table itself (SGDUpdater::Get semantics, l1_shrk from P);
   // standalone: interleaved weights addressed by positions

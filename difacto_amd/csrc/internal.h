@@ -58,10 +58,10 @@ struct DevState {
   unsigned long long diff_mask;
   unsigned int u_count;        // U of the current batch
   unsigned int n_init;         // InitV count of the current phase
-  unsigned int sortmeta[32];   // per-pass {active, src} + final selector (Localizer sort)
-  unsigned int sortmeta2[32];  // the same for the AUC sort
+  unsigned int sortmeta[32];   // radix sort plan + final buffer selector (sort.hip)
   unsigned int totals[8];      // scan totals of the current step
   unsigned int sort_epoch;     // radix sorts launched (tags their look-back words)
+  int probe_flag;              // Table::probe_flag (long insert probes: keys cluster)
   double auc_n;                // AUC * n of the current step
   double sum_u;                // sum of U over dfx_train_step calls (roofline bytes)
   double n_steps;
@@ -101,6 +101,19 @@ struct Workspace {
   int64_t rows = 0, nnz = 0;
 };
 
+struct Context;
+
+// A lane = a stream with its own scratch and its own small device state (U of its batch, sort
+// plan and look-back epoch), so work on two lanes never shares a buffer.  The main lane is the
+// context's stream + ws + ds; the fused step adds a Localizer lane per batch parity and an AUC
+// lane (step.hip).  err: the context's device error word.
+struct Lane {
+  hipStream_t stream;
+  Workspace* ws;
+  DevState* ds;
+  int* err;
+};
+
 struct Context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -115,17 +128,36 @@ struct Context {
   Workspace ws;
   // per-phase HIP-event timing of dfx_train_step (dfx_prof_*); events on c->stream
   std::vector<hipEvent_t> prof_ev;  // prof_max steps x kProfMarks
+  std::vector<hipEvent_t> lane_ev;  // prof_max steps x 4: loc start/end, AUC start/end
+  double lane_stats[4] = {0, 0, 0, 0};
   int prof_max = 0, prof_n = 0;
   // sharded store (dist.hip): keys received by this owner in the current step and each
   // source rank's offset among them; rows and unique keys of this worker's batch
   int64_t dist_R = 0, dist_rows = 0, dist_U = 0;
   std::vector<int64_t> dist_offs;
+  // fused-step pipelining (step.hip): batch t+1's Localizer runs on loc_stream while the main
+  // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
+  hipStream_t loc_stream = nullptr, aux_stream = nullptr;
+  hipStream_t in_stream = nullptr;  // where batches are produced (dfx_ctx_set_input_stream)
+  bool has_in_stream = false;
+  Workspace bws[2];
+  DevState* bds[2] = {nullptr, nullptr};
+  Workspace aws;
+  DevState* ads = nullptr;
+  hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
+  hipEvent_t ev_loc[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  int parity = 0;
 };
+
+inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }
 
 // masked gathers read zpad + ((index & 255) << 4) + [0, 1024): 256 spread 64-byte lines
 constexpr int kZpadFloats = 256 * 16 + 1024;
 
 constexpr int kProfMarks = 8;  // start, localize, feacnt, pull, fwd, auc, bwd, initv/end
+inline void lane_mark(Context* c, int m, hipStream_t st) {
+  if (c->prof_n < c->prof_max) (void)hipEventRecord(c->lane_ev[(size_t)c->prof_n * 4 + m], st);
+}
 inline void prof_mark(Context* c, int m) {
   if (c->prof_n < c->prof_max)
     (void)hipEventRecord(c->prof_ev[(size_t)c->prof_n * kProfMarks + m], c->stream);
@@ -142,7 +174,7 @@ inline void prof_mark(Context* c, int m) {
 // 8-bit digit position into ws.os_parts()[block % kOsParts] (begin_bit must be 0).
 constexpr int kSortDiffIsOrAnd = 1, kSortCountsReady = 2;
 template <typename K, typename P>
-int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
+int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
                      const uint32_t* n_dev = nullptr, int flags = 0);
 
@@ -152,43 +184,51 @@ int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
              const uint32_t* n_dev = nullptr);
 
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
-void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);
+void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);
 
-// Localizer::Compact on the device (localize.hip).  Leaves in the workspace the sorted
-// (key, payload) pairs (buffer selected by ds->sortmeta[31]) and U in ds->u_count.  Writes
-// uniq[U], col[nnz], and optionally cnt[U] and segstart[U+1].  With occ_row (and occ_x when
-// value != NULL) it also writes every occurrence's row (and value) in sorted order, for the
-// backward walk.  With segslot (fused step) every nnz's key is found-or-inserted in the model
-// table and segslot[U] receives each unique key's slot (uniq / col may then be NULL); per nnz
-// in input order it hands the forward either wv[nnz] = the key's {w, vrow} (no count push
-// before the forward) or nslot[nnz] = its slot.
+// Localizer::Compact on the device (localize.hip), on lane L.  Leaves in L's workspace the
+// sorted (key, {pos, row}) pairs (buffer selected by L.ds->sortmeta[31]) and U in
+// L.ds->u_count.  Writes uniq[U] and col[nnz] when given (col_heads: col[pos] = rank with bit
+// 31 set on each key's first occurrence in sorted order), and optionally cnt[U] and
+// segstart[U+1].  With occ_row (and occ_x when value != NULL) it also writes every
+// occurrence's row (and value) in sorted order, for the backward walk.  No model access.
 struct LocOut {
   uint64_t* uniq = nullptr;
   float* cnt = nullptr;
   uint32_t* col = nullptr;
+  bool col_heads = false;
   uint32_t* segstart = nullptr;
   const float* value = nullptr;
   uint32_t* occ_row = nullptr;
   float* occ_x = nullptr;
-  uint32_t* segslot = nullptr;
-  int2* wv = nullptr;
-  uint32_t* nslot = nullptr;
 };
-int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
+int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o);
 
 int ws_reserve(Context* c, int64_t rows, int64_t nnz);
+int pipeline_init(Context* c);
+// rehash with the multiplicative hash if inserts reported clustered keys (store.hip);
+// synchronises the context stream
+int table_unclump(Context* c);
+int step_reserve(Context* c, int64_t rows, int64_t nnz);  // ws_reserve + the step's lanes
+int loc_reserve(Workspace& w, int64_t nnz);              // a Localizer's buffers
 
 // store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
+// nds: the device state whose u_count holds the count when n_host < 0
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot);
-// fused Update(kFeaCount): one segment per unique key (count = segment length)
+              const uint32_t* slot, const DevState* nds = nullptr);
+// fused Update(kFeaCount): one segment per unique key (count = segment length = nds->u_count)
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
-                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev);
+                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,
+                     const DevState* nds);
 int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
-int auc_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
+int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev);
+// the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream
+int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
+                 const float* pred);
+int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

@@ -1,17 +1,14 @@
 // Localizer::Compact on gfx950 (src/data/localizer.cc:11-107).
 //
-//   1. k_loc_transform: key = ReverseBytes(id % max_index) and a 64-bit payload per nnz, plus
-//      the OR/AND of all keys so the radix sort skips digits that never vary (uniform 2^24 ids
-//      reverse into 24 high bits).  In the fused step it also finds-or-inserts every nnz's key
-//      in the model table (SGDUpdater::Get's model_[key]) and hands the forward pass the key's
-//      {w, V row} directly — the entry line the probe brought in — or, when a count push must
-//      run first, the slot.  Probes of several nnz are issued together (latency-bound loop).
+//   1. k_loc_transform: key = ReverseBytes(id % max_index), payload {pos, row} per nnz, the
+//      OR/AND of all keys so the radix sort skips digits that never vary (uniform 2^24 ids
+//      reverse into 24 high bits), and the digit counts of the sort.  No model access: the
+//      fused step runs the Localizer of the next batch beside this batch's backward.
 //   2. stable LSD radix sort of (key, payload)                          (localizer.cc:26-27)
-//   3. run heads -> tile counts -> scan -> per unique key (rank): uniq, segment start, slot;
+//   3. run heads -> tile counts -> scan -> per unique key (rank): uniq, segment start;
 //      per nnz: col[pos] = rank (CountUniqIndex's run-length pass + RemapIndex's merge-join,
-//      localizer.cc:31-107); per occurrence in sorted order: its row (and value), which the
-//      backward pass walks.  What a consumer needs travels in the payload, so the write pass
-//      reads sorted data only (no random gathers on binary data).
+//      localizer.cc:31-107), optionally flagged on the key's first occurrence; per occurrence
+//      in sorted order: its row (and value), which the backward pass walks.
 // Every index of the block is in its own dictionary, so the compacted block keeps all nnz:
 // its offsets/values/labels are the input's and only `col` is new.  Bit-exact by
 // construction (ranks depend only on keys).
@@ -21,37 +18,25 @@ namespace dfx {
 
 constexpr int kLocNT = 256;
 constexpr int kLocRows = 64;   // rows per transform block
-constexpr int kLocUnr = 4;     // probes in flight per thread
 constexpr int kLocItems = 8;
 constexpr int kLocTile = kLocNT * kLocItems;
 
-// payload layouts (lo32 | hi32 << 32)
-enum LocMode : int {
-  kLocPlain = 0,     // lo = pos, hi = row               (dfx_localize, sharded worker)
-  kLocFusedBin = 1,  // lo = row, hi = table slot        (binary data: no value to fetch)
-  kLocFusedVal = 2,  // lo = pos, hi = table slot        (+ rowid[pos], value[pos] gathers)
-};
-
+// payload of every nnz: lo32 = its position, hi32 = its row — what the write pass needs
+// travels through the sort, so it reads sorted data only (no gathers on binary data)
 struct TransformArgs {
-  uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
   int64_t B;
   const uint64_t* offset;
   const uint64_t* index;
   uint64_t max_index;
   uint64_t* keys;
   uint64_t* pay;
-  uint32_t* rowid;  // fused valued: row of each nnz
-  Table T;
-  int2* wv;         // fused, no count push: {w, vrow} of each nnz's key
-  uint32_t* nslot;  // fused with a count push: each nnz's slot
-  DevState* ds;
+  uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
+  DevState* ds;     // the lane's state: OR / AND of the keys
 };
 
-template <int MODE>
 __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
   __shared__ uint64_t offs[kLocRows + 1];
   __shared__ unsigned long long red_or[kLocNT / kWave], red_and[kLocNT / kWave];
-  __shared__ int red_ins[kLocNT / kWave];
   __shared__ uint32_t hist[kOsDigits][256];  // digit counts for the sort (no extra key read)
 #pragma unroll
   for (int p = 0; p < kOsDigits; ++p) hist[p][threadIdx.x] = 0;
@@ -61,96 +46,52 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
   __syncthreads();
   const uint64_t j0 = offs[0], j1 = offs[nr];
   unsigned long long vor = 0, vand = ~0ull;
-  int ins = 0;
-  for (uint64_t jb = j0 + threadIdx.x; jb < j1; jb += (uint64_t)kLocNT * kLocUnr) {
-    uint64_t key[kLocUnr], h[kLocUnr];
-    bool ok[kLocUnr];
+  for (uint64_t j = j0 + threadIdx.x; j < j1; j += kLocNT) {
+    const uint64_t id = a.index[j];
+    const uint64_t m = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+    const uint64_t k = reverse_bytes(m);
+    vor |= k;
+    vand &= k;
+    // digit counts; a digit the whole wave shares (every constant digit) costs one atomic
 #pragma unroll
-    for (int u = 0; u < kLocUnr; ++u) {
-      const uint64_t j = jb + (uint64_t)u * kLocNT;
-      ok[u] = j < j1;
-      const uint64_t id = ok[u] ? a.index[j] : 0ull;
-      const uint64_t m =
-          a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-      key[u] = reverse_bytes(m);
-    }
-    // probe the home slots of all items at once: key and {w, vrow} share the entry's line
-    unsigned long long kk[kLocUnr];
-    int2 wr[kLocUnr];
-    if (MODE != kLocPlain) {
-#pragma unroll
-      for (int u = 0; u < kLocUnr; ++u) {
-        h[u] = tbl_hash(key[u], a.T.logcap);
-        kk[u] = a.T.ent[h[u]].key;
-        wr[u] = *reinterpret_cast<const int2*>(a.T.ent + h[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kLocUnr; ++u) {
-      if (!ok[u]) continue;
-      const uint64_t j = jb + (uint64_t)u * kLocNT;
-      const uint64_t k = key[u];
-      vor |= k;
-      vand &= k;
-#pragma unroll
-      for (int p = 0; p < kOsDigits; ++p) atomicAdd(&hist[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
-      // row = upper_bound(j) - 1 over the block's offsets (empty rows skipped)
-      int lo = 0, hi = nr;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (offs[mid] <= j) lo = mid; else hi = mid;
-      }
-      const int row = (int)(r0 + lo);
-      if (MODE == kLocPlain) {
-        a.keys[j] = k;
-        a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)row << 32);
-        continue;
-      }
-      int64_t s;
-      if (kk[u] == k) {
-        s = (int64_t)h[u];
+    for (int p = 0; p < kOsDigits; ++p) {
+      const uint32_t dg = (uint32_t)(k >> (8 * p)) & 255u;
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(dg);
+      const uint64_t same = __ballot(dg == d0);
+      if (same == __ballot(true)) {
+        if (lane_id() == (int)__builtin_amdgcn_readfirstlane(lane_id()))
+          atomicAdd(&hist[p][d0], (uint32_t)__popcll(same));
       } else {
-        // model_[key] (sgd_updater.cc:37): duplicates of one key resolve to one slot via CAS
-        bool inserted;
-        s = tbl_insert(a.T, k, &inserted);
-        if (s < 0) {
-          atomicOr(&a.ds->err, kErrTableFull);
-          s = 0;
-        }
-        ins += inserted ? 1 : 0;
-        wr[u] = *reinterpret_cast<const int2*>(a.T.ent + s);
+        atomicAdd(&hist[p][dg], 1u);
       }
-      a.keys[j] = k;
-      const uint32_t lo32 = MODE == kLocFusedBin ? (uint32_t)row : (uint32_t)j;
-      a.pay[j] = (uint64_t)lo32 | ((uint64_t)(uint32_t)s << 32);
-      if (MODE == kLocFusedVal) a.rowid[j] = (uint32_t)row;
-      if (a.wv) a.wv[j] = wr[u];
-      if (a.nslot) a.nslot[j] = (uint32_t)s;
     }
+    // row = upper_bound(j) - 1 over the block's offsets (empty rows skipped)
+    int lo = 0, hi = nr;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offs[mid] <= j) lo = mid; else hi = mid;
+    }
+    a.keys[j] = k;
+    a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32);
   }
   for (int off = 32; off > 0; off >>= 1) {
     vor |= __shfl_xor(vor, off, kWave);
     vand &= __shfl_xor(vand, off, kWave);
-    ins += __shfl_xor(ins, off, kWave);
   }
   if (lane_id() == 0) {
     red_or[threadIdx.x / kWave] = vor;
     red_and[threadIdx.x / kWave] = vand;
-    red_ins[threadIdx.x / kWave] = ins;
   }
   __syncthreads();
   if (threadIdx.x == 0 && j1 > j0) {
     vor = red_or[0];
     vand = red_and[0];
-    ins = red_ins[0];
     for (int w = 1; w < kLocNT / kWave; ++w) {
       vor |= red_or[w];
       vand &= red_and[w];
-      ins += red_ins[w];
     }
     atomicOr(&a.ds->or_mask, vor);
     atomicAnd(&a.ds->and_mask, vand);
-    if (ins) atomicAdd(&a.ds->n_keys, (unsigned long long)ins);
   }
   uint32_t* dst = a.parts + (size_t)(blockIdx.x % kOsParts) * kOsDigits * 256;
 #pragma unroll
@@ -191,15 +132,13 @@ struct LocWriteArgs {
   const uint32_t* tilebase;
   uint64_t* uniq;
   uint32_t* col;
+  int col_heads;     // col[pos] = rank | (pos is its segment's head) << 31
   uint32_t* segstart;
-  const uint32_t* rowid;
   const float* value;
   uint32_t* occ_row;
   float* occ_x;
-  uint32_t* segslot;
 };
 
-template <int MODE>
 __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   const bool s1 = a.ds->sortmeta[31] != 0;
@@ -230,9 +169,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
       if (h[i]) {
         if (a.uniq) a.uniq[rank] = k[i];
         if (a.segstart) a.segstart[rank] = (uint32_t)idx;
-        if (MODE != kLocPlain) a.segslot[rank] = (uint32_t)(P[idx] >> 32);
       }
-      if (MODE == kLocPlain && a.col) a.col[(uint32_t)P[idx]] = rank;
+      if (a.col) a.col[(uint32_t)P[idx]] = rank | (a.col_heads && h[i] ? 0x80000000u : 0u);
       if (idx == n - 1) {
         a.ds->u_count = rank + 1;
         if (a.segstart) a.segstart[rank + 1] = (uint32_t)n;
@@ -247,15 +185,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
       const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
       if (idx < n) {
         const uint64_t p = P[idx];
-        const uint32_t lo = (uint32_t)p;
-        if (MODE == kLocPlain) {
-          a.occ_row[idx] = (uint32_t)(p >> 32);
-        } else if (MODE == kLocFusedBin) {
-          a.occ_row[idx] = lo;
-        } else {
-          a.occ_row[idx] = a.rowid[lo];
-        }
-        if (MODE != kLocFusedBin && a.occ_x) a.occ_x[idx] = a.value[lo];
+        a.occ_row[idx] = (uint32_t)(p >> 32);
+        if (a.occ_x) a.occ_x[idx] = a.value[(uint32_t)p];
       }
     }
   }
@@ -269,24 +200,22 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
-int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
+int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o) {
-  Workspace& ws = c->ws;
+  Workspace& ws = *L.ws;
+  DevState* ds = L.ds;
   DFX_CHECK_ARG(max_index != 0, "localize: max_index must be > 0");
   DFX_CHECK_ARG(nnz < (int64_t)0xFFFFFFFFll, "localize: nnz must fit u32 (localizer.cc:16)");
   if (B <= 0 || nnz <= 0) {
-    hipLaunchKernelGGL(k_set_u, dim3(1), dim3(1), 0, c->stream, c->ds, 0u);
-    if (o.segstart) DFX_HIP(hipMemsetAsync(o.segstart, 0, sizeof(uint32_t), c->stream));
+    hipLaunchKernelGGL(k_set_u, dim3(1), dim3(1), 0, L.stream, ds, 0u);
+    if (o.segstart) DFX_HIP(hipMemsetAsync(o.segstart, 0, sizeof(uint32_t), L.stream));
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
-  const bool fused = o.segslot != nullptr;
-  const int mode = !fused ? kLocPlain : (o.value ? kLocFusedVal : kLocFusedBin);
   DFX_TRY(ws.keys0.ensure(nnz * 8));
   DFX_TRY(ws.keys1.ensure(nnz * 8));
   DFX_TRY(ws.vals0.ensure(nnz * 8));
   DFX_TRY(ws.vals1.ensure(nnz * 8));
-  if (mode == kLocFusedVal) DFX_TRY(ws.rowid.ensure(nnz * 4));
   uint32_t* segs = o.segstart;
   if (o.cnt && !segs) {
     DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
@@ -297,47 +226,30 @@ int localize_run(Context* c, int64_t B, int64_t nnz, const uint64_t* offset,
   uint64_t* p0 = ws.vals0.as<uint64_t>();
   uint64_t* p1 = ws.vals1.as<uint64_t>();
   DFX_TRY(ws.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
-  hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, c->stream, c->ds);
+  hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, L.stream, ds);
   TransformArgs t{};
-  t.parts = ws.os_parts();
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
-  t.keys = k0; t.pay = p0; t.rowid = ws.rowid.as<uint32_t>(); t.T = c->T;
-  t.wv = o.wv; t.nslot = o.nslot; t.ds = c->ds;
-  const dim3 tg((unsigned)((B + kLocRows - 1) / kLocRows));
-  if (mode == kLocPlain) {
-    hipLaunchKernelGGL(k_loc_transform<kLocPlain>, tg, dim3(kLocNT), 0, c->stream, t);
-  } else if (mode == kLocFusedBin) {
-    hipLaunchKernelGGL(k_loc_transform<kLocFusedBin>, tg, dim3(kLocNT), 0, c->stream, t);
-  } else {
-    hipLaunchKernelGGL(k_loc_transform<kLocFusedVal>, tg, dim3(kLocNT), 0, c->stream, t);
-  }
+  t.keys = k0; t.pay = p0; t.parts = ws.os_parts(); t.ds = ds;
+  hipLaunchKernelGGL(k_loc_transform, dim3((unsigned)((B + kLocRows - 1) / kLocRows)),
+                     dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits
-  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(c, k0, p0, k1, p1, nnz, 0, 64, &c->ds->or_mask,
-                                                c->ds->sortmeta, nullptr,
+  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
+                                                ds->sortmeta, nullptr,
                                                 kSortDiffIsOrAnd | kSortCountsReady)));
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = ws.tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, c->stream, k0, k1, nnz, c->ds,
-                     ts);
-  scan_tiles_top(c, ts, ntiles, nullptr);
+  hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, L.stream, k0, k1, nnz, ds, ts);
+  scan_tiles_top(L, ts, ntiles, nullptr);
   LocWriteArgs a{};
   a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1;
-  a.n = nnz; a.ds = c->ds; a.tilebase = ts;
-  a.uniq = o.uniq; a.col = o.col; a.segstart = segs;
-  a.rowid = ws.rowid.as<uint32_t>();
+  a.n = nnz; a.ds = ds; a.tilebase = ts;
+  a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
-  a.segslot = o.segslot;
-  if (mode == kLocPlain) {
-    hipLaunchKernelGGL(k_loc_write<kLocPlain>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
-  } else if (mode == kLocFusedBin) {
-    hipLaunchKernelGGL(k_loc_write<kLocFusedBin>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
-  } else {
-    hipLaunchKernelGGL(k_loc_write<kLocFusedVal>, dim3(ntiles), dim3(kLocNT), 0, c->stream, a);
-  }
+  hipLaunchKernelGGL(k_loc_write, dim3(ntiles), dim3(kLocNT), 0, L.stream, a);
   if (o.cnt) {
-    hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, c->stream, c->ds, segs,
+    hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, L.stream, ds, segs,
                        o.cnt, nnz);
   }
   DFX_HIP(hipGetLastError());
@@ -359,7 +271,7 @@ extern "C" int dfx_localize(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint64_t
   o.uniq = uniq;
   o.cnt = cnt;
   o.col = col;
-  DFX_TRY(localize_run(c, B, nnz, offset, index, max_index, o));
+  DFX_TRY(localize_run(c, main_lane(c), B, nnz, offset, index, max_index, o));
   if (n_uniq) {
     unsigned u = 0;
     DFX_HIP(hipMemcpyAsync(&u, &c->ds->u_count, sizeof(unsigned), hipMemcpyDeviceToHost,

@@ -39,13 +39,13 @@ constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = 24;
 __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff, int or_and,
                                                    int npasses, int begin_bit, int end_bit,
                                                    unsigned int* meta, uint32_t* parts,
-                                                   uint32_t* counts, DevState* ds) {
+                                                   uint32_t* counts, unsigned int* epoch) {
   __shared__ int s_pos[kOsMaxPasses];
   __shared__ int s_nq;
   const int t = threadIdx.x;
   if (t == 0) {
-    // one epoch counter for every sort of the context: tags never repeat across sorts
-    meta[kMetaEpoch] = ++ds->sort_epoch;
+    // one epoch counter per lane (which owns the look-back words): tags never repeat
+    meta[kMetaEpoch] = ++*epoch;
     unsigned long long dm = ~0ull;
     if (diff) dm = or_and ? (diff[0] ^ diff[1]) : diff[0];
     int q = 0;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
                                                       const uint32_t* n_dev, unsigned int* meta,
                                                       int q, const uint32_t* counts,
                                                       unsigned long long* status,
-                                                      DevState* ds) {
+                                                      int* err) {
   const unsigned m = meta[q];
   if (m == kOsNone) return;
   const int shift = (int)(m & 0xFFFFu);
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
       if (k < 0) done = true;
       if (stalled && !done) {
         if (++spins > (1u << 24)) {  // a predecessor never published: give up loudly
-          atomicOr(&ds->err, kErrSort);
+          atomicOr(err, kErrSort);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -292,38 +292,40 @@ int Workspace::os_reserve(int64_t ntiles) {
 }
 
 template <typename K, typename P>
-int radix_sort_pairs(Context* c, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
+int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
                      const uint32_t* n_dev, int flags) {
+  Workspace& ws = *L.ws;
   const int64_t ntiles = n > 0 ? (n + kOsTile - 1) / kOsTile : 1;
-  DFX_TRY(c->ws.os_reserve(ntiles));
-  uint32_t* parts = c->ws.os_parts();
-  uint32_t* counts = c->ws.os_counts();
+  DFX_TRY(ws.os_reserve(ntiles));
+  uint32_t* parts = ws.os_parts();
+  uint32_t* counts = ws.os_counts();
+  unsigned int* epoch = &L.ds->sort_epoch;
   const int or_and = (flags & kSortDiffIsOrAnd) ? 1 : 0;
   if (n <= 0 || end_bit <= begin_bit) {
-    hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, or_and, 0,
-                       begin_bit, end_bit, sortmeta, parts, counts, c->ds);
+    hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, 0,
+                       begin_bit, end_bit, sortmeta, parts, counts, epoch);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
   const int npasses = (end_bit - begin_bit + 7) / 8;
-  unsigned long long* status = c->ws.os_status();
+  unsigned long long* status = ws.os_status();
   if (!(flags & kSortCountsReady)) {
-    hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)ntiles), dim3(kOsNT), 0, c->stream, k0, n,
+    hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)ntiles), dim3(kOsNT), 0, L.stream, k0, n,
                        n_dev, begin_bit, npasses, parts);
   }
-  hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, c->stream, diff_mask, or_and, npasses,
-                     begin_bit, end_bit, sortmeta, parts, counts, c->ds);
+  hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
+                     begin_bit, end_bit, sortmeta, parts, counts, epoch);
   for (int q = 0; q < npasses; ++q) {
-    hipLaunchKernelGGL((k_os_scatter<K, P>), dim3((unsigned)ntiles), dim3(kOsNT), 0, c->stream,
-                       k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, c->ds);
+    hipLaunchKernelGGL((k_os_scatter<K, P>), dim3((unsigned)ntiles), dim3(kOsNT), 0, L.stream,
+                       k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
 #define DFX_SORT_INST(K, P)                                                                 \
-  template int radix_sort_pairs<K, P>(Context*, K*, P*, K*, P*, int64_t, int, int,          \
+  template int radix_sort_pairs<K, P>(const Lane&, K*, P*, K*, P*, int64_t, int, int,       \
                                       const unsigned long long*, unsigned int*,             \
                                       const uint32_t*, int);
 DFX_SORT_INST(uint64_t, uint32_t)
@@ -394,8 +396,8 @@ __global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t 
   }
 }
 
-void scan_tiles_top(Context* c, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev) {
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, tilesum, ntiles, total_dev);
+void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev) {
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, tilesum, ntiles, total_dev);
 }
 
 int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,

@@ -22,96 +22,219 @@ void sum_parts(Context* c, const double* part, int64_t n, double* out, bool accu
 
 namespace dfx {
 
+// main lane: per-row arrays of the forward / backward and the InitV scan
 int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   Workspace& ws = c->ws;
   const int d = c->P.V_dim;
   if (rows < 1) rows = 1;
   if (nnz < 1) nnz = 1;
-  const int64_t ntiles = (nnz + 2047) / 2048;
-  DFX_TRY(ws.keys0.ensure(nnz * 8));
-  DFX_TRY(ws.keys1.ensure(nnz * 8));
-  DFX_TRY(ws.vals0.ensure(nnz * 8));
-  DFX_TRY(ws.vals1.ensure(nnz * 8));
-  DFX_TRY(ws.wv.ensure(nnz * 8));
-  DFX_TRY(ws.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
-  DFX_TRY(ws.rowid.ensure(nnz * 4));
-  DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
-  DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
-  DFX_TRY(ws.col.ensure(nnz * 4));
-  DFX_TRY(ws.slot.ensure((nnz + 1) * 4));
   DFX_TRY(ws.flags.ensure((nnz + 1) * 4));
-  DFX_TRY(ws.occ_row.ensure(nnz * 4));
-  DFX_TRY(ws.occ_x.ensure(nnz * 4));
+  DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
   DFX_TRY(ws.p.ensure(rows * 4));
   DFX_TRY(ws.pred.ensure(rows * 4));
   if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * d * 4));
   DFX_TRY(ws.dscratch.ensure((rows / 4 + 64) * 8));
-  DFX_TRY(ws.ak0.ensure(rows * 4));
-  DFX_TRY(ws.ak1.ensure(rows * 4));
-  DFX_TRY(ws.av0.ensure(rows * 4));
-  DFX_TRY(ws.av1.ensure(rows * 4));
-  const int64_t at = (rows + 2047) / 2048;
-  DFX_TRY(ws.atiles.ensure(at * 4 + at * 8 + 64));
+  DFX_TRY(ws.wv.ensure(nnz * 8));
+  DFX_TRY(ws.col.ensure(nnz * 4));
   ws.rows = rows;
   ws.nnz = nnz;
   return DFX_OK;
 }
 
-__global__ void k_step_finalize(DevState* ds, int64_t B, int train) {
-  // sgd::Progress: nrows, loss, auc (sgd_learner.cc:213-229)
-  ds->prog[0] += (double)B;
-  ds->prog[1] += ds->scratch[3];
-  ds->prog[2] += ds->auc_n;
-  ds->sum_u += (double)ds->u_count;
-  ds->n_steps += 1;
-  (void)train;
+// a Localizer lane: its sort buffers and per-nnz / per-key outputs
+int loc_reserve(Workspace& w, int64_t nnz) {
+  if (nnz < 1) nnz = 1;
+  DFX_TRY(w.keys0.ensure(nnz * 8));
+  DFX_TRY(w.keys1.ensure(nnz * 8));
+  DFX_TRY(w.vals0.ensure(nnz * 8));
+  DFX_TRY(w.vals1.ensure(nnz * 8));
+  DFX_TRY(w.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
+  DFX_TRY(w.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
+  DFX_TRY(w.segstart.ensure((nnz + 1) * 4));
+  DFX_TRY(w.col.ensure(nnz * 4));
+  DFX_TRY(w.uniq.ensure(nnz * 8));
+  DFX_TRY(w.slot.ensure((nnz + 1) * 4));
+  DFX_TRY(w.occ_row.ensure(nnz * 4));
+  DFX_TRY(w.occ_x.ensure(nnz * 4));
+  w.nnz = nnz;
+  return DFX_OK;
 }
 
+// the AUC lane (metric.hip auc_finish: sorted tiles of 4096, their positive prefixes, the
+// per-tile and per-pair partial sums)
+static int auc_reserve(Workspace& w, int64_t rows) {
+  if (rows < 1) rows = 1;
+  const int64_t nt = (rows + 4095) / 4096;
+  const int64_t nb2 = (rows * nt + 255) / 256;
+  DFX_TRY(w.ak0.ensure(rows * 4));
+  DFX_TRY(w.ak1.ensure(rows * 4));
+  DFX_TRY(w.av0.ensure(rows * 4));
+  DFX_TRY(w.av1.ensure((size_t)nt * 4097 * 4));
+  DFX_TRY(w.atiles.ensure(nt * 12 + nb2 * 8 + 64));
+  w.rows = rows;
+  return DFX_OK;
+}
+
+int step_reserve(Context* c, int64_t rows, int64_t nnz) {
+  DFX_TRY(pipeline_init(c));
+  DFX_TRY(ws_reserve(c, rows, nnz));
+  DFX_TRY(loc_reserve(c->bws[0], nnz));
+  DFX_TRY(loc_reserve(c->bws[1], nnz));
+  return auc_reserve(c->aws, rows);
+}
+
+// SGDUpdater::Get (sgd_updater.cc:34-58) over the batch's sorted unique keys, as the
+// reference's Pull does: find-or-insert each key (model_[key]), record its slot for the
+// backward and its {w, vrow} for the forward (pulled[rank]; the forward reaches it through
+// col).  In a count-push step the slots come first and the pull follows the push's InitV.
+// Keys arrive in sorted order; kProbeUnr home slots are read at once (latency-bound loop).
+constexpr int kProbeNT = 256, kProbeUnr = 4;
+__global__ __launch_bounds__(kProbeNT) void k_probe_keys(const uint64_t* __restrict__ uniq,
+                                                         const DevState* nds, Table T,
+                                                         int2* __restrict__ pulled,
+                                                         uint32_t* __restrict__ segslot,
+                                                         DevState* ds) {
+  __shared__ int red[kProbeNT / kWave];
+  const int64_t n = (int64_t)nds->u_count;
+  const int64_t ub = (int64_t)blockIdx.x * kProbeNT * kProbeUnr + threadIdx.x;
+  uint64_t key[kProbeUnr], h[kProbeUnr];
+  unsigned long long kk[kProbeUnr];
+  int2 wr[kProbeUnr];
+  int ins = 0;
+#pragma unroll
+  for (int v = 0; v < kProbeUnr; ++v) {
+    const int64_t u = ub + (int64_t)v * kProbeNT;
+    key[v] = u < n ? uniq[u] : 0ull;
+    h[v] = tbl_hash(key[v], T);
+  }
+#pragma unroll
+  for (int v = 0; v < kProbeUnr; ++v) {
+    const int64_t u = ub + (int64_t)v * kProbeNT;
+    if (u < n) {
+      kk[v] = T.ent[h[v]].key;
+      wr[v] = *reinterpret_cast<const int2*>(T.ent + h[v]);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < kProbeUnr; ++v) {
+    const int64_t u = ub + (int64_t)v * kProbeNT;
+    if (u >= n) continue;
+    int64_t s = (int64_t)h[v];
+    if (kk[v] != key[v]) {
+      bool inserted;
+      s = tbl_insert(T, key[v], &inserted);
+      if (s < 0) {
+        atomicOr(&ds->err, kErrTableFull);
+        s = 0;
+      }
+      ins += inserted ? 1 : 0;
+      wr[v] = *reinterpret_cast<const int2*>(T.ent + s);
+    }
+    segslot[u] = (uint32_t)s;
+    if (pulled) pulled[u] = wr[v];
+  }
+  for (int off = 32; off > 0; off >>= 1) ins += __shfl_xor(ins, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = ins;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < kProbeNT / kWave; ++i) t += red[i];
+    if (t) atomicAdd(&ds->n_keys, (unsigned long long)t);
+  }
+}
+
+// the pull after a count push: {w, vrow} of each unique key by slot
+__global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ segslot,
+                                                   const DevState* nds, const Entry* ent,
+                                                   int2* __restrict__ pulled) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u < (int64_t)nds->u_count) pulled[u] = *reinterpret_cast<const int2*>(ent + segslot[u]);
+}
+
+__global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B) {
+  // sgd::Progress: nrows, loss (sgd_learner.cc:213-229); the AUC lane adds its own
+  ds->prog[0] += (double)B;
+  ds->prog[1] += ds->scratch[3];
+  ds->sum_u += (double)bds->u_count;
+  ds->n_steps += 1;
+}
+
+// One minibatch, pipelined over three streams:
+//   loc lane   Localizer (transform + find-or-insert, sort, segments) of this batch.  It needs
+//              only the batch and the key -> slot map, which the backward never changes
+//              (inserts only claim empty slots; the backward writes values), so it runs while
+//              the main stream is still on the previous batch's forward / backward.  Its
+//              buffers alternate between two sets (parity), each reused only after the main
+//              stream finished the batch that used it before.
+//   main       [count push] -> forward -> backward + FTRL/AdaGrad -> InitV: reads the model
+//              strictly after the previous batch's update, so results equal the sequential
+//              schedule exactly (SGDLearner::IterateData with StoreLocal).
+//   aux lane   AUC of a snapshot of (pred, label) taken on the main stream, beside the
+//              backward; it adds into the progress itself and is joined by the next step's
+//              snapshot (and by dfx_progress_read / dfx_sync).
 int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint64_t max_index,
                float* pred_out) {
   const int64_t B = b->size, nnz = b->nnz;
   const int d = c->P.V_dim;
+  DFX_TRY(step_reserve(c, B, nnz));
   Workspace& ws = c->ws;
-  DFX_TRY(ws_reserve(c, B, nnz));
-  uint32_t* segstart = ws.segstart.as<uint32_t>();
-  uint32_t* nslot = ws.col.as<uint32_t>();   // per nnz: model-table slot of its key
-  uint32_t* segslot = ws.slot.as<uint32_t>();  // per unique key (sorted): its slot
+  const int k = c->parity;
+  c->parity ^= 1;
+  Workspace& bw = c->bws[k];
+  DevState* bds = c->bds[k];
+  const Lane LL{c->loc_stream, &bw, bds, &c->ds->err};
+  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  uint32_t* segstart = bw.segstart.as<uint32_t>();
+  uint32_t* col = bw.col.as<uint32_t>();       // per nnz: the rank of its key
+  uint64_t* uniq = bw.uniq.as<uint64_t>();     // per rank: the key
+  uint32_t* segslot = bw.slot.as<uint32_t>();  // per rank: its model-table slot
+  int2* pulled = ws.wv.as<int2>();             // per rank: {w, vrow} (the Pull)
+  uint32_t* occ_row = bw.occ_row.as<uint32_t>();
+  float* occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
   uint32_t* flags = ws.flags.as<uint32_t>();
   uint32_t* total = &c->ds->totals[0];
   float* pred = pred_out ? pred_out : ws.pred.as<float>();
-  uint32_t* occ_row = ws.occ_row.as<uint32_t>();
-  float* occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
 
-  prof_mark(c, 0);
-  // Localizer::Compact + the pull's key resolution: each nnz's key is found-or-inserted in
-  // the model table (Get's model_[key], sgd_updater.cc:37); segments come out in sorted key
-  // order, which is the order Update walks keys in (InitV draws) and the (row, nnz) order of
-  // every key's gradient sum.
-  // Without a count push nothing changes the table between this probe and the forward, so
-  // the probe hands each nnz's {w, vrow} straight to it; a count push (epoch 0) may InitV
-  // first, so the forward then re-reads the entry by slot.
-  const bool cnt_first = push_cnt && d > 0;
+  // ---- loc lane: the batch is ready on the caller's stream; this parity's buffers are free
+  // once the main stream finished the batch that used them before
+  DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_in, 0));
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[k], 0));
+  // Localizer::Compact: sorted unique keys (segments in key order, the order Update walks
+  // keys in — InitV draws — and, per key, the (row, nnz) order of its gradient sums)
   LocOut o;
   o.segstart = segstart;
   o.value = b->value;
   o.occ_row = occ_row;
   o.occ_x = occ_x;
-  o.segslot = segslot;
-  if (cnt_first) {
-    o.nslot = nslot;
-  } else {
-    o.wv = ws.wv.as<int2>();
-  }
-  DFX_TRY(localize_run(c, B, nnz, b->offset, b->index, max_index, o));
+  o.col = col;
+  o.uniq = uniq;
+  lane_mark(c, 0, c->loc_stream);
+  DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+  lane_mark(c, 1, c->loc_stream);
+  DFX_HIP(hipEventRecord(c->ev_loc[k], c->loc_stream));
+
+  // ---- main: wait for this batch's Localizer (the exposed part of it is the "localize" phase)
+  prof_mark(c, 0);
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_loc[k], 0));
   prof_mark(c, 1);
-  if (cnt_first) DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total));
+  // Get over the sorted unique keys (find-or-insert + pull); a count push goes in between
+  const bool cnt_first = push_cnt && d > 0;
+  const dim3 ug((unsigned)((nnz + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
+  if (nnz > 0)
+    hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, c->stream, uniq, bds, c->T,
+                       cnt_first ? nullptr : pulled, segslot, c->ds);
   prof_mark(c, 2);
-  prof_mark(c, 3);  // the pull is the forward's direct read of each key's table entry
+  if (cnt_first) {
+    DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total, bds));
+    hipLaunchKernelGGL(k_pull_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
+                       c->stream, segslot, bds, c->T.ent, pulled);
+  }
+  prof_mark(c, 3);
 
   FwdArgs a{};
-  a.B = B; a.offs = b->offset; a.col = nslot; a.wv = cnt_first ? nullptr : ws.wv.as<int2>();
-  a.val = b->value; a.T = c->T;
-  a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
+  a.B = B; a.offs = b->offset; a.col = col; a.wv_rank = pulled; a.val = b->value;
+  a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>();
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -119,23 +242,33 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk));
   prof_mark(c, 4);
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
-  DFX_TRY(auc_run(c, B, b->label, pred, &c->ds->auc_n));
+
+  // ---- aux lane: AUC of this batch's predictions, beside the backward.  The snapshot (on
+  // this stream) waits for the previous AUC to release the lane's buffers.
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+  DFX_TRY(auc_snapshot(AL, c->stream, B, b->label, pred));
+  DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
+  lane_mark(c, 2, c->aux_stream);
+  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true));
+  lane_mark(c, 3, c->aux_stream);
+  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   prof_mark(c, 5);
 
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
     BwdArgs g{};
-    g.segstart = segstart; g.ds = c->ds; g.nseg_host = -1; g.segcol = nullptr;
+    g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.d = d; g.slot = segslot; g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
     prof_mark(c, 6);
-    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot));
+    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds));
   } else {
     prof_mark(c, 6);
   }
-  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B,
-                     job_type == DFX_JOB_TRAINING);
+  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, bds, B);
+  DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
   prof_mark(c, 7);
   if (c->prof_n < c->prof_max) ++c->prof_n;
   DFX_HIP(hipGetLastError());
@@ -166,14 +299,26 @@ extern "C" int dfx_prof_enable(dfx_ctx* ctx, int max_steps) {
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   c->prof_ev.assign((size_t)max_steps * kProfMarks, nullptr);
   for (auto& e : c->prof_ev) DFX_HIP(hipEventCreate(&e));
+  for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
+  c->lane_ev.assign((size_t)max_steps * 4, nullptr);
+  for (auto& e : c->lane_ev) DFX_HIP(hipEventCreate(&e));
   c->prof_max = max_steps;
   c->prof_n = 0;
   return DFX_OK;
 }
 
-// ms[7]: summed milliseconds of localize, feacnt, pull, forward, auc+eval, backward+update,
-// initv+finalize over the recorded steps; *n_steps their count; *mean_u the mean U per step
+// ms[7]: summed milliseconds of localize (wait), probe+pull, feacnt, forward, eval + AUC
+// snapshot, backward+update, initv+finalize over the recorded steps; *n_steps their count; *mean_u the mean U per step
 // over all dfx_train_step calls since the last read.  Resets the recording.
+// after dfx_prof_read: out[4] = mean ms of the Localizer lane per batch, of its start after
+// the context stream reached that batch (negative: it ran ahead), of its end after that point
+// (positive: the exposed wait), and of the AUC lane
+extern "C" int dfx_prof_lanes(dfx_ctx* ctx, double* out) {
+  DFX_CHECK_ARG(ctx && out, "bad argument");
+  for (int i = 0; i < 4; ++i) out[i] = ctx->c.lane_stats[i];
+  return DFX_OK;
+}
+
 extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u) {
   DFX_CHECK_ARG(ctx && ms, "bad argument");
   Context* c = &ctx->c;
@@ -186,6 +331,21 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
                                   c->prof_ev[(size_t)s * kProfMarks + m + 1]));
       ms[m] += t;
     }
+  }
+  // lanes: mean Localizer-lane time, its start relative to the main stream's wait for it,
+  // the main stream's wait past its end, mean AUC-lane time
+  for (double& v : c->lane_stats) v = 0;
+  if (c->loc_stream) DFX_HIP(hipStreamSynchronize(c->loc_stream));
+  if (c->aux_stream) DFX_HIP(hipStreamSynchronize(c->aux_stream));
+  for (int s = 0; s < c->prof_n && !c->lane_ev.empty(); ++s) {
+    hipEvent_t* L = &c->lane_ev[(size_t)s * 4];
+    hipEvent_t* M = &c->prof_ev[(size_t)s * kProfMarks];
+    float t[4] = {0, 0, 0, 0};
+    DFX_HIP(hipEventElapsedTime(&t[0], L[0], L[1]));
+    DFX_HIP(hipEventElapsedTime(&t[1], M[0], L[0]));
+    DFX_HIP(hipEventElapsedTime(&t[2], M[0], L[1]));
+    DFX_HIP(hipEventElapsedTime(&t[3], L[2], L[3]));
+    for (int i = 0; i < 4; ++i) c->lane_stats[i] += t[i] / c->prof_n;
   }
   if (n_steps) *n_steps = c->prof_n;
   c->prof_n = 0;

@@ -47,9 +47,10 @@ __device__ inline int64_t count_of(int64_t n_host, const DevState* ds) {
 // each flagged key.
 __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t* excl,
                                                  const uint32_t* total, const uint32_t* slot,
-                                                 Table T, float scale, DevState* ds) {
+                                                 Table T, float scale, DevState* ds,
+                                                 const DevState* nds) {
   const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
-  const int64_t n = count_of(n_host, ds);
+  const int64_t n = count_of(n_host, nds);
   if (u >= n) return;
   const uint32_t e = excl[u];
   const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
@@ -79,11 +80,12 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot) {
+              const uint32_t* slot, const DevState* nds) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
-  DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &c->ds->u_count));
+  if (!nds) nds = c->ds;
+  DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count));
   hipLaunchKernelGGL(k_initv, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
-                     n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds);
+                     n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds);
   hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
                      c->T.vcap, c->ds);
   DFX_HIP(hipGetLastError());
@@ -134,12 +136,13 @@ __global__ __launch_bounds__(kStNT) void k_push_cnt_seg(const uint32_t* segstart
 }
 
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
-                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev) {
+                     const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,
+                     const DevState* nds) {
   if (n_bound <= 0) return DFX_OK;
   hipLaunchKernelGGL(k_push_cnt_seg, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0,
-                     c->stream, segstart, segslot, c->T, c->P, flags, c->ds);
+                     c->stream, segstart, segslot, c->T, c->P, flags, nds);
   DFX_HIP(hipGetLastError());
-  return run_initv(c, -1, n_bound, flags, total_dev, segslot);
+  return run_initv(c, -1, n_bound, flags, total_dev, segslot, nds);
 }
 
 // ---- standalone Get: interleaved [w | V] + lens ---------------------------------------------
@@ -267,6 +270,29 @@ static int table_alloc_entries(Table* T, int64_t cap, hipStream_t st) {
   return DFX_OK;
 }
 
+int table_unclump(Context* c) {
+  Table& T = c->T;
+  if (!T.ent) return DFX_OK;
+  int flag = 0;
+  DFX_HIP(hipMemcpyAsync(&flag, &c->ds->probe_flag, sizeof(int), hipMemcpyDeviceToHost,
+                         c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  if (!flag) return DFX_OK;
+  DFX_HIP(hipMemsetAsync(&c->ds->probe_flag, 0, sizeof(int), c->stream));
+  if (!T.ordered) return DFX_OK;
+  // the keys cluster in their top bits: rebuild with the multiplicative hash (same capacity)
+  Table NT = T;
+  NT.ordered = 0;
+  DFX_TRY(table_alloc_entries(&NT, c->cap, c->stream));
+  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
+                     c->cap, NT, c->ds);
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  (void)hipFree(T.ent);
+  T.ent = NT.ent;
+  T.ordered = 0;
+  return DFX_OK;
+}
+
 int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
   if (n_keys < 1024) n_keys = 1024;
   int64_t cap = 1;
@@ -308,6 +334,7 @@ static int read_counters(Context* c, HostCounters* h) {
 int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
   DFX_HIP(hipStreamSynchronize(c->stream));
   Table& T = c->T;
+  DFX_TRY(table_unclump(c));
   if (2 * n_keys > c->cap) {
     int64_t cap = c->cap;
     while (cap < 2 * n_keys) cap <<= 1;
@@ -529,7 +556,7 @@ int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has
   const Table& T = c->T;
   DFX_HIP(hipStreamSynchronize(c->stream));
   // host-side probe of the same hash sequence (test hook; not a hot path)
-  uint64_t h = tbl_hash(key, T.logcap);
+  uint64_t h = tbl_hash(key, T);
   *found = 0;
   for (uint64_t probe = 0; probe <= T.mask; ++probe) {
     Entry e;

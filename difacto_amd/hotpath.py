@@ -56,6 +56,11 @@ class Context:
         s = torch.cuda.current_stream(self.device)
         check(_lib.lib().dfx_ctx_set_stream(self.h, ctypes.c_void_p(s.cuda_stream)))
 
+    def set_input_stream(self, stream):
+        """batches of train_step are produced on this torch stream (None: the context's)"""
+        check(_lib.lib().dfx_ctx_set_input_stream(
+            self.h, None if stream is None else ctypes.c_void_p(stream.cuda_stream)))
+
     def close(self):
         if getattr(self, "h", None):
             _lib.lib().dfx_ctx_destroy(self.h)
@@ -244,7 +249,9 @@ def train_step(ctx, dblk, job_type=kTraining, push_cnt=False, max_index=MAX_INDE
                                     ctypes.c_uint64(max_index), _p(pred)))
 
 
-PHASES = ("localize", "feacnt", "pull", "forward", "eval_auc", "backward_update", "initv")
+# main-stream phases of dfx_train_step (the Localizer runs on its own lane; "localize" is
+# the part of it the main stream waits for)
+PHASES = ("localize", "probe_pull", "feacnt", "forward", "eval_auc", "backward_update", "initv")
 
 
 def prof_enable(ctx, max_steps):
@@ -258,6 +265,14 @@ def prof_read(ctx):
     mu = ctypes.c_double(0)
     check(_lib.lib().dfx_prof_read(ctx.h, ms, ctypes.byref(n), ctypes.byref(mu)))
     return dict(zip(PHASES, list(ms))), n.value, mu.value
+
+
+def prof_lanes(ctx):
+    """after prof_read: mean ms per batch of the Localizer lane, its start / end relative to
+    the main stream reaching the batch, and the AUC lane"""
+    out = (ctypes.c_double * 4)()
+    check(_lib.lib().dfx_prof_lanes(ctx.h, out))
+    return dict(zip(("loc_ms", "loc_start_rel_ms", "loc_end_rel_ms", "auc_ms"), list(out)))
 
 
 def progress(ctx, reset=True):

@@ -88,6 +88,11 @@ int dfx_ctx_destroy(dfx_ctx* ctx);
  * hipStream_t (NULL = the null stream, torch's default); use_own_stream switches back. */
 int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream);
 int dfx_ctx_use_own_stream(dfx_ctx* ctx);
+/* The stream on which dfx_train_step's batches are produced (a loader / copy stream; NULL =
+ * the context stream).  A batch's Localizer waits only for that stream, so it can run while
+ * the context stream is still on the previous batch's forward / backward.  The caller keeps a
+ * batch's buffers alive until the context stream has passed the dfx_train_step that took it. */
+int dfx_ctx_set_input_stream(dfx_ctx* ctx, void* hip_stream);
 int dfx_ctx_vdim(dfx_ctx* ctx);
 int dfx_sync(dfx_ctx* ctx); /* waits for the stream and reports deferred device errors */
 int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes);
@@ -159,11 +164,16 @@ int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset);
 
 /* ---- measurement ------------------------------------------------------------------------
  * HIP events on the context stream around each phase of dfx_train_step, for up to
- * max_steps calls.  dfx_prof_read returns summed ms[7] = {localize, feacnt push, pull,
- * forward, evaluate+AUC, backward+update, InitV+finalize}, the number of recorded steps,
+ * max_steps calls.  dfx_prof_read returns summed ms[7] = {localize (the part of the
+ * Localizer lane the context stream waits for), probe + pull, feacnt push, forward,
+ * evaluate + AUC snapshot, backward+update, InitV+finalize}, the number of recorded steps,
  * and the mean unique-key count U per step (for algorithmic-byte accounting); it resets. */
 int dfx_prof_enable(dfx_ctx* ctx, int max_steps);
 int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
+/* after dfx_prof_read: out[4] = mean ms per batch of the Localizer lane, of its start and of its
+ * end relative to the context stream reaching that batch (start < 0: it ran ahead; end > 0:
+ * the exposed wait), and of the AUC lane */
+int dfx_prof_lanes(dfx_ctx* ctx, double* out);
 
 /* ---- key-range-sharded store over N GPUs (KVStoreDist, src/store/kvstore_dist.h) --------
  * Every rank is a worker (its own batch) and the server of the keys with

@@ -401,3 +401,28 @@ def test_fused_async_batches_released(H):
     assert abs(p["loss"] - tot) <= 1e-4 * tot
     s = H.Store(c).stats()
     assert s["seed"] == up.seed and s["n_keys"] == up.size()
+
+
+@pytest.mark.parametrize("hash_kind", ["ordered", "mixed"])
+def test_fused_clustered_keys_rehash(H, hash_kind):
+    """Ids whose nibble-reversed keys share their top bits (ids = i << 40) pile onto one home
+    slot of the ordered table; the store detects the long probes and rehashes with the
+    multiplicative hash at the next sync.  Results must match the oracle either way."""
+    cfg = dict(V_dim=4, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    c = H.Context(0, max_keys=1 << 14, hash=hash_kind, **cfg)
+    up = O.Updater(**cfg)
+    rng = np.random.default_rng(5)
+    for step in range(4):
+        B, k = 500, 10
+        ids = (rng.integers(0, 3000, B * k).astype(np.uint64) << np.uint64(40))
+        blk = D.RowBlock(np.arange(0, B * k + 1, k, dtype=np.uint64), ids, None,
+                         np.where(rng.random(B) < .3, 1, -1).astype(np.float32))
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step == 0), want_pred=True)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step == 0))
+        p = H.progress(c)   # a sync point: the ordered table rehashes here after step 0
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
+        want = _auc_expect(blk.labels, opred, auc)
+        assert abs(p["auc"] - want) <= 1e-4 * blk.size
+    s = H.Store(c).stats()
+    assert s["n_keys"] == up.size() and s["seed"] == up.seed
