@@ -90,6 +90,22 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
+    (profiles/r1/pmc_hbm.json: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
+    tools/profile.sh).  None when absent."""
+    path = os.path.join(ROOT, "profiles", "r1", "pmc_hbm.json")
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, v in ks.items():
+        if name.startswith(kernel_prefix):
+            return int((v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]) * 1024)
+    return None
+
+
 def cpu_baseline(args):
     """The oracle (scalar C++ restatement, 1 thread) on a bounded sample of the same workload:
     epoch 0 (count push, untimed) then a timed epoch over the same rows (steady state)."""
@@ -228,7 +244,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": pmc_traffic("k_fm_bwd" if dom == "backward_update"
+                                            else "k_fm_fwd"),
+                     "traffic_source": "profiles/r1/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
+                                       "WRITE_SIZE per launch, raw counter bytes)",
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
