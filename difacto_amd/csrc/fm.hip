@@ -392,6 +392,29 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
           }
         }
       }
+    } else if (a.choff && len > (uint32_t)kChunkOcc) {
+      // a long segment: its chunks' partial sums (k_fm_bwd_chunks), combined in chunk order
+      const uint32_t c0 = a.choff[u];
+      const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+      const int P = d + 2;
+      float accp[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) accp[k] = 0.f;
+      for (uint32_t c = 0; c < nc; ++c) {
+        const float* pc = a.part + (int64_t)(c0 + c) * P;
+        gw += pc[0];
+        xxp += pc[1];
+        if (vq >= 0) {
+          float q[CPL];
+          load_coords<CPL, false>(pc + 2, l, d, q);
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) accp[k] += q[k];
+        }
+      }
+      if (vq >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = (g0[k] - vcur[k] * xxp) + accp[k];
+      }
     } else {
       for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
         uint32_t rw[UNR];
@@ -475,6 +498,77 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
     }
   }
+}
+
+// one group per chunk of a long segment: partial {g_w, XXp, sum (XV p) x} over its
+// kChunkOcc occurrences in order (the same terms as k_fm_bwd's walk)
+template <int G, int CPL>
+__global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
+  constexpr int CPB = kFmNT / G;
+  constexpr int UNR = 4;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t ch = (int64_t)blockIdx.x * CPB + g;
+  if (ch >= (int64_t)*a.nchunks) return;
+  const uint32_t u = a.chunk_seg[ch];
+  const uint32_t s0 = a.segstart[u] + (uint32_t)(ch - a.choff[u]) * kChunkOcc;
+  const uint32_t send = a.segstart[u + 1];
+  const uint32_t s1 = s0 + kChunkOcc < send ? s0 + kChunkOcc : send;
+  const bool valued = a.occ_x != nullptr;
+  const int d = a.d;
+  float gw = 0.f, xxp = 0.f, acc[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+  for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+    uint32_t rw[UNR];
+    float xw[UNR], pw[UNR], xr[UNR][CPL];
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
+      rw[t] = a.occ_row[i];
+      xw[t] = valued ? a.occ_x[i] : 1.f;
+    }
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      pw[t] = a.p[rw[t]];
+      load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)rw[t] * d : a.zpad, l, d, xr[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < UNR; ++t) {
+      if (i0 + t >= s1) continue;
+      if (pw[t] != 0.f) {  // SpMV::TransTimes skips p == 0
+        gw += valued ? pw[t] * xw[t] : pw[t];
+        xxp += valued ? pw[t] * (xw[t] * xw[t]) : pw[t];
+      }
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) acc[k] = valued ? acc[k] + xr[t][k] * xw[t] : acc[k] + xr[t][k];
+    }
+  }
+  float* pc = a.part + ch * (d + 2);
+  if (l == 0) {
+    pc[0] = gw;
+    pc[1] = xxp;
+  }
+  if (d > 0) store_coords<CPL, false>(pc + 2, l, d, acc);
+}
+
+int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
+  if (chunk_bound <= 0 || !a.choff) return DFX_OK;
+  int G, CPL;
+  bool vec;
+  lanes_for(a.d, false, &G, &CPL, &vec);
+  const int64_t cpb = kFmNT / G;
+  dim3 grid((unsigned)((chunk_bound + cpb - 1) / cpb));
+#define DFX_BWDC(GG, CC, VV)                                                              \
+  if (G == GG && CPL == CC) {                                                             \
+    hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC>), grid, dim3(kFmNT), 0, st, a);          \
+    DFX_HIP(hipGetLastError());                                                           \
+    return DFX_OK;                                                                        \
+  }
+  DFX_SCALAR_SET(DFX_BWDC)
+#undef DFX_BWDC
+  set_error("unsupported V_dim");
+  return DFX_ERR_ARG;
 }
 
 template <bool FUSED>

@@ -182,6 +182,18 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
 // n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.
 int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
              const uint32_t* n_dev = nullptr);
+int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
+             const uint32_t* n_dev = nullptr);
+
+// Long segments (keys with more than kChunkOcc occurrences in a batch: skewed / Zipf data)
+// are reduced in chunks of kChunkOcc occurrences by separate groups, then combined in chunk
+// order by the key's own group (fm.hip) — bounded work per group, deterministic sums.
+// chunk_plan (localize.hip, on lane L): choff[u] = first chunk of segment u (exclusive scan
+// of its chunk count, 0 for short segments), chunk_seg[c] = segment of chunk c, total in
+// *nchunks_dev.  Arrays sized for nnz + 1 (choff) and nnz / kChunkOcc + 1 (chunk_seg).
+constexpr int kChunkOcc = 256;
+int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
+               uint32_t* chunk_seg, uint32_t* nchunks_dev);
 
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
 void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);

@@ -200,6 +200,45 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
+// ---- chunk plan of long segments ------------------------------------------------------
+__global__ void k_seg_chunks(int64_t bound, const DevState* ds, const uint32_t* segstart,
+                             uint32_t* nch) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= bound) return;
+  uint32_t c = 0;
+  if (u < (int64_t)ds->u_count) {
+    const uint32_t len = segstart[u + 1] - segstart[u];
+    c = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
+  }
+  nch[u] = c;
+}
+
+// choff now holds the exclusive scan; a long segment lists its chunks
+__global__ void k_chunk_table(int64_t bound, const DevState* ds, const uint32_t* segstart,
+                              const uint32_t* choff, uint32_t* chunk_seg) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= bound || u >= (int64_t)ds->u_count) return;
+  const uint32_t len = segstart[u + 1] - segstart[u];
+  if (len <= (uint32_t)kChunkOcc) return;
+  const uint32_t n = (len + kChunkOcc - 1) / kChunkOcc;
+  for (uint32_t c = 0; c < n; ++c) chunk_seg[choff[u] + c] = (uint32_t)u;
+}
+
+int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
+               uint32_t* chunk_seg, uint32_t* nchunks_dev) {
+  if (nnz <= 0) {
+    DFX_HIP(hipMemsetAsync(nchunks_dev, 0, sizeof(uint32_t), L.stream));
+    return DFX_OK;
+  }
+  const dim3 g((unsigned)((nnz + 255) / 256));
+  hipLaunchKernelGGL(k_seg_chunks, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff);
+  DFX_TRY(scan_u32(L, choff, nnz, nchunks_dev, &L.ds->u_count));
+  hipLaunchKernelGGL(k_chunk_table, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff,
+                     chunk_seg);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
 int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o) {
   Workspace& ws = *L.ws;

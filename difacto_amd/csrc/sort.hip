@@ -400,22 +400,27 @@ void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* 
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, tilesum, ntiles, total_dev);
 }
 
-int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
+int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
              const uint32_t* n_dev) {
   if (n <= 0) {
-    if (total_dev) DFX_HIP(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), c->stream));
+    if (total_dev) DFX_HIP(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), L.stream));
     return DFX_OK;
   }
   const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
-  DFX_TRY(c->ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
-  uint32_t* ts = c->ws.tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, n_dev,
+  DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+  uint32_t* ts = L.ws->tiles.as<uint32_t>();
+  hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
                      ts);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, c->stream, ts, ntiles, total_dev);
-  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, c->stream, data, n, n_dev,
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, ts, ntiles, total_dev);
+  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
                      ts);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
+}
+
+int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
+             const uint32_t* n_dev) {
+  return scan_u32(main_lane(c), data, n, total_dev, n_dev);
 }
 
 }  // namespace dfx

@@ -35,7 +35,7 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * d * 4));
   DFX_TRY(ws.dscratch.ensure((rows / 4 + 64) * 8));
   DFX_TRY(ws.wv.ensure(nnz * 8));
-  DFX_TRY(ws.col.ensure(nnz * 4));
+  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 4));  // chunk partials
   ws.rows = rows;
   ws.nnz = nnz;
   return DFX_OK;
@@ -53,6 +53,8 @@ int loc_reserve(Workspace& w, int64_t nnz) {
   DFX_TRY(w.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(w.col.ensure(nnz * 4));
   DFX_TRY(w.uniq.ensure(nnz * 8));
+  DFX_TRY(w.flags.ensure((nnz + 1) * 4));                   // chunk plan: choff
+  DFX_TRY(w.rowtmp.ensure((nnz / kChunkOcc + 2) * 4));      // chunk plan: chunk_seg
   DFX_TRY(w.slot.ensure((nnz + 1) * 4));
   DFX_TRY(w.occ_row.ensure(nnz * 4));
   DFX_TRY(w.occ_x.ensure(nnz * 4));
@@ -211,6 +213,11 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   o.uniq = uniq;
   lane_mark(c, 0, c->loc_stream);
   DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+  // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
+  uint32_t* choff = bw.flags.as<uint32_t>();
+  uint32_t* chunk_seg = bw.rowtmp.as<uint32_t>();
+  uint32_t* nchunks = &bds->totals[1];
+  DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
   lane_mark(c, 1, c->loc_stream);
   DFX_HIP(hipEventRecord(c->ev_loc[k], c->loc_stream));
 
@@ -261,6 +268,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.d = d; g.slot = segslot; g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
+    g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<float>();
+    DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
     prof_mark(c, 6);
     DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds));

@@ -426,3 +426,55 @@ def test_fused_clustered_keys_rehash(H, hash_kind):
         assert abs(p["auc"] - want) <= 1e-4 * blk.size
     s = H.Store(c).stats()
     assert s["n_keys"] == up.size() and s["seed"] == up.seed
+
+
+@pytest.mark.parametrize("binary,d", [(True, 128), (False, 16), (True, 0)])
+def test_fused_zipf_skew_vs_oracle(H, binary, d):
+    """C5-shaped skew: Zipf(1.1) keys, so the hottest keys hold thousands of occurrences per
+    batch and their Xᵀ sums run in chunks (kChunkOcc) combined in chunk order.  Defaults
+    l1=1, V_threshold=10 (lazy V for hot keys only).  Sums are reordered for long segments,
+    so loss / AUC / model are compared within tolerance rather than bit-for-bit."""
+    cfg = dict(V_dim=d, lr=.05, V_lr=.01)
+    c = H.Context(0, max_keys=1 << 18, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(5):
+        blk = D.synthetic(4000, 39, 1 << 20, binary=binary, zipf=1.1, seed=300 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pred)
+        p = H.progress(c)
+        assert close(pred.cpu().numpy(), opred, rtol=1e-4)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
+        want = _auc_expect(blk.labels, opred, auc)
+        assert abs(p["auc"] - want) <= 1e-4 * blk.size
+    s = H.Store(c).stats()
+    assert s["seed"] == up.seed and s["n_keys"] == up.size()
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    v, l = H.Store(c).pull(c.tensor(uniq, torch.int64))
+    ov, ol = up.get(uniq)
+    if d > 0:
+        assert np.array_equal(l.cpu().numpy(), ol)
+    assert close(v.cpu().numpy(), ov, rtol=1e-3)
+
+
+def test_fused_hot_key_every_row(H):
+    """One key in every row (a bias-like feature): a 20000-occurrence segment."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    c = H.Context(0, max_keys=1 << 18, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(3):
+        blk = D.synthetic(20000, 20, 1 << 16, seed=70 + step)
+        ids = blk.ids.reshape(20000, 20).copy()
+        ids[:, 0] = 123456789
+        blk = D.RowBlock(blk.offs, ids.reshape(-1), None, blk.labels)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step == 0), want_pred=True)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step == 0))
+        p = H.progress(c)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
+    st_gpu = H.Store(c).entry(O.reverse_bytes(123456789))
+    st_cpu = up.entry(O.reverse_bytes(123456789)) if hasattr(up, "entry") else None
+    assert st_gpu is not None
+    if st_cpu is not None:
+        assert close(st_gpu[0], st_cpu[0], rtol=1e-4)
