@@ -10,7 +10,8 @@ import os
 
 import torch  # noqa: F401  (must precede CDLL, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdifacto_amd.so")
+LIB_PATH = os.environ.get("DFX_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libdifacto_amd.so")  # env: A/B builds
 
 _lib = None
 

@@ -264,7 +264,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   uint64_t* k1 = ws.keys1.as<uint64_t>();
   uint64_t* p0 = ws.vals0.as<uint64_t>();
   uint64_t* p1 = ws.vals1.as<uint64_t>();
-  DFX_TRY(ws.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
+  DFX_TRY(ws.os_reserve((nnz + 2047) / 2048));
   hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, L.stream, ds);
   TransformArgs t{};
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;

@@ -15,6 +15,8 @@
 // OR/AND reduction of the keys) get no pass: the active digits run first and the trailing
 // launches exit on the device — no host round trip, graph-capturable.  An optional
 // device-side count (n_dev) bounds the items when only the device knows it.
+#include <cstdlib>
+
 #include "internal.h"
 
 namespace dfx {
@@ -120,7 +122,7 @@ __device__ inline unsigned long long os_word(uint32_t tag, uint32_t flag, uint32
   return ((unsigned long long)((tag << 2) | flag) << 32) | v;
 }
 
-template <typename K, typename P>
+template <typename K, typename P, int IT>
 __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1, int64_t n0,
                                                       const uint32_t* n_dev, unsigned int* meta,
                                                       int q, const uint32_t* counts,
@@ -139,7 +141,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   const uint32_t tag = (meta[kMetaEpoch] * kOsMaxPasses + (unsigned)q) & 0x3FFFFFFFu;
 
   constexpr int kBuf = sizeof(K) > sizeof(P) ? sizeof(K) : sizeof(P);
-  __shared__ __attribute__((aligned(16))) unsigned char lbuf[kOsTile * kBuf];
+  __shared__ __attribute__((aligned(16))) unsigned char lbuf[(kOsNT * IT) * kBuf];
+  __shared__ uint8_t ldig[kOsNT * IT];  // digit of each tile-sorted position
   K* lk = reinterpret_cast<K*>(lbuf);
   P* lv = reinterpret_cast<P*>(lbuf);
   __shared__ uint32_t wcnt[kOsWaves][256];
@@ -155,21 +158,21 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   __syncthreads();
   const int64_t tile = s_tile;
   const int64_t n = os_count(n0, n_dev);
-  const int64_t tbase = tile * kOsTile;
+  const int64_t tbase = tile * (kOsNT * IT);
   if (tbase >= n) return;  // every later tile exits too: no waiter is left behind
 
-  // ---- keys (wave w owns a contiguous 64*kOsItems run); rank with ballots.  dr packs the
+  // ---- keys (wave w owns a contiguous 64*IT run); rank with ballots.  dr packs the
   // digit (bits 0-7) and the rank among the wave's items of that digit (bits 8-19).
-  K key[kOsItems];
-  uint32_t dr[kOsItems];
-  const int64_t wbase = tbase + (int64_t)w * kWave * kOsItems;
+  K key[IT];
+  uint32_t dr[IT];
+  const int64_t wbase = tbase + (int64_t)w * kWave * IT;
 #pragma unroll
-  for (int c = 0; c < kOsItems; ++c) {
+  for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     key[c] = idx < n ? kin[idx] : (K)0;
   }
 #pragma unroll
-  for (int c = 0; c < kOsItems; ++c) {
+  for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     const bool valid = idx < n;
     const uint32_t d = valid ? ((uint32_t)(key[c] >> shift) & dmask) : 0u;
@@ -244,9 +247,9 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   lstart[t] = block_excl_scan<kOsNT>(cnt, lds, nullptr);
   __syncthreads();
   // ---- keys: tile-local stable order through LDS, then stores in digit runs
-  const int64_t nvalid = (n - tbase) < kOsTile ? (n - tbase) : kOsTile;
+  const int64_t nvalid = (n - tbase) < (kOsNT * IT) ? (n - tbase) : (kOsNT * IT);
 #pragma unroll
-  for (int c = 0; c < kOsItems; ++c) {
+  for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     if (idx < n) {
       const uint32_t d = dr[c] & 255u;
@@ -255,29 +258,31 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
     }
   }
   __syncthreads();
-  uint32_t opos[kOsItems];
 #pragma unroll
-  for (int i = 0; i < kOsItems; ++i) {
+  for (int i = 0; i < IT; ++i) {
     const int qi = i * kOsNT + t;
     if (qi < nvalid) {
       const K kk = lk[qi];
       const uint32_t d = (uint32_t)(kk >> shift) & dmask;
-      opos[i] = gdig[d] + ((uint32_t)qi - lstart[d]);
-      kout[opos[i]] = kk;
+      ldig[qi] = (uint8_t)d;
+      kout[gdig[d] + ((uint32_t)qi - lstart[d])] = kk;
     }
   }
   __syncthreads();
   // ---- payloads: the same permutation through the same LDS buffer
 #pragma unroll
-  for (int c = 0; c < kOsItems; ++c) {
+  for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     if (idx < n) lv[dr[c]] = vin[idx];
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kOsItems; ++i) {
+  for (int i = 0; i < IT; ++i) {
     const int qi = i * kOsNT + t;
-    if (qi < nvalid) vout[opos[i]] = lv[qi];
+    if (qi < nvalid) {
+      const uint32_t d = ldig[qi];
+      vout[gdig[d] + ((uint32_t)qi - lstart[d])] = lv[qi];
+    }
   }
 }
 
@@ -297,7 +302,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                      const uint32_t* n_dev, int flags) {
   Workspace& ws = *L.ws;
   const int64_t ntiles = n > 0 ? (n + kOsTile - 1) / kOsTile : 1;
-  DFX_TRY(ws.os_reserve(ntiles));
+  DFX_TRY(ws.os_reserve(n > 0 ? (n + 2047) / 2048 : 1));  // look-back words for tiles >= 2048
   uint32_t* parts = ws.os_parts();
   uint32_t* counts = ws.os_counts();
   unsigned int* epoch = &L.ds->sort_epoch;
@@ -316,9 +321,20 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
                      begin_bit, end_bit, sortmeta, parts, counts, epoch);
+  static const int it = getenv("DFX_OS_ITEMS") ? atoi(getenv("DFX_OS_ITEMS")) : kOsItems;
   for (int q = 0; q < npasses; ++q) {
-    hipLaunchKernelGGL((k_os_scatter<K, P>), dim3((unsigned)ntiles), dim3(kOsNT), 0, L.stream,
-                       k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
+    if (it == 8) {
+      hipLaunchKernelGGL((k_os_scatter<K, P, 8>), dim3((unsigned)((n + 2047) / 2048)),
+                         dim3(kOsNT), 0, L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts,
+                         status, L.err);
+    } else if (it == 12) {
+      hipLaunchKernelGGL((k_os_scatter<K, P, 12>), dim3((unsigned)((n + 3071) / 3072)),
+                         dim3(kOsNT), 0, L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts,
+                         status, L.err);
+    } else {
+      hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems>), dim3((unsigned)ntiles), dim3(kOsNT), 0,
+                         L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
+    }
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;

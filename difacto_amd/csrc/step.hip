@@ -48,7 +48,7 @@ int loc_reserve(Workspace& w, int64_t nnz) {
   DFX_TRY(w.keys1.ensure(nnz * 8));
   DFX_TRY(w.vals0.ensure(nnz * 8));
   DFX_TRY(w.vals1.ensure(nnz * 8));
-  DFX_TRY(w.os_reserve((nnz + kOsSortTile - 1) / kOsSortTile));
+  DFX_TRY(w.os_reserve((nnz + 2047) / 2048));
   DFX_TRY(w.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
   DFX_TRY(w.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(w.col.ensure(nnz * 4));
