@@ -12,17 +12,35 @@ HDRS = $(wildcard $(CSRC)/*.h) include/difacto_amd.h
 LIB = difacto_amd/libdifacto_amd.so
 
 HOSTBIN = build/host_tests
-HOSTSRC = difacto_amd/host/gpu_adapters.cc tests/host/host_tests.cc
-HOSTHDR = difacto_amd/host/iface.h difacto_amd/host/gpu_adapters.h include/difacto_amd.h
+TRAINBIN = build/dfx_train
+HOSTLIB = difacto_amd/host/gpu_adapters.cc difacto_amd/host/reader.cc
+HOSTSRC = $(HOSTLIB) tests/host/host_tests.cc
+HOSTHDR = difacto_amd/host/iface.h difacto_amd/host/gpu_adapters.h difacto_amd/host/reader.h \
+  include/difacto_amd.h
+HOSTFLAGS = -std=c++14 -O2 -Wall -pthread
 
-all: $(LIB) oracle $(HOSTBIN)
+READERBIN = build/reader_tests
+
+all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN)
+
+# the readers alone (CPU only: no libdifacto_amd)
+$(READERBIN): difacto_amd/host/reader.cc tests/host/reader_tests.cc difacto_amd/host/reader.h \
+  difacto_amd/host/iface.h
+	@mkdir -p build
+	g++ $(HOSTFLAGS) -o $@ difacto_amd/host/reader.cc tests/host/reader_tests.cc
 
 # C++ host adapters (the reference's Loss/Updater/Store over the C-ABI) + their test driver;
 # plain g++ against the C-ABI, no HIP headers
 $(HOSTBIN): $(HOSTSRC) $(HOSTHDR) $(LIB)
 	@mkdir -p build
-	g++ -std=c++14 -O2 -Wall -o $@ $(HOSTSRC) -Ldifacto_amd -ldifacto_amd \
+	g++ $(HOSTFLAGS) -o $@ $(HOSTSRC) -Ldifacto_amd -ldifacto_amd \
 	  -Wl,-rpath,'$$ORIGIN/../difacto_amd'
+
+# the training driver (src/main.cc + SGDLearner::RunScheduler): reader -> feeder -> fused step
+$(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc $(HOSTHDR) $(LIB)
+	@mkdir -p build
+	g++ $(HOSTFLAGS) -o $@ $(HOSTLIB) difacto_amd/host/train_main.cc -Ldifacto_amd \
+	  -ldifacto_amd -Wl,-rpath,'$$ORIGIN/../difacto_amd'
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

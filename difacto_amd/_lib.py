@@ -36,6 +36,12 @@ class Progress(ctypes.Structure):
                 ("penalty", ctypes.c_double), ("nnz_w", ctypes.c_double)]
 
 
+class HostBatch(ctypes.Structure):
+    """dfx_host_batch: one pinned staging slot of a dfx_feeder"""
+    _fields_ = [("offset", vp), ("index", vp), ("value", vp), ("label", vp), ("weight", vp),
+                ("max_rows", c_i64), ("max_nnz", c_i64)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dfx_last_error": (ctypes.c_char_p, []),
@@ -74,6 +80,12 @@ _SIGS = {
     "dfx_progress_read": (ctypes.c_int, [vp, ctypes.POINTER(Progress), ctypes.c_int]),
     "dfx_prof_enable": (ctypes.c_int, [vp, ctypes.c_int]),
     "dfx_prof_read": (ctypes.c_int, [vp, f64p, ctypes.POINTER(ctypes.c_int), f64p]),
+    "dfx_feeder_create": (ctypes.c_int, [vp, c_i64, c_i64, ctypes.POINTER(vp)]),
+    "dfx_feeder_destroy": (ctypes.c_int, [vp]),
+    "dfx_feeder_slot": (ctypes.c_int, [vp, ctypes.POINTER(HostBatch)]),
+    "dfx_feeder_submit": (ctypes.c_int, [vp, c_i64, c_i64, ctypes.c_int, ctypes.c_int,
+                                         ctypes.POINTER(Batch)]),
+    "dfx_feeder_consumed": (ctypes.c_int, [vp]),
     "dfx_dist_record_floats": (ctypes.c_int, [vp]),
     "dfx_dist_localize": (ctypes.c_int, [vp, ctypes.POINTER(Batch), c_u64, ctypes.c_int, vp, vp,
                                          i64p, i64p]),

@@ -1,8 +1,13 @@
 // gpu_adapters.cc — see gpu_adapters.h.
 #include "gpu_adapters.h"
 
+#include <iterator>
+
+#include "reader.h"
+
 #include <unistd.h>
 
+#include <algorithm>
 #include <fstream>
 #include <set>
 #include <sstream>
@@ -345,19 +350,13 @@ GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs) {
     if (p.first == "loss") loss = p.second;
   }
   DFX_HOST_CHECK(loss == "fm" || loss == "logit", "unknown loss type " + loss);
+  if (loss == "logit") rest.push_back({"loss", "logit"});
   updater_ = std::make_shared<GpuSGDUpdater>();
   rest = updater_->Init(rest);
   V_dim_ = updater_->V_dim();
   store_.reset(new StoreGPU());
   store_->SetUpdater(updater_);
-  dfx_ctx* c = updater_->context()->h();
-  if (fused_) {
-    b_offs_.reset(new DevArray<uint64_t>(c));
-    b_idx_.reset(new DevArray<uint64_t>(c));
-    b_val_.reset(new DevArray<float>(c));
-    b_lab_.reset(new DevArray<float>(c));
-    b_wt_.reset(new DevArray<float>(c));
-  } else {
+  if (!fused_) {
     // V_dim is forwarded to the loss (sgd_learner.cc:37)
     loss_.reset(new GpuFMLoss(loss == "logit"));
     loss_->Init({{"V_dim", std::to_string(V_dim_)}});
@@ -365,28 +364,41 @@ GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs) {
   }
 }
 
+GpuSGDLearner::~GpuSGDLearner() {
+  if (feeder_) dfx_feeder_destroy(feeder_);
+}
+
 void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type,
-                                 bool push_cnt, Progress* prog) {
+                                 bool push_cnt) {
   push_cnt = push_cnt && job_type == kTraining && V_dim_ > 0;
   if (fused_) {
-    const size_t B = batch.size, nnz = B ? batch.offset[B] : 0;
-    dfx_batch b;
-    b.size = (int64_t)B;
-    b.nnz = (int64_t)nnz;
-    b.offset = b_offs_->upload(reinterpret_cast<const uint64_t*>(batch.offset), B + 1);
-    b.index = b_idx_->upload(batch.index, nnz);
-    b.value = b_val_->upload(batch.value, nnz);
-    b.label = b_lab_->upload(batch.label, B);
-    b.weight = b_wt_->upload(batch.weight, B);
+    const int64_t B = (int64_t)batch.size, nnz = B ? (int64_t)batch.offset[B] : 0;
     dfx_ctx* c = updater_->context()->h();
+    if (!feeder_ || B > feed_rows_ || nnz > feed_nnz_) {
+      if (feeder_) {
+        DfxCheck(dfx_sync(c), "dfx_sync");
+        dfx_feeder_destroy(feeder_);
+      }
+      feed_rows_ = std::max<int64_t>(B, feed_rows_);
+      feed_nnz_ = std::max<int64_t>(nnz, feed_nnz_);
+      DfxCheck(dfx_feeder_create(c, feed_rows_, feed_nnz_, &feeder_), "dfx_feeder_create");
+    }
+    dfx_host_batch hb;
+    DfxCheck(dfx_feeder_slot(feeder_, &hb), "dfx_feeder_slot");
+    static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t offsets");
+    std::memcpy(hb.offset, batch.offset, (B + 1) * 8);
+    std::memcpy(hb.index, batch.index, nnz * 8);
+    if (batch.value) std::memcpy(hb.value, batch.value, nnz * 4);
+    std::memcpy(hb.label, batch.label, B * 4);
+    if (batch.weight) std::memcpy(hb.weight, batch.weight, B * 4);
+    dfx_batch b;
+    DfxCheck(dfx_feeder_submit(feeder_, B, nnz, batch.value != nullptr, batch.weight != nullptr,
+                               &b),
+             "dfx_feeder_submit");
     DfxCheck(dfx_train_step(c, &b, job_type, push_cnt ? 1 : 0,
                             std::numeric_limits<uint64_t>::max(), nullptr),
              "dfx_train_step");
-    dfx_progress p;
-    DfxCheck(dfx_progress_read(c, &p, 1), "dfx_progress_read");
-    prog->nrows += p.nrows;
-    prog->loss += p.loss;
-    prog->auc += p.auc;
+    DfxCheck(dfx_feeder_consumed(feeder_), "dfx_feeder_consumed");
     return;
   }
   // the executor lambda of IterateData, through the plugin interfaces
@@ -400,15 +412,15 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   SArray<int> lengths;
   store_->Pull(keys, Store::kWeight, &values, V_dim_ > 0 ? &lengths : nullptr);
   dmlc::RowBlock<unsigned> blk = data.GetBlock();
-  prog->nrows += blk.size;
+  prog_.nrows += blk.size;
   SArray<real_t> pred(blk.size);
   SArray<int> w_pos, V_pos;
   if (V_dim_ > 0) GetPos(lengths, &w_pos, &V_pos);
   std::vector<SArray<char>> inputs = {SArray<char>(values), SArray<char>(w_pos),
                                       SArray<char>(V_pos)};
   loss_->Predict(blk, inputs, &pred);
-  prog->loss += loss_->Evaluate(blk.label, pred);
-  prog->auc += loss_->AUC(blk.label, pred);
+  prog_.loss += loss_->Evaluate(blk.label, pred);
+  prog_.auc += loss_->AUC(blk.label, pred);
   if (job_type == kTraining) {
     SArray<real_t> grads(values.size());
     inputs.push_back(SArray<char>(pred));
@@ -417,28 +429,28 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   }
 }
 
+Progress GpuSGDLearner::TakeProgress() {
+  Progress out = prog_;
+  prog_ = Progress();
+  if (fused_) {
+    dfx_progress p;
+    DfxCheck(dfx_progress_read(updater_->context()->h(), &p, 1), "dfx_progress_read");
+    out.nrows += p.nrows;
+    out.loss += p.loss;
+    out.auc += p.auc;
+  }
+  return out;
+}
+
 // ---- reader ------------------------------------------------------------------------------
 bool ReadLibSVM(const std::string& path, RowBlockContainer<feaid_t>* out) {
-  std::ifstream in(path);
+  std::ifstream in(path, std::ios::binary);
   if (!in) return false;
+  const std::string text((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
   *out = RowBlockContainer<feaid_t>();
-  std::string line;
+  ParseLibSVM(text.data(), text.data() + text.size(), out);
   bool all_one = true;
-  while (std::getline(in, line)) {
-    std::istringstream ls(line);
-    real_t y;
-    if (!(ls >> y)) continue;
-    out->label.push_back(y);
-    std::string tok;
-    while (ls >> tok) {
-      const size_t colon = tok.find(':');
-      out->index.push_back(std::stoull(tok.substr(0, colon)));
-      const real_t v = colon == std::string::npos ? 1.f : std::stof(tok.substr(colon + 1));
-      out->value.push_back(v);
-      all_one = all_one && v == 1.f;
-    }
-    out->offset.push_back(out->index.size());
-  }
+  for (float v : out->value) all_one = all_one && v == 1.f;
   if (all_one) out->value.clear();  // binary data (batch_reader.cc:71-73)
   return true;
 }

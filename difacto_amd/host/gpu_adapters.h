@@ -169,11 +169,16 @@ struct Progress {
 class GpuSGDLearner {
  public:
   enum JobType { kTraining = 3, kValidation = 4, kPrediction = 5 };
-  /** kwargs: the .conf keys (loss, V_dim, lr, l1, ...), plus `fused` (1: dfx_train_step) */
+  /** kwargs: the .conf keys (loss, V_dim, lr, l1, ...), plus `fused` (1: dfx_train_step,
+   * batches uploaded through a dfx_feeder; 0: through the Loss/Store interfaces) */
   explicit GpuSGDLearner(const KWArgs& kwargs);
-  /** one minibatch of raw feature ids; push_cnt = epoch 0 of training with V_dim > 0 */
-  void ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type, bool push_cnt,
-                    Progress* prog);
+  ~GpuSGDLearner();
+  /** one minibatch of raw feature ids; push_cnt = epoch 0 of training with V_dim > 0.
+   * Asynchronous on the fused path: the batch is copied into pinned staging and uploaded on
+   * the feeder's loader stream; the step runs behind the previous one. */
+  void ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type, bool push_cnt);
+  /** sgd::Progress accumulated since the last call (joins the device) */
+  Progress TakeProgress();
   std::shared_ptr<GpuSGDUpdater> updater() const { return updater_; }
   bool fused() const { return fused_; }
 
@@ -184,8 +189,9 @@ class GpuSGDLearner {
   std::unique_ptr<StoreGPU> store_;
   std::unique_ptr<GpuFMLoss> loss_;
   std::unique_ptr<GpuLocalizer> localizer_;
-  std::unique_ptr<DevArray<uint64_t>> b_offs_, b_idx_;
-  std::unique_ptr<DevArray<float>> b_val_, b_lab_, b_wt_;
+  dfx_feeder* feeder_ = nullptr;
+  int64_t feed_rows_ = 0, feed_nnz_ = 0;
+  Progress prog_;
 };
 
 /** a libsvm reader ("label idx:val ..."): the thin CSR producer the path's caller uses */

@@ -1,0 +1,85 @@
+// reader.h — the CPU side in front of the path: text parsers and the minibatch reader.
+//
+// The reference keeps reading and batching on the CPU (BASELINE.json north_star); these are
+// its readers restated for this build, feeding the device through dfx_feeder (pinned staging,
+// H2D on a loader stream, double-buffered):
+//   ParseLibSVM     dmlc libsvm parser ("label idx[:val] ..."), as the reference reads
+//                   tests/data
+//   ParseCriteo     src/reader/criteo_parser.h:40-92: label, 13 integer and 26 categorical
+//                   tab-separated columns; each non-empty column j hashes to
+//                   (CityHash64(text) << 12) | j  (EncodeFeaGrpID, include/difacto/base.h:60)
+//   TextReader      src/reader/reader.h:18-55 over a byte range of a file (part k of n, cut
+//                   at line boundaries like dmlc::InputSplit), parsed by worker threads
+//   BatchReader     src/reader/batch_reader.cc:29-78: batch_size rows per batch, a shuffle
+//                   buffer of shuf_buf rows, negative down-sampling with rand_r, all-one
+//                   values dropped (binary data)
+//
+// Parity notes: CityHash64 is the published v1.1 algorithm restated (the library is not in
+// the reference tree; no test vectors are available here, so criteo ids are parity unpinned).
+// The shuffle permutes with std::mt19937 (seed 0) where the reference calls
+// std::random_shuffle on glibc rand(); shuffled batch membership is parity unpinned
+// (SURVEY.md §8(d)), unshuffled reading (shuffle = 0) matches the reference's row order.
+#ifndef DIFACTO_AMD_HOST_READER_H_
+#define DIFACTO_AMD_HOST_READER_H_
+
+#include <cstdint>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "iface.h"
+
+namespace difacto {
+
+uint64_t CityHash64(const char* s, size_t len);
+
+/** parse [b, e) (whole lines) appending rows to out */
+void ParseLibSVM(const char* b, const char* e, RowBlockContainer<feaid_t>* out);
+void ParseCriteo(const char* b, const char* e, bool is_train, RowBlockContainer<feaid_t>* out);
+
+/** append rows [begin, end) of src to dst */
+void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
+                RowBlockContainer<feaid_t>* dst);
+
+/** reads part `part` of `nparts` of a text file in chunks, parsed by `nthreads` threads */
+class TextReader {
+ public:
+  TextReader(const std::string& path, const std::string& format, int part, int nparts,
+             size_t chunk_bytes = 64 << 20, int nthreads = 8);
+  bool Next();
+  const RowBlockContainer<feaid_t>& Value() const { return blk_; }
+  size_t BytesRead() const { return read_; }
+
+ private:
+  std::string path_, format_;
+  size_t begin_ = 0, end_ = 0, pos_ = 0, chunk_, read_ = 0;
+  int nthreads_;
+  std::vector<char> buf_;
+  RowBlockContainer<feaid_t> blk_;
+};
+
+/** minibatches of a TextReader (batch_reader.cc) */
+class BatchReader {
+ public:
+  BatchReader(const std::string& path, const std::string& format, int part, int nparts,
+              size_t batch_size, size_t shuf_buf, float neg_sampling, int nthreads = 8);
+  bool Next();
+  const RowBlockContainer<feaid_t>& Value() const { return batch_; }
+
+ private:
+  bool Refill();
+  TextReader reader_;
+  size_t batch_size_, shuf_buf_;
+  float neg_sampling_;
+  unsigned seed_ = 0;  // rand_r state of the negative sampling (batch_reader.cc:58)
+  std::mt19937 shuffle_rng_{0};
+  RowBlockContainer<feaid_t> pending_;  // the parsed chunk the shuffle buffer draws from
+  size_t pend_pos_ = 0;
+  RowBlockContainer<feaid_t> in_;  // rows waiting to be batched
+  std::vector<size_t> order_;
+  size_t start_ = 0;
+  RowBlockContainer<feaid_t> batch_;
+};
+
+}  // namespace difacto
+#endif  // DIFACTO_AMD_HOST_READER_H_

@@ -1,0 +1,148 @@
+// train_main.cc — dfx_train: the reference's `difacto` executable for the SGD learner
+// (src/main.cc + SGDLearner::RunScheduler, src/sgd/sgd_learner.cc:51-117) on one GPU.
+//
+//   build/dfx_train data_in=FILE [data_val=FILE] [data_format=libsvm|criteo|criteo_test]
+//                   [batch_size=100] [shuffle=10] [neg_sampling=1] [max_num_epochs=20]
+//                   [num_jobs_per_epoch=10] [stop_rel_objv=1e-5] [model_in=F] [model_out=F]
+//                   [fused=1] [nthreads=8] [V_dim=..] [lr=..] [l1=..] ...  (SGDUpdaterParam)
+//
+// Each epoch reads data_in in num_jobs_per_epoch parts (the reference's jobs, here run in
+// order), minibatched by BatchReader (reader.h) and trained through GpuSGDLearner, i.e. one
+// dfx_train_step per batch behind a pinned-staging dfx_feeder.  It prints the reference's
+// "Epoch[k] Training: Rows = .., loss = .., AUC = .." line per epoch, plus the rate including
+// parsing and PCIe (host ex/s), which is NOT the device-resident rate bench.py reports.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "gpu_adapters.h"
+#include "reader.h"
+
+using namespace difacto;
+
+namespace {
+struct Param {
+  std::string data_in, data_val, data_format = "libsvm", model_in, model_out;
+  size_t batch_size = 100, shuffle = 10;
+  float neg_sampling = 1.f;
+  int max_num_epochs = 20, num_jobs_per_epoch = 10, nthreads = 8;
+  double stop_rel_objv = 1e-5;
+};
+
+double Now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// sgd_utils.h:59-63
+std::string Text(const Progress& p) {
+  char buf[256];
+  std::snprintf(buf, sizeof(buf), "Rows = %.0f, loss = %.9g, AUC = %.9g", p.nrows,
+                p.loss / p.nrows, p.auc / p.nrows);
+  return buf;
+}
+
+Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_type) {
+  Progress prog;
+  const bool train = job_type == GpuSGDLearner::kTraining;
+  const std::string& path = train ? P.data_in : P.data_val;
+  for (int part = 0; part < P.num_jobs_per_epoch; ++part) {
+    if (train) {
+      // sgd_learner.cc:273-280
+      BatchReader reader(path, P.data_format, part, P.num_jobs_per_epoch, P.batch_size,
+                         P.batch_size * P.shuffle, P.neg_sampling, P.nthreads);
+      while (reader.Next()) {
+        const auto blk = reader.Value().GetBlock();
+        learner->ProcessBatch(blk, job_type, epoch == 0);
+      }
+    } else {
+      // sgd_learner.cc:281-286: validation reads whole 256 MB chunks as one batch
+      TextReader reader(path, P.data_format, part, P.num_jobs_per_epoch, 256 << 20, P.nthreads);
+      while (reader.Next()) {
+        const auto& v = reader.Value();
+        if (v.Size() == 0) continue;
+        learner->ProcessBatch(v.GetBlock(), job_type, false);
+      }
+    }
+    const Progress p = learner->TakeProgress();
+    prog.nrows += p.nrows;
+    prog.loss += p.loss;
+    prog.auc += p.auc;
+  }
+  return prog;
+}
+}  // namespace
+
+int main(int argc, char** argv) {
+  Param P;
+  KWArgs rest;
+  bool fused_given = false;
+  for (int i = 1; i < argc; ++i) {
+    const char* eq = std::strchr(argv[i], '=');
+    if (!eq) {
+      std::fprintf(stderr, "argument '%s' is not key=value\n", argv[i]);
+      return 2;
+    }
+    const std::string k(argv[i], eq - argv[i]), v(eq + 1);
+    if (k == "data_in") P.data_in = v;
+    else if (k == "data_val") P.data_val = v;
+    else if (k == "data_format") P.data_format = v;
+    else if (k == "model_in") P.model_in = v;
+    else if (k == "model_out") P.model_out = v;
+    else if (k == "batch_size") P.batch_size = std::stoul(v);
+    else if (k == "shuffle") P.shuffle = std::stoul(v);
+    else if (k == "neg_sampling") P.neg_sampling = std::stof(v);
+    else if (k == "max_num_epochs") P.max_num_epochs = std::stoi(v);
+    else if (k == "num_jobs_per_epoch") P.num_jobs_per_epoch = std::stoi(v);
+    else if (k == "stop_rel_objv") P.stop_rel_objv = std::stod(v);
+    else if (k == "nthreads") P.nthreads = std::stoi(v);
+    else {
+      fused_given = fused_given || k == "fused";
+      rest.push_back({k, v});
+    }
+  }
+  if (P.data_in.empty()) {
+    std::fprintf(stderr, "usage: %s data_in=FILE [key=value ...]\n", argv[0]);
+    return 2;
+  }
+  if (!fused_given) rest.push_back({"fused", "1"});
+  GpuSGDLearner learner(rest);
+  if (!P.model_in.empty()) {
+    FileStream fi(P.model_in.c_str(), "rb");
+    learner.updater()->Load(&fi);
+  }
+  const double t0 = Now();
+  double pre_loss = 0, pre_val_auc = 0;  // sgd_learner.cc:52
+  for (int k = 0; k < P.max_num_epochs; ++k) {
+    const double te = Now();
+    const Progress tr = RunEpoch(&learner, P, k, GpuSGDLearner::kTraining);
+    const double dt = Now() - te;
+    std::printf("Epoch[%d] Training: %s  (%.0f ex/s incl. parse+PCIe, %.2f s)\n", k,
+                Text(tr).c_str(), tr.nrows / dt, Now() - t0);
+    Progress va;
+    if (!P.data_val.empty()) {
+      va = RunEpoch(&learner, P, k, GpuSGDLearner::kValidation);
+      std::printf("Epoch[%d] Validation: %s\n", k, Text(va).c_str());
+    }
+    std::fflush(stdout);
+    // stop criteria, sgd_learner.cc:89-108
+    double eps = std::fabs(tr.loss - pre_loss) / pre_loss;
+    if (eps < P.stop_rel_objv) {
+      std::printf("Change of loss [%g] < stop_rel_objv [%g]\n", eps, P.stop_rel_objv);
+      break;
+    }
+    if (va.auc > 0) {
+      eps = (va.auc - pre_val_auc) / va.nrows;
+      if (eps < 1e-5) break;
+    }
+    pre_loss = tr.loss;
+    pre_val_auc = va.auc;
+  }
+  if (!P.model_out.empty()) {
+    FileStream fo(P.model_out.c_str(), "wb");
+    learner.updater()->Save(false, &fo);
+  }
+  return 0;
+}

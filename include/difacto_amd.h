@@ -102,6 +102,30 @@ int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind)
 /* pre-size the fused-path workspace so dfx_train_step allocates nothing (graph capture) */
 int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz);
 
+/* ---- batch feeder (SGDLearner::IterateData's producer loop, sgd_learner.cc:289-314) -----
+ * Host RowBlocks to device batches through pinned staging and a loader stream that becomes
+ * the context's input stream; two slots, so the upload of batch t+1 overlaps the step on t.
+ *   dfx_feeder_slot     the next slot's pinned host arrays (waits until the step that used
+ *                       the slot two batches ago has passed the device); fill them
+ *   dfx_feeder_submit   enqueue their upload; *out receives the device batch
+ *   dfx_feeder_consumed after dfx_train_step(*out): marks the slot in use until then */
+typedef struct dfx_feeder dfx_feeder;
+typedef struct dfx_host_batch {
+  uint64_t* offset; /* max_rows + 1 */
+  uint64_t* index;  /* max_nnz */
+  float* value;     /* max_nnz */
+  float* label;     /* max_rows */
+  float* weight;    /* max_rows */
+  int64_t max_rows;
+  int64_t max_nnz;
+} dfx_host_batch;
+int dfx_feeder_create(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz, dfx_feeder** out);
+int dfx_feeder_destroy(dfx_feeder* f);
+int dfx_feeder_slot(dfx_feeder* f, dfx_host_batch* hb);
+int dfx_feeder_submit(dfx_feeder* f, int64_t B, int64_t nnz, int has_value, int has_weight,
+                      dfx_batch* out);
+int dfx_feeder_consumed(dfx_feeder* f);
+
 /* ---- Localizer::Compact (localizer.h:41-51) -------------------------------------------
  * keys = ReverseBytes(index % max_index); uniq[U] ascending, cnt[U] occurrence counts
  * (float, may be NULL), col[nnz] = rank of each nnz's key (the u32 CSR index).  Offsets,

@@ -114,8 +114,8 @@ static void TestSGDLearnerBasic(const RowBlockContainer<feaid_t>& data, bool fus
   GpuSGDLearner learner({{"V_dim", "0"}, {"l2", "1"}, {"l1", "1"}, {"lr", "1"},
                          {"fused", fused ? "1" : "0"}, {"max_keys", "16384"}});
   for (int ep = 0; ep < 20; ++ep) {
-    Progress prog;
-    learner.ProcessBatch(data.GetBlock(), GpuSGDLearner::kTraining, ep == 0, &prog);
+    learner.ProcessBatch(data.GetBlock(), GpuSGDLearner::kTraining, ep == 0);
+    const Progress prog = learner.TakeProgress();
     EXPECT(std::fabs(prog.loss - objv[ep]) < 5e-5, "epoch %d objv %.6f want %.6f", ep, prog.loss,
            objv[ep]);
     EXPECT(prog.nrows == 100, "nrows");
@@ -134,9 +134,9 @@ static void TestDriversAgree(const RowBlockContainer<feaid_t>& data) {
   RowSlice h0 = Slice(data, 0, 50), h1 = Slice(data, 50, 100);
   for (int ep = 0; ep < 5; ++ep) {
     for (RowSlice* h : {&h0, &h1}) {
-      Progress pa, pb;
-      a.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0, &pa);
-      b.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0, &pb);
+      a.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0);
+      b.ProcessBatch(h->blk, GpuSGDLearner::kTraining, ep == 0);
+      const Progress pa = a.TakeProgress(), pb = b.TakeProgress();
       EXPECT(std::fabs(pa.loss - pb.loss) <= 1e-4 * std::fabs(pb.loss), "epoch %d loss %.7f vs %.7f",
              ep, pa.loss, pb.loss);
       EXPECT(std::fabs(pa.auc - pb.auc) <= 1e-4 * 50, "epoch %d auc %.7f vs %.7f", ep, pa.auc,

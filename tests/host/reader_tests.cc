@@ -1,0 +1,218 @@
+// reader_tests.cc — CPU tests of difacto_amd/host/reader.{h,cc} (no GPU, no libdifacto_amd).
+//
+// BatchReader.Read / RandRead / PartRead restate the reference's known answers
+// (tests/cpp/batch_reader_test.cc:9-62, on tests/data == tests/golden/rcv1_100.libsvm).
+// The rest are properties: chunked / threaded parsing equals one-shot parsing, parts of a
+// file partition its rows, negative down-sampling drops only negatives, and the criteo
+// parser's id layout (CityHash64 << 12 | column), criteo_parser.h:40-92.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <set>
+#include <string>
+
+#include "../../difacto_amd/host/reader.h"
+
+using namespace difacto;
+
+static int g_fail = 0;
+#define EXPECT(c, msg)                                                  \
+  do {                                                                  \
+    if (!(c)) {                                                         \
+      std::printf("  FAIL %s:%d %s\n", __FILE__, __LINE__, msg);        \
+      ++g_fail;                                                         \
+    }                                                                   \
+  } while (0)
+
+template <typename T>
+static double Norm1(const T* d, size_t n) {
+  double s = 0;
+  for (size_t i = 0; i < n; ++i) s += std::fabs((double)d[i]);
+  return s;
+}
+static double Norm2(const float* d, size_t n) {
+  double s = 0;
+  for (size_t i = 0; i < n; ++i) s += (double)d[i] * d[i];
+  return s;
+}
+
+// batch_reader_test.cc:8-13
+static const int kBatch = 37;
+static const double kLabel[] = {11, 15, 10};
+static const size_t kLen[] = {37, 37, 26};
+static const double kOs[] = {85035, 63968, 31323};
+static const double kIdx[] = {95285478, 70504854, 62972349};
+static const double kVal[] = {37, 37, 26};
+
+static void TestRead(const std::string& data, size_t shuf, int nthreads) {
+  BatchReader reader(data, "libsvm", 0, 1, kBatch, shuf, 1.f, nthreads);
+  int i = 0;
+  while (reader.Next()) {
+    EXPECT(i < 3, "more than 3 batches");
+    if (i >= 3) break;
+    const auto& b = reader.Value();
+    const size_t n = b.Size(), nnz = b.offset[n];
+    EXPECT(n == kLen[i], "batch size");
+    double ls = 0;
+    for (size_t r = 0; r < n; ++r) ls += b.label[r];
+    EXPECT(ls == kLabel[i], "label sum");
+    const double os = Norm1(b.offset.data(), n + 1);
+    if (shuf == 0) {
+      EXPECT(os == kOs[i], "offset norm1");
+    } else {
+      EXPECT(os != kOs[i], "shuffled batch keeps the file's row order");
+    }
+    EXPECT(Norm1(b.index.data(), nnz) == kIdx[i], "index norm1");
+    EXPECT(std::fabs(Norm2(b.value.data(), b.value.size()) - kVal[i]) <= 1e-5, "value norm2");
+    ++i;
+  }
+  EXPECT(i == 3, "3 batches");
+}
+
+// batch_reader_test.cc:47-62
+static void TestPartRead(const std::string& data) {
+  size_t ttl = 0;
+  for (int part = 0; part < 2; ++part) {
+    BatchReader reader(data, "libsvm", part, 2, kBatch, 0, 1.f);
+    size_t rows = 0;
+    while (reader.Next()) {
+      const auto& b = reader.Value();
+      const size_t n = b.Size();
+      EXPECT(std::fabs(n - Norm2(b.value.data(), b.offset[n])) <= 1e-5, "part value norm2");
+      rows += n;
+    }
+    if (part == 1) EXPECT(rows <= 60 && rows >= 40, "part 1 of 2 holds 40..60 rows");
+    ttl += rows;
+  }
+  EXPECT(ttl == 100, "the two parts partition the file");
+}
+
+static RowBlockContainer<feaid_t> ReadAll(const std::string& path, const std::string& fmt,
+                                          int part, int nparts, size_t chunk, int nthreads) {
+  TextReader r(path, fmt, part, nparts, chunk, nthreads);
+  RowBlockContainer<feaid_t> all;
+  while (r.Next()) AppendRows(r.Value(), 0, r.Value().Size(), &all);
+  return all;
+}
+
+static bool Same(const RowBlockContainer<feaid_t>& a, const RowBlockContainer<feaid_t>& b) {
+  return a.offset == b.offset && a.index == b.index && a.value == b.value && a.label == b.label;
+}
+
+static void TestChunking(const std::string& data) {
+  const auto ref = ReadAll(data, "libsvm", 0, 1, 64 << 20, 1);
+  EXPECT(ref.Size() == 100 && ref.index.size() == 9648, "rcv1_100: 100 rows, 9648 nnz");
+  for (size_t chunk : {size_t(1000), size_t(4096), size_t(77777)})
+    for (int th : {1, 3, 8}) EXPECT(Same(ref, ReadAll(data, "libsvm", 0, 1, chunk, th)),
+                                    "chunked/threaded parse differs");
+  for (int np : {3, 7, 100, 150}) {
+    RowBlockContainer<feaid_t> cat;
+    for (int p = 0; p < np; ++p) {
+      const auto part = ReadAll(data, "libsvm", p, np, 2000, 2);
+      AppendRows(part, 0, part.Size(), &cat);
+    }
+    EXPECT(Same(ref, cat), "parts do not partition the rows");
+  }
+}
+
+static void TestNegSampling(const std::string& data) {
+  size_t pos = 0, neg = 0;
+  {
+    BatchReader r(data, "libsvm", 0, 1, 10, 0, 1.f);
+    while (r.Next())
+      for (float y : r.Value().label) (y > 0 ? pos : neg) += 1;
+  }
+  size_t pos2 = 0, neg2 = 0, batches = 0;
+  BatchReader r(data, "libsvm", 0, 1, 10, 0, 0.3f);
+  while (r.Next()) {
+    ++batches;
+    EXPECT(r.Value().Size() <= 10, "batch larger than batch_size");
+    for (float y : r.Value().label) (y > 0 ? pos2 : neg2) += 1;
+  }
+  EXPECT(pos2 == pos, "down-sampling dropped a positive");
+  EXPECT(neg2 < neg && neg2 > 0, "down-sampling kept every (or no) negative");
+  // deterministic (rand_r from seed 0, batch_reader.cc:17)
+  size_t neg3 = 0;
+  BatchReader r3(data, "libsvm", 0, 1, 10, 0, 0.3f);
+  while (r3.Next())
+    for (float y : r3.Value().label) neg3 += y <= 0;
+  EXPECT(neg3 == neg2, "down-sampling not deterministic");
+}
+
+static void TestShuffleIsPermutation(const std::string& data) {
+  const auto ref = ReadAll(data, "libsvm", 0, 1, 64 << 20, 1);
+  std::multiset<double> want, got;
+  for (size_t r = 0; r < ref.Size(); ++r)
+    want.insert(Norm1(ref.index.data() + ref.offset[r], ref.offset[r + 1] - ref.offset[r]));
+  BatchReader br(data, "libsvm", 0, 1, 16, 48, 1.f);
+  size_t rows = 0;
+  while (br.Next()) {
+    const auto& b = br.Value();
+    EXPECT(b.Size() <= 16, "batch size");
+    rows += b.Size();
+    for (size_t r = 0; r < b.Size(); ++r)
+      got.insert(Norm1(b.index.data() + b.offset[r], b.offset[r + 1] - b.offset[r]));
+  }
+  EXPECT(rows == 100 && want == got, "shuffled epoch is not a permutation of the rows");
+}
+
+static void TestCriteo(const std::string& dir) {
+  const std::string path = dir + "/criteo_sample.txt";
+  {
+    std::ofstream f(path);
+    // label, 13 integer columns, 26 categorical; empty columns are skipped
+    f << "1\t5\t\t3\t0\t1\t2\t3\t4\t5\t6\t7\t8\t9\t68fd1e64\t80e26c9b\t\t1e88c74f\t"
+         "a\tb\tc\td\te\tf\tg\th\ti\tj\tk\tl\tm\tn\to\tp\tq\tr\ts\tt\tu\tv\n";
+    f << "0\t\t\t\t\t\t\t\t\t\t\t\t\t\tx\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\t\n";
+  }
+  const auto all = ReadAll(path, "criteo", 0, 1, 64 << 20, 1);
+  EXPECT(all.Size() == 2, "criteo rows");
+  EXPECT(all.label.size() == 2 && all.label[0] == 1 && all.label[1] == 0, "criteo labels");
+  EXPECT(all.offset[1] == 12 + 25, "row 0: 12 integer + 25 categorical non-empty columns");
+  EXPECT(all.offset[2] - all.offset[1] == 1, "row 1: one non-empty column");
+  std::set<int> groups;
+  for (size_t k = 0; k < all.offset[1]; ++k) groups.insert((int)(all.index[k] & 4095));
+  EXPECT(groups.size() == 37 && !groups.count(1) && !groups.count(15), "criteo group ids");
+  EXPECT(all.index[all.offset[1]] == ((CityHash64("x", 1) << 12) | 13), "criteo id layout");
+  EXPECT(all.index[0] == ((CityHash64("5", 1) << 12) | 0), "criteo integer id");
+  std::remove(path.c_str());
+}
+
+static void TestCityHash() {
+  EXPECT(CityHash64("", 0) == 0x9ae16a3b2f90404fULL, "CityHash64('') == k2");
+  // every length class, determinism and sensitivity to each byte
+  std::string s(200, 'a');
+  for (size_t i = 0; i < s.size(); ++i) s[i] = (char)('a' + (i * 7) % 26);
+  std::set<uint64_t> seen;
+  for (size_t len = 0; len <= 200; ++len) seen.insert(CityHash64(s.data(), len));
+  EXPECT(seen.size() == 201, "CityHash64 collides across prefix lengths");
+  for (size_t len : {3, 7, 15, 31, 63, 129}) {
+    std::string t = s.substr(0, len);
+    const uint64_t h0 = CityHash64(t.data(), len);
+    for (size_t i = 0; i < len; ++i) {
+      t[i] ^= 1;
+      EXPECT(CityHash64(t.data(), len) != h0, "CityHash64 ignores a byte");
+      t[i] ^= 1;
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::fprintf(stderr, "usage: %s rcv1_100.libsvm tmpdir\n", argv[0]);
+    return 2;
+  }
+  const std::string data = argv[1];
+  TestRead(data, 0, 8);
+  TestRead(data, 0, 1);
+  TestRead(data, kBatch, 4);
+  TestPartRead(data);
+  TestChunking(data);
+  TestNegSampling(data);
+  TestShuffleIsPermutation(data);
+  TestCriteo(argv[2]);
+  TestCityHash();
+  std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -8,6 +8,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "build", "host_tests")
+READER_BIN = os.path.join(ROOT, "build", "reader_tests")
+TRAIN_BIN = os.path.join(ROOT, "build", "dfx_train")
 DATA = os.path.join(ROOT, "tests", "golden", "rcv1_100.libsvm")
 
 
@@ -31,3 +33,75 @@ def test_host_adapters_reference_gtests():
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL PASSED" in r.stdout
+
+
+def test_readers_reference_batch_reader_known_answers(tmp_path):
+    """difacto_amd/host/reader.cc on the CPU: the reference's BatchReader.Read / RandRead /
+    PartRead known answers (tests/cpp/batch_reader_test.cc) plus chunking, part, shuffle,
+    down-sampling and criteo-layout properties (tests/host/reader_tests.cc)."""
+    subprocess.check_call(["make", "-s", "build/reader_tests"], cwd=ROOT)
+    r = subprocess.run([READER_BIN, DATA, str(tmp_path)], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
+
+
+def test_train_driver_builds():
+    subprocess.check_call(["make", "-s", "build/dfx_train"], cwd=ROOT)
+    syms = subprocess.check_output(["nm", "-D", "--undefined-only", TRAIN_BIN], text=True)
+    for s in ("dfx_feeder_create", "dfx_feeder_slot", "dfx_feeder_submit", "dfx_train_step"):
+        assert s in syms, s
+    r = subprocess.run([TRAIN_BIN], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
+
+
+# SGDLearner.Basic (tests/cpp/sgd_learner_test.cc:9-30): the summed loss per epoch
+_BASIC_OBJV = [69.314718, 69.314718, 67.151912, 61.414778, 56.244989, 53.218700, 51.248737,
+               49.846688, 48.650164, 47.698351, 46.924038, 46.388223, 45.970721, 45.499307,
+               45.102245, 44.798413, 44.565211, 44.386417, 44.240657, 44.109764]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", ["0", "10"])
+def test_train_driver_sgd_learner_basic(shuffle):
+    """dfx_train (BatchReader -> dfx_feeder -> dfx_train_step) reproduces the reference's
+    SGDLearner.Basic trace: same kwargs as sgd_learner_test.cc:32-39; stop_rel_objv=0 so all
+    20 epochs run (epochs 0 and 1 have equal loss, which would stop the reference's loop)."""
+    assert os.path.exists(TRAIN_BIN), "build/dfx_train missing: run make"
+    r = subprocess.run([TRAIN_BIN, "data_in=" + DATA, "V_dim=0", "l2=1", "l1=1", "lr=1",
+                        "num_jobs_per_epoch=1", "batch_size=100", "max_num_epochs=20",
+                        "shuffle=" + shuffle, "stop_rel_objv=0", "max_keys=16384"],
+                       capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    losses = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
+              if "Training:" in l]
+    assert len(losses) == 20
+    for ep, (got, want) in enumerate(zip(losses, _BASIC_OBJV)):
+        assert abs(got * 100 - want) < 5e-5, (ep, got * 100, want)
+
+
+def _train_losses(args):
+    r = subprocess.run([TRAIN_BIN, "data_in=" + DATA] + args, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = [(float(l.split("loss = ")[1].split(",")[0]), float(l.split("AUC = ")[1].split()[0]))
+           for l in r.stdout.splitlines() if "Training:" in l]
+    assert out, r.stdout
+    return out
+
+
+@pytest.mark.gpu
+def test_train_driver_feeder_matches_interface_path():
+    """Many small batches through the feeder's two pinned slots (fused=1) against the same
+    batches through the Localizer/Loss/Store interfaces (fused=0): FM with V_dim 4, 3 jobs per
+    epoch, batch 7, shuffled and down-sampled, 4 epochs.  Same kernels, so the traces agree to
+    float rounding of the differently ordered reductions."""
+    common = ["V_dim=4", "V_threshold=2", "lr=0.1", "V_lr=0.05", "l1=0.1",
+              "num_jobs_per_epoch=3", "batch_size=7", "shuffle=3", "neg_sampling=0.7",
+              "max_num_epochs=4", "stop_rel_objv=0", "max_keys=65536"]
+    a = _train_losses(common + ["fused=1"])
+    b = _train_losses(common + ["fused=0"])
+    assert len(a) == len(b) == 4
+    for (la, aa), (lb, ab) in zip(a, b):
+        assert abs(la - lb) <= 1e-4 * abs(lb), (la, lb)
+        assert abs(aa - ab) <= 1e-3, (aa, ab)
