@@ -20,8 +20,13 @@ HOSTHDR = difacto_amd/host/iface.h difacto_amd/host/gpu_adapters.h difacto_amd/h
 HOSTFLAGS = -std=c++14 -O2 -Wall -pthread
 
 READERBIN = build/reader_tests
+GENBIN = build/gen_criteo
 
-all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN)
+all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN)
+
+$(GENBIN): tools/gen_criteo.cc
+	@mkdir -p build
+	g++ -O2 -o $@ $<
 
 # the readers alone (CPU only: no libdifacto_amd)
 $(READERBIN): difacto_amd/host/reader.cc tests/host/reader_tests.cc difacto_amd/host/reader.h \

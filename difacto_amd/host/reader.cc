@@ -189,15 +189,24 @@ void ParseCriteo(const char* p, const char* e, bool is_train, RowBlockContainer<
 
 void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
                 RowBlockContainer<feaid_t>* dst) {
-  for (size_t r = begin; r < end; ++r) {
-    const size_t o0 = src.offset[r], o1 = src.offset[r + 1];
-    dst->index.insert(dst->index.end(), src.index.begin() + o0, src.index.begin() + o1);
-    if (!src.value.empty())
-      dst->value.insert(dst->value.end(), src.value.begin() + o0, src.value.begin() + o1);
-    dst->label.push_back(src.label[r]);
-    if (!src.weight.empty()) dst->weight.push_back(src.weight[r]);
-    dst->offset.push_back(dst->index.size());
-  }
+  if (end <= begin) return;
+  // one contiguous range: bulk copies, offsets rebased onto dst's end
+  const size_t o0 = src.offset[begin], o1 = src.offset[end], base = dst->index.size();
+  dst->index.insert(dst->index.end(), src.index.begin() + o0, src.index.begin() + o1);
+  if (!src.value.empty())
+    dst->value.insert(dst->value.end(), src.value.begin() + o0, src.value.begin() + o1);
+  dst->label.insert(dst->label.end(), src.label.begin() + begin, src.label.begin() + end);
+  if (!src.weight.empty())
+    dst->weight.insert(dst->weight.end(), src.weight.begin() + begin, src.weight.begin() + end);
+  for (size_t r = begin + 1; r <= end; ++r) dst->offset.push_back(src.offset[r] - o0 + base);
+}
+
+static void ClearRows(RowBlockContainer<feaid_t>* c) {  // keeps the capacity
+  c->offset.resize(1);
+  c->label.clear();
+  c->weight.clear();
+  c->index.clear();
+  c->value.clear();
 }
 
 // ---- TextReader -------------------------------------------------------------------------
@@ -227,7 +236,7 @@ TextReader::TextReader(const std::string& path, const std::string& format, int p
 }
 
 bool TextReader::Next() {
-  blk_ = RowBlockContainer<feaid_t>();
+  ClearRows(&blk_);
   if (pos_ >= end_) return false;
   std::ifstream f(path_, std::ios::binary);
   size_t want = std::min(chunk_, end_ - pos_), got = 0, cut = 0;
@@ -256,24 +265,31 @@ bool TextReader::Next() {
     cuts.push_back(std::min(c < cut ? c + 1 : cut, cut));
   }
   cuts.push_back(cut);
-  std::vector<RowBlockContainer<feaid_t>> parts(nthreads_);
+  parts_.resize(nthreads_);
   std::vector<std::thread> th;
   const bool train = format_ != "criteo_test";
   for (int t = 0; t < nthreads_; ++t) {
     th.emplace_back([&, t]() {
+      // parse into a thread-local container that owns this part's buffers (reused across
+      // chunks: first touches of fresh pages are the expensive part): neighbouring parts_[]
+      // headers share cache lines, and every push_back would bounce them
+      RowBlockContainer<feaid_t> local;
+      std::swap(local, parts_[t]);
+      ClearRows(&local);
       const char* a = buf_.data() + cuts[t];
       const char* b = buf_.data() + std::max(cuts[t], cuts[t + 1]);
       if (format_ == "libsvm") {
-        ParseLibSVM(a, b, &parts[t]);
+        ParseLibSVM(a, b, &local);
       } else {
-        ParseCriteo(a, b, train, &parts[t]);
+        ParseCriteo(a, b, train, &local);
       }
+      std::swap(local, parts_[t]);
     });
   }
   for (auto& x : th) x.join();
   bool valued = false;
-  for (auto& pt : parts) valued = valued || !pt.value.empty();
-  for (auto& pt : parts) {
+  for (auto& pt : parts_) valued = valued || !pt.value.empty();
+  for (auto& pt : parts_) {
     if (valued && pt.value.empty()) pt.value.assign(pt.index.size(), 1.f);
     AppendRows(pt, 0, pt.Size(), &blk_);
   }
@@ -292,46 +308,56 @@ BatchReader::BatchReader(const std::string& path, const std::string& format, int
   DFX_HOST_CHECK(shuf_buf == 0 || shuf_buf >= batch_size, "shuffle buffer < batch size");
 }
 
-// rows for the next batches: the next shuf_buf rows, shuffled (the inner
-// BatchReader(shuf_buf) of batch_reader.cc:18-21), or the next parsed chunk
+// rows for the next batches: the next shuf_buf rows of the reader's chunks, shuffled (the
+// inner BatchReader(shuf_buf) of batch_reader.cc:18-21), or the next parsed chunk itself
 bool BatchReader::Refill() {
-  in_ = RowBlockContainer<feaid_t>();
-  const size_t want = shuf_buf_ ? shuf_buf_ : std::numeric_limits<size_t>::max();
-  while (in_.Size() < want) {
-    if (pend_pos_ >= pending_.Size()) {
+  start_ = 0;
+  order_.clear();
+  if (!shuf_buf_) {
+    do {
+      if (!reader_.Next()) return false;
+    } while (reader_.Value().Size() == 0);
+    src_ = &reader_.Value();
+    order_.resize(src_->Size());
+    for (size_t i = 0; i < order_.size(); ++i) order_[i] = i;
+    return true;
+  }
+  ClearRows(&in_);
+  src_ = &in_;
+  while (in_.Size() < shuf_buf_) {
+    if (pend_pos_ >= reader_.Value().Size()) {
       if (!reader_.Next()) break;
-      pending_ = reader_.Value();
       pend_pos_ = 0;
-      if (!shuf_buf_) {  // no shuffle: batch straight out of the parsed chunk
-        std::swap(in_, pending_);
-        pending_ = RowBlockContainer<feaid_t>();
-        break;
-      }
       continue;
     }
-    const size_t take = std::min(want - in_.Size(), pending_.Size() - pend_pos_);
-    AppendRows(pending_, pend_pos_, pend_pos_ + take, &in_);
+    const size_t take = std::min(shuf_buf_ - in_.Size(), reader_.Value().Size() - pend_pos_);
+    AppendRows(reader_.Value(), pend_pos_, pend_pos_ + take, &in_);
     pend_pos_ += take;
   }
   order_.resize(in_.Size());
   for (size_t i = 0; i < order_.size(); ++i) order_[i] = i;
-  if (shuf_buf_) std::shuffle(order_.begin(), order_.end(), shuffle_rng_);
-  start_ = 0;
+  std::shuffle(order_.begin(), order_.end(), shuffle_rng_);
   return in_.Size() > 0;
 }
 
 bool BatchReader::Next() {
-  batch_ = RowBlockContainer<feaid_t>();
+  ClearRows(&batch_);  // keep the batch's capacity (no fresh pages per batch)
   while (batch_.Size() < batch_size_) {
     if (start_ >= order_.size() && !Refill()) break;
+    if (!shuf_buf_ && neg_sampling_ >= 1.f) {  // rows in file order: one bulk copy
+      const size_t len = std::min(order_.size() - start_, batch_size_ - batch_.Size());
+      AppendRows(*src_, start_, start_ + len, &batch_);
+      start_ += len;
+      continue;
+    }
     while (start_ < order_.size() && batch_.Size() < batch_size_) {
       const size_t j = order_[start_++];
       if (neg_sampling_ < 1.f) {
         // batch_reader.cc:57-63: drop a negative when rand_r / RAND_MAX > 1 - neg_sampling
         const float p = (float)rand_r(&seed_) / (float)RAND_MAX;
-        if (in_.label[j] <= 0 && p > 1 - neg_sampling_) continue;
+        if (src_->label[j] <= 0 && p > 1 - neg_sampling_) continue;
       }
-      AppendRows(in_, j, j + 1, &batch_);
+      AppendRows(*src_, j, j + 1, &batch_);
     }
   }
   // batch_reader.cc:71-73: all-one values mean binary data
@@ -343,6 +369,63 @@ bool BatchReader::Next() {
     }
   if (binary) batch_.value.clear();
   return batch_.Size() > 0;
+}
+
+// ---- ThreadedBatchReader ----------------------------------------------------------------
+ThreadedBatchReader::ThreadedBatchReader(const std::string& path, const std::string& format,
+                                         int part, int nparts, size_t batch_size,
+                                         size_t shuf_buf, float neg_sampling, int nthreads,
+                                         int depth)
+    : reader_(path, format, part, nparts, batch_size, shuf_buf, neg_sampling, nthreads),
+      depth_(depth < 1 ? 1 : (size_t)depth) {
+  free_.resize(depth_ + 1);
+  worker_ = std::thread([this]() { Run(); });
+}
+
+ThreadedBatchReader::~ThreadedBatchReader() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+}
+
+void ThreadedBatchReader::Run() {
+  for (;;) {
+    RowBlockContainer<feaid_t> slot;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this]() { return stop_ || !free_.empty(); });
+      if (stop_) return;
+      slot = std::move(free_.front());
+      free_.pop_front();
+    }
+    const bool more = reader_.Next();
+    if (more) reader_.Swap(&slot);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (more) {
+        full_.push_back(std::move(slot));
+      } else {
+        done_ = true;
+      }
+    }
+    cv_.notify_all();
+    if (!more) return;
+  }
+}
+
+bool ThreadedBatchReader::Next() {
+  std::unique_lock<std::mutex> lk(mu_);
+  free_.push_back(std::move(cur_));  // the caller is done with the previous batch
+  cur_ = RowBlockContainer<feaid_t>();
+  cv_.notify_all();
+  cv_.wait(lk, [this]() { return done_ || !full_.empty(); });
+  if (full_.empty()) return false;
+  cur_ = std::move(full_.front());
+  full_.pop_front();
+  return true;
 }
 
 }  // namespace difacto

@@ -22,8 +22,12 @@
 #ifndef DIFACTO_AMD_HOST_READER_H_
 #define DIFACTO_AMD_HOST_READER_H_
 
+#include <condition_variable>
 #include <cstdint>
+#include <deque>
+#include <mutex>
 #include <random>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -55,6 +59,7 @@ class TextReader {
   size_t begin_ = 0, end_ = 0, pos_ = 0, chunk_, read_ = 0;
   int nthreads_;
   std::vector<char> buf_;
+  std::vector<RowBlockContainer<feaid_t>> parts_;  // per parser thread, reused
   RowBlockContainer<feaid_t> blk_;
 };
 
@@ -65,6 +70,8 @@ class BatchReader {
               size_t batch_size, size_t shuf_buf, float neg_sampling, int nthreads = 8);
   bool Next();
   const RowBlockContainer<feaid_t>& Value() const { return batch_; }
+  /** exchange the current batch with *c (hands the batch over, takes c's buffers) */
+  void Swap(RowBlockContainer<feaid_t>* c) { std::swap(batch_, *c); }
 
  private:
   bool Refill();
@@ -73,12 +80,36 @@ class BatchReader {
   float neg_sampling_;
   unsigned seed_ = 0;  // rand_r state of the negative sampling (batch_reader.cc:58)
   std::mt19937 shuffle_rng_{0};
-  RowBlockContainer<feaid_t> pending_;  // the parsed chunk the shuffle buffer draws from
-  size_t pend_pos_ = 0;
-  RowBlockContainer<feaid_t> in_;  // rows waiting to be batched
+  size_t pend_pos_ = 0;             // rows of the reader's chunk already in the shuffle buffer
+  RowBlockContainer<feaid_t> in_;   // the shuffle buffer
+  const RowBlockContainer<feaid_t>* src_ = nullptr;  // rows being batched (in_ or the chunk)
   std::vector<size_t> order_;
   size_t start_ = 0;
   RowBlockContainer<feaid_t> batch_;
+};
+
+/** a BatchReader on its own thread, `depth` batches ahead: the producer half of
+ * SGDLearner::IterateData (sgd_learner.cc:289-314), where reading and localizing run on one
+ * thread while the executor trains on the previous batch.  Batch buffers are recycled. */
+class ThreadedBatchReader {
+ public:
+  ThreadedBatchReader(const std::string& path, const std::string& format, int part, int nparts,
+                      size_t batch_size, size_t shuf_buf, float neg_sampling, int nthreads = 8,
+                      int depth = 2);
+  ~ThreadedBatchReader();
+  bool Next();
+  const RowBlockContainer<feaid_t>& Value() const { return cur_; }
+
+ private:
+  void Run();
+  BatchReader reader_;
+  std::thread worker_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<RowBlockContainer<feaid_t>> full_, free_;
+  RowBlockContainer<feaid_t> cur_;
+  size_t depth_;
+  bool done_ = false, stop_ = false;
 };
 
 }  // namespace difacto

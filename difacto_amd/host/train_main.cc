@@ -51,8 +51,8 @@ Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_typ
   for (int part = 0; part < P.num_jobs_per_epoch; ++part) {
     if (train) {
       // sgd_learner.cc:273-280
-      BatchReader reader(path, P.data_format, part, P.num_jobs_per_epoch, P.batch_size,
-                         P.batch_size * P.shuffle, P.neg_sampling, P.nthreads);
+      ThreadedBatchReader reader(path, P.data_format, part, P.num_jobs_per_epoch, P.batch_size,
+                                 P.batch_size * P.shuffle, P.neg_sampling, P.nthreads);
       while (reader.Next()) {
         const auto blk = reader.Value().GetBlock();
         learner->ProcessBatch(blk, job_type, epoch == 0);

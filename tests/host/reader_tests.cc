@@ -7,6 +7,7 @@
 // parser's id layout (CityHash64 << 12 | column), criteo_parser.h:40-92.
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <set>
@@ -157,6 +158,33 @@ static void TestShuffleIsPermutation(const std::string& data) {
   EXPECT(rows == 100 && want == got, "shuffled epoch is not a permutation of the rows");
 }
 
+static bool SameBatch(const RowBlockContainer<feaid_t>& a, const RowBlockContainer<feaid_t>& b) {
+  return a.offset == b.offset && a.index == b.index && a.value == b.value && a.label == b.label;
+}
+
+// the prefetching reader hands over exactly the batches of the plain one
+static void TestThreaded(const std::string& data) {
+  for (size_t shuf : {size_t(0), size_t(40)})
+    for (float neg : {1.f, 0.5f})
+      for (size_t bs : {size_t(1), size_t(7), size_t(37), size_t(1000)}) {
+        BatchReader a(data, "libsvm", 0, 1, bs, shuf ? std::max(shuf, bs) : 0, neg, 2);
+        ThreadedBatchReader b(data, "libsvm", 0, 1, bs, shuf ? std::max(shuf, bs) : 0, neg, 3,
+                              2);
+        size_t n = 0;
+        for (;;) {
+          const bool ma = a.Next(), mb = b.Next();
+          EXPECT(ma == mb, "threaded reader: different batch count");
+          if (!ma || !mb) break;
+          EXPECT(SameBatch(a.Value(), b.Value()), "threaded reader: different batch");
+          ++n;
+        }
+        EXPECT(n > 0, "no batches");
+      }
+  // abandoned half way: the destructor stops the worker
+  ThreadedBatchReader c(data, "libsvm", 0, 1, 5, 0, 1.f, 2, 3);
+  EXPECT(c.Next() && c.Value().Size() == 5, "first batch");
+}
+
 static void TestCriteo(const std::string& dir) {
   const std::string path = dir + "/criteo_sample.txt";
   {
@@ -211,6 +239,7 @@ int main(int argc, char** argv) {
   TestChunking(data);
   TestNegSampling(data);
   TestShuffleIsPermutation(data);
+  TestThreaded(data);
   TestCriteo(argv[2]);
   TestCityHash();
   std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
