@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="use the key-range-sharded store even at N=1 (default for N>1)")
+    ap.add_argument("--sync", action="store_true",
+                    help="sharded store: bulk-synchronous steps instead of the pipelined "
+                         "(1-step-stale) schedule")
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-batch", type=int, default=10_000)
     return ap.parse_args()
@@ -282,8 +285,16 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev)
 
+    pipe = None if args.sync else DI.ShardedPipeline([shard], comm)
+    live = []  # a batch stays alive until the submit after the one that took it
+
     def step(batch, push_cnt, mark=None):
-        DI.sharded_step([shard], [batch], comm, H.kTraining, push_cnt=push_cnt, mark=mark)
+        if pipe is None:
+            DI.sharded_step([shard], [batch], comm, H.kTraining, push_cnt=push_cnt, mark=mark)
+        else:
+            pipe.submit([batch], H.kTraining, push_cnt=push_cnt, mark=mark)
+            live.append(batch)
+            del live[:-2]
 
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (world * B * k)))
     for i in range(n_warm_epoch):
@@ -295,7 +306,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     torch.cuda.synchronize()
     H.progress(ctx)
     # per-phase events on the stream everything is ordered on (torch's current stream: the
-    # library's kernels and the wait on each RCCL collective)
+    # library's kernels and the wait on each RCCL collective).  In the pipelined schedule
+    # the phases of neighbouring steps overlap; the marks are in issue order.
     nph = len(DI.PHASES)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nph + 1)]
            for _ in range(args.steps)]
@@ -305,15 +317,21 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     t0 = time.perf_counter()
     for i, bt in enumerate(batches):
         step(bt, False, mark=lambda j, e=evs[i]: e[j + 1].record())
+    if pipe is not None:
+        pipe.flush()
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=comm.cgroup)
     elapsed = float(t.item())
 
+    names = DI.PHASES if pipe is None else DI.PIPE_PHASES
     ph = {p: sum(evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)) / args.steps
-          for j, p in enumerate(DI.PHASES)}
+          for j, p in enumerate(names)}
+    # the worker's forward+backward launch pair (pipelined: including the wait for the record
+    # exchange, so `achieved` is a lower bound)
+    fb_ms = ph["fwd_bwd"] if pipe is None else ph["xchg_pull+fwd_bwd"]
     prog = H.progress(ctx)
     ctx.sync()
     st = H.Store(ctx).stats()
@@ -321,7 +339,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                                float(st["n_vrows"]), float(shard._U)]])[0]
     # roofline of the worker's forward+backward launch pair on this rank
     ab = algorithmic_bytes_sharded(B, B * k, shard._U, d)
-    achieved = ab / (ph["fwd_bwd"] * 1e-3) / 1e9
+    achieved = ab / (fb_ms * 1e-3) / 1e9
     value = world * B * args.steps / elapsed
     out = {
         "metric": "train examples/sec (FM V_dim=16) at 1/8 GPU + achieved HBM GB/s",
@@ -338,14 +356,16 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         "data": "synthetic (device-generated, resident in HBM before timing)",
         "config": {"workload": "C3 Criteo-shaped FM V_dim=%d, %d binary nnz/row, 2^%d keys, "
                                "l1=0 V_threshold=0, key-range-sharded store over %d GPUs "
-                               "(RCCL all-to-all-v)" % (d, k, kb, world),
+                               "(RCCL all-to-all-v), %s schedule"
+                               % (d, k, kb, world,
+                                  "bulk-synchronous" if args.sync else "pipelined 1-step-stale"),
                    "rows_per_gpu_step": B, "global_batch": B * world,
                    "parallelism": "dp%d + model sharded by key range" % world},
         "roofline": {"bound": "hbm", "kernel": "fwd_bwd (dist forward+AUC+backward, rank 0)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "algorithmic_bytes_per_launch": int(ab),
-                     "launch_ms": round(ph["fwd_bwd"], 4)},
+                     "launch_ms": round(fb_ms, 4)},
         "phases_ms_per_step_rank0": {p: round(v, 4) for p, v in ph.items()},
         "train_loss_per_row": round(tot[0] / max(tot[2], 1), 6),
         "train_auc": round(tot[1] / max(tot[2], 1), 6),

@@ -87,12 +87,14 @@ _SIGS = {
                                          ctypes.POINTER(Batch)]),
     "dfx_feeder_consumed": (ctypes.c_int, [vp]),
     "dfx_dist_record_floats": (ctypes.c_int, [vp]),
-    "dfx_dist_localize": (ctypes.c_int, [vp, ctypes.POINTER(Batch), c_u64, ctypes.c_int, vp, vp,
-                                         i64p, i64p]),
-    "dfx_dist_owner_begin": (ctypes.c_int, [vp, vp, i64p, ctypes.c_int, vp]),
-    "dfx_dist_owner_pull": (ctypes.c_int, [vp, vp]),
-    "dfx_dist_fwd_bwd": (ctypes.c_int, [vp, ctypes.POINTER(Batch), vp, ctypes.c_int, vp, vp]),
-    "dfx_dist_owner_push": (ctypes.c_int, [vp, vp]),
+    "dfx_dist_localize": (ctypes.c_int, [vp, ctypes.POINTER(Batch), c_u64, ctypes.c_int,
+                                         ctypes.c_int, vp, vp]),
+    "dfx_dist_localize_wait": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i64p, i64p]),
+    "dfx_dist_owner_begin": (ctypes.c_int, [vp, ctypes.c_int, vp, i64p, ctypes.c_int, vp]),
+    "dfx_dist_owner_pull": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_dist_fwd_bwd": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp,
+                                        ctypes.c_int, vp, vp]),
+    "dfx_dist_owner_push": (ctypes.c_int, [vp, ctypes.c_int, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -124,10 +124,13 @@ int pipeline_init(Context* c) {
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
                         &c->ev_free[0], &c->ev_free[1]})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads}) {
+  for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads, &c->ods[0], &c->ods[1]}) {
     DFX_HIP(hipMalloc(d, sizeof(DevState)));
     DFX_HIP(hipMemset(*d, 0, sizeof(DevState)));
   }
+  for (auto& h : c->dist_host)
+    DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), (kMaxDistRanks + 2) * 8,
+                          hipHostMallocDefault));
   return DFX_OK;
 }
 
@@ -196,10 +199,14 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   release_ws(c->bws[0]);
   release_ws(c->bws[1]);
   release_ws(c->aws);
+  release_ws(c->ows[0]);
+  release_ws(c->ows[1]);
+  for (auto h : c->dist_host)
+    if (h) (void)hipHostFree(h);
   for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_loc[0], c->ev_loc[1],
                        c->ev_free[0], c->ev_free[1]})
     if (e) (void)hipEventDestroy(e);
-  for (DevState* d : {c->bds[0], c->bds[1], c->ads})
+  for (DevState* d : {c->bds[0], c->bds[1], c->ads, c->ods[0], c->ods[1]})
     if (d) (void)hipFree(d);
   if (c->loc_stream) (void)hipStreamDestroy(c->loc_stream);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);

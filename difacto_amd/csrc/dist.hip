@@ -33,7 +33,7 @@
 namespace dfx {
 
 constexpr int kDNT = 256;
-constexpr int kMaxRanks = 64;
+constexpr int kMaxRanks = kMaxDistRanks;
 
 // launchers shared with fm.hip / metric.hip
 int launch_fwd_records(const FwdArgs& a, hipStream_t st, int* nblk);
@@ -62,15 +62,21 @@ __device__ inline int rank_of(const RankOffs& ro, int64_t i) {
 }
 
 // ---- worker: split sorted unique keys by owner --------------------------------------------
-__global__ void k_owner_counts(const uint64_t* uniq, int64_t U, uint32_t nranks,
-                               unsigned long long* counts) {
-  __shared__ unsigned int c[kMaxRanks];
-  if (threadIdx.x < kMaxRanks) c[threadIdx.x] = 0;
-  __syncthreads();
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < U) atomicAdd(&c[owner_of(uniq[u], nranks)], 1u);
-  __syncthreads();
-  if (threadIdx.x < nranks && c[threadIdx.x]) atomicAdd(&counts[threadIdx.x], c[threadIdx.x]);
+// out[r] = first rank u of the sorted unique keys with owner(uniq[u]) >= r (r <= nranks, so
+// out[nranks] = U), out[kMaxRanks + 1] = U
+__global__ void k_owner_splits(const uint64_t* uniq, const DevState* lds, uint32_t nranks,
+                               unsigned long long* out) {
+  const uint32_t U = lds->u_count;
+  const uint32_t r = threadIdx.x;
+  if (r <= nranks) {
+    uint32_t lo = 0, hi = U;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (owner_of(uniq[mid], nranks) < r) lo = mid + 1; else hi = mid;
+    }
+    out[r] = lo;
+  }
+  if (r == 0) out[kMaxRanks + 1] = U;
 }
 
 // ---- worker: positions of the pulled records -----------------------------------------------
@@ -268,10 +274,11 @@ __global__ void k_dist_initv_list(const uint32_t* flags_excl, const uint32_t* ft
 
 // InitV (sgd_updater.cc:144-152) of the q-th draw: seed jumped 3*d*q steps, pool row n_vrows+q
 __global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uint32_t* ftotal,
-                             const uint32_t* segslot, Table T, float scale, DevState* ds) {
+                             const uint32_t* segslot, Table T, float scale, DevState* ds,
+                             const unsigned int* sortmeta) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= (int64_t)*ftotal) return;
-  const uint32_t* rv = ds->sortmeta[31] ? rv1 : rv0;
+  const uint32_t* rv = sortmeta[31] ? rv1 : rv0;
   const int d = T.d;
   uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)q);
   const int64_t vr = (int64_t)ds->n_vrows + q;
@@ -405,37 +412,44 @@ static int vec_group(int d) {
 
 #define DFX_DIST_GROUPS(X) X(1) X(2) X(4) X(8) X(16) X(32) X(64)
 
+// the owner lane of a step slot: the main stream with the slot's owner buffers and state
+static Lane owner_lane(Context* c, int slot) {
+  return Lane{c->stream, &c->ows[slot], c->ods[slot], &c->ds->err};
+}
+
 // InitV of the flagged keys in (pushing rank, key) order, all on the device
-static int owner_initv(Context* c, int nranks) {
-  Workspace& ws = c->ws;
-  const int64_t R = c->dist_R;
+static int owner_initv(Context* c, int slot, int nranks) {
+  const Lane OL = owner_lane(c, slot);
+  Workspace& ws = *OL.ws;
+  const int64_t R = c->dist_R[slot];
   uint32_t* flags = ws.oflags.as<uint32_t>();
-  uint32_t* nuniq = &c->ds->totals[1];
-  uint32_t* ftotal = &c->ds->totals[2];
-  DFX_TRY(scan_u32(c, flags, R, ftotal, nuniq));
+  uint32_t* nuniq = &OL.ds->totals[1];
+  uint32_t* ftotal = &OL.ds->totals[2];
+  DFX_TRY(scan_u32(OL, flags, R, ftotal, nuniq));
   uint32_t* rk0 = ws.vals0.as<uint32_t>();
   uint32_t* rv0 = ws.vals1.as<uint32_t>();
   uint32_t* rk1 = reinterpret_cast<uint32_t*>(ws.keys0.as<uint64_t>());
   uint32_t* rv1 = reinterpret_cast<uint32_t*>(ws.keys1.as<uint64_t>());
   const dim3 grid((R + kDNT - 1) / kDNT);
-  hipLaunchKernelGGL(k_dist_initv_list, grid, dim3(kDNT), 0, c->stream, flags, ftotal,
+  hipLaunchKernelGGL(k_dist_initv_list, grid, dim3(kDNT), 0, OL.stream, flags, ftotal,
                      ws.ofrank.as<uint32_t>(), nuniq, R, rk0, rv0);
   int bits = 0;
   while ((1 << bits) < nranks) ++bits;
   // stable by rank; the tail (0xFF) sorts last and is never read
-  DFX_TRY(radix_sort_pairs<uint32_t>(main_lane(c), rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
-                                     c->ds->sortmeta));
-  hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, c->stream, rv0, rv1, ftotal,
-                     ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds);
-  hipLaunchKernelGGL(k_dist_initv_finalize, dim3(1), dim3(1), 0, c->stream, ftotal, c->P.V_dim,
+  DFX_TRY(radix_sort_pairs<uint32_t>(OL, rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
+                                     OL.ds->sortmeta));
+  hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, OL.stream, rv0, rv1, ftotal,
+                     ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds,
+                     OL.ds->sortmeta);
+  hipLaunchKernelGGL(k_dist_initv_finalize, dim3(1), dim3(1), 0, OL.stream, ftotal, c->P.V_dim,
                      c->T.vcap, c->ds);
   return DFX_OK;
 }
 
-static RankOffs rank_offs(const Context* c) {
+static RankOffs rank_offs(const Context* c, int slot) {
   RankOffs ro{};
-  ro.n = (int)c->dist_offs.size() - 1;
-  for (int r = 0; r <= ro.n; ++r) ro.off[r] = c->dist_offs[r];
+  ro.n = (int)c->dist_offs[slot].size() - 1;
+  for (int r = 0; r <= ro.n; ++r) ro.off[r] = c->dist_offs[slot][r];
   return ro;
 }
 
@@ -447,60 +461,83 @@ extern "C" {
 
 int dfx_dist_record_floats(dfx_ctx* ctx) { return ctx ? rec_floats(ctx->c.P.V_dim) : -1; }
 
+#define DFX_CHECK_SLOT(slot) DFX_CHECK_ARG((slot) == 0 || (slot) == 1, "dist: slot must be 0 or 1")
+
+// Localizer lane: Compact of the batch into the slot's buffers, then the owner splits, copied
+// to pinned memory; dfx_dist_localize_wait joins it on the host
 int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* b, uint64_t max_index, int nranks,
-                      uint64_t* keys_out, float* cnt_out, int64_t* split_counts,
-                      int64_t* n_uniq) {
-  DFX_CHECK_ARG(ctx && b && split_counts && n_uniq, "null argument");
+                      int slot, uint64_t* keys_out, float* cnt_out) {
+  DFX_CHECK_ARG(ctx && b, "null argument");
+  DFX_CHECK_SLOT(slot);
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   DFX_CHECK_ARG(b->size >= 0 && b->nnz >= 0, "dist_localize: negative sizes");
   DFX_CHECK_ARG(b->size == 0 || b->offset, "dist_localize: null offset");
   DFX_CHECK_ARG(b->nnz == 0 || (b->index && keys_out), "dist_localize: null buffer");
   Context* c = &ctx->c;
-  Workspace& ws = c->ws;
+  DFX_TRY(pipeline_init(c));
   const int64_t B = b->size, nnz = b->nnz;
   DFX_TRY(ws_reserve(c, B, nnz));
-  DFX_TRY(loc_reserve(ws, nnz));
-  DFX_TRY(ws.oflags.ensure(kMaxRanks * 8));
+  Workspace& bw = c->bws[slot];
+  DFX_TRY(loc_reserve(bw, nnz));
+  DFX_TRY(bw.ofrank.ensure((kMaxRanks + 2) * 8));
+  const Lane LL{c->loc_stream, &bw, c->bds[slot], &c->ds->err};
+  // the batch is ready on the caller's (input) stream; the slot's buffers are free once the
+  // main stream passed the dfx_dist_fwd_bwd that read them
+  DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_in, 0));
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[slot], 0));
   LocOut o;
   o.uniq = keys_out;
   o.cnt = cnt_out;
-  o.col = ws.col.as<uint32_t>();
-  o.segstart = ws.segstart.as<uint32_t>();
+  o.col = bw.col.as<uint32_t>();
+  o.segstart = bw.segstart.as<uint32_t>();
   o.value = b->value;
-  o.occ_row = ws.occ_row.as<uint32_t>();
-  o.occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
-  DFX_TRY(localize_run(c, main_lane(c), B, nnz, b->offset, b->index, max_index, o));
-  uint32_t u = 0;
-  DFX_HIP(hipMemcpyAsync(&u, &c->ds->u_count, 4, hipMemcpyDeviceToHost, c->stream));
-  DFX_HIP(hipStreamSynchronize(c->stream));
-  unsigned long long* counts = reinterpret_cast<unsigned long long*>(ws.oflags.p);
-  DFX_HIP(hipMemsetAsync(counts, 0, kMaxRanks * 8, c->stream));
-  if (u > 0)
-    hipLaunchKernelGGL(k_owner_counts, dim3((u + 255) / 256), dim3(256), 0, c->stream, keys_out,
-                       (int64_t)u, (uint32_t)nranks, counts);
-  unsigned long long h[kMaxRanks];
-  DFX_HIP(hipMemcpyAsync(h, counts, kMaxRanks * 8, hipMemcpyDeviceToHost, c->stream));
-  DFX_HIP(hipStreamSynchronize(c->stream));
-  for (int r = 0; r < nranks; ++r) split_counts[r] = (int64_t)h[r];
-  *n_uniq = u;
-  c->dist_U = u;
-  c->dist_rows = B;
+  o.occ_row = bw.occ_row.as<uint32_t>();
+  o.occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
+  DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+  unsigned long long* splits = bw.ofrank.as<unsigned long long>();
+  hipLaunchKernelGGL(k_owner_splits, dim3(1), dim3(kMaxRanks + 1), 0, c->loc_stream,
+                     keys_out, c->bds[slot], (uint32_t)nranks, splits);
+  DFX_HIP(hipMemcpyAsync(c->dist_host[slot], splits, (kMaxRanks + 2) * 8,
+                         hipMemcpyDeviceToHost, c->loc_stream));
+  DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
+  DFX_HIP(hipGetLastError());
+  c->dist_rows[slot] = B;
+  c->dist_U[slot] = -1;  // known after dfx_dist_localize_wait
   return DFX_OK;
 }
 
-int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* b, const float* pulled, int job_type,
-                     float* grads_out, float* pred_out) {
+int dfx_dist_localize_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_counts,
+                           int64_t* n_uniq) {
+  DFX_CHECK_ARG(ctx && split_counts && n_uniq, "null argument");
+  DFX_CHECK_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(c->loc_stream, "dist_localize_wait: no dfx_dist_localize issued");
+  DFX_HIP(hipEventSynchronize(c->ev_loc[slot]));
+  const unsigned long long* h = c->dist_host[slot];
+  for (int r = 0; r < nranks; ++r) split_counts[r] = (int64_t)(h[r + 1] - h[r]);
+  *n_uniq = (int64_t)h[kMaxRanks + 1];
+  c->dist_U[slot] = *n_uniq;
+  return DFX_OK;
+}
+
+int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pulled,
+                     int job_type, float* grads_out, float* pred_out) {
   DFX_CHECK_ARG(ctx && b, "null argument");
+  DFX_CHECK_SLOT(slot);
   DFX_CHECK_ARG(job_type == DFX_JOB_TRAINING || job_type == DFX_JOB_VALIDATION ||
                     job_type == DFX_JOB_PREDICTION,
                 "dist_fwd_bwd: bad job type");
   Context* c = &ctx->c;
   Workspace& ws = c->ws;
+  Workspace& bw = c->bws[slot];
   const int d = c->P.V_dim;
   const int64_t B = b->size;
-  DFX_CHECK_ARG(B == c->dist_rows,"dist_fwd_bwd: batch differs from dist_localize's");
+  DFX_CHECK_ARG(c->dist_U[slot] >= 0, "dist_fwd_bwd: dfx_dist_localize_wait first");
+  DFX_CHECK_ARG(B == c->dist_rows[slot], "dist_fwd_bwd: batch differs from dist_localize's");
   DFX_CHECK_ARG(B == 0 || b->label, "dist_fwd_bwd: null label");
-  const int64_t U = c->dist_U;
+  const int64_t U = c->dist_U[slot];
   DFX_CHECK_ARG(U == 0 || pulled, "dist_fwd_bwd: null pulled records");
   const bool train = job_type == DFX_JOB_TRAINING && U > 0;
   DFX_CHECK_ARG(!train || grads_out, "dist_fwd_bwd: grads_out required for training");
@@ -514,7 +551,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* b, const float* pulled, int 
     hipLaunchKernelGGL(k_record_pos, dim3((U + 255) / 256), dim3(256), 0, c->stream, pulled, U,
                        d, wpos, vpos);
   FwdArgs a{};
-  a.B = B; a.offs = b->offset; a.col = ws.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
+  a.B = B; a.offs = b->offset; a.col = bw.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
   a.wpos = wpos; a.vpos = vpos; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
   a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -526,32 +563,37 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* b, const float* pulled, int 
   if (train) {
     DFX_HIP(hipMemsetAsync(grads_out, 0, (size_t)U * S * 4, c->stream));
     BwdArgs g{};
-    g.segstart = ws.segstart.as<uint32_t>(); g.ds = c->ds; g.nseg_host = U; g.segcol = nullptr;
-    g.occ_row = ws.occ_row.as<uint32_t>();
-    g.occ_x = b->value ? ws.occ_x.as<float>() : nullptr;
+    g.segstart = bw.segstart.as<uint32_t>(); g.ds = c->ds; g.nseg_host = U; g.segcol = nullptr;
+    g.occ_row = bw.occ_row.as<uint32_t>();
+    g.occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = ws.p.as<float>(); g.XVp = ws.XVp.as<float>(); g.d = d;
     g.wpos = wpos; g.vpos = vpos; g.W = pulled; g.grad = grads_out;
     DFX_TRY(launch_bwd_positions(g, U, c->stream));
   }
+  // the slot's Localizer buffers may be refilled once the main stream is past this point
+  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t* recv_offsets,
-                         int nranks, const float* recv_cnt) {
+int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
+                         const int64_t* recv_offsets, int nranks, const float* recv_cnt) {
   DFX_CHECK_ARG(ctx && recv_offsets, "null argument");
+  DFX_CHECK_SLOT(slot);
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   Context* c = &ctx->c;
-  Workspace& ws = c->ws;
+  DFX_TRY(pipeline_init(c));
+  const Lane OL = owner_lane(c, slot);
+  Workspace& ws = *OL.ws;
   DFX_CHECK_ARG(recv_offsets[0] == 0, "dist_owner_begin: recv_offsets[0] must be 0");
   for (int r = 0; r < nranks; ++r)
     DFX_CHECK_ARG(recv_offsets[r + 1] >= recv_offsets[r], "dist_owner_begin: bad offsets");
   const int64_t R = recv_offsets[nranks];
   DFX_CHECK_ARG(R < 0x7FFFFFFFll, "dist_owner_begin: too many keys");
   DFX_CHECK_ARG(R == 0 || recv_keys, "dist_owner_begin: null keys");
-  c->dist_R = R;
-  c->dist_offs.assign(recv_offsets, recv_offsets + nranks + 1);
-  DFX_HIP(hipMemsetAsync(&c->ds->totals[1], 0, 8, c->stream));
+  c->dist_R[slot] = R;
+  c->dist_offs[slot].assign(recv_offsets, recv_offsets + nranks + 1);
+  DFX_HIP(hipMemsetAsync(&OL.ds->totals[1], 0, 8, OL.stream));
   if (R == 0) return DFX_OK;
   DFX_TRY(ws.keys0.ensure(R * 8));
   DFX_TRY(ws.keys1.ensure(R * 8));
@@ -564,7 +606,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t*
   DFX_TRY(ws.oseg_of.ensure((R + 1) * 4));
   DFX_TRY(ws.osorted.ensure((R + 1) * 4));
   uint32_t* flags = ws.oflags.as<uint32_t>();
-  uint32_t* nuniq = &c->ds->totals[1];
+  uint32_t* nuniq = &OL.ds->totals[1];
   const dim3 grid((R + kDNT - 1) / kDNT);
   // stable merge of the N sorted runs (none for one run)
   const uint64_t* K = recv_keys;
@@ -587,7 +629,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t*
         pl.n = p + 1;
       }
       next.push_back(runs[m]);
-      hipLaunchKernelGGL(k_merge_pairs, mgrid, dim3(kDNT), 0, c->stream, K, Pm, kb[sel],
+      hipLaunchKernelGGL(k_merge_pairs, mgrid, dim3(kDNT), 0, OL.stream, K, Pm, kb[sel],
                          vb[sel], R, pl);
       K = kb[sel];
       Pm = vb[sel];
@@ -595,72 +637,77 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t*
       runs.swap(next);
     }
   }
-  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, c->stream, K, R, flags);
-  DFX_TRY(scan_u32(c, flags, R, nuniq));
-  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, c->stream, K, Pm, R, c->ds, flags, nuniq,
+  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, OL.stream, K, R, flags);
+  DFX_TRY(scan_u32(OL, flags, R, nuniq));
+  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, OL.stream, K, Pm, R, c->ds, flags, nuniq,
                      c->T, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
                      ws.oseg_of.as<uint32_t>(), ws.osorted.as<uint32_t>());
   if (recv_cnt) {
-    hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, c->stream,
+    hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, OL.stream,
                        ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
-                       ws.osorted.as<uint32_t>(), recv_cnt, rank_offs(c), c->T, c->P, nuniq,
-                       flags, ws.ofrank.as<uint32_t>());
-    if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, nranks));
+                       ws.osorted.as<uint32_t>(), recv_cnt, rank_offs(c, slot), c->T, c->P,
+                       nuniq, flags, ws.ofrank.as<uint32_t>());
+    if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, nranks));
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-int dfx_dist_owner_pull(dfx_ctx* ctx, float* vals_out) {
+int dfx_dist_owner_pull(dfx_ctx* ctx, int slot, float* vals_out) {
   DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_SLOT(slot);
   Context* c = &ctx->c;
-  const int64_t R = c->dist_R;
+  const int64_t R = c->dist_R[slot];
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(vals_out, "dist_owner_pull: null buffer");
+  const Lane OL = owner_lane(c, slot);
   const int G = vec_group(c->P.V_dim);
 #define DFX_PULL(GG)                                                                         \
   if (G == GG) {                                                                             \
     const int64_t per = kDNT / GG;                                                           \
     hipLaunchKernelGGL(k_dist_pull_vec<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0,        \
-                       c->stream, R, c->ws.oseg_of.as<uint32_t>(),                           \
-                       c->ws.osegslot.as<uint32_t>(), c->T, c->P, vals_out);                \
+                       OL.stream, R, OL.ws->oseg_of.as<uint32_t>(),                          \
+                       OL.ws->osegslot.as<uint32_t>(), c->T, c->P, vals_out);               \
   }
   DFX_DIST_GROUPS(DFX_PULL)
 #undef DFX_PULL
   if (G == 0)
-    hipLaunchKernelGGL(k_dist_pull, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream, R,
-                       c->ws.oseg_of.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(), c->T, c->P,
-                       vals_out);
+    hipLaunchKernelGGL(k_dist_pull, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, OL.stream, R,
+                       OL.ws->oseg_of.as<uint32_t>(), OL.ws->osegslot.as<uint32_t>(), c->T,
+                       c->P, vals_out);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-int dfx_dist_owner_push(dfx_ctx* ctx, const float* recv_grads) {
+int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_SLOT(slot);
   Context* c = &ctx->c;
-  const int64_t R = c->dist_R;
+  const int64_t R = c->dist_R[slot];
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(recv_grads, "dist_owner_push: null buffer");
+  const Lane OL = owner_lane(c, slot);
+  Workspace& ws = *OL.ws;
   const int G = vec_group(c->P.V_dim);
-  const RankOffs ro = rank_offs(c);
+  const RankOffs ro = rank_offs(c, slot);
 #define DFX_PUSH(GG)                                                                         \
   if (G == GG) {                                                                             \
     const int64_t per = kDNT / GG;                                                           \
     hipLaunchKernelGGL(k_dist_push_vec<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0,        \
-                       c->stream, c->ws.osegstart.as<uint32_t>(),                            \
-                       c->ws.osegslot.as<uint32_t>(), c->ws.osorted.as<uint32_t>(),          \
-                       recv_grads, ro, c->T, c->P, &c->ds->totals[1],                       \
-                       c->ws.oflags.as<uint32_t>(), c->ws.ofrank.as<uint32_t>(), c->ds);     \
+                       OL.stream, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),   \
+                       ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,               \
+                       &OL.ds->totals[1], ws.oflags.as<uint32_t>(),                          \
+                       ws.ofrank.as<uint32_t>(), c->ds);                                     \
   }
   DFX_DIST_GROUPS(DFX_PUSH)
 #undef DFX_PUSH
   if (G == 0)
-    hipLaunchKernelGGL(k_dist_push, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, c->stream,
-                       c->ws.osegstart.as<uint32_t>(), c->ws.osegslot.as<uint32_t>(),
-                       c->ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,
-                       &c->ds->totals[1], c->ws.oflags.as<uint32_t>(),
-                       c->ws.ofrank.as<uint32_t>(), c->ds);
-  if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, (int)c->dist_offs.size() - 1));
+    hipLaunchKernelGGL(k_dist_push, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, OL.stream,
+                       ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
+                       ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,
+                       &OL.ds->totals[1], ws.oflags.as<uint32_t>(), ws.ofrank.as<uint32_t>(),
+                       c->ds);
+  if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, (int)c->dist_offs[slot].size() - 1));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -68,6 +68,7 @@ struct DevState {
   double scratch[8];
 };
 
+constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
 constexpr int kOsSortTile = 4096;  // radix sort tile (sort.hip)
 constexpr int kOsDigits = 8;       // 8-bit digit positions of a u64 key
 constexpr int kOsParts = 16;       // partial digit-count copies (spread the atomics)
@@ -131,10 +132,15 @@ struct Context {
   std::vector<hipEvent_t> lane_ev;  // prof_max steps x 4: loc start/end, AUC start/end
   double lane_stats[4] = {0, 0, 0, 0};
   int prof_max = 0, prof_n = 0;
-  // sharded store (dist.hip): keys received by this owner in the current step and each
-  // source rank's offset among them; rows and unique keys of this worker's batch
-  int64_t dist_R = 0, dist_rows = 0, dist_U = 0;
-  std::vector<int64_t> dist_offs;
+  // sharded store (dist.hip), per step slot (two steps in flight when pipelined): keys
+  // received by this owner and each source rank's offset among them (owner buffers ows /
+  // state ods), rows and unique keys of this worker's batch (Localizer buffers bws / bds,
+  // shared with the fused step), owner split counts + U of the batch in pinned memory
+  Workspace ows[2];
+  DevState* ods[2] = {nullptr, nullptr};
+  int64_t dist_R[2] = {0, 0}, dist_rows[2] = {0, 0}, dist_U[2] = {-1, -1};
+  std::vector<int64_t> dist_offs[2];
+  unsigned long long* dist_host[2] = {nullptr, nullptr};
   // fused-step pipelining (step.hip): batch t+1's Localizer runs on loc_stream while the main
   // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
   hipStream_t loc_stream = nullptr, aux_stream = nullptr;

@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 from ._lib import check
-from .hotpath import MAX_INDEX, kTraining, _p
+from .hotpath import MAX_INDEX, kTraining, kValidation, _p  # noqa: F401
 
 
 def owner_of(keys_u64, nranks):
@@ -35,65 +35,103 @@ def owner_of(keys_u64, nranks):
 
 
 class Shard:
-    """One rank's device context in the sharded store: worker and key-range server."""
+    """One rank's device context in the sharded store: worker and key-range server.  Every
+    call takes the step slot (0 or 1) whose buffers it uses; two steps can be in flight."""
 
     def __init__(self, ctx, nranks):
         self.ctx = ctx
         self.nranks = int(nranks)
         self.S = _lib.lib().dfx_dist_record_floats(ctx.h)
-        self._U = 0
-        self._R = 0
+        self._U = [0, 0]
+        self._R = [0, 0]
+        # the Localizer lane writes these; they live until the slot's fwd_bwd
+        self._keys = [None, None]
+        self._cnt = [None, None]
+
+    def _slot_buffers(self, slot, n, want_cnt):
+        dev = self.ctx.device
+        grow = self._keys[slot] is None or self._keys[slot].numel() < n
+        grow = grow or (want_cnt and (self._cnt[slot] is None or self._cnt[slot].numel() < n))
+        if grow:
+            if self._keys[slot] is not None and torch.device(dev).type == "cuda":
+                torch.cuda.synchronize(dev)  # the old buffers may still be in use on a lane
+            cap = max(n, 1) + max(n, 1) // 8
+            self._keys[slot] = torch.empty(cap, dtype=torch.int64, device=dev)
+            self._cnt[slot] = torch.empty(cap, dtype=torch.float32, device=dev)
+        return self._keys[slot], (self._cnt[slot] if want_cnt else None)
 
     # worker ---------------------------------------------------------------------------------
-    def localize(self, dblk, want_cnt, max_index=MAX_INDEX):
-        ctx = self.ctx
-        n = max(dblk.nnz, 1)
-        keys = torch.empty(n, dtype=torch.int64, device=ctx.device)
-        cnt = torch.empty(n, dtype=torch.float32, device=ctx.device) if want_cnt else None
+    def localize(self, dblk, want_cnt, slot=0, max_index=MAX_INDEX):
+        """issue Localizer::Compact of the batch on the Localizer lane (asynchronous)"""
+        keys, cnt = self._slot_buffers(slot, dblk.nnz, want_cnt)
+        self._want_cnt = want_cnt
+        b = dblk.as_batch()
+        check(_lib.lib().dfx_dist_localize(self.ctx.h, ctypes.byref(b),
+                                           ctypes.c_uint64(max_index), self.nranks, slot,
+                                           _p(keys), _p(cnt)))
+
+    def localize_wait(self, slot=0):
+        """-> (sorted unique keys, their counts or None, keys per owner rank)"""
         splits = (ctypes.c_int64 * self.nranks)()
         U = ctypes.c_int64(0)
-        b = dblk.as_batch()
-        check(_lib.lib().dfx_dist_localize(ctx.h, ctypes.byref(b), ctypes.c_uint64(max_index),
-                                           self.nranks, _p(keys), _p(cnt), splits,
-                                           ctypes.byref(U)))
-        self._U = U.value
-        return keys[:self._U], (cnt[:self._U] if want_cnt else None), list(splits)
+        check(_lib.lib().dfx_dist_localize_wait(self.ctx.h, slot, self.nranks, splits,
+                                                ctypes.byref(U)))
+        self._U[slot] = U.value
+        cnt = self._cnt[slot][:U.value] if self._want_cnt else None
+        return self._keys[slot][:U.value], cnt, list(splits)
 
-    def fwd_bwd(self, dblk, pulled, job_type, pred=None):
+    def fwd_bwd(self, dblk, pulled, job_type, slot=0, pred=None):
         ctx = self.ctx
+        U = self._U[slot]
         grads = None
         if job_type == kTraining:
-            grads = torch.empty(max(self._U * self.S, 1), dtype=torch.float32, device=ctx.device)
+            grads = torch.empty(max(U * self.S, 1), dtype=torch.float32, device=ctx.device)
         b = dblk.as_batch()
-        check(_lib.lib().dfx_dist_fwd_bwd(ctx.h, ctypes.byref(b), _p(pulled), int(job_type),
-                                          _p(grads), _p(pred)))
-        return None if grads is None else grads[:self._U * self.S]
+        check(_lib.lib().dfx_dist_fwd_bwd(ctx.h, slot, ctypes.byref(b), _p(pulled),
+                                          int(job_type), _p(grads), _p(pred)))
+        return None if grads is None else grads[:U * self.S]
 
     # server ---------------------------------------------------------------------------------
-    def owner_begin(self, recv_keys, recv_splits, recv_cnt=None):
+    def owner_begin(self, recv_keys, recv_splits, recv_cnt=None, slot=0):
         offs = [0]
         for s in recv_splits:
             offs.append(offs[-1] + int(s))
-        self._R = offs[-1]
+        self._R[slot] = offs[-1]
         arr = (ctypes.c_int64 * len(offs))(*offs)
-        check(_lib.lib().dfx_dist_owner_begin(self.ctx.h, _p(recv_keys), arr, self.nranks,
-                                              _p(recv_cnt)))
+        check(_lib.lib().dfx_dist_owner_begin(self.ctx.h, slot, _p(recv_keys), arr,
+                                              self.nranks, _p(recv_cnt)))
 
-    def owner_pull(self):
-        vals = torch.empty(max(self._R * self.S, 1), dtype=torch.float32, device=self.ctx.device)
-        check(_lib.lib().dfx_dist_owner_pull(self.ctx.h, _p(vals)))
-        return vals[:self._R * self.S]
+    def owner_pull(self, slot=0):
+        R = self._R[slot]
+        vals = torch.empty(max(R * self.S, 1), dtype=torch.float32, device=self.ctx.device)
+        check(_lib.lib().dfx_dist_owner_pull(self.ctx.h, slot, _p(vals)))
+        return vals[:R * self.S]
 
-    def owner_push(self, recv_grads):
-        check(_lib.lib().dfx_dist_owner_push(self.ctx.h, _p(recv_grads)))
+    def owner_push(self, recv_grads, slot=0):
+        check(_lib.lib().dfx_dist_owner_push(self.ctx.h, slot, _p(recv_grads)))
+
+
+class _Done:
+    """an exchange that completed when it was issued"""
+
+    def __init__(self, out):
+        self.out = out
+
+    def wait(self):
+        return self.out
 
 
 class TorchComm:
     """Exchange over torch.distributed; this process holds one shard (its rank).
 
-    device: where the count exchange lives (the GPU for nccl/RCCL, cpu for gloo).
+    device: the shard's device (the count exchange always goes through host memory).
     stage_cpu: route device tensors through host memory (gloo between processes that share
-    one GPU — the single-GPU test box; RCCL needs one GPU per rank)."""
+    one GPU — the single-GPU test box; RCCL needs one GPU per rank).
+
+    With the nccl (RCCL) backend the exchanges are asynchronous: records and gradients go
+    over the default group, keys over a second communicator issued from an idle stream, so
+    that step t+1's key exchange neither queues behind step t's gradient exchange nor waits
+    for the compute stream; the split counts go over a gloo group on the host."""
 
     def __init__(self, group=None, device=None, stage_cpu=False):
         import torch.distributed as dist
@@ -103,32 +141,72 @@ class TorchComm:
         self.rank = dist.get_rank(group)
         self.device = device
         self.stage_cpu = stage_cpu
+        self.nccl = dist.get_backend(group) == "nccl"
+        if self.nccl:
+            ranks = list(range(self.world))
+            self.kgroup = dist.new_group(ranks)
+            self.cgroup = dist.new_group(ranks, backend="gloo")
+            self.kstream = torch.cuda.Stream(device=device)
+        else:
+            self.kgroup = self.cgroup = group
 
     def exchange_counts(self, send_splits):
         (s,) = send_splits
-        t = torch.tensor(s, dtype=torch.int64, device=self.device)
-        out = torch.empty_like(t)
-        self.dist.all_to_all_single(out, t, group=self.group)
-        return [out.tolist()]
+        t = torch.tensor(s, dtype=torch.int64)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.cgroup)
+        return [[int(o[self.rank]) for o in out]]
 
-    def alltoallv(self, tensors, send_splits, recv_splits, row=1):
-        (x,), (ss,), (rs,) = tensors, send_splits, recv_splits
+    def _a2a(self, x, ss, rs, row, group, async_op):
         home = x.device
         x = x[:sum(ss) * row]
         if self.stage_cpu:
             x = x.cpu()
         out = torch.empty(sum(rs) * row, dtype=x.dtype, device=x.device)
-        self.dist.all_to_all_single(out, x.contiguous(),
-                                    output_split_sizes=[int(r) * row for r in rs],
-                                    input_split_sizes=[int(s) * row for s in ss],
-                                    group=self.group)
-        return [out.to(home) if self.stage_cpu else out]
+        work = self.dist.all_to_all_single(out, x.contiguous(),
+                                           output_split_sizes=[int(r) * row for r in rs],
+                                           input_split_sizes=[int(s) * row for s in ss],
+                                           group=group, async_op=async_op)
+        if self.stage_cpu:
+            out = out.to(home)
+        return out, work
+
+    def alltoallv(self, tensors, send_splits, recv_splits, row=1):
+        return self.alltoallv_async(tensors, send_splits, recv_splits, row).wait()
+
+    def alltoallv_async(self, tensors, send_splits, recv_splits, row=1):
+        """-> handle whose wait() returns [received tensor] (the current stream then waits
+        for the exchange)"""
+        (x,), (ss,), (rs,) = tensors, send_splits, recv_splits
+        if not self.nccl:
+            return _Done([self._a2a(x, ss, rs, row, self.group, False)[0]])
+        out, work = self._a2a(x, ss, rs, row, self.group, True)
+        return _Work(work, [out])
+
+    def alltoallv_keys_async(self, tensors, send_splits, recv_splits, row=1):
+        """the key exchange: its inputs are complete (the host joined the Localizer lane), so
+        it is issued from an idle stream over the second communicator"""
+        (x,), (ss,), (rs,) = tensors, send_splits, recv_splits
+        if not self.nccl:
+            return _Done([self._a2a(x, ss, rs, row, self.kgroup, False)[0]])
+        with torch.cuda.stream(self.kstream):
+            out, work = self._a2a(x, ss, rs, row, self.kgroup, True)
+        return _Work(work, [out])
 
     def allreduce_sum(self, values):
         (v,) = values
-        t = torch.tensor(v, dtype=torch.float64, device=self.device)
-        self.dist.all_reduce(t, group=self.group)
+        t = torch.tensor(v, dtype=torch.float64)
+        self.dist.all_reduce(t, group=self.cgroup)
         return [t.tolist()]
+
+
+class _Work:
+    def __init__(self, work, out):
+        self.work, self.out = work, out
+
+    def wait(self):
+        self.work.wait()  # the current stream waits for the exchange
+        return self.out
 
 
 class LoopbackComm:
@@ -153,6 +231,11 @@ class LoopbackComm:
             out.append(torch.cat(parts) if parts else tensors[g][:0])
         return out
 
+    def alltoallv_async(self, tensors, send_splits, recv_splits, row=1):
+        return _Done(self.alltoallv(tensors, send_splits, recv_splits, row))
+
+    alltoallv_keys_async = alltoallv_async
+
     def allreduce_sum(self, values):
         tot = [sum(v[i] for v in values) for i in range(len(values[0]))]
         return [list(tot) for _ in values]
@@ -160,20 +243,27 @@ class LoopbackComm:
 
 PHASES = ("localize", "xchg_keys", "owner_begin", "owner_pull", "xchg_pull", "fwd_bwd",
           "xchg_grads", "owner_push")
+# ShardedPipeline.submit's marks: the previous step's push sits between the pull and the
+# forward/backward, which starts after the record exchange
+PIPE_PHASES = ("localize", "xchg_keys", "owner_begin", "owner_pull", "owner_push_prev",
+               "xchg_pull+fwd_bwd", "xchg_grads_issue", "end")
 
 
 def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index=MAX_INDEX,
                  preds=None, mark=None):
-    """One synchronous step of the sharded store.  shards / dblks (/ preds): this process's
-    shards and their batches (one each under torch.distributed, N under LoopbackComm).
-    push_cnt: epoch-0 Update(kFeaCount) (sgd_learner.cc:272, 304-307); ignored when V_dim == 0
-    like the reference's do_embedding_.  mark(i): called after phase PHASES[i] is issued
-    (and with -1 first), e.g. to record stream events."""
+    """One bulk-synchronous step of the sharded store (oracle: ShardedOracle.step).  shards /
+    dblks (/ preds): this process's shards and their batches (one each under
+    torch.distributed, N under LoopbackComm).  push_cnt: epoch-0 Update(kFeaCount)
+    (sgd_learner.cc:272, 304-307); ignored when V_dim == 0 like the reference's
+    do_embedding_.  mark(i): called after phase PHASES[i] is issued (and with -1 first), e.g.
+    to record stream events."""
     mark = mark or (lambda i: None)
     mark(-1)
     n = len(shards)
     want_cnt = bool(push_cnt) and shards[0].ctx.V_dim > 0
-    loc = [shards[i].localize(dblks[i], want_cnt, max_index) for i in range(n)]
+    for i in range(n):
+        shards[i].localize(dblks[i], want_cnt, 0, max_index)
+    loc = [shards[i].localize_wait(0) for i in range(n)]
     mark(0)
     send = [l[2] for l in loc]
     recv = comm.exchange_counts(send)
@@ -181,22 +271,95 @@ def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_in
     rcnt = comm.alltoallv([l[1] for l in loc], send, recv) if want_cnt else [None] * n
     mark(1)
     for i in range(n):
-        shards[i].owner_begin(rkeys[i], recv[i], rcnt[i])
+        shards[i].owner_begin(rkeys[i], recv[i], rcnt[i], 0)
     mark(2)
     S = shards[0].S
-    vals = [s.owner_pull() for s in shards]
+    vals = [s.owner_pull(0) for s in shards]
     mark(3)
     pulled = comm.alltoallv(vals, recv, send, S)
     mark(4)
-    grads = [shards[i].fwd_bwd(dblks[i], pulled[i], job_type, preds[i] if preds else None)
+    grads = [shards[i].fwd_bwd(dblks[i], pulled[i], job_type, 0, preds[i] if preds else None)
              for i in range(n)]
     mark(5)
     if job_type == kTraining:
         rgrads = comm.alltoallv(grads, send, recv, S)
         mark(6)
         for i in range(n):
-            shards[i].owner_push(rgrads[i])
+            shards[i].owner_push(rgrads[i], 0)
     else:
         mark(6)
     mark(7)
     return [sum(s) for s in recv]  # keys served per shard (for accounting)
+
+
+class ShardedPipeline:
+    """The pipelined (1-step-stale) schedule of the sharded store (oracle: StaleOracle).
+
+    submit(step t+1) issues, in order:
+      Localizer lane   localize(t+1) into slot (t+1) % 2, beside step t's forward/backward
+      host             join it; exchange the split counts
+      exchange         keys(t+1) (+ counts) to their owners
+      main stream      owner_begin(t+1), owner_pull(t+1)       beside step t's gradient exchange
+      exchange         records(t+1) back to the workers
+      main stream      owner_push(t)                          beside the record exchange
+      main stream      fwd_bwd(t+1); exchange gradients(t+1)  (pending until the next submit)
+    so every pull is answered before the previous step's push: pulls are at most one step
+    stale, the reference's two batches in flight against an asynchronous server
+    (sgd_learner.cc:310-312, kvstore_dist.h:137-150).  flush() applies the last push.
+    A batch must stay alive until the submit after the one that took it."""
+
+    def __init__(self, shards, comm, max_index=MAX_INDEX):
+        self.shards, self.comm, self.max_index = shards, comm, max_index
+        self.slot = 0
+        self.pending = None
+
+    def submit(self, dblks, job_type=kTraining, push_cnt=False, preds=None, mark=None):
+        mark = mark or (lambda i: None)
+        mark(-1)
+        shards, comm = self.shards, self.comm
+        n = len(shards)
+        s = self.slot
+        self.slot ^= 1
+        want_cnt = bool(push_cnt) and shards[0].ctx.V_dim > 0
+        for i in range(n):
+            shards[i].localize(dblks[i], want_cnt, s, self.max_index)
+        loc = [shards[i].localize_wait(s) for i in range(n)]
+        mark(0)
+        send = [l[2] for l in loc]
+        recv = comm.exchange_counts(send)
+        hk = comm.alltoallv_keys_async([l[0] for l in loc], send, recv)
+        hc = comm.alltoallv_keys_async([l[1] for l in loc], send, recv) if want_cnt else None
+        rkeys = hk.wait()
+        rcnt = hc.wait() if hc else [None] * n
+        mark(1)
+        for i in range(n):
+            shards[i].owner_begin(rkeys[i], recv[i], rcnt[i], s)
+        mark(2)
+        S = shards[0].S
+        vals = [sh.owner_pull(s) for sh in shards]
+        mark(3)
+        hr = comm.alltoallv_async(vals, recv, send, S)
+        self._push_pending()
+        mark(4)
+        pulled = hr.wait()
+        grads = [shards[i].fwd_bwd(dblks[i], pulled[i], job_type, s, preds[i] if preds else None)
+                 for i in range(n)]
+        mark(5)
+        if job_type == kTraining:
+            self.pending = (s, comm.alltoallv_async(grads, send, recv, S), dblks)
+        mark(6)
+        mark(7)
+        return [sum(x) for x in recv]
+
+    def _push_pending(self):
+        if self.pending is None:
+            return
+        s, hg, _ = self.pending
+        self.pending = None
+        rgrads = hg.wait()
+        for i, sh in enumerate(self.shards):
+            sh.owner_push(rgrads[i], s)
+
+    def flush(self):
+        """apply the last step's push"""
+        self._push_pending()

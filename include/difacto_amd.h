@@ -201,35 +201,43 @@ int dfx_prof_lanes(dfx_ctx* ctx, double* out);
 
 /* ---- key-range-sharded store over N GPUs (KVStoreDist, src/store/kvstore_dist.h) --------
  * Every rank is a worker (its own batch) and the server of the keys with
- * floor(key * N / 2^64) == rank.  One synchronous step, collectives in between done by the
- * caller (torch.distributed over RCCL, see difacto_amd/dist.py):
- *   dfx_dist_localize     Localizer::Compact; keys_out[U] sorted unique keys, cnt_out[U]
- *                         their occurrence counts (NULL: skip), split_counts[nranks] (host)
- *                         the number of keys each rank owns; *n_uniq = U (synchronises)
+ * floor(key * N / 2^64) == rank.  A step is the sequence below, the collectives in between
+ * done by the caller (torch.distributed over RCCL, see difacto_amd/dist.py).  slot (0 or 1)
+ * selects one of two sets of step buffers, so that two steps can be in flight: the
+ * pipelined schedule issues step t+1's localize / begin / pull before step t's push
+ * (dist.py ShardedPipeline); the synchronous schedule can use one slot throughout.
+ *   dfx_dist_localize      Localizer::Compact on the Localizer lane (asynchronous): keys_out
+ *                          sorted unique keys, cnt_out their occurrence counts (NULL: skip);
+ *                          both need room for nnz entries and stay in use until the step's
+ *                          dfx_dist_fwd_bwd
+ *   dfx_dist_localize_wait host join: split_counts[nranks] the number of keys each rank owns
+ *                          (they are contiguous in keys_out), *n_uniq = U
  *   -> alltoallv keys (+ counts) to their owners
- *   dfx_dist_owner_begin  recv_keys: the concatenation of what every rank sent, in rank
- *                         order, recv_offsets[nranks+1] (host) its rank boundaries; with
- *                         recv_cnt the ranks' Update(kFeaCount) pushes in rank order
- *                         (kvstore_dist.h:158-165) and their InitV draws
- *   dfx_dist_owner_pull   Get per received key (kvstore_dist.h:167-175): vals_out[R*S]
- *                         records of S = dfx_dist_record_floats() floats [V | w | live | 0 0]
+ *   dfx_dist_owner_begin   recv_keys: the concatenation of what every rank sent, in rank
+ *                          order, recv_offsets[nranks+1] (host) its rank boundaries; with
+ *                          recv_cnt the ranks' Update(kFeaCount) pushes in rank order
+ *                          (kvstore_dist.h:158-165) and their InitV draws
+ *   dfx_dist_owner_pull    Get per received key (kvstore_dist.h:167-175): vals_out[R*S]
+ *                          records of S = dfx_dist_record_floats() floats [V | w | live | 0 0]
  *   -> alltoallv records back
- *   dfx_dist_fwd_bwd      forward + Evaluate + AUC of this worker's batch (progress on the
- *                         device), and for training CalcGrad into grads_out[U*S] records
- *                         [gV | gw | 0 0 0]; pred_out optional device B floats
+ *   dfx_dist_fwd_bwd       forward + Evaluate + AUC of this worker's batch (progress on the
+ *                          device), and for training CalcGrad into grads_out[U*S] records
+ *                          [gV | gw | 0 0 0]; pred_out optional device B floats
  *   -> alltoallv gradient records to their owners
- *   dfx_dist_owner_push   the ranks' Update(kGradient) pushes in rank order
- * All arrays except split_counts / recv_offsets are device pointers. */
+ *   dfx_dist_owner_push    the ranks' Update(kGradient) pushes in rank order
+ * Owner calls run on the context stream in call order.  All arrays except split_counts /
+ * recv_offsets are device pointers. */
 int dfx_dist_record_floats(dfx_ctx* ctx);
 int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* batch, uint64_t max_index, int nranks,
-                      uint64_t* keys_out, float* cnt_out, int64_t* split_counts,
-                      int64_t* n_uniq);
-int dfx_dist_owner_begin(dfx_ctx* ctx, const uint64_t* recv_keys, const int64_t* recv_offsets,
-                         int nranks, const float* recv_cnt);
-int dfx_dist_owner_pull(dfx_ctx* ctx, float* vals_out);
-int dfx_dist_fwd_bwd(dfx_ctx* ctx, const dfx_batch* batch, const float* pulled, int job_type,
-                     float* grads_out, float* pred_out);
-int dfx_dist_owner_push(dfx_ctx* ctx, const float* recv_grads);
+                      int slot, uint64_t* keys_out, float* cnt_out);
+int dfx_dist_localize_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_counts,
+                           int64_t* n_uniq);
+int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
+                         const int64_t* recv_offsets, int nranks, const float* recv_cnt);
+int dfx_dist_owner_pull(dfx_ctx* ctx, int slot, float* vals_out);
+int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* pulled,
+                     int job_type, float* grads_out, float* pred_out);
+int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads);
 
 #ifdef __cplusplus
 }

@@ -182,3 +182,100 @@ def test_sharded_oracle_one_server_is_the_local_step():
         if a[1] is not None:
             assert np.array_equal(a[1], b[1])
     assert up.seed == so.up[0].seed
+
+
+# ---- the pipelined (1-step-stale) schedule ---------------------------------------------------
+# job per step: (job type, push_cnt); a validation step in the middle checks that it neither
+# pushes nor loses the pending push
+_PIPE_JOBS = [(DI.kTraining, True), (DI.kTraining, True), (DI.kTraining, False),
+              (DI.kValidation, False), (DI.kTraining, False)]
+
+
+def _run_stale_oracle(batches, nranks):
+    so = DO.StaleOracle(nranks, **KW)
+    losses = []
+    for step, (job, cnt) in zip(batches, _PIPE_JOBS):
+        out = so.submit(step, push_cnt=cnt, train=job == DI.kTraining)
+        losses.append([o[0] for o in out])
+    so.flush()
+    return so, losses
+
+
+def test_stale_oracle_differs_from_synchronous():
+    """the pipelined schedule is a different (stale-by-one) schedule, not a relabelling"""
+    batches = _batches(2, 4)
+    a, la = _run_oracle(batches, 2, 2)
+    b = DO.StaleOracle(2, **KW)
+    lb = [[o[0] for o in b.submit(step, push_cnt=s < 2)] for s, step in enumerate(batches)]
+    b.flush()
+    assert la[0] == lb[0]  # the first pull sees the same (empty) model
+    assert la[1] != lb[1]
+
+
+def test_loopback_cpu_pipeline_matches_stale_oracle():
+    N = 3
+    batches = _batches(N, len(_PIPE_JOBS))
+    shards = [CpuShard(N, **KW) for _ in range(N)]
+    pipe = DI.ShardedPipeline(shards, DI.LoopbackComm(N))
+    for step, (job, cnt) in zip(batches, _PIPE_JOBS):
+        pipe.submit(step, job, push_cnt=cnt)
+    pipe.flush()
+    so, losses = _run_stale_oracle(batches, N)
+    for r in range(N):
+        assert shards[r].losses == [l[r] for l in losses]
+    assert _check_against_oracle(shards, so.so, batches) > 0
+
+
+def _gloo_pipe_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shard = CpuShard(world, **KW)
+        pipe = DI.ShardedPipeline([shard], DI.TorchComm(device="cpu"))
+        batches = _batches(world, len(_PIPE_JOBS))
+        for step, (job, cnt) in zip(batches, _PIPE_JOBS):
+            pipe.submit([step[rank]], job, push_cnt=cnt)
+        pipe.flush()
+        keys = _all_keys(batches)
+        own = keys[DO.owner_of(keys, world) == rank]
+        st = {int(k): v for k, v in _state(shard, own).items()}
+        q.put((rank, shard.losses, st, shard.up.seed, shard.up.new_w))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_pipeline_matches_stale_oracle():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_pipe_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, losses, st, seed, new_w = q.get(timeout=240)
+            res[r] = (losses, st, seed, new_w)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    so, losses = _run_stale_oracle(_batches(world, len(_PIPE_JOBS)), world)
+    for r in range(world):
+        rl, st, seed, new_w = res[r]
+        assert rl == [l[r] for l in losses]
+        assert seed == so.up[r].seed and new_w == so.up[r].new_w
+        n_v = 0
+        for k, (s, V) in st.items():
+            e = so.up[r].entry(k)
+            assert e is not None and np.array_equal(s, e[0])
+            assert (V is None) == (e[1] is None)
+            if V is not None:
+                n_v += 1
+                assert np.array_equal(V, e[1])
+        assert n_v > 0

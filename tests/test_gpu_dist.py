@@ -91,6 +91,62 @@ def test_sharded_loopback_matches_sharded_oracle(name):
         c.close()
 
 
+PIPE_JOBS = [(3, True), (3, True), (3, False), (4, False), (3, False), (3, False)]
+
+
+@pytest.mark.parametrize("name", ["fm_v4", "fm_v16", "logit", "fm_v8_n6"])
+def test_sharded_pipeline_matches_stale_oracle(name):
+    """the pipelined schedule (two step slots in flight, Localizer lane ahead, push of step t
+    after the pull of step t+1) against oracle/dist_oracle.StaleOracle"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS[name]
+    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    pipe = DI.ShardedPipeline(shards, DI.LoopbackComm(N))
+    so = DO.StaleOracle(N, **kw)
+    batches = _batches(N, len(PIPE_JOBS))
+    live = []  # batches stay alive until the submit after the one that took them
+    for s, (step, (job, cnt)) in enumerate(zip(batches, PIPE_JOBS)):
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        preds = [torch.zeros(step[r].size, dtype=torch.float32, device=ctxs[r].device)
+                 for r in range(N)]
+        pipe.submit(dbs, job, push_cnt=cnt, preds=preds)
+        live.append(dbs)
+        out = so.submit(step, push_cnt=cnt, train=job == 3)
+        for r in range(N):
+            assert close(preds[r].cpu().numpy(), out[r][2]), (name, s, r)
+            pr = H.progress(ctxs[r])
+            assert pr["loss"] == pytest.approx(out[r][0], rel=1e-4)
+    pipe.flush()
+    so.flush()
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
+                                     for step in batches for b in step]))
+    n_v = 0
+    for g in range(N):
+        ctxs[g].sync()
+        st = H.Store(ctxs[g]).stats()
+        assert st["seed"] == so.up[g].seed, (name, g)
+        assert st["n_keys"] == so.up[g].size(), (name, g)
+        assert st["new_w"] == so.up[g].new_w, (name, g)
+        own = keys[DO.owner_of(keys, N) == g]
+        for k in own[:: max(1, len(own) // 150)]:
+            e = so.up[g].entry(k)
+            got = H.Store(ctxs[g]).entry(k)
+            assert (got is None) == (e is None)
+            if e is None:
+                continue
+            assert close(got[0], e[0]), (name, g, k)
+            assert (got[1] is None) == (e[1] is None), (name, g, k)
+            if e[1] is not None:
+                n_v += 1
+                assert close(got[1], e[1]), (name, g, k)
+    if kw.get("V_dim", 0) > 0:
+        assert n_v > 0
+    for c in ctxs:
+        c.close()
+
+
 def test_sharded_validation_does_not_update():
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
@@ -138,7 +194,7 @@ def test_sharded_empty_shard_and_batch():
         c.close()
 
 
-def _mp_worker(rank, world, port, q):
+def _mp_worker(rank, world, port, q, pipelined=False):
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -151,12 +207,19 @@ def _mp_worker(rank, world, port, q):
         ctx = H.Context(0, max_keys=1 << 15, **kw)
         shard = DI.Shard(ctx, world)
         comm = DI.TorchComm(device="cpu", stage_cpu=True)
-        preds = []
+        pipe = DI.ShardedPipeline([shard], comm) if pipelined else None
+        preds, live = [], []
         for s, step in enumerate(_batches(world, 4)):
             db = H.DeviceRowBlock(ctx, step[rank])
+            live.append(db)
             pred = torch.zeros(step[rank].size, dtype=torch.float32, device=ctx.device)
-            DI.sharded_step([shard], [db], comm, H.kTraining, push_cnt=s < 2, preds=[pred])
+            if pipe:
+                pipe.submit([db], H.kTraining, push_cnt=s < 2, preds=[pred])
+            else:
+                DI.sharded_step([shard], [db], comm, H.kTraining, push_cnt=s < 2, preds=[pred])
             preds.append(pred.cpu().numpy())
+        if pipe:
+            pipe.flush()
         ctx.sync()
         q.put((rank, preds, H.Store(ctx).stats()))
         ctx.close()
@@ -164,9 +227,11 @@ def _mp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_two_processes_one_gpu():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_sharded_two_processes_one_gpu(pipelined):
     """world_size 2 through torch.distributed with each process's shard on the GPU (the
-    exchange staged through host memory over gloo, since RCCL needs a GPU per rank)"""
+    exchange staged through host memory over gloo, since RCCL needs a GPU per rank), in the
+    synchronous and the pipelined schedule"""
     import socket
     import torch.multiprocessing as mp
     world = 2
@@ -176,7 +241,8 @@ def test_sharded_two_processes_one_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_mp_worker, args=(r, world, port, q, pipelined))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -189,8 +255,13 @@ def test_sharded_two_processes_one_gpu():
             p.join(timeout=30)
     assert all(p.exitcode == 0 for p in procs)
     _, kw = CFGS["fm_v4"]
-    so = DO.ShardedOracle(world, **kw)
-    outs = [so.step(step, push_cnt=s < 2) for s, step in enumerate(_batches(world, 4))]
+    if pipelined:
+        so = DO.StaleOracle(world, **kw)
+        outs = [so.submit(step, push_cnt=s < 2) for s, step in enumerate(_batches(world, 4))]
+        so.flush()
+    else:
+        so = DO.ShardedOracle(world, **kw)
+        outs = [so.step(step, push_cnt=s < 2) for s, step in enumerate(_batches(world, 4))]
     for r in range(world):
         preds, st = res[r]
         for s in range(4):
