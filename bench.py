@@ -336,9 +336,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     ctx.sync()
     st = H.Store(ctx).stats()
     tot = comm.allreduce_sum([[prog["loss"], prog["auc"], prog["nrows"], float(st["n_keys"]),
-                               float(st["n_vrows"]), float(shard._U)]])[0]
+                               float(st["n_vrows"]), float(max(shard._U))]])[0]
     # roofline of the worker's forward+backward launch pair on this rank
-    ab = algorithmic_bytes_sharded(B, B * k, shard._U, d)
+    ab = algorithmic_bytes_sharded(B, B * k, max(shard._U), d)
     achieved = ab / (fb_ms * 1e-3) / 1e9
     value = world * B * args.steps / elapsed
     out = {

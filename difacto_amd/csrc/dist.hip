@@ -79,15 +79,6 @@ __global__ void k_owner_splits(const uint64_t* uniq, const DevState* lds, uint32
   if (r == 0) out[kMaxRanks + 1] = U;
 }
 
-// ---- worker: positions of the pulled records -----------------------------------------------
-__global__ void k_record_pos(const float* rec, int64_t U, int d, int32_t* wpos, int32_t* vpos) {
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= U) return;
-  const int64_t S = rec_floats(d);
-  wpos[u] = (int32_t)(u * S + d);
-  vpos[u] = (d > 0 && rec[u * S + d + 1] != 0.f) ? (int32_t)(u * S) : -1;
-}
-
 __global__ void k_dist_worker_finalize(DevState* ds, int64_t B) {
   ds->prog[0] += (double)B;  // sgd::Progress of this worker (sgd_learner.cc:213-229)
   ds->prog[1] += ds->scratch[3];
@@ -211,8 +202,8 @@ __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
 }
 
 // The ranks' Update(kGradient) pushes in rank order (sgd_updater.cc:76-100): per pushing rank,
-// UpdateW (FTRL) and, when the rank pulled V (lens > 1), UpdateV (AdaGrad).  V was pulled iff
-// present and not (l1_shrk && w == 0) when the step's pulls were answered, before any push.
+// UpdateW (FTRL) and, when the rank pulled V (lens > 1: the record's live slot), UpdateV
+// (AdaGrad).  A V pulled by any rank exists at push time (V rows are never freed).
 __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
                             const uint32_t* sorted_idx, const float* g, RankOffs ro, Table T,
                             Params P, const uint32_t* nuniq, uint32_t* flags, uint32_t* frank,
@@ -225,10 +216,9 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
     Entry* en = &T.ent[segslot[u]];
     float4 e = ent_state(en);
     const int vr = en->vrow;
-    const bool pulled_v = vr >= 0 && !(P.l1_shrk && e.x == 0.f);
     bool has_v = vr >= 0;
-    float* V = pulled_v ? row_V(T, vr) : nullptr;
-    float* C = pulled_v ? row_C(T, vr) : nullptr;
+    float* V = has_v ? row_V(T, vr) : nullptr;
+    float* C = has_v ? row_C(T, vr) : nullptr;
     uint32_t f = 0, fr = 0;
     for (uint32_t i = segstart[u]; i < segstart[u + 1]; ++i) {
       const uint32_t src = sorted_idx[i];
@@ -240,7 +230,7 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
         f = 1;
         fr = (uint32_t)rank_of(ro, src);
       }
-      if (pulled_v)
+      if (d > 0 && gr[d + 1] != 0.f && V)
         for (int k = 0; k < d; ++k) adagrad_update(P, gr[k], V + k, C + k);
     }
     ent_set_state(en, e);
@@ -359,7 +349,6 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart
     Entry* en = &T.ent[segslot[u]];
     float4 e = ent_state(en);
     const int vr = en->vrow;
-    const bool pulled_v = vr >= 0 && !(P.l1_shrk && e.x == 0.f);
     bool has_v = vr >= 0;
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
     // UpdateW per pushing rank; every lane of the group runs the same sequence
@@ -380,14 +369,16 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart
       flags[u] = f;
       frank[u] = fr;
     }
-    // UpdateV per pushing rank (each coordinate independent)
-    if (pulled_v) {
+    // UpdateV per pushing rank that pulled V (each coordinate independent)
+    if (vr >= 0) {
       float4* V4 = reinterpret_cast<float4*>(row_V(T, vr));
       float4* C4 = reinterpret_cast<float4*>(row_C(T, vr));
       for (int c = l; c < nc; c += G) {
         float4 v = V4[c], cg = C4[c];
         for (uint32_t i = s0; i < s1; ++i) {
-          const float4 gv = reinterpret_cast<const float4*>(g + (int64_t)sorted_idx[i] * S)[c];
+          const float* gr = g + (int64_t)sorted_idx[i] * S;
+          if (gr[d + 1] == 0.f) continue;
+          const float4 gv = reinterpret_cast<const float4*>(gr)[c];
           adagrad_update(P, gv.x, &v.x, &cg.x);
           adagrad_update(P, gv.y, &v.y, &cg.y);
           adagrad_update(P, gv.z, &v.z, &cg.z);
@@ -542,17 +533,10 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   const bool train = job_type == DFX_JOB_TRAINING && U > 0;
   DFX_CHECK_ARG(!train || grads_out, "dist_fwd_bwd: grads_out required for training");
   const int64_t S = rec_floats(d);
-  DFX_TRY(ws.vpos.ensure((U + 1) * 4));
-  DFX_TRY(ws.wb.ensure((U + 1) * 4));
-  int32_t* wpos = ws.wb.as<int32_t>();
-  int32_t* vpos = ws.vpos.as<int32_t>();
   float* pred = pred_out ? pred_out : ws.pred.as<float>();
-  if (U > 0)
-    hipLaunchKernelGGL(k_record_pos, dim3((U + 255) / 256), dim3(256), 0, c->stream, pulled, U,
-                       d, wpos, vpos);
   FwdArgs a{};
   a.B = B; a.offs = b->offset; a.col = bw.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
-  a.wpos = wpos; a.vpos = vpos; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
+  a.rec_S = (int)S; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
   a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
   a.loss_part = ws.dscratch.as<double>() + 8;
   int nblk = 0;
@@ -561,13 +545,14 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   DFX_TRY(auc_run(main_lane(c), B, b->label, pred, &c->ds->auc_n));
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {
-    DFX_HIP(hipMemsetAsync(grads_out, 0, (size_t)U * S * 4, c->stream));
+    // every gradient record is written whole, the live slot carrying whether this worker
+    // pulled V (the lens of its push: the server updates V only then, sgd_updater.cc:89-98)
     BwdArgs g{};
     g.segstart = bw.segstart.as<uint32_t>(); g.ds = c->ds; g.nseg_host = U; g.segcol = nullptr;
     g.occ_row = bw.occ_row.as<uint32_t>();
     g.occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = ws.p.as<float>(); g.XVp = ws.XVp.as<float>(); g.d = d;
-    g.wpos = wpos; g.vpos = vpos; g.W = pulled; g.grad = grads_out;
+    g.rec_S = (int)S; g.W = pulled; g.grad = grads_out;
     DFX_TRY(launch_bwd_positions(g, U, c->stream));
   }
   // the slot's Localizer buffers may be refilled once the main stream is past this point

@@ -124,6 +124,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           w[t] = __int_as_float(wr[t].x);
           const int vr = wr[t].y;
           vp[t] = (vr >= 0 && !(a.l1_shrk && w[t] == 0.f)) ? vr : -1;
+        } else if (a.rec_S) {
+          // the pulled record: w and live follow V
+          const int64_t rb = (int64_t)c[t] * a.rec_S;
+          w[t] = a.W[rb + d];
+          vp[t] = (d > 0 && a.W[rb + d + 1] != 0.f) ? (int)rb : -1;
         } else {
           if (a.wpos) {
             const int q = a.wpos[c[t]];
@@ -321,6 +326,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       const Entry* en = a.T.ent + sl;
       h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
       fc = en->fea_cnt;
+    } else if (a.rec_S) {
+      wq = (int)((int64_t)cidx * a.rec_S + d);
+      vq = (d > 0 && a.W[wq + 1] != 0.f) ? (int)((int64_t)cidx * a.rec_S) : -1;
     } else {
       wq = a.wpos ? a.wpos[cidx] : (int)cidx;
       vq = d > 0 ? a.vpos[cidx] : -1;
@@ -347,6 +355,13 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) g0[k] = 0.f;
+    } else if (a.rec_S) {
+      load_coords<CPL, VEC>(vq >= 0 ? a.W + vq : zp, l, d, vcur);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        g0[k] = 0.f;
+        ccur[k] = 0.f;
+      }
     } else {
       gw = a.grad[wq < 0 ? 0 : wq];
       if (wq < 0) gw = 0.f;
@@ -466,7 +481,20 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         }
       }
     }
-    if (!FUSED) {
+    if (!FUSED && a.rec_S) {
+      // the whole gradient record: gV (zeros unless V was pulled), gw, live, padding
+      float* gr = a.grad + (int64_t)cidx * a.rec_S;
+      if (vq < 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+      }
+      store_coords<CPL, VEC>(gr, l, d, acc);
+      if (l == 0) {
+        gr[d] = gw;
+        gr[d + 1] = vq >= 0 ? 1.f : 0.f;
+        for (int k = d + 2; k < a.rec_S; ++k) gr[k] = 0.f;
+      }
+    } else if (!FUSED) {
       if (l == 0 && wq >= 0) a.grad[wq] = gw;
       if (vq >= 0) store_coords<CPL, VEC>(a.grad + vq, l, d, acc);
     } else {

@@ -21,6 +21,9 @@ struct FwdArgs {
   const float* Vbase;
   const float* zpad;     // kZpadFloats device zeros: targets of masked (clamped) gathers
   int d;
+  // sharded store: W holds one pulled record of rec_S floats [V(d) | w | live | 0 0] per
+  // column (wpos / vpos unused)
+  int rec_S;
   const float* label;
   const float* rw;
   const float* pred_in;  // gradient prep: p from this pred
@@ -46,6 +49,10 @@ struct BwdArgs {
   const int32_t* vpos;
   const float* W;
   float* grad;
+  // sharded store: W / grad hold one record of rec_S floats per column, pulled
+  // [V(d) | w | live | 0 0] and gradient [gV(d) | gw | live | 0 0]; every gradient record is
+  // written whole (no pre-zeroing)
+  int rec_S;
   // fused update
   const uint32_t* slot;      // model-table slot of each segment's key
   Table T;

@@ -222,7 +222,8 @@ int dfx_prof_lanes(dfx_ctx* ctx, double* out);
  *   -> alltoallv records back
  *   dfx_dist_fwd_bwd       forward + Evaluate + AUC of this worker's batch (progress on the
  *                          device), and for training CalcGrad into grads_out[U*S] records
- *                          [gV | gw | 0 0 0]; pred_out optional device B floats
+ *                          [gV | gw | live | 0 0] (live: this worker pulled V, the lens of
+ *                          its push); pred_out optional device B floats
  *   -> alltoallv gradient records to their owners
  *   dfx_dist_owner_push    the ranks' Update(kGradient) pushes in rank order
  * Owner calls run on the context stream in call order.  All arrays except split_counts /

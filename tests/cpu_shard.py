@@ -1,7 +1,7 @@
 """CPU test double of difacto_amd.dist.Shard built from the oracle, so the sharded step's
 orchestration (difacto_amd.dist.sharded_step over TorchComm / gloo) runs with world_size > 1
 in this container.  It speaks the same record layout as the C-ABI (include/difacto_amd.h):
-pulled records [V(d) | w | live | 0 | 0], gradient records [gV(d) | gw | 0 | 0 | 0]."""
+pulled records [V(d) | w | live | 0 | 0], gradient records [gV(d) | gw | live | 0 | 0]."""
 from types import SimpleNamespace
 
 import numpy as np
@@ -61,6 +61,7 @@ class CpuShard:
             out[u, d] = g[q]
             if live[u]:
                 out[u, :d] = g[vp[u]:vp[u] + d]
+                out[u, d + 1] = 1.0
         return torch.from_numpy(out.ravel())
 
     # server
@@ -108,7 +109,8 @@ class CpuShard:
             if not len(keys):
                 continue
             rows = rec[o["roffs"][r]:o["roffs"][r + 1]]
-            live = o["rlive"][r]
+            live = rows[:, d + 1] != 0 if d > 0 else np.zeros(len(keys), bool)
+            assert np.array_equal(live, o["rlive"][r])  # the push carries what was pulled
             vals = np.concatenate([np.concatenate([[rows[i, d]], rows[i, :d]]) if live[i]
                                    else rows[i, d:d + 1] for i in range(len(keys))])
             lens = (1 + d * live).astype(np.int32) if d > 0 else None

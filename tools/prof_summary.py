@@ -5,9 +5,12 @@ The timed window is the last N steps: it starts where the (N+1)-th-from-last ste
 `k_step_finalize` ended and stops where the last one ended.  Per kernel: dispatches per step,
 average duration, microseconds per step, and the busy fraction of the window.
 usage: prof_summary.py trace.csv N [fetch_pmc.csv write_pmc.csv]
+DFX_STEP_MARKER (default k_step_finalize; the sharded store: k_dist_worker_finalize) names
+the once-per-step kernel the window is anchored on.
 """
 import collections
 import csv
+import os
 import sys
 
 
@@ -30,7 +33,8 @@ def main():
     rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
             for r in csv.DictReader(open(trace))]
     rows.sort()
-    fin = [e for s, e, k in rows if "k_step_finalize" in k]
+    marker = os.environ.get("DFX_STEP_MARKER", "k_step_finalize")
+    fin = [e for s, e, k in rows if marker in k]
     if len(fin) < nsteps + 1:
         raise SystemExit("trace holds %d steps, need %d" % (len(fin), nsteps + 1))
     t0, t1 = fin[-nsteps - 1], fin[-1]
