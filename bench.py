@@ -294,13 +294,15 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         else:
             pipe.submit([batch], H.kTraining, push_cnt=push_cnt, mark=mark)
             live.append(batch)
-            del live[:-2]
+            del live[:-3]
 
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (world * B * k)))
     for i in range(n_warm_epoch):
         step(DevBatch(torch, dev, B, k, kb, seed=1_000_000 * (rank + 1) + i), True)
     for i in range(args.warmup):
         step(DevBatch(torch, dev, B, k, kb, seed=2_000_000 * (rank + 1) + i), False)
+    if pipe is not None:
+        pipe.flush()
     batches = [DevBatch(torch, dev, B, k, kb, seed=3_000_000 * (rank + 1) + i)
                for i in range(args.steps)]
     torch.cuda.synchronize()
@@ -316,9 +318,12 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i, bt in enumerate(batches):
-        step(bt, False, mark=lambda j, e=evs[i]: e[j + 1].record())
+        if pipe is None:
+            step(bt, False, mark=lambda j, e=evs[i]: e[j + 1].record())
+        else:  # a submit runs the previous batch's step
+            step(bt, False, mark=(lambda j, e=evs[i - 1]: e[j + 1].record()) if i else None)
     if pipe is not None:
-        pipe.flush()
+        pipe.flush(mark=lambda j, e=evs[-1]: e[j + 1].record())
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0

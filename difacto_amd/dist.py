@@ -47,6 +47,7 @@ class Shard:
         # the Localizer lane writes these; they live until the slot's fwd_bwd
         self._keys = [None, None]
         self._cnt = [None, None]
+        self._want_cnt = [False, False]
 
     def _slot_buffers(self, slot, n, want_cnt):
         dev = self.ctx.device
@@ -64,7 +65,7 @@ class Shard:
     def localize(self, dblk, want_cnt, slot=0, max_index=MAX_INDEX):
         """issue Localizer::Compact of the batch on the Localizer lane (asynchronous)"""
         keys, cnt = self._slot_buffers(slot, dblk.nnz, want_cnt)
-        self._want_cnt = want_cnt
+        self._want_cnt[slot] = want_cnt
         b = dblk.as_batch()
         check(_lib.lib().dfx_dist_localize(self.ctx.h, ctypes.byref(b),
                                            ctypes.c_uint64(max_index), self.nranks, slot,
@@ -77,7 +78,7 @@ class Shard:
         check(_lib.lib().dfx_dist_localize_wait(self.ctx.h, slot, self.nranks, splits,
                                                 ctypes.byref(U)))
         self._U[slot] = U.value
-        cnt = self._cnt[slot][:U.value] if self._want_cnt else None
+        cnt = self._cnt[slot][:U.value] if self._want_cnt[slot] else None
         return self._keys[slot][:U.value], cnt, list(splits)
 
     def fwd_bwd(self, dblk, pulled, job_type, slot=0, pred=None):
@@ -295,34 +296,48 @@ def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_in
 class ShardedPipeline:
     """The pipelined (1-step-stale) schedule of the sharded store (oracle: StaleOracle).
 
-    submit(step t+1) issues, in order:
-      Localizer lane   localize(t+1) into slot (t+1) % 2, beside step t's forward/backward
-      host             join it; exchange the split counts
-      exchange         keys(t+1) (+ counts) to their owners
-      main stream      owner_begin(t+1), owner_pull(t+1)       beside step t's gradient exchange
-      exchange         records(t+1) back to the workers
-      main stream      owner_push(t)                          beside the record exchange
-      main stream      fwd_bwd(t+1); exchange gradients(t+1)  (pending until the next submit)
+    submit(batch t+1) issues batch t+1's Localizer on its lane and then runs step t, whose
+    Localizer was issued one submit earlier:
+      host             join step t's Localizer; exchange the split counts
+      exchange         keys(t) (+ counts) to their owners
+      main stream      owner_begin(t), owner_pull(t)       beside step t-1's gradient exchange
+      exchange         records(t) back to the workers
+      main stream      owner_push(t-1)                    beside the record exchange
+      main stream      fwd_bwd(t); exchange gradients(t)  (pending until the next step)
     so every pull is answered before the previous step's push: pulls are at most one step
     stale, the reference's two batches in flight against an asynchronous server
-    (sgd_learner.cc:310-312, kvstore_dist.h:137-150).  flush() applies the last push.
-    A batch must stay alive until the submit after the one that took it."""
+    (sgd_learner.cc:310-312, kvstore_dist.h:137-150).  flush() runs the queued step and the
+    last push.  A step's predictions / progress are complete after the submit that follows
+    it (or flush()); its batch must stay alive until then and one submit longer."""
 
     def __init__(self, shards, comm, max_index=MAX_INDEX):
         self.shards, self.comm, self.max_index = shards, comm, max_index
         self.slot = 0
+        self.queue = []
         self.pending = None
 
     def submit(self, dblks, job_type=kTraining, push_cnt=False, preds=None, mark=None):
-        mark = mark or (lambda i: None)
-        mark(-1)
-        shards, comm = self.shards, self.comm
-        n = len(shards)
         s = self.slot
         self.slot ^= 1
-        want_cnt = bool(push_cnt) and shards[0].ctx.V_dim > 0
-        for i in range(n):
-            shards[i].localize(dblks[i], want_cnt, s, self.max_index)
+        want_cnt = bool(push_cnt) and self.shards[0].ctx.V_dim > 0
+        for i, sh in enumerate(self.shards):
+            sh.localize(dblks[i], want_cnt, s, self.max_index)
+        self.queue.append((s, dblks, job_type, want_cnt, preds))
+        if len(self.queue) > 1:
+            self._step(self.queue.pop(0), mark)
+
+    def flush(self, mark=None):
+        """run the queued step and apply the last push"""
+        while self.queue:
+            self._step(self.queue.pop(0), mark)
+        self._push_pending()
+
+    def _step(self, q, mark):
+        mark = mark or (lambda i: None)
+        s, dblks, job_type, want_cnt, preds = q
+        shards, comm = self.shards, self.comm
+        n = len(shards)
+        mark(-1)
         loc = [shards[i].localize_wait(s) for i in range(n)]
         mark(0)
         send = [l[2] for l in loc]
@@ -349,7 +364,6 @@ class ShardedPipeline:
             self.pending = (s, comm.alltoallv_async(grads, send, recv, S), dblks)
         mark(6)
         mark(7)
-        return [sum(x) for x in recv]
 
     def _push_pending(self):
         if self.pending is None:
@@ -359,7 +373,3 @@ class ShardedPipeline:
         rgrads = hg.wait()
         for i, sh in enumerate(self.shards):
             sh.owner_push(rgrads[i], s)
-
-    def flush(self):
-        """apply the last step's push"""
-        self._push_pending()

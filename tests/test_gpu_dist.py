@@ -106,20 +106,24 @@ def test_sharded_pipeline_matches_stale_oracle(name):
     pipe = DI.ShardedPipeline(shards, DI.LoopbackComm(N))
     so = DO.StaleOracle(N, **kw)
     batches = _batches(N, len(PIPE_JOBS))
-    live = []  # batches stay alive until the submit after the one that took them
+    live, got, want = [], [], []  # batches stay alive until the pipeline is flushed
     for s, (step, (job, cnt)) in enumerate(zip(batches, PIPE_JOBS)):
         dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
         preds = [torch.zeros(step[r].size, dtype=torch.float32, device=ctxs[r].device)
                  for r in range(N)]
         pipe.submit(dbs, job, push_cnt=cnt, preds=preds)
         live.append(dbs)
-        out = so.submit(step, push_cnt=cnt, train=job == 3)
-        for r in range(N):
-            assert close(preds[r].cpu().numpy(), out[r][2]), (name, s, r)
-            pr = H.progress(ctxs[r])
-            assert pr["loss"] == pytest.approx(out[r][0], rel=1e-4)
+        got.append(preds)
+        want.append(so.submit(step, push_cnt=cnt, train=job == 3))
     pipe.flush()
     so.flush()
+    for s in range(len(PIPE_JOBS)):
+        for r in range(N):
+            assert close(got[s][r].cpu().numpy(), want[s][r][2]), (name, s, r)
+    for r in range(N):
+        pr = H.progress(ctxs[r])
+        assert pr["nrows"] == sum(step[r].size for step in batches)
+        assert pr["loss"] == pytest.approx(sum(w[r][0] for w in want), rel=1e-4)
     keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
                                      for step in batches for b in step]))
     n_v = 0
@@ -217,10 +221,11 @@ def _mp_worker(rank, world, port, q, pipelined=False):
                 pipe.submit([db], H.kTraining, push_cnt=s < 2, preds=[pred])
             else:
                 DI.sharded_step([shard], [db], comm, H.kTraining, push_cnt=s < 2, preds=[pred])
-            preds.append(pred.cpu().numpy())
+            preds.append(pred)
         if pipe:
             pipe.flush()
         ctx.sync()
+        preds = [p.cpu().numpy() for p in preds]
         q.put((rank, preds, H.Store(ctx).stats()))
         ctx.close()
     finally:
