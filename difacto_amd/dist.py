@@ -34,6 +34,14 @@ def owner_of(keys_u64, nranks):
     return ((hi * n + ((lo * n) >> np.uint64(32))) >> np.uint64(32)).astype(np.int64)
 
 
+def model_name(prefix, rank, it=-1):
+    """SGDLearner::ModelName (sgd_learner.h:65-69): every server saves / loads its own part"""
+    name = str(prefix)
+    if it >= 0:
+        name += "_iter-%d" % it
+    return name + "_part-%d" % rank
+
+
 class Shard:
     """One rank's device context in the sharded store: worker and key-range server.  Every
     call takes the step slot (0 or 1) whose buffers it uses; two steps can be in flight."""
@@ -110,6 +118,18 @@ class Shard:
 
     def owner_push(self, recv_grads, slot=0):
         check(_lib.lib().dfx_dist_owner_push(self.ctx.h, slot, _p(recv_grads)))
+
+    # model files (SGDLearner::SaveLoadModel, sgd_learner.cc:180-196) ---------------------------
+    def save(self, prefix, rank, save_aux=False, it=-1):
+        """this server's part, in SGDUpdater::Save's format (flush a pipeline first)"""
+        self.ctx.sync()
+        check(_lib.lib().dfx_store_save(self.ctx.h, model_name(prefix, rank, it).encode(),
+                                        int(save_aux)))
+
+    def load(self, prefix, rank, it=-1):
+        """this server's part; the key ranges are those of the run that saved it (the same
+        number of ranks)"""
+        check(_lib.lib().dfx_store_load(self.ctx.h, model_name(prefix, rank, it).encode()))
 
 
 class _Done:

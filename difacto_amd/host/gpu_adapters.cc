@@ -369,7 +369,7 @@ GpuSGDLearner::~GpuSGDLearner() {
 }
 
 void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type,
-                                 bool push_cnt) {
+                                 bool push_cnt, std::vector<real_t>* pred_out) {
   push_cnt = push_cnt && job_type == kTraining && V_dim_ > 0;
   if (fused_) {
     const int64_t B = (int64_t)batch.size, nnz = B ? (int64_t)batch.offset[B] : 0;
@@ -395,10 +395,20 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
     DfxCheck(dfx_feeder_submit(feeder_, B, nnz, batch.value != nullptr, batch.weight != nullptr,
                                &b),
              "dfx_feeder_submit");
+    float* dp = nullptr;
+    if (pred_out) {
+      if (!dpred_) dpred_.reset(new DevArray<float>(c));
+      dpred_->ensure(B);
+      dp = dpred_->get();
+    }
     DfxCheck(dfx_train_step(c, &b, job_type, push_cnt ? 1 : 0,
-                            std::numeric_limits<uint64_t>::max(), nullptr),
+                            std::numeric_limits<uint64_t>::max(), dp),
              "dfx_train_step");
     DfxCheck(dfx_feeder_consumed(feeder_), "dfx_feeder_consumed");
+    if (pred_out) {
+      pred_out->resize(B);
+      dpred_->download(pred_out->data(), B);
+    }
     return;
   }
   // the executor lambda of IterateData, through the plugin interfaces
@@ -419,6 +429,7 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   std::vector<SArray<char>> inputs = {SArray<char>(values), SArray<char>(w_pos),
                                       SArray<char>(V_pos)};
   loss_->Predict(blk, inputs, &pred);
+  if (pred_out) pred_out->assign(pred.data(), pred.data() + pred.size());
   prog_.loss += loss_->Evaluate(blk.label, pred);
   prog_.auc += loss_->AUC(blk.label, pred);
   if (job_type == kTraining) {

@@ -175,8 +175,10 @@ class GpuSGDLearner {
   ~GpuSGDLearner();
   /** one minibatch of raw feature ids; push_cnt = epoch 0 of training with V_dim > 0.
    * Asynchronous on the fused path: the batch is copied into pinned staging and uploaded on
-   * the feeder's loader stream; the step runs behind the previous one. */
-  void ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type, bool push_cnt);
+   * the feeder's loader stream; the step runs behind the previous one.  pred (optional):
+   * receives the batch's predictions (joins the device), as SavePred writes them. */
+  void ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_type, bool push_cnt,
+                    std::vector<real_t>* pred = nullptr);
   /** sgd::Progress accumulated since the last call (joins the device) */
   Progress TakeProgress();
   std::shared_ptr<GpuSGDUpdater> updater() const { return updater_; }
@@ -191,6 +193,7 @@ class GpuSGDLearner {
   std::unique_ptr<GpuLocalizer> localizer_;
   dfx_feeder* feeder_ = nullptr;
   int64_t feed_rows_ = 0, feed_nnz_ = 0;
+  std::unique_ptr<DevArray<float>> dpred_;
   Progress prog_;
 };
 

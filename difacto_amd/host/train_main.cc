@@ -4,7 +4,13 @@
 //   build/dfx_train data_in=FILE [data_val=FILE] [data_format=libsvm|criteo|criteo_test]
 //                   [batch_size=100] [shuffle=10] [neg_sampling=1] [max_num_epochs=20]
 //                   [num_jobs_per_epoch=10] [stop_rel_objv=1e-5] [model_in=F] [model_out=F]
+//                   [load_epoch=-1] [has_aux=0] [task=0|2] [pred_out=F] [pred_prob=1]
 //                   [fused=1] [nthreads=8] [V_dim=..] [lr=..] [l1=..] ...  (SGDUpdaterParam)
+//
+// Model files are named like SGDLearner::ModelName (sgd_learner.h:65-69):
+// <prefix>[_iter-<epoch>]_part-0, in SGDUpdater::Save's format; task=2 predicts data_val with
+// model_in into <pred_out>_part-0, one "label\tprediction" line per row (SavePred,
+// sgd_learner.h:72-83).
 //
 // Each epoch reads data_in in num_jobs_per_epoch parts (the reference's jobs, here run in
 // order), minibatched by BatchReader (reader.h) and trained through GpuSGDLearner, i.e. one
@@ -15,6 +21,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 #include <string>
 
 #include "gpu_adapters.h"
@@ -24,12 +31,21 @@ using namespace difacto;
 
 namespace {
 struct Param {
-  std::string data_in, data_val, data_format = "libsvm", model_in, model_out;
+  std::string data_in, data_val, data_format = "libsvm", model_in, model_out, pred_out;
   size_t batch_size = 100, shuffle = 10;
   float neg_sampling = 1.f;
   int max_num_epochs = 20, num_jobs_per_epoch = 10, nthreads = 8;
+  int load_epoch = -1, task = 0;
+  bool has_aux = false, pred_prob = true;
   double stop_rel_objv = 1e-5;
 };
+
+// sgd_learner.h:65-69 (one server: rank 0)
+std::string ModelName(const std::string& prefix, int iter) {
+  std::string name = prefix;
+  if (iter >= 0) name += "_iter-" + std::to_string(iter);
+  return name + "_part-0";
+}
 
 double Now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
@@ -44,8 +60,10 @@ std::string Text(const Progress& p) {
   return buf;
 }
 
-Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_type) {
+Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_type,
+                  FILE* pred_file = nullptr) {
   Progress prog;
+  std::vector<real_t> pred;
   const bool train = job_type == GpuSGDLearner::kTraining;
   const std::string& path = train ? P.data_in : P.data_val;
   for (int part = 0; part < P.num_jobs_per_epoch; ++part) {
@@ -63,7 +81,10 @@ Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_typ
       while (reader.Next()) {
         const auto& v = reader.Value();
         if (v.Size() == 0) continue;
-        learner->ProcessBatch(v.GetBlock(), job_type, false);
+        learner->ProcessBatch(v.GetBlock(), job_type, false, pred_file ? &pred : nullptr);
+        for (size_t i = 0; pred_file && i < pred.size(); ++i)  // SavePred
+          std::fprintf(pred_file, "%g\t%g\n", v.label[i],
+                       P.pred_prob ? 1.0 / (1.0 + std::exp(-pred[i])) : (double)pred[i]);
       }
     }
     const Progress p = learner->TakeProgress();
@@ -98,24 +119,49 @@ int main(int argc, char** argv) {
     else if (k == "num_jobs_per_epoch") P.num_jobs_per_epoch = std::stoi(v);
     else if (k == "stop_rel_objv") P.stop_rel_objv = std::stod(v);
     else if (k == "nthreads") P.nthreads = std::stoi(v);
+    else if (k == "load_epoch") P.load_epoch = std::stoi(v);
+    else if (k == "task") P.task = std::stoi(v);
+    else if (k == "pred_out") P.pred_out = v;
+    else if (k == "pred_prob") P.pred_prob = std::stoi(v) != 0;
+    else if (k == "has_aux") P.has_aux = std::stoi(v) != 0;
     else {
       fused_given = fused_given || k == "fused";
       rest.push_back({k, v});
     }
   }
-  if (P.data_in.empty()) {
+  if (P.data_in.empty() && P.task != 2) {
     std::fprintf(stderr, "usage: %s data_in=FILE [key=value ...]\n", argv[0]);
     return 2;
   }
   if (!fused_given) rest.push_back({"fused", "1"});
   GpuSGDLearner learner(rest);
-  if (!P.model_in.empty()) {
-    FileStream fi(P.model_in.c_str(), "rb");
+  int k0 = 0;
+  if (!P.model_in.empty()) {  // sgd_learner.cc:58-67
+    FileStream fi(ModelName(P.model_in, P.load_epoch > 0 ? P.load_epoch : -1).c_str(), "rb");
     learner.updater()->Load(&fi);
+    if (P.load_epoch > 0) k0 = P.load_epoch + 1;
+  }
+  if (P.task == 2) {  // prediction, sgd_learner.cc:69-77
+    if (P.model_in.empty() || P.data_val.empty()) {
+      std::fprintf(stderr, "prediction needs model_in and data_val\n");
+      return 2;
+    }
+    FILE* pf = nullptr;
+    if (!P.pred_out.empty()) {
+      pf = std::fopen((P.pred_out + "_part-0").c_str(), "w");
+      if (!pf) {
+        std::fprintf(stderr, "cannot open %s_part-0\n", P.pred_out.c_str());
+        return 1;
+      }
+    }
+    const Progress pr = RunEpoch(&learner, P, k0, GpuSGDLearner::kPrediction, pf);
+    if (pf) std::fclose(pf);
+    std::printf("Prediction: %s\n", Text(pr).c_str());
+    return 0;
   }
   const double t0 = Now();
   double pre_loss = 0, pre_val_auc = 0;  // sgd_learner.cc:52
-  for (int k = 0; k < P.max_num_epochs; ++k) {
+  for (int k = k0; k < P.max_num_epochs; ++k) {
     const double te = Now();
     const Progress tr = RunEpoch(&learner, P, k, GpuSGDLearner::kTraining);
     const double dt = Now() - te;
@@ -140,9 +186,9 @@ int main(int argc, char** argv) {
     pre_loss = tr.loss;
     pre_val_auc = va.auc;
   }
-  if (!P.model_out.empty()) {
-    FileStream fo(P.model_out.c_str(), "wb");
-    learner.updater()->Save(false, &fo);
+  if (!P.model_out.empty()) {  // sgd_learner.cc:116-120
+    FileStream fo(ModelName(P.model_out, -1).c_str(), "wb");
+    learner.updater()->Save(P.has_aux, &fo);
   }
   return 0;
 }

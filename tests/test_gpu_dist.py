@@ -151,6 +151,62 @@ def test_sharded_pipeline_matches_stale_oracle(name):
         c.close()
 
 
+def test_sharded_save_load_parts(tmp_path):
+    """each server saves its part as <prefix>_part-<rank> (sgd_learner.h:65-69) in the
+    reference's SGDUpdater::Save format: the oracle server loads it back to its own state, and
+    fresh shards loading the parts continue training exactly like the original ones"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS["fm_v4"]
+    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.ShardedOracle(N, **kw)
+    batches = _batches(N, 4)
+    for s, step in enumerate(batches[:3]):
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=s < 2)
+        so.step(step, push_cnt=s < 2)
+    prefix = tmp_path / "model"
+    for r in range(N):
+        shards[r].save(prefix, r, save_aux=True)
+        assert (tmp_path / ("model_part-%d" % r)).exists()
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
+                                     for step in batches for b in step]))
+    for g in range(N):
+        up = O.Updater(**kw)
+        up.load(DI.model_name(prefix, g))
+        n_saved = 0
+        for k in keys[DO.owner_of(keys, N) == g]:
+            a, b = up.entry(k), so.up[g].entry(k)
+            if a is None:  # Save skips empty entries (w == 0, no V; sgd_updater.h:35-48)
+                assert b is None or (b[0][0] == 0 and b[1] is None)
+                continue
+            n_saved += 1
+            assert close(a[0][:3], b[0][:3]) and (a[1] is None) == (b[1] is None)
+            if a[1] is not None:
+                assert close(a[1], b[1])
+        assert n_saved == up.size() > 0
+    # fresh shards from the parts: one more step agrees with the original shards
+    ctx2 = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    sh2 = [DI.Shard(c, N) for c in ctx2]
+    for r in range(N):
+        sh2[r].load(prefix, r)
+    step = batches[3]
+    preds = []
+    for cs, shs in ((ctxs, shards), (ctx2, sh2)):
+        dbs = [H.DeviceRowBlock(cs[r], step[r]) for r in range(N)]
+        pr = [torch.zeros(step[r].size, dtype=torch.float32, device=cs[r].device)
+              for r in range(N)]
+        DI.sharded_step(shs, dbs, comm, H.kValidation, preds=pr)
+        preds.append([p.cpu().numpy() for p in pr])
+    for r in range(N):
+        assert np.array_equal(preds[0][r], preds[1][r])
+    for c in ctxs + ctx2:
+        c.sync()
+        c.close()
+
+
 def test_sharded_validation_does_not_update():
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H

@@ -105,3 +105,38 @@ def test_train_driver_feeder_matches_interface_path():
     for (la, aa), (lb, ab) in zip(a, b):
         assert abs(la - lb) <= 1e-4 * abs(lb), (la, lb)
         assert abs(aa - ab) <= 1e-3, (aa, ab)
+
+
+@pytest.mark.gpu
+def test_train_driver_model_parts_and_prediction(tmp_path):
+    """dfx_train model_out -> <prefix>_part-0 in SGDUpdater::Save's format (the oracle loads
+    it), then task=2 with model_in predicts data_val into <pred_out>_part-0 (SavePred): the
+    written probabilities equal the oracle's predictions from the loaded model"""
+    import numpy as np
+    from oracle import oracle as O
+    from difacto_amd import data as D
+    kw = ["V_dim=4", "V_threshold=1", "lr=0.1", "V_lr=0.05", "l1=0.1"]
+    model = str(tmp_path / "model")
+    preds = str(tmp_path / "pred")
+    r = subprocess.run([TRAIN_BIN, "data_in=" + DATA, "num_jobs_per_epoch=1", "shuffle=0",
+                        "batch_size=30", "max_num_epochs=3", "stop_rel_objv=0",
+                        "model_out=" + model, "max_keys=65536"] + kw,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert os.path.exists(model + "_part-0")
+    r = subprocess.run([TRAIN_BIN, "task=2", "data_val=" + DATA, "model_in=" + model,
+                        "pred_out=" + preds, "num_jobs_per_epoch=1", "max_keys=65536"] + kw,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Prediction:" in r.stdout
+    lines = [l.split("\t") for l in open(preds + "_part-0").read().splitlines()]
+    blk = D.read_libsvm(DATA)
+    assert len(lines) == blk.size
+    got = np.array([float(p) for _, p in lines])
+    assert np.array_equal(np.array([float(y) for y, _ in lines]), blk.labels)
+    up = O.Updater(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1)
+    up.load(model + "_part-0")
+    _, _, pred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels, train=False,
+                               want_pred=True)
+    want = 1.0 / (1.0 + np.exp(-pred.astype(np.float64)))
+    assert np.allclose(got, want, rtol=2e-5, atol=1e-6)
