@@ -21,8 +21,15 @@ HOSTFLAGS = -std=c++14 -O2 -Wall -pthread
 
 READERBIN = build/reader_tests
 GENBIN = build/gen_criteo
+CONVBIN = build/dfx_convert
 
-all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN)
+all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN)
+
+# the data converter (src/reader/converter.h): text formats -> rec (CompressedRowBlock RecordIO)
+$(CONVBIN): difacto_amd/host/reader.cc difacto_amd/host/convert_main.cc difacto_amd/host/reader.h \
+  difacto_amd/host/iface.h
+	@mkdir -p build
+	g++ $(HOSTFLAGS) -o $@ difacto_amd/host/reader.cc difacto_amd/host/convert_main.cc
 
 $(GENBIN): tools/gen_criteo.cc
 	@mkdir -p build
@@ -32,7 +39,7 @@ $(GENBIN): tools/gen_criteo.cc
 $(READERBIN): difacto_amd/host/reader.cc tests/host/reader_tests.cc difacto_amd/host/reader.h \
   difacto_amd/host/iface.h
 	@mkdir -p build
-	g++ $(HOSTFLAGS) -o $@ difacto_amd/host/reader.cc tests/host/reader_tests.cc
+	g++ $(HOSTFLAGS) -o $@ difacto_amd/host/reader.cc tests/host/reader_tests.cc -ldl
 
 # C++ host adapters (the reference's Loss/Updater/Store over the C-ABI) + their test driver;
 # plain g++ against the C-ABI, no HIP headers

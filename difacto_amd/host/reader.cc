@@ -187,6 +187,332 @@ void ParseCriteo(const char* p, const char* e, bool is_train, RowBlockContainer<
   }
 }
 
+// adfea_parser.h:39-80: whitespace-separated tokens; "idx:gid" is a feature
+// (EncodeFeaGrpID(idx, gid, 12)), other tokens cycle lineid, count, label — the label opens a
+// new row and is 1 iff the token starts with '1'
+void ParseAdfea(const char* p, const char* e, RowBlockContainer<feaid_t>* out) {
+  auto space = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; };
+  auto digit = [](char c) { return c >= '0' && c <= '9'; };
+  const size_t rows0 = out->label.size();
+  int i = 0;
+  while (p != e && space(*p)) ++p;
+  while (p != e) {
+    const char* head = p;
+    while (p != e && digit(*p)) ++p;
+    if (head == p) {  // not a number: skip the token
+      while (p != e && !space(*p)) ++p;
+    } else if (p != e && *p == ':') {
+      ++p;
+      const feaid_t idx = std::strtoull(head, nullptr, 10);
+      const feaid_t gid = std::strtoull(p, nullptr, 10);
+      if (out->label.size() > rows0) out->index.push_back((idx << 12) | (gid & 4095));
+      while (p != e && digit(*p)) ++p;
+    } else if (i == 2) {
+      i = 0;
+      if (out->label.size() > rows0) out->offset.push_back(out->index.size());
+      out->label.push_back(*head == '1' ? 1.f : 0.f);
+    } else {
+      ++i;
+    }
+    while (p != e && space(*p)) ++p;
+  }
+  if (out->label.size() > rows0) out->offset.push_back(out->index.size());
+}
+
+// ---- LZ4 block format ---------------------------------------------------------------------
+// Sequences of: token (literal length << 4 | match length - 4, 15 = extended by 255-runs),
+// literals, 2-byte little-endian offset, match extension.  The last 5 bytes are literals and
+// the last match starts at least 12 bytes before the end (the format's end conditions).
+namespace {
+constexpr int kLz4MinMatch = 4, kLz4LastLiterals = 5, kLz4MFLimit = 12;
+inline uint32_t Read32(const uint8_t* p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+inline void PutLen(uint8_t*& op, int len) {
+  for (len -= 15; len >= 255; len -= 255) *op++ = 255;
+  *op++ = (uint8_t)len;
+}
+}  // namespace
+
+int Lz4CompressBound(int n) { return n + n / 255 + 16; }
+
+int Lz4Compress(const char* src, int n, char* dst, int cap) {
+  if (n < 0 || cap < Lz4CompressBound(n)) return 0;
+  const uint8_t* const base = reinterpret_cast<const uint8_t*>(src);
+  const uint8_t* const end = base + n;
+  const uint8_t* ip = base;
+  const uint8_t* anchor = base;
+  uint8_t* op = reinterpret_cast<uint8_t*>(dst);
+  auto emit = [&](const uint8_t* lit_end, int match_len, int offset) {
+    const int lit = (int)(lit_end - anchor);
+    uint8_t* token = op++;
+    *token = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+    if (lit >= 15) PutLen(op, lit);
+    std::memcpy(op, anchor, lit);
+    op += lit;
+    if (match_len > 0) {
+      *op++ = (uint8_t)(offset & 255);
+      *op++ = (uint8_t)(offset >> 8);
+      const int ml = match_len - kLz4MinMatch;
+      *token |= (uint8_t)(ml >= 15 ? 15 : ml);
+      if (ml >= 15) PutLen(op, ml);
+    }
+  };
+  if (n > kLz4MFLimit) {
+    std::vector<int32_t> table(1 << 14, -1);
+    const uint8_t* const mflimit = end - kLz4MFLimit;        // last match start
+    const uint8_t* const matchlimit = end - kLz4LastLiterals;  // matches end before
+    while (ip <= mflimit) {
+      const uint32_t seq = Read32(ip);
+      const uint32_t h = (seq * 2654435761u) >> 18;
+      const int32_t cand = table[h];
+      table[h] = (int32_t)(ip - base);
+      if (cand >= 0 && (ip - base) - cand <= 65535 && Read32(base + cand) == seq) {
+        const uint8_t* m = base + cand;
+        int ml = kLz4MinMatch;
+        while (ip + ml < matchlimit && m[ml] == ip[ml]) ++ml;
+        emit(ip, ml, (int)(ip - m));
+        ip += ml;
+        anchor = ip;
+      } else {
+        ++ip;
+      }
+    }
+  }
+  emit(end, 0, 0);  // the last literals
+  return (int)(op - reinterpret_cast<uint8_t*>(dst));
+}
+
+int Lz4Decompress(const char* src, int n, char* dst, int dst_cap) {
+  const uint8_t* ip = reinterpret_cast<const uint8_t*>(src);
+  const uint8_t* const iend = ip + n;
+  uint8_t* const obase = reinterpret_cast<uint8_t*>(dst);
+  uint8_t* op = obase;
+  uint8_t* const oend = obase + dst_cap;
+  auto ext = [&](int* len) {
+    if (*len != 15) return true;
+    uint8_t b;
+    do {
+      if (ip >= iend) return false;
+      b = *ip++;
+      *len += b;
+    } while (b == 255);
+    return true;
+  };
+  for (;;) {
+    if (ip >= iend) return -1;
+    const uint8_t token = *ip++;
+    int lit = token >> 4;
+    if (!ext(&lit) || lit > iend - ip || lit > oend - op) return -1;
+    std::memcpy(op, ip, lit);
+    op += lit;
+    ip += lit;
+    if (ip == iend) break;  // the last sequence has no match
+    if (iend - ip < 2) return -1;
+    const int off = ip[0] | (ip[1] << 8);
+    ip += 2;
+    int ml = token & 15;
+    if (!ext(&ml)) return -1;
+    ml += kLz4MinMatch;
+    if (off == 0 || off > op - obase || ml > oend - op) return -1;
+    const uint8_t* m = op - off;
+    for (int i = 0; i < ml; ++i) op[i] = m[i];  // overlapping copies repeat the pattern
+    op += ml;
+  }
+  return (int)(op - obase);
+}
+
+// ---- CompressedRowBlock -------------------------------------------------------------------
+namespace {
+constexpr int kCrbMagic = 1196140743;
+void PutInt(std::string* s, int v) { s->append(reinterpret_cast<const char*>(&v), 4); }
+void PutSection(std::string* s, const void* data, size_t bytes) {
+  if (!data) {
+    PutInt(s, 0);
+    return;
+  }
+  std::vector<char> buf(Lz4CompressBound((int)bytes));
+  const int m = Lz4Compress(static_cast<const char*>(data), (int)bytes, buf.data(),
+                            (int)buf.size());
+  DFX_HOST_CHECK(m > 0, "lz4 compression failed");
+  PutInt(s, m);
+  s->append(buf.data(), m);
+}
+}  // namespace
+
+void CompressRowBlock(const RowBlockContainer<feaid_t>& blk, size_t begin, size_t end,
+                      std::string* out) {
+  out->clear();
+  const int nrows = (int)(end - begin);
+  const size_t o0 = blk.offset[begin], nnz = blk.offset[end] - o0;
+  bool binary = true;  // Compress drops all-one values
+  for (size_t j = o0; j < o0 + nnz && binary && !blk.value.empty(); ++j)
+    binary = blk.value[j] == 1.f;
+  std::vector<size_t> offs(nrows + 1);
+  for (int i = 0; i <= nrows; ++i) offs[i] = blk.offset[begin + i] - o0;
+  PutInt(out, kCrbMagic);
+  PutInt(out, (int)sizeof(feaid_t));
+  PutInt(out, nrows);
+  PutSection(out, blk.label.data() + begin, nrows * sizeof(float));
+  PutSection(out, offs.data(), (nrows + 1) * sizeof(size_t));
+  PutSection(out, blk.index.data() + o0, nnz * sizeof(feaid_t));
+  PutSection(out, blk.value.empty() || binary ? nullptr : blk.value.data() + o0,
+             nnz * sizeof(float));
+  PutSection(out, blk.weight.empty() ? nullptr : blk.weight.data() + begin,
+             nrows * sizeof(float));
+}
+
+bool DecompressRowBlock(const char* data, size_t size, RowBlockContainer<feaid_t>* out) {
+  size_t cur = 0;
+  auto get = [&](int* v) {
+    if (cur + 4 > size) return false;
+    std::memcpy(v, data + cur, 4);
+    cur += 4;
+    return true;
+  };
+  int magic, isz, nrows;
+  if (!get(&magic) || magic != kCrbMagic || !get(&isz) || (isz != 8 && isz != 4) ||
+      !get(&nrows) || nrows < 0)
+    return false;
+  // one section -> bytes (empty when absent)
+  auto section = [&](std::vector<char>* dst, size_t bytes, bool* present) {
+    int cp;
+    if (!get(&cp)) return false;
+    *present = cp > 0;
+    if (cp <= 0) return true;
+    if (cur + (size_t)cp > size) return false;
+    dst->resize(bytes);
+    const int got = Lz4Decompress(data + cur, cp, dst->data(), (int)bytes);
+    cur += cp;
+    return got == (int)bytes;
+  };
+  std::vector<char> lab, off, idx, val, wt;
+  bool has_lab, has_off, has_idx, has_val, has_wt;
+  if (!section(&lab, nrows * 4ull, &has_lab) || !section(&off, (nrows + 1) * 8ull, &has_off) ||
+      !has_off)
+    return false;
+  const size_t* o = reinterpret_cast<const size_t*>(off.data());
+  if (o[nrows] < o[0]) return false;
+  const size_t nnz = o[nrows] - o[0];
+  if (!section(&idx, nnz * isz, &has_idx) || !section(&val, nnz * 4, &has_val) ||
+      !section(&wt, nrows * 4ull, &has_wt))
+    return false;
+  if (nnz && !has_idx) return false;
+  // append, keeping out's value / weight arrays aligned with its rows
+  const size_t base = out->index.size(), rows0 = out->label.size();
+  if (has_val && out->value.size() < base) out->value.resize(base, 1.f);
+  if (has_wt && out->weight.size() < rows0) out->weight.resize(rows0, 1.f);
+  for (int i = 0; i < nrows; ++i) {
+    out->label.push_back(has_lab ? reinterpret_cast<const float*>(lab.data())[i] : 0.f);
+    out->offset.push_back(base + o[i + 1] - o[0]);
+  }
+  for (size_t j = 0; j < nnz; ++j)
+    out->index.push_back(isz == 8 ? reinterpret_cast<const uint64_t*>(idx.data())[j]
+                                  : reinterpret_cast<const uint32_t*>(idx.data())[j]);
+  if (has_val) {
+    const float* v = reinterpret_cast<const float*>(val.data());
+    out->value.insert(out->value.end(), v, v + nnz);
+  } else if (!out->value.empty()) {
+    out->value.resize(out->index.size(), 1.f);
+  }
+  if (has_wt) {
+    const float* w = reinterpret_cast<const float*>(wt.data());
+    out->weight.insert(out->weight.end(), w, w + nrows);
+  } else if (!out->weight.empty()) {
+    out->weight.resize(out->label.size(), 1.f);
+  }
+  return cur == size;
+}
+
+// ---- dmlc RecordIO ------------------------------------------------------------------------
+// A record is [magic][lrec = cflag << 29 | length][data][pad to 4].  Data words equal to the
+// magic (at 4-byte aligned offsets) split the record into parts, cflag 1 (first), 2 (middle),
+// 3 (last); the reader puts the magic back between the parts.  0 = a whole record.
+namespace {
+constexpr uint32_t kRecMagic = 0xced7230au;
+inline uint32_t EncodeLRec(uint32_t cflag, uint32_t len) { return (cflag << 29u) | len; }
+}  // namespace
+
+void RecordIOWriter::WriteRecord(const std::string& rec) {
+  DFX_HOST_CHECK(rec.size() < (1u << 29), "RecordIO records are < 2^29 bytes");
+  const char* b = rec.data();
+  const uint32_t len = (uint32_t)rec.size();
+  const uint32_t lower = len & ~3u, upper = (len + 3u) & ~3u;
+  auto put = [&](const void* p, size_t n) {
+    if (n) DFX_HOST_CHECK(std::fwrite(p, 1, n, f_) == n, "short write");
+    bytes_ += n;
+  };
+  uint32_t dptr = 0;
+  for (uint32_t i = 0; i < lower; i += 4) {
+    uint32_t w;
+    std::memcpy(&w, b + i, 4);
+    if (w != kRecMagic) continue;
+    const uint32_t lrec = EncodeLRec(dptr == 0 ? 1u : 2u, i - dptr);
+    put(&kRecMagic, 4);
+    put(&lrec, 4);
+    put(b + dptr, i - dptr);
+    dptr = i + 4;
+  }
+  const uint32_t lrec = EncodeLRec(dptr != 0 ? 3u : 0u, len - dptr);
+  put(&kRecMagic, 4);
+  put(&lrec, 4);
+  put(b + dptr, len - dptr);
+  const uint32_t zero = 0;
+  put(&zero, upper - len);
+}
+
+RecordIOReader::RecordIOReader(const std::string& path, int part, int nparts) {
+  f_ = std::fopen(path.c_str(), "rb");
+  DFX_HOST_CHECK(f_ != nullptr, "cannot open " + path);
+  std::fseek(f_, 0, SEEK_END);
+  const size_t size = (size_t)std::ftell(f_);
+  // a part owns the records whose head lies in its byte range: seek each end to the next
+  // record head (a magic word at a 4-byte aligned offset followed by cflag 0 or 1)
+  auto head_at_or_after = [&](size_t at) {
+    at = (at + 3) & ~(size_t)3;
+    std::vector<uint32_t> w(4096);
+    while (at + 8 <= size) {
+      std::fseek(f_, (long)at, SEEK_SET);
+      const size_t n = std::fread(w.data(), 4, w.size(), f_);
+      if (n < 2) break;
+      for (size_t i = 0; i + 1 < n; ++i)
+        if (w[i] == kRecMagic && (w[i + 1] >> 29u) <= 1u) return at + 4 * i;
+      at += 4 * (n - 1);
+    }
+    return size;
+  };
+  begin_ = part == 0 ? 0 : head_at_or_after(size * part / nparts);
+  end_ = part + 1 == nparts ? size : head_at_or_after(size * (part + 1) / nparts);
+  pos_ = begin_;
+  std::fseek(f_, (long)pos_, SEEK_SET);
+}
+
+RecordIOReader::~RecordIOReader() {
+  if (f_) std::fclose(f_);
+}
+
+bool RecordIOReader::Next(std::string* rec) {
+  rec->clear();
+  if (pos_ >= end_) return false;
+  for (;;) {
+    uint32_t hdr[2];
+    if (std::fread(hdr, 4, 2, f_) != 2) return !rec->empty();
+    DFX_HOST_CHECK(hdr[0] == kRecMagic, "RecordIO: bad record head");
+    const uint32_t cflag = hdr[1] >> 29u, len = hdr[1] & ((1u << 29) - 1);
+    const uint32_t upper = (len + 3u) & ~3u;
+    const size_t at = rec->size();
+    rec->resize(at + upper);
+    DFX_HOST_CHECK(std::fread(&(*rec)[at], 1, upper, f_) == upper, "RecordIO: truncated");
+    rec->resize(at + len);
+    pos_ += 8 + upper;
+    read_ += 8 + upper;
+    if (cflag == 0 || cflag == 3) return true;
+    rec->append(reinterpret_cast<const char*>(&kRecMagic), 4);
+  }
+}
+
 void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
                 RowBlockContainer<feaid_t>* dst) {
   if (end <= begin) return;
@@ -213,8 +539,13 @@ static void ClearRows(RowBlockContainer<feaid_t>* c) {  // keeps the capacity
 TextReader::TextReader(const std::string& path, const std::string& format, int part,
                        int nparts, size_t chunk_bytes, int nthreads)
     : path_(path), format_(format), chunk_(chunk_bytes), nthreads_(nthreads < 1 ? 1 : nthreads) {
-  DFX_HOST_CHECK(format == "libsvm" || format == "criteo" || format == "criteo_test",
+  DFX_HOST_CHECK(format == "libsvm" || format == "criteo" || format == "criteo_test" ||
+                     format == "adfea" || format == "rec",
                  "unknown data_format " + format);
+  if (format == "rec") {
+    rec_.reset(new RecordIOReader(path, part, nparts));
+    return;
+  }
   std::ifstream f(path, std::ios::binary | std::ios::ate);
   DFX_HOST_CHECK(f.good(), "cannot open " + path);
   const size_t size = (size_t)f.tellg();
@@ -235,8 +566,47 @@ TextReader::TextReader(const std::string& path, const std::string& format, int p
   pos_ = begin_;
 }
 
+// format "rec": records of about chunk_ bytes, decompressed by the worker threads
+bool TextReader::NextRec() {
+  recs_.clear();
+  size_t bytes = 0;
+  std::string r;
+  while (bytes < chunk_ && rec_->Next(&r)) {
+    bytes += r.size();
+    recs_.push_back(std::move(r));
+  }
+  read_ = rec_->BytesRead();
+  if (recs_.empty()) return false;
+  const int T = std::min<int>(nthreads_, (int)recs_.size());
+  parts_.resize(T);
+  std::vector<std::thread> th;
+  std::vector<int> ok(T, 1);
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t]() {
+      RowBlockContainer<feaid_t> local;
+      std::swap(local, parts_[t]);
+      ClearRows(&local);
+      const size_t r0 = recs_.size() * t / T, r1 = recs_.size() * (t + 1) / T;
+      for (size_t i = r0; i < r1 && ok[t]; ++i)
+        ok[t] = DecompressRowBlock(recs_[i].data(), recs_[i].size(), &local);
+      std::swap(local, parts_[t]);
+    });
+  }
+  for (auto& x : th) x.join();
+  for (int t = 0; t < T; ++t) DFX_HOST_CHECK(ok[t], "malformed CompressedRowBlock record");
+  bool valued = false;
+  for (int t = 0; t < T; ++t) valued = valued || !parts_[t].value.empty();
+  for (int t = 0; t < T; ++t) {
+    auto& pt = parts_[t];
+    if (valued && pt.value.empty()) pt.value.assign(pt.index.size(), 1.f);
+    AppendRows(pt, 0, pt.Size(), &blk_);
+  }
+  return true;
+}
+
 bool TextReader::Next() {
   ClearRows(&blk_);
+  if (rec_) return NextRec();
   if (pos_ >= end_) return false;
   std::ifstream f(path_, std::ios::binary);
   size_t want = std::min(chunk_, end_ - pos_), got = 0, cut = 0;
@@ -280,6 +650,8 @@ bool TextReader::Next() {
       const char* b = buf_.data() + std::max(cuts[t], cuts[t + 1]);
       if (format_ == "libsvm") {
         ParseLibSVM(a, b, &local);
+      } else if (format_ == "adfea") {
+        ParseAdfea(a, b, &local);
       } else {
         ParseCriteo(a, b, train, &local);
       }

@@ -8,13 +8,20 @@
 //   ParseCriteo     src/reader/criteo_parser.h:40-92: label, 13 integer and 26 categorical
 //                   tab-separated columns; each non-empty column j hashes to
 //                   (CityHash64(text) << 12) | j  (EncodeFeaGrpID, include/difacto/base.h:60)
+//   ParseAdfea      src/reader/adfea_parser.h:28-80: "lineid count label idx:gid ..." tokens,
+//                   each feature (idx << 12) | gid, label = (token starts with '1')
+//   "rec"           src/reader/crb_parser.h + src/data/compressed_row_block.h: dmlc RecordIO
+//                   records, each one CompressedRowBlock (LZ4 block sections)
 //   TextReader      src/reader/reader.h:18-55 over a byte range of a file (part k of n, cut
 //                   at line boundaries like dmlc::InputSplit), parsed by worker threads
 //   BatchReader     src/reader/batch_reader.cc:29-78: batch_size rows per batch, a shuffle
 //                   buffer of shuf_buf rows, negative down-sampling with rand_r, all-one
 //                   values dropped (binary data)
 //
-// Parity notes: CityHash64 is the published v1.1 algorithm restated (the library is not in
+// Parity notes: the LZ4 block codec and the dmlc RecordIO framing are third-party formats
+// (lz4, dmlc-core: un-vendored in the reference tree) restated from their published
+// specifications; the CPU tests pin the codec against the image's liblz4.so.1 in both
+// directions.  CityHash64 is the published v1.1 algorithm restated (the library is not in
 // the reference tree; no test vectors are available here, so criteo ids are parity unpinned).
 // The shuffle permutes with std::mt19937 (seed 0) where the reference calls
 // std::random_shuffle on glibc rand(); shuffled batch membership is parity unpinned
@@ -24,7 +31,9 @@
 
 #include <condition_variable>
 #include <cstdint>
+#include <cstdio>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -40,6 +49,47 @@ uint64_t CityHash64(const char* s, size_t len);
 /** parse [b, e) (whole lines) appending rows to out */
 void ParseLibSVM(const char* b, const char* e, RowBlockContainer<feaid_t>* out);
 void ParseCriteo(const char* b, const char* e, bool is_train, RowBlockContainer<feaid_t>* out);
+void ParseAdfea(const char* b, const char* e, RowBlockContainer<feaid_t>* out);
+
+// ---- LZ4 block format (the codec of CompressedRowBlock) -----------------------------------
+int Lz4CompressBound(int n);
+/** -> compressed size, 0 on failure (dst too small) */
+int Lz4Compress(const char* src, int n, char* dst, int cap);
+/** -> decompressed size, -1 on malformed input or overflow of dst_cap */
+int Lz4Decompress(const char* src, int n, char* dst, int dst_cap);
+
+// ---- CompressedRowBlock (compressed_row_block.h:20-142) ------------------------------------
+/** rows [begin, end) of blk as one record (binary values are dropped, like Compress) */
+void CompressRowBlock(const RowBlockContainer<feaid_t>& blk, size_t begin, size_t end,
+                      std::string* out);
+/** append the rows of one record to out; false on a malformed record */
+bool DecompressRowBlock(const char* data, size_t size, RowBlockContainer<feaid_t>* out);
+
+// ---- dmlc RecordIO framing (dmlc-core include/dmlc/recordio.h) ----------------------------
+class RecordIOWriter {
+ public:
+  explicit RecordIOWriter(FILE* f) : f_(f) {}
+  void WriteRecord(const std::string& rec);
+  size_t BytesWritten() const { return bytes_; }
+
+ private:
+  FILE* f_;
+  size_t bytes_ = 0;
+};
+
+/** the records of part `part` of `nparts` of a file (a record belongs to the part its head
+ * lies in, InputSplit semantics) */
+class RecordIOReader {
+ public:
+  RecordIOReader(const std::string& path, int part, int nparts);
+  ~RecordIOReader();
+  bool Next(std::string* rec);
+  size_t BytesRead() const { return read_; }
+
+ private:
+  FILE* f_ = nullptr;
+  size_t begin_ = 0, end_ = 0, pos_ = 0, read_ = 0;
+};
 
 /** append rows [begin, end) of src to dst */
 void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
@@ -58,9 +108,12 @@ class TextReader {
   std::string path_, format_;
   size_t begin_ = 0, end_ = 0, pos_ = 0, chunk_, read_ = 0;
   int nthreads_;
+  bool NextRec();
   std::vector<char> buf_;
   std::vector<RowBlockContainer<feaid_t>> parts_;  // per parser thread, reused
   RowBlockContainer<feaid_t> blk_;
+  std::unique_ptr<RecordIOReader> rec_;  // format "rec"
+  std::vector<std::string> recs_;
 };
 
 /** minibatches of a TextReader (batch_reader.cc) */

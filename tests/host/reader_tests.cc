@@ -7,8 +7,11 @@
 // parser's id layout (CityHash64 << 12 | column), criteo_parser.h:40-92.
 #include <cmath>
 #include <cstdio>
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstring>
+#include <random>
 #include <fstream>
 #include <set>
 #include <string>
@@ -207,6 +210,167 @@ static void TestCriteo(const std::string& dir) {
   std::remove(path.c_str());
 }
 
+// ---- LZ4 block codec: our encoder and decoder against the image's liblz4 (both directions)
+typedef int (*lz4_fn)(const char*, char*, int, int);
+static void TestLz4() {
+  void* h = dlopen("liblz4.so.1", RTLD_NOW);
+  lz4_fn ref_c = h ? (lz4_fn)dlsym(h, "LZ4_compress_default") : nullptr;
+  lz4_fn ref_d = h ? (lz4_fn)dlsym(h, "LZ4_decompress_safe") : nullptr;
+  if (!ref_c || !ref_d) std::printf("  note: liblz4.so.1 not found, codec checked by round trip\n");
+  std::mt19937 rng(7);
+  std::vector<std::string> inputs = {"", "a", "abcd", std::string(12, 'x'), std::string(13, 'x'),
+                                     std::string(100000, 'z')};
+  for (int n : {1, 5, 17, 64, 255, 256, 270, 1000, 65536, 70000, 300000}) {
+    std::string r(n, 0), t(n, 0), u(n, 0);
+    for (int i = 0; i < n; ++i) {
+      r[i] = (char)(rng() & 255);                 // incompressible
+      t[i] = (char)("abcabd"[(i * 7 / 3) % 6]);   // periodic
+      u[i] = (char)((rng() % 4 == 0) ? rng() % 3 : u[i > 0 ? i - 1 : 0]);  // runs
+    }
+    inputs.push_back(r);
+    inputs.push_back(t);
+    inputs.push_back(u);
+  }
+  // a row block's offsets / ids (the real payload)
+  {
+    std::vector<uint64_t> v(50000);
+    for (size_t i = 0; i < v.size(); ++i) v[i] = i * 39 + (rng() % 7);
+    inputs.emplace_back(reinterpret_cast<const char*>(v.data()), v.size() * 8);
+  }
+  for (const auto& in : inputs) {
+    const int n = (int)in.size();
+    std::vector<char> c(Lz4CompressBound(n)), d(n + 1);
+    const int m = Lz4Compress(in.data(), n, c.data(), (int)c.size());
+    EXPECT(m > 0, "lz4 compress failed");
+    EXPECT(Lz4Decompress(c.data(), m, d.data(), n) == n && std::memcmp(d.data(), in.data(), n) == 0,
+           "lz4 round trip");
+    EXPECT(Lz4Decompress(c.data(), m, d.data(), n > 0 ? n - 1 : 0) == (n == 0 ? 0 : -1),
+           "lz4 decoder must refuse to overflow its output");
+    if (!ref_c) continue;
+    EXPECT(ref_d(c.data(), d.data(), m, n) == n && std::memcmp(d.data(), in.data(), n) == 0,
+           "liblz4 cannot decode our block");
+    std::vector<char> c2(Lz4CompressBound(n) + 64);
+    const int m2 = ref_c(in.data(), c2.data(), n, (int)c2.size());
+    EXPECT(m2 > 0 && Lz4Decompress(c2.data(), m2, d.data(), n) == n &&
+               std::memcmp(d.data(), in.data(), n) == 0,
+           "we cannot decode liblz4's block");
+  }
+  // malformed input never reads or writes out of bounds
+  for (int trial = 0; trial < 2000; ++trial) {
+    std::vector<char> junk(1 + rng() % 64), out(256);
+    for (auto& b : junk) b = (char)(rng() & 255);
+    const int r = Lz4Decompress(junk.data(), (int)junk.size(), out.data(), (int)out.size());
+    EXPECT(r >= -1 && r <= 256, "lz4 junk");
+  }
+  if (h) dlclose(h);
+}
+
+// ---- RecordIO framing and CompressedRowBlock records
+static void TestRecordIO(const std::string& data, const std::string& dir) {
+  const std::string path = dir + "/recio_test.rec";
+  std::mt19937 rng(3);
+  std::vector<std::string> recs;
+  const uint32_t magic = 0xced7230au;
+  for (int i = 0; i < 300; ++i) {
+    std::string r(rng() % 200, 0);
+    for (auto& c : r) c = (char)(rng() & 255);
+    // plant the magic at aligned offsets (escaped into multi-part records)
+    for (size_t at = 0; at + 4 <= r.size(); at += 4)
+      if (rng() % 9 == 0) std::memcpy(&r[at], &magic, 4);
+    if (i % 17 == 0) r.clear();
+    recs.push_back(r);
+  }
+  {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    RecordIOWriter w(f);
+    for (const auto& r : recs) w.WriteRecord(r);
+    std::fclose(f);
+  }
+  for (int np : {1, 2, 3, 7, 64}) {
+    std::vector<std::string> got;
+    for (int p = 0; p < np; ++p) {
+      RecordIOReader rd(path, p, np);
+      std::string r;
+      while (rd.Next(&r)) got.push_back(r);
+    }
+    EXPECT(got == recs, "RecordIO parts do not return every record once, in order");
+  }
+  std::remove(path.c_str());
+  // libsvm -> rec (one record per 13 rows) -> the same rows; the reference's BatchReader
+  // known answers read through "rec"
+  const auto ref = ReadAll(data, "libsvm", 0, 1, 64 << 20, 1);
+  const std::string rp = dir + "/rcv1_test.rec";
+  {
+    FILE* f = std::fopen(rp.c_str(), "wb");
+    RecordIOWriter w(f);
+    std::string buf;
+    for (size_t b = 0; b < ref.Size(); b += 13) {
+      CompressRowBlock(ref, b, std::min(ref.Size(), b + 13), &buf);
+      w.WriteRecord(buf);
+    }
+    std::fclose(f);
+  }
+  for (int th : {1, 4}) EXPECT(Same(ref, ReadAll(rp, "rec", 0, 1, 3000, th)), "rec rows differ");
+  RowBlockContainer<feaid_t> cat;
+  for (int p = 0; p < 3; ++p) {
+    const auto part = ReadAll(rp, "rec", p, 3, 1 << 20, 2);
+    AppendRows(part, 0, part.Size(), &cat);
+  }
+  EXPECT(Same(ref, cat), "rec parts do not partition the rows");
+  {
+    BatchReader reader(rp, "rec", 0, 1, kBatch, 0, 1.f, 2);
+    int i = 0;
+    while (reader.Next() && i < 3) {
+      const auto& b = reader.Value();
+      const size_t n = b.Size();
+      double ls = 0;
+      for (size_t r = 0; r < n; ++r) ls += b.label[r];
+      EXPECT(n == kLen[i] && ls == kLabel[i] && Norm1(b.offset.data(), n + 1) == kOs[i] &&
+                 Norm1(b.index.data(), b.offset[n]) == kIdx[i],
+             "rec: BatchReader.Read known answers");
+      ++i;
+    }
+    EXPECT(i == 3, "rec: 3 batches");
+  }
+  // a malformed record is refused
+  std::string buf;
+  CompressRowBlock(ref, 0, 5, &buf);
+  RowBlockContainer<feaid_t> tmp;
+  EXPECT(DecompressRowBlock(buf.data(), buf.size(), &tmp) && tmp.Size() == 5, "crb decode");
+  for (size_t cut : {size_t(3), size_t(11), buf.size() / 2, buf.size() - 1}) {
+    RowBlockContainer<feaid_t> t2;
+    EXPECT(!DecompressRowBlock(buf.data(), cut, &t2), "truncated record accepted");
+  }
+  // binary blocks drop their values (Compress), weights survive
+  RowBlockContainer<feaid_t> bin = ref;
+  for (auto& v : bin.value) v = 1.f;
+  bin.weight.assign(bin.Size(), 0.5f);
+  CompressRowBlock(bin, 10, 20, &buf);
+  RowBlockContainer<feaid_t> t3;
+  EXPECT(DecompressRowBlock(buf.data(), buf.size(), &t3) && t3.value.empty() &&
+             t3.weight.size() == 10 && t3.weight[3] == 0.5f,
+         "binary / weighted record");
+  std::remove(rp.c_str());
+}
+
+static void TestAdfea(const std::string& dir) {
+  const std::string path = dir + "/adfea_sample.txt";
+  {
+    std::ofstream f(path);
+    f << "1001 3 1 17:2 9:0 123456789:4095\n";
+    f << "1002 1 0 5:1\n";
+    f << "1003 2 1\n";
+  }
+  const auto all = ReadAll(path, "adfea", 0, 1, 64 << 20, 2);
+  EXPECT(all.Size() == 3, "adfea rows");
+  EXPECT(all.label == std::vector<float>({1.f, 0.f, 1.f}), "adfea labels");
+  EXPECT(all.offset == std::vector<size_t>({0, 3, 4, 4}), "adfea offsets");
+  EXPECT(all.index.size() == 4 && all.index[0] == ((17ull << 12) | 2) &&
+             all.index[2] == ((123456789ull << 12) | 4095) && all.index[3] == ((5ull << 12) | 1),
+         "adfea ids: EncodeFeaGrpID(idx, gid, 12)");
+  std::remove(path.c_str());
+}
+
 static void TestCityHash() {
   EXPECT(CityHash64("", 0) == 0x9ae16a3b2f90404fULL, "CityHash64('') == k2");
   // every length class, determinism and sensitivity to each byte
@@ -242,6 +406,9 @@ int main(int argc, char** argv) {
   TestThreaded(data);
   TestCriteo(argv[2]);
   TestCityHash();
+  TestLz4();
+  TestRecordIO(data, argv[2]);
+  TestAdfea(argv[2]);
   std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
   return g_fail ? 1 : 0;
 }

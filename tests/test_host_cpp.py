@@ -140,3 +140,51 @@ def test_train_driver_model_parts_and_prediction(tmp_path):
                                want_pred=True)
     want = 1.0 / (1.0 + np.exp(-pred.astype(np.float64)))
     assert np.allclose(got, want, rtol=2e-5, atol=1e-6)
+
+
+CONV_BIN = os.path.join(ROOT, "build", "dfx_convert")
+
+
+def _convert(*args):
+    subprocess.check_call(["make", "-s", "build/dfx_convert"], cwd=ROOT)
+    r = subprocess.run([CONV_BIN] + list(args), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def test_converter_libsvm_rec_round_trip(tmp_path):
+    """dfx_convert (src/reader/converter.h): libsvm -> rec (CompressedRowBlock RecordIO) ->
+    libsvm gives back the same rows (values to the %g precision of the libsvm writer), also
+    split into parts"""
+    import numpy as np
+    from difacto_amd import data as D
+    rec, txt = str(tmp_path / "rcv1.rec"), str(tmp_path / "rcv1.txt")
+    _convert("data_in=" + DATA, "data_format=libsvm", "data_out=" + rec,
+             "data_out_format=rec", "chunk_size=0.01")
+    _convert("data_in=" + rec, "data_format=rec", "data_out=" + txt, "data_out_format=libsvm")
+    a, b = D.read_libsvm(DATA), D.read_libsvm(txt)
+    assert np.array_equal(a.offs, b.offs) and np.array_equal(a.ids, b.ids)
+    assert np.array_equal(a.labels, b.labels)
+    assert np.allclose(a.vals, b.vals, rtol=1e-5, atol=0)
+    parts = str(tmp_path / "p.rec")
+    _convert("data_in=" + DATA, "data_format=libsvm", "data_out=" + parts,
+             "data_out_format=rec", "chunk_size=0.01", "part_size=0")
+    assert os.path.exists(parts + "-part_0")
+
+
+@pytest.mark.gpu
+def test_train_driver_reads_rec(tmp_path):
+    """SGDLearner.Basic through dfx_train on the rec conversion of the data"""
+    rec = str(tmp_path / "rcv1.rec")
+    _convert("data_in=" + DATA, "data_format=libsvm", "data_out=" + rec,
+             "data_out_format=rec", "chunk_size=0.02")
+    r = subprocess.run([TRAIN_BIN, "data_in=" + rec, "data_format=rec", "V_dim=0", "l2=1",
+                        "l1=1", "lr=1", "num_jobs_per_epoch=1", "batch_size=100",
+                        "max_num_epochs=20", "shuffle=0", "stop_rel_objv=0", "max_keys=16384"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    losses = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
+              if "Training:" in l]
+    assert len(losses) == 20
+    for ep, (got, want) in enumerate(zip(losses, _BASIC_OBJV)):
+        assert abs(got * 100 - want) < 5e-5, (ep, got * 100, want)
