@@ -308,7 +308,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   const int64_t u = (int64_t)blockIdx.x * SPB + g;
   const int64_t nseg = a.nseg_host >= 0 ? a.nseg_host : (int64_t)a.ds->u_count;
   __shared__ int red[kFmNT / kWave];
-  int dnew = 0;
+  __shared__ int redn[kFmNT / kWave];
+  int dnew = 0, ninit = 0;
   if (u < nseg) {
     const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
@@ -513,17 +514,29 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
         const bool need = tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
         a.flags[u] = need ? 1u : 0u;
+        ninit = need ? 1 : 0;
       }
     }
   }
   if (FUSED) {
-    for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
-    if (lane_id() == 0) red[threadIdx.x / kWave] = dnew;
+    // new_w, and the InitV requests (dsw->n_init gates the InitV pass on the device)
+    for (int off = 32; off > 0; off >>= 1) {
+      dnew += __shfl_xor(dnew, off, kWave);
+      ninit += __shfl_xor(ninit, off, kWave);
+    }
+    if (lane_id() == 0) {
+      red[threadIdx.x / kWave] = dnew;
+      redn[threadIdx.x / kWave] = ninit;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-      int s = 0;
-      for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+      int s = 0, q = 0;
+      for (int i = 0; i < kFmNT / kWave; ++i) {
+        s += red[i];
+        q += redn[i];
+      }
       if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
+      if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
     }
   }
 }

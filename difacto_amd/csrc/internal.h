@@ -57,7 +57,7 @@ struct DevState {
   unsigned long long and_mask;
   unsigned long long diff_mask;
   unsigned int u_count;        // U of the current batch
-  unsigned int n_init;         // InitV count of the current phase
+  unsigned int n_init;         // InitV requests of the fused backward (gates its InitV pass)
   unsigned int sortmeta[32];   // radix sort plan + final buffer selector (sort.hip)
   unsigned int totals[8];      // scan totals of the current step
   unsigned int sort_epoch;     // radix sorts launched (tags their look-back words)
@@ -186,10 +186,12 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
 
 // exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
 // n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.
+// gate (optional, device): when *gate == 0 the data are all zero and the scan is skipped on
+// the device (*total_dev = 0)
 int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
-             const uint32_t* n_dev = nullptr);
+             const uint32_t* n_dev = nullptr, const uint32_t* gate = nullptr);
 int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
-             const uint32_t* n_dev = nullptr);
+             const uint32_t* n_dev = nullptr, const uint32_t* gate = nullptr);
 
 // Long segments (keys with more than kChunkOcc occurrences in a batch: skewed / Zipf data)
 // are reduced in chunks of kChunkOcc occurrences by separate groups, then combined in chunk
@@ -233,8 +235,10 @@ int loc_reserve(Workspace& w, int64_t nnz);              // a Localizer's buffer
 
 // store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
 // nds: the device state whose u_count holds the count when n_host < 0
+// gate (optional, device): the number of set flags, or any nonzero; zero skips the pass
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot, const DevState* nds = nullptr);
+              const uint32_t* slot, const DevState* nds = nullptr,
+              const uint32_t* gate = nullptr);
 // fused Update(kFeaCount): one segment per unique key (count = segment length = nds->u_count)
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
                      const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,

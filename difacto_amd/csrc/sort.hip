@@ -362,9 +362,12 @@ __device__ inline int64_t scan_limit(int64_t n, const uint32_t* n_dev) {
   return m < n ? m : n;
 }
 
+// gate (optional, device): a zero there skips the scan (the data are known to be all zero)
 __global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, int64_t n0,
                                                          const uint32_t* n_dev,
-                                                         uint32_t* tilesum) {
+                                                         uint32_t* tilesum,
+                                                         const uint32_t* gate) {
+  if (gate && *gate == 0u) return;
   __shared__ uint32_t lds[kScanNT / kWave + 1];
   const int64_t n = scan_limit(n0, n_dev);
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
@@ -377,7 +380,11 @@ __global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, i
 }
 
 __global__ __launch_bounds__(1024) void k_scan_top(uint32_t* tilesum, int64_t ntiles,
-                                                   uint32_t* total) {
+                                                   uint32_t* total, const uint32_t* gate) {
+  if (gate && *gate == 0u) {
+    if (threadIdx.x == 0 && total) *total = 0u;
+    return;
+  }
   __shared__ uint32_t lds[1024 / kWave + 1];
   uint32_t run = 0;
   for (int64_t s = 0; s < ntiles; s += 1024) {
@@ -393,7 +400,9 @@ __global__ __launch_bounds__(1024) void k_scan_top(uint32_t* tilesum, int64_t nt
 
 __global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t n0,
                                                         const uint32_t* n_dev,
-                                                        const uint32_t* tilesum) {
+                                                        const uint32_t* tilesum,
+                                                        const uint32_t* gate) {
+  if (gate && *gate == 0u) return;
   __shared__ uint32_t lds[kScanNT / kWave + 1];
   const int64_t n = scan_limit(n0, n_dev);
   const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
@@ -413,11 +422,12 @@ __global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t 
 }
 
 void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev) {
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, tilesum, ntiles, total_dev);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, tilesum, ntiles, total_dev,
+                     nullptr);
 }
 
 int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
-             const uint32_t* n_dev) {
+             const uint32_t* n_dev, const uint32_t* gate) {
   if (n <= 0) {
     if (total_dev) DFX_HIP(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), L.stream));
     return DFX_OK;
@@ -426,17 +436,17 @@ int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
   DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = L.ws->tiles.as<uint32_t>();
   hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
-                     ts);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, ts, ntiles, total_dev);
+                     ts, gate);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, ts, ntiles, total_dev, gate);
   hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
-                     ts);
+                     ts, gate);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
 int scan_u32(Context* c, uint32_t* data, int64_t n, uint32_t* total_dev,
-             const uint32_t* n_dev) {
-  return scan_u32(main_lane(c), data, n, total_dev, n_dev);
+             const uint32_t* n_dev, const uint32_t* gate) {
+  return scan_u32(main_lane(c), data, n, total_dev, n_dev, gate);
 }
 
 }  // namespace dfx

@@ -159,6 +159,7 @@ __global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B) {
   ds->prog[1] += ds->scratch[3];
   ds->sum_u += (double)bds->u_count;
   ds->n_steps += 1;
+  ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
 }
 
 // One minibatch, pipelined over three streams:
@@ -272,7 +273,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
     prof_mark(c, 6);
-    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds));
+    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init));
   } else {
     prof_mark(c, 6);
   }

@@ -48,7 +48,8 @@ __device__ inline int64_t count_of(int64_t n_host, const DevState* ds) {
 __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t* excl,
                                                  const uint32_t* total, const uint32_t* slot,
                                                  Table T, float scale, DevState* ds,
-                                                 const DevState* nds) {
+                                                 const DevState* nds, const uint32_t* gate) {
+  if (gate && *gate == 0u) return;
   const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   const int64_t n = count_of(n_host, nds);
   if (u >= n) return;
@@ -80,12 +81,12 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot, const DevState* nds) {
+              const uint32_t* slot, const DevState* nds, const uint32_t* gate) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
-  DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count));
+  DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count, gate));
   hipLaunchKernelGGL(k_initv, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
-                     n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds);
+                     n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate);
   hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
                      c->T.vcap, c->ds);
   DFX_HIP(hipGetLastError());
