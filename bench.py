@@ -84,12 +84,12 @@ def algorithmic_bytes(B, nnz, U, d):
 
 def algorithmic_bytes_sharded(B, nnz, U, d):
     """Essential HBM bytes of the worker's dfx_dist_fwd_bwd (forward + backward over pulled
-    records, binary data, all V live): forward per row offs/label/pred/p/XVp, per nnz
-    col/wpos/vpos/w/V; backward per key segstart/wpos/vpos/V + gradient record write (the
-    zero fill included), per occurrence occ_row/p/XVp."""
+    records of S = d + 4 floats, binary data, all V live): forward per row offs / label / pred /
+    p / XVp, per nnz col + the record's {w, live} + V; backward per key segstart + {w, live} +
+    V + the whole gradient record written, per occurrence occ_row / p / XVp."""
     S = d + 4
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (4 + 4 + 4 + 4 + 4 * d)
-    bwd = U * (4 + 4 + 4 + 4 * d + 2 * 4 * S) + nnz * (4 + 4 + 4 * d)
+    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (4 + 8 + 4 * d)
+    bwd = U * (4 + 8 + 4 * d + 4 * S) + nnz * (4 + 4 + 4 * d)
     return fwd + bwd
 
 

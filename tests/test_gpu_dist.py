@@ -30,10 +30,14 @@ CFGS = {
     "fm_v5_odd": (4, dict(V_dim=5, V_threshold=2, lr=0.05, l1=0.1, seed=11)),
     "logit": (2, dict(V_dim=0, lr=0.2, l1=0.05)),
     "fm_v8_n6": (6, dict(V_dim=8, V_threshold=1, lr=0.1, V_lr=0.02, l1=0.2, seed=5)),
+    # C4-shaped: V_dim 64 over 8 shards (keys drawn from 2^30 in _batches when V_dim == 64)
+    "fm_v64_n8": (8, dict(V_dim=64, V_threshold=0, lr=0.05, V_lr=0.01, l1=0.0, seed=9)),
 }
 
 
 def _batches(nranks, steps, rows=300, nnz=8, key_space=3000, seed=0):
+    if nranks == 8:  # the C4-shaped case: a 2^30 key space, few repeats
+        key_space = 1 << 30
     return [[D.synthetic(rows, nnz, key_space, binary=(r % 2 == 0), seed=seed + 131 * s + r,
                          ragged=(s == 2)) for r in range(nranks)] for s in range(steps)]
 
@@ -94,7 +98,7 @@ def test_sharded_loopback_matches_sharded_oracle(name):
 PIPE_JOBS = [(3, True), (3, True), (3, False), (4, False), (3, False), (3, False)]
 
 
-@pytest.mark.parametrize("name", ["fm_v4", "fm_v16", "logit", "fm_v8_n6"])
+@pytest.mark.parametrize("name", ["fm_v4", "fm_v16", "logit", "fm_v8_n6", "fm_v64_n8"])
 def test_sharded_pipeline_matches_stale_oracle(name):
     """the pipelined schedule (two step slots in flight, Localizer lane ahead, push of step t
     after the pull of step t+1) against oracle/dist_oracle.StaleOracle"""

@@ -18,3 +18,12 @@ timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o p
   --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline \
   > gpurun_out/pmc_write_${TAG}.log 2>&1 || exit $?
 echo "write ok"
+# the lanes serialised (per-kernel cost in isolation), and the sharded store's synchronous step
+DFX_SERIAL=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_serial \
+  -o trace --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_${TAG}_serial.log 2>&1 \
+  || exit $?
+echo "serial ok"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_sharded -o trace \
+  --output-format csv -- python3 bench.py --sharded --sync $ARGS \
+  > gpurun_out/prof_${TAG}_sharded.log 2>&1 || exit $?
+echo "sharded ok"
