@@ -48,11 +48,19 @@ $(HOSTBIN): $(HOSTSRC) $(HOSTHDR) $(LIB)
 	g++ $(HOSTFLAGS) -o $@ $(HOSTSRC) -Ldifacto_amd -ldifacto_amd \
 	  -Wl,-rpath,'$$ORIGIN/../difacto_amd'
 
-# the training driver (src/main.cc + SGDLearner::RunScheduler): reader -> feeder -> fused step
-$(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc $(HOSTHDR) $(LIB)
+# the sharded store's C++ driver (host code: HIP runtime API + RCCL, built by hipcc)
+build/obj/dist_host.o: difacto_amd/host/dist_host.cc difacto_amd/host/dist_host.h include/difacto_amd.h
+	@mkdir -p build/obj
+	$(HIPCC) -std=c++17 -O2 -fPIC -Wall -c $< -o $@
+
+# the training driver (src/main.cc + SGDLearner::RunScheduler): reader -> feeder -> fused step,
+# or the sharded store over RCCL / loopback
+$(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc $(HOSTHDR) difacto_amd/host/dist_host.h \
+  build/obj/dist_host.o $(LIB)
 	@mkdir -p build
-	g++ $(HOSTFLAGS) -o $@ $(HOSTLIB) difacto_amd/host/train_main.cc -Ldifacto_amd \
-	  -ldifacto_amd -Wl,-rpath,'$$ORIGIN/../difacto_amd'
+	g++ $(HOSTFLAGS) -o $@ $(HOSTLIB) difacto_amd/host/train_main.cc build/obj/dist_host.o \
+	  -Ldifacto_amd -ldifacto_amd -L/opt/rocm/lib -lrccl -lamdhip64 \
+	  -Wl,-rpath,'$$ORIGIN/../difacto_amd' -Wl,-rpath,/opt/rocm/lib
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -7,6 +7,15 @@
 //                   [load_epoch=-1] [has_aux=0] [task=0|2] [pred_out=F] [pred_prob=1]
 //                   [fused=1] [nthreads=8] [V_dim=..] [lr=..] [l1=..] ...  (SGDUpdaterParam)
 //
+// Sharded store (KVStoreDist over GPUs, dist_host.h): `shards=N` holds N shards on this GPU
+// (loopback exchange, for tests); `shards=-1` or a launch with WORLD_SIZE > 1 (RANK / LOCAL_RANK as
+// torchrun sets them; DFX_COMM_ID_FILE or /tmp/dfx_comm_<MASTER_PORT> as the node-local
+// rendezvous) runs one shard per process over RCCL.  Every epoch is split into
+// num_jobs_per_epoch x shards parts; shard r reads parts r, r + shards, ... in order, the shards
+// step together (an exhausted shard submits empty batches until all are done), and
+// `pipelined=1` (default) selects the 1-step-stale schedule.  Each server saves
+// <model_out>_part-<rank>.
+//
 // Model files are named like SGDLearner::ModelName (sgd_learner.h:65-69):
 // <prefix>[_iter-<epoch>]_part-0, in SGDUpdater::Save's format; task=2 predicts data_val with
 // model_in into <pred_out>_part-0, one "label\tprediction" line per row (SavePred,
@@ -20,10 +29,12 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include <string>
 
+#include "dist_host.h"
 #include "gpu_adapters.h"
 #include "reader.h"
 
@@ -36,15 +47,20 @@ struct Param {
   float neg_sampling = 1.f;
   int max_num_epochs = 20, num_jobs_per_epoch = 10, nthreads = 8;
   int load_epoch = -1, task = 0;
+  int shards = 0;  // > 0: that many loopback shards in this process; -1: one shard, RCCL
+  bool pipelined = true;
   bool has_aux = false, pred_prob = true;
   double stop_rel_objv = 1e-5;
 };
 
-// sgd_learner.h:65-69 (one server: rank 0)
-std::string ModelName(const std::string& prefix, int iter) {
+// sgd_learner.h:65-69
+std::string ModelNamePart(const std::string& prefix, int iter, int rank) {
   std::string name = prefix;
   if (iter >= 0) name += "_iter-" + std::to_string(iter);
-  return name + "_part-0";
+  return name + "_part-" + std::to_string(rank);
+}
+std::string ModelName(const std::string& prefix, int iter) {  // one server: rank 0
+  return ModelNamePart(prefix, iter, 0);
 }
 
 double Now() {
@@ -94,6 +110,154 @@ Progress RunEpoch(GpuSGDLearner* learner, const Param& P, int epoch, int job_typ
   }
   return prog;
 }
+// ---- the sharded store ----------------------------------------------------------------------
+// a batch in device memory, uploaded on the context's stream (three per shard in flight)
+struct DevBatch {
+  dfx_ctx* c = nullptr;
+  std::unique_ptr<DevArray<uint64_t>> off, idx;
+  std::unique_ptr<DevArray<float>> val, lab, wt;
+  dfx_batch b{};
+  void Upload(dfx_ctx* ctx, const RowBlockContainer<feaid_t>* blk) {
+    if (!off) {
+      c = ctx;
+      off.reset(new DevArray<uint64_t>(c));
+      idx.reset(new DevArray<uint64_t>(c));
+      val.reset(new DevArray<float>(c));
+      lab.reset(new DevArray<float>(c));
+      wt.reset(new DevArray<float>(c));
+    }
+    const size_t B = blk ? blk->Size() : 0, nnz = blk ? blk->index.size() : 0;
+    static const uint64_t zero = 0;
+    b = dfx_batch{};
+    b.size = (int64_t)B;
+    b.nnz = (int64_t)nnz;
+    b.offset = blk ? reinterpret_cast<uint64_t*>(off->upload(
+                         reinterpret_cast<const uint64_t*>(blk->offset.data()), B + 1))
+                   : off->upload(&zero, 1);
+    b.index = nnz ? idx->upload(blk->index.data(), nnz) : nullptr;
+    b.value = blk && !blk->value.empty() ? val->upload(blk->value.data(), nnz) : nullptr;
+    b.label = B ? lab->upload(blk->label.data(), B) : nullptr;
+    b.weight = blk && !blk->weight.empty() ? wt->upload(blk->weight.data(), B) : nullptr;
+  }
+};
+
+std::string KwString(const KWArgs& kw) {
+  std::string s;
+  for (const auto& p : kw) {
+    if (p.first == "fused") continue;
+    if (!s.empty()) s += ",";
+    s += p.first + "=" + p.second;
+  }
+  return s;
+}
+
+int RunSharded(const Param& P, const KWArgs& rest) {
+  const char* ws = std::getenv("WORLD_SIZE");
+  const int world = ws ? std::atoi(ws) : 1;
+  const bool rccl = world > 1 || P.shards < 0;
+  const int rank = rccl && std::getenv("RANK") ? std::atoi(std::getenv("RANK")) : 0;
+  const int local = std::getenv("LOCAL_RANK") ? std::atoi(std::getenv("LOCAL_RANK")) : 0;
+  const int nlocal = rccl ? 1 : P.shards;
+  const int nshards = rccl ? world : P.shards;
+  if (P.task == 2 || !P.data_val.empty()) {
+    std::fprintf(stderr, "sharded store: training only (task=0, no data_val)\n");
+    return 2;
+  }
+  std::vector<dfx_ctx*> ctxs(nlocal, nullptr);
+  const std::string kw = KwString(rest);
+  for (int l = 0; l < nlocal; ++l)
+    DfxCheck(dfx_ctx_create(rccl ? local : 0, kw.c_str(), &ctxs[l]), "dfx_ctx_create");
+  std::unique_ptr<ShardExchange> ex;
+  if (rccl) {
+    std::string id_file;
+    if (const char* f = std::getenv("DFX_COMM_ID_FILE")) {
+      id_file = f;
+    } else {
+      const char* port = std::getenv("MASTER_PORT");
+      id_file = std::string("/tmp/dfx_comm_") + (port ? port : "0");
+    }
+    ex = MakeRcclExchange(ctxs[0], rank, world, id_file);
+  } else {
+    ex = MakeLoopbackExchange(ctxs);
+  }
+  if (!P.model_in.empty())
+    for (int l = 0; l < nlocal; ++l)
+      DfxCheck(dfx_store_load(ctxs[l],
+                              ModelNamePart(P.model_in, P.load_epoch > 0 ? P.load_epoch : -1,
+                                            ex->rank(l)).c_str()),
+               "dfx_store_load");
+  {
+    GpuShardedStore store(ex.get(), P.pipelined);
+    std::vector<std::vector<DevBatch>> dev(nlocal);
+    for (auto& v : dev) v.resize(3);
+    int ring = 0;
+    const double t0 = Now();
+    double pre_loss = 0;
+    for (int k = std::max(0, P.load_epoch > 0 ? P.load_epoch + 1 : 0); k < P.max_num_epochs; ++k) {
+      const double te = Now();
+      for (int job = 0; job < P.num_jobs_per_epoch; ++job) {
+        // shard r reads part job * nshards + r of num_jobs_per_epoch * nshards
+        const int nparts = P.num_jobs_per_epoch * nshards;
+        std::vector<std::unique_ptr<ThreadedBatchReader>> rd(nlocal);
+        for (int l = 0; l < nlocal; ++l)
+          rd[l].reset(new ThreadedBatchReader(P.data_in, P.data_format,
+                                              job * nshards + ex->rank(l), nparts, P.batch_size,
+                                              P.batch_size * P.shuffle, P.neg_sampling,
+                                              P.nthreads));
+        std::vector<bool> more(nlocal, true);
+        for (;;) {
+          std::vector<dfx_batch> bs(nlocal);
+          std::vector<double> any(1, 0.0);
+          for (int l = 0; l < nlocal; ++l) {
+            if (more[l]) more[l] = rd[l]->Next();
+            if (more[l]) any[0] += 1;
+          }
+          ex->AllReduceSum(&any);
+          bool local_any = false;
+          for (int l = 0; l < nlocal; ++l) local_any = local_any || more[l];
+          if (any[0] == 0 && !local_any) break;
+          for (int l = 0; l < nlocal; ++l) {
+            DevBatch& db = dev[l][ring];
+            db.Upload(ctxs[l], more[l] ? &rd[l]->Value() : nullptr);
+            bs[l] = db.b;
+          }
+          ring = (ring + 1) % 3;
+          store.Submit(bs, GpuSGDLearner::kTraining, k == 0);
+        }
+      }
+      store.Flush();
+      std::vector<double> pr(3, 0.0);
+      for (int l = 0; l < nlocal; ++l) {
+        dfx_progress p;
+        DfxCheck(dfx_progress_read(ctxs[l], &p, 1), "dfx_progress_read");
+        pr[0] += p.nrows;
+        pr[1] += p.loss;
+        pr[2] += p.auc;
+      }
+      ex->AllReduceSum(&pr);
+      Progress tr;
+      tr.nrows = pr[0];
+      tr.loss = pr[1];
+      tr.auc = pr[2];
+      const double dt = Now() - te;
+      if (rank == 0)
+        std::printf("Epoch[%d] Training: %s  (%.0f ex/s incl. parse+PCIe, %d shards, %.2f s)\n", k,
+                    Text(tr).c_str(), tr.nrows / dt, nshards, Now() - t0);
+      std::fflush(stdout);
+      const double eps = std::fabs(tr.loss - pre_loss) / pre_loss;
+      if (eps < P.stop_rel_objv) break;
+      pre_loss = tr.loss;
+    }
+  }
+  if (!P.model_out.empty())
+    for (int l = 0; l < nlocal; ++l)
+      DfxCheck(dfx_store_save(ctxs[l], ModelNamePart(P.model_out, -1, ex->rank(l)).c_str(),
+                              P.has_aux ? 1 : 0),
+               "dfx_store_save");
+  ex.reset();
+  for (auto c : ctxs) dfx_ctx_destroy(c);
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -124,6 +288,8 @@ int main(int argc, char** argv) {
     else if (k == "pred_out") P.pred_out = v;
     else if (k == "pred_prob") P.pred_prob = std::stoi(v) != 0;
     else if (k == "has_aux") P.has_aux = std::stoi(v) != 0;
+    else if (k == "shards") P.shards = std::stoi(v);
+    else if (k == "pipelined") P.pipelined = std::stoi(v) != 0;
     else {
       fused_given = fused_given || k == "fused";
       rest.push_back({k, v});
@@ -133,6 +299,8 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s data_in=FILE [key=value ...]\n", argv[0]);
     return 2;
   }
+  const char* ws = std::getenv("WORLD_SIZE");
+  if (P.shards != 0 || (ws && std::atoi(ws) > 1)) return RunSharded(P, rest);
   if (!fused_given) rest.push_back({"fused", "1"});
   GpuSGDLearner learner(rest);
   int k0 = 0;

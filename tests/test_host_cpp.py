@@ -188,3 +188,120 @@ def test_train_driver_reads_rec(tmp_path):
     assert len(losses) == 20
     for ep, (got, want) in enumerate(zip(losses, _BASIC_OBJV)):
         assert abs(got * 100 - want) < 5e-5, (ep, got * 100, want)
+
+
+def _part_rows(path, part, nparts):
+    """row indices of part k of n of a text file: byte range [size*k/n, size*(k+1)/n), both
+    ends moved to the next line start (reader.cc TextReader, InputSplit semantics)"""
+    data = open(path, "rb").read()
+    size = len(data)
+
+    def line_start(at):
+        if at == 0 or at >= size:
+            return min(at, size)
+        nl = data.find(b"\n", at - 1)
+        return size if nl < 0 else nl + 1
+
+    b, e = line_start(size * part // nparts), line_start(size * (part + 1) // nparts)
+    starts = [0] + [i + 1 for i, c in enumerate(data) if c == 10][:-1]
+    return [r for r, s in enumerate(starts) if b <= s < e]
+
+
+def _slice(blk, rows):
+    from difacto_amd import data as D
+    import numpy as np
+    if not rows:
+        return D.RowBlock(np.zeros(1, np.uint64), np.zeros(0, np.uint64), None,
+                          np.zeros(0, np.float32))
+    offs = blk.offs.astype(np.int64)
+    lo, hi = rows[0], rows[-1] + 1
+    o = offs[lo:hi + 1] - offs[lo]
+    vals = blk.vals[offs[lo]:offs[hi]]
+    if np.all(vals == 1):
+        vals = None  # batch_reader.cc:71-73
+    return D.RowBlock(o.astype(np.uint64), blk.ids[offs[lo]:offs[hi]], vals,
+                      blk.labels[lo:hi])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipelined", [1, 0])
+def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined):
+    """dfx_train shards=3: the C++ sharded store (dist_host.cc, loopback exchange) against the
+    sharded oracle of the same schedule, on the batches the driver forms (shard r reads part
+    r of 3, batches of 10 rows, shards step together with empty batches once done): per-epoch
+    loss, and every server's saved part against the oracle's server state"""
+    import numpy as np
+    from oracle import dist_oracle as DO
+    from oracle import oracle as O
+    from difacto_amd import data as D
+    N, bs, epochs = 3, 10, 3
+    kw = dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1, seed=7)
+    model = str(tmp_path / "m")
+    args = [TRAIN_BIN, "data_in=" + DATA, "shards=%d" % N, "pipelined=%d" % pipelined,
+            "num_jobs_per_epoch=1", "shuffle=0", "batch_size=%d" % bs,
+            "max_num_epochs=%d" % epochs, "stop_rel_objv=0", "model_out=" + model, "has_aux=1",
+            "max_keys=65536"] + ["%s=%s" % kv for kv in kw.items()]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
+           if "Training:" in l]
+    assert len(got) == epochs, r.stdout
+    blk = D.read_libsvm(DATA)
+    parts = [_part_rows(DATA, p, N) for p in range(N)]
+    nsteps = max((len(p) + bs - 1) // bs for p in parts)
+    so = DO.StaleOracle(N, **kw) if pipelined else DO.ShardedOracle(N, **kw)
+    for ep in range(epochs):
+        loss = 0.0
+        for t in range(nsteps):
+            step = [_slice(blk, parts[p][t * bs:(t + 1) * bs]) for p in range(N)]
+            out = (so.submit(step, push_cnt=ep == 0) if pipelined
+                   else so.step(step, push_cnt=ep == 0))
+            loss += sum(o[0] for o in out)
+        if pipelined:
+            so.flush()
+        assert abs(got[ep] - loss / blk.size) <= 1e-5 * abs(loss / blk.size), (ep, got[ep])
+    ups = so.up
+    for g in range(N):
+        up = O.Updater(**kw)
+        up.load(model + "_part-%d" % g)
+        keys = np.unique(blk.ids)
+        n = 0
+        for k in O.localize(blk.offs, blk.ids)[0]:
+            a, b = up.entry(k), ups[g].entry(k)
+            if a is None:
+                continue
+            n += 1
+            assert b is not None
+            assert np.allclose(a[0][:3], b[0][:3], rtol=1e-5, atol=1e-6), (g, k)
+            assert (a[1] is None) == (b[1] is None)
+            if a[1] is not None:
+                assert np.allclose(a[1], b[1], rtol=1e-5, atol=1e-6)
+        assert n == up.size() > 0
+
+
+@pytest.mark.gpu
+def test_train_driver_sharded_rccl_world1(tmp_path):
+    """shards=-1: one shard per process over RCCL (communicators from a node-local id file);
+    at world size 1 it trains like the single-context store: the same batches (one part),
+    the same stale-by-one pipelined schedule as a 1-shard StaleOracle"""
+    from oracle import dist_oracle as DO
+    from difacto_amd import data as D
+    kw = dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1, seed=7)
+    env = dict(os.environ, DFX_COMM_ID_FILE=str(tmp_path / "id"))
+    r = subprocess.run([TRAIN_BIN, "data_in=" + DATA, "shards=-1", "num_jobs_per_epoch=1",
+                        "shuffle=0", "batch_size=25", "max_num_epochs=2", "stop_rel_objv=0",
+                        "max_keys=65536"] + ["%s=%s" % kv for kv in kw.items()],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
+           if "Training:" in l]
+    blk = D.read_libsvm(DATA)
+    so = DO.StaleOracle(1, **kw)
+    for ep in range(2):
+        loss = 0.0
+        for t in range(4):
+            loss += so.submit([_slice(blk, list(range(25 * t, 25 * t + 25)))],
+                              push_cnt=ep == 0)[0][0]
+        so.flush()
+        assert abs(got[ep] - loss / 100) <= 1e-5 * abs(loss / 100), (ep, got[ep])
+    assert not os.path.exists(str(tmp_path / "id"))
