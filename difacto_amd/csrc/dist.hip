@@ -81,8 +81,7 @@ __global__ void k_owner_splits(const uint64_t* uniq, const DevState* lds, uint32
 
 __global__ void k_dist_worker_finalize(DevState* ds, int64_t B) {
   ds->prog[0] += (double)B;  // sgd::Progress of this worker (sgd_learner.cc:213-229)
-  ds->prog[1] += ds->scratch[3];
-  ds->prog[2] += ds->auc_n;
+  ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
 }
 
 // ---- owner: received keys -> unique segments -----------------------------------------------
@@ -542,7 +541,15 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   int nblk = 0;
   DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
-  DFX_TRY(auc_run(main_lane(c), B, b->label, pred, &c->ds->auc_n));
+  // AUC on its own lane beside the backward (as in the fused step): a snapshot of (pred,
+  // label) on the main stream, joined by the next snapshot / dfx_sync / dfx_progress_read
+  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+  DFX_TRY(auc_snapshot(AL, c->stream, B, b->label, pred));
+  DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
+  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true));
+  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {
     // every gradient record is written whole, the live slot carrying whether this worker
