@@ -103,7 +103,7 @@ static void release_ws(Workspace& w) {
   DevBuf* bufs[] = {&w.keys0, &w.keys1, &w.vals0, &w.vals1, &w.rowid, &w.hist, &w.tiles,
                     &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
-                    &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1, &w.atiles,
+                    &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted};
   for (DevBuf* b : bufs) b->release();
 }

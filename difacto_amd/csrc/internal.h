@@ -84,7 +84,7 @@ struct Workspace {
   DevBuf wv;              // per nnz: {w, vrow} of its key (fused forward)
   // per-row arrays
   DevBuf p, pred, XVp, rowtmp;
-  DevBuf ak0, ak1, av0, av1, atiles;  // AUC sort buffers
+  DevBuf ak0, ak1, av0, av1;  // AUC sort buffers (keys, labels; double-buffered)
   DevBuf dscratch;  // double partials
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)

@@ -107,31 +107,27 @@ int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
   return DFX_OK;
 }
 
-// ---- the AUC lane: sorted runs + binary-search counting, no inter-block waits ----------
-// Beside the backward the AUC needs only to finish within a step, and its blocks must never
-// park on CUs the backward needs (a look-back sort's spinning blocks would).  So:
+// ---- the AUC lane: a stable sort without inter-block waits, then one counting pass ---------
+// Beside the backward the AUC needs only to finish within a step, and it should take as few
+// CU slots and as little memory traffic from the backward as possible (a look-back sort's
+// spinning blocks would park on CUs; a search per (item, tile) pair floods them):
 //   k_auc_runs   one block per 4096-item tile (input order): stable LSD sort of the tile in
-//                LDS; sorted keys, the exclusive prefix count of positives, the tile's own
-//                area (positives before each negative inside the tile) and positive count
-//   k_auc_cross  one thread per (item, other tile): a negative with key x in tile r counts
-//                the positives of tile r' < r with key <= x (they precede it in a stable
-//                sort) and of tile r' > r with key < x — a binary search in the sorted tile
-//   k_auc_sum    area and positives summed in a fixed order -> AUC*n (flip, P = 0 / n rule)
-// Every partial is an integer held exactly in double, so the result is deterministic and
-// equals the global stable sort's rank-sum.
+//                LDS, sorted keys and labels out
+//   k_auc_merge  log2(tiles) rounds of stable pairwise merge-path merges (the earlier run wins
+//                ties), so the result is the global stable sort by key
+//   k_auc_area   one block: positives before each negative, summed exactly in double (every
+//                partial is an integer) -> AUC*n (flip, P = 0 / n rule)
+// The result is deterministic and equals the global stable sort's rank-sum.
 constexpr int kArNT = 256, kArItems = 16, kArTile = kArNT * kArItems;  // 4096
 
 __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ lab,
                                                    uint32_t* __restrict__ skey,
-                                                   uint32_t* __restrict__ ppre,
-                                                   double* __restrict__ part,
-                                                   uint32_t* __restrict__ npos) {
+                                                   uint32_t* __restrict__ slab) {
   __shared__ uint32_t lk[2][kArTile];
   __shared__ uint8_t ll[2][kArTile];
   __shared__ uint32_t wcnt[kArNT / kWave][256];
   __shared__ uint32_t lds[kArNT / kWave + 1];
-  __shared__ double dred[kArNT / kWave];
   const int t = threadIdx.x, w = t / kWave, l = lane_id();
   const int64_t tb = (int64_t)blockIdx.x * kArTile;
   const int m = (int)((n - tb) < kArTile ? (n - tb) : kArTile);
@@ -193,97 +189,71 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
     __syncthreads();
     src ^= 1;
   }
-  // sorted tile out; exclusive prefix of positives; the tile's own area
+  // the sorted tile out
+  for (int i = t; i < m; i += kArNT) {
+    skey[tb + i] = lk[src][i];
+    slab[tb + i] = ll[src][i];
+  }
+}
+
+constexpr int kAmNT = 256, kAmItems = 8;  // merge: outputs per thread
+
+// one round: runs of width w, pair p = [2pw, 2pw + w) + [2pw + w, 2pw + 2w) (clamped to n)
+__global__ __launch_bounds__(kAmNT) void k_auc_merge(int64_t n, int64_t w,
+                                                    const uint32_t* __restrict__ kin,
+                                                    const uint32_t* __restrict__ lin,
+                                                    uint32_t* __restrict__ kout,
+                                                    uint32_t* __restrict__ lout) {
+  int64_t t = ((int64_t)blockIdx.x * kAmNT + threadIdx.x) * kAmItems;
+  if (t >= n) return;
+  const int64_t tend = t + kAmItems < n ? t + kAmItems : n;
+  const int64_t a0 = (t / (2 * w)) * (2 * w);
+  const int64_t a1 = a0 + w < n ? a0 + w : n;
+  const int64_t b1 = a0 + 2 * w < n ? a0 + 2 * w : n;
+  const int64_t na = a1 - a0, nb = b1 - a1, k = t - a0;
+  // merge path: how many of the first k outputs come from A (A wins ties)
+  int64_t lo = k - nb > 0 ? k - nb : 0, hi = k < na ? k : na;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (kin[a0 + m] <= kin[a1 + k - 1 - m]) lo = m + 1; else hi = m;
+  }
+  int64_t i = a0 + lo, j = a1 + (k - lo);
+  const int64_t stop = tend < b1 ? tend : b1;
+  for (; t < stop; ++t) {
+    const bool takeA = i < a1 && (j >= b1 || kin[i] <= kin[j]);
+    const int64_t src = takeA ? i++ : j++;
+    kout[t] = kin[src];
+    lout[t] = lin[src];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_auc_area(int64_t n, const uint32_t* __restrict__ slab,
+                                                   double* out, int accumulate) {
+  __shared__ uint32_t lds[1024 / kWave + 1];
+  __shared__ double red[1024 / kWave];
   double area = 0;
   uint32_t carry = 0;
-  uint32_t* pp = ppre + (int64_t)blockIdx.x * (kArTile + 1);
-  for (int cb = 0; cb < kArTile; cb += kArNT) {
-    const int i = cb + t;
-    const uint32_t y = i < m ? (uint32_t)ll[src][i] : 0u;
+  for (int64_t c = 0; c < n; c += 1024) {
+    const int64_t i = c + threadIdx.x;
+    const uint32_t y = i < n ? slab[i] : 0u;
     uint32_t tot;
-    const uint32_t before = block_excl_scan<kArNT>(y, lds, &tot) + carry;
-    if (i < m) {
-      skey[tb + i] = lk[src][i];
-      pp[i] = before;
-      if (!y) area += (double)before;
-    }
+    const uint32_t before = block_excl_scan<1024>(y, lds, &tot) + carry;
+    if (i < n && !y) area += (double)before;
     carry += tot;
   }
-  if (t == 0) pp[m] = carry;
   for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
-  if (l == 0) dred[w] = area;
-  __syncthreads();
-  if (t == 0) {
-    double a = 0;
-    for (int i = 0; i < kArNT / kWave; ++i) a += dred[i];
-    part[blockIdx.x] = a;
-    npos[blockIdx.x] = carry;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_auc_cross(int64_t n, int ntiles,
-                                                   const uint32_t* __restrict__ key,
-                                                   const uint32_t* __restrict__ lab,
-                                                   const uint32_t* __restrict__ skey,
-                                                   const uint32_t* __restrict__ ppre,
-                                                   double* __restrict__ part2) {
-  __shared__ double dred[256 / kWave];
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t i = g / ntiles;
-  const int rr = (int)(g % ntiles);
-  double add = 0;
-  if (i < n && !lab[i]) {
-    const int r = (int)(i / kArTile);
-    if (rr != r) {
-      const uint32_t x = key[i];
-      const int64_t b = (int64_t)rr * kArTile;
-      const int len = (int)((n - b) < kArTile ? (n - b) : kArTile);
-      const uint32_t* sk = skey + b;
-      int lo = 0, hi = len;  // first index with sk > x (rr < r) or sk >= x (rr > r)
-      if (rr < r) {
-        while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] <= x) lo = mid + 1; else hi = mid; }
-      } else {
-        while (lo < hi) { const int mid = (lo + hi) >> 1; if (sk[mid] < x) lo = mid + 1; else hi = mid; }
-      }
-      add = (double)ppre[(int64_t)rr * (kArTile + 1) + lo];
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, kWave);
-  if (lane_id() == 0) dred[threadIdx.x / kWave] = add;
+  if (lane_id() == 0) red[threadIdx.x / kWave] = area;
   __syncthreads();
   if (threadIdx.x == 0) {
     double a = 0;
-    for (int k = 0; k < 256 / kWave; ++k) a += dred[k];
-    part2[blockIdx.x] = a;
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_auc_sum(int64_t n, int ntiles, const double* part,
-                                                  const uint32_t* npos, int64_t nb2,
-                                                  const double* part2, double* out,
-                                                  int accumulate) {
-  __shared__ double red[1024 / kWave];
-  __shared__ uint32_t pred_[1024 / kWave];
-  double a = 0;
-  uint32_t P = 0;
-  for (int64_t i = threadIdx.x; i < nb2; i += 1024) a += part2[i];
-  for (int i = threadIdx.x; i < ntiles; i += 1024) { a += part[i]; P += npos[i]; }
-  for (int off = 32; off > 0; off >>= 1) {
-    a += __shfl_xor(a, off, kWave);
-    P += __shfl_xor(P, off, kWave);
-  }
-  if (lane_id() == 0) { red[threadIdx.x / kWave] = a; pred_[threadIdx.x / kWave] = P; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double area = 0;
-    double Pd = 0;
-    for (int i = 0; i < 1024 / kWave; ++i) { area += red[i]; Pd += (double)pred_[i]; }
+    for (int i = 0; i < 1024 / kWave; ++i) a += red[i];
+    const double P = (double)carry;
     double r;
-    if (Pd == 0 || Pd == (double)n) {
+    if (P == 0 || P == (double)n) {
       r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
     } else {
-      area /= Pd * ((double)n - Pd);
-      r = (area < 0.5 ? 1 - area : area) * (double)n;
+      a /= P * ((double)n - P);
+      r = (a < 0.5 ? 1 - a : a) * (double)n;
     }
     *out = accumulate ? *out + r : r;
   }
@@ -297,25 +267,22 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate) {
     return DFX_OK;
   }
   const int ntiles = (int)((B + kArTile - 1) / kArTile);
-  const int64_t pairs = B * (int64_t)ntiles;
-  const int64_t nb2 = (pairs + 255) / 256;
-  // ak1: sorted keys; av1: per-tile positive prefixes (ntiles * (kArTile + 1) u32); atiles:
-  // per-tile area + positive count, then the cross partials
+  // snapshot in (ak0 keys, av0 labels); ping-pong (ak1, av1) <-> (ak0, av0)
   DFX_TRY(ws.ak1.ensure(B * 4));
-  DFX_TRY(ws.av1.ensure((size_t)ntiles * (kArTile + 1) * 4));
-  DFX_TRY(ws.atiles.ensure(ntiles * 8 + ntiles * 4 + nb2 * 8 + 64));
-  double* part = ws.atiles.as<double>();
-  uint32_t* npos = reinterpret_cast<uint32_t*>(part + ntiles);
-  double* part2 = reinterpret_cast<double*>(ws.atiles.as<char>() +
-                                            ((ntiles * 12 + 15) / 16) * 16);
-  const uint32_t* k0 = ws.ak0.as<uint32_t>();
-  const uint32_t* v0 = ws.av0.as<uint32_t>();
-  hipLaunchKernelGGL(k_auc_runs, dim3(ntiles), dim3(kArNT), 0, L.stream, B, k0, v0,
-                     ws.ak1.as<uint32_t>(), ws.av1.as<uint32_t>(), part, npos);
-  hipLaunchKernelGGL(k_auc_cross, dim3((unsigned)nb2), dim3(256), 0, L.stream, B, ntiles, k0, v0,
-                     ws.ak1.as<uint32_t>(), ws.av1.as<uint32_t>(), part2);
-  hipLaunchKernelGGL(k_auc_sum, dim3(1), dim3(1024), 0, L.stream, B, ntiles, part, npos, nb2,
-                     part2, out_dev, accumulate ? 1 : 0);
+  DFX_TRY(ws.av1.ensure(B * 4));
+  uint32_t* k[2] = {ws.ak1.as<uint32_t>(), ws.ak0.as<uint32_t>()};
+  uint32_t* v[2] = {ws.av1.as<uint32_t>(), ws.av0.as<uint32_t>()};
+  hipLaunchKernelGGL(k_auc_runs, dim3(ntiles), dim3(kArNT), 0, L.stream, B, k[1], v[1], k[0],
+                     v[0]);
+  int cur = 0;
+  for (int64_t w = kArTile; w < B; w *= 2) {
+    const int64_t per = (int64_t)kAmNT * kAmItems;
+    hipLaunchKernelGGL(k_auc_merge, dim3((unsigned)((B + per - 1) / per)), dim3(kAmNT), 0,
+                       L.stream, B, w, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1]);
+    cur ^= 1;
+  }
+  hipLaunchKernelGGL(k_auc_area, dim3(1), dim3(1024), 0, L.stream, B, v[cur], out_dev,
+                     accumulate ? 1 : 0);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

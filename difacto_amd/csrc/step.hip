@@ -62,17 +62,13 @@ int loc_reserve(Workspace& w, int64_t nnz) {
   return DFX_OK;
 }
 
-// the AUC lane (metric.hip auc_finish: sorted tiles of 4096, their positive prefixes, the
-// per-tile and per-pair partial sums)
+// the AUC lane (metric.hip auc_finish: keys and labels, double-buffered for the merges)
 static int auc_reserve(Workspace& w, int64_t rows) {
   if (rows < 1) rows = 1;
-  const int64_t nt = (rows + 4095) / 4096;
-  const int64_t nb2 = (rows * nt + 255) / 256;
   DFX_TRY(w.ak0.ensure(rows * 4));
   DFX_TRY(w.ak1.ensure(rows * 4));
   DFX_TRY(w.av0.ensure(rows * 4));
-  DFX_TRY(w.av1.ensure((size_t)nt * 4097 * 4));
-  DFX_TRY(w.atiles.ensure(nt * 12 + nb2 * 8 + 64));
+  DFX_TRY(w.av1.ensure(rows * 4));
   w.rows = rows;
   return DFX_OK;
 }
