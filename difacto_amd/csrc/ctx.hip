@@ -111,6 +111,7 @@ static void release_ws(Workspace& w) {
 // streams, events and lane states of the fused step's pipeline, created on first use
 int pipeline_init(Context* c) {
   if (c->loc_stream) return DFX_OK;
+  if (const char* fp = getenv("DFX_FWD_PROBE")) c->fwd_probe = atoi(fp) != 0;
   // the side lanes run latency-bound chains of small launches beside a full-occupancy
   // backward: give them priority so their workgroups are not queued behind its tail
   int lo = 0, hi = 0;

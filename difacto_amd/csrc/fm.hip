@@ -24,7 +24,8 @@ namespace dfx {
 
 constexpr int kFmNT = 256;
 
-enum FwdMode { kPredict = 0, kGradPrep = 1, kFused = 2 };
+// kFusedProbe: kFused whose nnz find their keys in the table (FwdArgs::index)
+enum FwdMode { kPredict = 0, kGradPrep = 1, kFused = 2, kFusedProbe = 3 };
 
 // p = -y / (1 + exp(y * pred)) [* weight]   (fm_loss.h:155-165).  exp in double, rounded:
 // correctly rounded like glibc's expf in all but rare ties (within the 1e-5 tolerance).
@@ -79,7 +80,9 @@ __device__ inline void store_coords(float* row, int l, int d, const float (&v)[C
 template <int G, int CPL, int MODE, bool PACKED, bool VEC>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   constexpr int RPB = kFmNT / G;  // rows per block
-  constexpr int UNR = CPL <= 4 ? 8 : (CPL <= 8 ? 4 : 2);
+  constexpr bool PROBE = MODE == kFusedProbe;
+  // probe mode carries keys and home slots per item: fewer items per batch, more waves
+  constexpr int UNR = PROBE ? (CPL <= 4 ? 4 : 2) : (CPL <= 4 ? 8 : (CPL <= 8 ? 4 : 2));
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t r = (int64_t)blockIdx.x * RPB + g;
@@ -97,16 +100,45 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       uint32_t c[UNR];
       float x[UNR];
       int2 wr[UNR];
+      uint64_t key[UNR], hs[UNR];
 #pragma unroll
       for (int t = 0; t < UNR; ++t) {
         const uint64_t jj = (j0 + t < o1) ? j0 + t : o1 - 1;
-        if (PACKED && a.wv) {
+        if constexpr (PROBE) {
+          // the Localizer's key (localize.hip k_loc_transform) and its home slot
+          const uint64_t id = a.index[jj];
+          const uint64_t m = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+          key[t] = reverse_bytes(m);
+          hs[t] = tbl_hash(key[t], a.T);
+          c[t] = (uint32_t)jj;
+        } else if (PACKED && a.wv) {
           wr[t] = a.wv[jj];
           c[t] = (uint32_t)jj;
         } else {
           c[t] = a.col[jj];
         }
         x[t] = valued ? a.val[jj] : 1.f;
+      }
+      if constexpr (PROBE) {
+        // first probes of all UNR items, then the (rare) longer probe chains
+        uint64_t ek[UNR];
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          const Entry* e = a.T.ent + hs[t];
+          wr[t] = *reinterpret_cast<const int2*>(e);
+          ek[t] = e->key;
+        }
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          uint64_t h = hs[t];
+          for (uint64_t probe = 0; ek[t] != key[t] && probe < a.T.mask; ++probe) {
+            h = (h + 1) & a.T.mask;
+            const Entry* e = a.T.ent + h;
+            ek[t] = e->key;
+            wr[t] = *reinterpret_cast<const int2*>(e);
+          }
+          if (ek[t] != key[t]) wr[t] = make_int2(0, -1);  // unreachable: Get inserted it
+        }
       }
       float w[UNR];
       int vp[UNR];
@@ -116,7 +148,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           // the key's table entry: {w, vrow} in one 8-byte load (or handed over by the
           // Localizer's probe); V is visible only if present and not (l1_shrk && w == 0)
           // (SGDUpdater::Get, sgd_updater.cc:40-43)
-          if (a.wv_rank) {
+          if (PROBE) {
+            // found above
+          } else if (a.wv_rank) {
             wr[t] = a.wv_rank[c[t]];
           } else if (!a.wv) {
             wr[t] = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
@@ -199,7 +233,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       const float p = logit_p(a.label[r], predv, a.rw, r);
       if (l == 0) {
         a.p_out[r] = p;
-        if (MODE == kFused) {
+        if (MODE == kFused || PROBE) {
           a.pred[r] = pr;
           double yy = a.label[r] > 0 ? 1.0 : -1.0;
           loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
@@ -213,7 +247,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       }
     }
   }
-  if (MODE == kFused) {
+  if (MODE == kFused || PROBE) {
     for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
     if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
     __syncthreads();
@@ -264,7 +298,7 @@ static int launch_fwd_gc(const FwdArgs& a, int G, int CPL, bool vec, hipStream_t
     return DFX_OK;                                                                           \
   }
   DFX_SCALAR_SET(DFX_FWD)
-  if constexpr (PACKED || MODE == kFused) { DFX_VEC_SET(DFX_FWD) }
+  if constexpr (PACKED || MODE >= kFused) { DFX_VEC_SET(DFX_FWD) }
 #undef DFX_FWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -284,6 +318,7 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
   lanes_for(a.d, true, &G, &CPL, &vec);
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
+  if (a.index) return launch_fwd_gc<kFusedProbe, true>(a, G, CPL, vec, st);
   return launch_fwd_gc<kFused, true>(a, G, CPL, vec, st);
 }
 

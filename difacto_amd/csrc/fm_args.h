@@ -10,6 +10,10 @@ struct FwdArgs {
   const uint32_t* col;   // remapped column, or (fused) the nnz's model-table slot
   const int2* wv;        // the nnz's {w, vrow} (col unused)
   const int2* wv_rank;   // {w, vrow} per key rank, reached through col (the Pull's output)
+  // fused, probe mode: the nnz's raw feature id; the forward finds its key in the table
+  // (every key of the batch was inserted by the Get before), so the Localizer writes no col
+  const uint64_t* index;
+  uint64_t max_index;
   const float* val;
   // fused: the model table itself (SGDUpdater::Get semantics, l1_shrk from P);
   // standalone: interleaved weights addressed by positions

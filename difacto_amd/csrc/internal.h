@@ -153,6 +153,9 @@ struct Context {
   hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
   hipEvent_t ev_loc[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   int parity = 0;
+  // the fused forward finds every nnz's key in the table (no Localizer col scatter, no pulled
+  // {w, vrow} per key); 0: col + pulled (DFX_FWD_PROBE=0)
+  int fwd_probe = 1;
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }

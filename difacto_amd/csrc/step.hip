@@ -206,7 +206,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   o.value = b->value;
   o.occ_row = occ_row;
   o.occ_x = occ_x;
-  o.col = col;
+  o.col = c->fwd_probe ? nullptr : col;  // probe mode: the forward finds keys itself
   o.uniq = uniq;
   lane_mark(c, 0, c->loc_stream);
   DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
@@ -227,17 +227,23 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   const dim3 ug((unsigned)((nnz + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
   if (nnz > 0)
     hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, c->stream, uniq, bds, c->T,
-                       cnt_first ? nullptr : pulled, segslot, c->ds);
+                       cnt_first || c->fwd_probe ? nullptr : pulled, segslot, c->ds);
   prof_mark(c, 2);
   if (cnt_first) {
     DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total, bds));
-    hipLaunchKernelGGL(k_pull_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
-                       c->stream, segslot, bds, c->T.ent, pulled);
+    if (!c->fwd_probe)
+      hipLaunchKernelGGL(k_pull_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
+                         c->stream, segslot, bds, c->T.ent, pulled);
   }
   prof_mark(c, 3);
 
   FwdArgs a{};
-  a.B = B; a.offs = b->offset; a.col = col; a.wv_rank = pulled; a.val = b->value;
+  a.B = B; a.offs = b->offset; a.val = b->value;
+  if (c->fwd_probe) {
+    a.index = b->index; a.max_index = max_index;
+  } else {
+    a.col = col; a.wv_rank = pulled;
+  }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>();
