@@ -30,6 +30,7 @@ struct TransformArgs {
   uint64_t max_index;
   uint64_t* keys;
   uint64_t* pay;
+  uint32_t* pay32;  // narrow payload (row only): no col to scatter and no values to gather
   uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
   DevState* ds;     // the lane's state: OR / AND of the keys
 };
@@ -72,7 +73,10 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
       if (offs[mid] <= j) lo = mid; else hi = mid;
     }
     a.keys[j] = k;
-    a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32);
+    if (a.pay32)
+      a.pay32[j] = (uint32_t)(r0 + lo);
+    else
+      a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32);
   }
   for (int off = 32; off > 0; off >>= 1) {
     vor |= __shfl_xor(vor, off, kWave);
@@ -102,6 +106,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
 __global__ void k_loc_init(DevState* ds) {
   ds->or_mask = 0;
   ds->and_mask = ~0ull;
+  ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
 }
 
 // heads per tile
@@ -127,6 +132,8 @@ struct LocWriteArgs {
   const uint64_t* k1;
   const uint64_t* p0;
   const uint64_t* p1;
+  const uint32_t* q0;  // narrow payload (rows), when set
+  const uint32_t* q1;
   int64_t n;
   DevState* ds;
   const uint32_t* tilebase;
@@ -144,6 +151,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   const bool s1 = a.ds->sortmeta[31] != 0;
   const uint64_t* K = s1 ? a.k1 : a.k0;
   const uint64_t* P = s1 ? a.p1 : a.p0;
+  const uint32_t* Q = s1 ? a.q1 : a.q0;
   const int64_t n = a.n;
   const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint64_t k[kLocItems];
@@ -184,9 +192,13 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     for (int i = 0; i < kLocItems; ++i) {
       const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
       if (idx < n) {
-        const uint64_t p = P[idx];
-        a.occ_row[idx] = (uint32_t)(p >> 32);
-        if (a.occ_x) a.occ_x[idx] = a.value[(uint32_t)p];
+        if (Q) {
+          a.occ_row[idx] = Q[idx];
+        } else {
+          const uint64_t p = P[idx];
+          a.occ_row[idx] = (uint32_t)(p >> 32);
+          if (a.occ_x) a.occ_x[idx] = a.value[(uint32_t)p];
+        }
       }
     }
   }
@@ -201,7 +213,9 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
-__global__ void k_seg_chunks(int64_t bound, const DevState* ds, const uint32_t* segstart,
+// ds->n_init counts the long segments (reset by k_loc_init): when there are none (uniform
+// keys) the scan and the table exit at once on the device
+__global__ void k_seg_chunks(int64_t bound, DevState* ds, const uint32_t* segstart,
                              uint32_t* nch) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= bound) return;
@@ -211,11 +225,13 @@ __global__ void k_seg_chunks(int64_t bound, const DevState* ds, const uint32_t* 
     c = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
   }
   nch[u] = c;
+  if (c) atomicAdd(&ds->n_init, 1u);
 }
 
 // choff now holds the exclusive scan; a long segment lists its chunks
 __global__ void k_chunk_table(int64_t bound, const DevState* ds, const uint32_t* segstart,
                               const uint32_t* choff, uint32_t* chunk_seg) {
+  if (ds->n_init == 0u) return;
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= bound || u >= (int64_t)ds->u_count) return;
   const uint32_t len = segstart[u + 1] - segstart[u];
@@ -232,7 +248,7 @@ int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* c
   }
   const dim3 g((unsigned)((nnz + 255) / 256));
   hipLaunchKernelGGL(k_seg_chunks, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff);
-  DFX_TRY(scan_u32(L, choff, nnz, nchunks_dev, &L.ds->u_count));
+  DFX_TRY(scan_u32(L, choff, nnz, nchunks_dev, &L.ds->u_count, &L.ds->n_init));
   hipLaunchKernelGGL(k_chunk_table, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff,
                      chunk_seg);
   DFX_HIP(hipGetLastError());
@@ -266,22 +282,34 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   uint64_t* p1 = ws.vals1.as<uint64_t>();
   DFX_TRY(ws.os_reserve((nnz + 2047) / 2048));
   hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, L.stream, ds);
+  // nothing but the row travels with a key when there is no col to scatter and no value to
+  // gather (the fused step on binary data): a 4-byte payload, 12 instead of 16 bytes per item
+  // and sort pass
+  const bool narrow = !o.col && !o.value && o.occ_row;
+  uint32_t* q0 = narrow ? ws.vals0.as<uint32_t>() : nullptr;
+  uint32_t* q1 = narrow ? ws.vals1.as<uint32_t>() : nullptr;
   TransformArgs t{};
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
-  t.keys = k0; t.pay = p0; t.parts = ws.os_parts(); t.ds = ds;
+  t.keys = k0; t.pay = p0; t.pay32 = q0; t.parts = ws.os_parts(); t.ds = ds;
   hipLaunchKernelGGL(k_loc_transform, dim3((unsigned)((B + kLocRows - 1) / kLocRows)),
                      dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits
-  DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
-                                                ds->sortmeta, nullptr,
-                                                kSortDiffIsOrAnd | kSortCountsReady)));
+  if (narrow) {
+    DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, k0, q0, k1, q1, nnz, 0, 64, &ds->or_mask,
+                                                  ds->sortmeta, nullptr,
+                                                  kSortDiffIsOrAnd | kSortCountsReady)));
+  } else {
+    DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
+                                                  ds->sortmeta, nullptr,
+                                                  kSortDiffIsOrAnd | kSortCountsReady)));
+  }
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = ws.tiles.as<uint32_t>();
   hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, L.stream, k0, k1, nnz, ds, ts);
   scan_tiles_top(L, ts, ntiles, nullptr);
   LocWriteArgs a{};
-  a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1;
+  a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1; a.q0 = q0; a.q1 = q1;
   a.n = nnz; a.ds = ds; a.tilebase = ts;
   a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
