@@ -77,7 +77,8 @@ class DevBatch:
 
 def algorithmic_bytes(B, nnz, U, d):
     """Essential HBM bytes per launch, binary data, all V live."""
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (4 + 8 + 4 * d)
+    # forward (probe mode): per nnz its id and its key's {w, vrow} entry bytes, then V
+    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + 4 * d)
     bwd = U * (8 + 4 + 8 + 32 + 16 * d + 4) + nnz * (4 + 4 + 4 + 4 * d)
     return {"forward": fwd, "backward_update": bwd}
 
@@ -88,7 +89,8 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     p / XVp, per nnz col + the record's {w, live} + V; backward per key segstart + {w, live} +
     V + the whole gradient record written, per occurrence occ_row / p / XVp."""
     S = d + 4
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (4 + 8 + 4 * d)
+    # forward (probe mode): per nnz its id and its key's {w, vrow} entry bytes, then V
+    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + 4 * d)
     bwd = U * (4 + 8 + 4 * d + 4 * S) + nnz * (4 + 4 + 4 * d)
     return fwd + bwd
 
