@@ -357,6 +357,33 @@ def test_fused_criteo_like_vs_oracle(H):
     assert s["seed"] == up.seed and s["n_keys"] == up.size()
 
 
+@pytest.mark.parametrize("max_index", [1000, 65537, (1 << 64) - 1])
+def test_fused_max_index_vs_oracle(H, max_index):
+    """Localizer keys = ReverseBytes(id % max_index) (localizer.cc:20-24): the fused step's
+    forward recomputes them per nnz (probe mode), so a modding max_index (ids colliding into
+    one key, repeated keys inside rows) and the ~0 corner id must match the oracle"""
+    import numpy as np
+    cfg = dict(V_dim=8, V_threshold=1, l1=0.01, lr=.1, V_lr=.02)
+    c = H.Context(0, max_keys=1 << 18, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(2000, 12, 1 << 40, binary=(step % 2 == 0), seed=90 + step)
+        ids = blk.ids.copy()
+        ids[::97] = np.uint64((1 << 64) - 1)  # the all-ones id
+        blk = D.RowBlock(blk.offs, ids, blk.vals, blk.labels)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         max_index=max_index, push_cnt=(step < 2),
+                                         want_pred=True)
+        db = H.DeviceRowBlock(c, blk)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, db, H.kTraining, push_cnt=(step < 2), max_index=max_index, pred=pred)
+        p = H.progress(c)
+        assert close(pred.cpu().numpy(), opred, rtol=1e-4), (max_index, step)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss)
+    s = H.Store(c).stats()
+    assert s["seed"] == up.seed and s["n_keys"] == up.size()
+
+
 def test_fused_validation_does_not_update(H, rcv1):
     c = H.Context(0, V_dim=4, V_threshold=0, l1=0, lr=.1, max_keys=1 << 14)
     db = H.DeviceRowBlock(c, rcv1)
