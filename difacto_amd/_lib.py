@@ -69,6 +69,7 @@ _SIGS = {
     "dfx_store_push": (ctypes.c_int, [vp, vp, c_i64, ctypes.c_int, vp, c_i64, vp]),
     "dfx_store_save": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int]),
     "dfx_store_load": (ctypes.c_int, [vp, ctypes.c_char_p]),
+    "dfx_store_load_part": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "dfx_store_dump": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     "dfx_store_stats": (ctypes.c_int, [vp, i64p, i64p, f64p, ctypes.POINTER(ctypes.c_uint32)]),
     "dfx_store_evaluate": (ctypes.c_int, [vp, f64p, i64p]),

@@ -609,7 +609,14 @@ int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux) {
 
 // SGDUpdater::Load (sgd_updater.h:84-96, SGDEntry::LoadEntry :50-68)
 int dfx_store_load(dfx_ctx* ctx, const char* path) {
+  return dfx_store_load_part(ctx, path, 0, 1);
+}
+
+// the keys of `path` that rank `rank` of `nranks` owns under the sharded store's rule
+// owner(k) = floor(k * nranks / 2^64) (dist.hip): a model saved by N servers loads into M
+int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks) {
   DFX_CHECK_ARG(ctx && path, "null argument");
+  DFX_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "store_load_part: bad rank");
   Context* c = &ctx->c;
   Table& T = c->T;
   FILE* f = fopen(path, "rb");
@@ -645,6 +652,13 @@ int dfx_store_load(dfx_ctx* ctx, const char* path) {
         fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
       }
       row = (int32_t)vnext++;
+    }
+    if ((int)(((unsigned __int128)key * (unsigned)nranks) >> 64) != rank) {
+      if (row >= 0) {  // not ours: drop its V row again
+        VV.resize(VV.size() - 2 * T.d);
+        --vnext;
+      }
+      continue;
     }
     keys.push_back(key);
     st.push_back(e);

@@ -126,10 +126,15 @@ class Shard:
         check(_lib.lib().dfx_store_save(self.ctx.h, model_name(prefix, rank, it).encode(),
                                         int(save_aux)))
 
-    def load(self, prefix, rank, it=-1):
-        """this server's part; the key ranges are those of the run that saved it (the same
-        number of ranks)"""
-        check(_lib.lib().dfx_store_load(self.ctx.h, model_name(prefix, rank, it).encode()))
+    def load(self, prefix, rank, it=-1, saved_ranks=None):
+        """this server's part.  saved_ranks (the number of servers that saved the model, when
+        it differs from this run's): read every part and keep the keys this rank owns"""
+        if saved_ranks is None or saved_ranks == self.nranks:
+            check(_lib.lib().dfx_store_load(self.ctx.h, model_name(prefix, rank, it).encode()))
+            return
+        for r in range(int(saved_ranks)):
+            check(_lib.lib().dfx_store_load_part(self.ctx.h, model_name(prefix, r, it).encode(),
+                                                 int(rank), self.nranks))
 
 
 class _Done:

@@ -14,7 +14,8 @@
 // num_jobs_per_epoch x shards parts; shard r reads parts r, r + shards, ... in order, the shards
 // step together (an exhausted shard submits empty batches until all are done), and
 // `pipelined=1` (default) selects the 1-step-stale schedule.  Each server saves
-// <model_out>_part-<rank>.
+// <model_out>_part-<rank>; `model_in_parts=K` loads a model K servers saved into this run's
+// shards (each keeps the keys it owns).
 //
 // Model files are named like SGDLearner::ModelName (sgd_learner.h:65-69):
 // <prefix>[_iter-<epoch>]_part-0, in SGDUpdater::Save's format; task=2 predicts data_val with
@@ -48,6 +49,7 @@ struct Param {
   int max_num_epochs = 20, num_jobs_per_epoch = 10, nthreads = 8;
   int load_epoch = -1, task = 0;
   int shards = 0;  // > 0: that many loopback shards in this process; -1: one shard, RCCL
+  int model_in_parts = 0;  // servers that saved model_in, when not this run's shard count
   bool pipelined = true;
   bool has_aux = false, pred_prob = true;
   double stop_rel_objv = 1e-5;
@@ -180,12 +182,20 @@ int RunSharded(const Param& P, const KWArgs& rest) {
   } else {
     ex = MakeLoopbackExchange(ctxs);
   }
-  if (!P.model_in.empty())
-    for (int l = 0; l < nlocal; ++l)
-      DfxCheck(dfx_store_load(ctxs[l],
-                              ModelNamePart(P.model_in, P.load_epoch > 0 ? P.load_epoch : -1,
-                                            ex->rank(l)).c_str()),
-               "dfx_store_load");
+  if (!P.model_in.empty()) {
+    const int it = P.load_epoch > 0 ? P.load_epoch : -1;
+    for (int l = 0; l < nlocal; ++l) {
+      if (P.model_in_parts <= 0 || P.model_in_parts == nshards) {
+        DfxCheck(dfx_store_load(ctxs[l], ModelNamePart(P.model_in, it, ex->rank(l)).c_str()),
+                 "dfx_store_load");
+      } else {  // saved by a different number of servers: keep the keys this shard owns
+        for (int r = 0; r < P.model_in_parts; ++r)
+          DfxCheck(dfx_store_load_part(ctxs[l], ModelNamePart(P.model_in, it, r).c_str(),
+                                       ex->rank(l), nshards),
+                   "dfx_store_load_part");
+      }
+    }
+  }
   {
     GpuShardedStore store(ex.get(), P.pipelined);
     std::vector<std::vector<DevBatch>> dev(nlocal);
@@ -290,6 +300,7 @@ int main(int argc, char** argv) {
     else if (k == "has_aux") P.has_aux = std::stoi(v) != 0;
     else if (k == "shards") P.shards = std::stoi(v);
     else if (k == "pipelined") P.pipelined = std::stoi(v) != 0;
+    else if (k == "model_in_parts") P.model_in_parts = std::stoi(v);
     else {
       fused_given = fused_given || k == "fused";
       rest.push_back({k, v});

@@ -167,6 +167,10 @@ int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, cons
                    int64_t n_vals, const int32_t* lens);
 int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux);
 int dfx_store_load(dfx_ctx* ctx, const char* path);
+/* only the keys rank `rank` of `nranks` owns in the sharded store (floor(key·nranks/2^64)):
+ * a model saved by N servers (<prefix>_part-<r>, r < N) loads into M servers by every server
+ * loading every part */
+int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks);
 int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_reverse);
 int dfx_store_stats(dfx_ctx* ctx, int64_t* n_keys, int64_t* n_vrows, double* new_w,
                     uint32_t* seed);

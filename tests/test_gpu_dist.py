@@ -211,6 +211,52 @@ def test_sharded_save_load_parts(tmp_path):
         c.close()
 
 
+@pytest.mark.parametrize("m", [1, 2, 5])
+def test_sharded_load_into_other_rank_count(tmp_path, m):
+    """a model saved by 3 servers loads into m servers: every server reads every part and keeps
+    the keys it owns (dfx_store_load_part); each key lands on its new owner with the state
+    the old one saved"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS["fm_v4"]
+    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    batches = _batches(N, 3)
+    for s, step in enumerate(batches):
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=s < 2)
+    prefix = tmp_path / "model"
+    for r in range(N):
+        shards[r].save(prefix, r, save_aux=True)
+    new = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(m)]
+    for g in range(m):
+        DI.Shard(new[g], m).load(prefix, g, saved_ranks=N)
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
+                                     for step in batches for b in step]))
+    total = 0
+    for k in keys:
+        old = H.Store(ctxs[DO.owner_of(np.array([k]), N)[0]]).entry(k)
+        g = DO.owner_of(np.array([k]), m)[0]
+        got = H.Store(new[g]).entry(k)
+        for h in range(m):
+            if h != g:
+                assert H.Store(new[h]).entry(k) is None
+        if old is None or (old[0][0] == 0 and old[1] is None):
+            continue  # Save skips empty entries
+        total += 1
+        assert got is not None, k
+        assert np.array_equal(got[0][:3], old[0][:3])
+        assert (got[1] is None) == (old[1] is None)
+        if got[1] is not None:
+            assert np.array_equal(got[1], old[1])
+    assert total > 0
+    assert sum(H.Store(c).stats()["n_keys"] for c in new) == total
+    for c in ctxs + new:
+        c.sync()
+        c.close()
+
+
 def test_sharded_validation_does_not_update():
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
