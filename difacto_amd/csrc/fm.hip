@@ -133,13 +133,16 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
           uint64_t h = hs[t];
-          for (uint64_t probe = 0; ek[t] != key[t] && probe < a.T.mask; ++probe) {
+          for (uint64_t probe = 0; ek[t] != key[t] && ek[t] != kEmptyKey && probe < a.T.mask;
+               ++probe) {
             h = (h + 1) & a.T.mask;
             const Entry* e = a.T.ent + h;
             ek[t] = e->key;
             wr[t] = *reinterpret_cast<const int2*>(e);
           }
-          if (ek[t] != key[t]) wr[t] = make_int2(0, -1);  // unreachable: Get inserted it
+          // absent (a training step inserts its new keys in the backward): the empty entry
+          // model_[key] default-constructs, w = 0 and no V (sgd_updater.h:20-34)
+          if (ek[t] != key[t]) wr[t] = make_int2(0, -1);
         }
       }
       float w[UNR];
@@ -346,7 +349,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   const int64_t nseg = a.nseg_host >= 0 ? a.nseg_host : (int64_t)a.ds->u_count;
   __shared__ int red[kFmNT / kWave];
   __shared__ int redn[kFmNT / kWave];
-  int dnew = 0, ninit = 0;
+  __shared__ int redi[kFmNT / kWave];
+  int dnew = 0, ninit = 0, nins = 0;
   if (u < nseg) {
     const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
@@ -360,7 +364,28 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
     float fc = 0.f;
     if (FUSED) {
-      sl = a.slot[cidx];
+      if (a.insert_keys) {
+        // Get's find-or-insert (model_[key]) here instead of a separate pass: the home slot
+        // first (every lane), a longer chain or an insert by the group's first lane
+        const uint64_t key = a.uniq[cidx];
+        const uint64_t hh = tbl_hash(key, a.T);
+        int s = (int)hh;
+        if (a.T.ent[hh].key != key) {
+          int s0 = 0;
+          if (l == 0) {
+            bool inserted;
+            const int64_t r = tbl_insert(a.T, key, &inserted);
+            if (r < 0) atomicOr(&a.dsw->err, kErrTableFull);
+            s0 = r < 0 ? 0 : (int)r;
+            nins = inserted ? 1 : 0;
+          }
+          s = __shfl(s0, (int)(threadIdx.x % kWave) - l, kWave);
+        }
+        sl = (uint32_t)s;
+        if (l == 0) a.slot[cidx] = sl;  // InitV's slot
+      } else {
+        sl = a.slot[cidx];
+      }
       const Entry* en = a.T.ent + sl;
       h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
       fc = en->fea_cnt;
@@ -560,20 +585,24 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     for (int off = 32; off > 0; off >>= 1) {
       dnew += __shfl_xor(dnew, off, kWave);
       ninit += __shfl_xor(ninit, off, kWave);
+      nins += __shfl_xor(nins, off, kWave);
     }
     if (lane_id() == 0) {
       red[threadIdx.x / kWave] = dnew;
       redn[threadIdx.x / kWave] = ninit;
+      redi[threadIdx.x / kWave] = nins;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      int s = 0, q = 0;
+      int s = 0, q = 0, i2 = 0;
       for (int i = 0; i < kFmNT / kWave; ++i) {
         s += red[i];
         q += redn[i];
+        i2 += redi[i];
       }
       if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
       if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
+      if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
     }
   }
 }

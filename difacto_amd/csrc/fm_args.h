@@ -58,7 +58,11 @@ struct BwdArgs {
   // written whole (no pre-zeroing)
   int rec_S;
   // fused update
-  const uint32_t* slot;      // model-table slot of each segment's key
+  uint32_t* slot;            // model-table slot of each segment's key (written when inserting)
+  // training step without a separate Get pass: the backward finds-or-inserts each key itself
+  // (the forward read absent keys as the empty entry); uniq: the sorted unique keys
+  const uint64_t* uniq;
+  int insert_keys;
   Table T;
   Params Pm;
   uint32_t* flags;  // InitV request per key

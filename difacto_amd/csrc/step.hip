@@ -224,8 +224,12 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   prof_mark(c, 1);
   // Get over the sorted unique keys (find-or-insert + pull); a count push goes in between
   const bool cnt_first = push_cnt && d > 0;
+  // a training step whose forward finds keys itself needs no Get pass: absent keys read as
+  // the empty entry and the backward inserts them (its find-or-insert is Get's)
+  const bool bwd_inserts = c->fwd_probe && !cnt_first && job_type == DFX_JOB_TRAINING &&
+                           B > 0 && nnz > 0;
   const dim3 ug((unsigned)((nnz + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
-  if (nnz > 0)
+  if (nnz > 0 && !bwd_inserts)
     hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, c->stream, uniq, bds, c->T,
                        cnt_first || c->fwd_probe ? nullptr : pulled, segslot, c->ds);
   prof_mark(c, 2);
@@ -271,6 +275,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.d = d; g.slot = segslot; g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
+    g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<float>();
     DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
