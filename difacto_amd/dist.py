@@ -217,7 +217,7 @@ class TorchComm:
             return _Done([self._a2a(x, ss, rs, row, self.kgroup, False)[0]])
         with torch.cuda.stream(self.kstream):
             out, work = self._a2a(x, ss, rs, row, self.kgroup, True)
-        return _Work(work, [out])
+        return _Work(work, [out], foreign=True)
 
     def allreduce_sum(self, values):
         (v,) = values
@@ -227,11 +227,17 @@ class TorchComm:
 
 
 class _Work:
-    def __init__(self, work, out):
-        self.work, self.out = work, out
+    def __init__(self, work, out, foreign=False):
+        self.work, self.out, self.foreign = work, out, foreign
 
     def wait(self):
         self.work.wait()  # the current stream waits for the exchange
+        if self.foreign:
+            # allocated on the exchange's own stream, read on this one: keep the caching
+            # allocator from handing the memory out again before this stream is past its use
+            s = torch.cuda.current_stream()
+            for o in self.out:
+                o.record_stream(s)
         return self.out
 
 
