@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--sync", action="store_true",
                     help="sharded store: bulk-synchronous steps instead of the pipelined "
                          "(1-step-stale) schedule")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="sharded store transport; gloo (staged through host memory) runs "
+                         "several ranks on one GPU, for tests")
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-batch", type=int, default=10_000)
     return ap.parse_args()
@@ -142,6 +145,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())  # ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     sharded = world > 1 or args.sharded
@@ -150,7 +155,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29511")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from difacto_amd import hotpath as H
     import ctypes
@@ -285,7 +293,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01, max_keys=per,
                     max_vrows=per)
     shard = DI.Shard(ctx, world)
-    comm = DI.TorchComm(device=dev)
+    comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo")
 
     pipe = None if args.sync else DI.ShardedPipeline([shard], comm)
     live = []  # a batch stays alive until the submit after the one that took it

@@ -380,3 +380,33 @@ def test_sharded_two_processes_one_gpu(pipelined):
         assert st["seed"] == so.up[r].seed
         assert st["n_keys"] == so.up[r].size()
         assert st["new_w"] == so.up[r].new_w
+
+
+@pytest.mark.parametrize("sync", [False, True])
+def test_bench_two_ranks_gloo(sync):
+    """bench.py's multi-GPU path end to end under torchrun with 2 ranks (the driver's SCALE
+    command, with the exchange staged through host memory over gloo since both ranks share
+    the test box's GPU): one JSON line from rank 0, whole-job throughput over both ranks"""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--steps", "3", "--warmup", "1", "--batch", "20000", "--key-bits", "20",
+           "--backend", "gloo", "--no-cpu-baseline"] + (["--sync"] if sync else [])
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0
+    assert out["config"]["global_batch"] == 40000
+    assert 0.3 < out["train_loss_per_row"] < 0.8 and 0.3 < out["train_auc"] < 0.7
+    assert ("bulk-synchronous" in out["config"]["workload"]) == sync
