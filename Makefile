@@ -22,8 +22,13 @@ HOSTFLAGS = -std=c++14 -O2 -Wall -pthread
 READERBIN = build/reader_tests
 GENBIN = build/gen_criteo
 CONVBIN = build/dfx_convert
+RBENCH = build/reader_bench
 
-all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN)
+all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH)
+
+$(RBENCH): difacto_amd/host/reader.cc tools/reader_bench.cc difacto_amd/host/reader.h
+	@mkdir -p build
+	g++ $(HOSTFLAGS) -o $@ difacto_amd/host/reader.cc tools/reader_bench.cc
 
 # the data converter (src/reader/converter.h): text formats -> rec (CompressedRowBlock RecordIO)
 $(CONVBIN): difacto_amd/host/reader.cc difacto_amd/host/convert_main.cc difacto_amd/host/reader.h \

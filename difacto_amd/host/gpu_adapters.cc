@@ -11,6 +11,7 @@
 #include <fstream>
 #include <set>
 #include <sstream>
+#include <thread>
 
 namespace difacto {
 
@@ -341,6 +342,25 @@ void GetPos(const SArray<int>& len, SArray<int>* w_pos, SArray<int>* V_pos) {
   }
 }
 
+// large host copies into pinned staging, split over a few threads (one thread's memcpy bandwidth
+// would bound the host-side batch rate)
+static void ParallelCopy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kSplit = 4 << 20;
+  const int T = (int)std::min<size_t>(8, bytes / kSplit);
+  if (T < 2) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    const size_t a = bytes * t / T, b = bytes * (t + 1) / T;
+    th.emplace_back([=]() {
+      std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
 GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs) {
   KWArgs mine;
   KWArgs rest = Consume(kwargs, {"fused", "loss"}, &mine);
@@ -387,8 +407,8 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
     DfxCheck(dfx_feeder_slot(feeder_, &hb), "dfx_feeder_slot");
     static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t offsets");
     std::memcpy(hb.offset, batch.offset, (B + 1) * 8);
-    std::memcpy(hb.index, batch.index, nnz * 8);
-    if (batch.value) std::memcpy(hb.value, batch.value, nnz * 4);
+    ParallelCopy(hb.index, batch.index, nnz * 8);
+    if (batch.value) ParallelCopy(hb.value, batch.value, nnz * 4);
     std::memcpy(hb.label, batch.label, B * 4);
     if (batch.weight) std::memcpy(hb.weight, batch.weight, B * 4);
     dfx_batch b;

@@ -1,6 +1,11 @@
 // reader.cc — see reader.h.
 #include "reader.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -306,7 +311,11 @@ int Lz4Decompress(const char* src, int n, char* dst, int dst_cap) {
     const uint8_t token = *ip++;
     int lit = token >> 4;
     if (!ext(&lit) || lit > iend - ip || lit > oend - op) return -1;
-    std::memcpy(op, ip, lit);
+    if (lit <= 16 && iend - ip >= 16 && oend - op >= 16) {
+      std::memcpy(op, ip, 16);  // short literal runs: one fixed-size copy (room checked)
+    } else {
+      std::memcpy(op, ip, lit);
+    }
     op += lit;
     ip += lit;
     if (ip == iend) break;  // the last sequence has no match
@@ -318,7 +327,14 @@ int Lz4Decompress(const char* src, int n, char* dst, int dst_cap) {
     ml += kLz4MinMatch;
     if (off == 0 || off > op - obase || ml > oend - op) return -1;
     const uint8_t* m = op - off;
-    for (int i = 0; i < ml; ++i) op[i] = m[i];  // overlapping copies repeat the pattern
+    int i = 0;
+    if (off >= 16 && ml <= 16 && oend - op >= 16) {
+      std::memcpy(op, m, 16);  // non-overlapping short match, one fixed-size copy
+      i = ml;
+    } else if (off >= 8) {  // 8-byte steps never read bytes this match has yet to write
+      for (; i + 8 <= ml; i += 8) std::memcpy(op + i, m + i, 8);
+    }
+    for (; i < ml; ++i) op[i] = m[i];  // overlapping copies repeat the pattern
     op += ml;
   }
   return (int)(op - obase);
@@ -376,52 +392,72 @@ bool DecompressRowBlock(const char* data, size_t size, RowBlockContainer<feaid_t
   if (!get(&magic) || magic != kCrbMagic || !get(&isz) || (isz != 8 && isz != 4) ||
       !get(&nrows) || nrows < 0)
     return false;
-  // one section -> bytes (empty when absent)
-  auto section = [&](std::vector<char>* dst, size_t bytes, bool* present) {
+  // one section, decompressed straight to dst (bytes long); false on a malformed section
+  auto section = [&](void* dst, size_t bytes, bool* present) {
     int cp;
     if (!get(&cp)) return false;
     *present = cp > 0;
     if (cp <= 0) return true;
     if (cur + (size_t)cp > size) return false;
-    dst->resize(bytes);
-    const int got = Lz4Decompress(data + cur, cp, dst->data(), (int)bytes);
+    const int got = Lz4Decompress(data + cur, cp, static_cast<char*>(dst), (int)bytes);
     cur += cp;
     return got == (int)bytes;
   };
-  std::vector<char> lab, off, idx, val, wt;
-  bool has_lab, has_off, has_idx, has_val, has_wt;
-  if (!section(&lab, nrows * 4ull, &has_lab) || !section(&off, (nrows + 1) * 8ull, &has_off) ||
-      !has_off)
+  const size_t rows0 = out->label.size(), base = out->index.size();
+  const bool had_val = !out->value.empty(), had_wt = !out->weight.empty();
+  bool has_lab = false, has_off = false, has_idx = false, has_val = false, has_wt = false;
+  out->label.resize(rows0 + nrows, 0.f);
+  std::vector<size_t> off(nrows + 1);
+  if (!section(out->label.data() + rows0, nrows * 4ull, &has_lab) ||
+      !section(off.data(), (nrows + 1) * 8ull, &has_off) || !has_off || off[nrows] < off[0]) {
+    out->label.resize(rows0);
     return false;
-  const size_t* o = reinterpret_cast<const size_t*>(off.data());
-  if (o[nrows] < o[0]) return false;
-  const size_t nnz = o[nrows] - o[0];
-  if (!section(&idx, nnz * isz, &has_idx) || !section(&val, nnz * 4, &has_val) ||
-      !section(&wt, nrows * 4ull, &has_wt))
+  }
+  if (!has_lab) std::fill(out->label.begin() + rows0, out->label.end(), 0.f);
+  const size_t nnz = off[nrows] - off[0];
+  bool ok;
+  if (isz == 8) {
+    out->index.resize(base + nnz);
+    ok = section(out->index.data() + base, nnz * 8, &has_idx);
+  } else {
+    std::vector<uint32_t> idx32(nnz);
+    ok = section(idx32.data(), nnz * 4, &has_idx);
+    out->index.resize(base + nnz);
+    for (size_t j = 0; j < nnz; ++j) out->index[base + j] = idx32[j];
+  }
+  // values: this record's, or ones when the block so far carries values
+  const size_t vbase = out->value.size();
+  out->value.resize(vbase + nnz);
+  ok = ok && section(out->value.data() + vbase, nnz * 4, &has_val);
+  const size_t wbase = out->weight.size();
+  out->weight.resize(wbase + nrows);
+  ok = ok && section(out->weight.data() + wbase, nrows * 4ull, &has_wt);
+  if (!ok || (nnz && !has_idx)) {
+    out->label.resize(rows0);
+    out->index.resize(base);
+    out->value.resize(vbase);
+    out->weight.resize(wbase);
     return false;
-  if (nnz && !has_idx) return false;
-  // append, keeping out's value / weight arrays aligned with its rows
-  const size_t base = out->index.size(), rows0 = out->label.size();
-  if (has_val && out->value.size() < base) out->value.resize(base, 1.f);
-  if (has_wt && out->weight.size() < rows0) out->weight.resize(rows0, 1.f);
-  for (int i = 0; i < nrows; ++i) {
-    out->label.push_back(has_lab ? reinterpret_cast<const float*>(lab.data())[i] : 0.f);
-    out->offset.push_back(base + o[i + 1] - o[0]);
   }
-  for (size_t j = 0; j < nnz; ++j)
-    out->index.push_back(isz == 8 ? reinterpret_cast<const uint64_t*>(idx.data())[j]
-                                  : reinterpret_cast<const uint32_t*>(idx.data())[j]);
-  if (has_val) {
-    const float* v = reinterpret_cast<const float*>(val.data());
-    out->value.insert(out->value.end(), v, v + nnz);
-  } else if (!out->value.empty()) {
-    out->value.resize(out->index.size(), 1.f);
+  for (int i = 0; i < nrows; ++i) out->offset.push_back(base + off[i + 1] - off[0]);
+  // keep value / weight arrays aligned with the block's rows: absent sections mean all ones
+  if (!has_val) {
+    if (!had_val) {
+      out->value.resize(vbase);
+    } else {
+      std::fill(out->value.begin() + vbase, out->value.end(), 1.f);
+    }
+  } else if (vbase < base) {  // earlier records were binary
+    out->value.insert(out->value.begin() + vbase, base - vbase, 1.f);
   }
-  if (has_wt) {
-    const float* w = reinterpret_cast<const float*>(wt.data());
-    out->weight.insert(out->weight.end(), w, w + nrows);
-  } else if (!out->weight.empty()) {
-    out->weight.resize(out->label.size(), 1.f);
+  if (!has_wt) {
+    if (!had_wt) {
+      out->weight.resize(wbase);
+    } else {
+      std::fill(out->weight.begin() + wbase, out->weight.end(), 1.f);
+    }
+  } else if (wbase < rows0) {
+    out->weight.insert(out->weight.begin() + wbase, rows0 - wbase, 1.f);
   }
   return cur == size;
 }
@@ -535,6 +571,45 @@ static void ClearRows(RowBlockContainer<feaid_t>* c) {  // keeps the capacity
   c->value.clear();
 }
 
+// the parser threads' parts, in order, into one block: every part copies into its own
+// range concurrently (the copy is as large as the parse output)
+static void ConcatParts(std::vector<RowBlockContainer<feaid_t>>* parts,
+                        RowBlockContainer<feaid_t>* out) {
+  const size_t T = parts->size();
+  bool valued = false, weighted = false;
+  for (auto& pt : *parts) {
+    valued = valued || !pt.value.empty();
+    weighted = weighted || !pt.weight.empty();
+  }
+  std::vector<size_t> r0(T + 1, out->Size()), n0(T + 1, out->index.size());
+  for (size_t t = 0; t < T; ++t) {
+    r0[t + 1] = r0[t] + (*parts)[t].Size();
+    n0[t + 1] = n0[t] + (*parts)[t].index.size();
+  }
+  out->offset.resize(r0[T] + 1);
+  out->label.resize(r0[T]);
+  out->index.resize(n0[T]);
+  if (valued) out->value.resize(n0[T], 1.f);
+  if (weighted) out->weight.resize(r0[T], 1.f);
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < T; ++t) {
+    th.emplace_back([&, t]() {
+      const auto& pt = (*parts)[t];
+      const size_t n = pt.Size(), m = pt.index.size();
+      for (size_t i = 0; i < n; ++i) out->offset[r0[t] + i + 1] = n0[t] + pt.offset[i + 1];
+      if (n) std::memcpy(&out->label[r0[t]], pt.label.data(), n * sizeof(float));
+      if (m) std::memcpy(&out->index[n0[t]], pt.index.data(), m * sizeof(feaid_t));
+      if (!pt.value.empty())
+        std::memcpy(&out->value[n0[t]], pt.value.data(), m * sizeof(float));
+      else if (valued)
+        std::fill(out->value.begin() + n0[t], out->value.begin() + n0[t] + m, 1.f);
+      if (!pt.weight.empty())
+        std::memcpy(&out->weight[r0[t]], pt.weight.data(), n * sizeof(float));
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
 // ---- TextReader -------------------------------------------------------------------------
 TextReader::TextReader(const std::string& path, const std::string& format, int part,
                        int nparts, size_t chunk_bytes, int nthreads)
@@ -546,24 +621,33 @@ TextReader::TextReader(const std::string& path, const std::string& format, int p
     rec_.reset(new RecordIOReader(path, part, nparts));
     return;
   }
-  std::ifstream f(path, std::ios::binary | std::ios::ate);
-  DFX_HOST_CHECK(f.good(), "cannot open " + path);
-  const size_t size = (size_t)f.tellg();
+  // the file is mapped, not read: the parser threads read the page cache directly
+  fd_ = open(path.c_str(), O_RDONLY);
+  DFX_HOST_CHECK(fd_ >= 0, "cannot open " + path);
+  struct stat sb;
+  DFX_HOST_CHECK(fstat(fd_, &sb) == 0, "cannot stat " + path);
+  const size_t size = (size_t)sb.st_size;
+  if (size > 0) {
+    void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd_, 0);
+    DFX_HOST_CHECK(m != MAP_FAILED, "cannot map " + path);
+    map_ = static_cast<const char*>(m);
+    map_size_ = size;
+    (void)madvise(m, size, MADV_SEQUENTIAL);
+  }
   // part k of n: byte range [size*k/n, size*(k+1)/n), both ends moved to the next line start
   auto line_start = [&](size_t at) {
     if (at == 0 || at >= size) return at >= size ? size : (size_t)0;
-    f.seekg((std::streamoff)(at - 1));
-    char ch;
-    size_t q = at - 1;
-    while (f.get(ch)) {
-      ++q;
-      if (ch == '\n') return q;
-    }
-    return size;
+    const void* nl = std::memchr(map_ + at - 1, '\n', size - (at - 1));
+    return nl ? (size_t)(static_cast<const char*>(nl) - map_) + 1 : size;
   };
   begin_ = line_start(size * part / nparts);
   end_ = line_start(size * (part + 1) / nparts);
   pos_ = begin_;
+}
+
+TextReader::~TextReader() {
+  if (map_) munmap(const_cast<char*>(map_), map_size_);
+  if (fd_ >= 0) close(fd_);
 }
 
 // format "rec": records of about chunk_ bytes, decompressed by the worker threads
@@ -594,13 +678,7 @@ bool TextReader::NextRec() {
   }
   for (auto& x : th) x.join();
   for (int t = 0; t < T; ++t) DFX_HOST_CHECK(ok[t], "malformed CompressedRowBlock record");
-  bool valued = false;
-  for (int t = 0; t < T; ++t) valued = valued || !parts_[t].value.empty();
-  for (int t = 0; t < T; ++t) {
-    auto& pt = parts_[t];
-    if (valued && pt.value.empty()) pt.value.assign(pt.index.size(), 1.f);
-    AppendRows(pt, 0, pt.Size(), &blk_);
-  }
+  ConcatParts(&parts_, &blk_);
   return true;
 }
 
@@ -608,30 +686,36 @@ bool TextReader::Next() {
   ClearRows(&blk_);
   if (rec_) return NextRec();
   if (pos_ >= end_) return false;
-  std::ifstream f(path_, std::ios::binary);
-  size_t want = std::min(chunk_, end_ - pos_), got = 0, cut = 0;
-  for (;;) {
-    buf_.resize(want);
-    f.seekg((std::streamoff)pos_);
-    f.read(buf_.data(), (std::streamsize)want);
-    got = (size_t)f.gcount();
-    f.clear();
-    // whole lines only: the chunk ends after its last newline unless the part ends there
-    cut = got;
-    if (pos_ + got < end_) {
-      while (cut > 0 && buf_[cut - 1] != '\n') --cut;
+  // whole lines only: the chunk ends after its last newline (or, for a line longer than the
+  // chunk, after that line) unless the part ends first
+  const char* buf = map_ + pos_;
+  size_t cut = std::min(chunk_, end_ - pos_);
+  if (pos_ + cut < end_) {
+    size_t c = cut;
+    while (c > 0 && buf[c - 1] != '\n') --c;
+    if (c == 0) {
+      const void* nl = std::memchr(buf + cut, '\n', end_ - pos_ - cut);
+      c = nl ? (size_t)(static_cast<const char*>(nl) - buf) + 1 : end_ - pos_;
     }
-    if (cut > 0 || pos_ + got >= end_ || got < want) break;
-    want = std::min(want * 2, end_ - pos_);  // a line longer than the chunk: read more
+    cut = c;
   }
-  if (cut == 0) cut = got;
+  if (pos_ + cut == map_size_ && cut > 0 && buf[cut - 1] != '\n') {
+    // the file's last line has no newline: parse a terminated copy (the number parsers read
+    // until a non-digit, which past the mapping's end could fault)
+    tail_.assign(buf, cut);
+    tail_.push_back('\n');
+    buf = tail_.data();
+    ++cut;
+    --read_;
+    --pos_;
+  }
   pos_ += cut;
   read_ += cut;
   // split at line boundaries over the worker threads, parse, concatenate in order
   std::vector<size_t> cuts{0};
   for (int t = 1; t < nthreads_; ++t) {
     size_t c = cut * t / nthreads_;
-    while (c < cut && buf_[c] != '\n') ++c;
+    while (c < cut && buf[c] != '\n') ++c;
     cuts.push_back(std::min(c < cut ? c + 1 : cut, cut));
   }
   cuts.push_back(cut);
@@ -646,8 +730,8 @@ bool TextReader::Next() {
       RowBlockContainer<feaid_t> local;
       std::swap(local, parts_[t]);
       ClearRows(&local);
-      const char* a = buf_.data() + cuts[t];
-      const char* b = buf_.data() + std::max(cuts[t], cuts[t + 1]);
+      const char* a = buf + cuts[t];
+      const char* b = buf + std::max(cuts[t], cuts[t + 1]);
       if (format_ == "libsvm") {
         ParseLibSVM(a, b, &local);
       } else if (format_ == "adfea") {
@@ -659,12 +743,7 @@ bool TextReader::Next() {
     });
   }
   for (auto& x : th) x.join();
-  bool valued = false;
-  for (auto& pt : parts_) valued = valued || !pt.value.empty();
-  for (auto& pt : parts_) {
-    if (valued && pt.value.empty()) pt.value.assign(pt.index.size(), 1.f);
-    AppendRows(pt, 0, pt.Size(), &blk_);
-  }
+  ConcatParts(&parts_, &blk_);
   return blk_.Size() > 0 || pos_ < end_;
 }
 

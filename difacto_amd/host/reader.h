@@ -100,6 +100,9 @@ class TextReader {
  public:
   TextReader(const std::string& path, const std::string& format, int part, int nparts,
              size_t chunk_bytes = 64 << 20, int nthreads = 8);
+  ~TextReader();
+  TextReader(const TextReader&) = delete;
+  TextReader& operator=(const TextReader&) = delete;
   bool Next();
   const RowBlockContainer<feaid_t>& Value() const { return blk_; }
   size_t BytesRead() const { return read_; }
@@ -109,7 +112,10 @@ class TextReader {
   size_t begin_ = 0, end_ = 0, pos_ = 0, chunk_, read_ = 0;
   int nthreads_;
   bool NextRec();
-  std::vector<char> buf_;
+  int fd_ = -1;
+  const char* map_ = nullptr;  // the file, mapped read-only
+  size_t map_size_ = 0;
+  std::string tail_;  // a terminated copy of an unterminated last line
   std::vector<RowBlockContainer<feaid_t>> parts_;  // per parser thread, reused
   RowBlockContainer<feaid_t> blk_;
   std::unique_ptr<RecordIOReader> rec_;  // format "rec"

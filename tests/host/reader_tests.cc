@@ -353,6 +353,25 @@ static void TestRecordIO(const std::string& data, const std::string& dir) {
   std::remove(rp.c_str());
 }
 
+// a file whose last line has no newline (and sizes around the page size)
+static void TestUnterminated(const std::string& dir) {
+  const std::string path = dir + "/unterminated.txt";
+  for (size_t pad : {size_t(0), size_t(1), size_t(4093), size_t(4094), size_t(4095)}) {
+    std::string text = std::string("1 ") + std::string(pad % 7 + 1, '7') + ":0.5\n";
+    while (text.size() < pad) text += "0 3:1\n";
+    text += "1 12:0.25 13:2";  // no newline
+    {
+      std::ofstream f(path, std::ios::binary);
+      f << text;
+    }
+    const auto all = ReadAll(path, "libsvm", 0, 1, 64 << 20, 2);
+    EXPECT(all.Size() >= 2 && all.label.back() == 1.f && all.index.back() == 13 &&
+               all.value.back() == 2.f,
+           "unterminated last line");
+  }
+  std::remove(path.c_str());
+}
+
 static void TestAdfea(const std::string& dir) {
   const std::string path = dir + "/adfea_sample.txt";
   {
@@ -409,6 +428,7 @@ int main(int argc, char** argv) {
   TestLz4();
   TestRecordIO(data, argv[2]);
   TestAdfea(argv[2]);
+  TestUnterminated(argv[2]);
   std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
   return g_fail ? 1 : 0;
 }
