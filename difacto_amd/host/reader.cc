@@ -563,6 +563,51 @@ void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
   for (size_t r = begin + 1; r <= end; ++r) dst->offset.push_back(src.offset[r] - o0 + base);
 }
 
+void GatherRows(const RowBlockContainer<feaid_t>& src, const size_t* rows, size_t begin,
+                size_t n, RowBlockContainer<feaid_t>* dst, int nthreads) {
+  if (n == 0) return;
+  auto row = [&](size_t i) { return rows ? rows[i] : begin + i; };
+  const size_t r0 = dst->label.size(), base = dst->index.size();
+  const bool valued = !src.value.empty(), weighted = !src.weight.empty();
+  dst->offset.resize(r0 + n + 1);
+  size_t* off = dst->offset.data() + r0;
+  for (size_t i = 0; i < n; ++i) {
+    const size_t j = row(i);
+    off[i + 1] = off[i] + (src.offset[j + 1] - src.offset[j]);
+  }
+  const size_t nnz = off[n] - base;
+  // value / weight arrays stay aligned with the rows: a binary side reads as ones
+  if (valued && dst->value.size() < base) dst->value.resize(base, 1.f);
+  if (weighted && dst->weight.size() < r0) dst->weight.resize(r0, 1.f);
+  const bool dval = !dst->value.empty() || valued, dwt = !dst->weight.empty() || weighted;
+  dst->index.resize(base + nnz);
+  dst->label.resize(r0 + n);
+  if (dval) dst->value.resize(base + nnz, 1.f);
+  if (dwt) dst->weight.resize(r0 + n, 1.f);
+  auto copy = [&](size_t i0, size_t i1) {
+    for (size_t i = i0; i < i1;) {
+      // a run of consecutive source rows is one copy
+      const size_t j0 = row(i);
+      size_t k = i + 1;
+      while (k < i1 && row(k) == j0 + (k - i)) ++k;
+      const size_t s0 = src.offset[j0], s1 = src.offset[j0 + (k - i)];
+      std::memcpy(&dst->index[off[i]], &src.index[s0], (s1 - s0) * sizeof(feaid_t));
+      if (valued) std::memcpy(&dst->value[off[i]], &src.value[s0], (s1 - s0) * 4);
+      std::memcpy(&dst->label[r0 + i], &src.label[j0], (k - i) * 4);
+      if (weighted) std::memcpy(&dst->weight[r0 + i], &src.weight[j0], (k - i) * 4);
+      i = k;
+    }
+  };
+  const int T = (int)std::min<size_t>(std::max(nthreads, 1), 1 + nnz / (1 << 16));
+  if (T <= 1) {
+    copy(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back(copy, n * t / T, n * (t + 1) / T);
+  for (auto& x : th) x.join();
+}
+
 static void ClearRows(RowBlockContainer<feaid_t>* c) {  // keeps the capacity
   c->offset.resize(1);
   c->label.clear();
@@ -612,8 +657,12 @@ static void ConcatParts(std::vector<RowBlockContainer<feaid_t>>* parts,
 
 // ---- TextReader -------------------------------------------------------------------------
 TextReader::TextReader(const std::string& path, const std::string& format, int part,
-                       int nparts, size_t chunk_bytes, int nthreads)
-    : path_(path), format_(format), chunk_(chunk_bytes), nthreads_(nthreads < 1 ? 1 : nthreads) {
+                       int nparts, size_t chunk_bytes, int nthreads, int ahead)
+    : ahead_(ahead < 0 ? 0 : ahead),
+      path_(path),
+      format_(format),
+      chunk_(chunk_bytes),
+      nthreads_(nthreads < 1 ? 1 : nthreads) {
   DFX_HOST_CHECK(format == "libsvm" || format == "criteo" || format == "criteo_test" ||
                      format == "adfea" || format == "rec",
                  "unknown data_format " + format);
@@ -646,6 +695,14 @@ TextReader::TextReader(const std::string& path, const std::string& format, int p
 }
 
 TextReader::~TextReader() {
+  if (parser_.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    parser_.join();
+  }
   if (map_) munmap(const_cast<char*>(map_), map_size_);
   if (fd_ >= 0) close(fd_);
 }
@@ -683,6 +740,49 @@ bool TextReader::NextRec() {
 }
 
 bool TextReader::Next() {
+  if (!ahead_) return ParseNext();
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!parser_.joinable()) {
+    for (int i = 0; i < ahead_; ++i) free_.emplace_back();
+    parser_ = std::thread([this]() { RunAhead(); });
+  }
+  free_.push_back(std::move(cur_));  // the caller is done with the previous chunk
+  cur_ = RowBlockContainer<feaid_t>();
+  cv_.notify_all();
+  cv_.wait(lk, [this]() { return done_ || !full_.empty(); });
+  if (full_.empty()) return false;
+  cur_ = std::move(full_.front());
+  full_.pop_front();
+  return true;
+}
+
+void TextReader::RunAhead() {
+  for (;;) {
+    RowBlockContainer<feaid_t> buf;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [this]() { return stop_ || !free_.empty(); });
+      if (stop_) return;
+      buf = std::move(free_.front());
+      free_.pop_front();
+    }
+    std::swap(buf, blk_);  // parse into a recycled buffer
+    const bool more = ParseNext();
+    std::swap(buf, blk_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (more) {
+        full_.push_back(std::move(buf));
+      } else {
+        done_ = true;
+      }
+    }
+    cv_.notify_all();
+    if (!more) return;
+  }
+}
+
+bool TextReader::ParseNext() {
   ClearRows(&blk_);
   if (rec_) return NextRec();
   if (pos_ >= end_) return false;
@@ -751,10 +851,11 @@ bool TextReader::Next() {
 BatchReader::BatchReader(const std::string& path, const std::string& format, int part,
                          int nparts, size_t batch_size, size_t shuf_buf, float neg_sampling,
                          int nthreads)
-    : reader_(path, format, part, nparts, 64 << 20, nthreads),
+    : reader_(path, format, part, nparts, 64 << 20, nthreads, shuf_buf ? 4 : 2),
       batch_size_(batch_size),
       shuf_buf_(shuf_buf),
-      neg_sampling_(neg_sampling) {
+      neg_sampling_(neg_sampling),
+      nthreads_(nthreads) {
   DFX_HOST_CHECK(batch_size > 0, "batch_size must be > 0");
   DFX_HOST_CHECK(shuf_buf == 0 || shuf_buf >= batch_size, "shuffle buffer < batch size");
 }
@@ -782,7 +883,7 @@ bool BatchReader::Refill() {
       continue;
     }
     const size_t take = std::min(shuf_buf_ - in_.Size(), reader_.Value().Size() - pend_pos_);
-    AppendRows(reader_.Value(), pend_pos_, pend_pos_ + take, &in_);
+    GatherRows(reader_.Value(), nullptr, pend_pos_, take, &in_, nthreads_);
     pend_pos_ += take;
   }
   order_.resize(in_.Size());
@@ -793,24 +894,34 @@ bool BatchReader::Refill() {
 
 bool BatchReader::Next() {
   ClearRows(&batch_);  // keep the batch's capacity (no fresh pages per batch)
-  while (batch_.Size() < batch_size_) {
-    if (start_ >= order_.size() && !Refill()) break;
+  sel_.clear();
+  // rows are picked in order, then copied in parallel before src_ changes (Refill)
+  auto flush = [&]() {
+    GatherRows(*src_, sel_.data(), 0, sel_.size(), &batch_, nthreads_);
+    sel_.clear();
+  };
+  while (batch_.Size() + sel_.size() < batch_size_) {
+    if (start_ >= order_.size()) {
+      if (src_ && !sel_.empty()) flush();
+      if (!Refill()) break;
+    }
     if (!shuf_buf_ && neg_sampling_ >= 1.f) {  // rows in file order: one bulk copy
       const size_t len = std::min(order_.size() - start_, batch_size_ - batch_.Size());
-      AppendRows(*src_, start_, start_ + len, &batch_);
+      GatherRows(*src_, nullptr, start_, len, &batch_, nthreads_);
       start_ += len;
       continue;
     }
-    while (start_ < order_.size() && batch_.Size() < batch_size_) {
+    while (start_ < order_.size() && batch_.Size() + sel_.size() < batch_size_) {
       const size_t j = order_[start_++];
       if (neg_sampling_ < 1.f) {
         // batch_reader.cc:57-63: drop a negative when rand_r / RAND_MAX > 1 - neg_sampling
         const float p = (float)rand_r(&seed_) / (float)RAND_MAX;
         if (src_->label[j] <= 0 && p > 1 - neg_sampling_) continue;
       }
-      AppendRows(*src_, j, j + 1, &batch_);
+      sel_.push_back(j);
     }
   }
+  if (!sel_.empty()) flush();
   // batch_reader.cc:71-73: all-one values mean binary data
   bool binary = true;
   for (float v : batch_.value)

@@ -91,23 +91,38 @@ class RecordIOReader {
   size_t begin_ = 0, end_ = 0, pos_ = 0, read_ = 0;
 };
 
+/** rows[0..n) of src (rows == nullptr: src rows [begin, begin + n)) appended to dst, the
+ * copies split over up to nthreads threads */
+void GatherRows(const RowBlockContainer<feaid_t>& src, const size_t* rows, size_t begin,
+                size_t n, RowBlockContainer<feaid_t>* dst, int nthreads);
 /** append rows [begin, end) of src to dst */
 void AppendRows(const RowBlockContainer<feaid_t>& src, size_t begin, size_t end,
                 RowBlockContainer<feaid_t>* dst);
 
-/** reads part `part` of `nparts` of a text file in chunks, parsed by `nthreads` threads */
+/** reads part `part` of `nparts` of a text file in chunks, parsed by `nthreads` threads.
+ * ahead > 0: a parser thread runs up to `ahead` chunks in front of the caller, so parsing
+ * overlaps whatever the caller does with the chunks (BytesRead then counts parsed bytes). */
 class TextReader {
  public:
   TextReader(const std::string& path, const std::string& format, int part, int nparts,
-             size_t chunk_bytes = 64 << 20, int nthreads = 8);
+             size_t chunk_bytes = 64 << 20, int nthreads = 8, int ahead = 0);
   ~TextReader();
   TextReader(const TextReader&) = delete;
   TextReader& operator=(const TextReader&) = delete;
   bool Next();
-  const RowBlockContainer<feaid_t>& Value() const { return blk_; }
+  const RowBlockContainer<feaid_t>& Value() const { return ahead_ ? cur_ : blk_; }
   size_t BytesRead() const { return read_; }
 
  private:
+  bool ParseNext();  // the next chunk into blk_
+  void RunAhead();
+  int ahead_ = 0;
+  std::thread parser_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<RowBlockContainer<feaid_t>> full_, free_;
+  RowBlockContainer<feaid_t> cur_;
+  bool done_ = false, stop_ = false;
   std::string path_, format_;
   size_t begin_ = 0, end_ = 0, pos_ = 0, chunk_, read_ = 0;
   int nthreads_;
@@ -137,6 +152,8 @@ class BatchReader {
   TextReader reader_;
   size_t batch_size_, shuf_buf_;
   float neg_sampling_;
+  int nthreads_;
+  std::vector<size_t> sel_;         // rows of src_ picked for the batch, not yet copied
   unsigned seed_ = 0;  // rand_r state of the negative sampling (batch_reader.cc:58)
   std::mt19937 shuffle_rng_{0};
   size_t pend_pos_ = 0;             // rows of the reader's chunk already in the shuffle buffer
