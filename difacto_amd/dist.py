@@ -173,6 +173,11 @@ class TorchComm:
             self.kgroup = dist.new_group(ranks)
             self.cgroup = dist.new_group(ranks, backend="gloo")
             self.kstream = torch.cuda.Stream(device=device)
+            # communicators up before the first grouped send/recv, which need not involve
+            # every rank
+            if self.world > 1:
+                dist.barrier(group=self.group)
+                dist.barrier(group=self.kgroup)
         else:
             self.kgroup = self.cgroup = group
 
@@ -184,15 +189,36 @@ class TorchComm:
         return [[int(o[self.rank]) for o in out]]
 
     def _a2a(self, x, ss, rs, row, group, async_op):
+        """all-to-all-v as grouped point-to-point transfers with the peers; this rank's own
+        part is a device copy (one process alone: the input itself), not an RCCL self-send"""
         home = x.device
         x = x[:sum(ss) * row]
         if self.stage_cpu:
             x = x.cpu()
-        out = torch.empty(sum(rs) * row, dtype=x.dtype, device=x.device)
-        work = self.dist.all_to_all_single(out, x.contiguous(),
-                                           output_split_sizes=[int(r) * row for r in rs],
-                                           input_split_sizes=[int(s) * row for s in ss],
-                                           group=group, async_op=async_op)
+        x = x.contiguous()
+        if self.world == 1:
+            return (x.to(home) if self.stage_cpu else x), None
+        so, ro = [0], [0]
+        for a, b in zip(ss, rs):
+            so.append(so[-1] + int(a) * row)
+            ro.append(ro[-1] + int(b) * row)
+        out = torch.empty(ro[-1], dtype=x.dtype, device=x.device)
+        ops = []
+        for p in range(self.world):
+            if p == self.rank:
+                continue
+            if so[p + 1] > so[p]:
+                ops.append(self.dist.P2POp(self.dist.isend, x[so[p]:so[p + 1]], p, group=group))
+            if ro[p + 1] > ro[p]:
+                ops.append(self.dist.P2POp(self.dist.irecv, out[ro[p]:ro[p + 1]], p, group=group))
+        works = self.dist.batch_isend_irecv(ops) if ops else []
+        me = self.rank
+        if so[me + 1] > so[me]:
+            out[ro[me]:ro[me + 1]].copy_(x[so[me]:so[me + 1]])
+        work = _Works(works)
+        if not async_op:
+            work.wait()
+            work = None
         if self.stage_cpu:
             out = out.to(home)
         return out, work
@@ -226,12 +252,24 @@ class TorchComm:
         return [t.tolist()]
 
 
+class _Works:
+    """the transfers of one grouped exchange"""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
 class _Work:
     def __init__(self, work, out, foreign=False):
         self.work, self.out, self.foreign = work, out, foreign
 
     def wait(self):
-        self.work.wait()  # the current stream waits for the exchange
+        if self.work is not None:
+            self.work.wait()  # the current stream waits for the exchange
         if self.foreign:
             # allocated on the exchange's own stream, read on this one: keep the caching
             # allocator from handing the memory out again before this stream is past its use

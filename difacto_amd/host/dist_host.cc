@@ -203,8 +203,17 @@ class RcclExchange : public ShardExchange {
       HipCheck(hipStreamWaitEvent(cs, in_, 0), "wait");
     }
     const std::vector<int64_t> so = Offsets(send_rows[0]), ro = Offsets(recv_rows[0]);
+    // this rank's own rows: a device copy, not an RCCL self-send (whose copy kernel runs on a
+    // few channels' blocks)
+    if (send_rows[0][rank_] > 0)
+      HipCheck(hipMemcpyAsync(static_cast<char*>(recv[0]) + ro[rank_] * row_bytes,
+                              static_cast<const char*>(send[0]) + so[rank_] * row_bytes,
+                              (size_t)send_rows[0][rank_] * row_bytes, hipMemcpyDeviceToDevice,
+                              cs),
+               "self copy");
     NcclCheck(ncclGroupStart(), "group");
     for (int p = 0; p < n_; ++p) {
+      if (p == rank_) continue;
       if (send_rows[0][p] > 0)
         NcclCheck(ncclSend(static_cast<const char*>(send[0]) + so[p] * row_bytes,
                            (size_t)send_rows[0][p] * row_bytes, ncclUint8, p, comm_[channel], cs),

@@ -127,9 +127,9 @@ def _gloo_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_matches_sharded_oracle():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_world2_matches_sharded_oracle(world):
     import torch.multiprocessing as mp
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
