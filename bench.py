@@ -290,11 +290,42 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     B, k, kb, d = args.batch, args.nnz, args.key_bits, args.vdim
     keyspace = 1 << kb
     per = keyspace // world + keyspace // (8 * world) + 4096
-    ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01, max_keys=per,
-                    max_vrows=per)
+    # max_keys sizes the table (cap = pow2 >= 2 * max_keys; a soft bound): the owner's share
+    # of the key space, so its table runs at the single-GPU bench's load factor (~0.5);
+    # max_vrows (a hard bound) has headroom for an uneven share
+    ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
+                    max_keys=max(keyspace // world, 1), max_vrows=per)
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo")
 
+    host_t = None
+    if os.environ.get("DFX_HOSTTIME"):  # host seconds per call of each shard / comm method
+        import collections
+        host_t = collections.defaultdict(float)
+
+        def timed(obj, name):
+            f = getattr(obj, name)
+
+            def w(*a, **kw):
+                t = time.perf_counter()
+                r = f(*a, **kw)
+                host_t[name] += time.perf_counter() - t
+                return r
+            setattr(obj, name, w)
+        for nm in ("localize", "localize_wait", "fwd_bwd", "owner_begin", "owner_pull",
+                   "owner_push"):
+            timed(shard, nm)
+        lw = shard.localize_wait
+
+        def lw_probe(*a, **kw):  # was the main stream already drained when the Localizer joined?
+            e = torch.cuda.Event()
+            e.record()
+            r = lw(*a, **kw)
+            host_t["main_idle_at_join"] += 1e-3 * float(e.query())
+            return r
+        shard.localize_wait = lw_probe
+        for nm in ("exchange_counts", "alltoallv_async", "alltoallv_keys_async"):
+            timed(comm, nm)
     pipe = None if args.sync else DI.ShardedPipeline([shard], comm)
     live = []  # a batch stays alive until the submit after the one that took it
 
@@ -327,6 +358,13 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if host_t is not None:
+        host_t.clear()
+    prof = None
+    if os.environ.get("DFX_PYPROF") and rank == 0:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     for i, bt in enumerate(batches):
         if pipe is None:
             step(bt, False, mark=lambda j, e=evs[i]: e[j + 1].record())
@@ -334,6 +372,14 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
             step(bt, False, mark=(lambda j, e=evs[i - 1]: e[j + 1].record()) if i else None)
     if pipe is not None:
         pipe.flush(mark=lambda j, e=evs[-1]: e[j + 1].record())
+    t_enq = time.perf_counter() - t0
+    if host_t is not None:
+        print("host ms/step", {k_: round(v / args.steps * 1e3, 4) for k_, v in host_t.items()},
+              file=sys.stderr, flush=True)
+        host_t.clear()
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["DFX_PYPROF"])
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -382,6 +428,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                      "algorithmic_bytes_per_launch": int(ab),
                      "launch_ms": round(fb_ms, 4)},
         "phases_ms_per_step_rank0": {p: round(v, 4) for p, v in ph.items()},
+        "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         "train_loss_per_row": round(tot[0] / max(tot[2], 1), 6),
         "train_auc": round(tot[1] / max(tot[2], 1), 6),
         "model_keys": int(tot[3]), "model_vrows": int(tot[4]),

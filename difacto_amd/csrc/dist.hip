@@ -27,6 +27,7 @@
 // Every per-key result therefore equals what N reference servers produce when worker r's push
 // reaches them r-th, with every pull of the step answered before any push.
 #include <algorithm>
+#include <cstdlib>
 
 #include "fm_args.h"
 
@@ -173,13 +174,66 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* K, const uin
   if (lane_id() == 0 && ins) atomicAdd(&ds->n_keys, (unsigned long long)ins);
 }
 
+// k_dist_segs and SGDUpdater::Get (sgd_updater.cc:34-58) in one pass, for a step with no
+// count push between the owner's find-or-insert and its pull: a group of G lanes per received
+// key.  Lane 0 keeps the segment books and finds-or-inserts the key (a repeat of a key sent by
+// several ranks finds the slot its head inserted: tbl_insert is safe against concurrent
+// inserts of one key); the group then writes the key's pull record [V(d) | w | live | 0 0] at
+// the key's received index.  d % 4 == 0.
+template <int G>
+__global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
+    const uint64_t* __restrict__ K, const uint32_t* __restrict__ P, int64_t R, DevState* ds,
+    const uint32_t* __restrict__ excl, const uint32_t* total, Table T, Params Pp,
+    uint32_t* segstart, uint32_t* segslot, uint32_t* sorted_idx, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int leader = (lane_id() / G) * G;
+  int ins = 0;
+  uint32_t slot = 0, src = 0;
+  if (i < R && l == 0) {
+    const uint64_t k = K[i];
+    const bool head = (i == 0 || k != K[i - 1]);
+    const uint32_t seg = head ? excl[i] : excl[i] - 1u;
+    src = P ? P[i] : (uint32_t)i;
+    sorted_idx[i] = src;
+    bool inserted;
+    int64_t s = tbl_insert(T, k, &inserted);
+    if (s < 0) {
+      atomicOr(&ds->err, kErrTableFull);
+      s = 0;
+    }
+    slot = (uint32_t)s;
+    ins = inserted;  // whichever of the key's items won the insert
+    if (head) {
+      segstart[seg] = (uint32_t)i;
+      segslot[seg] = slot;
+    }
+    if (i == R - 1) segstart[*total] = (uint32_t)R;
+  }
+  slot = (uint32_t)__shfl((int)slot, leader, kWave);
+  src = (uint32_t)__shfl((int)src, leader, kWave);
+  if (i < R) {
+    const int d = T.d, nc = d >> 2;
+    const int2 wr = *reinterpret_cast<const int2*>(&T.ent[slot]);  // {w, vrow}
+    const float w = __int_as_float(wr.x);
+    const int vr = wr.y;
+    const bool live = vr >= 0 && !(Pp.l1_shrk && w == 0.f);
+    float4* o = reinterpret_cast<float4*>(out + (int64_t)src * rec_floats(d));
+    const float4* V = reinterpret_cast<const float4*>(live ? row_V(T, vr) : T.V);
+    for (int c = l; c < nc; c += G) o[c] = live ? V[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (l == 0) o[nc] = make_float4(w, live ? 1.f : 0.f, 0.f, 0.f);
+  }
+  for (int off = 32; off > 0; off >>= 1) ins += __shfl_xor(ins, off, kWave);
+  if (lane_id() == 0 && ins) atomicAdd(&ds->n_keys, (unsigned long long)ins);
+}
+
 // The ranks' Update(kFeaCount) pushes in rank order (sgd_updater.cc:64-75), per owned key:
 // fea_cnt += count; InitV once V is absent, w != 0 and fea_cnt > V_threshold.  frank[u] = the
 // pushing rank whose Update draws the key's InitV.
 __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
                               const uint32_t* sorted_idx, const float* recv_cnt, RankOffs ro,
                               Table T, Params P, const uint32_t* nuniq, uint32_t* flags,
-                              uint32_t* frank) {
+                              uint32_t* frank, uint32_t* fcount) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= (int64_t)*nuniq) return;
   Entry* e = &T.ent[segslot[u]];
@@ -198,6 +252,7 @@ __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
   e->fea_cnt = st.w;
   flags[u] = f;
   frank[u] = fr;
+  if (f) atomicAdd(fcount, 1u);  // gates the InitV pass
 }
 
 // The ranks' Update(kGradient) pushes in rank order (sgd_updater.cc:76-100): per pushing rank,
@@ -206,9 +261,9 @@ __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
 __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
                             const uint32_t* sorted_idx, const float* g, RankOffs ro, Table T,
                             Params P, const uint32_t* nuniq, uint32_t* flags, uint32_t* frank,
-                            DevState* ds) {
+                            DevState* ds, uint32_t* fcount) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int dnew = 0;
+  int dnew = 0, nf = 0;
   if (u < (int64_t)*nuniq) {
     const int d = T.d;
     const int64_t S = rec_floats(d);
@@ -235,10 +290,15 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
     ent_set_state(en, e);
     flags[u] = f;
     frank[u] = fr;
+    nf = (int)f;
   }
-  for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
+  for (int off = 32; off > 0; off >>= 1) {
+    dnew += __shfl_xor(dnew, off, kWave);
+    nf += __shfl_xor(nf, off, kWave);
+  }
   if (lane_id() == 0 && dnew)
     atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+  if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
 }
 
 // flagged keys (key order) -> (rank, key) order: rank keys, segment payloads; the unused tail
@@ -247,9 +307,9 @@ __global__ void k_dist_initv_list(const uint32_t* flags_excl, const uint32_t* ft
                                   const uint32_t* frank, const uint32_t* nuniq, int64_t bound,
                                   uint32_t* rk, uint32_t* rv) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= bound) return;
-  const int64_t n = *nuniq;
   const uint32_t F = *ftotal;
+  if (u >= bound || F == 0) return;  // no InitV this step (the steady state)
+  const int64_t n = *nuniq;
   if (u < n) {
     const uint32_t e = flags_excl[u];
     const uint32_t nx = (u + 1 < n) ? flags_excl[u + 1] : F;
@@ -285,8 +345,9 @@ __global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uin
 }
 
 __global__ void k_dist_initv_finalize(const uint32_t* ftotal, int d, int64_t vcap,
-                                      DevState* ds) {
+                                      DevState* ds, uint32_t* fcount) {
   const uint32_t F = *ftotal;
+  *fcount = 0u;  // the flag count of the next Update of this slot
   ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * F);
   const unsigned long long nv = ds->n_vrows + F;
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
@@ -331,31 +392,52 @@ __global__ __launch_bounds__(kDNT) void k_dist_pull_vec(int64_t R, const uint32_
   if (l == 0) o[nc] = make_float4(w, live ? 1.f : 0.f, 0.f, 0.f);
 }
 
+// The loads run in three dependency levels, each level's loads issued together: the key's
+// segment bounds and slot; its table entry and its first pushing rank's record index; then
+// its V / Vaux chunk and that record's gradient chunk and {gw, pulled}.  A key pushed by more
+// than one rank (N > 1) reads its later records in the rank loop.
 template <int G>
-__global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart,
-                                                        const uint32_t* segslot,
-                                                        const uint32_t* sorted_idx,
-                                                        const float* g, RankOffs ro, Table T,
-                                                        Params P, const uint32_t* nuniq,
+__global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* __restrict__ segstart,
+                                                        const uint32_t* __restrict__ segslot,
+                                                        const uint32_t* __restrict__ sorted_idx,
+                                                        const float* __restrict__ g, RankOffs ro,
+                                                        Table T, Params P, const uint32_t* nuniq,
                                                         uint32_t* flags, uint32_t* frank,
-                                                        DevState* ds) {
+                                                        DevState* ds, uint32_t* fcount) {
   const int64_t u = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
   const int l = threadIdx.x % G;
-  int dnew = 0;
+  int dnew = 0, nf = 0;
   if (u < (int64_t)*nuniq) {
     const int d = T.d, nc = d >> 2;
     const int64_t S = rec_floats(d);
-    Entry* en = &T.ent[segslot[u]];
-    float4 e = ent_state(en);
-    const int vr = en->vrow;
-    bool has_v = vr >= 0;
+    // level 1
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
-    // UpdateW per pushing rank; every lane of the group runs the same sequence
+    const uint32_t sl = segslot[u];
+    // level 2
+    Entry* en = &T.ent[sl];
+    const float4 h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
+    const float fc = en->fea_cnt;
+    const uint32_t src0 = sorted_idx[s0];
+    // level 3
+    const int vr = __float_as_int(h.y);
+    const float* g0 = g + (int64_t)src0 * S;
+    const float2 gwp0 = *reinterpret_cast<const float2*>(g0 + d);  // {gw, pulled}
+    float4* V4 = reinterpret_cast<float4*>(row_V(T, vr >= 0 ? vr : 0));
+    float4* C4 = reinterpret_cast<float4*>(row_C(T, vr >= 0 ? vr : 0));
+    const bool mine = vr >= 0 && l < nc;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = mine ? V4[l] : z4, cg = mine ? C4[l] : z4;
+    const float4 gv0 = mine ? reinterpret_cast<const float4*>(g0)[l] : z4;
+    // UpdateW per pushing rank (sgd_updater.cc:76-100, 105-131); every lane of the group runs
+    // the same sequence
+    float4 e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
+    bool has_v = vr >= 0;
     uint32_t f = 0, fr = 0;
     for (uint32_t i = s0; i < s1; ++i) {
-      const uint32_t src = sorted_idx[i];
+      const uint32_t src = i == s0 ? src0 : sorted_idx[i];
+      const float gw = i == s0 ? gwp0.x : g[(int64_t)src * S + d];
       bool tr;
-      const int dw = ftrl_update(P, g[(int64_t)src * S + d], &e, &tr);
+      const int dw = ftrl_update(P, gw, &e, &tr);
       if (l == 0) dnew += dw;
       if (tr && d > 0 && !has_v && e.w > (float)P.V_threshold) {  // :118-121
         has_v = true;
@@ -367,17 +449,25 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart
       ent_set_state(en, e);
       flags[u] = f;
       frank[u] = fr;
+      nf = (int)f;
     }
     // UpdateV per pushing rank that pulled V (each coordinate independent)
     if (vr >= 0) {
-      float4* V4 = reinterpret_cast<float4*>(row_V(T, vr));
-      float4* C4 = reinterpret_cast<float4*>(row_C(T, vr));
       for (int c = l; c < nc; c += G) {
-        float4 v = V4[c], cg = C4[c];
+        if (c != l) {
+          v = V4[c];
+          cg = C4[c];
+        }
         for (uint32_t i = s0; i < s1; ++i) {
-          const float* gr = g + (int64_t)sorted_idx[i] * S;
-          if (gr[d + 1] == 0.f) continue;
-          const float4 gv = reinterpret_cast<const float4*>(gr)[c];
+          float4 gv;
+          if (i == s0 && c == l) {
+            if (gwp0.y == 0.f) continue;
+            gv = gv0;
+          } else {
+            const float* gr = g + (int64_t)sorted_idx[i] * S;
+            if (gr[d + 1] == 0.f) continue;
+            gv = reinterpret_cast<const float4*>(gr)[c];
+          }
           adagrad_update(P, gv.x, &v.x, &cg.x);
           adagrad_update(P, gv.y, &v.y, &cg.y);
           adagrad_update(P, gv.z, &v.z, &cg.z);
@@ -388,9 +478,13 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* segstart
       }
     }
   }
-  for (int off = 32; off > 0; off >>= 1) dnew += __shfl_xor(dnew, off, kWave);
+  for (int off = 32; off > 0; off >>= 1) {
+    dnew += __shfl_xor(dnew, off, kWave);
+    nf += __shfl_xor(nf, off, kWave);
+  }
   if (lane_id() == 0 && dnew)
     atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+  if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
 }
 
 static int vec_group(int d) {
@@ -415,7 +509,11 @@ static int owner_initv(Context* c, int slot, int nranks) {
   uint32_t* flags = ws.oflags.as<uint32_t>();
   uint32_t* nuniq = &OL.ds->totals[1];
   uint32_t* ftotal = &OL.ds->totals[2];
-  DFX_TRY(scan_u32(OL, flags, R, ftotal, nuniq));
+  uint32_t* fcount = &OL.ds->totals[3];
+  // gated on the device by the flag count: the scan, the sort and the draws exit at once
+  // when no key asked for V (the steady state)
+  static const bool no_gate = getenv("DFX_NO_INITV_GATE") != nullptr;  // A/B switch
+  DFX_TRY(scan_u32(OL, flags, R, ftotal, nuniq, no_gate ? nullptr : fcount));
   uint32_t* rk0 = ws.vals0.as<uint32_t>();
   uint32_t* rv0 = ws.vals1.as<uint32_t>();
   uint32_t* rk1 = reinterpret_cast<uint32_t*>(ws.keys0.as<uint64_t>());
@@ -427,13 +525,27 @@ static int owner_initv(Context* c, int slot, int nranks) {
   while ((1 << bits) < nranks) ++bits;
   // stable by rank; the tail (0xFF) sorts last and is never read
   DFX_TRY(radix_sort_pairs<uint32_t>(OL, rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
-                                     OL.ds->sortmeta));
+                                     OL.ds->sortmeta, ftotal));
   hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, OL.stream, rv0, rv1, ftotal,
                      ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds,
                      OL.ds->sortmeta);
   hipLaunchKernelGGL(k_dist_initv_finalize, dim3(1), dim3(1), 0, OL.stream, ftotal, c->P.V_dim,
-                     c->T.vcap, c->ds);
+                     c->T.vcap, c->ds, fcount);
   return DFX_OK;
+}
+
+// the owner's segments of a slot (find-or-insert of every received key), when still pending
+static void owner_segs(Context* c, int slot) {
+  if (!c->dist_segs_pending[slot]) return;
+  c->dist_segs_pending[slot] = false;
+  const Lane OL = owner_lane(c, slot);
+  Workspace& ws = *OL.ws;
+  const int64_t R = c->dist_R[slot];
+  hipLaunchKernelGGL(k_dist_segs, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0, OL.stream,
+                     c->dist_K[slot], c->dist_P[slot], R, c->ds, ws.oflags.as<uint32_t>(),
+                     &OL.ds->totals[1], c->T, ws.osegstart.as<uint32_t>(),
+                     ws.osegslot.as<uint32_t>(), ws.oseg_of.as<uint32_t>(),
+                     ws.osorted.as<uint32_t>());
 }
 
 static RankOffs rank_offs(const Context* c, int slot) {
@@ -585,7 +697,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_CHECK_ARG(R == 0 || recv_keys, "dist_owner_begin: null keys");
   c->dist_R[slot] = R;
   c->dist_offs[slot].assign(recv_offsets, recv_offsets + nranks + 1);
-  DFX_HIP(hipMemsetAsync(&OL.ds->totals[1], 0, 8, OL.stream));
+  DFX_HIP(hipMemsetAsync(&OL.ds->totals[1], 0, 12, OL.stream));
   if (R == 0) return DFX_OK;
   DFX_TRY(ws.keys0.ensure(R * 8));
   DFX_TRY(ws.keys1.ensure(R * 8));
@@ -631,14 +743,17 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   }
   hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, OL.stream, K, R, flags);
   DFX_TRY(scan_u32(OL, flags, R, nuniq));
-  hipLaunchKernelGGL(k_dist_segs, grid, dim3(kDNT), 0, OL.stream, K, Pm, R, c->ds, flags, nuniq,
-                     c->T, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
-                     ws.oseg_of.as<uint32_t>(), ws.osorted.as<uint32_t>());
+  c->dist_K[slot] = K;
+  c->dist_P[slot] = Pm;
+  c->dist_segs_pending[slot] = true;
+  // with no count push the segments are built by the pull (k_dist_segs_pull), in one pass
+  static const bool no_fuse = getenv("DFX_NO_SEGS_PULL") != nullptr;  // A/B switch
+  if (recv_cnt || vec_group(c->P.V_dim) == 0 || no_fuse) owner_segs(c, slot);
   if (recv_cnt) {
     hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, OL.stream,
                        ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
                        ws.osorted.as<uint32_t>(), recv_cnt, rank_offs(c, slot), c->T, c->P,
-                       nuniq, flags, ws.ofrank.as<uint32_t>());
+                       nuniq, flags, ws.ofrank.as<uint32_t>(), &OL.ds->totals[3]);
     if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, nranks));
   }
   DFX_HIP(hipGetLastError());
@@ -654,6 +769,24 @@ int dfx_dist_owner_pull(dfx_ctx* ctx, int slot, float* vals_out) {
   DFX_CHECK_ARG(vals_out, "dist_owner_pull: null buffer");
   const Lane OL = owner_lane(c, slot);
   const int G = vec_group(c->P.V_dim);
+  if (c->dist_segs_pending[slot] && G > 0) {
+    c->dist_segs_pending[slot] = false;
+    Workspace& ws = *OL.ws;
+#define DFX_SEGS_PULL(GG)                                                                    \
+    if (G == GG) {                                                                           \
+      const int64_t per = kDNT / GG;                                                         \
+      hipLaunchKernelGGL(k_dist_segs_pull<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0,     \
+                         OL.stream, c->dist_K[slot], c->dist_P[slot], R, c->ds,              \
+                         ws.oflags.as<uint32_t>(), &OL.ds->totals[1], c->T, c->P,            \
+                         ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),            \
+                         ws.osorted.as<uint32_t>(), vals_out);                               \
+    }
+    DFX_DIST_GROUPS(DFX_SEGS_PULL)
+#undef DFX_SEGS_PULL
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
+  }
+  owner_segs(c, slot);
 #define DFX_PULL(GG)                                                                         \
   if (G == GG) {                                                                             \
     const int64_t per = kDNT / GG;                                                           \
@@ -678,6 +811,7 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   const int64_t R = c->dist_R[slot];
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(recv_grads, "dist_owner_push: null buffer");
+  owner_segs(c, slot);  // a push with no pull before it
   const Lane OL = owner_lane(c, slot);
   Workspace& ws = *OL.ws;
   const int G = vec_group(c->P.V_dim);
@@ -689,7 +823,7 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
                        OL.stream, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),   \
                        ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,               \
                        &OL.ds->totals[1], ws.oflags.as<uint32_t>(),                          \
-                       ws.ofrank.as<uint32_t>(), c->ds);                                     \
+                       ws.ofrank.as<uint32_t>(), c->ds, &OL.ds->totals[3]);                  \
   }
   DFX_DIST_GROUPS(DFX_PUSH)
 #undef DFX_PUSH
@@ -698,7 +832,7 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
                        ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
                        ws.osorted.as<uint32_t>(), recv_grads, ro, c->T, c->P,
                        &OL.ds->totals[1], ws.oflags.as<uint32_t>(), ws.ofrank.as<uint32_t>(),
-                       c->ds);
+                       c->ds, &OL.ds->totals[3]);
   if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, (int)c->dist_offs[slot].size() - 1));
   DFX_HIP(hipGetLastError());
   return DFX_OK;

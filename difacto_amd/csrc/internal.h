@@ -140,6 +140,11 @@ struct Context {
   DevState* ods[2] = {nullptr, nullptr};
   int64_t dist_R[2] = {0, 0}, dist_rows[2] = {0, 0}, dist_U[2] = {-1, -1};
   std::vector<int64_t> dist_offs[2];
+  // owner segments of a slot not yet built: owner_begin leaves them to the pull, which
+  // builds them and answers the pull in one pass (k_dist_segs_pull)
+  bool dist_segs_pending[2] = {false, false};
+  const uint64_t* dist_K[2] = {nullptr, nullptr};  // the slot's owner keys, merged
+  const uint32_t* dist_P[2] = {nullptr, nullptr};  // their received indices (null: identity)
   unsigned long long* dist_host[2] = {nullptr, nullptr};
   // fused-step pipelining (step.hip): batch t+1's Localizer runs on loc_stream while the main
   // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
