@@ -301,16 +301,16 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
   if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
 }
 
-// flagged keys (key order) -> (rank, key) order: rank keys, segment payloads; the unused tail
-// sorts last
+// flagged keys (key order) -> (rank, key) order: rank keys, segment payloads (the sort that
+// follows reads the first *ftotal of them).  Strided over a capped grid.
 __global__ void k_dist_initv_list(const uint32_t* flags_excl, const uint32_t* ftotal,
                                   const uint32_t* frank, const uint32_t* nuniq, int64_t bound,
                                   uint32_t* rk, uint32_t* rv) {
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t F = *ftotal;
-  if (u >= bound || F == 0) return;  // no InitV this step (the steady state)
-  const int64_t n = *nuniq;
-  if (u < n) {
+  if (F == 0) return;  // no InitV this step (the steady state)
+  const int64_t n = std::min<int64_t>(*nuniq, bound);
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t e = flags_excl[u];
     const uint32_t nx = (u + 1 < n) ? flags_excl[u + 1] : F;
     if (nx != e) {
@@ -318,30 +318,31 @@ __global__ void k_dist_initv_list(const uint32_t* flags_excl, const uint32_t* ft
       rv[e] = (uint32_t)u;
     }
   }
-  if (u >= F) rk[u] = 0xFFu;
 }
 
 // InitV (sgd_updater.cc:144-152) of the q-th draw: seed jumped 3*d*q steps, pool row n_vrows+q
 __global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uint32_t* ftotal,
                              const uint32_t* segslot, Table T, float scale, DevState* ds,
                              const unsigned int* sortmeta) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= (int64_t)*ftotal) return;
+  const int64_t F = (int64_t)*ftotal;
   const uint32_t* rv = sortmeta[31] ? rv1 : rv0;
   const int d = T.d;
-  uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)q);
-  const int64_t vr = (int64_t)ds->n_vrows + q;
-  if (vr >= T.vcap) {
-    atomicOr(&ds->err, kErrPoolFull);
-    return;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < F;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)q);
+    const int64_t vr = (int64_t)ds->n_vrows + q;
+    if (vr >= T.vcap) {
+      atomicOr(&ds->err, kErrPoolFull);
+      continue;
+    }
+    float* V = row_V(T, vr);
+    float* C = row_C(T, vr);
+    for (int k = 0; k < d; ++k) {
+      V[k] = initv_value(rand_r_dev(&s), scale);
+      C[k] = 0.f;
+    }
+    T.ent[segslot[rv[q]]].vrow = (int32_t)vr;
   }
-  float* V = row_V(T, vr);
-  float* C = row_C(T, vr);
-  for (int k = 0; k < d; ++k) {
-    V[k] = initv_value(rand_r_dev(&s), scale);
-    C[k] = 0.f;
-  }
-  T.ent[segslot[rv[q]]].vrow = (int32_t)vr;
 }
 
 __global__ void k_dist_initv_finalize(const uint32_t* ftotal, int d, int64_t vcap,
@@ -519,14 +520,15 @@ static int owner_initv(Context* c, int slot, int nranks) {
   uint32_t* rk1 = reinterpret_cast<uint32_t*>(ws.keys0.as<uint64_t>());
   uint32_t* rv1 = reinterpret_cast<uint32_t*>(ws.keys1.as<uint64_t>());
   const dim3 grid((R + kDNT - 1) / kDNT);
-  hipLaunchKernelGGL(k_dist_initv_list, grid, dim3(kDNT), 0, OL.stream, flags, ftotal,
+  const dim3 igrid((unsigned)std::min<int64_t>((R + kDNT - 1) / kDNT, 1024));
+  hipLaunchKernelGGL(k_dist_initv_list, igrid, dim3(kDNT), 0, OL.stream, flags, ftotal,
                      ws.ofrank.as<uint32_t>(), nuniq, R, rk0, rv0);
   int bits = 0;
   while ((1 << bits) < nranks) ++bits;
-  // stable by rank; the tail (0xFF) sorts last and is never read
+  // stable by rank, over the *ftotal flagged keys
   DFX_TRY(radix_sort_pairs<uint32_t>(OL, rk0, rv0, rk1, rv1, R, 0, bits > 0 ? 8 : 0, nullptr,
                                      OL.ds->sortmeta, ftotal));
-  hipLaunchKernelGGL(k_dist_initv, grid, dim3(kDNT), 0, OL.stream, rv0, rv1, ftotal,
+  hipLaunchKernelGGL(k_dist_initv, igrid, dim3(kDNT), 0, OL.stream, rv0, rv1, ftotal,
                      ws.osegslot.as<uint32_t>(), c->T, c->P.V_init_scale, c->ds,
                      OL.ds->sortmeta);
   hipLaunchKernelGGL(k_dist_initv_finalize, dim3(1), dim3(1), 0, OL.stream, ftotal, c->P.V_dim,

@@ -362,7 +362,12 @@ __device__ inline int64_t scan_limit(int64_t n, const uint32_t* n_dev) {
   return m < n ? m : n;
 }
 
-// gate (optional, device): a zero there skips the scan (the data are known to be all zero)
+// gate (optional, device): a zero there skips the scan (the data are known to be all zero).
+// A gated scan runs on a capped grid (kScanGatedBlocks, tiles strided over the blocks), so
+// that when the gate is closed — the common case — its launches cost a few hundred
+// workgroups, not one per tile.
+constexpr int kScanGatedBlocks = 1024;
+
 __global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, int64_t n0,
                                                          const uint32_t* n_dev,
                                                          uint32_t* tilesum,
@@ -370,13 +375,17 @@ __global__ __launch_bounds__(kScanNT) void k_scan_reduce(const uint32_t* data, i
   if (gate && *gate == 0u) return;
   __shared__ uint32_t lds[kScanNT / kWave + 1];
   const int64_t n = scan_limit(n0, n_dev);
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  uint32_t s = 0;
+  const int64_t ntiles = (n0 + kScanTile - 1) / kScanTile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t base = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    uint32_t s = 0;
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) s += base + i < n ? data[base + i] : 0u;
-  uint32_t tot;
-  block_excl_scan<kScanNT>(s, lds, &tot);
-  if (threadIdx.x == 0) tilesum[blockIdx.x] = tot;
+    for (int i = 0; i < kScanItems; ++i) s += base + i < n ? data[base + i] : 0u;
+    uint32_t tot;
+    block_excl_scan<kScanNT>(s, lds, &tot);
+    if (threadIdx.x == 0) tilesum[tile] = tot;
+    __syncthreads();  // lds is reused by the next tile
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_scan_top(uint32_t* tilesum, int64_t ntiles,
@@ -405,19 +414,23 @@ __global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t 
   if (gate && *gate == 0u) return;
   __shared__ uint32_t lds[kScanNT / kWave + 1];
   const int64_t n = scan_limit(n0, n_dev);
-  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
-  uint32_t s = 0;
+  const int64_t ntiles = (n0 + kScanTile - 1) / kScanTile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t base = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    v[i] = base + i < n ? data[base + i] : 0u;
-    s += v[i];
-  }
-  uint32_t ex = block_excl_scan<kScanNT>(s, lds, nullptr) + tilesum[blockIdx.x];
+    for (int i = 0; i < kScanItems; ++i) {
+      v[i] = base + i < n ? data[base + i] : 0u;
+      s += v[i];
+    }
+    uint32_t ex = block_excl_scan<kScanNT>(s, lds, nullptr) + tilesum[tile];
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    if (base + i < n) data[base + i] = ex;
-    ex += v[i];
+    for (int i = 0; i < kScanItems; ++i) {
+      if (base + i < n) data[base + i] = ex;
+      ex += v[i];
+    }
+    __syncthreads();  // lds is reused by the next tile
   }
 }
 
@@ -435,11 +448,12 @@ int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
   const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
   DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   uint32_t* ts = L.ws->tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_scan_reduce, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
-                     ts, gate);
+  const unsigned nb = (unsigned)(gate && ntiles > kScanGatedBlocks ? kScanGatedBlocks : ntiles);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanNT), 0, L.stream, data, n, n_dev, ts,
+                     gate);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, ts, ntiles, total_dev, gate);
-  hipLaunchKernelGGL(k_scan_apply, dim3(ntiles), dim3(kScanNT), 0, L.stream, data, n, n_dev,
-                     ts, gate);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanNT), 0, L.stream, data, n, n_dev, ts,
+                     gate);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

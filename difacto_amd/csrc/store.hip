@@ -50,26 +50,28 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
                                                  Table T, float scale, DevState* ds,
                                                  const DevState* nds, const uint32_t* gate) {
   if (gate && *gate == 0u) return;
-  const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   const int64_t n = count_of(n_host, nds);
-  if (u >= n) return;
-  const uint32_t e = excl[u];
-  const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
-  if (nx == e) return;
-  const int d = T.d;
-  uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
-  const int64_t vr = (int64_t)ds->n_vrows + e;
-  if (vr >= T.vcap) {
-    atomicOr(&ds->err, kErrPoolFull);
-    return;
+  // strided over a grid capped like a gated scan's (run_initv)
+  for (int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * kStNT) {
+    const uint32_t e = excl[u];
+    const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
+    if (nx == e) continue;
+    const int d = T.d;
+    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+    const int64_t vr = (int64_t)ds->n_vrows + e;
+    if (vr >= T.vcap) {
+      atomicOr(&ds->err, kErrPoolFull);
+      continue;
+    }
+    float* V = row_V(T, vr);
+    float* C = row_C(T, vr);
+    for (int k = 0; k < d; ++k) {
+      V[k] = initv_value(rand_r_dev(&s), scale);
+      C[k] = 0.f;
+    }
+    T.ent[slot[u]].vrow = (int32_t)vr;
   }
-  float* V = row_V(T, vr);
-  float* C = row_C(T, vr);
-  for (int k = 0; k < d; ++k) {
-    V[k] = initv_value(rand_r_dev(&s), scale);
-    C[k] = 0.f;
-  }
-  T.ent[slot[u]].vrow = (int32_t)vr;
 }
 
 __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, DevState* ds) {
@@ -85,7 +87,9 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
   DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count, gate));
-  hipLaunchKernelGGL(k_initv, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0, c->stream,
+  const int64_t nb = (n_bound + kStNT - 1) / kStNT;
+  hipLaunchKernelGGL(k_initv, dim3((unsigned)(gate && nb > 1024 ? 1024 : nb)), dim3(kStNT), 0,
+                     c->stream,
                      n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate);
   hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
                      c->T.vcap, c->ds);
