@@ -49,6 +49,12 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="sharded store transport; gloo (staged through host memory) runs "
                          "several ranks on one GPU, for tests")
+    ap.add_argument("--main-prio", default=None, choices=("normal", "high"),
+                    help="priority of the compute stream (default: high for the sharded "
+                         "store, normal for the fused step).  Streams of one HIP priority "
+                         "share that priority's hardware queues, whose packets run in order: "
+                         "a high-priority compute stream keeps the step's kernels off the "
+                         "queues of RCCL's (normal-priority) streams")
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-batch", type=int, default=10_000)
     return ap.parse_args()
@@ -163,6 +169,11 @@ def main():
     from difacto_amd import hotpath as H
     import ctypes
 
+    prio = args.main_prio or ("high" if sharded else "normal")
+    if prio == "high":
+        # everything below (the library context takes torch's current stream) on it
+        cs = torch.cuda.Stream(device=dev, priority=-1)
+        torch.cuda.set_stream(cs)
     if sharded:
         run_sharded(args, torch, dist, dev, rank, world, local)
         dist.destroy_process_group()

@@ -27,3 +27,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_sha
   --output-format csv -- python3 bench.py --sharded --sync $ARGS \
   > gpurun_out/prof_${TAG}_sharded.log 2>&1 || exit $?
 echo "sharded ok"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_sharded_pipe -o trace \
+  --output-format csv -- python3 bench.py --sharded $ARGS \
+  > gpurun_out/prof_${TAG}_sharded_pipe.log 2>&1 || exit $?
+echo "sharded pipelined ok"
