@@ -80,6 +80,7 @@ _SIGS = {
                                       c_u64, vp]),
     "dfx_progress_read": (ctypes.c_int, [vp, ctypes.POINTER(Progress), ctypes.c_int]),
     "dfx_prof_enable": (ctypes.c_int, [vp, ctypes.c_int]),
+    "dfx_prof_enable_marks": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_uint]),
     "dfx_prof_read": (ctypes.c_int, [vp, f64p, ctypes.POINTER(ctypes.c_int), f64p]),
     "dfx_feeder_create": (ctypes.c_int, [vp, c_i64, c_i64, ctypes.POINTER(vp)]),
     "dfx_feeder_destroy": (ctypes.c_int, [vp]),

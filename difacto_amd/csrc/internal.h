@@ -132,6 +132,7 @@ struct Context {
   std::vector<hipEvent_t> lane_ev;  // prof_max steps x 4: loc start/end, AUC start/end
   double lane_stats[4] = {0, 0, 0, 0};
   int prof_max = 0, prof_n = 0;
+  unsigned prof_mask = ~0u;  // marks recorded (dfx_prof_enable_marks)
   // sharded store (dist.hip), per step slot (two steps in flight when pipelined): keys
   // received by this owner and each source rank's offset among them (owner buffers ows /
   // state ods), rows and unique keys of this worker's batch (Localizer buffers bws / bds,
@@ -170,10 +171,11 @@ constexpr int kZpadFloats = 256 * 16 + 1024;
 
 constexpr int kProfMarks = 8;  // start, localize, feacnt, pull, fwd, auc, bwd, initv/end
 inline void lane_mark(Context* c, int m, hipStream_t st) {
-  if (c->prof_n < c->prof_max) (void)hipEventRecord(c->lane_ev[(size_t)c->prof_n * 4 + m], st);
+  if (c->prof_n < c->prof_max && (c->prof_mask >> kProfMarks & 1u))
+    (void)hipEventRecord(c->lane_ev[(size_t)c->prof_n * 4 + m], st);
 }
 inline void prof_mark(Context* c, int m) {
-  if (c->prof_n < c->prof_max)
+  if (c->prof_n < c->prof_max && (c->prof_mask >> m & 1u))
     (void)hipEventRecord(c->prof_ev[(size_t)c->prof_n * kProfMarks + m], c->stream);
 }
 

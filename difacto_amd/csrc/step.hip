@@ -310,8 +310,13 @@ extern "C" int dfx_train_step(dfx_ctx* ctx, const dfx_batch* batch, int job_type
 
 // ---- phase timing ----------------------------------------------------------------------
 extern "C" int dfx_prof_enable(dfx_ctx* ctx, int max_steps) {
+  return dfx_prof_enable_marks(ctx, max_steps, ~0u);
+}
+
+extern "C" int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask) {
   DFX_CHECK_ARG(ctx && max_steps >= 0, "bad argument");
   Context* c = &ctx->c;
+  c->prof_mask = mask;
   DFX_HIP(hipStreamSynchronize(c->stream));
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   c->prof_ev.assign((size_t)max_steps * kProfMarks, nullptr);
@@ -343,6 +348,7 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
   for (int m = 0; m < kProfMarks - 1; ++m) ms[m] = 0;
   for (int s = 0; s < c->prof_n; ++s) {
     for (int m = 0; m < kProfMarks - 1; ++m) {
+      if ((c->prof_mask >> m & 3u) != 3u) continue;  // a mark of this phase not recorded
       float t = 0;
       DFX_HIP(hipEventElapsedTime(&t, c->prof_ev[(size_t)s * kProfMarks + m],
                                   c->prof_ev[(size_t)s * kProfMarks + m + 1]));
@@ -354,7 +360,8 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
   for (double& v : c->lane_stats) v = 0;
   if (c->loc_stream) DFX_HIP(hipStreamSynchronize(c->loc_stream));
   if (c->aux_stream) DFX_HIP(hipStreamSynchronize(c->aux_stream));
-  for (int s = 0; s < c->prof_n && !c->lane_ev.empty(); ++s) {
+  const bool lanes = (c->prof_mask >> kProfMarks & 1u) && (c->prof_mask & 1u);
+  for (int s = 0; s < c->prof_n && !c->lane_ev.empty() && lanes; ++s) {
     hipEvent_t* L = &c->lane_ev[(size_t)s * 4];
     hipEvent_t* M = &c->prof_ev[(size_t)s * kProfMarks];
     float t[4] = {0, 0, 0, 0};

@@ -254,8 +254,17 @@ def train_step(ctx, dblk, job_type=kTraining, push_cnt=False, max_index=MAX_INDE
 PHASES = ("localize", "probe_pull", "feacnt", "forward", "eval_auc", "backward_update", "initv")
 
 
-def prof_enable(ctx, max_steps):
-    check(_lib.lib().dfx_prof_enable(ctx.h, int(max_steps)))
+def prof_enable(ctx, max_steps, phases=None):
+    """time the next max_steps dfx_train_step calls: every phase and the lanes, or only the
+    named phases (e.g. ("backward_update",): fewer events, less added latency)"""
+    if phases is None:
+        check(_lib.lib().dfx_prof_enable(ctx.h, int(max_steps)))
+        return
+    mask = 0
+    for p in phases:
+        m = PHASES.index(p)
+        mask |= 3 << m
+    check(_lib.lib().dfx_prof_enable_marks(ctx.h, int(max_steps), mask))
 
 
 def prof_read(ctx):

@@ -197,6 +197,11 @@ int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset);
  * evaluate + AUC snapshot, backward+update, InitV+finalize}, the number of recorded steps,
  * and the mean unique-key count U per step (for algorithmic-byte accounting); it resets. */
 int dfx_prof_enable(dfx_ctx* ctx, int max_steps);
+/* dfx_prof_enable recording only the marks in mask: bit m (0..7) = the event at the start of
+ * phase m (bit 7: the step's end), bit 8 = the lanes' events.  A phase is timed when both its
+ * marks are recorded (0 otherwise); each timing event costs the step a little latency, so a
+ * throughput run records only the phase it reports (the backward: bits 5 and 6). */
+int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask);
 int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
 /* after dfx_prof_read: out[4] = mean ms per batch of the Localizer lane, of its start and of its
  * end relative to the context stream reaching that batch (start < 0: it ran ahead; end > 0:
