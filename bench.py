@@ -286,7 +286,10 @@ def main():
                      "traffic": pmc_traffic("k_fm_bwd" if dom == "backward_update"
                                             else "k_fm_fwd"),
                      "traffic_source": "profiles/r1/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
-                                       "WRITE_SIZE per launch, raw counter bytes)",
+                                       "WRITE_SIZE per launch); counters calibrated for "
+                                       "these access shapes in "
+                                       "profiles/r1/pmc_calibration.json (64-B requests "
+                                       "counted exactly, factor 1.00)",
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
