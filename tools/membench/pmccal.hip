@@ -58,6 +58,20 @@ __global__ void k_rmw(float4* t, unsigned n, unsigned mask) {
   *p = v;
 }
 
+// a 128-B row read-modify-written by 4 lanes in two 64-B instructions (V, then Vaux: the
+// backward's shape) — timed against k_rmw<8> (one 128-B instruction)
+__global__ void k_rmw2x64(float4* t, unsigned n, unsigned mask) {
+  const unsigned g = (blockIdx.x * blockDim.x + threadIdx.x) / 4;
+  const int l = threadIdx.x % 4;
+  if (g >= n) return;
+  float4* p = t + row_of(g, mask) * 8;
+  float4 v = p[l], c = p[4 + l];
+  v.x += 1.f;
+  c.y += 1.f;
+  p[l] = v;
+  p[4 + l] = c;
+}
+
 // 32-B entries, two per 64-B line; only even entries touched: one entry per line
 __global__ void k_e32(float4* t, unsigned n, unsigned mask) {
   const unsigned g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,8 +97,17 @@ int main(int argc, char** argv) {
     if (strcmp(which, "all") && strcmp(which, name)) return;
     for (int rep = 0; rep < 3; ++rep) launch();
     CK(hipDeviceSynchronize());
-    printf("%s rows=%u known_read_bytes=%.0f known_write_bytes=%.0f\n", name, n, bytes_r,
-           bytes_w);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int rep = 0; rep < 10; ++rep) launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%s rows=%u known_read_bytes=%.0f known_write_bytes=%.0f us=%.1f GB/s=%.0f\n", name,
+           n, bytes_r, bytes_w, ms * 100.f, (bytes_r + bytes_w) / (ms * 1e-4) / 1e9);
   };
   const unsigned m64 = (unsigned)(table / 64) - 1, m128 = (unsigned)(table / 128) - 1;
   run("r64", 64.0 * n, 0, [&] {
@@ -98,6 +121,9 @@ int main(int argc, char** argv) {
   });
   run("rmw128", 128.0 * n, 128.0 * n, [&] {
     hipLaunchKernelGGL(k_rmw<8>, dim3(n * 8 / NT), dim3(NT), 0, 0, t, n, m128);
+  });
+  run("rmw2x64", 128.0 * n, 128.0 * n, [&] {
+    hipLaunchKernelGGL(k_rmw2x64, dim3(n * 4 / NT), dim3(NT), 0, 0, t, n, m128);
   });
   run("e32", 16.0 * n, 16.0 * n, [&] {
     hipLaunchKernelGGL(k_e32, dim3(n / NT), dim3(NT), 0, 0, t, n, m64);
