@@ -137,7 +137,13 @@ class RcclExchange : public ShardExchange {
       }
       if (!ok) Fail("no communicator id in " + id_file);
     }
-    HipCheck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+    // the compute stream at high priority: HIP maps the streams of one priority onto that
+    // priority's hardware queues, which run their packets in order, so this keeps the step's
+    // kernels (and the library's high-priority side lanes) off the queues of the
+    // communication streams, whose send / receive kernels wait for peers
+    int least = 0, greatest = 0;
+    HipCheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+    HipCheck(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, greatest), "stream");
     DfxOk(dfx_ctx_set_stream(ctx, stream_), "dfx_ctx_set_stream");
     for (int c = 0; c < 2; ++c) {
       NcclCheck(ncclCommInitRank(&comm_[c], nranks, id[c], rank), "ncclCommInitRank");
