@@ -120,6 +120,10 @@ struct Table {
   int64_t vcap;
   int ordered;      // home slot = top bits of the key (see tbl_hash)
   int* probe_flag;  // device word: set when an insert probed past kClusterProbe slots
+  // ordered hash of a key-range server: the table holds the keys of one of range_mul equal
+  // ranges of the key space (dist.hip, owner(k) = floor(k * N / 2^64)), whose top bits are
+  // constant; k * range_mul (mod 2^64) is the key's position inside its range, monotone in k
+  uint64_t range_mul;
 };
 
 __host__ __device__ inline float* row_V(const Table& t, int64_t vr) {
@@ -150,7 +154,8 @@ __device__ inline void ent_set_state(Entry* e, float4 s) {
 // multiplicative hash at the next sync point (store.hip: table_unclump).
 constexpr int kClusterProbe = 64;
 __host__ __device__ inline uint64_t tbl_hash(uint64_t k, const Table& t) {
-  return t.ordered ? (k >> (64 - t.logcap)) : ((k * 0x9E3779B97F4A7C15ull) >> (64 - t.logcap));
+  return t.ordered ? ((k * t.range_mul) >> (64 - t.logcap))
+                   : ((k * 0x9E3779B97F4A7C15ull) >> (64 - t.logcap));
 }
 
 __device__ inline int64_t tbl_find(const Table& t, uint64_t k) {

@@ -181,6 +181,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   (void)hipMemcpy(c->ds, &init, sizeof(init), hipMemcpyHostToDevice);
   int64_t vrows = kw.max_vrows >= 0 ? kw.max_vrows : (c->P.V_dim > 0 ? kw.max_keys : 0);
   c->T.ordered = kw.ordered;
+  c->T.range_mul = 1;
   c->T.probe_flag = &c->ds->probe_flag;
   int rc = table_alloc(c, kw.max_keys, vrows);
   if (rc != DFX_OK) {

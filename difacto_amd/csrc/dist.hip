@@ -689,6 +689,8 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_TRY(pipeline_init(c));
+  // this table serves one of nranks key ranges: hash keys by their position in the range
+  DFX_TRY(table_set_ranges(c, nranks));
   const Lane OL = owner_lane(c, slot);
   Workspace& ws = *OL.ws;
   DFX_CHECK_ARG(recv_offsets[0] == 0, "dist_owner_begin: recv_offsets[0] must be 0");

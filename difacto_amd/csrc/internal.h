@@ -240,6 +240,7 @@ int pipeline_init(Context* c);
 // rehash with the multiplicative hash if inserts reported clustered keys (store.hip);
 // synchronises the context stream
 int table_unclump(Context* c);
+int table_set_ranges(Context* c, int nranks);
 int step_reserve(Context* c, int64_t rows, int64_t nnz);  // ws_reserve + the step's lanes
 int loc_reserve(Workspace& w, int64_t nnz);              // a Localizer's buffers
 

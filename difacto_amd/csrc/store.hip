@@ -298,6 +298,31 @@ int table_unclump(Context* c) {
   return DFX_OK;
 }
 
+// A key-range server's table (dist.hip): the ordered hash over the position of a key inside
+// the server's range (Table::range_mul = the number of ranges).  The plain ordered hash would
+// send all of one server's keys, which share their top bits, into 1/N of the table — probe
+// chains the length of the whole key set.  Rebuilds the table once when the range count
+// changes (same capacity); a table on the multiplicative hash needs nothing.
+int table_set_ranges(Context* c, int nranks) {
+  Table& T = c->T;
+  const uint64_t mul = (uint64_t)(nranks > 0 ? nranks : 1);
+  if (!T.ent || T.range_mul == mul) return DFX_OK;
+  if (!T.ordered) {
+    T.range_mul = mul;
+    return DFX_OK;
+  }
+  Table NT = T;
+  NT.range_mul = mul;
+  DFX_TRY(table_alloc_entries(&NT, c->cap, c->stream));
+  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
+                     c->cap, NT, c->ds);
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  (void)hipFree(T.ent);
+  T.ent = NT.ent;
+  T.range_mul = mul;
+  return DFX_OK;
+}
+
 int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
   if (n_keys < 1024) n_keys = 1024;
   int64_t cap = 1;
@@ -622,6 +647,7 @@ int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks) {
   DFX_CHECK_ARG(ctx && path, "null argument");
   DFX_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "store_load_part: bad rank");
   Context* c = &ctx->c;
+  DFX_TRY(table_set_ranges(c, nranks));  // this server keeps the keys of range `rank`
   Table& T = c->T;
   FILE* f = fopen(path, "rb");
   if (!f) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
