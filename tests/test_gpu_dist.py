@@ -410,3 +410,35 @@ def test_bench_two_ranks_gloo(sync):
     assert out["config"]["global_batch"] == 40000
     assert 0.3 < out["train_loss_per_row"] < 0.8 and 0.3 < out["train_auc"] < 0.7
     assert ("bulk-synchronous" in out["config"]["workload"]) == sync
+
+
+@pytest.mark.timeout(240)
+def test_sharded_eight_ranges_at_scale():
+    """8 key-range servers, each with its table sized for its own range (1/8 of 2^24 keys),
+    fed Criteo-shaped batches of 20,000 rows: every server's keys share their top 3 bits, so
+    the ordered hash must place keys by their position inside the range (Table::range_mul) —
+    with the plain top-bits hash one server's keys crowd into 1/8 of its table and each probe
+    walks ~10^6 slots (this test then runs into its timeout).  Results against the sharded
+    oracle: loss per shard within 1e-4, the model's key and V-row counts and seeds exact."""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, rows, kb = 8, 20_000, 24
+    kw = dict(V_dim=16, V_threshold=0, lr=0.1, V_lr=0.01, l1=0.0, seed=3)
+    ctxs = [H.Context(0, max_keys=(1 << kb) // N, max_vrows=(1 << kb) // N + 65536, **kw)
+            for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.ShardedOracle(N, **kw)
+    for s in range(3):
+        step = [D.synthetic(rows, 39, 1 << kb, seed=900 + 17 * s + r) for r in range(N)]
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=(s == 0))
+        out = so.step(step, push_cnt=(s == 0))
+        for r in range(N):
+            pr = H.progress(ctxs[r])
+            assert pr["loss"] == pytest.approx(out[r][0], rel=1e-4), (s, r)
+    for g in range(N):
+        st = H.Store(ctxs[g]).stats()
+        assert st["n_keys"] == so.up[g].size() and st["seed"] == so.up[g].seed, g
+    for c in ctxs:
+        c.close()
