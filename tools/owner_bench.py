@@ -36,11 +36,14 @@ def main():
         lab = torch.where(torch.rand(B, device=dev, generator=g) < .25, 1.0, -1.0)
         return _Dev(offs, ids, lab.to(torch.float32))
 
-    for s in range(steps):
+    # count-push steps until the key space is covered (as bench.py's epoch 0), so the timed
+    # steps run in the steady state: every key present, no inserts
+    warm = max(1, -(-int(4.6 * (1 << kb)) // (N * B * k)))
+    for s in range(warm + steps):
         dbs = [batch(1000 * s + r) for r in range(N)]
-        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=(s == 0))
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=(s < warm))
         torch.cuda.synchronize()
-        print("step", s, flush=True)
+        print("step", s, "warm" if s < warm else "", flush=True)
     print("owner_bench N=%d B=%d steps=%d done" % (N, B, steps))
 
 
