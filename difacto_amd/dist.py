@@ -189,8 +189,10 @@ class TorchComm:
         return [[int(o[self.rank]) for o in out]]
 
     def _a2a(self, x, ss, rs, row, group, async_op):
-        """all-to-all-v as grouped point-to-point transfers with the peers; this rank's own
-        part is a device copy (one process alone: the input itself), not an RCCL self-send"""
+        """all-to-all-v of rows of `row` elements: ss[p] rows to rank p, rs[p] rows from it.
+        One process alone: the input itself.  RCCL: one all_to_all_single.  gloo (tests,
+        ranks sharing a GPU): grouped point-to-point transfers with the peers and a copy of
+        this rank's own part."""
         home = x.device
         x = x[:sum(ss) * row]
         if self.stage_cpu:
@@ -198,6 +200,15 @@ class TorchComm:
         x = x.contiguous()
         if self.world == 1:
             return (x.to(home) if self.stage_cpu else x), None
+        if self.nccl:
+            # one all-to-all-v call (RCCL groups the per-peer sends / receives in C++): a
+            # Python-side P2POp per peer costs tens of microseconds of host time each, which at
+            # 8 ranks (14 transfers, three exchanges a step) approaches the step itself
+            out = torch.empty(sum(int(b) for b in rs) * row, dtype=x.dtype, device=x.device)
+            work = self.dist.all_to_all_single(
+                out, x, output_split_sizes=[int(b) * row for b in rs],
+                input_split_sizes=[int(a) * row for a in ss], group=group, async_op=async_op)
+            return out, work
         so, ro = [0], [0]
         for a, b in zip(ss, rs):
             so.append(so[-1] + int(a) * row)
