@@ -106,11 +106,11 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/r1/pmc_hbm.json: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
+    (profiles/r1/<fname>: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
     tools/profile.sh).  None when absent."""
-    path = os.path.join(ROOT, "profiles", "r1", "pmc_hbm.json")
+    path = os.path.join(ROOT, "profiles", "r1", fname)
     try:
         with open(path) as f:
             ks = json.load(f)["kernels"]
@@ -120,6 +120,13 @@ def pmc_traffic(kernel_prefix):
         if name.startswith(kernel_prefix):
             return int((v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]) * 1024)
     return None
+
+
+def sharded_traffic():
+    """the sharded worker's forward + backward (record mode) HBM bytes per step"""
+    f = pmc_traffic("k_fm_fwd<4, 4, 2, false, true>", "pmc_hbm_sharded.json")
+    b = pmc_traffic("k_fm_bwd<4, 4, false, true>", "pmc_hbm_sharded.json")
+    return f + b if f is not None and b is not None else None
 
 
 def cpu_baseline(args):
@@ -471,7 +478,10 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                    "parallelism": "dp%d + model sharded by key range" % world},
         "roofline": {"bound": "hbm", "kernel": "fwd_bwd (dist forward+AUC+backward, rank 0)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": sharded_traffic(),
+                     "traffic_source": "profiles/r1/pmc_hbm_sharded.json (rocprofv3 "
+                                       "FETCH_SIZE + WRITE_SIZE per launch of the worker's "
+                                       "forward and backward, N = 1 sharded bench)",
                      "algorithmic_bytes_per_launch": int(ab),
                      "launch_ms": round(fb_ms, 4)},
         "phases_ms_per_step_rank0": {p: round(v, 4) for p, v in ph.items()},

@@ -9,7 +9,7 @@ import json
 import sys
 
 KERNELS = ("k_probe_keys", "k_fm_fwd<", "k_fm_bwd<", "k_loc_write", "k_loc_transform",
-           "k_os_scatter<", "k_initv")
+           "k_os_scatter<", "k_initv", "k_dist_")
 
 
 def load(path):
@@ -33,8 +33,8 @@ def main():
                       "write_size_kb_per_dispatch": sum(w) / len(w)}
     doc = {"_source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
                       "bench.py --steps 3 --warmup 1 (tools/profile.sh %s); last %d dispatches "
-                      "averaged; KB as rocprofv3 reports them (FETCH_SIZE = TCC_EA0_RDREQ x 64 B, "
-                      "uncalibrated for random 64-B line reads, see DESIGN.md)" % (tag, n),
+                      "averaged; KB as rocprofv3 reports them (FETCH_SIZE = TCC_EA0_RDREQ x 64 B; "
+                      "calibration: profiles/r1/pmc_calibration.json)" % (tag, n),
            "kernels": res}
     json.dump(doc, open(out, "w"), indent=1)
 

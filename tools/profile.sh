@@ -31,3 +31,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_sha
   --output-format csv -- python3 bench.py --sharded $ARGS \
   > gpurun_out/prof_${TAG}_sharded_pipe.log 2>&1 || exit $?
 echo "sharded pipelined ok"
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_${TAG}_sharded -o pmc \
+  --output-format csv -- python3 bench.py --sharded --steps 3 --warmup 1 --no-cpu-baseline \
+  > gpurun_out/pmc_fetch_${TAG}_sharded.log 2>&1 || exit $?
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_${TAG}_sharded -o pmc \
+  --output-format csv -- python3 bench.py --sharded --steps 3 --warmup 1 --no-cpu-baseline \
+  > gpurun_out/pmc_write_${TAG}_sharded.log 2>&1 || exit $?
+echo "sharded pmc ok"
