@@ -690,6 +690,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   a.B = B; a.offs = b->offset; a.col = bw.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
   a.rec_S = (int)S; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
   a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
+  a.xs = xvp_stride(d);
   a.loss_part = ws.dscratch.as<double>() + 8;
   int nblk = 0;
   DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
@@ -712,6 +713,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
     g.occ_row = bw.occ_row.as<uint32_t>();
     g.occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = ws.p.as<float>(); g.XVp = ws.XVp.as<float>(); g.d = d;
+    g.xs = xvp_stride(d);
     g.rec_S = (int)S; g.W = pulled; g.grad = grads_out;
     DFX_TRY(launch_bwd_positions(g, U, c->stream));
   }

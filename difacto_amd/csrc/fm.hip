@@ -236,8 +236,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
     } else {
       const float predv = (MODE == kGradPrep) ? a.pred_in[r] : pr;
       const float p = logit_p(a.label[r], predv, a.rw, r);
+      const int64_t xs = a.xs > d ? a.xs : d;
       if (l == 0) {
         a.p_out[r] = p;
+        if (xs > d) a.XVp[r * xs + d] = p;
         if (MODE == kFused || PROBE) {
           a.pred[r] = pr;
           double yy = a.label[r] > 0 ? 1.0 : -1.0;
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         float o[CPL];
 #pragma unroll
         for (int k = 0; k < CPL; ++k) o[k] = xv[k] * p;  // XV_ *= p (fm_loss.h:196-199)
-        store_coords<CPL, VEC>(a.XVp + r * d, l, d, o);
+        store_coords<CPL, VEC>(a.XVp + r * xs, l, d, o);
       }
     }
   }
@@ -356,6 +358,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
     const bool valued = a.occ_x != nullptr;
     const int d = a.d;
+    const int64_t xs = a.xs > d ? a.xs : d;
     const uint32_t len = s1 - s0;
     // ---- level-2 loads, mutually independent: the key's table entry (or its positions in
     // the pulled layout) and the first UNR occurrences of its segment
@@ -436,8 +439,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float pr[UNR], xr[UNR][CPL];
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
-      pr[t] = a.p[row[t]];
-      load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)row[t] * d : zp, l, d, xr[t]);
+      pr[t] = xs > d ? a.XVp[(int64_t)row[t] * xs + d] : a.p[row[t]];
+      load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)row[t] * xs : zp, l, d, xr[t]);
     }
     float xxp = 0.f;
     float acc[CPL];
@@ -504,7 +507,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
           xw[t] = valued ? a.occ_x[i] : 1.f;
         }
 #pragma unroll
-        for (int t = 0; t < UNR; ++t) pw[t] = a.p[rw[t]];
+        for (int t = 0; t < UNR; ++t)
+          pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
           if (i0 + t < s1 && pw[t] != 0.f) {
@@ -532,7 +536,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
           }
 #pragma unroll
           for (int t = 0; t < UNR; ++t)
-            load_coords<CPL, VEC>(a.XVp + (int64_t)rw[t] * d, l, d, xrw[t]);
+            load_coords<CPL, VEC>(a.XVp + (int64_t)rw[t] * xs, l, d, xrw[t]);
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
             if (i0 + t < s1) {
@@ -623,6 +627,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   const uint32_t s1 = s0 + kChunkOcc < send ? s0 + kChunkOcc : send;
   const bool valued = a.occ_x != nullptr;
   const int d = a.d;
+  const int64_t xs = a.xs > d ? a.xs : d;
   float gw = 0.f, xxp = 0.f, acc[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
@@ -637,8 +642,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
     }
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
-      pw[t] = a.p[rw[t]];
-      load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)rw[t] * d : a.zpad, l, d, xr[t]);
+      pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+      load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)rw[t] * xs : a.zpad, l, d, xr[t]);
     }
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {

@@ -33,7 +33,10 @@ struct FwdArgs {
   const float* pred_in;  // gradient prep: p from this pred
   float* pred;           // predict: in/out (+=); fused: out
   float* p_out;
-  float* XVp;            // B*d: XV_ * p
+  float* XVp;            // B rows of xs floats: XV_ * p (xs = 0: d)
+  // xs > d: row r also carries p at XVp[r*xs + d], so the backward reads p from the line it
+  // reads XV_*p from (one random row instead of two)
+  int xs;
   double* loss_part;     // fused: per-block partial sums of Evaluate
 };
 
@@ -47,6 +50,7 @@ struct BwdArgs {
   const float* zpad;
   const float* p;
   const float* XVp;
+  int xs;                    // XVp row stride (0: d); xs > d: p at XVp[row*xs + d]
   int d;
   // standalone CalcGrad: positions into grad
   const int32_t* wpos;
@@ -75,6 +79,8 @@ struct BwdArgs {
   float* part;
 };
 
+// the XVp row stride the workspace is sized for (step.hip): p rides in each row
+int xvp_stride(int d);
 // fused forward; *nblk receives the number of loss partials written
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk);
 // fused backward + FTRL/AdaGrad update over at most nseg_bound segments

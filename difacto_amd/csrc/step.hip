@@ -22,6 +22,14 @@ void sum_parts(Context* c, const double* part, int64_t n, double* out, bool accu
 
 namespace dfx {
 
+// Row stride of the fused step's XV_*p rows: a multiple of 32 floats (128 B) carrying p after
+// XV_*p, so the backward's per-occurrence p and XV_*p sit in one 128-byte line (+3 % of the
+// step at d = 16, same-box A/B).  DFX_XVP_ROW=0 (A/B switch): rows of d floats, p apart.
+int xvp_stride(int d) {
+  static const bool on = !getenv("DFX_XVP_ROW") || atoi(getenv("DFX_XVP_ROW")) != 0;
+  return (on && d > 0) ? (d + 1 + 31) / 32 * 32 : d;
+}
+
 // main lane: per-row arrays of the forward / backward and the InitV scan
 int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   Workspace& ws = c->ws;
@@ -32,7 +40,7 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
   DFX_TRY(ws.p.ensure(rows * 4));
   DFX_TRY(ws.pred.ensure(rows * 4));
-  if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * d * 4));
+  if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * xvp_stride(d) * 4));
   DFX_TRY(ws.dscratch.ensure((rows / 4 + 64) * 8));
   DFX_TRY(ws.wv.ensure(nnz * 8));
   DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 4));  // chunk partials
@@ -250,7 +258,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
-  a.XVp = ws.XVp.as<float>();
+  a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(d);
   a.loss_part = ws.dscratch.as<double>() + 8;
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk));
@@ -273,7 +281,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     BwdArgs g{};
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
-    g.XVp = ws.XVp.as<float>(); g.d = d; g.slot = segslot; g.T = c->T; g.Pm = c->P;
+    g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(d); g.d = d; g.slot = segslot;
+    g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<float>();
