@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr bool PROBE = MODE == kFusedProbe;
   // probe mode carries keys and home slots per item; at CPL 4, 8 items in flight per lane
-  // (+1.4 % of the step over 4, same-box A/B; 16 spills the forward to 0.375 ms)
+  // (+1.4 % of the step over 4, same-box A/B; 16 is slower: forward 0.30 -> 0.375 ms)
   constexpr int UNR = PROBE ? (CPL <= 4 ? 8 : 2) : (CPL <= 4 ? 8 : (CPL <= 8 ? 4 : 2));
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
