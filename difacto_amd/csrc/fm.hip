@@ -367,14 +367,24 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     uint32_t sl = 0;
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
     float fc = 0.f;
+    bool home = false;  // the key's entry was read at its home slot already
     if (FUSED) {
       if (a.insert_keys) {
         // Get's find-or-insert (model_[key]) here instead of a separate pass: the home slot
         // first (every lane), a longer chain or an insert by the group's first lane
         const uint64_t key = a.uniq[cidx];
         const uint64_t hh = tbl_hash(key, a.T);
+        // the whole home entry in two 16-byte loads issued together: {w, vrow, sqrt_g, z} and
+        // {fea_cnt, pad, key}; a key found at home (the common case) needs no second trip
+        const float4* eh = reinterpret_cast<const float4*>(a.T.ent + hh);
+        const float4 h0 = eh[0], h1 = eh[1];
+        const uint64_t ek =
+            ((uint64_t)__float_as_uint(h1.w) << 32) | (uint64_t)__float_as_uint(h1.z);
+        home = ek == key;
+        h = h0;
+        fc = h1.x;
         int s = (int)hh;
-        if (a.T.ent[hh].key != key) {
+        if (!home) {
           int s0 = 0;
           if (l == 0) {
             bool inserted;
@@ -390,9 +400,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       } else {
         sl = a.slot[cidx];
       }
-      const Entry* en = a.T.ent + sl;
-      h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
-      fc = en->fea_cnt;
+      if (!home) {
+        const Entry* en = a.T.ent + sl;
+        h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
+        fc = en->fea_cnt;
+      }
     } else if (a.rec_S) {
       wq = (int)((int64_t)cidx * a.rec_S + d);
       vq = (d > 0 && a.W[wq + 1] != 0.f) ? (int)((int64_t)cidx * a.rec_S) : -1;
