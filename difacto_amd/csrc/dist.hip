@@ -229,14 +229,25 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
   const int leader = (lane_id() / G) * G;
   int ins = 0;
   uint32_t slot = 0, src = 0;
+  int2 wr = make_int2(0, -1);
+  int found = 0;  // the key sat at its home slot: wr already holds its {w, vrow}
   if (i < R && l == 0) {
     const uint64_t k = K[i];
     const bool head = (i == 0 || k != K[i - 1]);
     const uint32_t seg = head ? excl[i] : excl[i] - 1u;
     src = P ? P[i] : (uint32_t)i;
     sorted_idx[i] = src;
-    bool inserted;
-    int64_t s = tbl_insert(T, k, &inserted);
+    // the home entry's {w, vrow} and key in one trip (w / vrow of a slot are not written in
+    // this kernel, and a fresh slot already holds the zero state)
+    const uint64_t hh = tbl_hash(k, T);
+    wr = *reinterpret_cast<const int2*>(&T.ent[hh]);
+    bool inserted = false;
+    int64_t s = (int64_t)hh;
+    if (T.ent[hh].key == k) {
+      found = 1;
+    } else {
+      s = tbl_insert(T, k, &inserted);
+    }
     if (s < 0) {
       atomicOr(&ds->err, kErrTableFull);
       s = 0;
@@ -251,9 +262,12 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
   }
   slot = (uint32_t)__shfl((int)slot, leader, kWave);
   src = (uint32_t)__shfl((int)src, leader, kWave);
+  found = __shfl(found, leader, kWave);
+  wr.x = __shfl(wr.x, leader, kWave);
+  wr.y = __shfl(wr.y, leader, kWave);
   if (i < R) {
     const int d = T.d, nc = d >> 2;
-    const int2 wr = *reinterpret_cast<const int2*>(&T.ent[slot]);  // {w, vrow}
+    if (!found) wr = *reinterpret_cast<const int2*>(&T.ent[slot]);  // {w, vrow}
     const float w = __int_as_float(wr.x);
     const int vr = wr.y;
     const bool live = vr >= 0 && !(Pp.l1_shrk && w == 0.f);
