@@ -130,26 +130,39 @@ def sharded_traffic():
 
 
 def cpu_baseline(args):
-    """The oracle (scalar C++ restatement, 1 thread) on a bounded sample of the same workload:
-    epoch 0 (count push, untimed) then a timed epoch over the same rows (steady state)."""
+    """The reference's CPU hot path restated WITH its threading (oracle/cpu_ref.cc: OpenMP
+    row / column splits of SpMV / SpMM, ParallelSort, the two-thread IterateData pipeline, the
+    single-threaded unordered_map SGDUpdater of StoreLocal) on a bounded sample of the same
+    workload: one untimed count-push epoch, then one timed steady-state epoch per thread count
+    over the same rows — 1 thread, the reference's default blk_nthreads_ = 2, and every host
+    core this job may use (OMP_NUM_THREADS, else the CPU count)."""
     from difacto_amd import data as D
-    from oracle import oracle as O
-    O.build()
-    up = O.Updater(V_dim=args.vdim, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    from oracle import cpu_ref as C
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or (os.cpu_count() or 1)
     nb = max(1, args.cpu_rows // args.cpu_batch)
     blocks = [D.synthetic(args.cpu_batch, args.nnz, 1 << args.key_bits, seed=1000 + i)
               for i in range(nb)]
+    ref = C.CpuRef(cores, V_dim=args.vdim, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     for b in blocks:
-        up.train_step(b.offs, b.ids, b.vals, b.labels, push_cnt=True)
-    t0 = time.perf_counter()
-    for b in blocks:
-        up.train_step(b.offs, b.ids, b.vals, b.labels, push_cnt=False)
-    dt = time.perf_counter() - t0
-    return {"value": round(nb * args.cpu_batch / dt, 1), "unit": "train examples/sec",
-            "cores": 1, "kind": "port",
-            "sample": "%d rows (%d batches of %d), Criteo-shaped C3, steady-state epoch 2 after a "
-                      "count-push epoch; oracle/oracle.cc full hot path incl. Localizer/AUC, "
-                      "1 thread" % (nb * args.cpu_batch, nb, args.cpu_batch)}
+        ref.step(b, push_cnt=True)
+    by_threads, phases = {}, {}
+    for nt in sorted({1, 2, cores}):
+        ref.nt = nt
+        C.phases()
+        dt, _, _, n = ref.iterate(blocks)
+        by_threads[str(nt)] = round(n / dt, 1)
+        phases[str(nt)] = {k: round(v / n * 1e6, 3) for k, v in C.phases().items()}
+    ref.close()
+    return {"value": by_threads[str(cores)], "unit": "train examples/sec", "cores": cores,
+            "kind": "port",
+            "by_threads": by_threads,
+            "us_per_row_by_phase": phases,
+            "vs_survey_2thr": round(by_threads["2"] / 35800.0, 3),
+            "sample": "%d rows (%d batches of %d), Criteo-shaped C3, one steady-state epoch per "
+                      "thread count after a count-push epoch; oracle/cpu_ref.cc: the reference's "
+                      "threading (OpenMP SpMV/SpMM row/column splits, ParallelSort, reader + "
+                      "executor threads, single-threaded unordered_map updater)"
+                      % (nb * args.cpu_batch, nb, args.cpu_batch)}
 
 
 def main():

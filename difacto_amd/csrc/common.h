@@ -8,6 +8,9 @@ namespace dfx {
 
 constexpr int kWave = 64;
 constexpr uint64_t kEmptyKey = ~0ull;  // never produced by the Localizer
+// the slot of a key whose insert failed (table full, or the reserved key ~0): every consumer
+// skips it — no update ever lands in another key's entry
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 // include/difacto/base.h:39-51 — nibble reversal (involution).
 __host__ __device__ inline uint64_t reverse_bytes(uint64_t x) {
@@ -159,6 +162,7 @@ __host__ __device__ inline uint64_t tbl_hash(uint64_t k, const Table& t) {
 }
 
 __device__ inline int64_t tbl_find(const Table& t, uint64_t k) {
+  if (k == kEmptyKey) return -1;  // the reserved key is never stored
   uint64_t h = tbl_hash(k, t);
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
     uint64_t kk = t.ent[h].key;
@@ -169,12 +173,15 @@ __device__ inline int64_t tbl_find(const Table& t, uint64_t k) {
   return -1;
 }
 
-// find-or-insert; -1 when the table is full.  Keys of one launch must be distinct.
+// find-or-insert; -1 when the table is full, -2 for the reserved key kEmptyKey (it marks free
+// slots, so it cannot be stored: the raw-key store calls reject it, the Localizer never makes
+// it).  Concurrent inserts of one key are safe (the CAS loser finds the winner's slot).
 // Fresh slots already hold zero state and vrow -1 (the table is never compacted), which is
 // what `model_[key]` default-constructs (sgd_updater.h:20-34).
 __device__ inline int64_t tbl_insert(const Table& t, uint64_t k, bool* inserted) {
-  uint64_t h = tbl_hash(k, t);
   *inserted = false;
+  if (k == kEmptyKey) return -2;
+  uint64_t h = tbl_hash(k, t);
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
     uint64_t kk = t.ent[h].key;
     if (kk == k) return (int64_t)h;
@@ -200,7 +207,11 @@ enum : int {
   kErrLens = 4,
   kErrNoV = 8,
   kErrSort = 16,
+  kErrBadKey = 32,
 };
+
+// the error bit of a failed tbl_insert
+__device__ inline int insert_error(int64_t s) { return s == -2 ? kErrBadKey : kErrTableFull; }
 
 struct Params {
   float l1, l2, V_l2, lr, lr_beta, V_lr, V_lr_beta, V_init_scale;

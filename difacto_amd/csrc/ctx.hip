@@ -46,6 +46,11 @@ struct Kw {
   long long max_vrows = -1;
   int loss_fm = 1;
   int ordered = 1;
+  // execution choices (context kwargs, not behaviour switches of the process environment)
+  int fwd_probe = 1;    // fwd_probe=0: Localizer col + pulled {w, vrow} instead of probing
+  int xvp_row = 1;      // xvp_row=0: XV*p rows of d floats, p in its own array
+  long bwd_lds = -1;    // bwd_lds=<bytes>: LDS reserved per backward block (-1: default cap)
+  int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -76,6 +81,10 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "seed") kw->seed = (unsigned)strtoul(cv, nullptr, 10);
     else if (k == "max_keys") kw->max_keys = atoll(cv);
     else if (k == "max_vrows") kw->max_vrows = atoll(cv);
+    else if (k == "fwd_probe") kw->fwd_probe = atoi(cv) != 0;
+    else if (k == "xvp_row") kw->xvp_row = atoi(cv) != 0;
+    else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
+    else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;
     else if (k == "hash") {
       if (v == "ordered") kw->ordered = 1;
       else if (v == "mixed") kw->ordered = 0;
@@ -111,17 +120,13 @@ static void release_ws(Workspace& w) {
 // streams, events and lane states of the fused step's pipeline, created on first use
 int pipeline_init(Context* c) {
   if (c->loc_stream) return DFX_OK;
-  if (const char* fp = getenv("DFX_FWD_PROBE")) c->fwd_probe = atoi(fp) != 0;
   // the side lanes run latency-bound chains of small launches beside a full-occupancy
-  // backward: give them priority so their workgroups are not queued behind its tail
+  // backward: give them priority so their workgroups are not queued behind its tail (a
+  // normal-priority side lane cost 9 % of the sharded step)
   int lo = 0, hi = 0;
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const char* lp = getenv("DFX_LOC_PRIO");  // experiment: 0 low, 1 high, else normal
-  int locp = lp ? (atoi(lp) == 0 ? lo : (atoi(lp) == 1 ? hi : 0)) : hi;
-  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, locp));
-  const char* ap = getenv("DFX_AUX_PRIO");  // experiment: 0 low, 1 high, else normal
-  int auxp = ap ? (atoi(ap) == 0 ? lo : (atoi(ap) == 1 ? hi : 0)) : hi;
-  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, auxp));
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, hi));
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
                         &c->ev_free[0], &c->ev_free[1]})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -157,6 +162,10 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->device = device;
   c->P = kw.P;
   c->loss_fm = kw.loss_fm;
+  c->fwd_probe = kw.fwd_probe;
+  c->xvp_row = kw.xvp_row;
+  c->bwd_lds = kw.bwd_lds;
+  c->autogrow = kw.autogrow;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");
@@ -215,6 +224,11 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
   table_release(c);
+  cap_release(c);
+  for (auto& st : c->staging) {
+    if (st.ev) (void)hipEventDestroy(st.ev);
+    if (st.p) (void)hipHostFree(st.p);
+  }
   if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -252,7 +266,10 @@ int dfx_sync(dfx_ctx* ctx) {
   int err = 0;
   DFX_HIP(hipMemcpyAsync(&err, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
-  if (!err) DFX_TRY(table_unclump(c));
+  if (!err) {
+    DFX_TRY(table_unclump(c));
+    DFX_TRY(store_maybe_grow(c));  // a sync point: grow once the load passes 0.5
+  }
   if (err) {
     (void)hipMemsetAsync(&c->ds->err, 0, sizeof(int), c->stream);
     (void)hipStreamSynchronize(c->stream);
@@ -262,6 +279,7 @@ int dfx_sync(dfx_ctx* ctx) {
     if (err & kErrLens) m += " CHECK_EQ(lens[i], V_dim+1) failed (sgd_updater.cc:83);";
     if (err & kErrNoV) m += " CHECK(e.V != nullptr) failed (sgd_updater.cc:84);";
     if (err & kErrSort) m += " radix sort look-back never completed;";
+    if (err & kErrBadKey) m += " key 0xffffffffffffffff is reserved (the empty-slot marker);";
     set_error(m);
     return (err & (kErrTableFull | kErrPoolFull)) ? DFX_ERR_CAPACITY : DFX_ERR_CHECK;
   }
@@ -281,9 +299,61 @@ int dfx_free(dfx_ctx* ctx, void* ptr) {
   return DFX_OK;
 }
 
+static bool is_pinned_host(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+// host -> device from pageable memory: copy into a pinned staging buffer whose previous copy
+// has run, then an async copy from it (the caller's buffer is free when this returns)
+static int staged_h2d(Context* c, void* dst, const void* src, size_t bytes) {
+  constexpr size_t kMaxStaged = 32;
+  Context::Staged* pick = nullptr;
+  for (auto& s : c->staging) {
+    if (s.bytes < bytes) continue;
+    const hipError_t q = hipEventQuery(s.ev);
+    if (q == hipErrorNotReady) continue;
+    DFX_HIP(q);
+    pick = &s;
+    break;
+  }
+  if (!pick && c->staging.size() >= kMaxStaged) {
+    // every buffer is in flight: wait for the next in turn, and grow it if it is too small
+    pick = &c->staging[c->staging_next++ % c->staging.size()];
+    DFX_HIP(hipEventSynchronize(pick->ev));
+    if (pick->bytes < bytes) {
+      DFX_HIP(hipHostFree(pick->p));
+      pick->p = nullptr;
+      pick->bytes = 0;
+    }
+  }
+  if (!pick) {
+    c->staging.emplace_back();
+    pick = &c->staging.back();
+    DFX_HIP(hipEventCreateWithFlags(&pick->ev, hipEventDisableTiming));
+  }
+  if (!pick->p) {
+    size_t want = 1 << 20;
+    while (want < bytes) want <<= 1;
+    DFX_HIP(hipHostMalloc(&pick->p, want, hipHostMallocDefault));
+    pick->bytes = want;
+  }
+  std::memcpy(pick->p, src, bytes);
+  DFX_HIP(hipMemcpyAsync(dst, pick->p, bytes, hipMemcpyHostToDevice, c->stream));
+  DFX_HIP(hipEventRecord(pick->ev, c->stream));
+  return DFX_OK;
+}
+
 int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
   DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_ARG(kind >= 0 && kind <= 2, "dfx_memcpy: kind must be 0, 1 or 2");
   if (bytes == 0) return DFX_OK;
+  DFX_CHECK_ARG(dst && src, "dfx_memcpy: null pointer");
+  if (kind == 0 && !is_pinned_host(src)) return staged_h2d(&ctx->c, dst, src, bytes);
   hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
                               : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
   DFX_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->c.stream));

@@ -200,12 +200,9 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs(const uint64_t* K, const uin
       segstart[seg] = (uint32_t)i;
       bool inserted;
       int64_t s = tbl_insert(T, K[i], &inserted);
-      if (s < 0) {
-        atomicOr(&ds->err, kErrTableFull);
-        s = 0;
-      }
+      if (s < 0) atomicOr(&ds->err, insert_error(s));
       ins = inserted;
-      segslot[seg] = (uint32_t)s;
+      segslot[seg] = s < 0 ? kNoSlot : (uint32_t)s;
     }
     if (i == R - 1) segstart[*total] = (uint32_t)R;
   }
@@ -248,11 +245,8 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
     } else {
       s = tbl_insert(T, k, &inserted);
     }
-    if (s < 0) {
-      atomicOr(&ds->err, kErrTableFull);
-      s = 0;
-    }
-    slot = (uint32_t)s;
+    if (s < 0) atomicOr(&ds->err, insert_error(s));
+    slot = s < 0 ? kNoSlot : (uint32_t)s;
     ins = inserted;  // whichever of the key's items won the insert
     if (head) {
       segstart[seg] = (uint32_t)i;
@@ -267,7 +261,8 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
   wr.y = __shfl(wr.y, leader, kWave);
   if (i < R) {
     const int d = T.d, nc = d >> 2;
-    if (!found) wr = *reinterpret_cast<const int2*>(&T.ent[slot]);  // {w, vrow}
+    if (!found)  // {w, vrow}; a key that could not be inserted reads as absent
+      wr = slot == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(&T.ent[slot]);
     const float w = __int_as_float(wr.x);
     const int vr = wr.y;
     const bool live = vr >= 0 && !(Pp.l1_shrk && w == 0.f);
@@ -289,6 +284,11 @@ __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
                               uint32_t* frank, uint32_t* fcount) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= (int64_t)*nuniq) return;
+  if (segslot[u] == kNoSlot) {  // not inserted (the error word says why): no update
+    flags[u] = 0;
+    frank[u] = 0;
+    return;
+  }
   Entry* e = &T.ent[segslot[u]];
   float4 st = ent_state(e);  // {w, sqrt_g, z, fea_cnt}
   bool has_v = e->vrow >= 0;
@@ -317,7 +317,10 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
                             DevState* ds, uint32_t* fcount) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int dnew = 0, nf = 0;
-  if (u < (int64_t)*nuniq) {
+  if (u < (int64_t)*nuniq && segslot[u] == kNoSlot) {  // not inserted: no update
+    flags[u] = 0;
+    frank[u] = 0;
+  } else if (u < (int64_t)*nuniq) {
     const int d = T.d;
     const int64_t S = rec_floats(d);
     Entry* en = &T.ent[segslot[u]];
@@ -413,9 +416,9 @@ __global__ void k_dist_pull(int64_t R, const uint32_t* seg_of, const uint32_t* s
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= R) return;
   const int d = T.d;
-  const Entry* e = &T.ent[segslot[seg_of[i]]];
-  const float w = e->w;
-  const int vr = e->vrow;
+  const uint32_t sl = segslot[seg_of[i]];
+  const float w = sl == kNoSlot ? 0.f : T.ent[sl].w;
+  const int vr = sl == kNoSlot ? -1 : T.ent[sl].vrow;
   const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
   float* o = out + i * rec_floats(d);
   const float* V = live ? row_V(T, vr) : nullptr;
@@ -435,8 +438,9 @@ __global__ __launch_bounds__(kDNT) void k_dist_pull_vec(int64_t R, const uint32_
   const int l = threadIdx.x % G;
   if (i >= R) return;
   const int d = T.d, nc = d >> 2;
-  const Entry* e = &T.ent[segslot[seg_of[i]]];
-  const int2 wr = *reinterpret_cast<const int2*>(e);  // {w, vrow}
+  const uint32_t sl = segslot[seg_of[i]];
+  const int2 wr = sl == kNoSlot ? make_int2(0, -1)
+                                : *reinterpret_cast<const int2*>(&T.ent[sl]);  // {w, vrow}
   const float w = __int_as_float(wr.x);
   const int vr = wr.y;
   const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
@@ -461,12 +465,17 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* __restri
   const int64_t u = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
   const int l = threadIdx.x % G;
   int dnew = 0, nf = 0;
-  if (u < (int64_t)*nuniq) {
+  const uint32_t sl = u < (int64_t)*nuniq ? segslot[u] : kNoSlot;
+  if (u < (int64_t)*nuniq && sl == kNoSlot) {  // not inserted: no update
+    if (l == 0) {
+      flags[u] = 0;
+      frank[u] = 0;
+    }
+  } else if (u < (int64_t)*nuniq) {
     const int d = T.d, nc = d >> 2;
     const int64_t S = rec_floats(d);
     // level 1
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
-    const uint32_t sl = segslot[u];
     // level 2
     Entry* en = &T.ent[sl];
     const float4 h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
@@ -566,8 +575,7 @@ static int owner_initv(Context* c, int slot, int nranks) {
   uint32_t* fcount = &OL.ds->totals[3];
   // gated on the device by the flag count: the scan, the sort and the draws exit at once
   // when no key asked for V (the steady state)
-  static const bool no_gate = getenv("DFX_NO_INITV_GATE") != nullptr;  // A/B switch
-  DFX_TRY(scan_u32(OL, flags, R, ftotal, nuniq, no_gate ? nullptr : fcount));
+  DFX_TRY(scan_u32(OL, flags, R, ftotal, nuniq, fcount));
   uint32_t* rk0 = ws.vals0.as<uint32_t>();
   uint32_t* rv0 = ws.vals1.as<uint32_t>();
   uint32_t* rk1 = reinterpret_cast<uint32_t*>(ws.keys0.as<uint64_t>());
@@ -704,7 +712,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   a.B = B; a.offs = b->offset; a.col = bw.col.as<uint32_t>(); a.val = b->value; a.W = pulled;
   a.rec_S = (int)S; a.Vbase = pulled; a.zpad = c->zpad; a.d = d; a.label = b->label;
   a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
-  a.xs = xvp_stride(d);
+  a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
   int nblk = 0;
   DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
@@ -727,7 +735,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
     g.occ_row = bw.occ_row.as<uint32_t>();
     g.occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = ws.p.as<float>(); g.XVp = ws.XVp.as<float>(); g.d = d;
-    g.xs = xvp_stride(d);
+    g.xs = xvp_stride(c);
     g.rec_S = (int)S; g.W = pulled; g.grad = grads_out;
     DFX_TRY(launch_bwd_positions(g, U, c->stream));
   }
@@ -744,6 +752,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_TRY(pipeline_init(c));
+  c->dist_used = true;  // slots now carry table slots across steps: no growth at sync points
   // this table serves one of nranks key ranges: hash keys by their position in the range
   DFX_TRY(table_set_ranges(c, nranks));
   const Lane OL = owner_lane(c, slot);
@@ -810,8 +819,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   c->dist_P[slot] = Pm;
   c->dist_segs_pending[slot] = true;
   // with no count push the segments are built by the pull (k_dist_segs_pull), in one pass
-  static const bool no_fuse = getenv("DFX_NO_SEGS_PULL") != nullptr;  // A/B switch
-  if (recv_cnt || vec_group(c->P.V_dim) == 0 || no_fuse) owner_segs(c, slot);
+  if (recv_cnt || vec_group(c->P.V_dim) == 0) owner_segs(c, slot);
   if (recv_cnt) {
     hipLaunchKernelGGL(k_dist_feacnt, grid, dim3(kDNT), 0, OL.stream,
                        ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),

@@ -368,6 +368,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
     float fc = 0.f;
     bool home = false;  // the key's entry was read at its home slot already
+    bool dead = false;  // the key has no slot (failed insert): nothing is written for it
     if (FUSED) {
       if (a.insert_keys) {
         // Get's find-or-insert (model_[key]) here instead of a separate pass: the home slot
@@ -389,8 +390,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
           if (l == 0) {
             bool inserted;
             const int64_t r = tbl_insert(a.T, key, &inserted);
-            if (r < 0) atomicOr(&a.dsw->err, kErrTableFull);
-            s0 = r < 0 ? 0 : (int)r;
+            if (r < 0) atomicOr(&a.dsw->err, insert_error(r));
+            s0 = r < 0 ? (int)kNoSlot : (int)r;
             nins = inserted ? 1 : 0;
           }
           s = __shfl(s0, (int)(threadIdx.x % kWave) - l, kWave);
@@ -400,7 +401,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       } else {
         sl = a.slot[cidx];
       }
-      if (!home) {
+      dead = sl == kNoSlot;
+      if (dead) {  // not in the table (the error word says why): read as absent, no update
+        h = make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
+        fc = 0.f;
+      } else if (!home) {
         const Entry* en = a.T.ent + sl;
         h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
         fc = en->fea_cnt;
@@ -487,27 +492,32 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         }
       }
     } else if (a.choff && len > (uint32_t)kChunkOcc) {
-      // a long segment: its chunks' partial sums (k_fm_bwd_chunks), combined in chunk order
+      // a long segment (a skewed key): its chunks' partial sums (k_fm_bwd_chunks), combined in
+      // chunk order, all in double and rounded once — the sums differ from the reference's
+      // sequential float sums only by that float rounding (reordering error)
       const uint32_t c0 = a.choff[u];
       const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
       const int P = d + 2;
-      float accp[CPL];
+      double gwd = 0, xxpd = 0, accp[CPL];
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) accp[k] = 0.f;
+      for (int k = 0; k < CPL; ++k) accp[k] = 0;
       for (uint32_t c = 0; c < nc; ++c) {
-        const float* pc = a.part + (int64_t)(c0 + c) * P;
-        gw += pc[0];
-        xxp += pc[1];
+        const double* pc = a.part + (int64_t)(c0 + c) * P;
+        gwd += pc[0];
+        xxpd += pc[1];
         if (vq >= 0) {
-          float q[CPL];
-          load_coords<CPL, false>(pc + 2, l, d, q);
 #pragma unroll
-          for (int k = 0; k < CPL; ++k) accp[k] += q[k];
+          for (int k = 0; k < CPL; ++k) {
+            const int cd = l * CPL + k;
+            accp[k] += cd < d ? pc[2 + cd] : 0.0;
+          }
         }
       }
+      gw = (float)gwd;
+      xxp = (float)xxpd;
       if (vq >= 0) {
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) acc[k] = (g0[k] - vcur[k] * xxp) + accp[k];
+        for (int k = 0; k < CPL; ++k) acc[k] = (float)((double)(g0[k] - vcur[k] * xxp) + accp[k]);
       }
     } else {
       for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
@@ -588,10 +598,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur);
       }
       if (l == 0) {
-        ent_set_state(a.T.ent + sl, e);
-        dnew = dw;
+        if (!dead) ent_set_state(a.T.ent + sl, e);
+        dnew = dead ? 0 : dw;
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
-        const bool need = tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
+        const bool need =
+            !dead && tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
         a.flags[u] = need ? 1u : 0u;
         ninit = need ? 1 : 0;
       }
@@ -641,9 +652,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   const bool valued = a.occ_x != nullptr;
   const int d = a.d;
   const int64_t xs = a.xs > d ? a.xs : d;
-  float gw = 0.f, xxp = 0.f, acc[CPL];
+  double gw = 0, xxp = 0, acc[CPL];
 #pragma unroll
-  for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
+  for (int k = 0; k < CPL; ++k) acc[k] = 0;
   for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
     uint32_t rw[UNR];
     float xw[UNR], pw[UNR], xr[UNR][CPL];
@@ -662,19 +673,25 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
     for (int t = 0; t < UNR; ++t) {
       if (i0 + t >= s1) continue;
       if (pw[t] != 0.f) {  // SpMV::TransTimes skips p == 0
-        gw += valued ? pw[t] * xw[t] : pw[t];
-        xxp += valued ? pw[t] * (xw[t] * xw[t]) : pw[t];
+        // each term as the reference forms it in float, summed in double
+        gw += valued ? (double)(pw[t] * xw[t]) : (double)pw[t];
+        xxp += valued ? (double)(pw[t] * (xw[t] * xw[t])) : (double)pw[t];
       }
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) acc[k] = valued ? acc[k] + xr[t][k] * xw[t] : acc[k] + xr[t][k];
+      for (int k = 0; k < CPL; ++k)
+        acc[k] += valued ? (double)(xr[t][k] * xw[t]) : (double)xr[t][k];
     }
   }
-  float* pc = a.part + ch * (d + 2);
+  double* pc = a.part + ch * (d + 2);
   if (l == 0) {
     pc[0] = gw;
     pc[1] = xxp;
   }
-  if (d > 0) store_coords<CPL, false>(pc + 2, l, d, acc);
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int cd = l * CPL + k;
+    if (cd < d) pc[2 + cd] = acc[k];
+  }
 }
 
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
@@ -700,16 +717,13 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
 // block caps it at 5 blocks (20 waves) per CU, so the Localizer and AUC lanes' blocks always
 // find slots beside it — their look-back chains then do not stall behind it.  Same-box A/B:
 // +3 % step throughput, the backward itself unchanged (5 waves / SIMD already saturate its
-// random-line traffic).  DFX_BWD_LDS overrides (bytes, 0 = no cap).
+// random-line traffic).  The context kwarg bwd_lds overrides (bytes, 0 = no cap).
 constexpr size_t kBwdLdsCap = 32768;
-static size_t bwd_lds(bool fused) {
-  static const long e = getenv("DFX_BWD_LDS") ? atol(getenv("DFX_BWD_LDS")) : -1;
-  if (e >= 0) return (size_t)e;
-  return fused ? kBwdLdsCap : 0;
-}
 
 template <bool FUSED>
-int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligned = FUSED) {
+int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligned = FUSED,
+               long lds = -1) {
+  const size_t lds_bytes = lds >= 0 ? (size_t)lds : (FUSED ? kBwdLdsCap : 0);
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;
   bool vec;
@@ -718,8 +732,7 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   dim3 grid((unsigned)((nseg_bound + spb - 1) / spb));
 #define DFX_BWD(GG, CC, VV)                                                              \
   if (G == GG && CPL == CC && vec == VV) {                                               \
-    hipLaunchKernelGGL((k_fm_bwd<GG, CC, FUSED, VV>), grid, dim3(kFmNT), bwd_lds(FUSED), st, \
-                       a);                                                                   \
+    hipLaunchKernelGGL((k_fm_bwd<GG, CC, FUSED, VV>), grid, dim3(kFmNT), lds_bytes, st, a);  \
     DFX_HIP(hipGetLastError());                                                          \
     return DFX_OK;                                                                       \
   }
@@ -730,8 +743,8 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   return DFX_ERR_ARG;
 }
 
-int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st) {
-  return launch_bwd<true>(a, nseg_bound, st);
+int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds) {
+  return launch_bwd<true>(a, nseg_bound, st, true, lds);
 }
 
 // sharded store: per-key gradient records in the pulled-record layout (aligned rows)
@@ -833,6 +846,9 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   DFX_TRY(ws.occ_row.ensure(nnz * 4));
   DFX_TRY(ws.occ_x.ensure(nnz * 4));
   DFX_TRY(ws.cnt.ensure(4 * 4));
+  DFX_TRY(ws.col.ensure((nnz + 1) * 4));                                      // chunk offsets
+  DFX_TRY(ws.vpos.ensure((nnz / kChunkOcc + 2) * 4));                         // chunk -> segment
+  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (V_dim + 2) * 8));    // chunk partials
   // 1) p and XV*p per row
   FwdArgs a{};
   a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
@@ -857,7 +873,15 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
                      ws.segstart.as<uint32_t>(), ws.slot.as<uint32_t>(), total,
                      ws.rowid.as<uint32_t>(), value, ws.occ_row.as<uint32_t>(),
                      ws.occ_x.as<float>());
-  // 3) segmented reduction into grad
+  // 3) long segments (skewed keys) in chunks, combined in double (as in the fused step)
+  DFX_HIP(hipMemcpyAsync(&c->ds->u_count, total, sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                         c->stream));
+  DFX_HIP(hipMemsetAsync(&c->ds->n_init, 0, sizeof(uint32_t), c->stream));
+  uint32_t* choff = ws.col.as<uint32_t>();
+  uint32_t* chunk_seg = ws.vpos.as<uint32_t>();
+  uint32_t* nchunks = total + 1;
+  DFX_TRY(chunk_plan(main_lane(c), nnz, ws.segstart.as<uint32_t>(), choff, chunk_seg, nchunks));
+  // 4) segmented reduction into grad
   BwdArgs b{};
   b.segstart = ws.segstart.as<uint32_t>();
   b.ds = c->ds;
@@ -868,10 +892,13 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   b.zpad = c->zpad;
   b.p = ws.p.as<float>(); b.XVp = ws.XVp.as<float>(); b.d = V_dim;
   b.wpos = w_pos; b.vpos = V_pos; b.W = weights; b.grad = grad;
-  // the number of segments is device-side; store it where k_fm_bwd reads it
-  DFX_HIP(hipMemcpyAsync(&c->ds->u_count, total, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                         c->stream));
-  return launch_bwd<false>(b, nnz, c->stream);
+  b.choff = choff; b.chunk_seg = chunk_seg; b.nchunks = nchunks; b.part = ws.Vb.as<double>();
+  // the number of segments is device-side (ds->u_count, set above), where k_fm_bwd reads it
+  DFX_TRY(launch_bwd_chunks(b, nnz / kChunkOcc + 1, c->stream));
+  DFX_TRY(launch_bwd<false>(b, nnz, c->stream));
+  // n_init served as the chunk plan's gate; it counts the fused step's InitV requests
+  DFX_HIP(hipMemsetAsync(&c->ds->n_init, 0, sizeof(uint32_t), c->stream));
+  return DFX_OK;
 }
 
 __global__ void k_get_pos(int64_t n, const int32_t* lens, const uint32_t* excl, int32_t* w_pos,

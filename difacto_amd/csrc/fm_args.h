@@ -72,19 +72,20 @@ struct BwdArgs {
   uint32_t* flags;  // InitV request per key
   DevState* dsw;
   // long segments (chunk_plan): first chunk of each segment, segment of each chunk, the
-  // chunk count (device) and the chunks' partials [g_w, XXp, sum (XV p) x (d)]
+  // chunk count (device) and the chunks' partials [g_w, XXp, sum (XV p) x (d)] in double
   const uint32_t* choff;
   const uint32_t* chunk_seg;
   const uint32_t* nchunks;
-  float* part;
+  double* part;
 };
 
 // the XVp row stride the workspace is sized for (step.hip): p rides in each row
-int xvp_stride(int d);
+int xvp_stride(const Context* c);
 // fused forward; *nblk receives the number of loss partials written
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk);
-// fused backward + FTRL/AdaGrad update over at most nseg_bound segments
-int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st);
+// fused backward + FTRL/AdaGrad update over at most nseg_bound segments; lds: bytes of LDS
+// reserved per block (-1: the default cap)
+int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds = -1);
 // the chunk partials of long segments (before the backward reads them)
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st);
 

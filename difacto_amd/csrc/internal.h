@@ -104,6 +104,21 @@ struct Workspace {
 
 struct Context;
 
+// Growth without a stall per step: every step records a D2H copy of {n_keys, n_vrows} and an
+// event; a new step's inserts are bounded by its nnz, so the host knows an upper bound of the
+// counts when it enqueues, from the latest completed record plus the bounds enqueued since.
+// Only when that bound nears capacity does it wait — first for older records, at last for the
+// stream — and grow at that sync point (cap_check).
+constexpr int kCapRing = 8;
+struct CapGuard {
+  hipEvent_t ev[kCapRing] = {};
+  unsigned long long* host = nullptr;  // pinned: {n_keys, n_vrows} per ring entry
+  int64_t enq_at[kCapRing] = {};       // enqueued-insert total when the entry was recorded
+  int head = 0, count = 0;
+  int64_t enq_total = 0;               // upper bound of inserts enqueued so far
+  int64_t known_keys = 0, known_vrows = 0, known_enq = 0;
+};
+
 // A lane = a stream with its own scratch and its own small device state (U of its batch, sort
 // plan and look-back epoch), so work on two lanes never shares a buffer.  The main lane is the
 // context's stream + ws + ds; the fused step adds a Localizer lane per batch parity and an AUC
@@ -160,8 +175,24 @@ struct Context {
   hipEvent_t ev_loc[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
   int parity = 0;
   // the fused forward finds every nnz's key in the table (no Localizer col scatter, no pulled
-  // {w, vrow} per key); 0: col + pulled (DFX_FWD_PROBE=0)
+  // {w, vrow} per key); 0: col + pulled (kwarg fwd_probe=0)
   int fwd_probe = 1;
+  int xvp_row = 1;    // p rides in the XV*p rows (kwarg xvp_row)
+  long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
+  int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
+  // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
+  // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
+  CapGuard capg;
+  // pinned staging of host->device copies from pageable memory (dfx_memcpy): a buffer is
+  // reused once the copy that read it has run (its event)
+  struct Staged {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+  };
+  std::vector<Staged> staging;
+  size_t staging_next = 0;
+  bool dist_used = false;  // a key-range server: its slots hold table slots across steps
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }
@@ -255,6 +286,14 @@ int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
                      const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,
                      const DevState* nds);
 int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows);
+// before enqueueing work that inserts at most `add` keys (and draws at most `add` V rows):
+// make sure the table stays below 0.9 load and the V pool cannot overflow, growing at a sync
+// point when needed (kwarg autogrow=0: no-op).  cap_record after that work is enqueued.
+int cap_check(Context* c, int64_t add);
+int cap_record(Context* c);
+void cap_release(Context* c);
+// at a sync point (the stream is idle): grow the table once its load passes 0.5
+int store_maybe_grow(Context* c);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev);

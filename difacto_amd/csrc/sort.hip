@@ -321,21 +321,9 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
                      begin_bit, end_bit, sortmeta, parts, counts, epoch);
-  static const int it = getenv("DFX_OS_ITEMS") ? atoi(getenv("DFX_OS_ITEMS")) : kOsItems;
-  for (int q = 0; q < npasses; ++q) {
-    if (it == 8) {
-      hipLaunchKernelGGL((k_os_scatter<K, P, 8>), dim3((unsigned)((n + 2047) / 2048)),
-                         dim3(kOsNT), 0, L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts,
-                         status, L.err);
-    } else if (it == 12) {
-      hipLaunchKernelGGL((k_os_scatter<K, P, 12>), dim3((unsigned)((n + 3071) / 3072)),
-                         dim3(kOsNT), 0, L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts,
-                         status, L.err);
-    } else {
-      hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems>), dim3((unsigned)ntiles), dim3(kOsNT), 0,
-                         L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
-    }
-  }
+  for (int q = 0; q < npasses; ++q)
+    hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems>), dim3((unsigned)ntiles), dim3(kOsNT), 0,
+                       L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -24,10 +24,10 @@ namespace dfx {
 
 // Row stride of the fused step's XV_*p rows: a multiple of 32 floats (128 B) carrying p after
 // XV_*p, so the backward's per-occurrence p and XV_*p sit in one 128-byte line (+3 % of the
-// step at d = 16, same-box A/B).  DFX_XVP_ROW=0 (A/B switch): rows of d floats, p apart.
-int xvp_stride(int d) {
-  static const bool on = !getenv("DFX_XVP_ROW") || atoi(getenv("DFX_XVP_ROW")) != 0;
-  return (on && d > 0) ? (d + 1 + 31) / 32 * 32 : d;
+// step at d = 16, same-box A/B).  Context kwarg xvp_row=0: rows of d floats, p apart.
+int xvp_stride(const Context* c) {
+  const int d = c->P.V_dim;
+  return (c->xvp_row && d > 0) ? (d + 1 + 31) / 32 * 32 : d;
 }
 
 // main lane: per-row arrays of the forward / backward and the InitV scan
@@ -40,10 +40,10 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
   DFX_TRY(ws.p.ensure(rows * 4));
   DFX_TRY(ws.pred.ensure(rows * 4));
-  if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * xvp_stride(d) * 4));
+  if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * xvp_stride(c) * 4));
   DFX_TRY(ws.dscratch.ensure((rows / 4 + 64) * 8));
   DFX_TRY(ws.wv.ensure(nnz * 8));
-  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 4));  // chunk partials
+  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 8));  // chunk partials (f64)
   ws.rows = rows;
   ws.nnz = nnz;
   return DFX_OK;
@@ -129,14 +129,15 @@ __global__ __launch_bounds__(kProbeNT) void k_probe_keys(const uint64_t* __restr
     if (kk[v] != key[v]) {
       bool inserted;
       s = tbl_insert(T, key[v], &inserted);
-      if (s < 0) {
-        atomicOr(&ds->err, kErrTableFull);
-        s = 0;
-      }
       ins += inserted ? 1 : 0;
-      wr[v] = *reinterpret_cast<const int2*>(T.ent + s);
+      if (s < 0) {  // the key reads as absent and is never updated (kNoSlot)
+        atomicOr(&ds->err, insert_error(s));
+        wr[v] = make_int2(0, -1);
+      } else {
+        wr[v] = *reinterpret_cast<const int2*>(T.ent + s);
+      }
     }
-    segslot[u] = (uint32_t)s;
+    segslot[u] = s < 0 ? kNoSlot : (uint32_t)s;
     if (pulled) pulled[u] = wr[v];
   }
   for (int off = 32; off > 0; off >>= 1) ins += __shfl_xor(ins, off, kWave);
@@ -154,7 +155,9 @@ __global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ 
                                                    const DevState* nds, const Entry* ent,
                                                    int2* __restrict__ pulled) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (u < (int64_t)nds->u_count) pulled[u] = *reinterpret_cast<const int2*>(ent + segslot[u]);
+  if (u >= (int64_t)nds->u_count) return;
+  const uint32_t s = segslot[u];
+  pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent + s);
 }
 
 __global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B) {
@@ -184,6 +187,9 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   const int64_t B = b->size, nnz = b->nnz;
   const int d = c->P.V_dim;
   DFX_TRY(step_reserve(c, B, nnz));
+  // this step inserts at most nnz keys and draws at most nnz V rows: grow the store first if
+  // they might not fit (at a sync point; in the steady state the check costs no wait)
+  DFX_TRY(cap_check(c, nnz));
   Workspace& ws = c->ws;
   const int k = c->parity;
   c->parity ^= 1;
@@ -258,7 +264,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
-  a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(d);
+  a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk));
@@ -281,13 +287,13 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     BwdArgs g{};
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
-    g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(d); g.d = d; g.slot = segslot;
+    g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
     g.T = c->T; g.Pm = c->P;
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
-    g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<float>();
+    g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
     DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
-    DFX_TRY(launch_bwd_fused(g, nnz, c->stream));
+    DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     prof_mark(c, 6);
     DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init));
   } else {
@@ -295,6 +301,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   }
   hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, bds, B);
   DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
+  DFX_TRY(cap_record(c));
   prof_mark(c, 7);
   if (c->prof_n < c->prof_max) ++c->prof_n;
   DFX_HIP(hipGetLastError());

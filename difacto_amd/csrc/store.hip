@@ -12,6 +12,8 @@
 // InitV (sgd_updater.cc:144-152) draws glibc rand_r in key order; on the GPU every key that
 // needs V gets its exclusive-scan rank r among this push's InitV keys and jumps the LCG by
 // 3*V_dim*r steps, which reproduces the reference's sequential draws exactly.
+#include <algorithm>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(kStNT) void k_push_cnt(int64_t n, const uint64_t* k
     ins = inserted;
     uint32_t f = 0;
     if (s < 0) {
-      atomicOr(&ds->err, kErrTableFull);
+      atomicOr(&ds->err, insert_error(s));
     } else {
       f = feacnt_apply(T, P, s, cnt[u]);
       slot[u] = (uint32_t)s;
@@ -137,7 +139,8 @@ __global__ __launch_bounds__(kStNT) void k_push_cnt_seg(const uint32_t* segstart
   const int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   if (u >= (int64_t)ds->u_count) return;
   const float c = (float)(segstart[u + 1] - segstart[u]);
-  flags[u] = feacnt_apply(T, P, segslot[u], c);
+  const uint32_t s = segslot[u];
+  flags[u] = s == kNoSlot ? 0u : feacnt_apply(T, P, s, c);
 }
 
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
@@ -155,9 +158,10 @@ int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
 // Missing keys read as w = 0 without V; Get's insertion of empty entries is not observable.
 __global__ __launch_bounds__(kStNT) void k_pull_lens(int64_t n, const uint64_t* keys, Table T,
                                                      Params P, int32_t* slot_out,
-                                                     uint32_t* len_out) {
+                                                     uint32_t* len_out, DevState* ds) {
   const int64_t i = (int64_t)blockIdx.x * kStNT + threadIdx.x;
   if (i >= n) return;
+  if (keys[i] == kEmptyKey) atomicOr(&ds->err, kErrBadKey);  // reported at the next sync
   int64_t s = tbl_find(T, keys[i]);
   int vr = -1;
   float w = 0.f;
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* 
     ins = inserted;
     uint32_t f = 0;
     if (s < 0) {
-      atomicOr(&ds->err, kErrTableFull);
+      atomicOr(&ds->err, insert_error(s));
     } else {
       const int d = T.d;
       const uint32_t o = lens ? off[i] : (uint32_t)i;
@@ -275,6 +279,32 @@ static int table_alloc_entries(Table* T, int64_t cap, hipStream_t st) {
   return DFX_OK;
 }
 
+// Rebuild the table as NT (new hash parameters and/or capacity): every entry of the old
+// table is re-inserted.  The old table is freed only once every entry landed; on a failure
+// (a full new table) the old one stays and the error is returned.
+static int table_rebuild(Context* c, Table NT, int64_t new_cap) {
+  Table& T = c->T;
+  DFX_TRY(table_alloc_entries(&NT, new_cap, c->stream));
+  int err0 = 0, err1 = 0;
+  DFX_HIP(hipMemcpyAsync(&err0, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
+                     c->cap, NT, c->ds);
+  DFX_HIP(hipGetLastError());
+  DFX_HIP(hipMemcpyAsync(&err1, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  if ((err1 & ~err0) & kErrTableFull) {
+    (void)hipFree(NT.ent);
+    DFX_HIP(hipMemcpy(&c->ds->err, &err0, sizeof(int), hipMemcpyHostToDevice));
+    set_error("table rebuild: the new table cannot hold every key; the old table is kept");
+    return DFX_ERR_CAPACITY;
+  }
+  (void)hipFree(T.ent);
+  T = NT;
+  c->cap = new_cap;
+  return DFX_OK;
+}
+
 int table_unclump(Context* c) {
   Table& T = c->T;
   if (!T.ent) return DFX_OK;
@@ -288,14 +318,7 @@ int table_unclump(Context* c) {
   // the keys cluster in their top bits: rebuild with the multiplicative hash (same capacity)
   Table NT = T;
   NT.ordered = 0;
-  DFX_TRY(table_alloc_entries(&NT, c->cap, c->stream));
-  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
-                     c->cap, NT, c->ds);
-  DFX_HIP(hipStreamSynchronize(c->stream));
-  (void)hipFree(T.ent);
-  T.ent = NT.ent;
-  T.ordered = 0;
-  return DFX_OK;
+  return table_rebuild(c, NT, c->cap);
 }
 
 // A key-range server's table (dist.hip): the ordered hash over the position of a key inside
@@ -313,14 +336,7 @@ int table_set_ranges(Context* c, int nranks) {
   }
   Table NT = T;
   NT.range_mul = mul;
-  DFX_TRY(table_alloc_entries(&NT, c->cap, c->stream));
-  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
-                     c->cap, NT, c->ds);
-  DFX_HIP(hipStreamSynchronize(c->stream));
-  (void)hipFree(T.ent);
-  T.ent = NT.ent;
-  T.range_mul = mul;
-  return DFX_OK;
+  return table_rebuild(c, NT, c->cap);
 }
 
 int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
@@ -368,14 +384,7 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
   if (2 * n_keys > c->cap) {
     int64_t cap = c->cap;
     while (cap < 2 * n_keys) cap <<= 1;
-    Table NT = T;
-    DFX_TRY(table_alloc_entries(&NT, cap, c->stream));
-    hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
-                       c->cap, NT, c->ds);
-    DFX_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(T.ent);
-    T.ent = NT.ent; T.mask = NT.mask; T.logcap = NT.logcap;
-    c->cap = cap;
+    DFX_TRY(table_rebuild(c, T, cap));
   }
   if (T.d > 0 && n_vrows > T.vcap) {
     HostCounters h;
@@ -392,6 +401,113 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
   return DFX_OK;
 }
 
+// ---- automatic growth ---------------------------------------------------------------------
+// consume the oldest recorded counts (wait: block for them; else only when complete)
+static int cap_pop_oldest(Context* c, bool wait, bool* popped) {
+  CapGuard& g = c->capg;
+  *popped = false;
+  if (g.count == 0) return DFX_OK;
+  const int i = (g.head - g.count + kCapRing) % kCapRing;
+  if (wait) {
+    DFX_HIP(hipEventSynchronize(g.ev[i]));
+  } else {
+    const hipError_t q = hipEventQuery(g.ev[i]);
+    if (q == hipErrorNotReady) return DFX_OK;
+    DFX_HIP(q);
+  }
+  g.known_keys = (int64_t)g.host[2 * i];
+  g.known_vrows = (int64_t)g.host[2 * i + 1];
+  g.known_enq = g.enq_at[i];
+  --g.count;
+  *popped = true;
+  return DFX_OK;
+}
+
+int cap_record(Context* c) {
+  if (!c->autogrow) return DFX_OK;
+  CapGuard& g = c->capg;
+  if (!g.host) {
+    DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&g.host), 2 * kCapRing * 8,
+                          hipHostMallocDefault));
+    for (auto& e : g.ev) DFX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  bool popped;
+  if (g.count == kCapRing) DFX_TRY(cap_pop_oldest(c, true, &popped));
+  const int i = g.head;
+  static_assert(offsetof(DevState, n_vrows) == offsetof(DevState, n_keys) + 8, "layout");
+  DFX_HIP(hipMemcpyAsync(g.host + 2 * i, &c->ds->n_keys, 16, hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipEventRecord(g.ev[i], c->stream));
+  g.enq_at[i] = g.enq_total;
+  g.head = (g.head + 1) % kCapRing;
+  ++g.count;
+  return DFX_OK;
+}
+
+void cap_release(Context* c) {
+  CapGuard& g = c->capg;
+  for (auto& e : g.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g.host) (void)hipHostFree(g.host);
+  g = CapGuard{};
+}
+
+// table capacity >= 2 * need_keys, V pool >= need_vrows (doubling at least)
+static int grow_to(Context* c, int64_t need_keys, int64_t need_vrows) {
+  const Table& T = c->T;
+  const bool gk = 2 * need_keys > c->cap;
+  const bool gv = T.d > 0 && need_vrows > T.vcap;
+  if (!gk && !gv) return DFX_OK;
+  return store_reserve(c, gk ? need_keys : 0, gv ? std::max<int64_t>(2 * T.vcap, need_vrows) : 0);
+}
+
+int cap_check(Context* c, int64_t add) {
+  if (!c->autogrow || !c->T.ent) return DFX_OK;
+  CapGuard& g = c->capg;
+  bool popped = true;
+  while (popped) DFX_TRY(cap_pop_oldest(c, false, &popped));
+  const bool has_v = c->T.d > 0;
+  for (;;) {
+    const int64_t pend = g.enq_total - g.known_enq + add;
+    const bool keys_ok = 10 * (g.known_keys + pend) <= 9 * c->cap;
+    const bool vrows_ok = !has_v || g.known_vrows + pend <= c->T.vcap;
+    if (keys_ok && vrows_ok) break;
+    if (g.count > 0) {  // an older step's counts may show room: wait for it, not the stream
+      DFX_TRY(cap_pop_oldest(c, true, &popped));
+      continue;
+    }
+    // exact counts at a sync point; grow so that this step fits below 0.9 load
+    DFX_HIP(hipStreamSynchronize(c->stream));
+    HostCounters h;
+    DFX_TRY(read_counters(c, &h));
+    g.known_keys = (int64_t)h.n_keys;
+    g.known_vrows = (int64_t)h.n_vrows;
+    g.known_enq = g.enq_total;
+    const int64_t need = g.known_keys + add;
+    const int64_t need_cap_keys = (10 * need + 8) / 9;  // 0.9 load after this step
+    DFX_TRY(grow_to(c, std::max<int64_t>(need_cap_keys / 2 + 1,
+                                         2 * g.known_keys > c->cap ? g.known_keys : 0),
+                    has_v ? g.known_vrows + add : 0));
+    break;
+  }
+  g.enq_total += add;
+  return DFX_OK;
+}
+
+int store_maybe_grow(Context* c) {
+  if (!c->T.ent) return DFX_OK;
+  HostCounters h;
+  DFX_TRY(read_counters(c, &h));
+  if (c->autogrow && !c->dist_used && 2 * (int64_t)h.n_keys > c->cap)
+    DFX_TRY(grow_to(c, (int64_t)h.n_keys, 0));
+  // the stream is idle: every recorded count is complete, and the exact ones are at hand
+  CapGuard& g = c->capg;
+  g.count = 0;
+  g.known_keys = (int64_t)h.n_keys;
+  g.known_vrows = (int64_t)h.n_vrows;
+  g.known_enq = g.enq_total;
+  return DFX_OK;
+}
+
 // load: host-parsed entries uploaded and inserted (SGDEntry::LoadEntry keeps fea_cnt, and
 // keeps sqrt_g/z when the file has no aux data)
 __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const int32_t* vr,
@@ -403,7 +519,7 @@ __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const 
     int64_t s = tbl_insert(T, keys[i], &inserted);
     ins = inserted;
     if (s < 0) {
-      atomicOr(&ds->err, kErrTableFull);
+      atomicOr(&ds->err, insert_error(s));
     } else {
       Entry* en = &T.ent[s];
       float4 e = ent_state(en);
@@ -488,7 +604,8 @@ int dfx_store_pull(dfx_ctx* ctx, const uint64_t* keys, int64_t n, float* vals, i
   int32_t* sl = ws.slot.as<int32_t>();
   uint32_t* total = ws.cnt.as<uint32_t>();
   dim3 grid((n + kStNT - 1) / kStNT);
-  hipLaunchKernelGGL(k_pull_lens, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, c->P, sl, off);
+  hipLaunchKernelGGL(k_pull_lens, grid, dim3(kStNT), 0, c->stream, n, keys, c->T, c->P, sl, off,
+                     c->ds);
   DFX_TRY(scan_u32(c, off, n, total));
   hipLaunchKernelGGL(k_pull_write, grid, dim3(kStNT), 0, c->stream, n, c->T, c->P, sl, off, vals,
                      d > 0 ? lens : nullptr);
@@ -502,6 +619,9 @@ int dfx_store_pull(dfx_ctx* ctx, const uint64_t* keys, int64_t n, float* vals, i
   return DFX_OK;
 }
 
+static int store_push(Context* c, const uint64_t* keys, int64_t n, int type, const float* vals,
+                      int64_t n_vals, const int32_t* lens);
+
 int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, const float* vals,
                    int64_t n_vals, const int32_t* lens) {
   DFX_CHECK_ARG(ctx, "null ctx");
@@ -509,6 +629,13 @@ int dfx_store_push(dfx_ctx* ctx, const uint64_t* keys, int64_t n, int type, cons
   DFX_CHECK_ARG(n >= 0, "push: negative n");
   if (n == 0) return DFX_OK;
   DFX_CHECK_ARG(keys && vals, "push: null buffer");
+  DFX_TRY(cap_check(c, n));
+  DFX_TRY(store_push(c, keys, n, type, vals, n_vals, lens));
+  return cap_record(c);
+}
+
+static int store_push(Context* c, const uint64_t* keys, int64_t n, int type, const float* vals,
+                      int64_t n_vals, const int32_t* lens) {
   Workspace& ws = c->ws;
   DFX_TRY(ws.flags.ensure((n + 1) * 4));
   DFX_TRY(ws.slot.ensure((n + 1) * 4));
@@ -682,6 +809,11 @@ int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks) {
         fclose(f); set_error("truncated model file"); return DFX_ERR_IO;
       }
       row = (int32_t)vnext++;
+    }
+    if (key == kEmptyKey) {
+      fclose(f);
+      set_error("model file holds key 0xffffffffffffffff, reserved as the empty-slot marker");
+      return DFX_ERR_ARG;
     }
     if ((int)(((unsigned __int128)key * (unsigned)nranks) >> 64) != rank) {
       if (row >= 0) {  // not ours: drop its V row again

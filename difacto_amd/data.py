@@ -104,11 +104,30 @@ def synthetic(rows, nnz_per_row, key_space, binary=True, pos_frac=0.25, seed=42,
     return RowBlock(offs, ids, vals, labels)
 
 
+_ZIPF_CDF = {}
+
+
 def zipf_keys(rng, n, s, key_space):
-    """Zipf(s) over ranks 1..key_space by inverse-CDF on a truncated table."""
-    m = int(min(key_space, 1 << 22))
-    ranks = np.arange(1, m + 1, dtype=np.float64)
-    cdf = np.cumsum(ranks ** (-s))
-    cdf /= cdf[-1]
-    u = rng.random(n)
-    return (np.searchsorted(cdf, u) + 1).astype(np.uint64)
+    """Zipf(s) over ranks 1..key_space by inverse CDF.  The CDF table is exact up to 2^25
+    ranks (C5: Zipf(1.1) over [1, 2^24] uses the whole table); beyond that the tail's mass is
+    the continuous power-law integral and tail ranks are drawn by inverting it."""
+    m = int(min(key_space, 1 << 25))
+    key = (m, s)
+    if key not in _ZIPF_CDF:
+        ranks = np.arange(1, m + 1, dtype=np.float64)
+        _ZIPF_CDF[key] = np.cumsum(ranks ** (-s))
+    head = _ZIPF_CDF[key]
+    tail = 0.0
+    if key_space > m:  # integral of x^-s over [m + 1/2, key_space + 1/2]
+        a, b = m + 0.5, key_space + 0.5
+        tail = (a ** (1 - s) - b ** (1 - s)) / (s - 1)
+    total = head[-1] + tail
+    u = rng.random(n) * total
+    out = (np.searchsorted(head, u) + 1).astype(np.uint64)
+    t = u > head[-1]
+    if np.any(t):  # invert the tail integral
+        a = m + 0.5
+        r = a ** (1 - s) - (u[t] - head[-1]) * (s - 1)
+        x = np.floor(r ** (1.0 / (1 - s)) + 0.5)
+        out[t] = np.clip(x, m + 1, key_space).astype(np.uint64)
+    return out

@@ -97,7 +97,10 @@ int dfx_ctx_vdim(dfx_ctx* ctx);
 int dfx_sync(dfx_ctx* ctx); /* waits for the stream and reports deferred device errors */
 int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes);
 int dfx_free(dfx_ctx* ctx, void* ptr);
-/* kind: 0 host->device, 1 device->host, 2 device->device; async on the stream */
+/* kind: 0 host->device, 1 device->host, 2 device->device; async on the stream.  Host->device
+ * from pageable memory goes through the context's pinned staging pool, so the caller may reuse
+ * src as soon as the call returns (HIP may read a pageable source only when the copy reaches
+ * the head of a busy stream).  Device->host returns once the data are on the host. */
 int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
 /* pre-size the fused-path workspace so dfx_train_step allocates nothing (graph capture) */
 int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz);

@@ -4,7 +4,9 @@ Every expected value below is read from tests/golden/reference_known_answers.jso
 transcribes the reference's gtest assertions (file:line in that JSON).
 """
 import numpy as np
+import pytest
 
+from difacto_amd import data as D
 from oracle import oracle as O
 
 
@@ -117,3 +119,32 @@ def test_auc_tie_convention_agrees_without_ties():
         pred = rng.permutation(np.linspace(-3, 3, n)).astype(np.float32)
         assert not O.has_ties(pred)
         assert abs(O.auc_stable_ties(label, pred) - O.auc(label, pred)) <= 1e-4 * n
+
+
+@pytest.mark.parametrize("nt", [1, 3, 8])
+def test_cpu_ref_matches_oracle(nt):
+    """oracle/cpu_ref.cc (the CPU baseline: the reference's threading) computes what the pinned
+    restatement computes: predictions bitwise for any thread count (row- and column-range
+    splits keep every sum's order), the same model size and rand_r state, loss within 1e-4 (the
+    reference sums Evaluate as a float reduction), AUC*n equal; also through the two-thread
+    IterateData pipeline"""
+    from oracle import cpu_ref as C
+    cfg = dict(V_dim=8, V_threshold=2, l1=0.5, lr=.1, V_lr=.05)
+    up = O.Updater(**cfg)
+    ref = C.CpuRef(nt, **cfg)
+    for s in range(4):
+        blk = D.synthetic(1500, 20, 1 << 12, seed=80 + s, binary=(s % 2 == 0), ragged=(s == 3))
+        l1, a1, p1 = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels, push_cnt=s < 2,
+                                   want_pred=True)
+        l2, a2, p2 = ref.step(blk, push_cnt=s < 2, want_pred=True)
+        assert np.array_equal(p1, p2), s
+        assert abs(l1 - l2) <= 1e-4 * abs(l1) and (a1 == a2 or O.has_ties(p1)), s
+    assert up.size() == ref.size() and up.seed == ref.seed
+    blocks = [D.synthetic(800, 20, 1 << 12, seed=90 + s) for s in range(5)]
+    tot = 0.0
+    for b in blocks:
+        tot += up.train_step(b.offs, b.ids, b.vals, b.labels)[0]
+    dt, loss, _, n = ref.iterate(blocks)
+    assert n == 4000 and dt > 0 and abs(loss - tot) <= 1e-4 * abs(tot)
+    assert up.size() == ref.size() and up.seed == ref.seed
+    ref.close()
