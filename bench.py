@@ -48,6 +48,11 @@ def parse():
     ap.add_argument("--sync", action="store_true",
                     help="sharded store: bulk-synchronous steps instead of the pipelined "
                          "(1-step-stale) schedule")
+    ap.add_argument("--push-agg", default="sum", choices=("sum", "ranks"),
+                    help="sharded store: sum = one Update per key per step on the workers' "
+                         "summed gradients (SURVEY §8(e): a step is one reference step over "
+                         "the concatenated batches); ranks = one Update per pushing worker "
+                         "(KVStoreDist HandlePush)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="sharded store transport; gloo (staged through host memory) runs "
                          "several ranks on one GPU, for tests")
@@ -345,7 +350,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     # of the key space, so its table runs at the single-GPU bench's load factor (~0.5);
     # max_vrows (a hard bound) has headroom for an uneven share
     ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
-                    max_keys=max(keyspace // world, 1), max_vrows=per)
+                    max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg)
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo")
 
@@ -484,9 +489,10 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         "data": "synthetic (device-generated, resident in HBM before timing)",
         "config": {"workload": "C3 Criteo-shaped FM V_dim=%d, %d binary nnz/row, 2^%d keys, "
                                "l1=0 V_threshold=0, key-range-sharded store over %d GPUs "
-                               "(RCCL all-to-all-v), %s schedule"
+                               "(RCCL all-to-all-v), %s schedule, push_agg=%s"
                                % (d, k, kb, world,
-                                  "bulk-synchronous" if args.sync else "pipelined 1-step-stale"),
+                                  "bulk-synchronous" if args.sync else "pipelined 1-step-stale",
+                                  args.push_agg),
                    "rows_per_gpu_step": B, "global_batch": B * world,
                    "parallelism": "dp%d + model sharded by key range" % world},
         "roofline": {"bound": "hbm", "kernel": "fwd_bwd (dist forward+AUC+backward, rank 0)",

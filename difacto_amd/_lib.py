@@ -97,6 +97,9 @@ _SIGS = {
     "dfx_dist_fwd_bwd": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp,
                                         ctypes.c_int, vp, vp]),
     "dfx_dist_owner_push": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_dist_initv_local": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_dist_initv_draw": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int]),
+    "dfx_dist_push_agg_sum": (ctypes.c_int, [vp]),
 }
 
 EXPORTED = tuple(_SIGS)

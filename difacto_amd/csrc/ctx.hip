@@ -51,6 +51,7 @@ struct Kw {
   int xvp_row = 1;      // xvp_row=0: XV*p rows of d floats, p in its own array
   long bwd_lds = -1;    // bwd_lds=<bytes>: LDS reserved per backward block (-1: default cap)
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
+  int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -85,6 +86,11 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "xvp_row") kw->xvp_row = atoi(cv) != 0;
     else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
     else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;
+    else if (k == "push_agg") {
+      if (v == "sum") kw->dist_sum = 1;
+      else if (v == "ranks") kw->dist_sum = 0;
+      else { set_error("unknown push_agg: " + v + " (sum|ranks)"); return DFX_ERR_ARG; }
+    }
     else if (k == "hash") {
       if (v == "ordered") kw->ordered = 1;
       else if (v == "mixed") kw->ordered = 0;
@@ -166,6 +172,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->xvp_row = kw.xvp_row;
   c->bwd_lds = kw.bwd_lds;
   c->autogrow = kw.autogrow;
+  c->dist_sum = kw.dist_sum;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");
@@ -225,10 +232,6 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
   table_release(c);
   cap_release(c);
-  for (auto& st : c->staging) {
-    if (st.ev) (void)hipEventDestroy(st.ev);
-    if (st.p) (void)hipHostFree(st.p);
-  }
   if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -299,61 +302,11 @@ int dfx_free(dfx_ctx* ctx, void* ptr) {
   return DFX_OK;
 }
 
-static bool is_pinned_host(const void* p) {
-  hipPointerAttribute_t at;
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return at.type == hipMemoryTypeHost;
-}
-
-// host -> device from pageable memory: copy into a pinned staging buffer whose previous copy
-// has run, then an async copy from it (the caller's buffer is free when this returns)
-static int staged_h2d(Context* c, void* dst, const void* src, size_t bytes) {
-  constexpr size_t kMaxStaged = 32;
-  Context::Staged* pick = nullptr;
-  for (auto& s : c->staging) {
-    if (s.bytes < bytes) continue;
-    const hipError_t q = hipEventQuery(s.ev);
-    if (q == hipErrorNotReady) continue;
-    DFX_HIP(q);
-    pick = &s;
-    break;
-  }
-  if (!pick && c->staging.size() >= kMaxStaged) {
-    // every buffer is in flight: wait for the next in turn, and grow it if it is too small
-    pick = &c->staging[c->staging_next++ % c->staging.size()];
-    DFX_HIP(hipEventSynchronize(pick->ev));
-    if (pick->bytes < bytes) {
-      DFX_HIP(hipHostFree(pick->p));
-      pick->p = nullptr;
-      pick->bytes = 0;
-    }
-  }
-  if (!pick) {
-    c->staging.emplace_back();
-    pick = &c->staging.back();
-    DFX_HIP(hipEventCreateWithFlags(&pick->ev, hipEventDisableTiming));
-  }
-  if (!pick->p) {
-    size_t want = 1 << 20;
-    while (want < bytes) want <<= 1;
-    DFX_HIP(hipHostMalloc(&pick->p, want, hipHostMallocDefault));
-    pick->bytes = want;
-  }
-  std::memcpy(pick->p, src, bytes);
-  DFX_HIP(hipMemcpyAsync(dst, pick->p, bytes, hipMemcpyHostToDevice, c->stream));
-  DFX_HIP(hipEventRecord(pick->ev, c->stream));
-  return DFX_OK;
-}
-
 int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_CHECK_ARG(kind >= 0 && kind <= 2, "dfx_memcpy: kind must be 0, 1 or 2");
   if (bytes == 0) return DFX_OK;
   DFX_CHECK_ARG(dst && src, "dfx_memcpy: null pointer");
-  if (kind == 0 && !is_pinned_host(src)) return staged_h2d(&ctx->c, dst, src, bytes);
   hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
                               : (kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice);
   DFX_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->c.stream));

@@ -550,6 +550,174 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* __restri
   if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
 }
 
+// ---- aggregated push (push_agg=sum) -----------------------------------
+// One step over N workers is one reference step over the concatenation of their batches: a
+// key's gradient is the sum of the workers' gradient records (in rank order), applied by ONE
+// Update (sgd_updater.cc:76-142) — UpdateW, and UpdateV when V was pulled (every worker of the
+// step pulled the same state, so the records agree on `live`).  InitV requests are flagged in
+// key order; their draws are ranked over all owners (k_dist_initv_sum), so the rand_r stream is
+// the single reference updater's.
+template <int G>
+__global__ __launch_bounds__(kDNT) void k_dist_push_sum_vec(
+    const uint32_t* __restrict__ segstart, const uint32_t* __restrict__ segslot,
+    const uint32_t* __restrict__ sorted_idx, const float* __restrict__ g, Table T, Params P,
+    const uint32_t* nuniq, uint32_t* flags, DevState* ds, uint32_t* fcount) {
+  const int64_t u = (int64_t)blockIdx.x * (kDNT / G) + threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  int dnew = 0, nf = 0;
+  const uint32_t sl = u < (int64_t)*nuniq ? segslot[u] : kNoSlot;
+  if (u < (int64_t)*nuniq && sl == kNoSlot) {  // not inserted: no update
+    if (l == 0) flags[u] = 0;
+  } else if (u < (int64_t)*nuniq) {
+    const int d = T.d, nc = d >> 2;
+    const int64_t S = rec_floats(d);
+    const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
+    Entry* en = &T.ent[sl];
+    const float4 h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
+    const float fc = en->fea_cnt;
+    const uint32_t src0 = sorted_idx[s0];
+    const float* g0 = g + (int64_t)src0 * S;
+    const float2 gwp0 = *reinterpret_cast<const float2*>(g0 + d);  // {gw, pulled}
+    const int vr = __float_as_int(h.y);
+    float4* V4 = reinterpret_cast<float4*>(row_V(T, vr >= 0 ? vr : 0));
+    float4* C4 = reinterpret_cast<float4*>(row_C(T, vr >= 0 ? vr : 0));
+    const bool upd_v = vr >= 0 && gwp0.y != 0.f;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = upd_v && l < nc ? V4[l] : z4, cg = upd_v && l < nc ? C4[l] : z4;
+    float4 gv = upd_v && l < nc ? reinterpret_cast<const float4*>(g0)[l] : z4;
+    float gw = gwp0.x;
+    for (uint32_t i = s0 + 1; i < s1; ++i) gw += g[(int64_t)sorted_idx[i] * S + d];
+    float4 e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
+    bool tr;
+    const int dw = ftrl_update(P, gw, &e, &tr);
+    if (l == 0) {
+      ent_set_state(en, e);
+      dnew = dw;
+      // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
+      const bool need = tr && d > 0 && vr < 0 && e.w > (float)P.V_threshold;
+      flags[u] = need ? 1u : 0u;
+      nf = need ? 1 : 0;
+    }
+    if (upd_v) {
+      for (int c = l; c < nc; c += G) {
+        if (c != l) {
+          v = V4[c];
+          cg = C4[c];
+          gv = reinterpret_cast<const float4*>(g0)[c];
+        }
+        for (uint32_t i = s0 + 1; i < s1; ++i) {
+          const float4 q = reinterpret_cast<const float4*>(g + (int64_t)sorted_idx[i] * S)[c];
+          gv.x += q.x; gv.y += q.y; gv.z += q.z; gv.w += q.w;
+        }
+        adagrad_update(P, gv.x, &v.x, &cg.x);
+        adagrad_update(P, gv.y, &v.y, &cg.y);
+        adagrad_update(P, gv.z, &v.z, &cg.z);
+        adagrad_update(P, gv.w, &v.w, &cg.w);
+        V4[c] = v;
+        C4[c] = cg;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    dnew += __shfl_xor(dnew, off, kWave);
+    nf += __shfl_xor(nf, off, kWave);
+  }
+  if (lane_id() == 0 && dnew)
+    atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+  if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
+}
+
+// the same for any V_dim (one lane per key)
+__global__ void k_dist_push_sum(const uint32_t* segstart, const uint32_t* segslot,
+                                const uint32_t* sorted_idx, const float* g, Table T, Params P,
+                                const uint32_t* nuniq, uint32_t* flags, DevState* ds,
+                                uint32_t* fcount) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int dnew = 0, nf = 0;
+  if (u < (int64_t)*nuniq && segslot[u] == kNoSlot) {
+    flags[u] = 0;
+  } else if (u < (int64_t)*nuniq) {
+    const int d = T.d;
+    const int64_t S = rec_floats(d);
+    Entry* en = &T.ent[segslot[u]];
+    float4 e = ent_state(en);
+    const int vr = en->vrow;
+    const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
+    const float* g0 = g + (int64_t)sorted_idx[s0] * S;
+    float gw = g0[d];
+    for (uint32_t i = s0 + 1; i < s1; ++i) gw += g[(int64_t)sorted_idx[i] * S + d];
+    bool tr;
+    dnew = ftrl_update(P, gw, &e, &tr);
+    ent_set_state(en, e);
+    if (vr >= 0 && g0[d + 1] != 0.f) {
+      float* V = row_V(T, vr);
+      float* C = row_C(T, vr);
+      for (int k = 0; k < d; ++k) {
+        float gk = g0[k];
+        for (uint32_t i = s0 + 1; i < s1; ++i) gk += g[(int64_t)sorted_idx[i] * S + k];
+        adagrad_update(P, gk, V + k, C + k);
+      }
+    }
+    const bool need = tr && d > 0 && vr < 0 && e.w > (float)P.V_threshold;
+    flags[u] = need ? 1u : 0u;
+    nf = need ? 1 : 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    dnew += __shfl_xor(dnew, off, kWave);
+    nf += __shfl_xor(nf, off, kWave);
+  }
+  if (lane_id() == 0 && dnew)
+    atomicAdd((unsigned long long*)&ds->new_w, (unsigned long long)(long long)dnew);
+  if (lane_id() == 0 && nf) atomicAdd(fcount, (uint32_t)nf);
+}
+
+__global__ void k_dist_initv_count(const uint32_t* ftotal, int64_t* out) {
+  *out = (int64_t)*ftotal;
+}
+
+// InitV draws of this owner's flagged keys (key order), ranked after every lower owner's
+// draws of this step: the q-th of them jumps the shared seed by 3*d*(sum_{h<rank} F_h + q)
+__global__ void k_dist_initv_sum(const uint32_t* excl, const uint32_t* ftotal,
+                                 const uint32_t* nuniq, int64_t bound,
+                                 const uint32_t* segslot, const int64_t* Fall, int rank,
+                                 Table T, float scale, const DevState* ds) {
+  const uint32_t F = *ftotal;
+  if (F == 0) return;
+  int64_t off = 0;
+  for (int h = 0; h < rank; ++h) off += Fall[h];
+  const int64_t n = std::min<int64_t>(*nuniq, bound);
+  const int d = T.d;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = excl[u];
+    const uint32_t nx = (u + 1 < n) ? excl[u + 1] : F;
+    if (nx == e) continue;
+    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
+    const int64_t vr = (int64_t)ds->n_vrows + e;
+    if (vr >= T.vcap) continue;  // kErrPoolFull is set by the finalize
+    float* V = row_V(T, vr);
+    float* C = row_C(T, vr);
+    for (int k = 0; k < d; ++k) {
+      V[k] = initv_value(rand_r_dev(&s), scale);
+      C[k] = 0.f;
+    }
+    T.ent[segslot[u]].vrow = (int32_t)vr;
+  }
+}
+
+__global__ void k_dist_initv_sum_finalize(const uint32_t* ftotal, const int64_t* Fall,
+                                          int nranks, int d, int64_t vcap, DevState* ds,
+                                          uint32_t* fcount) {
+  int64_t tot = 0;
+  for (int h = 0; h < nranks; ++h) tot += Fall[h];
+  const uint32_t F = *ftotal;
+  *fcount = 0u;
+  ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)tot);
+  const unsigned long long nv = ds->n_vrows + F;
+  if (nv > (unsigned long long)vcap) atomicOr(&ds->err, kErrPoolFull);
+  ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+}
+
 static int vec_group(int d) {
   if (d <= 0 || d % 4 != 0) return 0;
   int g = 1;
@@ -752,6 +920,8 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_TRY(pipeline_init(c));
+  DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1],
+                "dist_owner_begin: finish the pending InitV first (dfx_dist_initv_local / _draw)");
   c->dist_used = true;  // slots now carry table slots across steps: no growth at sync points
   // this table serves one of nranks key ranges: hash keys by their position in the range
   DFX_TRY(table_set_ranges(c, nranks));
@@ -825,7 +995,12 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
                        ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
                        ws.osorted.as<uint32_t>(), recv_cnt, rank_offs(c, slot), c->T, c->P,
                        nuniq, flags, ws.ofrank.as<uint32_t>(), &OL.ds->totals[3]);
-    if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, nranks));
+    if (c->P.V_dim > 0) {
+      if (c->dist_sum)
+        c->dist_initv_pending[slot] = true;  // drawn in global key order (dfx_dist_initv_*)
+      else
+        DFX_TRY(owner_initv(c, slot, nranks));
+    }
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
@@ -835,6 +1010,8 @@ int dfx_dist_owner_pull(dfx_ctx* ctx, int slot, float* vals_out) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_CHECK_SLOT(slot);
   Context* c = &ctx->c;
+  DFX_CHECK_ARG(!c->dist_initv_pending[slot],
+                "dist_owner_pull: the count push's InitV is pending (dfx_dist_initv_local / _draw)");
   const int64_t R = c->dist_R[slot];
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(vals_out, "dist_owner_pull: null buffer");
@@ -879,13 +1056,41 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_CHECK_SLOT(slot);
   Context* c = &ctx->c;
+  DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1],
+                "dist_owner_push: finish the pending InitV first (dfx_dist_initv_local / _draw)");
   const int64_t R = c->dist_R[slot];
-  if (R == 0) return DFX_OK;
-  DFX_CHECK_ARG(recv_grads, "dist_owner_push: null buffer");
+  if (R == 0 && !c->dist_sum) return DFX_OK;
+  DFX_CHECK_ARG(R == 0 || recv_grads, "dist_owner_push: null buffer");
   owner_segs(c, slot);  // a push with no pull before it
   const Lane OL = owner_lane(c, slot);
   Workspace& ws = *OL.ws;
   const int G = vec_group(c->P.V_dim);
+  if (c->dist_sum) {
+    // one Update per key on the summed gradient; InitV drawn in global key order next
+    if (R > 0) {
+#define DFX_PUSH_SUM(GG)                                                                     \
+      if (G == GG) {                                                                         \
+        const int64_t per = kDNT / GG;                                                       \
+        hipLaunchKernelGGL(k_dist_push_sum_vec<GG>, dim3((R + per - 1) / per), dim3(kDNT), 0, \
+                           OL.stream, ws.osegstart.as<uint32_t>(),                           \
+                           ws.osegslot.as<uint32_t>(), ws.osorted.as<uint32_t>(),            \
+                           recv_grads, c->T, c->P, &OL.ds->totals[1],                        \
+                           ws.oflags.as<uint32_t>(), c->ds, &OL.ds->totals[3]);              \
+      }
+      DFX_DIST_GROUPS(DFX_PUSH_SUM)
+#undef DFX_PUSH_SUM
+      if (G == 0)
+        hipLaunchKernelGGL(k_dist_push_sum, dim3((R + kDNT - 1) / kDNT), dim3(kDNT), 0,
+                           OL.stream, ws.osegstart.as<uint32_t>(), ws.osegslot.as<uint32_t>(),
+                           ws.osorted.as<uint32_t>(), recv_grads, c->T, c->P,
+                           &OL.ds->totals[1], ws.oflags.as<uint32_t>(), c->ds,
+                           &OL.ds->totals[3]);
+    }
+    // every owner takes part in the InitV ranking, with or without keys this step
+    if (c->P.V_dim > 0) c->dist_initv_pending[slot] = true;
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
+  }
   const RankOffs ro = rank_offs(c, slot);
 #define DFX_PUSH(GG)                                                                         \
   if (G == GG) {                                                                             \
@@ -908,5 +1113,55 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
+
+// push_agg=sum: the InitV requests of the slot's last count push or gradient push, ranked
+// over all owners.  initv_local scans this owner's flags (key order) and writes their number
+// to count_dev (device int64); the caller all-gathers the owners' counts (rank order) into
+// counts_all_dev[nranks] (device) and initv_draw draws this owner's keys after every lower
+// owner's, advancing the shared seed by the total (sgd_updater.cc:144-152 in global key order)
+int dfx_dist_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev) {
+  DFX_CHECK_ARG(ctx && count_dev, "null argument");
+  DFX_CHECK_SLOT(slot);
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(c->dist_sum, "dist_initv_local: only with push_agg=sum");
+  const Lane OL = owner_lane(c, slot);
+  uint32_t* ftotal = &OL.ds->totals[2];
+  if (!c->dist_initv_pending[slot] || c->dist_R[slot] == 0) {
+    DFX_HIP(hipMemsetAsync(ftotal, 0, sizeof(uint32_t), OL.stream));
+  } else {
+    DFX_TRY(scan_u32(OL, OL.ws->oflags.as<uint32_t>(), c->dist_R[slot], ftotal,
+                     &OL.ds->totals[1], &OL.ds->totals[3]));
+  }
+  hipLaunchKernelGGL(k_dist_initv_count, dim3(1), dim3(1), 0, OL.stream, ftotal, count_dev);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_dist_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
+                        int nranks) {
+  DFX_CHECK_ARG(ctx && counts_all_dev, "null argument");
+  DFX_CHECK_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks && rank >= 0 && rank < nranks,
+                "dist_initv_draw: bad rank");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(c->dist_sum, "dist_initv_draw: only with push_agg=sum");
+  const Lane OL = owner_lane(c, slot);
+  const int64_t R = c->dist_R[slot];
+  uint32_t* ftotal = &OL.ds->totals[2];
+  if (c->dist_initv_pending[slot] && R > 0) {
+    const dim3 igrid((unsigned)std::min<int64_t>((R + kDNT - 1) / kDNT, 1024));
+    hipLaunchKernelGGL(k_dist_initv_sum, igrid, dim3(kDNT), 0, OL.stream,
+                       OL.ws->oflags.as<uint32_t>(), ftotal, &OL.ds->totals[1], R,
+                       OL.ws->osegslot.as<uint32_t>(), counts_all_dev, rank, c->T,
+                       c->P.V_init_scale, c->ds);
+  }
+  hipLaunchKernelGGL(k_dist_initv_sum_finalize, dim3(1), dim3(1), 0, OL.stream, ftotal,
+                     counts_all_dev, nranks, c->P.V_dim, c->T.vcap, c->ds, &OL.ds->totals[3]);
+  c->dist_initv_pending[slot] = false;
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_dist_push_agg_sum(dfx_ctx* ctx) { return ctx ? ctx->c.dist_sum : -1; }
 
 }  // extern "C"

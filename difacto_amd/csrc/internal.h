@@ -183,16 +183,13 @@ struct Context {
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
   // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
   CapGuard capg;
-  // pinned staging of host->device copies from pageable memory (dfx_memcpy): a buffer is
-  // reused once the copy that read it has run (its event)
-  struct Staged {
-    void* p = nullptr;
-    size_t bytes = 0;
-    hipEvent_t ev = nullptr;
-  };
-  std::vector<Staged> staging;
-  size_t staging_next = 0;
+
   bool dist_used = false;  // a key-range server: its slots hold table slots across steps
+  // push_agg=sum (default): one Update per key per step on the workers' summed gradients, InitV
+  // ranked over all owners (dfx_dist_initv_local / _draw); push_agg=ranks: one Update per
+  // pushing worker in rank order, InitV per server (KVStoreDist's HandlePush)
+  int dist_sum = 1;
+  bool dist_initv_pending[2] = {false, false};
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }

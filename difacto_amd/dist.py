@@ -5,9 +5,11 @@ collectives (torch.distributed: RCCL over xGMI on GPUs, gloo on CPU).
 Every rank is a worker (its own minibatch, SGDLearner::IterateData's executor,
 src/sgd/sgd_learner.cc:201-317) and the server of the keys k with floor(k * N / 2^64) ==
 rank; keys are nibble-reversed feature ids, so ranges are balanced.  A step is bulk
-synchronous — every pull is answered before any push, pushes are applied in worker-rank
-order — which is the deterministic schedule of the reference's (unimplemented) sync_mode;
-each server applies one Update per pushing worker like HandlePush (kvstore_dist.h:158-165).
+synchronous — every pull is answered before any push — which is the deterministic schedule
+of the reference's (unimplemented) sync_mode.  With push_agg=sum (the default) a step is one
+reference step over the concatenation of the workers' batches: one Update
+per key on the summed gradient; with push_agg=ranks each server applies one Update per
+pushing worker in rank order like HandlePush (kvstore_dist.h:158-165).
 
 The device phases are the C-ABI's dfx_dist_* calls (include/difacto_amd.h); this module is
 only the orchestration between them.  ``Comm`` abstracts the exchange so the same step runs
@@ -44,12 +46,16 @@ def model_name(prefix, rank, it=-1):
 
 class Shard:
     """One rank's device context in the sharded store: worker and key-range server.  Every
-    call takes the step slot (0 or 1) whose buffers it uses; two steps can be in flight."""
+    call takes the step slot (0 or 1) whose buffers it uses; two steps can be in flight.
+    The context's push_agg kwarg picks the update semantics (include/difacto_amd.h): sum (one
+    Update per key on the workers' summed gradients, InitV ranked over all owners) or ranks
+    (one Update per pushing worker, KVStoreDist's HandlePush)."""
 
     def __init__(self, ctx, nranks):
         self.ctx = ctx
         self.nranks = int(nranks)
         self.S = _lib.lib().dfx_dist_record_floats(ctx.h)
+        self.agg_sum = _lib.lib().dfx_dist_push_agg_sum(ctx.h) == 1
         self._U = [0, 0]
         self._R = [0, 0]
         # the Localizer lane writes these; they live until the slot's fwd_bwd
@@ -119,6 +125,17 @@ class Shard:
     def owner_push(self, recv_grads, slot=0):
         check(_lib.lib().dfx_dist_owner_push(self.ctx.h, slot, _p(recv_grads)))
 
+    # push_agg=sum: InitV ranked over all owners (after a count push and after every push)
+    def initv_local(self, slot=0):
+        """-> device int64[1]: this owner's InitV request count"""
+        out = torch.empty(1, dtype=torch.int64, device=self.ctx.device)
+        check(_lib.lib().dfx_dist_initv_local(self.ctx.h, slot, _p(out)))
+        return out
+
+    def initv_draw(self, counts_all, rank, slot=0):
+        check(_lib.lib().dfx_dist_initv_draw(self.ctx.h, slot, _p(counts_all), int(rank),
+                                             self.nranks))
+
     # model files (SGDLearner::SaveLoadModel, sgd_learner.cc:180-196) ---------------------------
     def save(self, prefix, rank, save_aux=False, it=-1):
         """this server's part, in SGDUpdater::Save's format (flush a pipeline first)"""
@@ -181,12 +198,38 @@ class TorchComm:
         else:
             self.kgroup = self.cgroup = group
 
+    def ranks(self):
+        return [self.rank]
+
     def exchange_counts(self, send_splits):
+        """the split counts (a host round trip: the receivers size their buffers).  RCCL: one
+        all-to-all of N int64 on the key communicator's idle stream, read back into host
+        memory — no host-side (gloo / TCP) collective in the step; gloo: all_gather"""
         (s,) = send_splits
+        if self.nccl and self.world > 1:
+            with torch.cuda.stream(self.kstream):
+                t = torch.tensor(s, dtype=torch.int64, device=self.device)
+                out = torch.empty(self.world, dtype=torch.int64, device=self.device)
+                self.dist.all_to_all_single(out, t, group=self.kgroup)
+                return [out.cpu().tolist()]
         t = torch.tensor(s, dtype=torch.int64)
         out = [torch.empty_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t, group=self.cgroup)
         return [[int(o[self.rank]) for o in out]]
+
+    def allgather_i64(self, tensors):
+        """every rank's device int64[1] -> device int64[world] in rank order (stream-ordered
+        on the current stream: no host round trip)"""
+        (t,) = tensors
+        if self.world == 1:
+            return [t]
+        if self.stage_cpu:
+            out = [torch.empty(1, dtype=torch.int64) for _ in range(self.world)]
+            self.dist.all_gather(out, t.cpu(), group=self.group)
+            return [torch.cat(out).to(t.device)]
+        out = torch.empty(self.world, dtype=torch.int64, device=t.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        return [out]
 
     def _a2a(self, x, ss, rs, row, group, async_op):
         """all-to-all-v of rows of `row` elements: ss[p] rows to rank p, rs[p] rows from it.
@@ -296,6 +339,13 @@ class LoopbackComm:
     def __init__(self, world):
         self.world = int(world)
 
+    def ranks(self):
+        return list(range(self.world))
+
+    def allgather_i64(self, tensors):
+        allc = torch.cat([t.reshape(1) for t in tensors])
+        return [allc for _ in tensors]
+
     def exchange_counts(self, send_splits):
         return [[send_splits[r][g] for r in range(self.world)] for g in range(self.world)]
 
@@ -320,6 +370,17 @@ class LoopbackComm:
     def allreduce_sum(self, values):
         tot = [sum(v[i] for v in values) for i in range(len(values[0]))]
         return [list(tot) for _ in values]
+
+
+def _initv(shards, comm, slot):
+    """push_agg=sum: rank the owners' InitV requests over all owners (a tiny all-gather of
+    their counts, on the device) and draw them"""
+    if not shards[0].agg_sum or shards[0].ctx.V_dim <= 0:
+        return
+    cnt = [sh.initv_local(slot) for sh in shards]
+    allc = comm.allgather_i64(cnt)
+    for sh, a, r in zip(shards, allc, comm.ranks()):
+        sh.initv_draw(a, r, slot)
 
 
 PHASES = ("localize", "xchg_keys", "owner_begin", "owner_pull", "xchg_pull", "fwd_bwd",
@@ -353,6 +414,8 @@ def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_in
     mark(1)
     for i in range(n):
         shards[i].owner_begin(rkeys[i], recv[i], rcnt[i], 0)
+    if want_cnt:
+        _initv(shards, comm, 0)
     mark(2)
     S = shards[0].S
     vals = [s.owner_pull(0) for s in shards]
@@ -367,6 +430,7 @@ def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_in
         mark(6)
         for i in range(n):
             shards[i].owner_push(rgrads[i], 0)
+        _initv(shards, comm, 0)
     else:
         mark(6)
     mark(7)
@@ -429,6 +493,8 @@ class ShardedPipeline:
         mark(1)
         for i in range(n):
             shards[i].owner_begin(rkeys[i], recv[i], rcnt[i], s)
+        if want_cnt:
+            _initv(shards, comm, s)
         mark(2)
         S = shards[0].S
         vals = [sh.owner_pull(s) for sh in shards]
@@ -453,3 +519,4 @@ class ShardedPipeline:
         rgrads = hg.wait()
         for i, sh in enumerate(self.shards):
             sh.owner_push(rgrads[i], s)
+        _initv(self.shards, self.comm, s)

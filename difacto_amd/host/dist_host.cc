@@ -72,10 +72,13 @@ class LoopbackExchange : public ShardExchange {
       for (int g = 0; g < n; ++g) (*recv)[g][l] = send[l][g];
   }
 
+  // the copies run on the receiving shard's own stream, behind its earlier readers
+  void Release(int) override {}
+
   int Start(int, const std::vector<const void*>& send,
             const std::vector<std::vector<int64_t>>& send_rows, const std::vector<void*>& recv,
             const std::vector<std::vector<int64_t>>& recv_rows, size_t row_bytes,
-            bool) override {
+            bool, int) override {
     const int n = nranks();
     // every destination stream waits for every source stream; then copies; then every
     // source waits for every destination (the sources' buffers are free again)
@@ -103,6 +106,25 @@ class LoopbackExchange : public ShardExchange {
   }
   void Wait(int) override {}
   void AllReduceSum(std::vector<double>*) override {}
+
+  int Gather(const std::vector<const void*>& send, const std::vector<void*>& recv,
+             size_t bytes) override {
+    const int n = nranks();
+    for (int l = 0; l < n; ++l) HipCheck(hipEventRecord(done_[l], streams_[l]), "record");
+    for (int g = 0; g < n; ++g)
+      for (int l = 0; l < n; ++l)
+        if (l != g) HipCheck(hipStreamWaitEvent(streams_[g], done_[l], 0), "wait");
+    for (int g = 0; g < n; ++g)
+      for (int l = 0; l < n; ++l)
+        HipCheck(hipMemcpyAsync(static_cast<char*>(recv[g]) + l * bytes, send[l], bytes,
+                                hipMemcpyDeviceToDevice, streams_[g]),
+                 "loopback gather");
+    for (int g = 0; g < n; ++g) HipCheck(hipEventRecord(done_[g], streams_[g]), "record");
+    for (int l = 0; l < n; ++l)
+      for (int g = 0; g < n; ++g)
+        if (l != g) HipCheck(hipStreamWaitEvent(streams_[l], done_[g], 0), "wait");
+    return 0;
+  }
 
  private:
   std::vector<dfx_ctx*> ctxs_;
@@ -150,6 +172,7 @@ class RcclExchange : public ShardExchange {
       HipCheck(hipStreamCreateWithFlags(&cs_[c], hipStreamNonBlocking), "stream");
     }
     for (auto& e : ev_) HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+    for (auto& e : free_) HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     HipCheck(hipEventCreateWithFlags(&in_, hipEventDisableTiming), "event");
     HipCheck(hipHostMalloc(reinterpret_cast<void**>(&hcnt_), 2 * 8 * (nranks + 8),
                            hipHostMallocDefault),
@@ -168,6 +191,7 @@ class RcclExchange : public ShardExchange {
     for (auto s : cs_) (void)hipStreamSynchronize(s);
     for (auto c : comm_) (void)ncclCommDestroy(c);
     for (auto e : ev_) (void)hipEventDestroy(e);
+    for (auto e : free_) (void)hipEventDestroy(e);
     (void)hipEventDestroy(in_);
     (void)hipHostFree(hcnt_);
     (void)hipFree(dcnt_);
@@ -199,15 +223,21 @@ class RcclExchange : public ShardExchange {
     recv->assign(1, std::vector<int64_t>(hr, hr + n_));
   }
 
+  void Release(int slot) override {
+    HipCheck(hipEventRecord(free_[slot & 1], stream_), "record");
+  }
+
   int Start(int channel, const std::vector<const void*>& send,
             const std::vector<std::vector<int64_t>>& send_rows, const std::vector<void*>& recv,
             const std::vector<std::vector<int64_t>>& recv_rows, size_t row_bytes,
-            bool after_compute) override {
+            bool after_compute, int recv_free_slot) override {
     hipStream_t cs = cs_[channel];
     if (after_compute) {
       HipCheck(hipEventRecord(in_, stream_), "record");
       HipCheck(hipStreamWaitEvent(cs, in_, 0), "wait");
     }
+    if (recv_free_slot >= 0)  // the slot's receive buffers are free once its readers ran
+      HipCheck(hipStreamWaitEvent(cs, free_[recv_free_slot & 1], 0), "wait");
     const std::vector<int64_t> so = Offsets(send_rows[0]), ro = Offsets(recv_rows[0]);
     // this rank's own rows: a device copy, not an RCCL self-send (whose copy kernel runs on a
     // few channels' blocks)
@@ -236,6 +266,17 @@ class RcclExchange : public ShardExchange {
   }
   void Wait(int h) override { HipCheck(hipStreamWaitEvent(stream_, ev_[h], 0), "wait"); }
 
+  int Gather(const std::vector<const void*>& send, const std::vector<void*>& recv,
+             size_t bytes) override {
+    hipStream_t cs = cs_[1];
+    HipCheck(hipEventRecord(in_, stream_), "record");
+    HipCheck(hipStreamWaitEvent(cs, in_, 0), "wait");
+    NcclCheck(ncclAllGather(send[0], recv[0], bytes, ncclUint8, comm_[1], cs), "allgather");
+    const int h = next_++ % kEvents;
+    HipCheck(hipEventRecord(ev_[h], cs), "record");
+    return h;
+  }
+
   void AllReduceSum(std::vector<double>* v) override {
     const size_t n = v->size();
     std::vector<double> buf(*v);
@@ -260,6 +301,7 @@ class RcclExchange : public ShardExchange {
   hipStream_t cs_[2] = {nullptr, nullptr};
   ncclComm_t comm_[2] = {nullptr, nullptr};
   hipEvent_t ev_[kEvents] = {};
+  hipEvent_t free_[2] = {nullptr, nullptr};  // per slot: its key receive buffers' readers ran
   hipEvent_t in_ = nullptr;
   int next_ = 0;
   int64_t* hcnt_ = nullptr;
@@ -319,6 +361,9 @@ struct GpuShardedStore::Impl {
   // the pending gradient exchange: its slot, handle and the receive counts of that step
   bool pending = false;
   int pend_slot = 0, pend_handle = 0;
+  // push_agg=sum: InitV ranked over all owners (per local shard: its count, everyone's)
+  bool agg_sum = false;
+  std::vector<DBuf> icnt, iall;
 
   Impl(ShardExchange* e, bool pipe) : ex(e), pipelined(pipe) {
     N = ex->nranks();
@@ -332,6 +377,33 @@ struct GpuShardedStore::Impl {
                         &s[l].rpulled, &s[l].grads, &s[l].rgrads})
           b->c = ex->ctx(l);
     }
+    agg_sum = dfx_dist_push_agg_sum(ex->ctx(0)) == 1;
+    icnt.resize(L);
+    iall.resize(L);
+    for (int l = 0; l < L; ++l) {
+      icnt[l].c = iall[l].c = ex->ctx(l);
+      icnt[l].ensure(8);
+      iall[l].ensure(8 * N);
+    }
+  }
+
+  // push_agg=sum: every owner's InitV request count, gathered, then the draws ranked over all
+  // owners (after a count push, and after every gradient push)
+  void InitV(int s) {
+    if (!agg_sum || d <= 0) return;
+    std::vector<const void*> snd(L);
+    std::vector<void*> rcv(L);
+    for (int l = 0; l < L; ++l) {
+      DfxOk(dfx_dist_initv_local(ex->ctx(l), s, static_cast<int64_t*>(icnt[l].p)),
+            "dfx_dist_initv_local");
+      snd[l] = icnt[l].p;
+      rcv[l] = iall[l].p;
+    }
+    ex->Wait(ex->Gather(snd, rcv, 8));
+    for (int l = 0; l < L; ++l)
+      DfxOk(dfx_dist_initv_draw(ex->ctx(l), s, static_cast<const int64_t*>(iall[l].p),
+                                ex->rank(l), N),
+            "dfx_dist_initv_draw");
   }
 
   void Localize(const Step& q) {
@@ -354,6 +426,7 @@ struct GpuShardedStore::Impl {
       DfxOk(dfx_dist_owner_push(ex->ctx(l), pend_slot,
                                 static_cast<const float*>(slot[pend_slot][l].rgrads.p)),
             "dfx_dist_owner_push");
+    InitV(pend_slot);
   }
 
   void Run(const Step& q) {
@@ -375,8 +448,10 @@ struct GpuShardedStore::Impl {
       kr[l] = b.rkeys.ensure(R[l] * 8);
       if (q.want_cnt) cr[l] = b.rcnt.ensure(R[l] * 4);
     }
-    const int hk = ex->Start(0, ks, send, kr, recv, 8, false);
-    const int hc = q.want_cnt ? ex->Start(0, cs, send, cr, recv, 4, false) : -1;
+    // the keys' inputs are complete (the host joined the Localizer lane); their receive
+    // buffers are this slot's, free once the slot's previous owner_pull ran (Release below)
+    const int hk = ex->Start(0, ks, send, kr, recv, 8, false, s);
+    const int hc = q.want_cnt ? ex->Start(0, cs, send, cr, recv, 4, false, s) : -1;
     ex->Wait(hk);
     if (hc >= 0) ex->Wait(hc);
     for (int l = 0; l < L; ++l) {
@@ -385,12 +460,16 @@ struct GpuShardedStore::Impl {
                                  offs.data(), N,
                                  q.want_cnt ? static_cast<const float*>(cr[l]) : nullptr),
             "dfx_dist_owner_begin");
+    }
+    if (q.want_cnt) InitV(s);  // the count push's InitV draws, before the pull
+    for (int l = 0; l < L; ++l) {
       Slot& b = slot[s][l];
       float* pulled = static_cast<float*>(b.pulled.ensure((size_t)R[l] * S * 4));
       DfxOk(dfx_dist_owner_pull(ex->ctx(l), s, pulled), "dfx_dist_owner_pull");
       ps[l] = pulled;
       pr[l] = b.rpulled.ensure((size_t)U[l] * S * 4);
     }
+    ex->Release(s);  // the last reader of this slot's received keys (and counts) was queued
     // records go back to the workers: each owner's rows are grouped by source rank
     const int hr = ex->Start(1, ps, recv, pr, send, (size_t)S * 4, true);
     PushPending();  // the previous step's push, beside the record exchange

@@ -35,14 +35,24 @@ class ShardExchange {
   /** all-to-all-v of rows of row_bytes on channel (0: keys, 1: records / gradients).
    * send[l] holds local shard l's rows grouped by destination in rank order, recv[l] receives
    * them grouped by source.  after_compute: the inputs were produced on the shards' streams
-   * (otherwise they are complete already).  Returns a handle for Wait. */
+   * (otherwise they are complete already).  recv_free_slot >= 0: the receive buffers belong
+   * to that step slot, whose previous readers ran before the last Release(slot) on the
+   * shards' streams — the exchange writes them only after that point.  Returns a handle for
+   * Wait. */
   virtual int Start(int channel, const std::vector<const void*>& send,
                     const std::vector<std::vector<int64_t>>& send_rows,
                     const std::vector<void*>& recv,
                     const std::vector<std::vector<int64_t>>& recv_rows, size_t row_bytes,
-                    bool after_compute) = 0;
+                    bool after_compute, int recv_free_slot = -1) = 0;
+  /** the shards' streams are past the last reader of a slot's exchange receive buffers */
+  virtual void Release(int slot) = 0;
   /** the shards' streams wait for the exchange (enqueue only) */
   virtual void Wait(int handle) = 0;
+  /** all-gather of `bytes` per shard, stream-ordered after the shards' compute: recv[l]
+   * receives every shard's send in global rank order (the InitV counts of push_agg=sum).
+   * Returns a handle for Wait. */
+  virtual int Gather(const std::vector<const void*>& send, const std::vector<void*>& recv,
+                     size_t bytes) = 0;
   /** sum of v over all processes (host) */
   virtual void AllReduceSum(std::vector<double>* v) = 0;
 };
@@ -57,7 +67,9 @@ std::unique_ptr<ShardExchange> MakeRcclExchange(dfx_ctx* ctx, int rank, int nran
 
 /** KVStoreDist over the exchange: every local shard is a worker and the server of its key
  * range.  Pipelined (1-step-stale, dist.py ShardedPipeline / StaleOracle) or synchronous
- * (dist.sharded_step / ShardedOracle). */
+ * (dist.sharded_step / ShardedOracle, AggOracle).  The update aggregation follows the
+ * contexts' push_agg kwarg (sum: one Update per key per step, InitV ranked over all owners;
+ * ranks: one Update per pushing worker). */
 class GpuShardedStore {
  public:
   GpuShardedStore(ShardExchange* ex, bool pipelined);

@@ -97,10 +97,10 @@ int dfx_ctx_vdim(dfx_ctx* ctx);
 int dfx_sync(dfx_ctx* ctx); /* waits for the stream and reports deferred device errors */
 int dfx_malloc(dfx_ctx* ctx, void** ptr, size_t bytes);
 int dfx_free(dfx_ctx* ctx, void* ptr);
-/* kind: 0 host->device, 1 device->host, 2 device->device; async on the stream.  Host->device
- * from pageable memory goes through the context's pinned staging pool, so the caller may reuse
- * src as soon as the call returns (HIP may read a pageable source only when the copy reaches
- * the head of a busy stream).  Device->host returns once the data are on the host. */
+/* kind: 0 host->device, 1 device->host, 2 device->device; async on the stream.  A pageable
+ * host source may be reused when the call returns (HIP stages it during the call, measured
+ * behind a busy stream by tools/pageable_probe.hip); a pinned one only after the copy ran.
+ * Device->host returns once the data are on the host. */
 int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
 /* pre-size the fused-path workspace so dfx_train_step allocates nothing (graph capture) */
 int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz);
@@ -251,6 +251,24 @@ int dfx_dist_owner_pull(dfx_ctx* ctx, int slot, float* vals_out);
 int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* pulled,
                      int job_type, float* grads_out, float* pred_out);
 int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads);
+/* Update aggregation of the sharded store (context kwarg push_agg):
+ *   sum (default) — SURVEY §8(e)'s synchronous semantics: a step over N workers is one
+ *     reference step (sgd_learner.cc:201-317) on the concatenation of their batches.  The owner
+ *     sums the workers' gradient records of a key (rank order) and applies ONE Update
+ *     (sgd_updater.cc:76-142); a count push adds the summed counts.  InitV draws are ranked
+ *     over all owners in key order, so the rand_r stream is the single updater's: after an
+ *     owner_begin with counts, and after every owner_push, each owner calls
+ *     dfx_dist_initv_local (its request count -> count_dev, a device int64), the caller
+ *     all-gathers the counts (rank order) into counts_all_dev[nranks] (device), and
+ *     dfx_dist_initv_draw draws this owner's keys after the lower owners' (rank = this owner's
+ *     range).  owner_pull / owner_begin / owner_push refuse to run while that is pending.
+ *   ranks — KVStoreDist's HandlePush (kvstore_dist.h:158-165): one Update per pushing worker in
+ *     rank order, each server with its own rand_r stream (InitV inside begin / push).
+ * dfx_dist_push_agg_sum: 1 for sum, 0 for ranks. */
+int dfx_dist_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev);
+int dfx_dist_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
+                        int nranks);
+int dfx_dist_push_agg_sum(dfx_ctx* ctx);
 
 #ifdef __cplusplus
 }

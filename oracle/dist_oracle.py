@@ -7,8 +7,10 @@ with Get (HandlePull, :167-175).  Each worker runs SGDLearner::IterateData's exe
 (src/sgd/sgd_learner.cc:272-317) on its own batch: Localizer::Compact, the epoch-0 kFeaCount
 push (waited on, :304-307), Pull, Predict, Evaluate, AUC, CalcGrad, Push.
 ShardedOracle.step is bulk synchronous with pushes applied in worker-rank order: all count
-pushes, then all pulls, then all gradient pushes.  StaleOracle is the pipelined
-(1-step-stale) schedule of the same phases.
+pushes, then all pulls, then all gradient pushes (push_agg=ranks).  AggOracle is the
+push_agg=sum semantics (one Update per key on the workers' summed gradients: one reference
+step over the concatenated batches).  StaleOracle is the pipelined (1-step-stale) schedule of
+either.
 """
 import numpy as np
 
@@ -125,6 +127,104 @@ class ShardedOracle:
         return self.up[self.owner(key)].entry(key)
 
 
+class AggOracle:
+    """push_agg=sum (SURVEY.md §8(e)'s synchronous semantics): a step over N workers is one
+    reference step over the concatenation of their batches.  The N servers together hold
+    exactly one SGDUpdater's model (a key's state lives on its owner, and InitV draws are
+    ranked over all owners in key order, so one rand_r stream serves them all); this oracle
+    therefore keeps one Updater:
+      begin   every worker's Localizer::Compact; a count push adds, per key of the union, the
+              workers' counts (= the concatenated batch's Localizer count), in key order
+      pull    every worker's Get of its own keys from the same state
+      push    per key of the union the workers' gradients summed in rank order (float32, the
+              order the owner adds the received records), then ONE Update in key order
+    Same interface as ShardedOracle (begin / pull / compute / push / step / entry)."""
+
+    def __init__(self, nranks, **kw):
+        self.N = int(nranks)
+        self.one = O.Updater(**kw)
+        self.up = [self.one]
+        self.d = self.one.V_dim
+
+    def begin(self, blocks, push_cnt=False, max_index=(1 << 64) - 1):
+        d = self.d
+        assert len(blocks) == self.N
+        loc = []
+        for blk in blocks:
+            uniq, cnt, col = O.localize(blk.offs, blk.ids, max_index, want_cnt=True)
+            loc.append((uniq, cnt, col, owner_bounds(uniq, self.N)))
+        if push_cnt and d > 0:
+            keys, cnts = self._union([l[0] for l in loc], [l[1] for l in loc], 1)
+            if len(keys):
+                self.one.update(keys, O.Updater.kFeaCount, cnts)
+        return {"blocks": blocks, "loc": loc}
+
+    @staticmethod
+    def _union(keys, rows, width):
+        """union of the workers' sorted keys and their rows of `width` floats summed in rank
+        order (float32 adds, starting from the first worker's row)"""
+        allk = np.concatenate(keys) if keys else np.zeros(0, np.uint64)
+        uk = np.unique(allk)
+        acc = np.zeros((len(uk), width), np.float32)
+        seen = np.zeros(len(uk), bool)
+        for k, r in zip(keys, rows):
+            if len(k) == 0:
+                continue
+            idx = np.searchsorted(uk, k)
+            r = np.asarray(r, np.float32).reshape(len(k), width)
+            first = ~seen[idx]
+            acc[idx[first]] = r[first]
+            acc[idx[~first]] = (acc[idx[~first]] + r[~first]).astype(np.float32)
+            seen[idx] = True
+        return uk, acc.reshape(-1) if width == 1 else acc
+
+    def pull(self, st):
+        st["pulled"] = [self.one.get(l[0]) for l in st["loc"]]
+
+    compute = ShardedOracle.compute
+
+    def push(self, st):
+        d = self.d
+        keys, rows, lens_u = [], [], None
+        for r in range(self.N):
+            uniq = st["loc"][r][0]
+            vals, lens = st["pulled"][r]
+            g = st["grads"][r]
+            # each key's gradient as a full [gw | gV(d)] row (gV zero unless V was pulled)
+            full = np.zeros((len(uniq), 1 + d), np.float32)
+            if d > 0:
+                wp, vp = O.get_pos(lens)
+                full[:, 0] = g[wp]
+                live = lens > 1
+                if np.any(live):
+                    full[live, 1:] = g[vp[live][:, None] + np.arange(d)]
+            else:
+                full[:, 0] = g
+            keys.append(uniq)
+            rows.append(full)
+        uk, acc = self._union(keys, rows, 1 + d)
+        if len(uk) == 0:
+            return
+        if d == 0:  # acc is one float per key
+            self.one.update(uk, O.Updater.kGradient, acc)
+            return
+        # lens of the union keys: what the workers pulled (every worker pulled the same state)
+        lens_u = np.ones(len(uk), np.int32)
+        for r in range(self.N):
+            uniq = st["loc"][r][0]
+            lens = st["pulled"][r][1]
+            lens_u[np.searchsorted(uk, uniq)] = lens
+        parts = []
+        for i in range(len(uk)):
+            parts.append(acc[i] if lens_u[i] > 1 else acc[i, :1])
+        self.one.update(uk, O.Updater.kGradient, np.concatenate(parts), lens_u)
+
+    step = ShardedOracle.step
+
+    def entry(self, key):
+        return self.one.entry(key)
+
+
 class StaleOracle:
     """The pipelined schedule of the sharded store (difacto_amd.dist.ShardedPipeline): step
     t+1's count pushes and pulls are answered before step t's gradient pushes are applied,
@@ -133,8 +233,8 @@ class StaleOracle:
     (sgd_learner.cc:310-312, kvstore_dist.h:137-150), made deterministic:
         begin(t), pull(t), push(t-1), compute(t), ..., push(T-1) at flush()."""
 
-    def __init__(self, nranks, **kw):
-        self.so = ShardedOracle(nranks, **kw)
+    def __init__(self, nranks, agg="ranks", **kw):
+        self.so = AggOracle(nranks, **kw) if agg == "sum" else ShardedOracle(nranks, **kw)
         self.N, self.up, self.d = self.so.N, self.so.up, self.so.d
         self.pending = None
 

@@ -20,6 +20,7 @@ class CpuShard:
         self.d = self.up.V_dim
         self.S = self.d + 4
         self.ctx = SimpleNamespace(V_dim=self.d)
+        self.agg_sum = False  # the mock serves push_agg=ranks (one Update per pushing worker)
         self.losses, self.aucs = [], []
         self.wslot = [None, None]
         self.oslot = [{}, {}]

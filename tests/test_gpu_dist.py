@@ -42,15 +42,56 @@ def _batches(nranks, steps, rows=300, nnz=8, key_space=3000, seed=0):
                          ragged=(s == 2)) for r in range(nranks)] for s in range(steps)]
 
 
+def _oracle(N, kw, agg, stale=False):
+    if stale:
+        return DO.StaleOracle(N, agg=agg, **kw)
+    return DO.AggOracle(N, **kw) if agg == "sum" else DO.ShardedOracle(N, **kw)
+
+
+def _check_servers(name, ctxs, so, keys, N, agg):
+    """every server's counters and a sample of its entries against the oracle: per server
+    (push_agg=ranks: N SGDUpdaters) or against the one updater the servers together restate
+    (push_agg=sum: shared rand_r stream, keys split by owner)"""
+    from difacto_amd import hotpath as H
+    n_v = 0
+    stats = [H.Store(c).stats() for c in ctxs]
+    if agg == "sum":
+        one = so.up[0]
+        assert sum(st["n_keys"] for st in stats) == one.size(), name
+        assert sum(st["new_w"] for st in stats) == one.new_w, name
+        for g in range(N):
+            assert stats[g]["seed"] == one.seed, (name, g)
+    for g in range(N):
+        up = so.up[0] if agg == "sum" else so.up[g]
+        if agg != "sum":
+            assert stats[g]["seed"] == up.seed, (name, g)
+            assert stats[g]["n_keys"] == up.size(), (name, g)
+            assert stats[g]["new_w"] == up.new_w, (name, g)
+        own = keys[DO.owner_of(keys, N) == g]
+        for k in own[:: max(1, len(own) // 150)]:
+            e = up.entry(k)
+            got = H.Store(ctxs[g]).entry(k)
+            assert (got is None) == (e is None)
+            if e is None:
+                continue
+            assert close(got[0], e[0]), (name, g, k)
+            assert (got[1] is None) == (e[1] is None), (name, g, k)
+            if e[1] is not None:
+                n_v += 1
+                assert close(got[1], e[1]), (name, g, k)
+    return n_v
+
+
+@pytest.mark.parametrize("agg", ["sum", "ranks"])
 @pytest.mark.parametrize("name", list(CFGS))
-def test_sharded_loopback_matches_sharded_oracle(name):
+def test_sharded_loopback_matches_sharded_oracle(name, agg):
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
     N, kw = CFGS[name]
-    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    ctxs = [H.Context(0, max_keys=1 << 15, push_agg=agg, **kw) for _ in range(N)]
     shards = [DI.Shard(c, N) for c in ctxs]
     comm = DI.LoopbackComm(N)
-    so = DO.ShardedOracle(N, **kw)
+    so = _oracle(N, kw, agg)
     batches = _batches(N, 5)
     for s, step in enumerate(batches):
         push = s < 3
@@ -70,24 +111,7 @@ def test_sharded_loopback_matches_sharded_oracle(name):
             assert pr["auc"] == pytest.approx(want_auc, rel=1e-4, abs=1e-6)
     keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
                                      for step in batches for b in step]))
-    n_v = 0
-    for g in range(N):
-        st = H.Store(ctxs[g]).stats()
-        assert st["seed"] == so.up[g].seed, (name, g)
-        assert st["n_keys"] == so.up[g].size(), (name, g)
-        assert st["new_w"] == so.up[g].new_w, (name, g)
-        own = keys[DO.owner_of(keys, N) == g]
-        for k in own[:: max(1, len(own) // 150)]:
-            e = so.up[g].entry(k)
-            got = H.Store(ctxs[g]).entry(k)
-            assert (got is None) == (e is None)
-            if e is None:
-                continue
-            assert close(got[0], e[0]), (name, g, k)
-            assert (got[1] is None) == (e[1] is None), (name, g, k)
-            if e[1] is not None:
-                n_v += 1
-                assert close(got[1], e[1]), (name, g, k)
+    n_v = _check_servers(name, ctxs, so, keys, N, agg)
     if kw.get("V_dim", 0) > 0:
         assert n_v > 0
     for c in ctxs:
@@ -98,17 +122,18 @@ def test_sharded_loopback_matches_sharded_oracle(name):
 PIPE_JOBS = [(3, True), (3, True), (3, False), (4, False), (3, False), (3, False)]
 
 
+@pytest.mark.parametrize("agg", ["sum", "ranks"])
 @pytest.mark.parametrize("name", ["fm_v4", "fm_v16", "logit", "fm_v8_n6", "fm_v64_n8"])
-def test_sharded_pipeline_matches_stale_oracle(name):
+def test_sharded_pipeline_matches_stale_oracle(name, agg):
     """the pipelined schedule (two step slots in flight, Localizer lane ahead, push of step t
     after the pull of step t+1) against oracle/dist_oracle.StaleOracle"""
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
     N, kw = CFGS[name]
-    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    ctxs = [H.Context(0, max_keys=1 << 15, push_agg=agg, **kw) for _ in range(N)]
     shards = [DI.Shard(c, N) for c in ctxs]
     pipe = DI.ShardedPipeline(shards, DI.LoopbackComm(N))
-    so = DO.StaleOracle(N, **kw)
+    so = _oracle(N, kw, agg, stale=True)
     batches = _batches(N, len(PIPE_JOBS))
     live, got, want = [], [], []  # batches stay alive until the pipeline is flushed
     for s, (step, (job, cnt)) in enumerate(zip(batches, PIPE_JOBS)):
@@ -130,27 +155,59 @@ def test_sharded_pipeline_matches_stale_oracle(name):
         assert pr["loss"] == pytest.approx(sum(w[r][0] for w in want), rel=1e-4)
     keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
                                      for step in batches for b in step]))
-    n_v = 0
-    for g in range(N):
-        ctxs[g].sync()
-        st = H.Store(ctxs[g]).stats()
-        assert st["seed"] == so.up[g].seed, (name, g)
-        assert st["n_keys"] == so.up[g].size(), (name, g)
-        assert st["new_w"] == so.up[g].new_w, (name, g)
-        own = keys[DO.owner_of(keys, N) == g]
-        for k in own[:: max(1, len(own) // 150)]:
-            e = so.up[g].entry(k)
-            got = H.Store(ctxs[g]).entry(k)
-            assert (got is None) == (e is None)
-            if e is None:
-                continue
-            assert close(got[0], e[0]), (name, g, k)
-            assert (got[1] is None) == (e[1] is None), (name, g, k)
-            if e[1] is not None:
-                n_v += 1
-                assert close(got[1], e[1]), (name, g, k)
+    for c in ctxs:
+        c.sync()
+    n_v = _check_servers(name, ctxs, so, keys, N, agg)
     if kw.get("V_dim", 0) > 0:
         assert n_v > 0
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.parametrize("N", [2, 3, 8])
+def test_sharded_sum_equals_one_step_on_concatenated_batches(N):
+    """SURVEY.md §8(e)'s parity claim, pinned to the single-GPU reference semantics: with
+    push_agg=sum, one N-GPU step equals one reference local step (the oracle's SGDUpdater +
+    FMLoss, sgd_learner.cc:201-317) on the concatenation of the N batches in rank order.  Loss
+    is additive over rows; the model keys, V rows, rand_r state and new_w are exact; values
+    differ only by the order the gradient sums run in (per worker, then across workers), so
+    they are compared at 1e-4."""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    kw = dict(V_dim=8, V_threshold=2, lr=0.1, V_lr=0.05, l1=0.2, seed=13)
+    ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    one = O.Updater(**kw)
+    for s in range(6):
+        step = [D.synthetic(400, 12, 6000, binary=(r % 2 == 0), seed=900 + 37 * s + r)
+                for r in range(N)]
+        push = s < 2
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=push)
+        cat = D.concat(step)
+        loss, _ = one.train_step(cat.offs, cat.ids, cat.vals, cat.labels, push_cnt=push)
+        got = sum(H.progress(c)["loss"] for c in ctxs)
+        assert got == pytest.approx(loss, rel=1e-5), (N, s)
+    stats = [H.Store(c).stats() for c in ctxs]
+    assert sum(st["n_keys"] for st in stats) == one.size()
+    assert sum(st["new_w"] for st in stats) == one.new_w
+    assert all(st["seed"] == one.seed for st in stats)
+    cat_keys = np.unique(O.localize(cat.offs, cat.ids)[0])
+    n_v = 0
+    for k in cat_keys:
+        g = int(DO.owner_of(np.array([k], np.uint64), N)[0])
+        e = one.entry(k)
+        got = H.Store(ctxs[g]).entry(k)
+        assert (got is None) == (e is None)
+        if e is None:
+            continue
+        assert close(got[0], e[0], rtol=1e-4), k
+        assert (got[1] is None) == (e[1] is None), k
+        if e[1] is not None:
+            n_v += 1
+            assert close(got[1], e[1], rtol=1e-4), k
+    assert n_v > 0
     for c in ctxs:
         c.close()
 
@@ -162,7 +219,7 @@ def test_sharded_save_load_parts(tmp_path):
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
     N, kw = CFGS["fm_v4"]
-    ctxs = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    ctxs = [H.Context(0, max_keys=1 << 15, push_agg="ranks", **kw) for _ in range(N)]
     shards = [DI.Shard(c, N) for c in ctxs]
     comm = DI.LoopbackComm(N)
     so = DO.ShardedOracle(N, **kw)
@@ -192,7 +249,7 @@ def test_sharded_save_load_parts(tmp_path):
                 assert close(a[1], b[1])
         assert n_saved == up.size() > 0
     # fresh shards from the parts: one more step agrees with the original shards
-    ctx2 = [H.Context(0, max_keys=1 << 15, **kw) for _ in range(N)]
+    ctx2 = [H.Context(0, max_keys=1 << 15, push_agg="ranks", **kw) for _ in range(N)]
     sh2 = [DI.Shard(c, N) for c in ctx2]
     for r in range(N):
         sh2[r].load(prefix, r)
@@ -281,7 +338,7 @@ def test_sharded_empty_shard_and_batch():
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
     N, kw = 4, dict(V_dim=4, V_threshold=0, lr=0.1, l1=0.0)
-    ctxs = [H.Context(0, max_keys=1 << 12, **kw) for _ in range(N)]
+    ctxs = [H.Context(0, max_keys=1 << 12, push_agg="ranks", **kw) for _ in range(N)]
     shards = [DI.Shard(c, N) for c in ctxs]
     comm = DI.LoopbackComm(N)
     so = DO.ShardedOracle(N, **kw)
@@ -314,7 +371,7 @@ def _mp_worker(rank, world, port, q, pipelined=False):
         from difacto_amd import dist as DI
         from difacto_amd import hotpath as H
         _, kw = CFGS["fm_v4"]
-        ctx = H.Context(0, max_keys=1 << 15, **kw)
+        ctx = H.Context(0, max_keys=1 << 15, push_agg="ranks", **kw)
         shard = DI.Shard(ctx, world)
         comm = DI.TorchComm(device="cpu", stage_cpu=True)
         pipe = DI.ShardedPipeline([shard], comm) if pipelined else None
@@ -424,7 +481,8 @@ def test_sharded_eight_ranges_at_scale():
     from difacto_amd import hotpath as H
     N, rows, kb = 8, 20_000, 24
     kw = dict(V_dim=16, V_threshold=0, lr=0.1, V_lr=0.01, l1=0.0, seed=3)
-    ctxs = [H.Context(0, max_keys=(1 << kb) // N, max_vrows=(1 << kb) // N + 65536, **kw)
+    ctxs = [H.Context(0, max_keys=(1 << kb) // N, max_vrows=(1 << kb) // N + 65536,
+                      push_agg="ranks", **kw)
             for _ in range(N)]
     shards = [DI.Shard(c, N) for c in ctxs]
     comm = DI.LoopbackComm(N)

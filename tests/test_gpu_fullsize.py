@@ -124,10 +124,11 @@ def test_calcgrad_c5_chunked(H):
     Keys of <= 256 occurrences are summed in the reference's order (bit-exact up to expf);
     longer ones in 256-occurrence chunks combined in double.  Against float64 sums of the
     reference's own terms (tests/exact_sums.py) the device is within 1e-6 of each element's
-    condition scale (sum of |terms|); the reference itself (the oracle) is within ~1.2e-5 of that
-    scale there — its sequential float rounding — so the device and the reference agree within
-    1e-5 relative except where a sum cancels to far below its terms, and within 2e-5 of the
-    scale everywhere (measured: DESIGN.md, Determinism)."""
+    condition scale (sum of |terms|); the reference itself (the oracle) is up to ~3e-5 of that
+    scale away — its own sequential float rounding over ~45k terms — so the device and the
+    reference agree within 1e-5 relative except where a sum cancels far below its terms (84 of
+    8.07 M elements on the GPU box), and their distance is always the reference's rounding plus
+    at most 1e-6 of the scale (measured: DESIGN.md, Determinism)."""
     from tests.exact_sums import exact_calcgrad
     d = 128
     blk = D.synthetic(10_000, 39, 1 << 24, zipf=1.1, seed=7100)
@@ -162,8 +163,11 @@ def test_calcgrad_c5_chunked(H):
           "%.3g of scale; %d of %d elements beyond 1e-5 relative (cancelling sums)"
           % (dev_exact.max(), ref_exact.max(), (dev_ref / sc).max(), int((rel > RTOL).sum()),
              len(g)))
+    # the device sums every gradient to within 1e-6 of its condition scale ...
     assert dev_exact.max() <= 1e-6
-    assert (dev_ref / sc).max() <= 2e-5
-    # beyond 1e-5 relative only where the reference's own rounding is (sums that cancel)
-    assert np.all((rel <= RTOL) | (ref_exact * sc >= 0.1 * dev_ref))
+    # ... so its distance from the reference is the reference's own float rounding (measured
+    # up to ~3e-5 of the scale on hot keys of ~45k occurrences), plus at most that 1e-6
+    assert np.all(dev_ref <= ref_exact * sc + 1e-6 * sc)
+    # and beyond 1e-5 relative only where a sum cancels far below its terms
+    assert int((rel > RTOL).sum()) <= 1e-4 * len(g)
     c.close()

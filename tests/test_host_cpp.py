@@ -224,8 +224,9 @@ def _slice(blk, rows):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", ["sum", "ranks"])
 @pytest.mark.parametrize("pipelined", [1, 0])
-def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined):
+def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined, agg):
     """dfx_train shards=3: the C++ sharded store (dist_host.cc, loopback exchange) against the
     sharded oracle of the same schedule, on the batches the driver forms (shard r reads part
     r of 3, batches of 10 rows, shards step together with empty batches once done): per-epoch
@@ -240,7 +241,7 @@ def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined):
     args = [TRAIN_BIN, "data_in=" + DATA, "shards=%d" % N, "pipelined=%d" % pipelined,
             "num_jobs_per_epoch=1", "shuffle=0", "batch_size=%d" % bs,
             "max_num_epochs=%d" % epochs, "stop_rel_objv=0", "model_out=" + model, "has_aux=1",
-            "max_keys=65536"] + ["%s=%s" % kv for kv in kw.items()]
+            "max_keys=65536", "push_agg=" + agg] + ["%s=%s" % kv for kv in kw.items()]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
@@ -249,7 +250,10 @@ def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined):
     blk = D.read_libsvm(DATA)
     parts = [_part_rows(DATA, p, N) for p in range(N)]
     nsteps = max((len(p) + bs - 1) // bs for p in parts)
-    so = DO.StaleOracle(N, **kw) if pipelined else DO.ShardedOracle(N, **kw)
+    if pipelined:
+        so = DO.StaleOracle(N, agg=agg, **kw)
+    else:
+        so = DO.AggOracle(N, **kw) if agg == "sum" else DO.ShardedOracle(N, **kw)
     for ep in range(epochs):
         loss = 0.0
         for t in range(nsteps):
@@ -267,7 +271,7 @@ def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined):
         keys = np.unique(blk.ids)
         n = 0
         for k in O.localize(blk.offs, blk.ids)[0]:
-            a, b = up.entry(k), ups[g].entry(k)
+            a, b = up.entry(k), ups[0 if agg == "sum" else g].entry(k)
             if a is None:
                 continue
             n += 1
@@ -290,13 +294,13 @@ def test_train_driver_sharded_rccl_world1(tmp_path):
     env = dict(os.environ, DFX_COMM_ID_FILE=str(tmp_path / "id"))
     r = subprocess.run([TRAIN_BIN, "data_in=" + DATA, "shards=-1", "num_jobs_per_epoch=1",
                         "shuffle=0", "batch_size=25", "max_num_epochs=2", "stop_rel_objv=0",
-                        "max_keys=65536"] + ["%s=%s" % kv for kv in kw.items()],
+                        "max_keys=65536", "push_agg=sum"] + ["%s=%s" % kv for kv in kw.items()],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
            if "Training:" in l]
     blk = D.read_libsvm(DATA)
-    so = DO.StaleOracle(1, **kw)
+    so = DO.StaleOracle(1, agg="sum", **kw)
     for ep in range(2):
         loss = 0.0
         for t in range(4):

@@ -7,6 +7,7 @@
 // host overwrites its buffer at once, and the device copy is checked after a sync.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -55,6 +56,31 @@ int main() {
   std::printf("pageable hipMemcpyAsync reads the host buffer %s\n",
               bad_total ? "LATER (deferred): callers must keep it unchanged until the copy ran"
                         : "at the call (staged)");
+  // Does hipFree wait for kernels still running on another stream?  A workspace that grows
+  // (hipFree + hipMalloc at enqueue time) while the previous step's kernels are in flight
+  // would otherwise be freed under them.
+  {
+    float* buf = nullptr;
+    if (hipMalloc(&buf, 64 << 20) != hipSuccess) return 2;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, s);
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 40000000ull, buf);
+    (void)hipEventRecord(e1, s);
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipFree(buf);
+    const double free_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const bool done_at_return = hipEventQuery(e1) == hipSuccess;
+    (void)hipStreamSynchronize(s);
+    float kms = 0;
+    (void)hipEventElapsedTime(&kms, e0, e1);
+    std::printf("hipFree of a buffer in use by a %.1f ms kernel on a non-blocking stream returned "
+                "after %.1f ms, kernel %s at its return: hipFree %s\n",
+                kms, free_ms, done_at_return ? "finished" : "still running",
+                done_at_return ? "waits for in-flight work" : "does NOT wait for in-flight work");
+  }
   (void)hipFree(d);
   (void)hipFree(o);
   return 0;
