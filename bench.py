@@ -466,6 +466,32 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     ph = {p: sum(evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)) / args.steps
           for j, p in enumerate(names)}
     H.progress(ctx)
+    # the other collective schedules on the same batches, bulk synchronous (short runs): the
+    # all-to-all-v step, and the north_star's literal union all-gather / reduce-scatter
+    # (dist.rsag_step) — the measured baseline of the exchange design
+    colls = {}
+    if pipe is not None:
+        pipe.flush()
+    nb = min(args.steps, 20)
+    for cname, fn in (("a2a_sync", DI.sharded_step), ("rsag_sync", DI.rsag_step)):
+        if cname == "rsag_sync" and args.push_agg != "sum":
+            continue
+        for bt in batches[:2]:
+            fn([shard], [bt], comm, H.kTraining)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for bt in batches[:nb]:
+            fn([shard], [bt], comm, H.kTraining)
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t1
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=comm.cgroup)
+        dt = float(t.item())
+        colls[cname] = {"ms_per_step": round(dt / nb * 1e3, 4),
+                        "value": round(world * B * nb / dt, 1), "steps": nb}
+    H.progress(ctx)
     ctx.sync()
     st = H.Store(ctx).stats()
     tot = comm.allreduce_sum([[prog["loss"], prog["auc"], prog["nrows"], float(st["n_keys"]),
@@ -504,6 +530,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                      "algorithmic_bytes_per_launch": int(ab),
                      "launch_ms": round(fb_ms, 4)},
         "phases_ms_per_step_rank0": {p: round(v, 4) for p, v in ph.items()},
+        "collectives": dict({("a2a_sync" if args.sync else "a2a_pipelined"):
+                             {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                              "value": round(value, 1), "steps": args.steps}}, **colls),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         "train_loss_per_row": round(tot[0] / max(tot[2], 1), 6),
         "train_auc": round(tot[1] / max(tot[2], 1), 6),

@@ -100,6 +100,9 @@ _SIGS = {
     "dfx_dist_initv_local": (ctypes.c_int, [vp, ctypes.c_int, vp]),
     "dfx_dist_initv_draw": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int]),
     "dfx_dist_push_agg_sum": (ctypes.c_int, [vp]),
+    "dfx_dist_union": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]),
+    "dfx_dist_union_rows": (ctypes.c_int, [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int,
+                                           ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -219,6 +219,7 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   release_ws(c->aws);
   release_ws(c->ows[0]);
   release_ws(c->ows[1]);
+  release_ws(c->uws);
   for (auto h : c->dist_host)
     if (h) (void)hipHostFree(h);
   for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_loc[0], c->ev_loc[1],

@@ -718,6 +718,87 @@ __global__ void k_dist_initv_sum_finalize(const uint32_t* ftotal, const int64_t*
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
 }
 
+// Stable merge of sorted runs [runs[i], runs[i+1]) of *K (in place of the lane's keys0/1 and
+// vals0/1 ping-pong buffers): ceil(log2 n) rounds of pairwise tile merges.  On return *K is
+// the merged keys and *P their source indices (NULL when there was a single run: identity).
+static void merge_runs(const Lane& L, std::vector<int64_t> runs, const uint64_t** K,
+                       const uint32_t** P) {
+  Workspace& ws = *L.ws;
+  uint64_t* kb[2] = {ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>()};
+  uint32_t* vb[2] = {ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>()};
+  int sel = 0;
+  while (runs.size() > 2) {
+    const int m = (int)runs.size() - 1;
+    PairList pl{};
+    std::vector<int64_t> next;
+    int64_t nblk = 0;
+    for (int p = 0; 2 * p < m; ++p) {
+      pl.lo[p] = runs[2 * p];
+      pl.mid[p] = runs[std::min(2 * p + 1, m)];
+      pl.hi[p] = runs[std::min(2 * p + 2, m)];
+      pl.b0[p] = nblk;
+      nblk += (pl.hi[p] - pl.lo[p] + kMrgTile - 1) / kMrgTile;
+      next.push_back(runs[2 * p]);
+      pl.n = p + 1;
+    }
+    pl.b0[pl.n] = nblk;
+    next.push_back(runs[m]);
+    if (nblk > 0)
+      hipLaunchKernelGGL(k_merge_tiles, dim3((unsigned)nblk), dim3(kMrgNT), 0, L.stream, *K,
+                         *P, kb[sel], vb[sel], pl);
+    *K = kb[sel];
+    *P = vb[sel];
+    sel ^= 1;
+    runs.swap(next);
+  }
+}
+
+// ---- union-indexed collectives (the north_star's literal reduce-scatter / all-gather) -------
+// The union of every worker's keys, sorted: union[excl[i]] = K[i] at run heads; upos[src] =
+// the union position of the item the merge took from source index src
+__global__ void k_union_write(const uint64_t* K, const uint32_t* P, const uint32_t* excl,
+                              int64_t R, uint64_t* uni, uint32_t* upos) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= R) return;
+  const bool head = i == 0 || K[i] != K[i - 1];
+  const uint32_t u = head ? excl[i] : excl[i] - 1u;
+  if (head) uni[u] = K[i];
+  upos[P ? P[i] : (uint32_t)i] = u;
+}
+
+// out[r] = first union position owned by rank >= r (r <= nranks)
+__global__ void k_union_bounds(const uint64_t* uni, const uint32_t* n_uni, uint32_t nranks,
+                               int64_t* out) {
+  const uint32_t r = threadIdx.x;
+  if (r > nranks) return;
+  uint32_t lo = 0, hi = *n_uni;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (owner_of(uni[mid], nranks) < r) lo = mid + 1; else hi = mid;
+  }
+  out[r] = lo;
+}
+
+struct Bounds {
+  int n;
+  int64_t b[kMaxRanks + 1];
+};
+
+// a worker's key i <-> row (owner g) * M + (union position - bounds[g]) of a union-indexed,
+// owner-chunked buffer.  to_union: scatter src (the worker's rows) into dst (union rows);
+// else gather dst (the worker's rows) from src (union rows)
+__global__ void k_union_rows(const uint64_t* keys, const uint32_t* upos, int64_t U, Bounds bd,
+                             int64_t M, int width, int to_union, const float* src, float* dst) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 4) + threadIdx.x / 4;
+  const int l = threadIdx.x % 4;
+  if (i >= U) return;
+  const uint32_t g = owner_of(keys[i], (uint32_t)bd.n);
+  const int64_t row = (int64_t)g * M + ((int64_t)upos[i] - bd.b[g]);
+  const float* a = to_union ? src + i * width : src + row * width;
+  float* b = to_union ? dst + row * width : dst + i * width;
+  for (int k = l; k < width; k += 4) b[k] = a[k];
+}
+
 static int vec_group(int d) {
   if (d <= 0 || d % 4 != 0) return 0;
   int g = 1;
@@ -953,36 +1034,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   // stable merge of the N sorted runs (none for one run)
   const uint64_t* K = recv_keys;
   const uint32_t* Pm = nullptr;
-  {
-    std::vector<int64_t> runs(recv_offsets, recv_offsets + nranks + 1);
-    uint64_t* kb[2] = {ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>()};
-    uint32_t* vb[2] = {ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>()};
-    int sel = 0;
-    while (runs.size() > 2) {
-      const int m = (int)runs.size() - 1;
-      PairList pl{};
-      std::vector<int64_t> next;
-      int64_t nblk = 0;
-      for (int p = 0; 2 * p < m; ++p) {
-        pl.lo[p] = runs[2 * p];
-        pl.mid[p] = runs[std::min(2 * p + 1, m)];
-        pl.hi[p] = runs[std::min(2 * p + 2, m)];
-        pl.b0[p] = nblk;
-        nblk += (pl.hi[p] - pl.lo[p] + kMrgTile - 1) / kMrgTile;
-        next.push_back(runs[2 * p]);
-        pl.n = p + 1;
-      }
-      pl.b0[pl.n] = nblk;
-      next.push_back(runs[m]);
-      if (nblk > 0)
-        hipLaunchKernelGGL(k_merge_tiles, dim3((unsigned)nblk), dim3(kMrgNT), 0, OL.stream, K,
-                           Pm, kb[sel], vb[sel], pl);
-      K = kb[sel];
-      Pm = vb[sel];
-      sel ^= 1;
-      runs.swap(next);
-    }
-  }
+  merge_runs(OL, std::vector<int64_t>(recv_offsets, recv_offsets + nranks + 1), &K, &Pm);
   hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, OL.stream, K, R, flags);
   DFX_TRY(scan_u32(OL, flags, R, nuniq));
   c->dist_K[slot] = K;
@@ -1163,5 +1215,82 @@ int dfx_dist_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, i
 }
 
 int dfx_dist_push_agg_sum(dfx_ctx* ctx) { return ctx ? ctx->c.dist_sum : -1; }
+
+// The union of the workers' sorted unique keys (the literal north_star schedule: an all-gather
+// of keys, union-indexed all-gather of records and reduce-scatter of gradients).  runs: the
+// workers' key lists concatenated in rank order, run_offs[nruns+1] (host) their boundaries.
+// union_out (room for run_offs[nruns] keys) receives the sorted union, upos_out[i] the union
+// position of runs[i], bounds_out[nranks+1] (host) the union positions where each owner's
+// keys begin, *n_union (host) the union size.  Synchronises the context stream.
+int dfx_dist_union(dfx_ctx* ctx, const uint64_t* runs, const int64_t* run_offs, int nruns,
+                   int nranks, uint64_t* union_out, uint32_t* upos_out, int64_t* bounds_out,
+                   int64_t* n_union) {
+  DFX_CHECK_ARG(ctx && run_offs && bounds_out && n_union, "null argument");
+  DFX_CHECK_ARG(nruns >= 1 && nruns <= kMaxRanks && nranks >= 1 && nranks <= kMaxRanks,
+                "dist_union: 1 <= nruns, nranks <= 64");
+  Context* c = &ctx->c;
+  DFX_TRY(pipeline_init(c));
+  const int64_t R = run_offs[nruns];
+  DFX_CHECK_ARG(R < 0x7FFFFFFFll, "dist_union: too many keys");
+  for (int r = 0; r < nruns; ++r)
+    DFX_CHECK_ARG(run_offs[r + 1] >= run_offs[r] && run_offs[0] == 0, "dist_union: bad offsets");
+  if (R == 0) {
+    *n_union = 0;
+    for (int r = 0; r <= nranks; ++r) bounds_out[r] = 0;
+    return DFX_OK;
+  }
+  DFX_CHECK_ARG(runs && union_out && upos_out, "dist_union: null buffer");
+  Workspace& ws = c->uws;
+  DFX_TRY(ws.keys0.ensure(R * 8));
+  DFX_TRY(ws.keys1.ensure(R * 8));
+  DFX_TRY(ws.vals0.ensure(R * 4));
+  DFX_TRY(ws.vals1.ensure(R * 4));
+  DFX_TRY(ws.flags.ensure((R + 1) * 4));
+  DFX_TRY(ws.cnt.ensure(8 * (kMaxRanks + 2)));
+  const Lane L{c->stream, &ws, c->ds, &c->ds->err};
+  const uint64_t* K = runs;
+  const uint32_t* P = nullptr;
+  merge_runs(L, std::vector<int64_t>(run_offs, run_offs + nruns + 1), &K, &P);
+  uint32_t* flags = ws.flags.as<uint32_t>();
+  uint32_t* total = ws.cnt.as<uint32_t>();
+  const dim3 grid((R + kDNT - 1) / kDNT);
+  hipLaunchKernelGGL(k_dist_heads, grid, dim3(kDNT), 0, c->stream, K, R, flags);
+  DFX_TRY(scan_u32(L, flags, R, total));
+  hipLaunchKernelGGL(k_union_write, grid, dim3(kDNT), 0, c->stream, K, P, flags, R, union_out,
+                     upos_out);
+  int64_t* bd = reinterpret_cast<int64_t*>(ws.cnt.as<char>() + 8);
+  hipLaunchKernelGGL(k_union_bounds, dim3(1), dim3(kMaxRanks + 1), 0, c->stream, union_out,
+                     total, (uint32_t)nranks, bd);
+  std::vector<int64_t> h(kMaxRanks + 2);
+  DFX_HIP(hipMemcpyAsync(h.data(), ws.cnt.as<char>(), 8 * (nranks + 2), hipMemcpyDeviceToHost,
+                         c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  *n_union = (int64_t)(uint32_t)(h[0] & 0xFFFFFFFFll);
+  for (int r = 0; r <= nranks; ++r) bounds_out[r] = h[1 + r];
+  return DFX_OK;
+}
+
+// rows of `width` floats between a worker's key order (its sorted unique keys) and a
+// union-indexed buffer of nranks owner chunks of M rows (row = owner * M + union position -
+// bounds[owner]): to_union = 1 scatters the worker's rows there (the reduce-scatter's input;
+// other rows untouched), 0 gathers them back (from the all-gathered records)
+int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos, int64_t U,
+                        const int64_t* bounds, int nranks, int64_t M, int width, int to_union,
+                        const float* src, float* dst) {
+  DFX_CHECK_ARG(ctx && bounds, "null argument");
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks && width >= 1, "dist_union_rows: bad sizes");
+  if (U == 0) return DFX_OK;
+  DFX_CHECK_ARG(keys && upos && src && dst, "dist_union_rows: null buffer");
+  for (int r = 0; r < nranks; ++r)
+    DFX_CHECK_ARG(bounds[r + 1] - bounds[r] <= M, "dist_union_rows: a chunk exceeds M rows");
+  Bounds bd{};
+  bd.n = nranks;
+  for (int r = 0; r <= nranks; ++r) bd.b[r] = bounds[r];
+  Context* c = &ctx->c;
+  hipLaunchKernelGGL(k_union_rows, dim3((unsigned)((U + 63) / 64)), dim3(256), 0, c->stream,
+                     keys, upos, U, bd, M, width, to_union, src, dst);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
 
 }  // extern "C"

@@ -154,6 +154,7 @@ struct Context {
   // shared with the fused step), owner split counts + U of the batch in pinned memory
   Workspace ows[2];
   DevState* ods[2] = {nullptr, nullptr};
+  Workspace uws;  // the union of the workers' keys (dfx_dist_union)
   int64_t dist_R[2] = {0, 0}, dist_rows[2] = {0, 0}, dist_U[2] = {-1, -1};
   std::vector<int64_t> dist_offs[2];
   // owner segments of a slot not yet built: owner_begin leaves them to the pull, which

@@ -125,6 +125,28 @@ class Shard:
     def owner_push(self, recv_grads, slot=0):
         check(_lib.lib().dfx_dist_owner_push(self.ctx.h, slot, _p(recv_grads)))
 
+    # the literal north_star exchange (rsag_step) ------------------------------------------
+    def union(self, runs, run_offs):
+        """-> (sorted union of the runs, union position of every run item, owner bounds of the
+        union (host list, nranks + 1))"""
+        R = int(run_offs[-1])
+        dev = self.ctx.device
+        uni = torch.empty(max(R, 1), dtype=torch.int64, device=dev)
+        upos = torch.empty(max(R, 1), dtype=torch.int32, device=dev)
+        offs = (ctypes.c_int64 * len(run_offs))(*[int(o) for o in run_offs])
+        bounds = (ctypes.c_int64 * (self.nranks + 1))()
+        n = ctypes.c_int64(0)
+        check(_lib.lib().dfx_dist_union(self.ctx.h, _p(runs), offs, len(run_offs) - 1,
+                                        self.nranks, _p(uni), _p(upos), bounds,
+                                        ctypes.byref(n)))
+        return uni[:n.value], upos[:R], list(bounds)
+
+    def union_rows(self, keys, upos, bounds, M, width, to_union, src, dst):
+        bd = (ctypes.c_int64 * len(bounds))(*bounds)
+        check(_lib.lib().dfx_dist_union_rows(self.ctx.h, _p(keys), _p(upos), keys.numel(), bd,
+                                             self.nranks, int(M), int(width), int(to_union),
+                                             _p(src), _p(dst)))
+
     # push_agg=sum: InitV ranked over all owners (after a count push and after every push)
     def initv_local(self, slot=0):
         """-> device int64[1]: this owner's InitV request count"""
@@ -216,6 +238,37 @@ class TorchComm:
         out = [torch.empty_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t, group=self.cgroup)
         return [[int(o[self.rank]) for o in out]]
+
+    def allgather_rows(self, tensors, M, row):
+        """the north_star's all-gather: every rank's first rows (up to M rows of `row`
+        elements, padded to M) -> [world * M * row], rank-major"""
+        (x,) = tensors
+        buf = torch.zeros(M * row, dtype=x.dtype, device=x.device)
+        buf[:x.numel()] = x
+        if self.world == 1:
+            return [buf]
+        if self.stage_cpu:
+            out = [torch.empty(M * row, dtype=x.dtype) for _ in range(self.world)]
+            self.dist.all_gather(out, buf.cpu(), group=self.group)
+            return [torch.cat(out).to(x.device)]
+        out = torch.empty(self.world * M * row, dtype=x.dtype, device=x.device)
+        self.dist.all_gather_into_tensor(out, buf, group=self.group)
+        return [out]
+
+    def reduce_scatter_sum(self, tensors, M, row):
+        """the north_star's reduce-scatter: every rank's [world * M * row] buffer summed, rank
+        g receiving chunk g"""
+        (x,) = tensors
+        if self.world == 1:
+            return [x]
+        if self.stage_cpu:  # gloo has no reduce-scatter: all-reduce, keep this rank's chunk
+            t = x.cpu()
+            self.dist.all_reduce(t, group=self.group)
+            c = M * row
+            return [t[self.rank * c:(self.rank + 1) * c].to(x.device)]
+        out = torch.empty(M * row, dtype=x.dtype, device=x.device)
+        self.dist.reduce_scatter_tensor(out, x, group=self.group)
+        return [out]
 
     def allgather_i64(self, tensors):
         """every rank's device int64[1] -> device int64[world] in rank order (stream-ordered
@@ -346,6 +399,22 @@ class LoopbackComm:
         allc = torch.cat([t.reshape(1) for t in tensors])
         return [allc for _ in tensors]
 
+    def allgather_rows(self, tensors, M, row):
+        bufs = []
+        for x in tensors:
+            b = torch.zeros(M * row, dtype=x.dtype, device=x.device)
+            b[:x.numel()] = x
+            bufs.append(b)
+        allb = torch.cat(bufs)
+        return [allb for _ in tensors]
+
+    def reduce_scatter_sum(self, tensors, M, row):
+        acc = tensors[0].clone()
+        for x in tensors[1:]:
+            acc += x  # float32, in rank order
+        c = M * row
+        return [acc[g * c:(g + 1) * c] for g in range(self.world)]
+
     def exchange_counts(self, send_splits):
         return [[send_splits[r][g] for r in range(self.world)] for g in range(self.world)]
 
@@ -435,6 +504,82 @@ def sharded_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_in
         mark(6)
     mark(7)
     return [sum(s) for s in recv]  # keys served per shard (for accounting)
+
+
+def rsag_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index=MAX_INDEX,
+              preds=None):
+    """One bulk-synchronous step over the north_star's literal collectives:
+    an all-gather of the workers' keys forms the sorted union, every owner pulls its union
+    slice, an all-gather of the union-indexed records serves every worker's pull, and a
+    reduce-scatter of union-indexed gradient rows (and, in epoch 0, counts) hands each owner
+    the workers' summed rows of its slice — one Update per key (push_agg=sum semantics, oracle
+    AggOracle).  The measured baseline beside the all-to-all-v schedule: its exchanges move
+    union-sized, padded buffers instead of only the keys each worker touches."""
+    n = len(shards)
+    N = shards[0].nranks
+    assert all(sh.agg_sum for sh in shards), "rsag_step needs push_agg=sum"
+    want_cnt = bool(push_cnt) and shards[0].ctx.V_dim > 0
+    for i in range(n):
+        shards[i].localize(dblks[i], want_cnt, 0, max_index)
+    loc = [shards[i].localize_wait(0) for i in range(n)]
+    dev = shards[0].ctx.device
+    # 1. every worker's key count, then its keys (padded to the largest), all-gathered
+    cnts = comm.allgather_i64([torch.tensor([l[0].numel()], dtype=torch.int64, device=dev)
+                               for l in loc])
+    Us = [int(v) for v in cnts[0].cpu().tolist()]
+    Umax = max(max(Us), 1)
+    allk = comm.allgather_rows([l[0] for l in loc], Umax, 1)
+    run_offs = [0]
+    for u in Us:
+        run_offs.append(run_offs[-1] + u)
+    S = shards[0].S
+    outs = []
+    for i in range(n):
+        r = comm.ranks()[i]
+        ak = allk[i]
+        runs = torch.cat([ak[g * Umax:g * Umax + Us[g]] for g in range(N)])
+        uni, upos, bounds = shards[i].union(runs, run_offs)
+        outs.append((uni, upos[run_offs[r]:run_offs[r + 1]], bounds))
+    bounds = outs[0][2]
+    M = max(max(bounds[g + 1] - bounds[g] for g in range(N)), 1)
+    ranks = comm.ranks()
+    own = [outs[i][0][bounds[ranks[i]]:bounds[ranks[i] + 1]] for i in range(n)]
+    # 2. epoch 0: the workers' counts, union-indexed and reduce-scattered to the owners
+    rcnt = [None] * n
+    if want_cnt:
+        bufs = []
+        for i in range(n):
+            b = torch.zeros(N * M, dtype=torch.float32, device=dev)
+            shards[i].union_rows(loc[i][0], outs[i][1], bounds, M, 1, 1, loc[i][1], b)
+            bufs.append(b)
+        rcnt = comm.reduce_scatter_sum(bufs, M, 1)
+    for i in range(n):
+        R = own[i].numel()
+        shards[i].owner_begin(own[i], [R] + [0] * (N - 1),
+                              rcnt[i][:R] if want_cnt else None, 0)
+    if want_cnt:
+        _initv(shards, comm, 0)
+    # 3. the owners' records of their slices, all-gathered (union-indexed)
+    recs = comm.allgather_rows([sh.owner_pull(0) for sh in shards], M, S)
+    grads = []
+    for i in range(n):
+        U = loc[i][0].numel()
+        pulled = torch.empty(max(U * S, 1), dtype=torch.float32, device=dev)
+        shards[i].union_rows(loc[i][0], outs[i][1], bounds, M, S, 0, recs[i], pulled)
+        grads.append(shards[i].fwd_bwd(dblks[i], pulled[:U * S], job_type, 0,
+                                       preds[i] if preds else None))
+    if job_type != kTraining:
+        return
+    # 4. union-indexed gradient rows, reduce-scattered: each owner gets the summed rows
+    bufs = []
+    for i in range(n):
+        b = torch.zeros(N * M * S, dtype=torch.float32, device=dev)
+        shards[i].union_rows(loc[i][0], outs[i][1], bounds, M, S, 1, grads[i], b)
+        bufs.append(b)
+    rg = comm.reduce_scatter_sum(bufs, M, S)
+    for i in range(n):
+        shards[i].owner_push(rg[i][:own[i].numel() * S], 0)
+    _initv(shards, comm, 0)
 
 
 class ShardedPipeline:

@@ -269,6 +269,18 @@ int dfx_dist_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev);
 int dfx_dist_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
                         int nranks);
 int dfx_dist_push_agg_sum(dfx_ctx* ctx);
+/* The literal north_star exchange: all-gather of the workers' keys, their
+ * sorted union (dfx_dist_union), an all-gather of the owners' union-indexed pull records and a
+ * reduce-scatter of union-indexed gradient rows, each owner's chunk of M rows holding its keys
+ * in union order (dfx_dist_union_rows maps a worker's rows to and from that layout).  Kept as
+ * the measured baseline beside the all-to-all-v schedule; the owner phases are the same
+ * (owner_begin over its union slice as one run, push_agg=sum). */
+int dfx_dist_union(dfx_ctx* ctx, const uint64_t* runs, const int64_t* run_offs, int nruns,
+                   int nranks, uint64_t* union_out, uint32_t* upos_out, int64_t* bounds_out,
+                   int64_t* n_union);
+int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos, int64_t U,
+                        const int64_t* bounds, int nranks, int64_t M, int width, int to_union,
+                        const float* src, float* dst);
 
 #ifdef __cplusplus
 }

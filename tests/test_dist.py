@@ -279,3 +279,53 @@ def test_gloo_world2_pipeline_matches_stale_oracle():
                 n_v += 1
                 assert np.array_equal(V, e[1])
         assert n_v > 0
+
+
+def _coll_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = DI.TorchComm(device="cpu", stage_cpu=True)
+        M, row = 3, 2
+        x = torch.arange(rank * 10, rank * 10 + 2 * row, dtype=torch.float32)  # 2 rows
+        ag = comm.allgather_rows([x], M, row)[0]
+        buf = torch.full((world * M * row,), float(rank + 1))
+        rs = comm.reduce_scatter_sum([buf], M, row)[0]
+        ai = comm.allgather_i64([torch.tensor([rank + 5], dtype=torch.int64)])[0]
+        q.put((rank, ag.tolist(), rs.tolist(), ai.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_torchcomm_union_collectives_gloo():
+    """the rsag schedule's collectives over torch.distributed (world_size 2, gloo): padded
+    all-gather of rows, reduce-scatter of union-indexed rows (all-reduce + own chunk on gloo),
+    and the all-gather of the owners' InitV counts"""
+    import torch.multiprocessing as mp
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_coll_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ag, rs, ai = q.get(timeout=100)
+            res[r] = (ag, rs, ai)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs)
+    want_ag = [0, 1, 2, 3, 0, 0, 10, 11, 12, 13, 0, 0]
+    for r in range(world):
+        ag, rs, ai = res[r]
+        assert ag == want_ag
+        assert rs == [3.0] * 6  # 1 + 2 summed, this rank's chunk of M * row
+        assert ai == [5, 6]

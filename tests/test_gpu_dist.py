@@ -500,3 +500,37 @@ def test_sharded_eight_ranges_at_scale():
         assert st["n_keys"] == so.up[g].size() and st["seed"] == so.up[g].seed, g
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("name", ["fm_v4", "fm_v16", "logit", "fm_v64_n8"])
+def test_rsag_step_matches_agg_oracle(name):
+    """the north_star's literal schedule (dist.rsag_step: all-gather of keys -> union,
+    union-indexed all-gather of records, reduce-scatter of union-indexed gradients and counts)
+    against AggOracle — the same semantics as the all-to-all-v step with push_agg=sum"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N, kw = CFGS[name]
+    ctxs = [H.Context(0, max_keys=1 << 15, push_agg="sum", **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.AggOracle(N, **kw)
+    batches = _batches(N, 5)
+    for s, step in enumerate(batches):
+        push = s < 3
+        job = H.kValidation if s == 3 else H.kTraining
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        preds = [torch.zeros(step[r].size, dtype=torch.float32, device=ctxs[r].device)
+                 for r in range(N)]
+        DI.rsag_step(shards, dbs, comm, job, push_cnt=push, preds=preds)
+        out = so.step(step, push_cnt=push, train=job == H.kTraining)
+        for r in range(N):
+            assert close(preds[r].cpu().numpy(), out[r][2]), (name, s, r)
+            assert H.progress(ctxs[r])["loss"] == pytest.approx(out[r][0], rel=1e-4)
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0]
+                                     for step in batches for b in step]))
+    n_v = _check_servers(name, ctxs, so, keys, N, "sum")
+    if kw.get("V_dim", 0) > 0:
+        assert n_v > 0
+    for c in ctxs:
+        c.sync()
+        c.close()
