@@ -62,6 +62,9 @@ def parse():
                          "share that priority's hardware queues, whose packets run in order: "
                          "a high-priority compute stream keeps the step's kernels off the "
                          "queues of RCCL's (normal-priority) streams")
+    ap.add_argument("--ctx", default="",
+                    help="extra context kwargs k=v,... (A/B of execution choices, e.g. "
+                         "sort_pack=0)")
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-batch", type=int, default=10_000)
     return ap.parse_args()
@@ -208,8 +211,9 @@ def main():
 
     B, k, kb, d = args.batch, args.nnz, args.key_bits, args.vdim
     keyspace = 1 << kb
+    extra = dict(kv.split("=", 1) for kv in args.ctx.split(",") if kv)
     ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
-                    max_keys=keyspace, max_vrows=keyspace)
+                    max_keys=keyspace, max_vrows=keyspace, **extra)
     ctx.reserve(B, B * k)
     lib = H._lib.lib()
 

@@ -140,6 +140,12 @@ __device__ inline float4 ent_state(const Entry* e) {
   const float4 a = *reinterpret_cast<const float4*>(e);  // w, vrow, sqrt_g, z
   return make_float4(a.x, a.z, a.w, e->fea_cnt);          // {w, sqrt_g, z, fea_cnt}
 }
+// a gradient update's write-back: {w, vrow, sqrt_g, z} as one 16-byte store (fea_cnt does not
+// change in Update(kGradient); vrow is written back as read — InitV sets it later, in order)
+__device__ inline void ent_store_hot(Entry* e, float4 s, int vrow) {
+  *reinterpret_cast<float4*>(e) = make_float4(s.x, __int_as_float(vrow), s.y, s.z);
+}
+
 // writes back {w, sqrt_g, z, fea_cnt}; vrow is untouched
 __device__ inline void ent_set_state(Entry* e, float4 s) {
   e->w = s.x;

@@ -52,6 +52,7 @@ struct Kw {
   long bwd_lds = -1;    // bwd_lds=<bytes>: LDS reserved per backward block (-1: default cap)
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
+  int sort_pack = 1;    // sort_pack=0: the Localizer sorts 12-byte (key, row) pairs
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -86,6 +87,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "xvp_row") kw->xvp_row = atoi(cv) != 0;
     else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
     else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;
+    else if (k == "sort_pack") kw->sort_pack = atoi(cv) != 0;
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
       else if (v == "ranks") kw->dist_sum = 0;
@@ -173,6 +175,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->bwd_lds = kw.bwd_lds;
   c->autogrow = kw.autogrow;
   c->dist_sum = kw.dist_sum;
+  c->sort_pack = kw.sort_pack;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

@@ -85,94 +85,7 @@ __global__ void k_dist_worker_finalize(DevState* ds, int64_t B) {
   ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
 }
 
-// ---- owner: received keys -> unique segments -----------------------------------------------
-// The receive buffer is N sorted runs (one per source rank, in rank order), so the owner's
-// key order is a stable merge of the runs: ceil(log2 N) rounds of pairwise merges (run 2p
-// before run 2p+1 on equal keys = rank order).  Payload = received index.
-//
-// A block merges one tile of 2048 outputs of one pair: two threads find where the tile's
-// first and last merge-path diagonals cross the pair (binary searches in global memory), the
-// block stages that A and B stretch (keys + payloads) in LDS, every thread finds its own
-// diagonal in LDS and merges 8 outputs, and the tile goes out through LDS in order.  (One
-// global binary search per thread made every round ~5x slower: ~20 dependent random reads
-// per 8 outputs.)
-constexpr int kMrgNT = 256, kMrgItems = 8, kMrgTile = kMrgNT * kMrgItems;
-constexpr int kMaxPairs = kMaxRanks / 2 + 1;
-
-struct PairList {
-  int n;
-  int64_t lo[kMaxPairs], mid[kMaxPairs], hi[kMaxPairs];  // pair p: A = [lo, mid), B = [mid, hi)
-  int64_t b0[kMaxPairs + 1];                              // first tile (block) of pair p
-};
-
-// how many of the first `diag` outputs of merging A (na items) and B (nb) come from A (A wins
-// ties): the merge-path split
-template <typename KeyAt>
-__device__ inline int64_t merge_split(KeyAt key, int64_t a, int64_t b, int64_t na, int64_t nb,
-                                      int64_t diag) {
-  int64_t lo = diag - nb > 0 ? diag - nb : 0, hi = diag < na ? diag : na;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (key(a + m) <= key(b + diag - 1 - m)) lo = m + 1; else hi = m;
-  }
-  return lo;
-}
-
-__global__ __launch_bounds__(kMrgNT) void k_merge_tiles(const uint64_t* __restrict__ kin,
-                                                        const uint32_t* __restrict__ vin,
-                                                        uint64_t* __restrict__ kout,
-                                                        uint32_t* __restrict__ vout,
-                                                        PairList pl) {
-  __shared__ uint64_t sk[kMrgTile];
-  __shared__ uint32_t sv[kMrgTile];
-  __shared__ int64_t s_split[2];
-  int p = 0;
-  while (p + 1 < pl.n && pl.b0[p + 1] <= (int64_t)blockIdx.x) ++p;
-  const int64_t a0 = pl.lo[p], a1 = pl.mid[p], b1 = pl.hi[p];
-  const int64_t na = a1 - a0, nb = b1 - a1;
-  const int64_t d0 = ((int64_t)blockIdx.x - pl.b0[p]) * kMrgTile;
-  const int64_t d1 = d0 + kMrgTile < na + nb ? d0 + kMrgTile : na + nb;
-  if (threadIdx.x < 2) {
-    auto gkey = [&](int64_t i) { return kin[i]; };
-    s_split[threadIdx.x] = merge_split(gkey, a0, a1, na, nb, threadIdx.x == 0 ? d0 : d1);
-  }
-  __syncthreads();
-  const int64_t ia0 = s_split[0], ia1 = s_split[1];
-  const int la = (int)(ia1 - ia0), lb = (int)((d1 - ia1) - (d0 - ia0));
-  const int n = la + lb;
-  for (int j = threadIdx.x; j < n; j += kMrgNT) {
-    const int64_t g = j < la ? a0 + ia0 + j : a1 + (d0 - ia0) + (j - la);
-    sk[j] = kin[g];
-    sv[j] = vin ? vin[g] : (uint32_t)g;
-  }
-  __syncthreads();
-  const int dt = threadIdx.x * kMrgItems < n ? threadIdx.x * kMrgItems : n;
-  auto lkey = [&](int64_t i) { return sk[i]; };
-  int i = (int)merge_split(lkey, 0, la, la, lb, dt), j = dt - i;
-  uint64_t rk[kMrgItems];
-  uint32_t rv[kMrgItems];
-#pragma unroll
-  for (int q = 0; q < kMrgItems; ++q) {
-    if (dt + q < n) {
-      const bool takeA = i < la && (j >= lb || sk[i] <= sk[la + j]);
-      const int src = takeA ? i++ : la + j++;
-      rk[q] = sk[src];
-      rv[q] = sv[src];
-    }
-  }
-  __syncthreads();  // every thread is done reading the staged runs
-#pragma unroll
-  for (int q = 0; q < kMrgItems; ++q)
-    if (dt + q < n) {
-      sk[dt + q] = rk[q];
-      sv[dt + q] = rv[q];
-    }
-  __syncthreads();
-  for (int t = threadIdx.x; t < n; t += kMrgNT) {
-    kout[a0 + d0 + t] = sk[t];
-    vout[a0 + d0 + t] = sv[t];
-  }
-}
+// ---- owner: received keys -> unique segments (sort.hip merge_runs: stable tile merges)
 
 __global__ void k_dist_heads(const uint64_t* K, int64_t R, uint32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -718,41 +631,6 @@ __global__ void k_dist_initv_sum_finalize(const uint32_t* ftotal, const int64_t*
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
 }
 
-// Stable merge of sorted runs [runs[i], runs[i+1]) of *K (in place of the lane's keys0/1 and
-// vals0/1 ping-pong buffers): ceil(log2 n) rounds of pairwise tile merges.  On return *K is
-// the merged keys and *P their source indices (NULL when there was a single run: identity).
-static void merge_runs(const Lane& L, std::vector<int64_t> runs, const uint64_t** K,
-                       const uint32_t** P) {
-  Workspace& ws = *L.ws;
-  uint64_t* kb[2] = {ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>()};
-  uint32_t* vb[2] = {ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>()};
-  int sel = 0;
-  while (runs.size() > 2) {
-    const int m = (int)runs.size() - 1;
-    PairList pl{};
-    std::vector<int64_t> next;
-    int64_t nblk = 0;
-    for (int p = 0; 2 * p < m; ++p) {
-      pl.lo[p] = runs[2 * p];
-      pl.mid[p] = runs[std::min(2 * p + 1, m)];
-      pl.hi[p] = runs[std::min(2 * p + 2, m)];
-      pl.b0[p] = nblk;
-      nblk += (pl.hi[p] - pl.lo[p] + kMrgTile - 1) / kMrgTile;
-      next.push_back(runs[2 * p]);
-      pl.n = p + 1;
-    }
-    pl.b0[pl.n] = nblk;
-    next.push_back(runs[m]);
-    if (nblk > 0)
-      hipLaunchKernelGGL(k_merge_tiles, dim3((unsigned)nblk), dim3(kMrgNT), 0, L.stream, *K,
-                         *P, kb[sel], vb[sel], pl);
-    *K = kb[sel];
-    *P = vb[sel];
-    sel ^= 1;
-    runs.swap(next);
-  }
-}
-
 // ---- union-indexed collectives (the north_star's literal reduce-scatter / all-gather) -------
 // The union of every worker's keys, sorted: union[excl[i]] = K[i] at run heads; upos[src] =
 // the union position of the item the merge took from source index src
@@ -963,14 +841,16 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>(); a.XVp = ws.XVp.as<float>();
   a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
+  // AUC on its own lane beside the backward (as in the fused step): the forward writes the
+  // snapshot of (pred, label) once the previous AUC released the lane's buffers
+  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  DFX_TRY(auc_reserve(c->aws, B));
+  a.auc_key = c->aws.ak0.as<uint32_t>();
+  a.auc_lab = c->aws.av0.as<uint32_t>();
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   int nblk = 0;
   DFX_TRY(launch_fwd_records(a, c->stream, &nblk));
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
-  // AUC on its own lane beside the backward (as in the fused step): a snapshot of (pred,
-  // label) on the main stream, joined by the next snapshot / dfx_sync / dfx_progress_read
-  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
-  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
-  DFX_TRY(auc_snapshot(AL, c->stream, B, b->label, pred));
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true));

@@ -245,6 +245,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           a.pred[r] = pr;
           double yy = a.label[r] > 0 ? 1.0 : -1.0;
           loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+          if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
+            uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
+            a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
+          }
         }
       }
       if (d > 0) {
@@ -598,7 +603,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur);
       }
       if (l == 0) {
-        if (!dead) ent_set_state(a.T.ent + sl, e);
+        if (!dead) ent_store_hot(a.T.ent + sl, e, vrow);
         dnew = dead ? 0 : dw;
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
         const bool need =

@@ -38,6 +38,9 @@ struct FwdArgs {
   // reads XV_*p from (one random row instead of two)
   int xs;
   double* loss_part;     // fused: per-block partial sums of Evaluate
+  // fused: the AUC lane's snapshot (orderable pred key, label > 0), written by the forward
+  uint32_t* auc_key;
+  uint32_t* auc_lab;
 };
 
 struct BwdArgs {

@@ -181,6 +181,7 @@ struct Context {
   int xvp_row = 1;    // p rides in the XV*p rows (kwarg xvp_row)
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
   int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
+  int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
   // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
   CapGuard capg;
@@ -218,10 +219,38 @@ inline void prof_mark(Context* c, int m) {
 // their XOR); kSortCountsReady — the producer of the keys already added the counts of every
 // 8-bit digit position into ws.os_parts()[block % kOsParts] (begin_bit must be 0).
 constexpr int kSortDiffIsOrAnd = 1, kSortCountsReady = 2;
+// (u64 keys, u32 row payloads, bits [0, 64)): flags |= kSortPackRows(rb8) lets the sort carry
+// each item as one u64 when the varying key bits fit beside rb8 row bits (a multiple of 8);
+// sortmeta[25] then says so (sort_packed / sort_unpack) and the payload buffers are unused
+inline constexpr int kSortPackRows(int rb8) { return rb8 << 8; }
+constexpr int kSortMetaPack = 25;
+__device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
+// the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
+__device__ inline void sort_unpack(const unsigned* meta, uint64_t and_mask, uint64_t w,
+                                   uint64_t* key, uint32_t* row) {
+  const unsigned pk = meta[kSortMetaPack];
+  const int lo8 = (int)((pk >> 8) & 0xFFu), rb8 = (int)((pk >> 16) & 0xFFu);
+  const uint64_t win = (rb8 == 0 ? ~0ull : (~0ull >> rb8)) << lo8;  // the window, key bits
+  *key = (and_mask & ~win) | (((w >> rb8) << lo8) & win);
+  *row = (uint32_t)(w & ((1ull << rb8) - 1));
+}
+// what equal keys share in a sorted item (packed: the key window above the row)
+__device__ inline uint64_t sort_key_bits(const unsigned* meta, uint64_t w) {
+  const unsigned pk = meta[kSortMetaPack];
+  return pk ? (w >> ((pk >> 16) & 0xFFu)) : w;
+}
 template <typename K, typename P>
 int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int begin_bit,
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
                      const uint32_t* n_dev = nullptr, int flags = 0);
+
+// Stable merge of sorted u64 key runs [runs[i], runs[i+1]) of *K on lane L (ping-pong in the
+// lane's keys0/keys1 and vals0/vals1, sized by the caller): pairwise LDS-tiled merge rounds,
+// the earlier run winning ties.  On return *K holds the merged keys and *P their payloads
+// (*P on entry: the runs' payloads, or NULL for the source index).  At most 240 runs.
+void merge_runs(const Lane& L, std::vector<int64_t> runs, const uint64_t** K,
+                const uint32_t** P);
+constexpr int kMaxMergeRuns = 240;
 
 // exclusive scan of u32 values in place over n entries (n host-known); total -> *total_dev
 // n_dev (optional): a device count; entries at index >= *n_dev are treated as zero.
@@ -272,13 +301,15 @@ int table_unclump(Context* c);
 int table_set_ranges(Context* c, int nranks);
 int step_reserve(Context* c, int64_t rows, int64_t nnz);  // ws_reserve + the step's lanes
 int loc_reserve(Workspace& w, int64_t nnz);              // a Localizer's buffers
+int auc_reserve(Workspace& w, int64_t rows);             // the AUC lane's buffers
 
 // store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
 // nds: the device state whose u_count holds the count when n_host < 0
 // gate (optional, device): the number of set flags, or any nonzero; zero skips the pass
+// finalize = false: the caller advances the seed and the V-row count itself (by *total_dev)
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
               const uint32_t* slot, const DevState* nds = nullptr,
-              const uint32_t* gate = nullptr);
+              const uint32_t* gate = nullptr, bool finalize = true);
 // fused Update(kFeaCount): one segment per unique key (count = segment length = nds->u_count)
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
                      const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,

@@ -120,7 +120,10 @@ __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const 
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
-    if (idx < n) s += (idx == 0 || K[idx] != K[idx - 1]) ? 1u : 0u;
+    if (idx < n)
+      s += (idx == 0 || sort_key_bits(ds->sortmeta, K[idx]) !=
+                            sort_key_bits(ds->sortmeta, K[idx - 1]))
+               ? 1u : 0u;
   }
   uint32_t tot;
   block_excl_scan<kLocNT>(s, lds, &tot);
@@ -152,6 +155,9 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   const uint64_t* K = s1 ? a.k1 : a.k0;
   const uint64_t* P = s1 ? a.p1 : a.p0;
   const uint32_t* Q = s1 ? a.q1 : a.q0;
+  // packed items (sort.hip, kSortPackRows): one u64 holds the key window and the row
+  const bool packed = sort_packed(a.ds->sortmeta);
+  const uint64_t andm = a.ds->and_mask;
   const int64_t n = a.n;
   const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint64_t k[kLocItems];
@@ -163,7 +169,13 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     h[i] = 0;
     if (idx < n) {
       k[i] = K[idx];
-      h[i] = (idx == 0 || k[i] != K[idx - 1]) ? 1u : 0u;
+      h[i] = (idx == 0 || sort_key_bits(a.ds->sortmeta, k[i]) !=
+                              sort_key_bits(a.ds->sortmeta, K[idx - 1]))
+                 ? 1u : 0u;
+      if (packed) {
+        uint32_t row;
+        sort_unpack(a.ds->sortmeta, andm, k[i], &k[i], &row);
+      }
     }
     s += h[i];
   }
@@ -192,7 +204,10 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     for (int i = 0; i < kLocItems; ++i) {
       const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
       if (idx < n) {
-        if (Q) {
+        if (packed) {
+          a.occ_row[idx] = (uint32_t)(K[idx] & ((1ull << ((a.ds->sortmeta[kSortMetaPack] >> 16) &
+                                                             0xFFu)) - 1));
+        } else if (Q) {
           a.occ_row[idx] = Q[idx];
         } else {
           const uint64_t p = P[idx];
@@ -295,9 +310,13 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                      dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits
   if (narrow) {
+    // rows travel packed beside the key bits that vary, when they fit (sort.hip)
+    int rb8 = 8;
+    while (rb8 < 32 && (B - 1) >> rb8) rb8 += 8;
     DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, k0, q0, k1, q1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
-                                                  kSortDiffIsOrAnd | kSortCountsReady)));
+                                                  kSortDiffIsOrAnd | kSortCountsReady |
+                                                      (c->sort_pack ? kSortPackRows(rb8) : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,

@@ -6,6 +6,8 @@
 // integer (double up to 2^53); the reference accumulates it in float, so the two agree to
 // float rounding (ties between equal predictions are implementation-defined in the
 // reference's unstable std::sort; ours keep input order).
+#include <vector>
+
 #include "internal.h"
 
 namespace dfx {
@@ -24,11 +26,9 @@ __global__ void k_auc_keys(int64_t B, const float* label, const float* pred, uin
   v[i] = label[i] > 0 ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* v0, const uint32_t* v1,
-                                                    int64_t n, const DevState* ds,
+__global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* V, int64_t n,
                                                     uint32_t* tiles) {
   __shared__ uint32_t lds[kMNT / kWave + 1];
-  const uint32_t* V = ds->sortmeta[31] ? v1 : v0;
   const int64_t base = (int64_t)blockIdx.x * kMTile + (int64_t)threadIdx.x * kMItems;
   uint32_t s = 0;
 #pragma unroll
@@ -38,12 +38,13 @@ __global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* v0, const ui
   if (threadIdx.x == 0) tiles[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(kMNT) void k_auc_area(const uint32_t* v0, const uint32_t* v1,
-                                                   int64_t n, const DevState* ds,
-                                                   const uint32_t* tilebase, double* part) {
+// per tile of the sorted labels: every negative adds the positives ranked below it (the
+// tile's base from the scan of tile sums), summed exactly in double (integers below 2^53)
+__global__ __launch_bounds__(kMNT) void k_auc_area_tiles(const uint32_t* V, int64_t n,
+                                                         const uint32_t* tilebase,
+                                                         double* part) {
   __shared__ uint32_t lds[kMNT / kWave + 1];
   __shared__ double red[kMNT / kWave];
-  const uint32_t* V = ds->sortmeta[31] ? v1 : v0;
   const int64_t base = (int64_t)blockIdx.x * kMTile + (int64_t)threadIdx.x * kMItems;
   uint32_t lab[kMItems];
   uint32_t s = 0;
@@ -97,35 +98,34 @@ int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred) {
   Workspace& ws = *L.ws;
   if (B <= 0) return DFX_OK;
-  DFX_TRY(ws.ak0.ensure(B * 4));
-  DFX_TRY(ws.ak1.ensure(B * 4));
-  DFX_TRY(ws.av0.ensure(B * 4));
-  DFX_TRY(ws.av1.ensure(B * 4));
+  DFX_TRY(auc_reserve(ws, B));
   hipLaunchKernelGGL(k_auc_keys, dim3((B + 255) / 256), dim3(256), 0, st, B, label, pred,
                      ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>());
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-// ---- the AUC lane: a stable sort without inter-block waits, then one counting pass ---------
-// Beside the backward the AUC needs only to finish within a step, and it should take as few
-// CU slots and as little memory traffic from the backward as possible (a look-back sort's
-// spinning blocks would park on CUs; a search per (item, tile) pair floods them):
-//   k_auc_runs   one block per 4096-item tile (input order): stable LSD sort of the tile in
-//                LDS, sorted keys and labels out
-//   k_auc_merge  log2(tiles) rounds of stable pairwise merge-path merges (the earlier run wins
-//                ties), so the result is the global stable sort by key
-//   k_auc_area   one block: positives before each negative, summed exactly in double (every
-//                partial is an integer) -> AUC*n (flip, P = 0 / n rule)
+// ---- the AUC lane: a stable sort with few, short launches, then a tiled counting pass -------
+// Beside the backward the AUC needs only to finish within a step, taking as few CU slots and
+// as little memory traffic from the backward as possible (a look-back sort's spinning blocks
+// would park on CUs; a search per (item, tile) pair floods them):
+//   k_auc_runs        one block per 4096-item tile (input order): stable LSD sort of the tile
+//                     in LDS; out: u64 keys (orderable pred << 32 | input index) and labels
+//   merge_runs        log2(tiles) rounds of LDS-tiled pairwise merges (sort.hip): with the
+//                     input index in the key every comparison is strict, so the result is
+//                     the global stable sort by pred
+//   k_auc_tiles / k_auc_area_tiles / k_auc_final   positives per 2048-item tile, their scan,
+//                     each negative's count of positives ranked below it (exact in double),
+//                     AUC*n with the flip and the P = 0 / n rule
 // The result is deterministic and equals the global stable sort's rank-sum.
 constexpr int kArNT = 256, kArItems = 16, kArTile = kArNT * kArItems;  // 4096
 
 __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* __restrict__ key,
                                                    const uint32_t* __restrict__ lab,
-                                                   uint32_t* __restrict__ skey,
+                                                   uint64_t* __restrict__ skey,
                                                    uint32_t* __restrict__ slab) {
   __shared__ uint32_t lk[2][kArTile];
-  __shared__ uint8_t ll[2][kArTile];
+  __shared__ uint16_t ll[2][kArTile];  // (index in the tile << 1) | label
   __shared__ uint32_t wcnt[kArNT / kWave][256];
   __shared__ uint32_t lds[kArNT / kWave + 1];
   const int t = threadIdx.x, w = t / kWave, l = lane_id();
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
   const int m = (int)((n - tb) < kArTile ? (n - tb) : kArTile);
   for (int i = t; i < kArTile; i += kArNT) {
     lk[0][i] = i < m ? key[tb + i] : 0u;
-    ll[0][i] = i < m ? (uint8_t)lab[tb + i] : (uint8_t)0;
+    ll[0][i] = i < m ? (uint16_t)((i << 1) | (lab[tb + i] & 1u)) : (uint16_t)0;
   }
   __syncthreads();
   int src = 0;
@@ -189,99 +189,60 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
     __syncthreads();
     src ^= 1;
   }
-  // the sorted tile out
+  // the sorted tile out: the input index breaks ties, keeping the sort stable across tiles
   for (int i = t; i < m; i += kArNT) {
-    skey[tb + i] = lk[src][i];
-    slab[tb + i] = ll[src][i];
+    const uint32_t q = ll[src][i];
+    skey[tb + i] = ((uint64_t)lk[src][i] << 32) | (uint64_t)(tb + (q >> 1));
+    slab[tb + i] = q & 1u;
   }
 }
 
-constexpr int kAmNT = 256, kAmItems = 8;  // merge: outputs per thread
-
-// one round: runs of width w, pair p = [2pw, 2pw + w) + [2pw + w, 2pw + 2w) (clamped to n)
-__global__ __launch_bounds__(kAmNT) void k_auc_merge(int64_t n, int64_t w,
-                                                    const uint32_t* __restrict__ kin,
-                                                    const uint32_t* __restrict__ lin,
-                                                    uint32_t* __restrict__ kout,
-                                                    uint32_t* __restrict__ lout) {
-  int64_t t = ((int64_t)blockIdx.x * kAmNT + threadIdx.x) * kAmItems;
-  if (t >= n) return;
-  const int64_t tend = t + kAmItems < n ? t + kAmItems : n;
-  const int64_t a0 = (t / (2 * w)) * (2 * w);
-  const int64_t a1 = a0 + w < n ? a0 + w : n;
-  const int64_t b1 = a0 + 2 * w < n ? a0 + 2 * w : n;
-  const int64_t na = a1 - a0, nb = b1 - a1, k = t - a0;
-  // merge path: how many of the first k outputs come from A (A wins ties)
-  int64_t lo = k - nb > 0 ? k - nb : 0, hi = k < na ? k : na;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (kin[a0 + m] <= kin[a1 + k - 1 - m]) lo = m + 1; else hi = m;
-  }
-  int64_t i = a0 + lo, j = a1 + (k - lo);
-  const int64_t stop = tend < b1 ? tend : b1;
-  for (; t < stop; ++t) {
-    const bool takeA = i < a1 && (j >= b1 || kin[i] <= kin[j]);
-    const int64_t src = takeA ? i++ : j++;
-    kout[t] = kin[src];
-    lout[t] = lin[src];
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_auc_area(int64_t n, const uint32_t* __restrict__ slab,
-                                                   double* out, int accumulate) {
-  __shared__ uint32_t lds[1024 / kWave + 1];
-  __shared__ double red[1024 / kWave];
-  double area = 0;
-  uint32_t carry = 0;
-  for (int64_t c = 0; c < n; c += 1024) {
-    const int64_t i = c + threadIdx.x;
-    const uint32_t y = i < n ? slab[i] : 0u;
-    uint32_t tot;
-    const uint32_t before = block_excl_scan<1024>(y, lds, &tot) + carry;
-    if (i < n && !y) area += (double)before;
-    carry += tot;
-  }
-  for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
-  if (lane_id() == 0) red[threadIdx.x / kWave] = area;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0;
-    for (int i = 0; i < 1024 / kWave; ++i) a += red[i];
-    const double P = (double)carry;
-    double r;
-    if (P == 0 || P == (double)n) {
-      r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
-    } else {
-      a /= P * ((double)n - P);
-      r = (a < 0.5 ? 1 - a : a) * (double)n;
-    }
-    *out = accumulate ? *out + r : r;
-  }
-}
-
-// AUC*n of the snapshot into *out_dev (accumulate: += ), on the lane's stream
+// AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate) {
   Workspace& ws = *L.ws;
   if (B <= 0) {
     if (!accumulate) DFX_HIP(hipMemsetAsync(out_dev, 0, sizeof(double), L.stream));
     return DFX_OK;
   }
-  const int ntiles = (int)((B + kArTile - 1) / kArTile);
-  // snapshot in (ak0 keys, av0 labels); ping-pong (ak1, av1) <-> (ak0, av0)
-  DFX_TRY(ws.ak1.ensure(B * 4));
-  DFX_TRY(ws.av1.ensure(B * 4));
-  uint32_t* k[2] = {ws.ak1.as<uint32_t>(), ws.ak0.as<uint32_t>()};
-  uint32_t* v[2] = {ws.av1.as<uint32_t>(), ws.av0.as<uint32_t>()};
-  hipLaunchKernelGGL(k_auc_runs, dim3(ntiles), dim3(kArNT), 0, L.stream, B, k[1], v[1], k[0],
-                     v[0]);
-  int cur = 0;
-  for (int64_t w = kArTile; w < B; w *= 2) {
-    const int64_t per = (int64_t)kAmNT * kAmItems;
-    hipLaunchKernelGGL(k_auc_merge, dim3((unsigned)((B + per - 1) / per)), dim3(kAmNT), 0,
-                       L.stream, B, w, k[cur], v[cur], k[cur ^ 1], v[cur ^ 1]);
-    cur ^= 1;
+  DFX_TRY(auc_reserve(ws, B));
+  const int64_t ntiles = (B + kArTile - 1) / kArTile;
+  uint64_t* k0 = ws.keys0.as<uint64_t>();
+  uint32_t* v0 = ws.vals0.as<uint32_t>();
+  // runs into (keys1, vals1): merge_runs ping-pongs through keys0 / keys1
+  uint64_t* kr = ws.keys1.as<uint64_t>();
+  uint32_t* vr = ws.vals1.as<uint32_t>();
+  hipLaunchKernelGGL(k_auc_runs, dim3((unsigned)ntiles), dim3(kArNT), 0, L.stream, B,
+                     ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), kr, vr);
+  const uint64_t* K = kr;
+  const uint32_t* V = vr;
+  if (ntiles > 1) {
+    if (ntiles <= kMaxMergeRuns) {
+      std::vector<int64_t> runs;
+      for (int64_t r = 0; r < ntiles; ++r) runs.push_back(r * kArTile);
+      runs.push_back(B);
+      // merge_runs writes keys0 first: the runs in keys1 are read in the first round only
+      merge_runs(L, runs, &K, &V);
+    } else {  // a very large batch: one radix sort of the (unique) u64 keys
+      DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, kr, vr, k0, v0, B, 0, 64, nullptr,
+                                                    L.ds->sortmeta)));
+      // the sorted pairs sit in (kr, vr) or (k0, v0), by sortmeta[31]: read back which
+      uint32_t sel = 0;
+      DFX_HIP(hipMemcpyAsync(&sel, &L.ds->sortmeta[31], 4, hipMemcpyDeviceToHost, L.stream));
+      DFX_HIP(hipStreamSynchronize(L.stream));
+      V = sel ? v0 : vr;
+    }
   }
-  hipLaunchKernelGGL(k_auc_area, dim3(1), dim3(1024), 0, L.stream, B, v[cur], out_dev,
+  const int64_t nt = (B + kMTile - 1) / kMTile;
+  DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (nt + 2)));
+  DFX_TRY(ws.dscratch.ensure(sizeof(double) * (nt + 8)));
+  uint32_t* tiles = ws.tiles.as<uint32_t>();
+  uint32_t* npos = tiles + nt + 1;
+  hipLaunchKernelGGL(k_auc_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V, B, tiles);
+  scan_tiles_top(L, tiles, nt, npos);
+  double* part = ws.dscratch.as<double>();
+  hipLaunchKernelGGL(k_auc_area_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V, B,
+                     tiles, part);
+  hipLaunchKernelGGL(k_auc_final, dim3(1), dim3(1024), 0, L.stream, part, nt, npos, B, out_dev,
                      accumulate ? 1 : 0);
   DFX_HIP(hipGetLastError());
   return DFX_OK;

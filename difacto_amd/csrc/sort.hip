@@ -17,6 +17,9 @@
 // device-side count (n_dev) bounds the items when only the device knows it.
 #include <cstdlib>
 
+#include <algorithm>
+#include <vector>
+
 #include "internal.h"
 
 namespace dfx {
@@ -34,14 +37,24 @@ constexpr unsigned kOsNone = 0xFFFFFFFFu;
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
 // The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
 constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = 24;
+// [25]: packed mode (kSortPackRows): 1 | lo8 << 8 | rb8 << 16 — the items travel as one u64
+// ((key >> lo8) << rb8 | row), see k_os_plan; 0: (key, payload) pairs
+constexpr int kMetaPack = 25;
 
 // Reduce the partial digit counts (parts[kOsParts][8][256], digit position p = bits
 // [begin + 8p, +8)) into counts[q] for the active passes q, zero the parts for the next sort,
 // and write the plan.  diff: the bits that vary, or (or_and) a pointer to {OR, AND} of the keys.
+// pack_rb8 > 0 (u64 keys with u32 row payloads, begin_bit 0, end_bit 64): when the varying key
+// bits fit beside a row of pack_rb8 bits, the items are sorted as one u64 each: the varying
+// window of the key from its lowest varying 8-bit digit (lo8) up, shifted down by lo8, above the
+// row — (key >> lo8) << rb8 | row.  Digit boundaries are kept (lo8, rb8 multiples of 8), so the
+// counts of key digit p serve packed digit p - lo8/8 + rb8/8; the first active pass packs as it
+// loads, later passes and the consumers read 8 bytes per item instead of 12.
 __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff, int or_and,
                                                    int npasses, int begin_bit, int end_bit,
                                                    unsigned int* meta, uint32_t* parts,
-                                                   uint32_t* counts, unsigned int* epoch) {
+                                                   uint32_t* counts, unsigned int* epoch,
+                                                   int pack_rb8) {
   __shared__ int s_pos[kOsMaxPasses];
   __shared__ int s_nq;
   const int t = threadIdx.x;
@@ -50,6 +63,13 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
     meta[kMetaEpoch] = ++*epoch;
     unsigned long long dm = ~0ull;
     if (diff) dm = or_and ? (diff[0] ^ diff[1]) : diff[0];
+    int lo8 = 0;
+    bool pack = false;
+    if (pack_rb8 > 0 && dm != 0) {
+      lo8 = (__ffsll((long long)dm) - 1) & ~7;
+      // the window is key bits [lo8, lo8 + 64 - rb8): every varying bit must be inside it
+      pack = ((dm >> lo8) >> (64 - pack_rb8)) == 0;
+    }
     int q = 0;
     for (int p = 0; p < npasses; ++p) {
       const int shift = begin_bit + 8 * p;
@@ -57,7 +77,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
       const unsigned long long dmask = (1ull << bits) - 1;
       if (((dm >> shift) & dmask) != 0) {
         s_pos[q] = p;
-        meta[q++] = (unsigned)shift | ((unsigned)bits << 16);
+        const int sh = pack ? shift - lo8 + pack_rb8 : shift;
+        meta[q++] = (unsigned)sh | ((unsigned)bits << 16);
       }
     }
     for (int r = q; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
@@ -65,6 +86,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
       meta[kMetaSrc + r] = (unsigned)(r & 1);
       meta[kMetaTile + r] = 0;
     }
+    meta[kMetaPack] = (pack && q > 0) ? (1u | ((unsigned)lo8 << 8) | ((unsigned)pack_rb8 << 16))
+                                      : 0u;
     meta[31] = (unsigned)(q & 1);
     s_nq = q;
   }
@@ -139,6 +162,10 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   K* kout = from1 ? k0 : k1;
   P* vout = from1 ? v0 : v1;
   const uint32_t tag = (meta[kMetaEpoch] * kOsMaxPasses + (unsigned)q) & 0x3FFFFFFFu;
+  // packed mode (k_os_plan): u64 items, the first pass packs (key, row) as it loads
+  const unsigned pk = (sizeof(K) == 8 && sizeof(P) == 4) ? meta[kMetaPack] : 0u;
+  const bool packed = pk != 0, pack_now = packed && q == 0;
+  const int lo8 = (int)((pk >> 8) & 0xFFu), rb8 = (int)((pk >> 16) & 0xFFu);
 
   constexpr int kBuf = sizeof(K) > sizeof(P) ? sizeof(K) : sizeof(P);
   __shared__ __attribute__((aligned(16))) unsigned char lbuf[(kOsNT * IT) * kBuf];
@@ -170,6 +197,14 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
     key[c] = idx < n ? kin[idx] : (K)0;
+  }
+  if (pack_now) {
+#pragma unroll
+    for (int c = 0; c < IT; ++c) {
+      const int64_t idx = wbase + c * kWave + l;
+      if (idx < n)
+        key[c] = (K)((((uint64_t)key[c] >> lo8) << rb8) | (uint64_t)(uint32_t)vin[idx]);
+    }
   }
 #pragma unroll
   for (int c = 0; c < IT; ++c) {
@@ -268,6 +303,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
       kout[gdig[d] + ((uint32_t)qi - lstart[d])] = kk;
     }
   }
+  if (packed) return;  // the payload rides in the key
   __syncthreads();
   // ---- payloads: the same permutation through the same LDS buffer
 #pragma unroll
@@ -307,9 +343,10 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   uint32_t* counts = ws.os_counts();
   unsigned int* epoch = &L.ds->sort_epoch;
   const int or_and = (flags & kSortDiffIsOrAnd) ? 1 : 0;
+  const int pack_rb8 = (sizeof(K) == 8 && sizeof(P) == 4) ? (flags >> 8) & 0xFF : 0;
   if (n <= 0 || end_bit <= begin_bit) {
     hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, 0,
-                       begin_bit, end_bit, sortmeta, parts, counts, epoch);
+                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
@@ -320,7 +357,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                        n_dev, begin_bit, npasses, parts);
   }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
-                     begin_bit, end_bit, sortmeta, parts, counts, epoch);
+                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8);
   for (int q = 0; q < npasses; ++q)
     hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems>), dim3((unsigned)ntiles), dim3(kOsNT), 0,
                        L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
@@ -336,6 +373,131 @@ DFX_SORT_INST(uint64_t, uint32_t)
 DFX_SORT_INST(uint64_t, uint64_t)
 DFX_SORT_INST(uint32_t, uint32_t)
 #undef DFX_SORT_INST
+
+// ---- stable merge of sorted runs (the sharded store's owner keys, the AUC lane) ------------
+// The receive buffer is N sorted runs (one per source rank, in rank order), so the owner's
+// key order is a stable merge of the runs: ceil(log2 N) rounds of pairwise merges (run 2p
+// before run 2p+1 on equal keys = rank order).  Payload = received index.
+//
+// A block merges one tile of 2048 outputs of one pair: two threads find where the tile's
+// first and last merge-path diagonals cross the pair (binary searches in global memory), the
+// block stages that A and B stretch (keys + payloads) in LDS, every thread finds its own
+// diagonal in LDS and merges 8 outputs, and the tile goes out through LDS in order.  (One
+// global binary search per thread made every round ~5x slower: ~20 dependent random reads
+// per 8 outputs.)
+constexpr int kMrgNT = 256, kMrgItems = 8, kMrgTile = kMrgNT * kMrgItems;
+// pairs per merge round: the PairList kernel argument stays below the 4 KB argument limit
+constexpr int kMaxPairs = 120;
+
+struct PairList {
+  int n;
+  int64_t lo[kMaxPairs], mid[kMaxPairs], hi[kMaxPairs];  // pair p: A = [lo, mid), B = [mid, hi)
+  int64_t b0[kMaxPairs + 1];                              // first tile (block) of pair p
+};
+
+// how many of the first `diag` outputs of merging A (na items) and B (nb) come from A (A wins
+// ties): the merge-path split
+template <typename KeyAt>
+__device__ inline int64_t merge_split(KeyAt key, int64_t a, int64_t b, int64_t na, int64_t nb,
+                                      int64_t diag) {
+  int64_t lo = diag - nb > 0 ? diag - nb : 0, hi = diag < na ? diag : na;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (key(a + m) <= key(b + diag - 1 - m)) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(kMrgNT) void k_merge_tiles(const uint64_t* __restrict__ kin,
+                                                        const uint32_t* __restrict__ vin,
+                                                        uint64_t* __restrict__ kout,
+                                                        uint32_t* __restrict__ vout,
+                                                        PairList pl) {
+  __shared__ uint64_t sk[kMrgTile];
+  __shared__ uint32_t sv[kMrgTile];
+  __shared__ int64_t s_split[2];
+  int p = 0;
+  while (p + 1 < pl.n && pl.b0[p + 1] <= (int64_t)blockIdx.x) ++p;
+  const int64_t a0 = pl.lo[p], a1 = pl.mid[p], b1 = pl.hi[p];
+  const int64_t na = a1 - a0, nb = b1 - a1;
+  const int64_t d0 = ((int64_t)blockIdx.x - pl.b0[p]) * kMrgTile;
+  const int64_t d1 = d0 + kMrgTile < na + nb ? d0 + kMrgTile : na + nb;
+  if (threadIdx.x < 2) {
+    auto gkey = [&](int64_t i) { return kin[i]; };
+    s_split[threadIdx.x] = merge_split(gkey, a0, a1, na, nb, threadIdx.x == 0 ? d0 : d1);
+  }
+  __syncthreads();
+  const int64_t ia0 = s_split[0], ia1 = s_split[1];
+  const int la = (int)(ia1 - ia0), lb = (int)((d1 - ia1) - (d0 - ia0));
+  const int n = la + lb;
+  for (int j = threadIdx.x; j < n; j += kMrgNT) {
+    const int64_t g = j < la ? a0 + ia0 + j : a1 + (d0 - ia0) + (j - la);
+    sk[j] = kin[g];
+    sv[j] = vin ? vin[g] : (uint32_t)g;
+  }
+  __syncthreads();
+  const int dt = threadIdx.x * kMrgItems < n ? threadIdx.x * kMrgItems : n;
+  auto lkey = [&](int64_t i) { return sk[i]; };
+  int i = (int)merge_split(lkey, 0, la, la, lb, dt), j = dt - i;
+  uint64_t rk[kMrgItems];
+  uint32_t rv[kMrgItems];
+#pragma unroll
+  for (int q = 0; q < kMrgItems; ++q) {
+    if (dt + q < n) {
+      const bool takeA = i < la && (j >= lb || sk[i] <= sk[la + j]);
+      const int src = takeA ? i++ : la + j++;
+      rk[q] = sk[src];
+      rv[q] = sv[src];
+    }
+  }
+  __syncthreads();  // every thread is done reading the staged runs
+#pragma unroll
+  for (int q = 0; q < kMrgItems; ++q)
+    if (dt + q < n) {
+      sk[dt + q] = rk[q];
+      sv[dt + q] = rv[q];
+    }
+  __syncthreads();
+  for (int t = threadIdx.x; t < n; t += kMrgNT) {
+    kout[a0 + d0 + t] = sk[t];
+    vout[a0 + d0 + t] = sv[t];
+  }
+}
+
+// Stable merge of sorted runs [runs[i], runs[i+1]) of *K (in place of the lane's keys0/1 and
+// vals0/1 ping-pong buffers): ceil(log2 n) rounds of pairwise tile merges.  On return *K is
+// the merged keys and *P their source indices (NULL when there was a single run: identity).
+void merge_runs(const Lane& L, std::vector<int64_t> runs, const uint64_t** K,
+                const uint32_t** P) {
+  Workspace& ws = *L.ws;
+  uint64_t* kb[2] = {ws.keys0.as<uint64_t>(), ws.keys1.as<uint64_t>()};
+  uint32_t* vb[2] = {ws.vals0.as<uint32_t>(), ws.vals1.as<uint32_t>()};
+  int sel = 0;
+  while (runs.size() > 2) {
+    const int m = (int)runs.size() - 1;
+    PairList pl{};
+    std::vector<int64_t> next;
+    int64_t nblk = 0;
+    for (int p = 0; 2 * p < m; ++p) {
+      pl.lo[p] = runs[2 * p];
+      pl.mid[p] = runs[std::min(2 * p + 1, m)];
+      pl.hi[p] = runs[std::min(2 * p + 2, m)];
+      pl.b0[p] = nblk;
+      nblk += (pl.hi[p] - pl.lo[p] + kMrgTile - 1) / kMrgTile;
+      next.push_back(runs[2 * p]);
+      pl.n = p + 1;
+    }
+    pl.b0[pl.n] = nblk;
+    next.push_back(runs[m]);
+    if (nblk > 0)
+      hipLaunchKernelGGL(k_merge_tiles, dim3((unsigned)nblk), dim3(kMrgNT), 0, L.stream, *K,
+                         *P, kb[sel], vb[sel], pl);
+    *K = kb[sel];
+    *P = vb[sel];
+    sel ^= 1;
+    runs.swap(next);
+  }
+}
 
 // ---- device-wide exclusive scan (reduce -> scan tile sums -> scan + apply) -------------
 constexpr int kScanNT = 256;

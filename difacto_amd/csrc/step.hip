@@ -70,13 +70,18 @@ int loc_reserve(Workspace& w, int64_t nnz) {
   return DFX_OK;
 }
 
-// the AUC lane (metric.hip auc_finish: keys and labels, double-buffered for the merges)
-static int auc_reserve(Workspace& w, int64_t rows) {
+// the AUC lane (metric.hip auc_finish): the snapshot (keys ak0, labels av0) and the merge
+// ping-pong buffers (u64 keys, u32 labels)
+int auc_reserve(Workspace& w, int64_t rows) {
   if (rows < 1) rows = 1;
+  if (w.rows >= rows && w.ak0.p) return DFX_OK;
   DFX_TRY(w.ak0.ensure(rows * 4));
-  DFX_TRY(w.ak1.ensure(rows * 4));
   DFX_TRY(w.av0.ensure(rows * 4));
-  DFX_TRY(w.av1.ensure(rows * 4));
+  DFX_TRY(w.keys0.ensure(rows * 8));
+  DFX_TRY(w.keys1.ensure(rows * 8));
+  DFX_TRY(w.vals0.ensure(rows * 4));
+  DFX_TRY(w.vals1.ensure(rows * 4));
+  DFX_TRY(w.os_reserve((rows + 2047) / 2048));  // the radix-sort fallback's look-back words
   w.rows = rows;
   return DFX_OK;
 }
@@ -160,13 +165,20 @@ __global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ 
   pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent + s);
 }
 
-__global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B) {
+__global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B,
+                                const uint32_t* initv_total, int d, int64_t vcap) {
   // sgd::Progress: nrows, loss (sgd_learner.cc:213-229); the AUC lane adds its own
   ds->prog[0] += (double)B;
   ds->prog[1] += ds->scratch[3];
   ds->sum_u += (double)bds->u_count;
   ds->n_steps += 1;
   ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
+  if (initv_total) {  // the InitV pass's rand_r advance and V rows (k_initv_finalize's work)
+    const uint32_t n = *initv_total;
+    ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * n);
+    const unsigned long long nv = ds->n_vrows + n;
+    ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+  }
 }
 
 // One minibatch, pipelined over three streams:
@@ -266,15 +278,18 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
+  // the forward writes the AUC lane's snapshot of (pred, label): the lane's buffers are free
+  // once the previous AUC is done.  (A last-block loss reduction inside the forward cost more
+  // than the launch it saves: the device-scope fence of each block writes back its XCD's L2.)
+  a.auc_key = c->aws.ak0.as<uint32_t>();
+  a.auc_lab = c->aws.av0.as<uint32_t>();
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk));
   prof_mark(c, 4);
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
 
-  // ---- aux lane: AUC of this batch's predictions, beside the backward.  The snapshot (on
-  // this stream) waits for the previous AUC to release the lane's buffers.
-  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
-  DFX_TRY(auc_snapshot(AL, c->stream, B, b->label, pred));
+  // ---- aux lane: AUC of this batch's predictions, beside the backward
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   lane_mark(c, 2, c->aux_stream);
@@ -295,11 +310,13 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     prof_mark(c, 6);
-    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init));
+    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false));
   } else {
     prof_mark(c, 6);
   }
-  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, bds, B);
+  const bool initv = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 && d > 0;
+  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, bds, B,
+                     initv ? total : nullptr, d, c->T.vcap);
   DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
   DFX_TRY(cap_record(c));
   prof_mark(c, 7);

@@ -85,7 +85,7 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot, const DevState* nds, const uint32_t* gate) {
+              const uint32_t* slot, const DevState* nds, const uint32_t* gate, bool finalize) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
   DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count, gate));
@@ -93,8 +93,9 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
   hipLaunchKernelGGL(k_initv, dim3((unsigned)(gate && nb > 1024 ? 1024 : nb)), dim3(kStNT), 0,
                      c->stream,
                      n_host, flags, total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate);
-  hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
-                     c->T.vcap, c->ds);
+  if (finalize)
+    hipLaunchKernelGGL(k_initv_finalize, dim3(1), dim3(1), 0, c->stream, total_dev, c->P.V_dim,
+                       c->T.vcap, c->ds);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -337,12 +337,16 @@ def test_fused_matches_oracle_rcv1(H, rcv1, cfg):
     assert st.stats()["seed"] == up.seed
 
 
-def test_fused_criteo_like_vs_oracle(H):
+@pytest.mark.parametrize("key_space,pack", [(1 << 16, 1), (1 << 63, 1), (1 << 16, 0)])
+def test_fused_criteo_like_vs_oracle(H, key_space, pack):
+    """2^16 ids: the Localizer's sort carries (varying key bits, row) packed in one u64;
+    ids over 63 bits: every key bit varies, the sort falls back to (key, row) pairs on the
+    device; sort_pack=0: pairs always"""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    c = H.Context(0, max_keys=1 << 18, **cfg)
+    c = H.Context(0, max_keys=1 << 18, sort_pack=pack, **cfg)
     up = O.Updater(**cfg)
     for step in range(4):
-        blk = D.synthetic(3000, 39, 1 << 16, seed=50 + step)
+        blk = D.synthetic(3000, 39, key_space, seed=50 + step)
         loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
                                          push_cnt=(step < 2), want_pred=True)
         db = H.DeviceRowBlock(c, blk)
