@@ -47,7 +47,10 @@ struct Kw {
   int loss_fm = 1;
   int ordered = 1;
   // execution choices (context kwargs, not behaviour switches of the process environment)
-  int fwd_probe = 1;    // fwd_probe=0: Localizer col + pulled {w, vrow} instead of probing
+  // fwd_probe=1 (default): the forward finds its keys, lookups spread over the row's lanes;
+  // 2: the same with each lane walking all of its row's nnz (k_fm_fwd); 0: Localizer col +
+  // pulled {w, vrow} instead of probing
+  int fwd_probe = 1;
   int xvp_row = 1;      // xvp_row=0: XV*p rows of d floats, p in its own array
   long bwd_lds = -1;    // bwd_lds=<bytes>: LDS reserved per backward block (-1: default cap)
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
@@ -83,7 +86,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "seed") kw->seed = (unsigned)strtoul(cv, nullptr, 10);
     else if (k == "max_keys") kw->max_keys = atoll(cv);
     else if (k == "max_vrows") kw->max_vrows = atoll(cv);
-    else if (k == "fwd_probe") kw->fwd_probe = atoi(cv) != 0;
+    else if (k == "fwd_probe") kw->fwd_probe = atoi(cv);
     else if (k == "xvp_row") kw->xvp_row = atoi(cv) != 0;
     else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
     else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;

@@ -272,6 +272,158 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   }
 }
 
+// Probe-mode forward with the lookups spread over the row's lanes (CPL = 4: float4 per lane,
+// G lanes per row).  The row is walked in chunks of 32 nnz: first every lane of the group finds
+// the entries of its 32/G of them (id -> key -> home slot -> {w, vrow, key}), all loads issued
+// together; then the chunk's {w, V row} are handed round the group with lane shuffles and the
+// V rows loaded 8 nnz at a time, accumulated in nnz order.  Per 32 nnz that is one trip for the
+// ids, one for the entries and pipelined V trips — where the UNR loop of k_fm_fwd paid three
+// dependent trips per 8 nnz.  Sums run in exactly the same (row, nnz) order, so predictions
+// are bit-identical to k_fm_fwd's (and the reference's).
+template <int G>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
+  constexpr int RPB = kFmNT / G;  // rows per block
+  constexpr int CH = 32;          // nnz per chunk
+  constexpr int MA = CH / G;      // lookups per lane per chunk
+  constexpr int VB = 8;           // V rows in flight per batch
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int gbase = (threadIdx.x % kWave) - l;
+  const int64_t r = (int64_t)blockIdx.x * RPB + g;
+  const int d = a.d;
+  __shared__ double red[kFmNT / kWave];
+  double loss = 0;
+  if (r < a.B) {
+    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
+    float acc = 0.f;
+    float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool valued = a.val != nullptr;
+    for (uint64_t j0 = o0; j0 < o1; j0 += CH) {
+      // ---- the chunk's lookups, MA per lane: nnz j0 + l + G*m
+      uint64_t key[MA], hs[MA];
+      float xm[MA];
+#pragma unroll
+      for (int m = 0; m < MA; ++m) {
+        const uint64_t j = j0 + l + (uint64_t)G * m;
+        const uint64_t jj = j < o1 ? j : o1 - 1;
+        const uint64_t id = a.index[jj];
+        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+        key[m] = reverse_bytes(mm);
+        hs[m] = tbl_hash(key[m], a.T);
+        xm[m] = valued ? a.val[jj] : 1.f;
+      }
+      int2 wr[MA];
+      uint64_t ek[MA];
+#pragma unroll
+      for (int m = 0; m < MA; ++m) {
+        const Entry* e = a.T.ent + hs[m];
+        wr[m] = *reinterpret_cast<const int2*>(e);
+        ek[m] = e->key;
+      }
+      float wm[MA];
+      int vm[MA];
+#pragma unroll
+      for (int m = 0; m < MA; ++m) {
+        uint64_t h = hs[m];
+        for (uint64_t probe = 0; ek[m] != key[m] && ek[m] != kEmptyKey && probe < a.T.mask;
+             ++probe) {  // the (rare) longer probe chains
+          h = (h + 1) & a.T.mask;
+          const Entry* e = a.T.ent + h;
+          ek[m] = e->key;
+          wr[m] = *reinterpret_cast<const int2*>(e);
+        }
+        // absent (inserted by this training step's backward): the empty entry, w = 0, no V
+        if (ek[m] != key[m] || j0 + l + (uint64_t)G * m >= o1) wr[m] = make_int2(0, -1);
+        wm[m] = __int_as_float(wr[m].x);
+        const int vr = wr[m].y;
+        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
+        vm[m] = (vr >= 0 && !(a.l1_shrk && wm[m] == 0.f)) ? vr : -1;
+      }
+      // ---- V rows 8 nnz at a time, accumulated in nnz order
+      const int nin = (int)((o1 - j0) < (uint64_t)CH ? (o1 - j0) : (uint64_t)CH);
+#pragma unroll
+      for (int b = 0; b < CH / VB; ++b) {
+        if (b * VB >= nin) break;
+        float w[VB], x[VB];
+        int vp[VB];
+        float4 v[VB];
+#pragma unroll
+        for (int t = 0; t < VB; ++t) {
+          const int tt = b * VB + t;  // the chunk's nnz tt sits with lane tt % G, slot tt / G
+          w[t] = __shfl(wm[tt / G], gbase + tt % G, kWave);
+          vp[t] = __shfl(vm[tt / G], gbase + tt % G, kWave);
+          x[t] = valued ? __shfl(xm[tt / G], gbase + tt % G, kWave) : 1.f;
+        }
+#pragma unroll
+        for (int t = 0; t < VB; ++t) {
+          const float* Vr = vp[t] < 0 ? a.zpad + (((uint32_t)t & 255u) << 4) : row_V(a.T, vp[t]);
+          const int base = l * 4 < d ? l * 4 : 0;
+          v[t] = *reinterpret_cast<const float4*>(Vr + base);
+        }
+#pragma unroll
+        for (int t = 0; t < VB; ++t) {
+          if (b * VB + t >= nin) break;
+          // SpMV::Times skips w == 0 (spmv.h:124-125)
+          if (w[t] != 0.f) acc = valued ? acc + w[t] * x[t] : acc + w[t];
+          if (vp[t] >= 0) {
+            const float xx = x[t] * x[t];  // XX_ (fm_loss.h:86-92)
+            const float vk[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              xv[k] = valued ? xv[k] + vk[k] * x[t] : xv[k] + vk[k];
+              const float vv = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
+              xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
+            }
+          }
+        }
+      }
+    }
+    float pr = acc;
+    if (d > 0) {
+      // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
+      float t4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t4[k] = xv[k] * xv[k] - xxvv[k];
+      float s = 0.f;
+      for (int q = 0; q < G; ++q) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float tk = __shfl(t4[k], gbase + q, kWave);
+          if (q * 4 + k < d) s += tk;
+        }
+      }
+      double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
+      pr = (float)y;
+      pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
+    }
+    const float p = logit_p(a.label[r], pr, a.rw, r);
+    const int64_t xs = a.xs > d ? a.xs : d;
+    if (l == 0) {
+      a.p_out[r] = p;
+      if (xs > d) a.XVp[r * xs + d] = p;
+      a.pred[r] = pr;
+      double yy = a.label[r] > 0 ? 1.0 : -1.0;
+      loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+      if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
+        uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
+        a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
+      }
+    }
+    if (d > 0 && l * 4 < d)  // XV_ *= p (fm_loss.h:196-199)
+      *reinterpret_cast<float4*>(a.XVp + r * xs + l * 4) =
+          make_float4(xv[0] * p, xv[1] * p, xv[2] * p, xv[3] * p);
+  }
+  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+    a.loss_part[blockIdx.x] = s;
+  }
+}
+
 // Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
 // multiple of 4); otherwise scalar coordinates (the pulled interleaved layout is unaligned).
 void lanes_for(int d, bool vec, int* G, int* CPL, bool* use_vec) {
@@ -325,12 +477,23 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
   return launch_fwd_gc<MODE, PACKED>(a, G, CPL, vec, st);
 }
 
-int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk) {
+int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   int G, CPL;
   bool vec;
   lanes_for(a.d, true, &G, &CPL, &vec);
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
+  if (a.index && spread && vec && CPL == 4 && G >= 4 && G <= 32 && a.B > 0) {
+    const dim3 grid((unsigned)*nblk);
+#define DFX_FWDP(GG)                                                                     \
+    if (G == GG) {                                                                       \
+      hipLaunchKernelGGL(k_fm_fwd_probe<GG>, grid, dim3(kFmNT), 0, st, a);                \
+      DFX_HIP(hipGetLastError());                                                        \
+      return DFX_OK;                                                                     \
+    }
+    DFX_FWDP(4) DFX_FWDP(8) DFX_FWDP(16) DFX_FWDP(32)
+#undef DFX_FWDP
+  }
   if (a.index) return launch_fwd_gc<kFusedProbe, true>(a, G, CPL, vec, st);
   return launch_fwd_gc<kFused, true>(a, G, CPL, vec, st);
 }

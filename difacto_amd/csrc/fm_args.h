@@ -84,8 +84,9 @@ struct BwdArgs {
 
 // the XVp row stride the workspace is sized for (step.hip): p rides in each row
 int xvp_stride(const Context* c);
-// fused forward; *nblk receives the number of loss partials written
-int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk);
+// fused forward; *nblk receives the number of loss partials written.  spread: probe mode
+// with the lookups spread over the row's lanes (k_fm_fwd_probe) where the lane layout allows
+int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread = true);
 // fused backward + FTRL/AdaGrad update over at most nseg_bound segments; lds: bytes of LDS
 // reserved per block (-1: the default cap)
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds = -1);

@@ -285,7 +285,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.auc_lab = c->aws.av0.as<uint32_t>();
   DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   int nblk = 0;
-  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk));
+  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
   prof_mark(c, 4);
   sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
 

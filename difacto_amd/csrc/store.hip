@@ -557,6 +557,29 @@ __global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
   }
 }
 
+// probe distance of every occupied slot from its key's home slot (linear probing)
+__global__ void k_probe_stats(Table T, int64_t cap, unsigned long long* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long dist = 0, occ = 0, mx = 0;
+  if (i < cap && T.ent[i].key != kEmptyKey) {
+    const uint64_t h = tbl_hash(T.ent[i].key, T);
+    dist = ((uint64_t)i - h) & T.mask;
+    occ = 1;
+    mx = dist;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    dist += __shfl_xor(dist, off, kWave);
+    occ += __shfl_xor(occ, off, kWave);
+    const unsigned long long o = __shfl_xor(mx, off, kWave);
+    mx = o > mx ? o : mx;
+  }
+  if (lane_id() == 0 && occ) {
+    atomicAdd(&out[0], dist);
+    atomicAdd(&out[1], occ);
+    atomicMax(&out[2], mx);
+  }
+}
+
 // host copy of the table for save / dump
 struct HostTable {
   std::vector<Entry> ent;
@@ -690,6 +713,26 @@ int dfx_store_stats(dfx_ctx* ctx, int64_t* n_keys, int64_t* n_vrows, double* new
   if (new_w) *new_w = (double)h.new_w;
   if (seed) *seed = h.seed;
   return dfx_sync(ctx);
+}
+
+// table health: the mean and the longest distance of a stored key from its home slot, and the
+// capacity (slots) — the ordered hash keeps both small at load factor <= 0.5
+int dfx_store_probe_stats(dfx_ctx* ctx, double* mean_probe, int64_t* max_probe,
+                          int64_t* capacity) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  Context* c = &ctx->c;
+  DFX_TRY(c->ws.dscratch.ensure(64));
+  unsigned long long* acc = c->ws.dscratch.as<unsigned long long>();
+  DFX_HIP(hipMemsetAsync(acc, 0, 3 * 8, c->stream));
+  hipLaunchKernelGGL(k_probe_stats, dim3((unsigned)((c->cap + 255) / 256)), dim3(256), 0,
+                     c->stream, c->T, c->cap, acc);
+  unsigned long long h[3];
+  DFX_HIP(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  if (mean_probe) *mean_probe = h[1] ? (double)h[0] / (double)h[1] : 0.0;
+  if (max_probe) *max_probe = (int64_t)h[2];
+  if (capacity) *capacity = c->cap;
+  return DFX_OK;
 }
 
 int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz) {

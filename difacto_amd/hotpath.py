@@ -225,6 +225,13 @@ class Store:
         check(_lib.lib().dfx_store_evaluate(self.ctx.h, ctypes.byref(pen), ctypes.byref(nnz)))
         return pen.value, nnz.value
 
+    def probe_stats(self):
+        """-> (mean probe distance, longest probe distance, table capacity)"""
+        m, mx, cap = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        check(_lib.lib().dfx_store_probe_stats(self.ctx.h, ctypes.byref(m), ctypes.byref(mx),
+                                               ctypes.byref(cap)))
+        return m.value, mx.value, cap.value
+
     def reserve(self, n_keys, n_vrows):
         check(_lib.lib().dfx_store_reserve(self.ctx.h, int(n_keys), int(n_vrows)))
 

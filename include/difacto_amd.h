@@ -177,6 +177,10 @@ int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks);
 int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_reverse);
 int dfx_store_stats(dfx_ctx* ctx, int64_t* n_keys, int64_t* n_vrows, double* new_w,
                     uint32_t* seed);
+/* table health: mean and longest distance of a stored key from its home slot; capacity in
+ * slots (a test / diagnostics hook) */
+int dfx_store_probe_stats(dfx_ctx* ctx, double* mean_probe, int64_t* max_probe,
+                          int64_t* capacity);
 int dfx_store_evaluate(dfx_ctx* ctx, double* penalty, int64_t* nnz);
 int dfx_store_reserve(dfx_ctx* ctx, int64_t n_keys, int64_t n_vrows);
 /* test hook: state[4] = {w, sqrt_g, z, fea_cnt}, V/Vaux (2*V_dim floats, host) */

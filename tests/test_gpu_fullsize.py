@@ -171,3 +171,97 @@ def test_calcgrad_c5_chunked(H):
     # and beyond 1e-5 relative only where a sum cancels far below its terms
     assert int((rel > RTOL).sum()) <= 1e-4 * len(g)
     c.close()
+
+
+@pytest.mark.timeout(300)
+def test_c4_one_shard_full_table():
+    """C4 at its own scale on one GPU: one of 8 key-range servers of a 2^30-key model holds
+    2^27 keys at V_dim = 64 — its table (2^28 slots of 32 B = 8 GiB, load 0.5) and V pool
+    (2^27 rows of [V | Vaux] = 64 GiB) allocated and filled through the sharded owner phases:
+    count pushes (fea_cnt 11 > V_threshold 10), then a gradient push that moves every w off
+    zero, whose InitV gives every key its V row.  Checks the key and V-row counts, the rand_r
+    advance (3 draws per coordinate per key), and the table's probe lengths."""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    from oracle import oracle as O
+    N, g, d = 8, 1, 64
+    n_keys = 1 << 27
+    kw = dict(V_dim=d, V_threshold=10, l1=0, lr=.1, V_lr=.01, seed=3, push_agg="sum")
+    c = H.Context(0, max_keys=n_keys, max_vrows=n_keys, **kw)
+    sh = DI.Shard(c, N)
+    dev = c.device
+    chunk = 1 << 24
+    stride = (1 << 61) // n_keys  # keys spread over server g's range [g 2^61, (g+1) 2^61)
+    S = sh.S
+    for i in range(0, n_keys, chunk):
+        idx = torch.arange(i, i + chunk, dtype=torch.int64, device=dev)
+        keys = (g << 61) + idx * stride + (idx * 7919) % stride
+        cnt = torch.full((chunk,), 11.0, dtype=torch.float32, device=dev)
+        sh.owner_begin(keys, [chunk] + [0] * (N - 1), cnt, 0)
+        # this server's InitV ranking (none yet: w is still 0)
+        allc = torch.zeros(N, dtype=torch.int64, device=dev)
+        allc[g] = sh.initv_local(0)[0]
+        sh.initv_draw(allc, g, 0)
+        grads = torch.zeros(chunk * S, dtype=torch.float32, device=dev)
+        grads.view(chunk, S)[:, d] = -1.0  # gw: w leaves zero, FTRL with l1 = 0
+        sh.owner_push(grads, 0)
+        allc = torch.zeros(N, dtype=torch.int64, device=dev)
+        allc[g] = sh.initv_local(0)[0]
+        sh.initv_draw(allc, g, 0)
+        del grads, cnt, keys, idx
+    st = H.Store(c).stats()
+    assert st["n_keys"] == n_keys
+    assert st["n_vrows"] == n_keys
+    # rand_r: 3 LCG steps per draw, d draws per InitV, one InitV per key (glibc rand_r)
+    A, C, m, a_, c_ = 1, 0, 3 * d * n_keys, 1103515245, 12345
+    while m:  # the LCG jumped m steps: s -> A s + C (mod 2^32)
+        if m & 1:
+            A, C = (a_ * A) % (1 << 32), (a_ * C + c_) % (1 << 32)
+        a_, c_ = (a_ * a_) % (1 << 32), (a_ * c_ + c_) % (1 << 32)
+        m >>= 1
+    assert st["seed"] == (A * 3 + C) % (1 << 32)
+    mean, mx, cap = H.Store(c).probe_stats()
+    assert cap == 2 * n_keys
+    assert mean < 1.0 and mx < 64, (mean, mx)
+    # a few keys' state against the updater rule: w after one FTRL step from zero, V drawn
+    for i in (0, n_keys // 3, n_keys - 1):
+        k = (g << 61) + i * stride + (i * 7919) % stride
+        e = H.Store(c).entry(k)
+        assert e is not None and e[1] is not None
+        assert e[0][3] == 11.0 and e[0][0] != 0.0
+    c.close()
+
+
+@pytest.mark.timeout(300)
+def test_c4_eight_ranges_at_scale():
+    """C4-shaped twin of test_sharded_eight_ranges_at_scale: V_dim 64, 39 binary nnz per row,
+    keys drawn from 2^30, 8 loopback key-range servers each sized for its 2^27-key share of the
+    2^30 key space (a 1/8-range table: the range-aware ordered hash), against AggOracle (the
+    single reference updater on the concatenated batches)"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    from oracle import dist_oracle as DO
+    N, rows, kb, d = 8, 10_000, 30, 64
+    kw = dict(V_dim=d, V_threshold=0, lr=0.1, V_lr=0.01, l1=0.0, seed=9)
+    ctxs = [H.Context(0, max_keys=1 << 22, max_vrows=1 << 22, push_agg="sum", **kw)
+            for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    comm = DI.LoopbackComm(N)
+    so = DO.AggOracle(N, **kw)
+    for s in range(3):
+        step = [D.synthetic(rows, 39, 1 << kb, seed=1900 + 17 * s + r) for r in range(N)]
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        preds = [torch.zeros(rows, dtype=torch.float32, device=ctxs[r].device) for r in range(N)]
+        DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=(s == 0), preds=preds)
+        out = so.step(step, push_cnt=(s == 0))
+        for r in range(N):
+            assert close(preds[r].cpu().numpy(), out[r][2]), (s, r)
+            pr = H.progress(ctxs[r])
+            assert pr["loss"] == pytest.approx(out[r][0], rel=1e-4), (s, r)
+    stats = [H.Store(c).stats() for c in ctxs]
+    assert sum(st["n_keys"] for st in stats) == so.one.size()
+    assert all(st["seed"] == so.one.seed for st in stats)
+    for c in ctxs:
+        mean, mx, _ = H.Store(c).probe_stats()
+        assert mean < 1.0 and mx < 64, (mean, mx)
+        c.close()
