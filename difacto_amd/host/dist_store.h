@@ -1,0 +1,64 @@
+// dist_store.h — KVStoreDist (src/store/kvstore_dist.h:90-175) behind the reference's Store
+// interface (include/difacto/store.h:55-83), over the sharded store's device phases
+// (dfx_dist_*, include/difacto_amd.h) and a ShardExchange (dist_host.h).
+//
+// A worker calls Push / Pull exactly as SGDLearner::IterateData does (sgd_learner.cc:201-317):
+// Push(kFeaCount) + Wait, Pull(kWeight), Push(kGradient).  Each call is one exchange round among
+// all workers, so the workers issue the same sequence of calls (an idle worker passes an empty
+// key list).  Every call completes before it returns (on_complete runs inline; Wait is a no-op):
+//   Push(kFeaCount)  keys + counts all-to-all-v to their owners, owner_begin with the counts
+//                    (HandlePush -> Update(kFeaCount), kvstore_dist.h:158-165)
+//   Pull(kWeight)    keys to their owners, owner_begin + owner_pull, records back, the worker's
+//                    vals / lens in Get layout (HandlePull -> Get, kvstore_dist.h:167-175)
+//   Push(kGradient)  keys and gradient records to their owners, owner_push
+// The update aggregation follows the contexts' push_agg kwarg: sum (one Update per key on the
+// workers' summed gradients, InitV ranked over all owners) or ranks (KVStoreDist: one Update per
+// pushing worker, in rank order).
+//
+// One process per GPU (RCCL, Store::Create under a distributed launch) holds one worker; a
+// loopback store holds N workers in one process (tests on one GPU): each worker is used by
+// its own thread, and the last of the N calls of a round runs the round for all of them.
+// The worker's arrays are host SArrays (the reference's), so this path is PCIe-inclusive.
+#ifndef DIFACTO_AMD_HOST_DIST_STORE_H_
+#define DIFACTO_AMD_HOST_DIST_STORE_H_
+
+#include <memory>
+#include <string>
+
+#include "dist_host.h"
+#include "iface.h"
+
+namespace difacto {
+
+class GpuDistStore {
+ public:
+  /** n shards on device 0 of this process, loopback exchange.  kwargs: the shards' dfx_ctx
+   * kwargs (V_dim, lr, ..., max_keys, push_agg) */
+  static std::shared_ptr<GpuDistStore> CreateLoopback(int nshards, const KWArgs& kwargs);
+  /** one shard per process over RCCL, from the launch environment (RANK, WORLD_SIZE,
+   * LOCAL_RANK = the device; communicator ids through DFX_COMM_ID_FILE, else
+   * /tmp/dfx_comm_<MASTER_PORT>) */
+  static std::shared_ptr<GpuDistStore> CreateRccl(const KWArgs& kwargs);
+  ~GpuDistStore();
+
+  int nlocal() const;
+  /** the Store of local worker l (valid while this object lives) */
+  Store* worker(int local) const;
+  /** the server context of local shard l (model save / load / stats) */
+  dfx_ctx* shard(int local) const;
+  ShardExchange* exchange() const;
+
+  struct Core;
+
+ private:
+  explicit GpuDistStore(std::unique_ptr<Core> core);
+  std::unique_ptr<Core> core_;
+};
+
+/** Store::Create (store.cc:11-17): under a distributed launch (WORLD_SIZE > 1) a worker of an
+ * RCCL GpuDistStore built from kwargs, which the returned Store keeps alive; otherwise the
+ * single-GPU StoreGPU (store_local.h), which needs SetUpdater */
+std::shared_ptr<Store> CreateStore(const KWArgs& kwargs);
+
+}  // namespace difacto
+#endif  // DIFACTO_AMD_HOST_DIST_STORE_H_

@@ -59,6 +59,12 @@ void GpuLocalizer::Compact(const dmlc::RowBlock<feaid_t>& blk,
   const size_t B = blk.size;
   const size_t nnz = B ? blk.offset[B] - blk.offset[0] : 0;
   DFX_HOST_CHECK(B == 0 || blk.offset[0] == 0, "Compact: offset[0] must be 0");
+  if (B == 0) {
+    if (uniq_idx) uniq_idx->clear();
+    if (idx_frq) idx_frq->clear();
+    *compacted = RowBlockContainer<unsigned>();
+    return;
+  }
   DevArray<uint64_t> offs(c), idx(c), uniq(c);
   DevArray<float> cnt(c);
   DevArray<uint32_t> col(c);
@@ -106,13 +112,18 @@ struct GpuFMLoss::Dev {
 
 KWArgs GpuFMLoss::Init(const KWArgs& kwargs) {
   KWArgs mine;
-  KWArgs rest = Consume(kwargs, {"V_dim"}, &mine);  // FMLossParam (fm_loss.h:19-27)
-  for (const auto& p : mine) V_dim_ = std::stoi(p.second);
+  // FMLossParam (fm_loss.h:19-27), plus the device this loss runs on
+  KWArgs rest = Consume(kwargs, {"V_dim", "device"}, &mine);
+  int device = 0;
+  for (const auto& p : mine) {
+    if (p.first == "V_dim") V_dim_ = std::stoi(p.second);
+    if (p.first == "device") device = std::stoi(p.second);
+  }
   if (logit_) V_dim_ = 0;
   DFX_HOST_CHECK(V_dim_ >= 0 && V_dim_ <= 1024, "V_dim out of range");
   // the loss needs a stream and scratch only: keep its (unused) model table tiny
   ctx_ = std::make_shared<GpuContext>(
-      0, KWArgs{{"V_dim", std::to_string(V_dim_)}, {"max_keys", "16"}, {"max_vrows", "1"}});
+      device, KWArgs{{"V_dim", std::to_string(V_dim_)}, {"max_keys", "16"}, {"max_vrows", "1"}});
   dev_ = std::make_shared<Dev>(ctx_->h());
   return rest;
 }
@@ -361,20 +372,37 @@ static void ParallelCopy(void* dst, const void* src, size_t bytes) {
   for (auto& x : th) x.join();
 }
 
-GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs) {
+GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs, std::shared_ptr<Store> store) {
   KWArgs mine;
-  KWArgs rest = Consume(kwargs, {"fused", "loss"}, &mine);
+  KWArgs rest = Consume(kwargs, {"fused", "loss", "device"}, &mine);
   std::string loss = "fm";
+  int device = 0;
   for (const auto& p : mine) {
     if (p.first == "fused") fused_ = std::stoi(p.second) != 0;
     if (p.first == "loss") loss = p.second;
+    if (p.first == "device") device = std::stoi(p.second);
   }
   DFX_HOST_CHECK(loss == "fm" || loss == "logit", "unknown loss type " + loss);
+  if (store) {
+    // a given Store (a GpuDistStore worker) holds the model on its servers: this worker runs
+    // the interface path with a context of its own for the Localizer
+    DFX_HOST_CHECK(!fused_, "a given Store runs the interface path (fused=0)");
+    for (const auto& p : rest)
+      if (p.first == "V_dim") V_dim_ = std::stoi(p.second);
+    if (loss == "logit") V_dim_ = 0;
+    store_ = store;
+    loss_.reset(new GpuFMLoss(loss == "logit"));
+    loss_->Init({{"V_dim", std::to_string(V_dim_)}, {"device", std::to_string(device)}});
+    localizer_.reset(new GpuLocalizer(std::make_shared<GpuContext>(
+        device, KWArgs{{"V_dim", std::to_string(V_dim_)}, {"max_keys", "16"},
+                       {"max_vrows", "1"}})));
+    return;
+  }
   if (loss == "logit") rest.push_back({"loss", "logit"});
   updater_ = std::make_shared<GpuSGDUpdater>();
   rest = updater_->Init(rest);
   V_dim_ = updater_->V_dim();
-  store_.reset(new StoreGPU());
+  store_ = std::make_shared<StoreGPU>();
   store_->SetUpdater(updater_);
   if (!fused_) {
     // V_dim is forwarded to the loss (sgd_learner.cc:37)
@@ -442,6 +470,12 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   SArray<int> lengths;
   store_->Pull(keys, Store::kWeight, &values, V_dim_ > 0 ? &lengths : nullptr);
   dmlc::RowBlock<unsigned> blk = data.GetBlock();
+  if (blk.size == 0) {
+    // a worker with no rows this round (the sharded store's workers call in step): it takes
+    // part in the exchanges with no keys
+    if (job_type == kTraining) store_->Push(keys, Store::kGradient, SArray<real_t>(), SArray<int>());
+    return;
+  }
   prog_.nrows += blk.size;
   SArray<real_t> pred(blk.size);
   SArray<int> w_pos, V_pos;

@@ -90,7 +90,7 @@ class GpuLocalizer {
   feaid_t max_index_;
 };
 
-/** FMLoss (fm_loss.h) / LogitLoss (logit_loss.h, == V_dim 0) on the device */
+/** FMLoss (fm_loss.h) / LogitLoss (logit_loss.h, == V_dim 0) on the device (kwarg `device`) */
 class GpuFMLoss : public Loss {
  public:
   explicit GpuFMLoss(bool logit = false) : logit_(logit) {}
@@ -170,8 +170,10 @@ class GpuSGDLearner {
  public:
   enum JobType { kTraining = 3, kValidation = 4, kPrediction = 5 };
   /** kwargs: the .conf keys (loss, V_dim, lr, l1, ...), plus `fused` (1: dfx_train_step,
-   * batches uploaded through a dfx_feeder; 0: through the Loss/Store interfaces) */
-  explicit GpuSGDLearner(const KWArgs& kwargs);
+   * batches uploaded through a dfx_feeder; 0: through the Loss/Store interfaces) and `device`.
+   * store: a Store holding the model elsewhere (a GpuDistStore worker, dist_store.h; the
+   * interface path only); none: a StoreGPU over this learner's GpuSGDUpdater */
+  explicit GpuSGDLearner(const KWArgs& kwargs, std::shared_ptr<Store> store = nullptr);
   ~GpuSGDLearner();
   /** one minibatch of raw feature ids; push_cnt = epoch 0 of training with V_dim > 0.
    * Asynchronous on the fused path: the batch is copied into pinned staging and uploaded on
@@ -181,6 +183,7 @@ class GpuSGDLearner {
                     std::vector<real_t>* pred = nullptr);
   /** sgd::Progress accumulated since the last call (joins the device) */
   Progress TakeProgress();
+  /** the learner's own updater (null when a Store was given) */
   std::shared_ptr<GpuSGDUpdater> updater() const { return updater_; }
   bool fused() const { return fused_; }
 
@@ -188,7 +191,7 @@ class GpuSGDLearner {
   bool fused_ = false;
   int V_dim_ = 0;
   std::shared_ptr<GpuSGDUpdater> updater_;
-  std::unique_ptr<StoreGPU> store_;
+  std::shared_ptr<Store> store_;
   std::unique_ptr<GpuFMLoss> loss_;
   std::unique_ptr<GpuLocalizer> localizer_;
   dfx_feeder* feeder_ = nullptr;

@@ -8,9 +8,20 @@
 //   + the two drivers agree on an FM V_dim=8 run, and Save/Load round-trips through a Stream
 //
 // Usage: host_tests <path to tests/golden/rcv1_100.libsvm>.  Exit status 0 == all passed.
+//
+// host_tests dist <data> shards=N|-1 epochs=E batch_size=B [model_out=P] [dfx_ctx kwargs]:
+// SGDLearner::IterateData's executor (sgd_learner.cc:201-317: Compact -> Push(kFeaCount) + Wait
+// -> Pull -> Predict / Evaluate / AUC -> CalcGrad -> Push(kGradient)) through the Store interface
+// of a GpuDistStore (dist_store.h): N loopback workers, one thread each, or (shards=-1) one
+// RCCL worker per process.  Worker r trains rows [r n / N, (r + 1) n / N) in batches of B, the
+// workers stepping together (an idle worker passes empty batches).  Prints one line per epoch,
+// "epoch E loss L auc A nrows R" summed over the workers, which tests/test_host_cpp.py compares
+// with oracle/dist_oracle.py; model_out: each server saves its part (with aux) to P_part-<rank>.
 #include <cstdio>
 #include <string>
+#include <thread>
 
+#include "../../difacto_amd/host/dist_store.h"
 #include "../../difacto_amd/host/gpu_adapters.h"
 
 using namespace difacto;
@@ -174,7 +185,94 @@ static void TestDriversAgree(const RowBlockContainer<feaid_t>& data) {
   std::remove(path);
 }
 
+static int RunDist(int argc, char** argv) {
+  RowBlockContainer<feaid_t> data;
+  if (argc < 3 || !ReadLibSVM(argv[2], &data)) {
+    std::fprintf(stderr, "usage: %s dist <data> shards=N|-1 epochs=E batch_size=B ...\n", argv[0]);
+    return 2;
+  }
+  int shards = 1, epochs = 1;
+  size_t bs = 10;
+  std::string model_out, vdim = "0";
+  KWArgs kw;
+  for (int i = 3; i < argc; ++i) {
+    const std::string a = argv[i];
+    const size_t eq = a.find('=');
+    if (eq == std::string::npos) return 2;
+    const std::string k = a.substr(0, eq), v = a.substr(eq + 1);
+    if (k == "shards") {
+      shards = std::stoi(v);
+    } else if (k == "epochs") {
+      epochs = std::stoi(v);
+    } else if (k == "batch_size") {
+      bs = std::stoul(v);
+    } else if (k == "model_out") {
+      model_out = v;
+    } else {
+      if (k == "V_dim") vdim = v;
+      kw.push_back({k, v});
+    }
+  }
+  const char* lr_env = std::getenv("LOCAL_RANK");
+  const std::string device = shards < 0 && lr_env ? lr_env : "0";
+  std::shared_ptr<GpuDistStore> ds =
+      shards > 0 ? GpuDistStore::CreateLoopback(shards, kw) : GpuDistStore::CreateRccl(kw);
+  ShardExchange* ex = ds->exchange();
+  const int L = ds->nlocal(), N = ex->nranks();
+  const size_t n = data.Size();
+  size_t nsteps = 0;
+  for (int r = 0; r < N; ++r) {
+    const size_t rows = (size_t)(r + 1) * n / N - (size_t)r * n / N;
+    nsteps = std::max(nsteps, (rows + bs - 1) / bs);
+  }
+  std::vector<std::unique_ptr<GpuSGDLearner>> learners(L);
+  for (int l = 0; l < L; ++l) {
+    Store* w = ds->worker(l);
+    EXPECT(w->NumWorkers() == N && w->NumServers() == N && w->Rank() == ex->rank(l),
+           "worker %d: NumWorkers %d Rank %d", l, w->NumWorkers(), w->Rank());
+    // the aliasing shared_ptr keeps the store alive as long as the learner holds its worker
+    learners[l].reset(new GpuSGDLearner({{"fused", "0"}, {"V_dim", vdim}, {"device", device}},
+                                        std::shared_ptr<Store>(ds, w)));
+  }
+  for (int ep = 0; ep < epochs; ++ep) {
+    std::vector<Progress> prog(L);
+    std::vector<std::thread> th;
+    for (int l = 0; l < L; ++l) {
+      th.emplace_back([&, l]() {
+        const int r = ex->rank(l);
+        const size_t lo = (size_t)r * n / N, hi = (size_t)(r + 1) * n / N;
+        for (size_t t = 0; t < nsteps; ++t) {
+          const size_t b = std::min(hi, lo + t * bs), e = std::min(hi, lo + (t + 1) * bs);
+          RowSlice s = Slice(data, b, e);
+          learners[l]->ProcessBatch(s.blk, GpuSGDLearner::kTraining, ep == 0);
+        }
+        prog[l] = learners[l]->TakeProgress();
+      });
+    }
+    for (auto& t : th) t.join();
+    std::vector<double> sum(3, 0.0);
+    for (const Progress& p : prog) {
+      sum[0] += p.loss;
+      sum[1] += p.auc;
+      sum[2] += p.nrows;
+    }
+    ex->AllReduceSum(&sum);
+    if (ex->rank(0) == 0)
+      std::printf("epoch %d loss %.9e auc %.9e nrows %.0f\n", ep, sum[0], sum[1], sum[2]);
+    std::fflush(stdout);
+  }
+  if (!model_out.empty())
+    for (int l = 0; l < L; ++l)
+      DfxCheck(dfx_store_save(ds->shard(l),
+                              (model_out + "_part-" + std::to_string(ex->rank(l))).c_str(), 1),
+               "dfx_store_save");
+  learners.clear();
+  std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+  return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "dist") return RunDist(argc, argv);
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s rcv1_100.libsvm\n", argv[0]);
     return 2;
