@@ -56,6 +56,9 @@ struct Kw {
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
   int sort_pack = 1;    // sort_pack=0: the Localizer sorts 12-byte (key, row) pairs
+  int auc_radix = 1;    // auc_sort=merge: the AUC lane's tile sorts + merge rounds
+  int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
+  int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -91,6 +94,25 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
     else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;
     else if (k == "sort_pack") kw->sort_pack = atoi(cv) != 0;
+    else if (k == "sort_items") {
+      kw->sort_items = atoi(cv);
+      if (kw->sort_items != 8 && kw->sort_items != 16 && kw->sort_items != 32) {
+        set_error("sort_items must be 8, 16 or 32");
+        return DFX_ERR_ARG;
+      }
+    }
+    else if (k == "sort_lookback") {
+      kw->sort_lookback = atoi(cv);
+      if (kw->sort_lookback != 4 && kw->sort_lookback != 16 && kw->sort_lookback != 32) {
+        set_error("sort_lookback must be 4, 16 or 32");
+        return DFX_ERR_ARG;
+      }
+    }
+    else if (k == "auc_sort") {
+      if (v == "radix") kw->auc_radix = 1;
+      else if (v == "merge") kw->auc_radix = 0;
+      else { set_error("unknown auc_sort: " + v + " (radix|merge)"); return DFX_ERR_ARG; }
+    }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
       else if (v == "ranks") kw->dist_sum = 0;
@@ -179,6 +201,9 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->autogrow = kw.autogrow;
   c->dist_sum = kw.dist_sum;
   c->sort_pack = kw.sort_pack;
+  c->auc_radix = kw.auc_radix != 0;
+  c->sort_items = kw.sort_items;
+  c->sort_lookback = kw.sort_lookback;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

@@ -182,6 +182,9 @@ struct Context {
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
   int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
+  bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
+  int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)
+  int sort_lookback = 4;  // the Localizer sort's look-back step width (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
   // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
   CapGuard capg;
@@ -223,6 +226,10 @@ constexpr int kSortDiffIsOrAnd = 1, kSortCountsReady = 2;
 // each item as one u64 when the varying key bits fit beside rb8 row bits (a multiple of 8);
 // sortmeta[25] then says so (sort_packed / sort_unpack) and the payload buffers are unused
 inline constexpr int kSortPackRows(int rb8) { return rb8 << 8; }
+// flags |= kSortItems(it): it items per thread in a scatter tile (8, 16 = default, or 32)
+inline constexpr int kSortItems(int it) { return it << 16; }
+// flags |= kSortLookback(lb): predecessor words a look-back step reads (4 = default, 16, 32)
+inline constexpr int kSortLookback(int lb) { return lb << 24; }
 constexpr int kSortMetaPack = 25;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
 // the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
@@ -325,11 +332,12 @@ void cap_release(Context* c);
 int store_maybe_grow(Context* c);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
-int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev);
+int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
+            bool radix);
 // the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream
 int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred);
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate);
+int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

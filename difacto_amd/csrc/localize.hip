@@ -316,11 +316,15 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
     DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, k0, q0, k1, q1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
+                                                      kSortItems(c->sort_items) |
+                                                      kSortLookback(c->sort_lookback) |
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
-                                                  kSortDiffIsOrAnd | kSortCountsReady)));
+                                                  kSortDiffIsOrAnd | kSortCountsReady |
+                                                      kSortItems(c->sort_items) |
+                                                      kSortLookback(c->sort_lookback))));
   }
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));

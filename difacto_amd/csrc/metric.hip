@@ -26,9 +26,17 @@ __global__ void k_auc_keys(int64_t B, const float* label, const float* pred, uin
   v[i] = label[i] > 0 ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* V, int64_t n,
+// the sorted labels: V0, or V1 when *sel (a radix sort's result buffer, known on the device)
+__device__ inline const uint32_t* auc_labels(const uint32_t* V0, const uint32_t* V1,
+                                             const unsigned* sel) {
+  return (sel && *sel) ? V1 : V0;
+}
+
+__global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* V0, const uint32_t* V1,
+                                                    const unsigned* sel, int64_t n,
                                                     uint32_t* tiles) {
   __shared__ uint32_t lds[kMNT / kWave + 1];
+  const uint32_t* V = auc_labels(V0, V1, sel);
   const int64_t base = (int64_t)blockIdx.x * kMTile + (int64_t)threadIdx.x * kMItems;
   uint32_t s = 0;
 #pragma unroll
@@ -40,10 +48,12 @@ __global__ __launch_bounds__(kMNT) void k_auc_tiles(const uint32_t* V, int64_t n
 
 // per tile of the sorted labels: every negative adds the positives ranked below it (the
 // tile's base from the scan of tile sums), summed exactly in double (integers below 2^53)
-__global__ __launch_bounds__(kMNT) void k_auc_area_tiles(const uint32_t* V, int64_t n,
+__global__ __launch_bounds__(kMNT) void k_auc_area_tiles(const uint32_t* V0, const uint32_t* V1,
+                                                         const unsigned* sel, int64_t n,
                                                          const uint32_t* tilebase,
                                                          double* part) {
   __shared__ uint32_t lds[kMNT / kWave + 1];
+  const uint32_t* V = auc_labels(V0, V1, sel);
   __shared__ double red[kMNT / kWave];
   const int64_t base = (int64_t)blockIdx.x * kMTile + (int64_t)threadIdx.x * kMItems;
   uint32_t lab[kMItems];
@@ -105,19 +115,21 @@ int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
   return DFX_OK;
 }
 
-// ---- the AUC lane: a stable sort with few, short launches, then a tiled counting pass -------
+// ---- the AUC lane: a stable sort, then a tiled counting pass ---------------------------------
 // Beside the backward the AUC needs only to finish within a step, taking as few CU slots and
-// as little memory traffic from the backward as possible (a look-back sort's spinning blocks
-// would park on CUs; a search per (item, tile) pair floods them):
-//   k_auc_runs        one block per 4096-item tile (input order): stable LSD sort of the tile
-//                     in LDS; out: u64 keys (orderable pred << 32 | input index) and labels
-//   merge_runs        log2(tiles) rounds of LDS-tiled pairwise merges (sort.hip): with the
-//                     input index in the key every comparison is strict, so the result is
-//                     the global stable sort by pred
+// as little memory traffic from the backward as possible.  Two sorts (context kwarg auc_sort):
+//   radix (default)   the onesweep LSD radix sort (sort.hip) of (orderable pred, label) on the
+//                     pred's four 8-bit digits (constant digits skipped): a B = 100 k snapshot
+//                     is 25 tiles per pass, so the look-back blocks are few and short-lived
+//   merge             k_auc_runs: one block per 4096-item tile (input order) sorts the tile in
+//                     LDS into u64 keys (orderable pred << 32 | input index) and labels; then
+//                     log2(tiles) rounds of LDS-tiled pairwise merges (sort.hip merge_runs):
+//                     with the input index in the key every comparison is strict.  Each round
+//                     waits on dependent global binary searches (~35 us per round at 100 k)
+// Both are the global stable sort by pred (ties in input order), so the results are equal.
 //   k_auc_tiles / k_auc_area_tiles / k_auc_final   positives per 2048-item tile, their scan,
 //                     each negative's count of positives ranked below it (exact in double),
 //                     AUC*n with the flip and the P = 0 / n rule
-// The result is deterministic and equals the global stable sort's rank-sum.
 constexpr int kArNT = 256, kArItems = 16, kArTile = kArNT * kArItems;  // 4096
 
 __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* __restrict__ key,
@@ -198,7 +210,7 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
 }
 
 // AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate) {
+int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix) {
   Workspace& ws = *L.ws;
   if (B <= 0) {
     if (!accumulate) DFX_HIP(hipMemsetAsync(out_dev, 0, sizeof(double), L.stream));
@@ -206,51 +218,57 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate) {
   }
   DFX_TRY(auc_reserve(ws, B));
   const int64_t ntiles = (B + kArTile - 1) / kArTile;
-  uint64_t* k0 = ws.keys0.as<uint64_t>();
-  uint32_t* v0 = ws.vals0.as<uint32_t>();
-  // runs into (keys1, vals1): merge_runs ping-pongs through keys0 / keys1
-  uint64_t* kr = ws.keys1.as<uint64_t>();
-  uint32_t* vr = ws.vals1.as<uint32_t>();
-  hipLaunchKernelGGL(k_auc_runs, dim3((unsigned)ntiles), dim3(kArNT), 0, L.stream, B,
-                     ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), kr, vr);
-  const uint64_t* K = kr;
-  const uint32_t* V = vr;
-  if (ntiles > 1) {
-    if (ntiles <= kMaxMergeRuns) {
+  const uint32_t* V0 = nullptr;
+  const uint32_t* V1 = nullptr;
+  const unsigned* sel = nullptr;
+  if (radix || ntiles > kMaxMergeRuns) {
+    // the snapshot (ak0, av0) ping-pongs with (keys0, vals0) reinterpreted as u32; the
+    // result's buffer follows the number of active passes: sortmeta[31], read on the device
+    uint32_t* k1 = ws.keys0.as<uint32_t>();
+    uint32_t* v1 = ws.vals0.as<uint32_t>();
+    DFX_TRY((radix_sort_pairs<uint32_t, uint32_t>(L, ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(),
+                                                  k1, v1, B, 0, 32, nullptr, L.ds->sortmeta)));
+    V0 = ws.av0.as<uint32_t>();
+    V1 = v1;
+    sel = &L.ds->sortmeta[31];
+  } else {
+    // runs into (keys1, vals1): merge_runs ping-pongs through keys0 / keys1
+    uint64_t* kr = ws.keys1.as<uint64_t>();
+    uint32_t* vr = ws.vals1.as<uint32_t>();
+    hipLaunchKernelGGL(k_auc_runs, dim3((unsigned)ntiles), dim3(kArNT), 0, L.stream, B,
+                       ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), kr, vr);
+    const uint64_t* K = kr;
+    const uint32_t* V = vr;
+    if (ntiles > 1) {
       std::vector<int64_t> runs;
       for (int64_t r = 0; r < ntiles; ++r) runs.push_back(r * kArTile);
       runs.push_back(B);
       // merge_runs writes keys0 first: the runs in keys1 are read in the first round only
       merge_runs(L, runs, &K, &V);
-    } else {  // a very large batch: one radix sort of the (unique) u64 keys
-      DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, kr, vr, k0, v0, B, 0, 64, nullptr,
-                                                    L.ds->sortmeta)));
-      // the sorted pairs sit in (kr, vr) or (k0, v0), by sortmeta[31]: read back which
-      uint32_t sel = 0;
-      DFX_HIP(hipMemcpyAsync(&sel, &L.ds->sortmeta[31], 4, hipMemcpyDeviceToHost, L.stream));
-      DFX_HIP(hipStreamSynchronize(L.stream));
-      V = sel ? v0 : vr;
     }
+    V0 = V;
   }
   const int64_t nt = (B + kMTile - 1) / kMTile;
   DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (nt + 2)));
   DFX_TRY(ws.dscratch.ensure(sizeof(double) * (nt + 8)));
   uint32_t* tiles = ws.tiles.as<uint32_t>();
   uint32_t* npos = tiles + nt + 1;
-  hipLaunchKernelGGL(k_auc_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V, B, tiles);
+  hipLaunchKernelGGL(k_auc_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V0, V1, sel, B,
+                     tiles);
   scan_tiles_top(L, tiles, nt, npos);
   double* part = ws.dscratch.as<double>();
-  hipLaunchKernelGGL(k_auc_area_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V, B,
-                     tiles, part);
+  hipLaunchKernelGGL(k_auc_area_tiles, dim3((unsigned)nt), dim3(kMNT), 0, L.stream, V0, V1, sel,
+                     B, tiles, part);
   hipLaunchKernelGGL(k_auc_final, dim3(1), dim3(1024), 0, L.stream, part, nt, npos, B, out_dev,
                      accumulate ? 1 : 0);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev) {
+int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
+            bool radix) {
   DFX_TRY(auc_snapshot(L, L.stream, B, label, pred));
-  return auc_finish(L, B, out_dev, false);
+  return auc_finish(L, B, out_dev, false, radix);
 }
 
 __global__ void k_eval_part(int64_t B, const float* label, const float* pred, double* part) {
@@ -324,7 +342,7 @@ extern "C" int dfx_auc(dfx_ctx* ctx, int64_t B, const float* label, const float*
   DFX_CHECK_ARG(ctx && auc_n, "null argument");
   Context* c = &ctx->c;
   double* o = &c->ds->scratch[2];
-  DFX_TRY(auc_run(main_lane(c), B, label, pred, o));
+  DFX_TRY(auc_run(main_lane(c), B, label, pred, o, c->auc_radix));
   DFX_HIP(hipMemcpyAsync(auc_n, o, 8, hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;

@@ -30,8 +30,10 @@ constexpr int kOsItems = 16;
 constexpr int kOsTile = kOsNT * kOsItems;  // 4096 items per tile
 static_assert(kOsTile == kOsSortTile, "tile size");
 static_assert(kOsTile <= 4096, "rank packing below assumes < 2^12 items per wave");
+// k_os_scatter<.., IT>: IT <= 32 keeps a wave's 64 * IT items below 2^12 (rank packing), and
+// the look-back words are reserved for tiles of >= 2048 items (IT >= 8)
 constexpr int kOsMaxPasses = kOsDigits;
-constexpr int kOsLookback = 4;  // predecessor words read per look-back step
+constexpr int kOsLookback = 4;  // predecessor words read per look-back step (default)
 constexpr unsigned kOsNone = 0xFFFFFFFFu;
 // sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
@@ -145,7 +147,7 @@ __device__ inline unsigned long long os_word(uint32_t tag, uint32_t flag, uint32
   return ((unsigned long long)((tag << 2) | flag) << 32) | v;
 }
 
-template <typename K, typename P, int IT>
+template <typename K, typename P, int IT, int LB>
 __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1, int64_t n0,
                                                       const uint32_t* n_dev, unsigned int* meta,
                                                       int q, const uint32_t* counts,
@@ -245,15 +247,15 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
     uint32_t spins = 0;
     bool done = false;
     while (!done) {
-      unsigned long long v[kOsLookback];
+      unsigned long long v[LB];
 #pragma unroll
-      for (int i = 0; i < kOsLookback; ++i)
+      for (int i = 0; i < LB; ++i)
         v[i] = (k - i >= 0) ? __hip_atomic_load(status + (k - i) * 256 + t, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT)
                             : 0ull;
       bool stalled = false;
 #pragma unroll
-      for (int i = 0; i < kOsLookback; ++i) {
+      for (int i = 0; i < LB; ++i) {
         if (done || stalled || k < 0) continue;
         const uint32_t hi = (uint32_t)(v[i] >> 32);
         if ((hi >> 2) != tag || (hi & 3u) == 0) {
@@ -337,7 +339,18 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
                      const uint32_t* n_dev, int flags) {
   Workspace& ws = *L.ws;
-  const int64_t ntiles = n > 0 ? (n + kOsTile - 1) / kOsTile : 1;
+  const int it = (flags >> 16) & 0xFF ? (flags >> 16) & 0xFF : kOsItems;
+  const int lb = (flags >> 24) & 0x7F ? (flags >> 24) & 0x7F : kOsLookback;
+  if ((lb != 4 && lb != 16 && lb != 32) || (lb != 4 && it != 16)) {
+    set_error("radix_sort_pairs: look-back width 4, or 16 / 32 with 16 items per thread");
+    return DFX_ERR_ARG;
+  }
+  if (it != 8 && it != 16 && it != 32) {
+    set_error("radix_sort_pairs: items per thread must be 8, 16 or 32");
+    return DFX_ERR_ARG;
+  }
+  const int64_t tile = (int64_t)kOsNT * it;
+  const int64_t ntiles = n > 0 ? (n + tile - 1) / tile : 1;
   DFX_TRY(ws.os_reserve(n > 0 ? (n + 2047) / 2048 : 1));  // look-back words for tiles >= 2048
   uint32_t* parts = ws.os_parts();
   uint32_t* counts = ws.os_counts();
@@ -353,14 +366,24 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   const int npasses = (end_bit - begin_bit + 7) / 8;
   unsigned long long* status = ws.os_status();
   if (!(flags & kSortCountsReady)) {
-    hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)ntiles), dim3(kOsNT), 0, L.stream, k0, n,
-                       n_dev, begin_bit, npasses, parts);
+    hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)((n + kOsTile - 1) / kOsTile)), dim3(kOsNT),
+                       0, L.stream, k0, n, n_dev, begin_bit, npasses, parts);
   }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
                      begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8);
-  for (int q = 0; q < npasses; ++q)
-    hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems>), dim3((unsigned)ntiles), dim3(kOsNT), 0,
-                       L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status, L.err);
+  for (int q = 0; q < npasses; ++q) {
+#define DFX_OS_SCATTER(IT, LB)                                                               \
+    if (it == IT && lb == LB)                                                                \
+      hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)ntiles), dim3(kOsNT), 0, \
+                         L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status,     \
+                         L.err);
+    DFX_OS_SCATTER(8, 4)
+    DFX_OS_SCATTER(16, 4)
+    DFX_OS_SCATTER(32, 4)
+    DFX_OS_SCATTER(16, 16)
+    DFX_OS_SCATTER(16, 32)
+#undef DFX_OS_SCATTER
+  }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

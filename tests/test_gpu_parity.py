@@ -58,9 +58,12 @@ def test_localizer_rcv1_known_answers(H, rcv1, known):
     assert int(_rev(ou).sum()) == known["localizer_hash1000"]["sum_uidx"]
 
 
+@pytest.mark.parametrize("items,lookback", [(16, 4), (8, 4), (32, 4), (16, 16), (16, 32)])
 @pytest.mark.parametrize("kind", ["criteo", "ragged", "zipf", "u64", "dups", "big"])
-def test_localizer_synthetic(H, kind):
-    c = H.Context(0)
+def test_localizer_synthetic(H, kind, items, lookback):
+    """bit-exact Localizer; items: the radix sort's items per thread (tiles of 2048 / 4096 /
+    8192 items, context kwarg sort_items), lookback: predecessor words per look-back step"""
+    c = H.Context(0, sort_items=items, sort_lookback=lookback)
     if kind == "criteo":
         blk = D.synthetic(4000, 39, 1 << 24, seed=1)
     elif kind == "ragged":
@@ -197,6 +200,24 @@ def test_auc_and_evaluate(H):
     # degenerate batch: the reference returns 1 (not 1*n)
     assert H.auc(c, tl, c.tensor(np.ones(n, np.float32), torch.float32)) > 0
     assert H.auc(c, c.tensor(np.ones(n, np.float32), torch.float32), tp) == 1.0
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 100000, 1000003])
+def test_auc_radix_and_merge_sorts_agree(H, n):
+    """the AUC lane's two stable sorts (auc_sort=radix | merge): the same AUC*n, equal to the
+    input-order tie break of the oracle, with heavy ties (quantised predictions, one constant
+    digit pattern) and with all predictions equal (epoch 0, w = 0)"""
+    rng = np.random.default_rng(n)
+    label = np.where(rng.random(n) < 0.25, 1.0, -1.0).astype(np.float32)
+    for pred in [np.round(rng.standard_normal(n) * 8).astype(np.float32) / 8,
+                 np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32)]:
+        want = O.auc_stable_ties(label, pred) if O.has_ties(pred) else O.auc(label, pred)
+        got = []
+        for mode in ["radix", "merge"]:
+            c = H.Context(0, auc_sort=mode)
+            got.append(H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32)))
+        assert got[0] == got[1], got
+        assert abs(got[0] - want) <= 1e-4 * n, (got, want)
 
 
 # ---------------------------------------------------------------- Store / SGDUpdater
