@@ -104,6 +104,19 @@ _SIGS = {
     "dfx_dist_union": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]),
     "dfx_dist_union_rows": (ctypes.c_int, [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int,
                                            ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp, vp]),
+    "dfx_split_part_floats": (ctypes.c_int, [vp]),
+    "dfx_split_pxv_floats": (ctypes.c_int, [vp]),
+    "dfx_split_partition": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), c_u64,
+                                           ctypes.c_int, vp, vp, vp]),
+    "dfx_split_partition_wait": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i64p]),
+    "dfx_split_owner_begin": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64p, i64p,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "dfx_split_owner_forward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_split_combine": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp, c_i64,
+                                         ctypes.c_int, vp, vp]),
+    "dfx_split_owner_backward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_split_initv_local": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_split_initv_draw": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -631,6 +631,28 @@ __global__ void k_dist_initv_sum_finalize(const uint32_t* ftotal, const int64_t*
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
 }
 
+int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32_t* nuniq,
+                     uint32_t* ftotal, const uint32_t* gate, int64_t* count_dev) {
+  DFX_TRY(scan_u32(L, flags, bound, ftotal, nuniq, gate));
+  hipLaunchKernelGGL(k_dist_initv_count, dim3(1), dim3(1), 0, L.stream, ftotal, count_dev);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int initv_rank_draw(Context* c, const Lane& L, const uint32_t* excl, const uint32_t* ftotal,
+                    const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
+                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount) {
+  if (bound > 0) {
+    const dim3 igrid((unsigned)std::min<int64_t>((bound + kDNT - 1) / kDNT, 1024));
+    hipLaunchKernelGGL(k_dist_initv_sum, igrid, dim3(kDNT), 0, L.stream, excl, ftotal, nuniq,
+                       bound, segslot, counts_all, rank, c->T, c->P.V_init_scale, c->ds);
+  }
+  hipLaunchKernelGGL(k_dist_initv_sum_finalize, dim3(1), dim3(1), 0, L.stream, ftotal,
+                     counts_all, nranks, c->P.V_dim, c->T.vcap, c->ds, fcount);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
 // ---- union-indexed collectives (the north_star's literal reduce-scatter / all-gather) -------
 // The union of every worker's keys, sorted: union[excl[i]] = K[i] at run heads; upos[src] =
 // the union position of the item the merge took from source index src

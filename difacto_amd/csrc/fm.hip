@@ -29,17 +29,6 @@ constexpr int kFmNT = 256;
 // kFusedProbe: kFused whose nnz find their keys in the table (FwdArgs::index)
 enum FwdMode { kPredict = 0, kGradPrep = 1, kFused = 2, kFusedProbe = 3 };
 
-// p = -y / (1 + exp(y * pred)) [* weight]   (fm_loss.h:155-165).  exp in double, rounded:
-// correctly rounded like glibc's expf in all but rare ties (within the 1e-5 tolerance).
-__device__ inline float logit_p(float label, float pred, const float* rw, int64_t r) {
-  float y = label > 0 ? 1.f : -1.f;
-  float t = y * pred;
-  float e = (float)exp((double)t);
-  float den = 1.f + e;
-  float p = -y / den;
-  if (rw) p = p * rw[r];
-  return p;
-}
 
 // Coordinates [l*CPL, l*CPL+CPL) of a length-d row.  VEC: d is a multiple of the vector
 // width and the row 16-byte aligned, so a lane's chunk is wholly inside or wholly outside
@@ -111,7 +100,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           // the Localizer's key (localize.hip k_loc_transform) and its home slot
           const uint64_t id = a.index[jj];
           const uint64_t m = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-          key[t] = reverse_bytes(m);
+          key[t] = a.keys_ready ? id : reverse_bytes(m);
           hs[t] = tbl_hash(key[t], a.T);
           c[t] = (uint32_t)jj;
         } else if (PACKED && a.wv) {
@@ -214,7 +203,20 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       }
     }
     float pr = acc;
-    if (MODE != kGradPrep && d > 0) {
+    if (PROBE && a.part) {
+      // owner-computes split: this owner's share of the row; the worker sums the owners'
+      // shares and finishes the row (split.hip k_split_combine)
+      const int PS = split_part_floats(d);
+      float* pr_row = a.part + r * PS;
+      if (d > 0) {
+        store_coords<CPL, VEC>(pr_row, l, d, xv);
+        store_coords<CPL, VEC>(pr_row + d, l, d, xxvv);
+      }
+      if (l == 0) {
+        pr_row[2 * d] = acc;
+        pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+      }
+    } else if (MODE != kGradPrep && d > 0) {
       // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
       float t[CPL];
 #pragma unroll
@@ -232,7 +234,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       pr = (float)y;
       pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
     }
-    if (MODE == kPredict) {
+    if (PROBE && a.part) {
+      // written above
+    } else if (MODE == kPredict) {
       if (l == 0) a.pred[r] = pr;
     } else {
       const float predv = (MODE == kGradPrep) ? a.pred_in[r] : pr;
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
       }
     }
   }
-  if (MODE == kFused || PROBE) {
+  if ((MODE == kFused || PROBE) && !a.part) {
     for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
     if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
     __syncthreads();
@@ -308,7 +312,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
         const uint64_t jj = j < o1 ? j : o1 - 1;
         const uint64_t id = a.index[jj];
         const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-        key[m] = reverse_bytes(mm);
+        key[m] = a.keys_ready ? id : reverse_bytes(mm);
         hs[m] = tbl_hash(key[m], a.T);
         xm[m] = valued ? a.val[jj] : 1.f;
       }
@@ -378,8 +382,21 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
         }
       }
     }
+    if (a.part) {
+      // owner-computes split: this owner's share of the row (split.hip k_split_combine)
+      float* pr_row = a.part + r * split_part_floats(d);
+      if (l * 4 < d) {
+        *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+        *reinterpret_cast<float4*>(pr_row + d + l * 4) =
+            make_float4(xxvv[0], xxvv[1], xxvv[2], xxvv[3]);
+      }
+      if (l == 0) {
+        pr_row[2 * d] = acc;
+        pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+      }
+    }
     float pr = acc;
-    if (d > 0) {
+    if (d > 0 && !a.part) {
       // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
       float t4[4];
 #pragma unroll
@@ -396,9 +413,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
       pr = (float)y;
       pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
     }
-    const float p = logit_p(a.label[r], pr, a.rw, r);
+    const float p = a.part ? 0.f : logit_p(a.label[r], pr, a.rw, r);
     const int64_t xs = a.xs > d ? a.xs : d;
-    if (l == 0) {
+    if (a.part) {
+      // the partial is all this kernel writes
+    } else if (l == 0) {
       a.p_out[r] = p;
       if (xs > d) a.XVp[r * xs + d] = p;
       a.pred[r] = pr;
@@ -410,10 +429,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
         a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
       }
     }
-    if (d > 0 && l * 4 < d)  // XV_ *= p (fm_loss.h:196-199)
+    if (d > 0 && l * 4 < d && !a.part)  // XV_ *= p (fm_loss.h:196-199)
       *reinterpret_cast<float4*>(a.XVp + r * xs + l * 4) =
           make_float4(xv[0] * p, xv[1] * p, xv[2] * p, xv[3] * p);
   }
+  if (a.part) return;  // block-uniform: no loss partial in split mode
   for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
   if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
   __syncthreads();

@@ -4,6 +4,18 @@
 
 namespace dfx {
 
+// p = -y / (1 + exp(y * pred)) [* weight]   (fm_loss.h:155-165).  exp in double, rounded:
+// correctly rounded like glibc's expf in all but rare ties (within the 1e-5 tolerance).
+__device__ inline float logit_p(float label, float pred, const float* rw, int64_t r) {
+  float y = label > 0 ? 1.f : -1.f;
+  float t = y * pred;
+  float e = (float)exp((double)t);
+  float den = 1.f + e;
+  float p = -y / den;
+  if (rw) p = p * rw[r];
+  return p;
+}
+
 struct FwdArgs {
   int64_t B;
   const uint64_t* offs;
@@ -41,7 +53,16 @@ struct FwdArgs {
   // fused: the AUC lane's snapshot (orderable pred key, label > 0), written by the forward
   uint32_t* auc_key;
   uint32_t* auc_lab;
+  // owner-computes split (split.hip): index holds the final keys (no ReverseBytes / max_index),
+  // and the forward writes per row its partial [XV(d) | XXVV(d) | sum w x | 0 0 0]
+  // (split_part_floats(d) floats) instead of pred / p / XV*p / loss
+  int keys_ready;
+  float* part;
 };
+
+// the owner-computes split's per-row forward partial and its per-row [XV*p | p] record
+__host__ __device__ inline int split_part_floats(int d) { return 2 * d + 4; }
+__host__ __device__ inline int split_pxv_floats(int d) { return d + 4; }
 
 struct BwdArgs {
   const uint32_t* segstart;  // nseg+1

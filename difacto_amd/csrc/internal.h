@@ -195,6 +195,17 @@ struct Context {
   // pushing worker in rank order, InitV per server (KVStoreDist's HandlePush)
   int dist_sum = 1;
   bool dist_initv_pending[2] = {false, false};
+  // owner-computes split (split.hip), per step slot.  Worker: the batch's rows and its
+  // partition's owner-major block offsets.  Owner: the received sub-rows (all workers'
+  // concatenated) and their keys / values, localized into ows[slot]; split_resolved: a count
+  // push found-or-inserted the slot's keys (the backward then inserts none)
+  int64_t split_B[2] = {0, 0}, split_nblk[2] = {0, 0};
+  int64_t split_rows[2] = {0, 0}, split_nnz[2] = {0, 0};
+  const uint64_t* split_keys[2] = {nullptr, nullptr};
+  const float* split_x[2] = {nullptr, nullptr};
+  bool split_resolved[2] = {false, false};
+  bool split_initv_pending[2] = {false, false};
+  bool split_initv_gated[2] = {false, false};  // the requests came from the backward (n_init)
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }
@@ -296,6 +307,7 @@ struct LocOut {
   const float* value = nullptr;
   uint32_t* occ_row = nullptr;
   float* occ_x = nullptr;
+  bool keys_ready = false;  // index holds the final keys (the split owner's received keys)
 };
 int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o);
@@ -332,6 +344,22 @@ void cap_release(Context* c);
 int store_maybe_grow(Context* c);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
+// push_agg=sum InitV ranked over all owners (dist.hip), for the flags of any owner step: count
+// scans the flags (per unique key, key order) in place and writes their number to count_dev;
+// draw draws this owner's flagged keys after every lower owner's and advances the shared seed
+// by the total of counts_all[nranks]
+int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32_t* nuniq,
+                     uint32_t* ftotal, const uint32_t* gate, int64_t* count_dev);
+int initv_rank_draw(Context* c, const Lane& L, const uint32_t* excl, const uint32_t* ftotal,
+                    const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
+                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount);
+// Update(kFeaCount) of a localized batch's segments (count = segment length), InitV requests
+// into flags; no draws (store.hip)
+int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_t* segstart,
+                       const uint32_t* segslot, uint32_t* flags, const DevState* nds);
+// SGDUpdater::Get's find-or-insert over a lane's sorted unique keys (step.hip k_probe_keys)
+int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uniq,
+                   uint32_t* segslot);
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
             bool radix);
 // the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream

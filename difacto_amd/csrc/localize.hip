@@ -33,6 +33,7 @@ struct TransformArgs {
   uint32_t* pay32;  // narrow payload (row only): no col to scatter and no values to gather
   uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
   DevState* ds;     // the lane's state: OR / AND of the keys
+  int keys_ready;   // index holds the final keys (no ReverseBytes / max_index)
 };
 
 __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
   for (uint64_t j = j0 + threadIdx.x; j < j1; j += kLocNT) {
     const uint64_t id = a.index[j];
     const uint64_t m = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-    const uint64_t k = reverse_bytes(m);
+    const uint64_t k = a.keys_ready ? id : reverse_bytes(m);
     vor |= k;
     vand &= k;
     // digit counts; a digit the whole wave shares (every constant digit) costs one atomic
@@ -306,6 +307,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   TransformArgs t{};
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
   t.keys = k0; t.pay = p0; t.pay32 = q0; t.parts = ws.os_parts(); t.ds = ds;
+  t.keys_ready = o.keys_ready ? 1 : 0;
   hipLaunchKernelGGL(k_loc_transform, dim3((unsigned)((B + kLocRows - 1) / kLocRows)),
                      dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits

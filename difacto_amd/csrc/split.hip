@@ -1,0 +1,496 @@
+// Owner-computes FM over the key-range shards: SURVEY §8(e)'s synchronous semantics (one
+// reference step, sgd_learner.cc:201-317, on the concatenation of the workers' batches) with the
+// forward and backward run where the model rows live.
+//
+// The all-to-all-v schedule of dist.hip moves every touched key's model record to its worker
+// and a gradient record back (~5.8 KB per row at d = 16), and each owner reads a key's entry and
+// V twice per step.  Here the owners compute instead; only per-row quantities travel:
+//   worker  k_split_count / k_split_scatter   each nnz's key (ReverseBytes(id % max_index)) to
+//           its owner floor(key * N / 2^64), row order kept; nnz per (owner, row)
+//   -> alltoallv keys (+ values), row counts
+//   owner   owner_begin   the received sub-rows of all workers, concatenated in rank order, go
+//           through the Localizer (sorted unique keys, occurrences in (worker, row, nnz) order =
+//           the concatenated batch's order); epoch 0: Update(kFeaCount) + ranked InitV
+//   owner   owner_forward per received row its partial [XV(d) | XXVV(d) | sum w x | 0 0 0] over
+//           the owner's keys (the fused forward, fm.hip, in partial mode)
+//   -> alltoallv partials back
+//   worker  combine       per row the owners' partials summed in rank order -> pred (clip), p,
+//           logloss, the AUC snapshot, and the row [XV*p (d) | p | 0 0 0] (fm_loss.h:67-203)
+//   -> every owner receives every worker's rows
+//   owner   owner_backward the fused backward + FTRL/AdaGrad over the owner's keys, reading the
+//           rows' p and XV*p from the received records; ranked InitV
+// Per row that is ~40 keys + N partials + N records (~1.9 KB at d = 16, N = 8) instead of
+// ~5.8 KB, and each owner touches a key's entry and V once per step as the fused step does.
+// At N = 1 the partial is the whole row and the step equals the fused step bit for bit; at
+// N > 1 the forward's sums are regrouped by owner (within the 1e-5 tolerance), the gradients
+// are summed over the occurrences in the concatenated batch's order.
+#include "fm_args.h"
+
+namespace dfx {
+
+void sum_parts(Context* c, const double* part, int64_t n, double* out, bool accumulate);
+
+constexpr int kSpNT = 256;
+constexpr int kSpRows = 64;  // rows per partition block
+
+__device__ inline uint32_t split_owner(uint64_t k, uint32_t n) {
+  return (uint32_t)__umul64hi(k, (uint64_t)n);  // floor(k * n / 2^64), dist.hip owner_of
+}
+
+__device__ inline uint64_t split_key(uint64_t id, uint64_t max_index) {
+  const uint64_t m = max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % max_index;
+  return reverse_bytes(m);  // the Localizer's key (localize.hip k_loc_transform)
+}
+
+// the block's rows [r0, r0 + nr): offsets into LDS; nnz j's row by upper_bound
+__device__ inline int split_row_of(const uint64_t* so, int nr, uint64_t j) {
+  int lo = 0, hi = nr;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (so[mid] <= j) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// nnz per (owner, row) -> row_cnt[owner * B + row]; per (owner, block) -> blk[owner * nblk + b]
+__global__ __launch_bounds__(kSpNT) void k_split_count(int64_t B, const uint64_t* offs,
+                                                       const uint64_t* index, uint64_t max_index,
+                                                       uint32_t n, uint32_t* row_cnt,
+                                                       uint32_t* blk, int64_t nblk) {
+  __shared__ uint32_t cnt[kSpRows * kMaxDistRanks];  // [row][owner]
+  __shared__ uint64_t so[kSpRows + 1];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
+  const int nr = (int)((B - r0) < kSpRows ? (B - r0) : kSpRows);
+  for (int i = t; i < kSpRows * (int)n; i += kSpNT) cnt[i] = 0;
+  for (int i = t; i <= nr; i += kSpNT) so[i] = offs[r0 + i];
+  __syncthreads();
+  for (uint64_t j = so[0] + t; j < so[nr]; j += kSpNT) {
+    const uint32_t o = split_owner(split_key(index[j], max_index), n);
+    atomicAdd(&cnt[split_row_of(so, nr, j) * n + o], 1u);
+  }
+  __syncthreads();
+  for (int i = t; i < nr * (int)n; i += kSpNT) {
+    const int o = i / nr, rl = i % nr;  // owner-major: consecutive threads, consecutive rows
+    row_cnt[(int64_t)o * B + r0 + rl] = cnt[rl * n + o];
+  }
+  for (int o = t; o < (int)n; o += kSpNT) {
+    uint32_t s = 0;
+    for (int rl = 0; rl < nr; ++rl) s += cnt[rl * n + o];
+    blk[(int64_t)o * nblk + blockIdx.x] = s;
+  }
+}
+
+// split counts per owner from the scanned block totals, into the pinned host words
+__global__ void k_split_totals(const uint32_t* blk_excl, const uint32_t* total, int64_t nblk,
+                               uint32_t n, unsigned long long* out) {
+  const uint32_t o = threadIdx.x;
+  if (o >= n) return;
+  const uint32_t a = blk_excl[(int64_t)o * nblk];
+  const uint32_t b = (o + 1 < n) ? blk_excl[(int64_t)(o + 1) * nblk] : *total;
+  out[o] = (unsigned long long)(b - a);
+}
+
+// each nnz's key (and value) to its owner's run, in nnz order within each owner: the block's
+// chunks of kSpNT nnz are ranked by owner with wave ballots (exact and order preserving)
+__global__ __launch_bounds__(kSpNT) void k_split_scatter(int64_t B, const uint64_t* offs,
+                                                         const uint64_t* index,
+                                                         const float* value, uint64_t max_index,
+                                                         uint32_t n, const uint32_t* blk_excl,
+                                                         int64_t nblk, uint64_t* keys_out,
+                                                         float* x_out) {
+  constexpr int W = kSpNT / kWave;
+  __shared__ uint32_t run[kMaxDistRanks];
+  __shared__ uint32_t wc[W][kMaxDistRanks];
+  const int t = threadIdx.x, w = t / kWave;
+  const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
+  const int nr = (int)((B - r0) < kSpRows ? (B - r0) : kSpRows);
+  const uint64_t j0 = offs[r0], j1 = offs[r0 + nr];
+  for (int o = t; o < (int)n; o += kSpNT) run[o] = blk_excl[(int64_t)o * nblk + blockIdx.x];
+  int bits = 0;
+  while ((1u << bits) < n) ++bits;
+  for (uint64_t c0 = j0; c0 < j1; c0 += kSpNT) {
+    for (int i = t; i < W * (int)n; i += kSpNT) (&wc[0][0])[(i / n) * kMaxDistRanks + i % n] = 0;
+    __syncthreads();
+    const uint64_t j = c0 + t;
+    const bool valid = j < j1;
+    const uint64_t key = valid ? split_key(index[j], max_index) : 0ull;
+    const uint32_t o = valid ? split_owner(key, n) : 0u;
+    uint64_t peers = __ballot(valid);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (o >> b) & 1u;
+      const uint64_t mb = __ballot(valid && bit);
+      peers &= bit ? mb : ~mb;
+    }
+    const uint32_t rk = (uint32_t)__popcll(peers & lanemask_lt());
+    if (valid && rk == 0) wc[w][o] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[o] + rk;
+      for (int v = 0; v < w; ++v) pos += wc[v][o];
+      keys_out[pos] = key;
+      if (x_out) x_out[pos] = value ? value[j] : 1.f;  // binary rows carry 1 when asked
+    }
+    __syncthreads();
+    for (int oo = t; oo < (int)n; oo += kSpNT) {
+      uint32_t s = 0;
+      for (int v = 0; v < W; ++v) s += wc[v][oo];
+      run[oo] += s;
+    }
+    __syncthreads();
+  }
+}
+
+// owner: the received per-row counts (scanned in place) -> u64 row offsets
+__global__ void k_split_offsets(const uint32_t* excl, const uint32_t* total, int64_t R,
+                                uint64_t* offs) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) offs[r] = excl[r];
+  if (r == R) offs[R] = *total;
+}
+
+// worker: the owners' partials of each row summed in rank order, then FMLoss::Predict's tail
+// (fm_loss.h:110-119), Evaluate, the AUC snapshot and CalcGrad's per-row factors
+// (fm_loss.h:155-199): pxv row [XV*p (d) | p | 0 0 0]
+__global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, int n, int d,
+                                                         const float* __restrict__ parts,
+                                                         const float* label, const float* rw,
+                                                         float* pred_out, float* pxv,
+                                                         double* loss_part, uint32_t* auc_key,
+                                                         uint32_t* auc_lab) {
+  __shared__ double red[kSpNT / kWave];
+  const int64_t r = (int64_t)blockIdx.x * kSpNT + threadIdx.x;
+  const int PS = split_part_floats(d), PX = split_pxv_floats(d);
+  double loss = 0;
+  if (r < B) {
+    float acc = 0.f;
+    for (int o = 0; o < n; ++o) acc += parts[((int64_t)o * M + r) * PS + 2 * d];
+    float pr = acc;
+    if (d > 0) {
+      float s = 0.f;
+      for (int l = 0; l < d; ++l) {
+        float xv = 0.f, xx = 0.f;
+        for (int o = 0; o < n; ++o) {
+          const float* q = parts + ((int64_t)o * M + r) * PS;
+          xv += q[l];
+          xx += q[d + l];
+        }
+        s += xv * xv - xx;  // s = sum_l (XV_l^2 - XXVV_l), serially over l
+      }
+      const double y = (double)acc + .5 * (double)s;
+      pr = (float)y;
+      pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);
+    }
+    const float p = logit_p(label[r], pr, rw, r);
+    if (pred_out) pred_out[r] = pr;
+    float* x = pxv + r * PX;
+    for (int l = 0; l < d; ++l) {
+      float xv = 0.f;
+      for (int o = 0; o < n; ++o) xv += parts[((int64_t)o * M + r) * PS + l];
+      x[l] = xv * p;  // XV_ *= p (fm_loss.h:196-199)
+    }
+    x[d] = p;
+    x[d + 1] = x[d + 2] = x[d + 3] = 0.f;
+    const double yy = label[r] > 0 ? 1.0 : -1.0;
+    loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+    if (auc_key) {
+      const uint32_t u = __float_as_uint(pr + 0.0f);
+      auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      auc_lab[r] = label[r] > 0 ? 1u : 0u;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kSpNT / kWave; ++i) s += red[i];
+    loss_part[blockIdx.x] = s;
+  }
+}
+
+__global__ void k_split_worker_finalize(DevState* ds, int64_t B) {
+  ds->prog[0] += (double)B;       // sgd::Progress of this worker (sgd_learner.cc:213-229)
+  ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
+}
+
+__global__ void k_split_zero_count(uint32_t* ftotal, int64_t* out) {
+  *ftotal = 0u;
+  *out = 0;
+}
+
+static Lane split_owner_lane(Context* c, int slot) {
+  return Lane{c->stream, &c->ows[slot], c->ods[slot], &c->ds->err};
+}
+
+}  // namespace dfx
+
+using namespace dfx;
+
+extern "C" {
+
+#define DFX_SPLIT_SLOT(slot) DFX_CHECK_ARG((slot) == 0 || (slot) == 1, "split: slot must be 0 or 1")
+
+int dfx_split_part_floats(dfx_ctx* ctx) {
+  return ctx ? split_part_floats(ctx->c.P.V_dim) : -1;
+}
+
+int dfx_split_pxv_floats(dfx_ctx* ctx) { return ctx ? split_pxv_floats(ctx->c.P.V_dim) : -1; }
+
+int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* b, uint64_t max_index,
+                        int nranks, uint64_t* keys_out, float* x_out, uint32_t* row_cnt_out) {
+  DFX_CHECK_ARG(ctx && b, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
+  DFX_CHECK_ARG(b->size >= 0 && b->nnz >= 0, "split_partition: negative sizes");
+  DFX_CHECK_ARG(b->size == 0 || b->offset, "split_partition: null offset");
+  DFX_CHECK_ARG(b->nnz == 0 || (b->index && keys_out), "split_partition: null buffer");
+  DFX_CHECK_ARG(!b->value || b->nnz == 0 || x_out, "split_partition: valued data needs x_out");
+  if (b->nnz == 0) x_out = nullptr;
+  DFX_CHECK_ARG(b->size == 0 || row_cnt_out, "split_partition: null row counts");
+  DFX_CHECK_ARG(max_index != 0, "split_partition: max_index must be > 0");
+  DFX_CHECK_ARG(b->nnz < 0xFFFFFFFFll, "split_partition: nnz must fit u32");
+  Context* c = &ctx->c;
+  DFX_TRY(pipeline_init(c));
+  Workspace& bw = c->bws[slot];
+  const int64_t B = b->size;
+  const int64_t nblk = B > 0 ? (B + kSpRows - 1) / kSpRows : 0;
+  DFX_TRY(bw.hist.ensure((size_t)(nblk * nranks + 1) * 4));
+  uint32_t* blk = bw.hist.as<uint32_t>();
+  uint32_t* total = &c->bds[slot]->totals[0];
+  const Lane L{c->stream, &bw, c->bds[slot], &c->ds->err};
+  if (nblk > 0) {
+    hipLaunchKernelGGL(k_split_count, dim3((unsigned)nblk), dim3(kSpNT), 0, c->stream, B,
+                       b->offset, b->index, max_index, (uint32_t)nranks, row_cnt_out, blk, nblk);
+  }
+  DFX_TRY(scan_u32(L, blk, nblk * nranks, total));
+  if (nblk > 0) {
+    hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)nblk), dim3(kSpNT), 0, c->stream, B,
+                       b->offset, b->index, b->value, max_index, (uint32_t)nranks, blk, nblk,
+                       keys_out, x_out);
+    hipLaunchKernelGGL(k_split_totals, dim3(1), dim3(kMaxDistRanks), 0, c->stream, blk, total,
+                       nblk, (uint32_t)nranks, c->dist_host[slot]);
+  } else {
+    for (int o = 0; o < nranks; ++o) c->dist_host[slot][o] = 0;
+  }
+  DFX_HIP(hipEventRecord(c->ev_loc[slot], c->stream));
+  DFX_HIP(hipGetLastError());
+  c->split_B[slot] = B;
+  c->split_nblk[slot] = nblk;
+  return DFX_OK;
+}
+
+int dfx_split_partition_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_counts) {
+  DFX_CHECK_ARG(ctx && split_counts, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(c->loc_stream, "split_partition_wait: no dfx_split_partition issued");
+  DFX_HIP(hipEventSynchronize(c->ev_loc[slot]));
+  for (int o = 0; o < nranks; ++o) split_counts[o] = (int64_t)c->dist_host[slot][o];
+  return DFX_OK;
+}
+
+int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const float* x,
+                          uint32_t* row_cnt, const int64_t* rows_per_rank,
+                          const int64_t* keys_per_rank, int nranks, int job_type,
+                          int push_cnt) {
+  DFX_CHECK_ARG(ctx && rows_per_rank && keys_per_rank, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(c->dist_sum, "split: needs push_agg=sum (one Update per key per step)");
+  DFX_CHECK_ARG(!c->split_initv_pending[0] && !c->split_initv_pending[1],
+                "split_owner_begin: finish the pending InitV first (dfx_split_initv_*)");
+  DFX_TRY(pipeline_init(c));
+  int64_t R = 0, nnz = 0;
+  for (int g = 0; g < nranks; ++g) {
+    DFX_CHECK_ARG(rows_per_rank[g] >= 0 && keys_per_rank[g] >= 0, "split: negative sizes");
+    R += rows_per_rank[g];
+    nnz += keys_per_rank[g];
+  }
+  DFX_CHECK_ARG(R == 0 || row_cnt, "split_owner_begin: null row counts");
+  DFX_CHECK_ARG(nnz == 0 || keys, "split_owner_begin: null keys");
+  DFX_CHECK_ARG(nnz < 0xFFFFFFFFll && R < 0x7FFFFFFFll, "split_owner_begin: too many keys");
+  // this step inserts at most nnz keys and draws at most nnz V rows (slots are not carried
+  // across steps here, so the store may grow at this point)
+  DFX_TRY(cap_check(c, nnz));
+  // a server of one of nranks key ranges: hash keys by their position inside the range
+  DFX_TRY(table_set_ranges(c, nranks));
+  const Lane OL = split_owner_lane(c, slot);
+  Workspace& ows = c->ows[slot];
+  DFX_TRY(loc_reserve(ows, nnz));
+  DFX_TRY(ows.rowid.ensure((size_t)(R + 1) * 8));
+  DFX_TRY(ows.oflags.ensure((size_t)(nnz + 1) * 4));
+  uint64_t* offs = ows.rowid.as<uint64_t>();
+  uint32_t* rtotal = &OL.ds->totals[4];
+  DFX_TRY(scan_u32(OL, row_cnt, R, rtotal));
+  hipLaunchKernelGGL(k_split_offsets, dim3((unsigned)((R + 1 + 255) / 256)), dim3(256), 0,
+                     OL.stream, row_cnt, rtotal, R, offs);
+  LocOut o;
+  o.uniq = ows.uniq.as<uint64_t>();
+  o.segstart = ows.segstart.as<uint32_t>();
+  o.occ_row = ows.occ_row.as<uint32_t>();
+  o.value = x;
+  o.occ_x = x ? ows.occ_x.as<float>() : nullptr;
+  o.keys_ready = true;
+  DFX_TRY(localize_run(c, OL, R, nnz, offs, keys, ~0ull, o));
+  // long segments (hot keys): their chunk plan, as the fused step's Localizer lane makes it
+  DFX_TRY(chunk_plan(OL, nnz, o.segstart, ows.flags.as<uint32_t>(), ows.rowtmp.as<uint32_t>(),
+                     &OL.ds->totals[1]));
+  c->split_rows[slot] = R;
+  c->split_nnz[slot] = nnz;
+  c->split_keys[slot] = keys;
+  c->split_x[slot] = x;
+  c->split_resolved[slot] = false;
+  DFX_CHECK_ARG(job_type == DFX_JOB_TRAINING || job_type == DFX_JOB_VALIDATION ||
+                    job_type == DFX_JOB_PREDICTION,
+                "split_owner_begin: bad job type");
+  const bool cnt = push_cnt && job_type == DFX_JOB_TRAINING && c->P.V_dim > 0 && nnz > 0;
+  if (!cnt && job_type != DFX_JOB_TRAINING && nnz > 0) {
+    // a step without a backward: SGDUpdater::Get still inserts every key (model_[key],
+    // sgd_updater.cc:34-58), as the fused step's probe does
+    DFX_TRY(probe_keys_run(c, OL, nnz, o.uniq, ows.slot.as<uint32_t>()));
+    c->split_resolved[slot] = true;
+  }
+  if (cnt) {
+    // Update(kFeaCount) of the concatenated batch: find-or-insert every key (Get), add its
+    // occurrence count; InitV requests in key order, drawn ranked over all owners
+    DFX_TRY(probe_keys_run(c, OL, nnz, o.uniq, ows.slot.as<uint32_t>()));
+    DFX_TRY(push_cnt_seg_flags(c, OL, nnz, o.segstart, ows.slot.as<uint32_t>(),
+                               ows.oflags.as<uint32_t>(), OL.ds));
+    c->split_resolved[slot] = true;
+    c->split_initv_pending[slot] = true;
+    c->split_initv_gated[slot] = false;
+  }
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_SPLIT_SLOT(slot);
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(!c->split_initv_pending[slot],
+                "split_owner_forward: the count push's InitV is pending (dfx_split_initv_*)");
+  const int64_t R = c->split_rows[slot];
+  if (R == 0) return DFX_OK;
+  DFX_CHECK_ARG(part_out, "split_owner_forward: null buffer");
+  Workspace& ows = c->ows[slot];
+  FwdArgs a{};
+  a.B = R; a.offs = ows.rowid.as<uint64_t>(); a.val = c->split_x[slot];
+  a.index = c->split_keys[slot]; a.max_index = ~0ull; a.keys_ready = 1;
+  a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
+  a.part = part_out;
+  int nblk = 0;
+  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* parts,
+                      int64_t part_rows, int nranks, float* pxv_out, float* pred_out) {
+  DFX_CHECK_ARG(ctx && b, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
+  Context* c = &ctx->c;
+  const int64_t B = b->size;
+  DFX_CHECK_ARG(B == c->split_B[slot], "split_combine: batch differs from split_partition's");
+  DFX_CHECK_ARG(B == 0 || (b->label && parts && pxv_out), "split_combine: null buffer");
+  DFX_CHECK_ARG(part_rows >= B, "split_combine: part_rows < the batch's rows");
+  const int d = c->P.V_dim;
+  Workspace& ws = c->ws;
+  DFX_TRY(ws.dscratch.ensure((size_t)(B / kSpNT + 64) * 8));
+  double* loss_part = ws.dscratch.as<double>() + 8;
+  const int64_t nb = (B + kSpNT - 1) / kSpNT;
+  // the AUC lane's snapshot buffers are free once its previous AUC is done
+  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  DFX_TRY(auc_reserve(c->aws, B));
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+  if (B > 0) {
+    hipLaunchKernelGGL(k_split_combine, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, B,
+                       part_rows, nranks, d, parts, b->label, b->weight, pred_out, pxv_out, loss_part,
+                       c->aws.ak0.as<uint32_t>(), c->aws.av0.as<uint32_t>());
+  }
+  sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
+  DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
+  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
+  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_SPLIT_SLOT(slot);
+  Context* c = &ctx->c;
+  DFX_CHECK_ARG(!c->split_initv_pending[0] && !c->split_initv_pending[1],
+                "split_owner_backward: finish the pending InitV first (dfx_split_initv_*)");
+  const int64_t R = c->split_rows[slot], nnz = c->split_nnz[slot];
+  const int d = c->P.V_dim;
+  if (nnz > 0) {
+    DFX_CHECK_ARG(pxv, "split_owner_backward: null records");
+    Workspace& ows = c->ows[slot];
+    DevState* ods = c->ods[slot];
+    BwdArgs g{};
+    g.segstart = ows.segstart.as<uint32_t>(); g.ds = ods; g.nseg_host = -1; g.segcol = nullptr;
+    g.occ_row = ows.occ_row.as<uint32_t>();
+    g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
+    g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d); g.d = d;
+    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P;
+    g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
+    g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
+    g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();
+    g.nchunks = &ods->totals[1];
+    DFX_TRY(ows.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 8));
+    g.part = ows.Vb.as<double>();
+    DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
+    DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
+  }
+  (void)R;
+  // every owner takes part in the InitV ranking, with or without keys this step
+  if (d > 0) {
+    c->split_initv_pending[slot] = true;
+    c->split_initv_gated[slot] = true;
+  }
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_split_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev) {
+  DFX_CHECK_ARG(ctx && count_dev, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  Context* c = &ctx->c;
+  const Lane OL = split_owner_lane(c, slot);
+  uint32_t* ftotal = &OL.ds->totals[2];
+  const int64_t nnz = c->split_nnz[slot];
+  if (!c->split_initv_pending[slot] || nnz == 0) {
+    hipLaunchKernelGGL(k_split_zero_count, dim3(1), dim3(1), 0, OL.stream, ftotal, count_dev);
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
+  }
+  // the backward counts its requests in n_init: no requests (the steady state) skip the scan
+  return initv_rank_count(OL, c->ows[slot].oflags.as<uint32_t>(), nnz, &OL.ds->u_count, ftotal,
+                          c->split_initv_gated[slot] ? &c->ds->n_init : nullptr, count_dev);
+}
+
+int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
+                         int nranks) {
+  DFX_CHECK_ARG(ctx && counts_all_dev, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks && rank >= 0 && rank < nranks,
+                "split_initv_draw: bad rank");
+  Context* c = &ctx->c;
+  const Lane OL = split_owner_lane(c, slot);
+  const bool pend = c->split_initv_pending[slot] && c->split_nnz[slot] > 0;
+  DFX_TRY(initv_rank_draw(c, OL, c->ows[slot].oflags.as<uint32_t>(), &OL.ds->totals[2],
+                          &OL.ds->u_count, pend ? c->split_nnz[slot] : 0,
+                          c->ows[slot].slot.as<uint32_t>(), counts_all_dev, rank, nranks,
+                          &c->ds->n_init));
+  c->split_initv_pending[slot] = false;
+  return DFX_OK;
+}
+
+}  // extern "C"

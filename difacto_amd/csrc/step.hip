@@ -155,6 +155,17 @@ __global__ __launch_bounds__(kProbeNT) void k_probe_keys(const uint64_t* __restr
   }
 }
 
+// find-or-insert of a lane's sorted unique keys (u_count of the lane's state) into segslot
+int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uniq,
+                   uint32_t* segslot) {
+  if (bound <= 0) return DFX_OK;
+  const dim3 ug((unsigned)((bound + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
+  hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, L.stream, uniq, L.ds, c->T, nullptr,
+                     segslot, c->ds);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
 // the pull after a count push: {w, vrow} of each unique key by slot
 __global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ segslot,
                                                    const DevState* nds, const Entry* ent,

@@ -154,6 +154,15 @@ int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
   return run_initv(c, -1, n_bound, flags, total_dev, segslot, nds);
 }
 
+int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_t* segstart,
+                       const uint32_t* segslot, uint32_t* flags, const DevState* nds) {
+  if (n_bound <= 0) return DFX_OK;
+  hipLaunchKernelGGL(k_push_cnt_seg, dim3((n_bound + kStNT - 1) / kStNT), dim3(kStNT), 0,
+                     L.stream, segstart, segslot, c->T, c->P, flags, nds);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
 // ---- standalone Get: interleaved [w | V] + lens ---------------------------------------------
 // SGDUpdater::Get (sgd_updater.cc:34-58): V only if present and not (l1_shrk && w == 0).
 // Missing keys read as w = 0 without V; Get's insertion of empty entries is not observable.

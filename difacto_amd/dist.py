@@ -62,6 +62,8 @@ class Shard:
         self._keys = [None, None]
         self._cnt = [None, None]
         self._want_cnt = [False, False]
+        self._split = [None, None]
+        self._split_R = [0, 0]
 
     def _slot_buffers(self, slot, n, want_cnt):
         dev = self.ctx.device
@@ -158,6 +160,70 @@ class Shard:
         check(_lib.lib().dfx_dist_initv_draw(self.ctx.h, slot, _p(counts_all), int(rank),
                                              self.nranks))
 
+    # owner-computes split (csrc/split.hip) ---------------------------------------------------
+    def split_partition(self, dblk, slot=0, max_index=MAX_INDEX, want_x=False):
+        """issue the partition of the batch's nnz by owner (asynchronous); values travel for
+        valued data (want_x: binary data too, as 1s)"""
+        dev = self.ctx.device
+        b = dblk.as_batch()
+        B, nnz = int(dblk.size), int(dblk.nnz)
+        keys = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+        x = (torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+             if (b.value or want_x) else None)
+        rc = torch.empty(max(self.nranks * B, 1), dtype=torch.int32, device=dev)
+        check(_lib.lib().dfx_split_partition(self.ctx.h, slot, ctypes.byref(b),
+                                             ctypes.c_uint64(max_index), self.nranks, _p(keys),
+                                             _p(x), _p(rc)))
+        self._split[slot] = (keys, x, rc, B)
+
+    def split_partition_wait(self, slot=0):
+        """-> (keys grouped by owner, their values or None, nnz per (owner, row) [N * B], keys
+        per owner, B)"""
+        splits = (ctypes.c_int64 * self.nranks)()
+        check(_lib.lib().dfx_split_partition_wait(self.ctx.h, slot, self.nranks, splits))
+        keys, x, rc, B = self._split[slot]
+        return keys, x, rc[:self.nranks * B], list(splits), B
+
+    def split_owner_begin(self, keys, x, row_cnt, rows_per_rank, keys_per_rank, job_type,
+                          push_cnt, slot=0):
+        """row_cnt: the received per-row counts (scanned in place)"""
+        rows = (ctypes.c_int64 * self.nranks)(*[int(v) for v in rows_per_rank])
+        kpr = (ctypes.c_int64 * self.nranks)(*[int(v) for v in keys_per_rank])
+        self._split_R[slot] = sum(int(v) for v in rows_per_rank)
+        check(_lib.lib().dfx_split_owner_begin(self.ctx.h, slot, _p(keys), _p(x), _p(row_cnt),
+                                               rows, kpr, self.nranks, int(job_type),
+                                               int(bool(push_cnt))))
+
+    def split_owner_forward(self, slot=0):
+        R = self._split_R[slot]
+        PS = _lib.lib().dfx_split_part_floats(self.ctx.h)
+        part = torch.empty(max(R * PS, 1), dtype=torch.float32, device=self.ctx.device)
+        check(_lib.lib().dfx_split_owner_forward(self.ctx.h, slot, _p(part)))
+        return part[:R * PS]
+
+    def split_combine(self, dblk, parts, part_rows, slot=0, pred=None, pxv=None):
+        """-> the batch's [XV*p | p | 0 0 0] rows (into pxv when given, part_rows rows)"""
+        PX = _lib.lib().dfx_split_pxv_floats(self.ctx.h)
+        if pxv is None:
+            pxv = torch.zeros(max(int(part_rows) * PX, 1), dtype=torch.float32,
+                              device=self.ctx.device)
+        b = dblk.as_batch()
+        check(_lib.lib().dfx_split_combine(self.ctx.h, slot, ctypes.byref(b), _p(parts),
+                                           int(part_rows), self.nranks, _p(pxv), _p(pred)))
+        return pxv
+
+    def split_owner_backward(self, pxv, slot=0):
+        check(_lib.lib().dfx_split_owner_backward(self.ctx.h, slot, _p(pxv)))
+
+    def split_initv_local(self, slot=0):
+        out = torch.empty(1, dtype=torch.int64, device=self.ctx.device)
+        check(_lib.lib().dfx_split_initv_local(self.ctx.h, slot, _p(out)))
+        return out
+
+    def split_initv_draw(self, counts_all, rank, slot=0):
+        check(_lib.lib().dfx_split_initv_draw(self.ctx.h, slot, _p(counts_all), int(rank),
+                                              self.nranks))
+
     # model files (SGDLearner::SaveLoadModel, sgd_learner.cc:180-196) ---------------------------
     def save(self, prefix, rank, save_aux=False, it=-1):
         """this server's part, in SGDUpdater::Save's format (flush a pipeline first)"""
@@ -238,6 +304,29 @@ class TorchComm:
         out = [torch.empty_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t, group=self.cgroup)
         return [[int(o[self.rank]) for o in out]]
+
+    def exchange_counts2(self, send):
+        """send[0]: this rank's 2N ints [a_0 .. a_{N-1}, b_0 .. b_{N-1}] (a_g, b_g for peer g)
+        -> [[a from every peer .., b from every peer ..]] (one host round trip)"""
+        (s,) = send
+        N = self.world
+        pairs = [[int(s[g]), int(s[N + g])] for g in range(N)]
+        if self.nccl and N > 1:
+            with torch.cuda.stream(self.kstream):
+                t = torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(-1)
+                out = torch.empty(2 * N, dtype=torch.int64, device=self.device)
+                self.dist.all_to_all_single(out, t, group=self.kgroup)
+                o = out.cpu().tolist()
+        elif N > 1:
+            t = torch.tensor(pairs, dtype=torch.int64).reshape(-1)
+            outs = [torch.empty_like(t) for _ in range(N)]
+            self.dist.all_gather(outs, t, group=self.cgroup)
+            o = []
+            for g in range(N):
+                o += outs[g].tolist()[2 * self.rank:2 * self.rank + 2]
+        else:
+            o = pairs[0]
+        return [[o[2 * g] for g in range(N)] + [o[2 * g + 1] for g in range(N)]]
 
     def allgather_rows(self, tensors, M, row):
         """the north_star's all-gather: every rank's first rows (up to M rows of `row`
@@ -418,6 +507,11 @@ class LoopbackComm:
     def exchange_counts(self, send_splits):
         return [[send_splits[r][g] for r in range(self.world)] for g in range(self.world)]
 
+    def exchange_counts2(self, send):
+        N = self.world
+        return [[send[r][g] for r in range(N)] + [send[r][N + g] for r in range(N)]
+                for g in range(N)]
+
     def alltoallv(self, tensors, send_splits, recv_splits, row=1):
         offs = []
         for r in range(self.world):
@@ -580,6 +674,90 @@ def rsag_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index
     for i in range(n):
         shards[i].owner_push(rg[i][:own[i].numel() * S], 0)
     _initv(shards, comm, 0)
+
+
+def _split_initv(shards, comm, slot):
+    """InitV of the split owners' requests, ranked over all owners (a tiny device all-gather)"""
+    if shards[0].ctx.V_dim <= 0:
+        return
+    cnt = [sh.split_initv_local(slot) for sh in shards]
+    allc = comm.allgather_i64(cnt)
+    for sh, a, r in zip(shards, allc, comm.ranks()):
+        sh.split_initv_draw(a, r, slot)
+
+
+SPLIT_PHASES = ("partition", "xchg_keys", "owner_begin", "owner_forward", "xchg_parts",
+                "combine", "xchg_pxv", "owner_backward")
+
+
+def split_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index=MAX_INDEX,
+               preds=None, mark=None):
+    """One bulk-synchronous step of the owner-computes split (csrc/split.hip; oracle:
+    AggOracle.step, the single reference updater on the concatenated batch).  Every worker is
+    padded to M = the largest batch's rows with empty rows, so the row-sized collectives are
+    equal-size: the partials an all-to-all of M rows per owner, the [XV*p | p] rows an
+    all-gather.  mark(i): called after phase SPLIT_PHASES[i] is issued (and with -1 first)."""
+    mark = mark or (lambda i: None)
+    mark(-1)
+    n = len(shards)
+    N = shards[0].nranks
+    want_cnt = bool(push_cnt) and job_type == kTraining and shards[0].ctx.V_dim > 0
+    for i in range(n):
+        shards[i].split_partition(dblks[i], 0, max_index)
+    part = [sh.split_partition_wait(0) for sh in shards]
+    mark(0)
+    # keys per owner, every worker's row count and whether its rows carry values, in one host
+    # exchange (bit 40 of the row count: valued)
+    send = [p[3] + [p[4] | ((p[1] is not None) << 40)] * N for p in part]
+    both = comm.exchange_counts2(send)
+    recv = [b[:N] for b in both]
+    M = max(max(int(v) & ((1 << 40) - 1) for v in b[N:]) for b in both)
+    M = max(M, 1)
+    valued = any(int(v) >> 40 for v in both[0][N:])
+    rkeys = comm.alltoallv([p[0] for p in part], [p[3] for p in part], recv)
+    if valued:  # binary workers send 1s beside a valued worker
+        xs = [p[1] if p[1] is not None else
+              torch.ones(max(p[0].numel(), 1), dtype=torch.float32, device=p[0].device)
+              for p in part]
+        rx = comm.alltoallv(xs, [p[3] for p in part], recv)
+    else:
+        rx = [None] * n
+    # nnz per (owner, row), padded to M rows per owner
+    rcs = []
+    for p in part:
+        rc, B = p[2], p[4]
+        if B < M:
+            pad = torch.zeros(N * M, dtype=torch.int32, device=rc.device)
+            pad.view(N, M)[:, :B] = rc.view(N, B)
+            rc = pad
+        rcs.append(rc)
+    rrc = comm.alltoallv(rcs, [[M] * N] * n, [[M] * N] * n)
+    mark(1)
+    for i in range(n):
+        shards[i].split_owner_begin(rkeys[i], rx[i], rrc[i], [M] * N, recv[i], job_type,
+                                    want_cnt, 0)
+    if want_cnt:
+        _split_initv(shards, comm, 0)
+    mark(2)
+    PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h)
+    parts = [sh.split_owner_forward(0) for sh in shards]
+    mark(3)
+    rparts = comm.alltoallv(parts, [[M] * N] * n, [[M] * N] * n, PS)
+    mark(4)
+    pxv = [shards[i].split_combine(dblks[i], rparts[i], M, 0, preds[i] if preds else None)
+           for i in range(n)]
+    mark(5)
+    if job_type == kTraining:
+        PX = _lib.lib().dfx_split_pxv_floats(shards[0].ctx.h)
+        allp = comm.allgather_rows(pxv, M, PX)
+        mark(6)
+        for i in range(n):
+            shards[i].split_owner_backward(allp[i], 0)
+        _split_initv(shards, comm, 0)
+    else:
+        mark(6)
+    mark(7)
+    return [sum(r) for r in recv]  # keys received per owner (for accounting)
 
 
 class ShardedPipeline:

@@ -286,6 +286,55 @@ int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos
                         const int64_t* bounds, int nranks, int64_t M, int width, int to_union,
                         const float* src, float* dst);
 
+/* ---- owner-computes split of FM over the key-range shards (difacto_amd/csrc/split.hip) -----
+ * SURVEY §8(e)'s synchronous step (push_agg=sum: one reference step on the concatenation of the
+ * workers' batches, sgd_learner.cc:201-317), with the forward and backward run by the owners of
+ * the keys, so only per-row quantities cross the links.  Per step, every rank:
+ *   dfx_split_partition      worker: each nnz's key (ReverseBytes(id % max_index), the
+ *                            Localizer's) grouped by owner floor(key * N / 2^64), row order kept:
+ *                            keys_out[nnz], x_out[nnz] their values (required for valued data;
+ *                            binary data given x_out gets 1s), row_cnt_out[N][B]
+ *                            nnz per (owner, row); asynchronous on the context stream
+ *   dfx_split_partition_wait host join: split_counts[nranks] keys per owner
+ *   -> alltoallv keys (+ values) and row counts (B per owner) to the owners; a driver may pad
+ *      every worker to the same row count M with empty rows (equal-size collectives)
+ *   dfx_split_owner_begin    owner: the received keys / values / row counts, concatenated in
+ *                            rank order (rows_per_rank / keys_per_rank: host, per source rank;
+ *                            row_cnt is scanned in place); Localizer::Compact of them; push_cnt:
+ *                            Update(kFeaCount) of every key, InitV requests pending; a job
+ *                            other than training inserts every key (Get's model_[key])
+ *   dfx_split_owner_forward  owner: part_out[R][dfx_split_part_floats()] per received row
+ *                            [XV(d) | XXVV(d) | sum w x | 0 0 0] over this owner's keys
+ *   -> alltoallv partials back to the workers (rank-major: owner o's rows at o * part_rows)
+ *   dfx_split_combine        worker: pred / p / logloss / AUC of its rows from the owners'
+ *                            partials (summed in rank order), progress on the device,
+ *                            pxv_out[B][dfx_split_pxv_floats()] rows [XV*p (d) | p | 0 0 0],
+ *                            pred_out optional
+ *   -> every owner receives every worker's pxv rows, in rank order
+ *   dfx_split_owner_backward owner: CalcGrad of its keys over the received rows + one Update per
+ *                            key (FTRL / AdaGrad); InitV requests pending
+ *   after a count push and after every backward (V_dim > 0): dfx_split_initv_local (this owner's
+ *   request count -> count_dev, a device int64), the caller all-gathers the counts in rank order
+ *   (device int64[nranks]) and dfx_split_initv_draw draws this owner's keys after the lower
+ *   owners', so the rand_r stream is the single updater's.  Owner calls run on the context
+ *   stream in call order.  Arrays are device pointers unless noted. */
+int dfx_split_part_floats(dfx_ctx* ctx);
+int dfx_split_pxv_floats(dfx_ctx* ctx);
+int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* batch, uint64_t max_index,
+                        int nranks, uint64_t* keys_out, float* x_out, uint32_t* row_cnt_out);
+int dfx_split_partition_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_counts);
+int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const float* x,
+                          uint32_t* row_cnt, const int64_t* rows_per_rank,
+                          const int64_t* keys_per_rank, int nranks, int job_type,
+                          int push_cnt);
+int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out);
+int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* parts,
+                      int64_t part_rows, int nranks, float* pxv_out, float* pred_out);
+int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv);
+int dfx_split_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev);
+int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
+                         int nranks);
+
 #ifdef __cplusplus
 }
 #endif
