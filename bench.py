@@ -53,6 +53,13 @@ def parse():
                          "summed gradients (SURVEY §8(e): a step is one reference step over "
                          "the concatenated batches); ranks = one Update per pushing worker "
                          "(KVStoreDist HandlePush)")
+    ap.add_argument("--collective", default="split", choices=("split", "a2a"),
+                    help="sharded store schedule: split = owner-computes FM (owners run the "
+                         "forward partials and the backward on their keys; per-row partials "
+                         "all-to-all + [XV*p | p] all-gather, bulk synchronous); a2a = model "
+                         "records / gradients all-to-all-v (pipelined unless --sync).  The "
+                         "other schedules, and the north_star's literal union all-gather / "
+                         "reduce-scatter (rsag), are measured beside it on short runs")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="sharded store transport; gloo (staged through host memory) runs "
                          "several ranks on one GPU, for tests")
@@ -386,12 +393,19 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         shard.localize_wait = lw_probe
         for nm in ("exchange_counts", "alltoallv_async", "alltoallv_keys_async"):
             timed(comm, nm)
-    pipe = None if args.sync else DI.ShardedPipeline([shard], comm)
+    split = args.collective == "split"
+    if args.sync:
+        pipe = None
+    elif split:
+        pipe = DI.SplitPipeline([shard], comm)
+    else:
+        pipe = DI.ShardedPipeline([shard], comm)
     live = []  # a batch stays alive until the submit after the one that took it
+    sync_fn = DI.split_step if split else DI.sharded_step
 
     def step(batch, push_cnt, mark=None):
         if pipe is None:
-            DI.sharded_step([shard], [batch], comm, H.kTraining, push_cnt=push_cnt, mark=mark)
+            sync_fn([shard], [batch], comm, H.kTraining, push_cnt=push_cnt, mark=mark)
         else:
             pipe.submit([batch], H.kTraining, push_cnt=push_cnt, mark=mark)
             live.append(batch)
@@ -411,11 +425,12 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     # per-phase events on the stream everything is ordered on (torch's current stream: the
     # library's kernels and the wait on each RCCL collective).  In the pipelined schedule
     # the phases of neighbouring steps overlap; the marks are in issue order.
-    nph = len(DI.PHASES)
+    nph = len(DI.SPLIT_PHASES if split else DI.PHASES)
     # Timing events add latency to the step, so the timed steps record only the two marks
-    # around the worker's forward+backward (the roofline's launch time); the per-phase
-    # breakdown comes from an untimed diagnostic pass over the same batches afterwards.
-    FB = (4, 5)  # marks bracketing fwd_bwd (sync) / xchg_pull+fwd_bwd (pipelined)
+    # around the roofline's kernels (split: the owner's backward + its InitV; a2a: the worker's
+    # forward+backward); the per-phase breakdown comes from an untimed diagnostic pass over the
+    # same batches afterwards.
+    FB = ((6, 7) if pipe is None else (3, 4)) if split else (4, 5)
 
     def run_steps(js):
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nph + 1)]
@@ -466,7 +481,10 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     # diagnostic pass (untimed): every phase
     evs = run_steps(range(-1, nph))
     torch.cuda.synchronize()
-    names = DI.PHASES if pipe is None else DI.PIPE_PHASES
+    if split:
+        names = DI.SPLIT_PHASES if pipe is None else DI.SPLIT_PIPE_PHASES
+    else:
+        names = DI.PHASES if pipe is None else DI.PIPE_PHASES
     ph = {p: sum(evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)) / args.steps
           for j, p in enumerate(names)}
     H.progress(ctx)
@@ -476,9 +494,14 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     colls = {}
     if pipe is not None:
         pipe.flush()
+    if split:  # the owner's share of the last step, for the roofline's bytes
+        o_rows, o_nnz, o_uniq = shard.split_owner_stats(0)
     nb = min(args.steps, 20)
-    for cname, fn in (("a2a_sync", DI.sharded_step), ("rsag_sync", DI.rsag_step)):
-        if cname == "rsag_sync" and args.push_agg != "sum":
+    main_name = (("split_sync" if args.sync else "split_pipelined") if split else
+                 ("a2a_sync" if args.sync else "a2a_pipelined"))
+    for cname, fn in (("split_sync", DI.split_step), ("a2a_sync", DI.sharded_step),
+                      ("rsag_sync", DI.rsag_step)):
+        if cname == main_name or (cname != "a2a_sync" and args.push_agg != "sum"):
             continue
         for bt in batches[:2]:
             fn([shard], [bt], comm, H.kTraining)
@@ -500,8 +523,22 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     st = H.Store(ctx).stats()
     tot = comm.allreduce_sum([[prog["loss"], prog["auc"], prog["nrows"], float(st["n_keys"]),
                                float(st["n_vrows"]), float(max(shard._U))]])[0]
-    # roofline of the worker's forward+backward launch pair on this rank
-    ab = algorithmic_bytes_sharded(B, B * k, max(shard._U), d)
+    if split:
+        # roofline of the owner's fused backward + update on this rank (the fused step's
+        # backward formula over the owner's rows, keys and unique keys)
+        ab = algorithmic_bytes(o_rows, o_nnz, o_uniq, d)["backward_update"]
+        rkernel = "owner_backward (split: fused backward + FTRL/AdaGrad + InitV, rank 0)"
+        traffic, tsrc = pmc_traffic("k_fm_bwd"), ("profiles/r1/pmc_hbm.json (the fused "
+                                                  "backward's FETCH_SIZE + WRITE_SIZE per "
+                                                  "launch, the same kernel)")
+    else:
+        # roofline of the worker's forward+backward launch pair on this rank
+        ab = algorithmic_bytes_sharded(B, B * k, max(shard._U), d)
+        rkernel = "fwd_bwd (dist forward+AUC+backward, rank 0)"
+        traffic, tsrc = sharded_traffic(), ("profiles/r1/pmc_hbm_sharded.json (rocprofv3 "
+                                            "FETCH_SIZE + WRITE_SIZE per launch of the "
+                                            "worker's forward and backward, N = 1 sharded "
+                                            "bench)")
     achieved = ab / (fb_ms * 1e-3) / 1e9
     value = world * B * args.steps / elapsed
     out = {
@@ -518,23 +555,28 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         "dtype": "f32",
         "data": "synthetic (device-generated, resident in HBM before timing)",
         "config": {"workload": "C3 Criteo-shaped FM V_dim=%d, %d binary nnz/row, 2^%d keys, "
-                               "l1=0 V_threshold=0, key-range-sharded store over %d GPUs "
-                               "(RCCL all-to-all-v), %s schedule, push_agg=%s"
+                               "l1=0 V_threshold=0, key-range-sharded store over %d GPUs, %s, "
+                               "push_agg=%s"
                                % (d, k, kb, world,
-                                  "bulk-synchronous" if args.sync else "pipelined 1-step-stale",
+                                  "owner-computes split (RCCL all-to-all of per-row partials "
+                                  "+ all-gather of [XV*p | p] rows), bulk-synchronous%s"
+                                  % ("" if args.sync else " results, next step's partition / "
+                                     "key exchange / owner Localizer on the Localizer lane")
+                                  if split else
+                                  "RCCL all-to-all-v of records / gradients, %s schedule"
+                                  % ("bulk-synchronous" if args.sync
+                                     else "pipelined 1-step-stale"),
                                   args.push_agg),
                    "rows_per_gpu_step": B, "global_batch": B * world,
                    "parallelism": "dp%d + model sharded by key range" % world},
-        "roofline": {"bound": "hbm", "kernel": "fwd_bwd (dist forward+AUC+backward, rank 0)",
+        "roofline": {"bound": "hbm", "kernel": rkernel,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": sharded_traffic(),
-                     "traffic_source": "profiles/r1/pmc_hbm_sharded.json (rocprofv3 "
-                                       "FETCH_SIZE + WRITE_SIZE per launch of the worker's "
-                                       "forward and backward, N = 1 sharded bench)",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": tsrc,
                      "algorithmic_bytes_per_launch": int(ab),
                      "launch_ms": round(fb_ms, 4)},
         "phases_ms_per_step_rank0": {p: round(v, 4) for p, v in ph.items()},
-        "collectives": dict({("a2a_sync" if args.sync else "a2a_pipelined"):
+        "collectives": dict({main_name:
                              {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
                               "value": round(value, 1), "steps": args.steps}}, **colls),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),

@@ -110,11 +110,15 @@ _SIGS = {
                                            ctypes.c_int, vp, vp, vp]),
     "dfx_split_partition_wait": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i64p]),
     "dfx_split_owner_begin": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64p, i64p,
-                                             ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int]),
+    "dfx_ctx_lane_stream": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
+    "dfx_ctx_set_lane_stream": (ctypes.c_int, [vp, ctypes.c_int, vp]),
     "dfx_split_owner_forward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
     "dfx_split_combine": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp, c_i64,
                                          ctypes.c_int, vp, vp]),
     "dfx_split_owner_backward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_split_owner_stats": (ctypes.c_int, [vp, ctypes.c_int, i64p, i64p, i64p]),
     "dfx_split_initv_local": (ctypes.c_int, [vp, ctypes.c_int, vp]),
     "dfx_split_initv_draw": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int]),
 }

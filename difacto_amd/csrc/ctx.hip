@@ -159,9 +159,10 @@ int pipeline_init(Context* c) {
   int lo = 0, hi = 0;
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, hi));
+  c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
-                        &c->ev_free[0], &c->ev_free[1]})
+                        &c->ev_free[0], &c->ev_free[1], &c->ev_part[0], &c->ev_part[1]})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads, &c->ods[0], &c->ods[1]}) {
     DFX_HIP(hipMalloc(d, sizeof(DevState)));
@@ -254,11 +255,12 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   for (auto h : c->dist_host)
     if (h) (void)hipHostFree(h);
   for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_loc[0], c->ev_loc[1],
-                       c->ev_free[0], c->ev_free[1]})
+                       c->ev_free[0], c->ev_free[1], c->ev_part[0], c->ev_part[1]})
     if (e) (void)hipEventDestroy(e);
   for (DevState* d : {c->bds[0], c->bds[1], c->ads, c->ods[0], c->ods[1]})
     if (d) (void)hipFree(d);
-  if (c->loc_stream) (void)hipStreamDestroy(c->loc_stream);
+  if (c->loc_stream) (void)hipStreamSynchronize(c->loc_stream);
+  if (c->own_loc_stream) (void)hipStreamDestroy(c->own_loc_stream);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
@@ -282,6 +284,24 @@ int dfx_ctx_set_input_stream(dfx_ctx* ctx, void* hip_stream) {
   DFX_CHECK_ARG(ctx, "null ctx");
   ctx->c.in_stream = static_cast<hipStream_t>(hip_stream);
   ctx->c.has_in_stream = hip_stream != nullptr;
+  return DFX_OK;
+}
+
+int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out) {
+  DFX_CHECK_ARG(ctx && out, "null argument");
+  DFX_CHECK_ARG(which == 0 || which == 1, "dfx_ctx_lane_stream: 0 (Localizer) or 1 (AUC)");
+  DFX_TRY(pipeline_init(&ctx->c));
+  *out = which == 0 ? ctx->c.loc_stream : ctx->c.aux_stream;
+  return DFX_OK;
+}
+
+int dfx_ctx_set_lane_stream(dfx_ctx* ctx, int which, void* hip_stream) {
+  DFX_CHECK_ARG(ctx, "null ctx");
+  DFX_CHECK_ARG(which == 0, "dfx_ctx_set_lane_stream: only the Localizer lane (0)");
+  Context* c = &ctx->c;
+  DFX_TRY(pipeline_init(c));
+  DFX_HIP(hipStreamSynchronize(c->loc_stream));  // work queued on the previous lane is done
+  c->loc_stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->own_loc_stream;
   return DFX_OK;
 }
 

@@ -166,6 +166,7 @@ struct Context {
   // fused-step pipelining (step.hip): batch t+1's Localizer runs on loc_stream while the main
   // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
   hipStream_t loc_stream = nullptr, aux_stream = nullptr;
+  hipStream_t own_loc_stream = nullptr;  // the library's own Localizer lane (destroyed by it)
   hipStream_t in_stream = nullptr;  // where batches are produced (dfx_ctx_set_input_stream)
   bool has_in_stream = false;
   Workspace bws[2];
@@ -206,6 +207,10 @@ struct Context {
   bool split_resolved[2] = {false, false};
   bool split_initv_pending[2] = {false, false};
   bool split_initv_gated[2] = {false, false};  // the requests came from the backward (n_init)
+  // the slot's owner_begin ran on the Localizer lane (the forward waits for ev_loc[slot]);
+  // ev_part[slot]: the slot's partition is done (host join)
+  bool split_lane[2] = {false, false};
+  hipEvent_t ev_part[2] = {nullptr, nullptr};
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }

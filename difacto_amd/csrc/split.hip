@@ -258,22 +258,27 @@ int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* b, uint64_t max
   DFX_TRY(bw.hist.ensure((size_t)(nblk * nranks + 1) * 4));
   uint32_t* blk = bw.hist.as<uint32_t>();
   uint32_t* total = &c->bds[slot]->totals[0];
-  const Lane L{c->stream, &bw, c->bds[slot], &c->ds->err};
+  // on the Localizer lane, after the batch's producer: it reads only the batch, so it runs
+  // beside the previous step's forward / backward
+  hipStream_t st = c->loc_stream;
+  DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
+  DFX_HIP(hipStreamWaitEvent(st, c->ev_in, 0));
+  const Lane L{st, &bw, c->bds[slot], &c->ds->err};
   if (nblk > 0) {
-    hipLaunchKernelGGL(k_split_count, dim3((unsigned)nblk), dim3(kSpNT), 0, c->stream, B,
-                       b->offset, b->index, max_index, (uint32_t)nranks, row_cnt_out, blk, nblk);
+    hipLaunchKernelGGL(k_split_count, dim3((unsigned)nblk), dim3(kSpNT), 0, st, B, b->offset,
+                       b->index, max_index, (uint32_t)nranks, row_cnt_out, blk, nblk);
   }
   DFX_TRY(scan_u32(L, blk, nblk * nranks, total));
   if (nblk > 0) {
-    hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)nblk), dim3(kSpNT), 0, c->stream, B,
-                       b->offset, b->index, b->value, max_index, (uint32_t)nranks, blk, nblk,
-                       keys_out, x_out);
-    hipLaunchKernelGGL(k_split_totals, dim3(1), dim3(kMaxDistRanks), 0, c->stream, blk, total,
-                       nblk, (uint32_t)nranks, c->dist_host[slot]);
+    hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)nblk), dim3(kSpNT), 0, st, B, b->offset,
+                       b->index, b->value, max_index, (uint32_t)nranks, blk, nblk, keys_out,
+                       x_out);
+    hipLaunchKernelGGL(k_split_totals, dim3(1), dim3(kMaxDistRanks), 0, st, blk, total, nblk,
+                       (uint32_t)nranks, c->dist_host[slot]);
   } else {
     for (int o = 0; o < nranks; ++o) c->dist_host[slot][o] = 0;
   }
-  DFX_HIP(hipEventRecord(c->ev_loc[slot], c->stream));
+  DFX_HIP(hipEventRecord(c->ev_part[slot], st));
   DFX_HIP(hipGetLastError());
   c->split_B[slot] = B;
   c->split_nblk[slot] = nblk;
@@ -286,7 +291,7 @@ int dfx_split_partition_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_CHECK_ARG(c->loc_stream, "split_partition_wait: no dfx_split_partition issued");
-  DFX_HIP(hipEventSynchronize(c->ev_loc[slot]));
+  DFX_HIP(hipEventSynchronize(c->ev_part[slot]));
   for (int o = 0; o < nranks; ++o) split_counts[o] = (int64_t)c->dist_host[slot][o];
   return DFX_OK;
 }
@@ -294,7 +299,7 @@ int dfx_split_partition_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_
 int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const float* x,
                           uint32_t* row_cnt, const int64_t* rows_per_rank,
                           const int64_t* keys_per_rank, int nranks, int job_type,
-                          int push_cnt) {
+                          int push_cnt, int lane) {
   DFX_CHECK_ARG(ctx && rows_per_rank && keys_per_rank, "null argument");
   DFX_SPLIT_SLOT(slot);
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
@@ -312,12 +317,27 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   DFX_CHECK_ARG(R == 0 || row_cnt, "split_owner_begin: null row counts");
   DFX_CHECK_ARG(nnz == 0 || keys, "split_owner_begin: null keys");
   DFX_CHECK_ARG(nnz < 0xFFFFFFFFll && R < 0x7FFFFFFFll, "split_owner_begin: too many keys");
+  DFX_CHECK_ARG(job_type == DFX_JOB_TRAINING || job_type == DFX_JOB_VALIDATION ||
+                    job_type == DFX_JOB_PREDICTION,
+                "split_owner_begin: bad job type");
+  const bool cnt = push_cnt && job_type == DFX_JOB_TRAINING && c->P.V_dim > 0 && nnz > 0;
+  const bool get = !cnt && job_type != DFX_JOB_TRAINING && nnz > 0;
+  DFX_CHECK_ARG(!lane || (!cnt && !get),
+                "split_owner_begin: a step that touches the table (count push, Get) runs on "
+                "the context stream (lane = 0)");
   // this step inserts at most nnz keys and draws at most nnz V rows (slots are not carried
   // across steps here, so the store may grow at this point)
   DFX_TRY(cap_check(c, nnz));
   // a server of one of nranks key ranges: hash keys by their position inside the range
   DFX_TRY(table_set_ranges(c, nranks));
-  const Lane OL = split_owner_lane(c, slot);
+  Lane OL = split_owner_lane(c, slot);
+  if (lane) {
+    // the Localizer lane: the received keys are ready on the caller's current stream (the
+    // library's lane, which the caller made wait for the exchange); the slot's buffers are free
+    // once the main stream finished the step that used them before
+    OL.stream = c->loc_stream;
+    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[slot], 0));
+  }
   Workspace& ows = c->ows[slot];
   DFX_TRY(loc_reserve(ows, nnz));
   DFX_TRY(ows.rowid.ensure((size_t)(R + 1) * 8));
@@ -343,11 +363,7 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   c->split_keys[slot] = keys;
   c->split_x[slot] = x;
   c->split_resolved[slot] = false;
-  DFX_CHECK_ARG(job_type == DFX_JOB_TRAINING || job_type == DFX_JOB_VALIDATION ||
-                    job_type == DFX_JOB_PREDICTION,
-                "split_owner_begin: bad job type");
-  const bool cnt = push_cnt && job_type == DFX_JOB_TRAINING && c->P.V_dim > 0 && nnz > 0;
-  if (!cnt && job_type != DFX_JOB_TRAINING && nnz > 0) {
+  if (get) {
     // a step without a backward: SGDUpdater::Get still inserts every key (model_[key],
     // sgd_updater.cc:34-58), as the fused step's probe does
     DFX_TRY(probe_keys_run(c, OL, nnz, o.uniq, ows.slot.as<uint32_t>()));
@@ -363,6 +379,8 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
     c->split_initv_pending[slot] = true;
     c->split_initv_gated[slot] = false;
   }
+  c->split_lane[slot] = lane != 0;
+  if (lane) DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -374,6 +392,7 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   DFX_CHECK_ARG(!c->split_initv_pending[slot],
                 "split_owner_forward: the count push's InitV is pending (dfx_split_initv_*)");
   const int64_t R = c->split_rows[slot];
+  if (c->split_lane[slot]) DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_loc[slot], 0));
   if (R == 0) return DFX_OK;
   DFX_CHECK_ARG(part_out, "split_owner_forward: null buffer");
   Workspace& ows = c->ows[slot];
@@ -384,6 +403,8 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   a.part = part_out;
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+  // a step without a backward is done with the slot here
+  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -455,7 +476,25 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     c->split_initv_pending[slot] = true;
     c->split_initv_gated[slot] = true;
   }
+  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
   DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int dfx_split_owner_stats(dfx_ctx* ctx, int slot, int64_t* rows, int64_t* nnz,
+                          int64_t* n_uniq) {
+  DFX_CHECK_ARG(ctx && rows && nnz && n_uniq, "null argument");
+  DFX_SPLIT_SLOT(slot);
+  Context* c = &ctx->c;
+  *rows = c->split_rows[slot];
+  *nnz = c->split_nnz[slot];
+  unsigned u = 0;
+  if (c->ods[slot]) {
+    DFX_HIP(hipMemcpyAsync(&u, &c->ods[slot]->u_count, sizeof(u), hipMemcpyDeviceToHost,
+                           c->stream));
+    DFX_HIP(hipStreamSynchronize(c->stream));
+  }
+  *n_uniq = u;
   return DFX_OK;
 }
 
@@ -490,6 +529,7 @@ int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, 
                           c->ows[slot].slot.as<uint32_t>(), counts_all_dev, rank, nranks,
                           &c->ds->n_init));
   c->split_initv_pending[slot] = false;
+  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));  // the slot's last reader
   return DFX_OK;
 }
 

@@ -185,14 +185,14 @@ class Shard:
         return keys, x, rc[:self.nranks * B], list(splits), B
 
     def split_owner_begin(self, keys, x, row_cnt, rows_per_rank, keys_per_rank, job_type,
-                          push_cnt, slot=0):
+                          push_cnt, slot=0, lane=False):
         """row_cnt: the received per-row counts (scanned in place)"""
         rows = (ctypes.c_int64 * self.nranks)(*[int(v) for v in rows_per_rank])
         kpr = (ctypes.c_int64 * self.nranks)(*[int(v) for v in keys_per_rank])
         self._split_R[slot] = sum(int(v) for v in rows_per_rank)
         check(_lib.lib().dfx_split_owner_begin(self.ctx.h, slot, _p(keys), _p(x), _p(row_cnt),
                                                rows, kpr, self.nranks, int(job_type),
-                                               int(bool(push_cnt))))
+                                               int(bool(push_cnt)), int(bool(lane))))
 
     def split_owner_forward(self, slot=0):
         R = self._split_R[slot]
@@ -214,6 +214,13 @@ class Shard:
 
     def split_owner_backward(self, pxv, slot=0):
         check(_lib.lib().dfx_split_owner_backward(self.ctx.h, slot, _p(pxv)))
+
+    def split_owner_stats(self, slot=0):
+        """-> (rows, keys, unique keys) of the owner's last begin"""
+        r, k, u = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        check(_lib.lib().dfx_split_owner_stats(self.ctx.h, slot, ctypes.byref(r),
+                                               ctypes.byref(k), ctypes.byref(u)))
+        return r.value, k.value, u.value
 
     def split_initv_local(self, slot=0):
         out = torch.empty(1, dtype=torch.int64, device=self.ctx.device)
@@ -758,6 +765,126 @@ def split_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_inde
         mark(6)
     mark(7)
     return [sum(r) for r in recv]  # keys received per owner (for accounting)
+
+
+# SplitPipeline's main-stream marks (the next step's begin runs on the lanes)
+SPLIT_PIPE_PHASES = ("owner_forward", "xchg_parts", "combine", "xchg_pxv", "owner_backward",
+                     "initv", "end", "end2")
+
+
+class SplitPipeline:
+    """The owner-computes split (split_step's results exactly: every forward reads the model
+    after the previous step's update) with the fused step's overlap: submit(batch t+1) issues
+    batch t+1's partition on the Localizer lanes, then step t's forward, partial exchange,
+    combine, record all-gather and backward on the context stream, then batch t+1's key
+    exchange and owner Localizer (owner_begin, lane = 1) on the lanes, which run beside step
+    t's main-stream work.  A count push (epoch 0) or a step without a backward touches the
+    table in owner_begin, so that begin runs on the context stream after step t's update.
+    flush() runs the last step.  A batch must stay alive until the submit after the one that
+    took it (or flush())."""
+
+    def __init__(self, shards, comm, max_index=MAX_INDEX):
+        self.shards, self.comm, self.max_index = shards, comm, max_index
+        self.slot = 0
+        self.pending = None
+        # the contexts' Localizer lanes become torch streams (high priority, like the
+        # library's own): torch's allocator tracks the exchange buffers used on them, and the
+        # streams outlive the contexts
+        self.lanes = []
+        for sh in shards:
+            ln = torch.cuda.Stream(device=sh.ctx.device, priority=-1)
+            check(_lib.lib().dfx_ctx_set_lane_stream(sh.ctx.h, 0, ctypes.c_void_p(ln.cuda_stream)))
+            self.lanes.append(ln)
+
+    def submit(self, dblks, job_type=kTraining, push_cnt=False, preds=None, mark=None):
+        s = self.slot
+        self.slot ^= 1
+        want_cnt = bool(push_cnt) and job_type == kTraining and self.shards[0].ctx.V_dim > 0
+        for i, sh in enumerate(self.shards):
+            sh.split_partition(dblks[i], s, self.max_index)
+        if self.pending is not None:
+            self._main(self.pending, mark)
+        self.pending = self._begin(s, dblks, job_type, want_cnt, preds)
+
+    def flush(self, mark=None):
+        if self.pending is not None:
+            self._main(self.pending, mark)
+            self.pending = None
+
+    def _begin(self, s, dblks, job_type, want_cnt, preds):
+        shards, comm = self.shards, self.comm
+        n, N = len(shards), shards[0].nranks
+        part = [sh.split_partition_wait(s) for sh in shards]
+        send = [p[3] + [p[4] | ((p[1] is not None) << 40)] * N for p in part]
+        both = comm.exchange_counts2(send)
+        recv = [b[:N] for b in both]
+        M = max(1, max(max(int(v) & ((1 << 40) - 1) for v in b[N:]) for b in both))
+        valued = any(int(v) >> 40 for v in both[0][N:])
+        lane = not want_cnt and job_type == kTraining
+        main = torch.cuda.current_stream()
+        # the exchanges feed the owners' Localizer: issue them (and wait for them) on the lane
+        with torch.cuda.stream(self.lanes[0] if lane else main):
+            rcs = []
+            for p in part:
+                rc, B = p[2], p[4]
+                if B < M:
+                    pad = torch.zeros(N * M, dtype=torch.int32, device=rc.device)
+                    pad.view(N, M)[:, :B] = rc.view(N, B)
+                    rc = pad
+                rcs.append(rc)
+            hk = comm.alltoallv_keys_async([p[0] for p in part], [p[3] for p in part], recv)
+            hr = comm.alltoallv_keys_async(rcs, [[M] * N] * n, [[M] * N] * n)
+            if valued:
+                xs = [p[1] if p[1] is not None else
+                      torch.ones(max(p[0].numel(), 1), dtype=torch.float32, device=p[0].device)
+                      for p in part]
+                hx = comm.alltoallv_keys_async(xs, [p[3] for p in part], recv)
+            rkeys, rrc = hk.wait(), hr.wait()
+            rx = hx.wait() if valued else [None] * n
+            if lane and n > 1:  # loopback: every lane waits for the exchange on lane 0
+                ev = torch.cuda.Event()
+                ev.record()
+                for ln in self.lanes[1:]:
+                    ln.wait_event(ev)
+        for i in range(n):
+            # the forward reads the received keys / values on the context stream later
+            for t in (rkeys[i], rx[i]):
+                if t is not None and t.device.type == "cuda":
+                    t.record_stream(main)
+            shards[i].split_owner_begin(rkeys[i], rx[i], rrc[i], [M] * N, recv[i], job_type,
+                                        want_cnt, s, lane)
+        if want_cnt:
+            _split_initv(shards, comm, s)
+        return (s, dblks, job_type, preds, M, rkeys, rx, part)
+
+    def _main(self, q, mark):
+        mark = mark or (lambda i: None)
+        s, dblks, job_type, preds, M, _, _, _ = q
+        shards, comm = self.shards, self.comm
+        n, N = len(shards), shards[0].nranks
+        mark(-1)
+        PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h)
+        parts = [sh.split_owner_forward(s) for sh in shards]
+        mark(0)
+        rparts = comm.alltoallv(parts, [[M] * N] * n, [[M] * N] * n, PS)
+        mark(1)
+        pxv = [shards[i].split_combine(dblks[i], rparts[i], M, s, preds[i] if preds else None)
+               for i in range(n)]
+        mark(2)
+        if job_type == kTraining:
+            PX = _lib.lib().dfx_split_pxv_floats(shards[0].ctx.h)
+            allp = comm.allgather_rows(pxv, M, PX)
+            mark(3)
+            for i in range(n):
+                shards[i].split_owner_backward(allp[i], s)
+            mark(4)
+            _split_initv(shards, comm, s)
+        else:
+            mark(3)
+            mark(4)
+        mark(5)
+        mark(6)
+        mark(7)
 
 
 class ShardedPipeline:

@@ -88,6 +88,12 @@ int dfx_ctx_destroy(dfx_ctx* ctx);
  * hipStream_t (NULL = the null stream, torch's default); use_own_stream switches back. */
 int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream);
 int dfx_ctx_use_own_stream(dfx_ctx* ctx);
+/* the context's side lanes (hipStream_t): which = 0 the Localizer lane, 1 the AUC lane */
+int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out);
+/* run the Localizer lane (which = 0) on the caller's stream (it must outlive the context's use
+ * of it; NULL: back to the library's own lane), e.g. a stream of the caller's framework, whose
+ * allocator then tracks buffers used on it */
+int dfx_ctx_set_lane_stream(dfx_ctx* ctx, int which, void* hip_stream);
 /* The stream on which dfx_train_step's batches are produced (a loader / copy stream; NULL =
  * the context stream).  A batch's Localizer waits only for that stream, so it can run while
  * the context stream is still on the previous batch's forward / backward.  The caller keeps a
@@ -302,7 +308,14 @@ int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos
  *                            rank order (rows_per_rank / keys_per_rank: host, per source rank;
  *                            row_cnt is scanned in place); Localizer::Compact of them; push_cnt:
  *                            Update(kFeaCount) of every key, InitV requests pending; a job
- *                            other than training inserts every key (Get's model_[key])
+ *                            other than training inserts every key (Get's model_[key]).
+ *                            lane = 1 (a training step without count push): on the Localizer
+ *                            lane (dfx_ctx_lane_stream 0), whose queue the caller made wait for
+ *                            the received arrays; it waits for the slot's previous step and
+ *                            owner_forward waits for it, so it runs beside the previous step's
+ *                            owner_forward / owner_backward on the context stream
+ * dfx_split_partition also runs on the Localizer lane, after the batch's producer (the input
+ * stream, dfx_ctx_set_input_stream, else the context stream).
  *   dfx_split_owner_forward  owner: part_out[R][dfx_split_part_floats()] per received row
  *                            [XV(d) | XXVV(d) | sum w x | 0 0 0] over this owner's keys
  *   -> alltoallv partials back to the workers (rank-major: owner o's rows at o * part_rows)
@@ -326,11 +339,14 @@ int dfx_split_partition_wait(dfx_ctx* ctx, int slot, int nranks, int64_t* split_
 int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const float* x,
                           uint32_t* row_cnt, const int64_t* rows_per_rank,
                           const int64_t* keys_per_rank, int nranks, int job_type,
-                          int push_cnt);
+                          int push_cnt, int lane);
 int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out);
 int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* parts,
                       int64_t part_rows, int nranks, float* pxv_out, float* pred_out);
 int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv);
+/* the owner's last begin: received rows, keys and unique keys (synchronises the stream) */
+int dfx_split_owner_stats(dfx_ctx* ctx, int slot, int64_t* rows, int64_t* nnz,
+                          int64_t* n_uniq);
 int dfx_split_initv_local(dfx_ctx* ctx, int slot, int64_t* count_dev);
 int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, int rank,
                          int nranks);

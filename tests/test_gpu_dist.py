@@ -439,8 +439,9 @@ def test_sharded_two_processes_one_gpu(pipelined):
         assert st["new_w"] == so.up[r].new_w
 
 
-@pytest.mark.parametrize("sync", [False, True])
-def test_bench_two_ranks_gloo(sync):
+@pytest.mark.parametrize("collective,sync", [("split", False), ("split", True), ("a2a", False),
+                                             ("a2a", True)])
+def test_bench_two_ranks_gloo(collective, sync):
     """bench.py's multi-GPU path end to end under torchrun with 2 ranks (the driver's SCALE
     command, with the exchange staged through host memory over gloo since both ranks share
     the test box's GPU): one JSON line from rank 0, whole-job throughput over both ranks"""
@@ -457,7 +458,8 @@ def test_bench_two_ranks_gloo(sync):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--batch", "20000", "--key-bits", "20",
-           "--backend", "gloo", "--no-cpu-baseline"] + (["--sync"] if sync else [])
+           "--backend", "gloo", "--no-cpu-baseline", "--collective", collective] + (
+               ["--sync"] if sync else [])
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -466,7 +468,13 @@ def test_bench_two_ranks_gloo(sync):
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["value"] > 0
     assert out["config"]["global_batch"] == 40000
     assert 0.3 < out["train_loss_per_row"] < 0.8 and 0.3 < out["train_auc"] < 0.7
-    assert ("bulk-synchronous" in out["config"]["workload"]) == sync
+    wl = out["config"]["workload"]
+    if collective == "split":
+        assert "owner-computes" in wl and ("Localizer lane" in wl) == (not sync)
+    else:
+        assert "all-to-all-v" in wl and ("bulk-synchronous" in wl) == sync
+    main = collective + ("_sync" if sync else "_pipelined")
+    assert set(out["collectives"]) == {main, "split_sync", "a2a_sync", "rsag_sync"}
 
 
 @pytest.mark.timeout(240)

@@ -169,3 +169,55 @@ def test_split_one_owner_equals_fused_step(name):
             assert np.array_equal(a[1], b[1]), k
     cs.close()
     cf.close()
+
+
+@pytest.mark.parametrize("N", [1, 3])
+@pytest.mark.parametrize("name", ["fm_v16", "fm_v5_odd", "logit"])
+def test_split_pipeline_equals_sync_steps(name, N):
+    """SplitPipeline (the next step's partition, key exchange and owner Localizer on the
+    Localizer lanes beside the current step's forward / backward) gives split_step's results
+    bit for bit: predictions, progress and the model, over count-push, training and
+    validation steps"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    kw = CFGS[name]
+    jobs = [(H.kTraining, True), (H.kTraining, True), (H.kTraining, False),
+            (H.kValidation, False), (H.kTraining, False), (H.kTraining, False),
+            (H.kTraining, False)]
+    runs = []
+    for piped in (False, True):
+        ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(N)]
+        shards = [DI.Shard(c, N) for c in ctxs]
+        comm = DI.LoopbackComm(N)
+        pipe = DI.SplitPipeline(shards, comm) if piped else None
+        live, preds_all = [], []
+        for s, (job, cnt) in enumerate(jobs):
+            step = [D.synthetic(300, 12, 5000, binary=(r % 2 == 0), seed=500 + 31 * s + r,
+                                ragged=(s == 4)) for r in range(N)]
+            dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+            preds = [torch.zeros(300, dtype=torch.float32, device=ctxs[r].device)
+                     for r in range(N)]
+            if piped:
+                pipe.submit(dbs, job, push_cnt=cnt, preds=preds)
+                live.append(dbs)
+            else:
+                DI.split_step(shards, dbs, comm, job, push_cnt=cnt, preds=preds)
+            preds_all.append(preds)
+        if piped:
+            pipe.flush()
+        for c in ctxs:
+            c.sync()
+        out = {"preds": [[p.cpu().numpy() for p in ps] for ps in preds_all],
+               "prog": [H.progress(c) for c in ctxs],
+               "stats": [H.Store(c).stats() for c in ctxs]}
+        runs.append((ctxs, out))
+    (ca, a), (cb, b) = runs
+    for s in range(len(jobs)):
+        for r in range(N):
+            assert np.array_equal(a["preds"][s][r], b["preds"][s][r]), (name, N, s, r)
+    assert a["stats"] == b["stats"]
+    for pa, pb in zip(a["prog"], b["prog"]):
+        assert pa["nrows"] == pb["nrows"] and pa["auc"] == pb["auc"]
+        assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-12)
+    for c in ca + cb:
+        c.close()
