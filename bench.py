@@ -364,6 +364,15 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                     max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg)
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo")
+    # batches come from a loader stream (as a reader's host->device copies would): the
+    # worker's first phase (split partition / Localizer) waits only for that stream, not for
+    # the compute stream's previous step
+    loader = torch.cuda.Stream(device=dev)
+    ctx.set_input_stream(loader)
+
+    def make(seed):
+        with torch.cuda.stream(loader):
+            return DevBatch(torch, dev, B, k, kb, seed=seed)
 
     host_t = None
     if os.environ.get("DFX_HOSTTIME"):  # host seconds per call of each shard / comm method
@@ -413,13 +422,12 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
 
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (world * B * k)))
     for i in range(n_warm_epoch):
-        step(DevBatch(torch, dev, B, k, kb, seed=1_000_000 * (rank + 1) + i), True)
+        step(make(1_000_000 * (rank + 1) + i), True)
     for i in range(args.warmup):
-        step(DevBatch(torch, dev, B, k, kb, seed=2_000_000 * (rank + 1) + i), False)
+        step(make(2_000_000 * (rank + 1) + i), False)
     if pipe is not None:
         pipe.flush()
-    batches = [DevBatch(torch, dev, B, k, kb, seed=3_000_000 * (rank + 1) + i)
-               for i in range(args.steps)]
+    batches = [make(3_000_000 * (rank + 1) + i) for i in range(args.steps)]
     torch.cuda.synchronize()
     H.progress(ctx)
     # per-phase events on the stream everything is ordered on (torch's current stream: the

@@ -161,6 +161,8 @@ int pipeline_init(Context* c) {
   DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, hi));
   c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
+  DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
+  c->own_part_stream = c->part_stream;
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
                         &c->ev_free[0], &c->ev_free[1], &c->ev_part[0], &c->ev_part[1]})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -168,6 +170,8 @@ int pipeline_init(Context* c) {
     DFX_HIP(hipMalloc(d, sizeof(DevState)));
     DFX_HIP(hipMemset(*d, 0, sizeof(DevState)));
   }
+  // null-stream memsets are not ordered against the (non-blocking) lanes: complete them here
+  DFX_HIP(hipStreamSynchronize(nullptr));
   for (auto& h : c->dist_host)
     DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), (kMaxDistRanks + 2) * 8,
                           hipHostMallocDefault));
@@ -236,6 +240,12 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
     dfx_ctx_destroy(ctx);
     return rc;
   }
+  // the zpad memset (null stream) and the table's initialisation done before any stream runs
+  if (hipDeviceSynchronize() != hipSuccess) {
+    set_error("dfx_ctx_create: device synchronisation failed");
+    dfx_ctx_destroy(ctx);
+    return DFX_ERR_HIP;
+  }
   *out = ctx;
   return DFX_OK;
 }
@@ -261,6 +271,8 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
     if (d) (void)hipFree(d);
   if (c->loc_stream) (void)hipStreamSynchronize(c->loc_stream);
   if (c->own_loc_stream) (void)hipStreamDestroy(c->own_loc_stream);
+  if (c->part_stream) (void)hipStreamSynchronize(c->part_stream);
+  if (c->own_part_stream) (void)hipStreamDestroy(c->own_part_stream);
   if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->lane_ev) (void)hipEventDestroy(e);
@@ -297,11 +309,14 @@ int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out) {
 
 int dfx_ctx_set_lane_stream(dfx_ctx* ctx, int which, void* hip_stream) {
   DFX_CHECK_ARG(ctx, "null ctx");
-  DFX_CHECK_ARG(which == 0, "dfx_ctx_set_lane_stream: only the Localizer lane (0)");
+  DFX_CHECK_ARG(which == 0 || which == 2,
+                "dfx_ctx_set_lane_stream: the Localizer lane (0) or the split partition (2)");
   Context* c = &ctx->c;
   DFX_TRY(pipeline_init(c));
-  DFX_HIP(hipStreamSynchronize(c->loc_stream));  // work queued on the previous lane is done
-  c->loc_stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : c->own_loc_stream;
+  hipStream_t& cur = which == 0 ? c->loc_stream : c->part_stream;
+  hipStream_t own = which == 0 ? c->own_loc_stream : c->own_part_stream;
+  DFX_HIP(hipStreamSynchronize(cur));  // work queued on the previous stream is done
+  cur = hip_stream ? static_cast<hipStream_t>(hip_stream) : own;
   return DFX_OK;
 }
 

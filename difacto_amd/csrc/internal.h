@@ -167,6 +167,8 @@ struct Context {
   // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
   hipStream_t loc_stream = nullptr, aux_stream = nullptr;
   hipStream_t own_loc_stream = nullptr;  // the library's own Localizer lane (destroyed by it)
+  hipStream_t part_stream = nullptr;     // the split's partition (beside the Localizer lane)
+  hipStream_t own_part_stream = nullptr;
   hipStream_t in_stream = nullptr;  // where batches are produced (dfx_ctx_set_input_stream)
   bool has_in_stream = false;
   Workspace bws[2];
@@ -210,6 +212,7 @@ struct Context {
   // the slot's owner_begin ran on the Localizer lane (the forward waits for ev_loc[slot]);
   // ev_part[slot]: the slot's partition is done (host join)
   bool split_lane[2] = {false, false};
+  int split_job[2] = {0, 0};  // the slot's job type (the step's last call records its counts)
   hipEvent_t ev_part[2] = {nullptr, nullptr};
 };
 

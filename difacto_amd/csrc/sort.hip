@@ -329,7 +329,12 @@ int Workspace::os_reserve(int64_t ntiles) {
   void* before = os.p;
   const size_t want = kOsCountBytes + (size_t)ntiles * 256 * sizeof(unsigned long long);
   DFX_TRY(os.ensure(want));
-  if (os.p != before) DFX_HIP(hipMemset(os.p, 0, os.bytes));  // zero parts, no stale words
+  if (os.p != before) {
+    // zero the parts and the look-back words, complete before the host goes on: the lanes are
+    // non-blocking streams, which a memset on the null stream does not order against
+    DFX_HIP(hipMemset(os.p, 0, os.bytes));
+    DFX_HIP(hipStreamSynchronize(nullptr));
+  }
   os_tiles = ntiles;
   return DFX_OK;
 }

@@ -42,42 +42,30 @@ __device__ inline uint64_t split_key(uint64_t id, uint64_t max_index) {
   return reverse_bytes(m);  // the Localizer's key (localize.hip k_loc_transform)
 }
 
-// the block's rows [r0, r0 + nr): offsets into LDS; nnz j's row by upper_bound
-__device__ inline int split_row_of(const uint64_t* so, int nr, uint64_t j) {
-  int lo = 0, hi = nr;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (so[mid] <= j) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// nnz per (owner, row) -> row_cnt[owner * B + row]; per (owner, block) -> blk[owner * nblk + b]
+// nnz per (owner, row) -> row_cnt[owner * B + row]; per (owner, 64-row block) -> blk[owner *
+// nblk + b].  One thread per row counts its row's nnz by owner in its own LDS slice (no shared
+// counters: a thread per nnz made every nnz of a row hit one LDS word); a wave is one 64-row
+// block, whose totals are wave sums
 __global__ __launch_bounds__(kSpNT) void k_split_count(int64_t B, const uint64_t* offs,
                                                        const uint64_t* index, uint64_t max_index,
                                                        uint32_t n, uint32_t* row_cnt,
                                                        uint32_t* blk, int64_t nblk) {
-  __shared__ uint32_t cnt[kSpRows * kMaxDistRanks];  // [row][owner]
-  __shared__ uint64_t so[kSpRows + 1];
+  extern __shared__ uint32_t cnt[];  // [thread][owner]
+  static_assert(kSpRows == kWave, "a 64-row partition block is one wave");
   const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * kSpRows;
-  const int nr = (int)((B - r0) < kSpRows ? (B - r0) : kSpRows);
-  for (int i = t; i < kSpRows * (int)n; i += kSpNT) cnt[i] = 0;
-  for (int i = t; i <= nr; i += kSpNT) so[i] = offs[r0 + i];
-  __syncthreads();
-  for (uint64_t j = so[0] + t; j < so[nr]; j += kSpNT) {
-    const uint32_t o = split_owner(split_key(index[j], max_index), n);
-    atomicAdd(&cnt[split_row_of(so, nr, j) * n + o], 1u);
+  const int64_t r = (int64_t)blockIdx.x * kSpNT + t;
+  uint32_t* mine = cnt + (int64_t)t * n;
+  for (uint32_t o = 0; o < n; ++o) mine[o] = 0;
+  if (r < B) {
+    const uint64_t j1 = offs[r + 1];
+    for (uint64_t j = offs[r]; j < j1; ++j) ++mine[split_owner(split_key(index[j], max_index), n)];
   }
-  __syncthreads();
-  for (int i = t; i < nr * (int)n; i += kSpNT) {
-    const int o = i / nr, rl = i % nr;  // owner-major: consecutive threads, consecutive rows
-    row_cnt[(int64_t)o * B + r0 + rl] = cnt[rl * n + o];
-  }
-  for (int o = t; o < (int)n; o += kSpNT) {
-    uint32_t s = 0;
-    for (int rl = 0; rl < nr; ++rl) s += cnt[rl * n + o];
-    blk[(int64_t)o * nblk + blockIdx.x] = s;
+  const int64_t b = r / kSpRows;  // this wave's partition block
+  for (uint32_t o = 0; o < n; ++o) {
+    uint32_t v = mine[o];
+    if (r < B) row_cnt[(int64_t)o * B + r] = v;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    if (lane_id() == 0 && b < nblk) blk[(int64_t)o * nblk + b] = v;
   }
 }
 
@@ -258,15 +246,17 @@ int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* b, uint64_t max
   DFX_TRY(bw.hist.ensure((size_t)(nblk * nranks + 1) * 4));
   uint32_t* blk = bw.hist.as<uint32_t>();
   uint32_t* total = &c->bds[slot]->totals[0];
-  // on the Localizer lane, after the batch's producer: it reads only the batch, so it runs
-  // beside the previous step's forward / backward
-  hipStream_t st = c->loc_stream;
+  // on its own high-priority stream, after the batch's producer: it reads only the batch, so
+  // it runs beside the previous step's owner Localizer (the Localizer lane) and forward /
+  // backward, and the host has the next split counts as early as possible
+  hipStream_t st = c->part_stream;
   DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
   DFX_HIP(hipStreamWaitEvent(st, c->ev_in, 0));
   const Lane L{st, &bw, c->bds[slot], &c->ds->err};
   if (nblk > 0) {
-    hipLaunchKernelGGL(k_split_count, dim3((unsigned)nblk), dim3(kSpNT), 0, st, B, b->offset,
-                       b->index, max_index, (uint32_t)nranks, row_cnt_out, blk, nblk);
+    hipLaunchKernelGGL(k_split_count, dim3((unsigned)((B + kSpNT - 1) / kSpNT)), dim3(kSpNT),
+                       (size_t)kSpNT * nranks * 4, st, B, b->offset, b->index, max_index,
+                       (uint32_t)nranks, row_cnt_out, blk, nblk);
   }
   DFX_TRY(scan_u32(L, blk, nblk * nranks, total));
   if (nblk > 0) {
@@ -380,6 +370,7 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
     c->split_initv_gated[slot] = false;
   }
   c->split_lane[slot] = lane != 0;
+  c->split_job[slot] = job_type;
   if (lane) DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
@@ -403,8 +394,9 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   a.part = part_out;
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
-  // a step without a backward is done with the slot here
+  // a step without a backward is done with the slot (and the table) here
   DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
+  if (c->split_job[slot] != DFX_JOB_TRAINING) DFX_TRY(cap_record(c));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -477,6 +469,9 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     c->split_initv_gated[slot] = true;
   }
   DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
+  // the store's counts after this step (capacity guard, cap_check), once its updates are in:
+  // here at V_dim 0, after the ranked InitV draws otherwise
+  if (d == 0) DFX_TRY(cap_record(c));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -528,8 +523,10 @@ int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, 
                           &OL.ds->u_count, pend ? c->split_nnz[slot] : 0,
                           c->ows[slot].slot.as<uint32_t>(), counts_all_dev, rank, nranks,
                           &c->ds->n_init));
+  const bool after_backward = c->split_initv_gated[slot];
   c->split_initv_pending[slot] = false;
   DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));  // the slot's last reader
+  if (after_backward) DFX_TRY(cap_record(c));
   return DFX_OK;
 }
 

@@ -421,5 +421,6 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
   DFX_HIP(hipMemcpy(h, &c->ds->sum_u, sizeof(h), hipMemcpyDeviceToHost));
   if (mean_u) *mean_u = h[1] > 0 ? h[0] / h[1] : 0;
   DFX_HIP(hipMemset(&c->ds->sum_u, 0, sizeof(h)));
+  DFX_HIP(hipStreamSynchronize(nullptr));  // before any lane's next kernel
   return DFX_OK;
 }

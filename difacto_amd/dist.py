@@ -64,6 +64,7 @@ class Shard:
         self._want_cnt = [False, False]
         self._split = [None, None]
         self._split_R = [0, 0]
+        self._pstream = None
 
     def _slot_buffers(self, slot, n, want_cnt):
         dev = self.ctx.device
@@ -167,10 +168,18 @@ class Shard:
         dev = self.ctx.device
         b = dblk.as_batch()
         B, nnz = int(dblk.size), int(dblk.nnz)
-        keys = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
-        x = (torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
-             if (b.value or want_x) else None)
-        rc = torch.empty(max(self.nranks * B, 1), dtype=torch.int32, device=dev)
+        # the partition runs on a torch stream of its own and its outputs are allocated there,
+        # so the allocator reuses them only behind it; readers on other streams are recorded by
+        # the drivers
+        if self._pstream is None and torch.device(dev).type == "cuda":
+            self._pstream = torch.cuda.Stream(device=dev, priority=-1)
+            check(_lib.lib().dfx_ctx_set_lane_stream(self.ctx.h, 2,
+                                                     ctypes.c_void_p(self._pstream.cuda_stream)))
+        with torch.cuda.stream(self._pstream):
+            keys = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)
+            x = (torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+                 if (b.value or want_x) else None)
+            rc = torch.empty(max(self.nranks * B, 1), dtype=torch.int32, device=dev)
         check(_lib.lib().dfx_split_partition(self.ctx.h, slot, ctypes.byref(b),
                                              ctypes.c_uint64(max_index), self.nranks, _p(keys),
                                              _p(x), _p(rc)))
@@ -683,6 +692,14 @@ def rsag_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_index
     _initv(shards, comm, 0)
 
 
+def _keep(tensors, stream):
+    """tell the allocator that `stream` uses these (device) tensors: a buffer freed on the host
+    is handed out again only after that stream's work queued so far"""
+    for t in tensors:
+        if t is not None and t.device.type == "cuda":
+            t.record_stream(stream)
+
+
 def _split_initv(shards, comm, slot):
     """InitV of the split owners' requests, ranked over all owners (a tiny device all-gather)"""
     if shards[0].ctx.V_dim <= 0:
@@ -739,6 +756,11 @@ def split_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_inde
             rc = pad
         rcs.append(rc)
     rrc = comm.alltoallv(rcs, [[M] * N] * n, [[M] * N] * n)
+    cur = torch.cuda.current_stream() if torch.device(shards[0].ctx.device).type == "cuda" \
+        else None
+    if cur is not None:  # the partition's buffers (its own stream) are read here
+        for p in part:
+            _keep(p[:3], cur)
     mark(1)
     for i in range(n):
         shards[i].split_owner_begin(rkeys[i], rx[i], rrc[i], [M] * N, recv[i], job_type,
@@ -783,10 +805,13 @@ class SplitPipeline:
     flush() runs the last step.  A batch must stay alive until the submit after the one that
     took it (or flush())."""
 
+    AHEAD = 2  # steps the host may run ahead of the context stream
+
     def __init__(self, shards, comm, max_index=MAX_INDEX):
         self.shards, self.comm, self.max_index = shards, comm, max_index
         self.slot = 0
         self.pending = None
+        self.done = []  # one event per step's main-stream work: bounds the host's run-ahead
         # the contexts' Localizer lanes become torch streams (high priority, like the
         # library's own): torch's allocator tracks the exchange buffers used on them, and the
         # streams outlive the contexts
@@ -841,16 +866,19 @@ class SplitPipeline:
                 hx = comm.alltoallv_keys_async(xs, [p[3] for p in part], recv)
             rkeys, rrc = hk.wait(), hr.wait()
             rx = hx.wait() if valued else [None] * n
+            for p in part:  # the partition's buffers (its own stream) are read here
+                _keep(p[:3], torch.cuda.current_stream())
             if lane and n > 1:  # loopback: every lane waits for the exchange on lane 0
                 ev = torch.cuda.Event()
                 ev.record()
                 for ln in self.lanes[1:]:
                     ln.wait_event(ev)
         for i in range(n):
-            # the forward reads the received keys / values on the context stream later
-            for t in (rkeys[i], rx[i]):
-                if t is not None and t.device.type == "cuda":
-                    t.record_stream(main)
+            # the owner Localizer (lane) and the forward (context stream) read the received keys
+            # / values; at world size 1 they are the partition's own buffers
+            _keep((rkeys[i], rx[i]), main)
+            if lane:
+                _keep((rkeys[i], rx[i], rrc[i]), self.lanes[i])
             shards[i].split_owner_begin(rkeys[i], rx[i], rrc[i], [M] * N, recv[i], job_type,
                                         want_cnt, s, lane)
         if want_cnt:
@@ -885,6 +913,12 @@ class SplitPipeline:
         mark(5)
         mark(6)
         mark(7)
+        if torch.device(shards[0].ctx.device).type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+            self.done.append(ev)
+            while len(self.done) > self.AHEAD:
+                self.done.pop(0).synchronize()
 
 
 class ShardedPipeline:

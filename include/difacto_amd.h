@@ -90,9 +90,9 @@ int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream);
 int dfx_ctx_use_own_stream(dfx_ctx* ctx);
 /* the context's side lanes (hipStream_t): which = 0 the Localizer lane, 1 the AUC lane */
 int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out);
-/* run the Localizer lane (which = 0) on the caller's stream (it must outlive the context's use
- * of it; NULL: back to the library's own lane), e.g. a stream of the caller's framework, whose
- * allocator then tracks buffers used on it */
+/* run the Localizer lane (which = 0) or the split partition (which = 2) on the caller's stream
+ * (it must outlive the context's use of it; NULL: back to the library's own), e.g. a stream of
+ * the caller's framework, whose allocator then tracks buffers used on it */
 int dfx_ctx_set_lane_stream(dfx_ctx* ctx, int which, void* hip_stream);
 /* The stream on which dfx_train_step's batches are produced (a loader / copy stream; NULL =
  * the context stream).  A batch's Localizer waits only for that stream, so it can run while
@@ -314,7 +314,7 @@ int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos
  *                            the received arrays; it waits for the slot's previous step and
  *                            owner_forward waits for it, so it runs beside the previous step's
  *                            owner_forward / owner_backward on the context stream
- * dfx_split_partition also runs on the Localizer lane, after the batch's producer (the input
+ * dfx_split_partition runs on a stream of its own, after the batch's producer (the input
  * stream, dfx_ctx_set_input_stream, else the context stream).
  *   dfx_split_owner_forward  owner: part_out[R][dfx_split_part_floats()] per received row
  *                            [XV(d) | XXVV(d) | sum w x | 0 0 0] over this owner's keys

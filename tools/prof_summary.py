@@ -5,8 +5,9 @@ The timed window is the last N steps: it starts where the (N+1)-th-from-last ste
 `k_step_finalize` ended and stops where the last one ended.  Per kernel: dispatches per step,
 average duration, microseconds per step, and the busy fraction of the window.
 usage: prof_summary.py trace.csv N [fetch_pmc.csv write_pmc.csv]
-DFX_STEP_MARKER (default k_step_finalize; the sharded store: k_dist_worker_finalize) names
-the once-per-step kernel the window is anchored on.
+DFX_STEP_MARKER (default k_step_finalize; the sharded store: k_dist_worker_finalize, the split:
+k_split_worker_finalize) names the once-per-step kernel the window is anchored on;
+DFX_STEP_SKIP skips that many trailing steps (the bench's secondary schedule runs).
 """
 import collections
 import csv
@@ -35,9 +36,10 @@ def main():
     rows.sort()
     marker = os.environ.get("DFX_STEP_MARKER", "k_step_finalize")
     fin = [e for s, e, k in rows if marker in k]
-    if len(fin) < nsteps + 1:
-        raise SystemExit("trace holds %d steps, need %d" % (len(fin), nsteps + 1))
-    t0, t1 = fin[-nsteps - 1], fin[-1]
+    skip = int(os.environ.get("DFX_STEP_SKIP", "0"))
+    if len(fin) < nsteps + 1 + skip:
+        raise SystemExit("trace holds %d steps, need %d" % (len(fin), nsteps + 1 + skip))
+    t0, t1 = fin[-nsteps - 1 - skip], fin[-1 - skip]
     per = collections.defaultdict(list)
     busy = 0
     for s, e, k in rows:
