@@ -121,11 +121,14 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
+PMC_ROUND = "r2"  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
+
+
 def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
     """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/r1/<fname>: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
+    (profiles/<PMC_ROUND>/<fname>: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
     tools/profile.sh).  None when absent."""
-    path = os.path.join(ROOT, "profiles", "r1", fname)
+    path = os.path.join(ROOT, "profiles", PMC_ROUND, fname)
     try:
         with open(path) as f:
             ks = json.load(f)["kernels"]
@@ -138,10 +141,20 @@ def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
 
 
 def sharded_traffic():
-    """the sharded worker's forward + backward (record mode) HBM bytes per step"""
-    f = pmc_traffic("k_fm_fwd<4, 4, 2, false, true>", "pmc_hbm_sharded.json")
-    b = pmc_traffic("k_fm_bwd<4, 4, false, true>", "pmc_hbm_sharded.json")
-    return f + b if f is not None and b is not None else None
+    """the a2a sharded worker's forward + backward (record mode) HBM bytes per step (round 1's
+    passes: the a2a schedule is unchanged since)"""
+    path = os.path.join(ROOT, "profiles", "r1", "pmc_hbm_sharded.json")
+    try:
+        ks = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    tot = 0
+    for pre in ("k_fm_fwd<4, 4, 2, false, true>", "k_fm_bwd<4, 4, false, true>"):
+        v = next((v for n, v in ks.items() if n.startswith(pre)), None)
+        if v is None:
+            return None
+        tot += int((v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]) * 1024)
+    return tot
 
 
 def cpu_baseline(args):
@@ -323,11 +336,12 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic("k_fm_bwd" if dom == "backward_update"
                                             else "k_fm_fwd"),
-                     "traffic_source": "profiles/r1/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
-                                       "WRITE_SIZE per launch); counters calibrated for "
-                                       "these access shapes in "
+                     "traffic_source": "profiles/%s/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
+                                       "WRITE_SIZE per launch; request counts per key / nnz "
+                                       "in profiles/%s/pmc_requests.json); counters "
+                                       "calibrated for these access shapes in "
                                        "profiles/r1/pmc_calibration.json (64-B requests "
-                                       "counted exactly, factor 1.00)",
+                                       "counted exactly, factor 1.00)" % (PMC_ROUND, PMC_ROUND),
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
@@ -536,9 +550,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         # backward formula over the owner's rows, keys and unique keys)
         ab = algorithmic_bytes(o_rows, o_nnz, o_uniq, d)["backward_update"]
         rkernel = "owner_backward (split: fused backward + FTRL/AdaGrad + InitV, rank 0)"
-        traffic, tsrc = pmc_traffic("k_fm_bwd"), ("profiles/r1/pmc_hbm.json (the fused "
-                                                  "backward's FETCH_SIZE + WRITE_SIZE per "
-                                                  "launch, the same kernel)")
+        traffic, tsrc = (pmc_traffic("k_fm_bwd", "pmc_hbm_split.json"),
+                         "profiles/%s/pmc_hbm_split.json (rocprofv3 FETCH_SIZE + WRITE_SIZE "
+                         "per launch of the owner's backward, bench.py --sharded)" % PMC_ROUND)
     else:
         # roofline of the worker's forward+backward launch pair on this rank
         ab = algorithmic_bytes_sharded(B, B * k, max(shard._U), d)
