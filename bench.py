@@ -60,6 +60,9 @@ def parse():
                          "records / gradients all-to-all-v (pipelined unless --sync).  The "
                          "other schedules, and the north_star's literal union all-gather / "
                          "reduce-scatter (rsag), are measured beside it on short runs")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="sharded store: run every exchange as an RCCL collective even at N=1 "
+                         "(tests the multi-GPU code paths on one GPU)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="sharded store transport; gloo (staged through host memory) runs "
                          "several ranks on one GPU, for tests")
@@ -377,7 +380,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
                     max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg)
     shard = DI.Shard(ctx, world)
-    comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo")
+    comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo",
+                        force_collectives=args.force_collectives)
     # batches come from a loader stream (as a reader's host->device copies would): the
     # worker's first phase (split partition / Localizer) waits only for that stream, not for
     # the compute stream's previous step

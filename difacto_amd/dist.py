@@ -280,11 +280,14 @@ class TorchComm:
     that step t+1's key exchange neither queues behind step t's gradient exchange nor waits
     for the compute stream; the split counts go over a gloo group on the host."""
 
-    def __init__(self, group=None, device=None, stage_cpu=False):
+    def __init__(self, group=None, device=None, stage_cpu=False, force_collectives=False):
+        """force_collectives: run every exchange as a collective even at world size 1 (whose
+        exchanges are otherwise the inputs themselves) — exercises the RCCL paths on one GPU"""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
+        self.solo = self.world == 1 and not force_collectives
         self.rank = dist.get_rank(group)
         self.device = device
         self.stage_cpu = stage_cpu
@@ -310,7 +313,7 @@ class TorchComm:
         all-to-all of N int64 on the key communicator's idle stream, read back into host
         memory — no host-side (gloo / TCP) collective in the step; gloo: all_gather"""
         (s,) = send_splits
-        if self.nccl and self.world > 1:
+        if self.nccl and not self.solo:
             with torch.cuda.stream(self.kstream):
                 t = torch.tensor(s, dtype=torch.int64, device=self.device)
                 out = torch.empty(self.world, dtype=torch.int64, device=self.device)
@@ -327,13 +330,13 @@ class TorchComm:
         (s,) = send
         N = self.world
         pairs = [[int(s[g]), int(s[N + g])] for g in range(N)]
-        if self.nccl and N > 1:
+        if self.nccl and not self.solo:
             with torch.cuda.stream(self.kstream):
                 t = torch.tensor(pairs, dtype=torch.int64, device=self.device).reshape(-1)
                 out = torch.empty(2 * N, dtype=torch.int64, device=self.device)
                 self.dist.all_to_all_single(out, t, group=self.kgroup)
                 o = out.cpu().tolist()
-        elif N > 1:
+        elif not self.solo:
             t = torch.tensor(pairs, dtype=torch.int64).reshape(-1)
             outs = [torch.empty_like(t) for _ in range(N)]
             self.dist.all_gather(outs, t, group=self.cgroup)
@@ -350,7 +353,7 @@ class TorchComm:
         (x,) = tensors
         buf = torch.zeros(M * row, dtype=x.dtype, device=x.device)
         buf[:x.numel()] = x
-        if self.world == 1:
+        if self.solo:
             return [buf]
         if self.stage_cpu:
             out = [torch.empty(M * row, dtype=x.dtype) for _ in range(self.world)]
@@ -364,7 +367,7 @@ class TorchComm:
         """the north_star's reduce-scatter: every rank's [world * M * row] buffer summed, rank
         g receiving chunk g"""
         (x,) = tensors
-        if self.world == 1:
+        if self.solo:
             return [x]
         if self.stage_cpu:  # gloo has no reduce-scatter: all-reduce, keep this rank's chunk
             t = x.cpu()
@@ -379,7 +382,7 @@ class TorchComm:
         """every rank's device int64[1] -> device int64[world] in rank order (stream-ordered
         on the current stream: no host round trip)"""
         (t,) = tensors
-        if self.world == 1:
+        if self.solo:
             return [t]
         if self.stage_cpu:
             out = [torch.empty(1, dtype=torch.int64) for _ in range(self.world)]
@@ -399,7 +402,7 @@ class TorchComm:
         if self.stage_cpu:
             x = x.cpu()
         x = x.contiguous()
-        if self.world == 1:
+        if self.solo:
             return (x.to(home) if self.stage_cpu else x), None
         if self.nccl:
             # one all-to-all-v call (RCCL groups the per-peer sends / receives in C++): a
