@@ -72,6 +72,8 @@ def parse():
                          "share that priority's hardware queues, whose packets run in order: "
                          "a high-priority compute stream keeps the step's kernels off the "
                          "queues of RCCL's (normal-priority) streams")
+    ap.add_argument("--comm-prio", default="high", choices=("normal", "high"),
+                    help="priority of RCCL's streams (TorchComm comm_priority)")
     ap.add_argument("--ctx", default="",
                     help="extra context kwargs k=v,... (A/B of execution choices, e.g. "
                          "sort_pack=0)")
@@ -381,7 +383,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                     max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg)
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo",
-                        force_collectives=args.force_collectives)
+                        force_collectives=args.force_collectives, comm_priority=args.comm_prio)
     # batches come from a loader stream (as a reader's host->device copies would): the
     # worker's first phase (split partition / Localizer) waits only for that stream, not for
     # the compute stream's previous step
@@ -407,7 +409,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                 return r
             setattr(obj, name, w)
         for nm in ("localize", "localize_wait", "fwd_bwd", "owner_begin", "owner_pull",
-                   "owner_push"):
+                   "owner_push", "split_partition", "split_partition_wait", "split_owner_begin",
+                   "split_owner_forward", "split_combine", "split_owner_backward",
+                   "split_initv_local", "split_initv_draw"):
             timed(shard, nm)
         lw = shard.localize_wait
 
@@ -418,7 +422,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
             host_t["main_idle_at_join"] += 1e-3 * float(e.query())
             return r
         shard.localize_wait = lw_probe
-        for nm in ("exchange_counts", "alltoallv_async", "alltoallv_keys_async"):
+        for nm in ("exchange_counts", "exchange_counts2", "alltoallv_async",
+                   "alltoallv_keys_async", "allgather_rows", "allgather_i64"):
             timed(comm, nm)
     split = args.collective == "split"
     if args.sync:
@@ -482,9 +487,13 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         prof.enable()
     dist.barrier()
     torch.cuda.synchronize()
+    if isinstance(pipe, DI.SplitPipeline):
+        pipe.throttle_s = 0.0
     t0 = time.perf_counter()
     evs = run_steps(FB)
     t_enq = time.perf_counter() - t0
+    # the host's own work per step: enqueue time less its waits on the run-ahead bound
+    t_busy = t_enq - (pipe.throttle_s if isinstance(pipe, DI.SplitPipeline) else 0.0)
     if host_t is not None:
         print("host ms/step", {k_: round(v / args.steps * 1e3, 4) for k_, v in host_t.items()},
               file=sys.stderr, flush=True)
@@ -606,6 +615,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                              {"ms_per_step": round(elapsed / args.steps * 1e3, 4),
                               "value": round(value, 1), "steps": args.steps}}, **colls),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+        "host_busy_ms_per_step": round(t_busy / args.steps * 1e3, 4),
         "train_loss_per_row": round(tot[0] / max(tot[2], 1), 6),
         "train_auc": round(tot[1] / max(tot[2], 1), 6),
         "model_keys": int(tot[3]), "model_vrows": int(tot[4]),

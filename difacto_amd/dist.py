@@ -17,6 +17,7 @@ over torch.distributed (one shard per process) or, for single-GPU tests, over N 
 by one process (``LoopbackComm``).
 """
 import ctypes
+import time
 
 import torch
 
@@ -280,9 +281,13 @@ class TorchComm:
     that step t+1's key exchange neither queues behind step t's gradient exchange nor waits
     for the compute stream; the split counts go over a gloo group on the host."""
 
-    def __init__(self, group=None, device=None, stage_cpu=False, force_collectives=False):
+    def __init__(self, group=None, device=None, stage_cpu=False, force_collectives=False,
+                 comm_priority="high"):
         """force_collectives: run every exchange as a collective even at world size 1 (whose
-        exchanges are otherwise the inputs themselves) — exercises the RCCL paths on one GPU"""
+        exchanges are otherwise the inputs themselves) — exercises the RCCL paths on one GPU.
+        comm_priority: "high" runs RCCL's kernels on high-priority streams, like the
+        Localizer lanes beside them: on normal-priority streams their blocks wait behind the
+        lanes' for CU slots while the compute stream waits for the exchange"""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -294,7 +299,13 @@ class TorchComm:
         self.nccl = dist.get_backend(group) == "nccl"
         if self.nccl:
             ranks = list(range(self.world))
-            self.kgroup = dist.new_group(ranks)
+            opts = None
+            if comm_priority == "high":
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                if group is None:
+                    self.group = dist.new_group(ranks, backend="nccl", pg_options=opts)
+            self.kgroup = dist.new_group(ranks, backend="nccl", pg_options=opts)
             self.cgroup = dist.new_group(ranks, backend="gloo")
             self.kstream = torch.cuda.Stream(device=device)
             # communicators up before the first grouped send/recv, which need not involve
@@ -815,6 +826,7 @@ class SplitPipeline:
         self.slot = 0
         self.pending = None
         self.done = []  # one event per step's main-stream work: bounds the host's run-ahead
+        self.throttle_s = 0.0  # host seconds spent waiting on that bound
         # the contexts' Localizer lanes become torch streams (high priority, like the
         # library's own): torch's allocator tracks the exchange buffers used on them, and the
         # streams outlive the contexts
@@ -920,8 +932,10 @@ class SplitPipeline:
             ev = torch.cuda.Event()
             ev.record()
             self.done.append(ev)
+            t = time.perf_counter()
             while len(self.done) > self.AHEAD:
                 self.done.pop(0).synchronize()
+            self.throttle_s += time.perf_counter() - t
 
 
 class ShardedPipeline:
