@@ -24,7 +24,9 @@ GENBIN = build/gen_criteo
 CONVBIN = build/dfx_convert
 RBENCH = build/reader_bench
 
-all: $(LIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH)
+DISTLIB = difacto_amd/libdfx_dist.so
+
+all: $(LIB) $(DISTLIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH)
 
 $(RBENCH): difacto_amd/host/reader.cc tools/reader_bench.cc difacto_amd/host/reader.h
 	@mkdir -p build
@@ -68,6 +70,14 @@ $(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc $(HOSTHDR) difacto_amd/ho
 	  -Ldifacto_amd -ldifacto_amd -L/opt/rocm/lib -lrccl -lamdhip64 \
 	  -Wl,-rpath,'$$ORIGIN/../difacto_amd' -Wl,-rpath,/opt/rocm/lib
 
+# the multi-GPU split driver's C-ABI (include/difacto_amd_dist.h): host code (HIP runtime
+# API + RCCL) over libdifacto_amd.so, loaded by difacto_amd/_lib.py beside it
+$(DISTLIB): difacto_amd/host/split_host.cc difacto_amd/host/split_host.h \
+  include/difacto_amd_dist.h include/difacto_amd.h $(LIB)
+	g++ -std=c++17 -O2 -fPIC -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -shared -o $@ \
+	  difacto_amd/host/split_host.cc -Ldifacto_amd -ldifacto_amd -L/opt/rocm/lib -lrccl -lamdhip64 \
+	  -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
+
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -79,7 +89,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(DISTLIB)
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

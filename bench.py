@@ -72,6 +72,9 @@ def parse():
                          "share that priority's hardware queues, whose packets run in order: "
                          "a high-priority compute stream keeps the step's kernels off the "
                          "queues of RCCL's (normal-priority) streams")
+    ap.add_argument("--driver", default="cpp", choices=("cpp", "py"),
+                    help="the split step's driver over RCCL: C++ (libdfx_dist.so, its own "
+                         "communicators) or Python (dist.SplitPipeline over torch.distributed)")
     ap.add_argument("--comm-prio", default="high", choices=("normal", "high"),
                     help="priority of RCCL's streams (TorchComm comm_priority)")
     ap.add_argument("--ctx", default="",
@@ -426,7 +429,19 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                    "alltoallv_keys_async", "allgather_rows", "allgather_i64"):
             timed(comm, nm)
     split = args.collective == "split"
-    if args.sync:
+    # the split's C++ driver (libdfx_dist.so) over its own RCCL communicators: the schedule of
+    # split_step / SplitPipeline without the interpreter between the launches
+    cpp = split and args.driver == "cpp" and args.backend == "nccl"
+    store = None
+    if cpp:
+        ids = torch.zeros(3 * 128, dtype=torch.uint8)
+        if rank == 0:
+            ids = torch.frombuffer(bytearray(DI.SplitStore.rccl_ids()), dtype=torch.uint8)
+        dist.broadcast(ids, src=0, group=comm.cgroup)
+        store = DI.SplitStore([shard], pipelined=not args.sync,
+                              rccl=(rank, world, ids.numpy().tobytes(), args.force_collectives))
+        pipe = None
+    elif args.sync:
         pipe = None
     elif split:
         pipe = DI.SplitPipeline([shard], comm)
@@ -436,7 +451,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     sync_fn = DI.split_step if split else DI.sharded_step
 
     def step(batch, push_cnt, mark=None):
-        if pipe is None:
+        if store is not None:
+            store.submit([batch], H.kTraining, push_cnt=push_cnt)
+        elif pipe is None:
             sync_fn([shard], [batch], comm, H.kTraining, push_cnt=push_cnt, mark=mark)
         else:
             pipe.submit([batch], H.kTraining, push_cnt=push_cnt, mark=mark)
@@ -450,6 +467,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         step(make(2_000_000 * (rank + 1) + i), False)
     if pipe is not None:
         pipe.flush()
+    if store is not None:
+        store.flush()
     batches = [make(3_000_000 * (rank + 1) + i) for i in range(args.steps)]
     torch.cuda.synchronize()
     H.progress(ctx)
@@ -461,9 +480,16 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     # around the roofline's kernels (split: the owner's backward + its InitV; a2a: the worker's
     # forward+backward); the per-phase breakdown comes from an untimed diagnostic pass over the
     # same batches afterwards.
-    FB = ((6, 7) if pipe is None else (3, 4)) if split else (4, 5)
+    FB = ((6, 7) if pipe is None and store is None else (3, 4)) if split else (4, 5)
 
     def run_steps(js):
+        if store is not None:  # the driver's own events at its main-stream boundaries
+            store.set_marks([j + 1 for j in js if j < DI.SplitStore.MARKS - 1])
+            for bt in batches:
+                step(bt, False)
+            store.flush()
+            store.set_marks([])
+            return None
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(nph + 1)]
                for _ in range(args.steps)]
 
@@ -489,11 +515,14 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     torch.cuda.synchronize()
     if isinstance(pipe, DI.SplitPipeline):
         pipe.throttle_s = 0.0
+    if store is not None:
+        store.throttle_seconds()
     t0 = time.perf_counter()
     evs = run_steps(FB)
     t_enq = time.perf_counter() - t0
     # the host's own work per step: enqueue time less its waits on the run-ahead bound
-    t_busy = t_enq - (pipe.throttle_s if isinstance(pipe, DI.SplitPipeline) else 0.0)
+    t_busy = t_enq - (pipe.throttle_s if isinstance(pipe, DI.SplitPipeline) else
+                      store.throttle_seconds() if store is not None else 0.0)
     if host_t is not None:
         print("host ms/step", {k_: round(v / args.steps * 1e3, 4) for k_, v in host_t.items()},
               file=sys.stderr, flush=True)
@@ -509,19 +538,26 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     elapsed = float(t.item())
     # the worker's forward+backward launch pair (pipelined: including the wait for the record
     # exchange, so `achieved` is a lower bound)
-    fb_ms = sum(evs[i][FB[0] + 1].elapsed_time(evs[i][FB[1] + 1])
-                for i in range(args.steps)) / args.steps
+    if store is not None:
+        v, n = store.take_marks()["owner_backward"]
+        fb_ms = v / max(n, 1)
+    else:
+        fb_ms = sum(evs[i][FB[0] + 1].elapsed_time(evs[i][FB[1] + 1])
+                    for i in range(args.steps)) / args.steps
     prog = H.progress(ctx)
 
     # diagnostic pass (untimed): every phase
     evs = run_steps(range(-1, nph))
     torch.cuda.synchronize()
-    if split:
-        names = DI.SPLIT_PHASES if pipe is None else DI.SPLIT_PIPE_PHASES
+    if store is not None:
+        ph = {p: v / max(n, 1) for p, (v, n) in store.take_marks().items()}
     else:
-        names = DI.PHASES if pipe is None else DI.PIPE_PHASES
-    ph = {p: sum(evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps)) / args.steps
-          for j, p in enumerate(names)}
+        if split:
+            names = DI.SPLIT_PHASES if pipe is None else DI.SPLIT_PIPE_PHASES
+        else:
+            names = DI.PHASES if pipe is None else DI.PIPE_PHASES
+        ph = {p: sum(evs[i][j].elapsed_time(evs[i][j + 1]) for i in range(args.steps))
+              / args.steps for j, p in enumerate(names)}
     H.progress(ctx)
     # the other collective schedules on the same batches, bulk synchronous (short runs): the
     # all-to-all-v step, and the north_star's literal union all-gather / reduce-scatter
@@ -534,17 +570,34 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     nb = min(args.steps, 20)
     main_name = (("split_sync" if args.sync else "split_pipelined") if split else
                  ("a2a_sync" if args.sync else "a2a_pipelined"))
-    for cname, fn in (("split_sync", DI.split_step), ("a2a_sync", DI.sharded_step),
-                      ("rsag_sync", DI.rsag_step)):
+    if store is not None:
+        main_name += "_cpp"
+    py_pipe = [None]
+
+    def py_split_pipelined(shards, dblks, comm_, job):
+        if py_pipe[0] is None:
+            py_pipe[0] = DI.SplitPipeline(shards, comm_)
+        py_pipe[0].submit(dblks, job)
+
+    sched = [("split_sync", DI.split_step), ("a2a_sync", DI.sharded_step),
+             ("rsag_sync", DI.rsag_step)]
+    if store is not None and not args.sync:  # the same schedule driven from Python
+        sched.insert(0, ("split_pipelined_py", py_split_pipelined))
+    for cname, fn in sched:
         if cname == main_name or (cname != "a2a_sync" and args.push_agg != "sum"):
             continue
         for bt in batches[:2]:
             fn([shard], [bt], comm, H.kTraining)
+        if py_pipe[0] is not None:
+            py_pipe[0].flush()
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
         for bt in batches[:nb]:
             fn([shard], [bt], comm, H.kTraining)
+        if py_pipe[0] is not None:
+            py_pipe[0].flush()
+            py_pipe[0] = None
         torch.cuda.synchronize()
         dist.barrier()
         dt = time.perf_counter() - t1
@@ -603,7 +656,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                                      else "pipelined 1-step-stale"),
                                   args.push_agg),
                    "rows_per_gpu_step": B, "global_batch": B * world,
-                   "parallelism": "dp%d + model sharded by key range" % world},
+                   "parallelism": "dp%d + model sharded by key range" % world,
+                   "driver": "cpp (libdfx_dist.so)" if store is not None else "python"},
         "roofline": {"bound": "hbm", "kernel": rkernel,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -622,6 +676,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if store is not None:
+        store.close()
     ctx.close()
 
 

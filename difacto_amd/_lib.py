@@ -149,3 +149,52 @@ def check(rc):
     if rc != 0:
         msg = lib().dfx_last_error()
         raise DfxError("libdifacto_amd: status %d: %s" % (rc, msg.decode() if msg else "?"))
+
+
+# ---- libdfx_dist.so: the multi-GPU split driver (include/difacto_amd_dist.h) ----------------
+DIST_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdfx_dist.so")
+_dist = None
+u32 = ctypes.c_uint32
+
+_DIST_SIGS = {
+    "dfx_dist_last_error": (ctypes.c_char_p, []),
+    "dfx_dist_rccl_id_bytes": (ctypes.c_int, []),
+    "dfx_dist_rccl_ids": (ctypes.c_int, [ctypes.c_int, vp]),
+    "dfx_split_store_create_rccl": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp,
+                                                   ctypes.c_int, ctypes.c_int, c_u64,
+                                                   ctypes.POINTER(vp)]),
+    "dfx_split_store_create_loopback": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int,
+                                                       ctypes.c_int, c_u64, ctypes.POINTER(vp)]),
+    "dfx_split_store_submit": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.c_int,
+                                              ctypes.c_int, ctypes.POINTER(vp)]),
+    "dfx_split_store_flush": (ctypes.c_int, [vp]),
+    "dfx_split_store_throttle_seconds": (ctypes.c_int, [vp, f64p]),
+    "dfx_split_store_set_marks": (ctypes.c_int, [vp, u32]),
+    "dfx_split_store_take_marks": (ctypes.c_int, [vp, f64p, i64p]),
+    "dfx_split_store_destroy": (ctypes.c_int, [vp]),
+}
+
+DIST_EXPORTED = tuple(_DIST_SIGS)
+
+
+def dist_lib():
+    """the split driver's library (opened after libdifacto_amd.so, which it links)"""
+    global _dist
+    if _dist is None:
+        lib()
+        if not os.path.exists(DIST_PATH):
+            raise DfxError("libdfx_dist.so is not built (%s); run `make` at the repo root"
+                           % DIST_PATH)
+        L = ctypes.CDLL(DIST_PATH)
+        for name, (res, args) in _DIST_SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _dist = L
+    return _dist
+
+
+def dist_check(rc):
+    if rc != 0:
+        msg = dist_lib().dfx_dist_last_error()
+        raise DfxError("libdfx_dist: status %d: %s" % (rc, msg.decode() if msg else "?"))

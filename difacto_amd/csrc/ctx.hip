@@ -301,9 +301,13 @@ int dfx_ctx_set_input_stream(dfx_ctx* ctx, void* hip_stream) {
 
 int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out) {
   DFX_CHECK_ARG(ctx && out, "null argument");
-  DFX_CHECK_ARG(which == 0 || which == 1, "dfx_ctx_lane_stream: 0 (Localizer) or 1 (AUC)");
+  DFX_CHECK_ARG(which >= 0 && which <= 3,
+                "dfx_ctx_lane_stream: 0 (Localizer), 1 (AUC), 2 (split partition) or 3 (the "
+                "context stream)");
   DFX_TRY(pipeline_init(&ctx->c));
-  *out = which == 0 ? ctx->c.loc_stream : ctx->c.aux_stream;
+  const Context& c = ctx->c;
+  *out = which == 0 ? c.loc_stream : which == 1 ? c.aux_stream : which == 2 ? c.part_stream
+                                                                            : c.stream;
   return DFX_OK;
 }
 

@@ -1021,3 +1021,94 @@ class ShardedPipeline:
         for i, sh in enumerate(self.shards):
             sh.owner_push(rgrads[i], s)
         _initv(self.shards, self.comm, s)
+
+
+class SplitStore:
+    """The owner-computes split driven from C++ (libdfx_dist.so, host/split_host.cc): the
+    schedule of split_step (pipelined=False) or SplitPipeline (pipelined=True) without the
+    interpreter between the launches — the same results bit for bit.
+
+    Loopback: SplitStore(shards) drives N shards held by this process (one GPU).  RCCL:
+    SplitStore([shard], rccl=(rank, nranks, ids, force_exchange)), one shard per process,
+    ids = SplitStore.rccl_ids() made on rank 0 and handed to every rank by the caller.
+
+    Batches must stay alive until the second submit after the one that took them (the store
+    keeps them), a pipelined step's predictions / progress are complete after the next submit
+    (or flush())."""
+
+    MARKS = 7  # main-stream boundaries (dfx_split_store_set_marks)
+    PHASES = ("owner_forward", "xchg_parts", "combine", "xchg_pxv", "owner_backward", "initv")
+
+    def __init__(self, shards, pipelined=True, max_index=MAX_INDEX, rccl=None):
+        D = _lib.dist_lib()
+        self.n = len(shards)
+        self.shards = shards
+        h = ctypes.c_void_p()
+        if rccl is None:
+            arr = (ctypes.c_void_p * self.n)(*[sh.ctx.h for sh in shards])
+            _lib.dist_check(D.dfx_split_store_create_loopback(arr, self.n, int(bool(pipelined)),
+                                                              max_index, ctypes.byref(h)))
+        else:
+            if self.n != 1:
+                raise ValueError("SplitStore over RCCL holds one shard per process")
+            rank, nranks, ids, force = rccl
+            buf = ctypes.create_string_buffer(bytes(ids), len(ids))
+            _lib.dist_check(D.dfx_split_store_create_rccl(
+                shards[0].ctx.h, int(rank), int(nranks), buf, int(bool(force)),
+                int(bool(pipelined)), max_index, ctypes.byref(h)))
+        self.h = h
+        self._live = []
+
+    @staticmethod
+    def rccl_ids():
+        """fresh communicator ids (rank 0), as bytes for the caller's rendezvous"""
+        D = _lib.dist_lib()
+        n = 3 * D.dfx_dist_rccl_id_bytes()
+        buf = ctypes.create_string_buffer(n)
+        _lib.dist_check(D.dfx_dist_rccl_ids(3, buf))
+        return buf.raw
+
+    def submit(self, dblks, job_type=kTraining, push_cnt=False, preds=None):
+        D = _lib.dist_lib()
+        bs = (_lib.Batch * self.n)(*[b.as_batch() for b in dblks])
+        pp = None
+        if preds is not None:
+            pp = (ctypes.c_void_p * self.n)(*[p.data_ptr() if p is not None else None
+                                              for p in preds])
+        _lib.dist_check(D.dfx_split_store_submit(self.h, bs, int(job_type), int(bool(push_cnt)),
+                                                 pp))
+        self._live.append((dblks, preds))
+        del self._live[:-3]
+
+    def flush(self):
+        _lib.dist_check(_lib.dist_lib().dfx_split_store_flush(self.h))
+
+    def throttle_seconds(self):
+        v = ctypes.c_double(0)
+        _lib.dist_check(_lib.dist_lib().dfx_split_store_throttle_seconds(self.h, ctypes.byref(v)))
+        return v.value
+
+    def set_marks(self, boundaries):
+        mask = 0
+        for b in boundaries:
+            mask |= 1 << int(b)
+        _lib.dist_check(_lib.dist_lib().dfx_split_store_set_marks(self.h, mask))
+
+    def take_marks(self):
+        """-> {phase: (summed ms, steps)} of the marked steps"""
+        ms = (ctypes.c_double * (self.MARKS - 1))()
+        st = (ctypes.c_int64 * (self.MARKS - 1))()
+        _lib.dist_check(_lib.dist_lib().dfx_split_store_take_marks(self.h, ms, st))
+        return {p: (ms[i], st[i]) for i, p in enumerate(self.PHASES)}
+
+    def close(self):
+        if self.h:
+            _lib.dist_check(_lib.dist_lib().dfx_split_store_destroy(self.h))
+            self.h = None
+            self._live = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -88,7 +88,8 @@ int dfx_ctx_destroy(dfx_ctx* ctx);
  * hipStream_t (NULL = the null stream, torch's default); use_own_stream switches back. */
 int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream);
 int dfx_ctx_use_own_stream(dfx_ctx* ctx);
-/* the context's side lanes (hipStream_t): which = 0 the Localizer lane, 1 the AUC lane */
+/* the context's streams (hipStream_t): which = 0 the Localizer lane, 1 the AUC lane, 2 the
+ * split partition's stream, 3 the context stream itself */
 int dfx_ctx_lane_stream(dfx_ctx* ctx, int which, void** out);
 /* run the Localizer lane (which = 0) or the split partition (which = 2) on the caller's stream
  * (it must outlive the context's use of it; NULL: back to the library's own), e.g. a stream of

@@ -221,3 +221,92 @@ def test_split_pipeline_equals_sync_steps(name, N):
         assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-12)
     for c in ca + cb:
         c.close()
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+@pytest.mark.parametrize("N", [1, 3])
+@pytest.mark.parametrize("name", ["fm_v16", "fm_v5_odd", "logit"])
+def test_split_store_cpp_equals_python_schedule(name, N, pipelined):
+    """the C++ driver (libdfx_dist.so, host/split_host.cc, loopback transport) gives
+    split_step's results bit for bit: predictions, progress and the model, over count-push,
+    training and validation steps, mixed binary / valued workers and an empty worker"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    kw = CFGS[name]
+    jobs = [(H.kTraining, True), (H.kTraining, True), (H.kTraining, False),
+            (H.kValidation, False), (H.kTraining, False), (H.kTraining, False),
+            (H.kTraining, False)]
+    runs, blocks = [], []
+    for cpp in (False, True):
+        ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(N)]
+        shards = [DI.Shard(c, N) for c in ctxs]
+        comm = DI.LoopbackComm(N)
+        store = DI.SplitStore(shards, pipelined=pipelined) if cpp else None
+        preds_all = []
+        for s, (job, cnt) in enumerate(jobs):
+            step = [D.synthetic(0 if (s == 5 and r == 1) else 300, 12, 5000,
+                                binary=(r % 2 == 0), seed=700 + 31 * s + r, ragged=(s == 4))
+                    for r in range(N)]
+            if not cpp:
+                blocks += step
+            dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+            preds = [torch.zeros(300, dtype=torch.float32, device=ctxs[r].device)
+                     for r in range(N)]
+            if cpp:
+                store.submit(dbs, job, push_cnt=cnt, preds=preds)
+            else:
+                DI.split_step(shards, dbs, comm, job, push_cnt=cnt, preds=preds)
+            preds_all.append(preds)
+        if cpp:
+            store.flush()
+        for c in ctxs:
+            c.sync()
+        out = {"preds": [[p.cpu().numpy() for p in ps] for ps in preds_all],
+               "prog": [H.progress(c) for c in ctxs],
+               "stats": [H.Store(c).stats() for c in ctxs]}
+        if cpp:
+            store.close()
+        runs.append((ctxs, out))
+    (ca, a), (cb, b) = runs
+    for s in range(len(jobs)):
+        for r in range(N):
+            assert np.array_equal(a["preds"][s][r], b["preds"][s][r]), (name, N, s, r)
+    assert a["stats"] == b["stats"]
+    for pa, pb in zip(a["prog"], b["prog"]):
+        assert pa["nrows"] == pb["nrows"] and pa["auc"] == pb["auc"]
+        assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-12)
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0] for b in blocks if b.size]))
+    for k in keys[::max(1, len(keys) // 150)]:
+        for r in range(N):
+            ea, eb = H.Store(ca[r]).entry(k), H.Store(cb[r]).entry(k)
+            assert (ea is None) == (eb is None)
+            if ea is not None:
+                assert np.array_equal(ea[0], eb[0])
+                assert (ea[1] is None) == (eb[1] is None)
+                if ea[1] is not None:
+                    assert np.array_equal(ea[1], eb[1])
+    for c in ca + cb:
+        c.close()
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_split_store_marks(pipelined):
+    """the C++ driver's phase events: every marked step times every main-stream phase"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    kw = CFGS["fm_v16"]
+    ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(2)]
+    store = DI.SplitStore([DI.Shard(c, 2) for c in ctxs], pipelined=pipelined)
+    store.set_marks(range(DI.SplitStore.MARKS))
+    for s in range(4):
+        step = [D.synthetic(2000, 20, 50000, seed=40 + 2 * s + r) for r in range(2)]
+        store.submit([H.DeviceRowBlock(ctxs[r], step[r]) for r in range(2)], H.kTraining,
+                     push_cnt=s == 0)
+    store.flush()
+    m = store.take_marks()
+    assert all(n == 4 for _, n in m.values()), m
+    assert m["owner_forward"][0] > 0 and m["owner_backward"][0] > 0, m
+    assert all(n == 0 for _, n in store.take_marks().values())
+    store.close()
+    for c in ctxs:
+        c.close()
