@@ -549,7 +549,9 @@ def test_bench_rccl_collectives_at_world_one(collective):
     """bench.py's sharded path with every exchange forced through RCCL at world size 1 (the
     count all-to-all, the key / record / partial all-to-all-v, the all-gathers) gives the same
     training as the same run whose exchanges are the inputs themselves: the multi-GPU code
-    paths of dist.TorchComm exercised on the test box's one GPU"""
+    paths of dist.TorchComm — and, for the split, of the C++ driver's RCCL transport
+    (libdfx_dist.so) — exercised on the test box's one GPU.  The split's two drivers (C++ and
+    Python) train identically."""
     import json
     import os
     import socket
@@ -557,23 +559,26 @@ def test_bench_rccl_collectives_at_world_one(collective):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
-    for force in (False, True):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
-               "1", "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py",
-               "--sharded", "--steps", "4", "--warmup", "1", "--batch", "20000", "--key-bits",
-               "20", "--no-cpu-baseline", "--collective", collective] + (
-                   ["--force-collectives"] if force else [])
-        r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-        lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        assert len(lines) == 1, r.stdout
-        outs.append(json.loads(lines[0]))
-    a, b = outs
-    assert a["train_loss_per_row"] == b["train_loss_per_row"]
-    assert a["train_auc"] == b["train_auc"]
-    assert a["model_keys"] == b["model_keys"] and a["model_vrows"] == b["model_vrows"]
-    assert set(a["collectives"]) == set(b["collectives"])
+    drivers = ("cpp", "py") if collective == "split" else ("py",)
+    for driver in drivers:
+        for force in (False, True):
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+            s.close()
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
+                   str(port), "bench.py", "--sharded", "--steps", "4", "--warmup", "1",
+                   "--batch", "20000", "--key-bits", "20", "--no-cpu-baseline", "--collective",
+                   collective, "--driver", driver] + (["--force-collectives"] if force else [])
+            r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+            lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            assert len(lines) == 1, r.stdout
+            outs.append(json.loads(lines[0]))
+    a = outs[0]
+    for b in outs[1:]:
+        assert a["train_loss_per_row"] == b["train_loss_per_row"]
+        assert a["train_auc"] == b["train_auc"]
+        assert a["model_keys"] == b["model_keys"] and a["model_vrows"] == b["model_vrows"]
+    assert set(outs[0]["collectives"]) == set(outs[1]["collectives"])
