@@ -114,9 +114,10 @@ struct __attribute__((aligned(32))) Entry {
 static_assert(sizeof(Entry) == 32, "Entry must be 32 bytes");
 
 struct Table {
-  Entry* ent;       // cap entries
-  float* V;         // vcap rows of [V(d) | Vaux(d)]: a key's embedding and its AdaGrad
-                    // accumulators share one 2*d*4-byte row (one 128-byte line at d = 16)
+  Entry* ent;       // cap slots of 32 << es bytes, the entry first
+  float* V;         // split layout (es == 0): vcap rows of [V(d) | Vaux(d)] — a key's embedding
+                    // and its AdaGrad accumulators share one 2*d*4-byte row (one 128-byte line
+                    // at d = 16); fat slots (es > 0): cap rows of Vaux(d), row = slot
   uint64_t mask;    // cap - 1
   int logcap;
   int d;
@@ -127,13 +128,34 @@ struct Table {
   // ranges of the key space (dist.hip, owner(k) = floor(k * N / 2^64)), whose top bits are
   // constant; k * range_mul (mod 2^64) is the key's position inside its range, monotone in k
   uint64_t range_mul;
+  // slot stride: 32 << es bytes.  es = 0: the split layout (32-byte entries, V rows in the pool,
+  // vrow = pool row).  es = 1 / 2 (fat slots, 64 / 128 bytes, 4 <= d <= 24): the slot holds the
+  // entry and then the key's V, so the forward's lookup and its V read are one line; Vaux
+  // stays in the pool, one d-float row per slot; a key's vrow is its own slot (InitV sets it,
+  // a rehash moves the row with the slot)
+  int es;
 };
 
+__host__ __device__ inline Entry* ent_at(const Table& t, int64_t s) { return t.ent + (s << t.es); }
+
 __host__ __device__ inline float* row_V(const Table& t, int64_t vr) {
-  return t.V + vr * 2 * (int64_t)t.d;
+  return t.es ? reinterpret_cast<float*>(t.ent + (vr << t.es) + 1) : t.V + vr * 2 * (int64_t)t.d;
 }
 __host__ __device__ inline float* row_C(const Table& t, int64_t vr) {
-  return t.V + vr * 2 * (int64_t)t.d + t.d;
+  return t.es ? t.V + vr * (int64_t)t.d : t.V + vr * 2 * (int64_t)t.d + t.d;
+}
+
+// the V row InitV gives a key: the q-th new row of this Update in the split layout (rows are
+// allocated in key order), the key's own slot with fat slots
+__host__ __device__ inline int64_t initv_row(const Table& t, uint64_t n_vrows, int64_t q,
+                                             uint32_t slot) {
+  return t.es ? (int64_t)slot : (int64_t)n_vrows + q;
+}
+
+// fat slot stride for V_dim d (0: the split layout): the entry and V in 64 or 128 bytes
+__host__ __device__ inline int fat_es(int d) {
+  if (d < 4 || d % 4 != 0 || 32 + 4 * d > 128) return 0;
+  return 32 + 4 * d <= 64 ? 1 : 2;
 }
 
 __device__ inline float4 ent_state(const Entry* e) {
@@ -171,7 +193,7 @@ __device__ inline int64_t tbl_find(const Table& t, uint64_t k) {
   if (k == kEmptyKey) return -1;  // the reserved key is never stored
   uint64_t h = tbl_hash(k, t);
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-    uint64_t kk = t.ent[h].key;
+    uint64_t kk = ent_at(t, h)->key;
     if (kk == k) return (int64_t)h;
     if (kk == kEmptyKey) return -1;
     h = (h + 1) & t.mask;
@@ -189,10 +211,10 @@ __device__ inline int64_t tbl_insert(const Table& t, uint64_t k, bool* inserted)
   if (k == kEmptyKey) return -2;
   uint64_t h = tbl_hash(k, t);
   for (uint64_t probe = 0; probe <= t.mask; ++probe) {
-    uint64_t kk = t.ent[h].key;
+    uint64_t kk = ent_at(t, h)->key;
     if (kk == k) return (int64_t)h;
     if (kk == kEmptyKey) {
-      unsigned long long old = atomicCAS(&t.ent[h].key, (unsigned long long)kEmptyKey,
+      unsigned long long old = atomicCAS(&ent_at(t, h)->key, (unsigned long long)kEmptyKey,
                                          (unsigned long long)k);
       if (old == kEmptyKey) {
         *inserted = true;

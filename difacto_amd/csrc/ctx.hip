@@ -59,6 +59,9 @@ struct Kw {
   int auc_radix = 1;    // auc_sort=merge: the AUC lane's tile sorts + merge rounds
   int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
   int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
+  // slot_layout=auto (default): fat slots (entry + V in one 64/128-byte slot, common.h Table)
+  // when V_dim allows them (4 <= d <= 24, d % 4 == 0), else the split layout; split | fat force
+  int slot_layout = -1;
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -108,6 +111,12 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
         return DFX_ERR_ARG;
       }
     }
+    else if (k == "slot_layout") {
+      if (v == "auto") kw->slot_layout = -1;
+      else if (v == "split") kw->slot_layout = 0;
+      else if (v == "fat") kw->slot_layout = 1;
+      else { set_error("unknown slot_layout: " + v + " (auto|split|fat)"); return DFX_ERR_ARG; }
+    }
     else if (k == "auc_sort") {
       if (v == "radix") kw->auc_radix = 1;
       else if (v == "merge") kw->auc_radix = 0;
@@ -134,6 +143,10 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     return DFX_ERR_ARG;
   }
   if (!kw->loss_fm) kw->P.V_dim = 0;  // LogitLoss ignores V (logit_loss.h)
+  if (kw->slot_layout == 1 && fat_es(kw->P.V_dim) == 0) {
+    set_error("slot_layout=fat needs 4 <= V_dim <= 24 with V_dim % 4 == 0");
+    return DFX_ERR_ARG;
+  }
   return DFX_OK;
 }
 
@@ -209,6 +222,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->auc_radix = kw.auc_radix != 0;
   c->sort_items = kw.sort_items;
   c->sort_lookback = kw.sort_lookback;
+  c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

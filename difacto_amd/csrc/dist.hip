@@ -150,10 +150,10 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
     // the home entry's {w, vrow} and key in one trip (w / vrow of a slot are not written in
     // this kernel, and a fresh slot already holds the zero state)
     const uint64_t hh = tbl_hash(k, T);
-    wr = *reinterpret_cast<const int2*>(&T.ent[hh]);
+    wr = *reinterpret_cast<const int2*>(ent_at(T, hh));
     bool inserted = false;
     int64_t s = (int64_t)hh;
-    if (T.ent[hh].key == k) {
+    if (ent_at(T, hh)->key == k) {
       found = 1;
     } else {
       s = tbl_insert(T, k, &inserted);
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kDNT) void k_dist_segs_pull(
   if (i < R) {
     const int d = T.d, nc = d >> 2;
     if (!found)  // {w, vrow}; a key that could not be inserted reads as absent
-      wr = slot == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(&T.ent[slot]);
+      wr = slot == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent_at(T, slot));
     const float w = __int_as_float(wr.x);
     const int vr = wr.y;
     const bool live = vr >= 0 && !(Pp.l1_shrk && w == 0.f);
@@ -202,7 +202,7 @@ __global__ void k_dist_feacnt(const uint32_t* segstart, const uint32_t* segslot,
     frank[u] = 0;
     return;
   }
-  Entry* e = &T.ent[segslot[u]];
+  Entry* e = ent_at(T, segslot[u]);
   float4 st = ent_state(e);  // {w, sqrt_g, z, fea_cnt}
   bool has_v = e->vrow >= 0;
   uint32_t f = 0, fr = 0;
@@ -236,7 +236,7 @@ __global__ void k_dist_push(const uint32_t* segstart, const uint32_t* segslot,
   } else if (u < (int64_t)*nuniq) {
     const int d = T.d;
     const int64_t S = rec_floats(d);
-    Entry* en = &T.ent[segslot[u]];
+    Entry* en = ent_at(T, segslot[u]);
     float4 e = ent_state(en);
     const int vr = en->vrow;
     bool has_v = vr >= 0;
@@ -299,7 +299,7 @@ __global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uin
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < F;
        q += (int64_t)gridDim.x * blockDim.x) {
     uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)q);
-    const int64_t vr = (int64_t)ds->n_vrows + q;
+    const int64_t vr = initv_row(T, ds->n_vrows, q, segslot[rv[q]]);
     if (vr >= T.vcap) {
       atomicOr(&ds->err, kErrPoolFull);
       continue;
@@ -310,7 +310,7 @@ __global__ void k_dist_initv(const uint32_t* rv0, const uint32_t* rv1, const uin
       V[k] = initv_value(rand_r_dev(&s), scale);
       C[k] = 0.f;
     }
-    T.ent[segslot[rv[q]]].vrow = (int32_t)vr;
+    ent_at(T, segslot[rv[q]])->vrow = (int32_t)vr;
   }
 }
 
@@ -330,8 +330,8 @@ __global__ void k_dist_pull(int64_t R, const uint32_t* seg_of, const uint32_t* s
   if (i >= R) return;
   const int d = T.d;
   const uint32_t sl = segslot[seg_of[i]];
-  const float w = sl == kNoSlot ? 0.f : T.ent[sl].w;
-  const int vr = sl == kNoSlot ? -1 : T.ent[sl].vrow;
+  const float w = sl == kNoSlot ? 0.f : ent_at(T, sl)->w;
+  const int vr = sl == kNoSlot ? -1 : ent_at(T, sl)->vrow;
   const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
   float* o = out + i * rec_floats(d);
   const float* V = live ? row_V(T, vr) : nullptr;
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kDNT) void k_dist_pull_vec(int64_t R, const uint32_
   const int d = T.d, nc = d >> 2;
   const uint32_t sl = segslot[seg_of[i]];
   const int2 wr = sl == kNoSlot ? make_int2(0, -1)
-                                : *reinterpret_cast<const int2*>(&T.ent[sl]);  // {w, vrow}
+                                : *reinterpret_cast<const int2*>(ent_at(T, sl));  // {w, vrow}
   const float w = __int_as_float(wr.x);
   const int vr = wr.y;
   const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_vec(const uint32_t* __restri
     // level 1
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
     // level 2
-    Entry* en = &T.ent[sl];
+    Entry* en = ent_at(T, sl);
     const float4 h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
     const float fc = en->fea_cnt;
     const uint32_t src0 = sorted_idx[s0];
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(kDNT) void k_dist_push_sum_vec(
     const int d = T.d, nc = d >> 2;
     const int64_t S = rec_floats(d);
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
-    Entry* en = &T.ent[sl];
+    Entry* en = ent_at(T, sl);
     const float4 h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
     const float fc = en->fea_cnt;
     const uint32_t src0 = sorted_idx[s0];
@@ -552,7 +552,7 @@ __global__ void k_dist_push_sum(const uint32_t* segstart, const uint32_t* segslo
   } else if (u < (int64_t)*nuniq) {
     const int d = T.d;
     const int64_t S = rec_floats(d);
-    Entry* en = &T.ent[segslot[u]];
+    Entry* en = ent_at(T, segslot[u]);
     float4 e = ent_state(en);
     const int vr = en->vrow;
     const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
@@ -606,7 +606,7 @@ __global__ void k_dist_initv_sum(const uint32_t* excl, const uint32_t* ftotal,
     const uint32_t nx = (u + 1 < n) ? excl[u + 1] : F;
     if (nx == e) continue;
     uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
-    const int64_t vr = (int64_t)ds->n_vrows + e;
+    const int64_t vr = initv_row(T, ds->n_vrows, e, segslot[u]);
     if (vr >= T.vcap) continue;  // kErrPoolFull is set by the finalize
     float* V = row_V(T, vr);
     float* C = row_C(T, vr);
@@ -614,7 +614,7 @@ __global__ void k_dist_initv_sum(const uint32_t* excl, const uint32_t* ftotal,
       V[k] = initv_value(rand_r_dev(&s), scale);
       C[k] = 0.f;
     }
-    T.ent[segslot[u]].vrow = (int32_t)vr;
+    ent_at(T, segslot[u])->vrow = (int32_t)vr;
   }
 }
 

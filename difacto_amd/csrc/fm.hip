@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
         uint64_t ek[UNR];
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
-          const Entry* e = a.T.ent + hs[t];
+          const Entry* e = ent_at(a.T, hs[t]);
           wr[t] = *reinterpret_cast<const int2*>(e);
           ek[t] = e->key;
         }
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           for (uint64_t probe = 0; ek[t] != key[t] && ek[t] != kEmptyKey && probe < a.T.mask;
                ++probe) {
             h = (h + 1) & a.T.mask;
-            const Entry* e = a.T.ent + h;
+            const Entry* e = ent_at(a.T, h);
             ek[t] = e->key;
             wr[t] = *reinterpret_cast<const int2*>(e);
           }
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
           } else if (a.wv_rank) {
             wr[t] = a.wv_rank[c[t]];
           } else if (!a.wv) {
-            wr[t] = *reinterpret_cast<const int2*>(a.T.ent + c[t]);
+            wr[t] = *reinterpret_cast<const int2*>(ent_at(a.T, c[t]));
           }
           w[t] = __int_as_float(wr[t].x);
           const int vr = wr[t].y;
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
       uint64_t ek[MA];
 #pragma unroll
       for (int m = 0; m < MA; ++m) {
-        const Entry* e = a.T.ent + hs[m];
+        const Entry* e = ent_at(a.T, hs[m]);
         wr[m] = *reinterpret_cast<const int2*>(e);
         ek[m] = e->key;
       }
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
         for (uint64_t probe = 0; ek[m] != key[m] && ek[m] != kEmptyKey && probe < a.T.mask;
              ++probe) {  // the (rare) longer probe chains
           h = (h + 1) & a.T.mask;
-          const Entry* e = a.T.ent + h;
+          const Entry* e = ent_at(a.T, h);
           ek[m] = e->key;
           wr[m] = *reinterpret_cast<const int2*>(e);
         }
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         const uint64_t hh = tbl_hash(key, a.T);
         // the whole home entry in two 16-byte loads issued together: {w, vrow, sqrt_g, z} and
         // {fea_cnt, pad, key}; a key found at home (the common case) needs no second trip
-        const float4* eh = reinterpret_cast<const float4*>(a.T.ent + hh);
+        const float4* eh = reinterpret_cast<const float4*>(ent_at(a.T, hh));
         const float4 h0 = eh[0], h1 = eh[1];
         const uint64_t ek =
             ((uint64_t)__float_as_uint(h1.w) << 32) | (uint64_t)__float_as_uint(h1.z);
@@ -594,7 +594,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         h = make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
         fc = 0.f;
       } else if (!home) {
-        const Entry* en = a.T.ent + sl;
+        const Entry* en = ent_at(a.T, sl);
         h = *reinterpret_cast<const float4*>(en);  // w, vrow, sqrt_g, z
         fc = en->fea_cnt;
       }
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur);
       }
       if (l == 0) {
-        if (!dead) ent_store_hot(a.T.ent + sl, e, vrow);
+        if (!dead) ent_store_hot(ent_at(a.T, sl), e, vrow);
         dnew = dead ? 0 : dw;
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
         const bool need =

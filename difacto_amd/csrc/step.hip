@@ -122,8 +122,8 @@ __global__ __launch_bounds__(kProbeNT) void k_probe_keys(const uint64_t* __restr
   for (int v = 0; v < kProbeUnr; ++v) {
     const int64_t u = ub + (int64_t)v * kProbeNT;
     if (u < n) {
-      kk[v] = T.ent[h[v]].key;
-      wr[v] = *reinterpret_cast<const int2*>(T.ent + h[v]);
+      kk[v] = ent_at(T, h[v])->key;
+      wr[v] = *reinterpret_cast<const int2*>(ent_at(T, h[v]));
     }
   }
 #pragma unroll
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kProbeNT) void k_probe_keys(const uint64_t* __restr
         atomicOr(&ds->err, insert_error(s));
         wr[v] = make_int2(0, -1);
       } else {
-        wr[v] = *reinterpret_cast<const int2*>(T.ent + s);
+        wr[v] = *reinterpret_cast<const int2*>(ent_at(T, s));
       }
     }
     segslot[u] = s < 0 ? kNoSlot : (uint32_t)s;
@@ -168,12 +168,12 @@ int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uni
 
 // the pull after a count push: {w, vrow} of each unique key by slot
 __global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ segslot,
-                                                   const DevState* nds, const Entry* ent,
+                                                   const DevState* nds, Table T,
                                                    int2* __restrict__ pulled) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= (int64_t)nds->u_count) return;
   const uint32_t s = segslot[u];
-  pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent + s);
+  pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent_at(T, s));
 }
 
 __global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B,
@@ -274,7 +274,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total, bds));
     if (!c->fwd_probe)
       hipLaunchKernelGGL(k_pull_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
-                         c->stream, segslot, bds, c->T.ent, pulled);
+                         c->stream, segslot, bds, c->T, pulled);
   }
   prof_mark(c, 3);
 

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
     if (nx == e) continue;
     const int d = T.d;
     uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
-    const int64_t vr = (int64_t)ds->n_vrows + e;
+    const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
     if (vr >= T.vcap) {
       atomicOr(&ds->err, kErrPoolFull);
       continue;
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
       V[k] = initv_value(rand_r_dev(&s), scale);
       C[k] = 0.f;
     }
-    T.ent[slot[u]].vrow = (int32_t)vr;
+    ent_at(T, slot[u])->vrow = (int32_t)vr;
   }
 }
 
@@ -102,7 +102,7 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
 
 // ---- Update(kFeaCount) (sgd_updater.cc:64-75) ---------------------------------------------
 __device__ inline uint32_t feacnt_apply(const Table& T, const Params& P, int64_t s, float c) {
-  Entry* e = &T.ent[s];
+  Entry* e = ent_at(T, s);
   float4 st = ent_state(e);
   st.w += c;  // fea_cnt
   ent_set_state(e, st);
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kStNT) void k_pull_lens(int64_t n, const uint64_t* 
   int64_t s = tbl_find(T, keys[i]);
   int vr = -1;
   float w = 0.f;
-  if (s >= 0) { w = T.ent[s].w; vr = T.ent[s].vrow; }
+  if (s >= 0) { w = ent_at(T, s)->w; vr = ent_at(T, s)->vrow; }
   bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
   slot_out[i] = (int32_t)s;
   len_out[i] = live ? (uint32_t)(T.d + 1) : 1u;
@@ -189,8 +189,8 @@ __global__ __launch_bounds__(kStNT) void k_pull_write(int64_t n, Table T, Params
   if (i >= n) return;
   const int32_t s = slot_in[i];
   const uint32_t o = off[i];
-  const float w = s >= 0 ? T.ent[s].w : 0.f;
-  const int vr = s >= 0 ? T.ent[s].vrow : -1;
+  const float w = s >= 0 ? ent_at(T, s)->w : 0.f;
+  const int vr = s >= 0 ? ent_at(T, s)->vrow : -1;
   const bool live = vr >= 0 && !(P.l1_shrk && w == 0.f);
   vals[o] = w;
   const int d = T.d;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kStNT) void k_push_grad(int64_t n, const uint64_t* 
     } else {
       const int d = T.d;
       const uint32_t o = lens ? off[i] : (uint32_t)i;
-      Entry* en = &T.ent[s];
+      Entry* en = ent_at(T, s);
       float4 e = ent_state(en);
       bool tr;
       dnew = ftrl_update(P, vals[o], &e, &tr);
@@ -256,7 +256,7 @@ __global__ void k_lens_u32(int64_t n, const int32_t* lens, uint32_t* out) {
 }
 
 // ---- table allocation / growth ------------------------------------------------------------
-__global__ void k_tbl_init(Entry* ent, int64_t cap) {
+__global__ void k_tbl_init(Table T, int64_t cap) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   Entry e;
@@ -264,23 +264,41 @@ __global__ void k_tbl_init(Entry* ent, int64_t cap) {
   e.key = kEmptyKey;
   e.vrow = -1;
   e.pad = 0;
-  ent[i] = e;
+  *ent_at(T, i) = e;
 }
 
-__global__ void k_rehash(const Entry* old, int64_t ocap, Table T, DevState* ds) {
+// re-insert every key of table O into T; with fat slots a key's V and Vaux rows move with it
+// (its vrow is its slot)
+__global__ void k_rehash(Table O, int64_t ocap, Table T, DevState* ds) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ocap) return;
-  const Entry e = old[i];
+  Entry e = *ent_at(O, i);
   if (e.key == kEmptyKey) return;
   bool ins;
   int64_t s = tbl_insert(T, e.key, &ins);
   if (s < 0) { atomicOr(&ds->err, kErrTableFull); return; }
-  T.ent[s] = e;
+  if (T.es && e.vrow >= 0) {
+    const float* V0 = row_V(O, e.vrow);
+    const float* C0 = row_C(O, e.vrow);
+    float* V1 = row_V(T, s);
+    float* C1 = row_C(T, s);
+    for (int k = 0; k < T.d; ++k) {
+      V1[k] = V0[k];
+      C1[k] = C0[k];
+    }
+    e.vrow = (int32_t)s;
+  }
+  *ent_at(T, s) = e;
 }
 
+// slots (and, with fat slots, the Vaux pool: one row per slot) for capacity cap
 static int table_alloc_entries(Table* T, int64_t cap, hipStream_t st) {
-  DFX_HIP(hipMalloc(&T->ent, cap * sizeof(Entry)));
-  hipLaunchKernelGGL(k_tbl_init, dim3((cap + 255) / 256), dim3(256), 0, st, T->ent, cap);
+  DFX_HIP(hipMalloc(&T->ent, cap * (sizeof(Entry) << T->es)));
+  if (T->es) {
+    DFX_HIP(hipMalloc(&T->V, cap * (int64_t)T->d * sizeof(float)));
+    T->vcap = cap;
+  }
+  hipLaunchKernelGGL(k_tbl_init, dim3((cap + 255) / 256), dim3(256), 0, st, *T, cap);
   DFX_HIP(hipGetLastError());
   int lg = 0;
   while ((1ll << lg) < cap) ++lg;
@@ -298,18 +316,20 @@ static int table_rebuild(Context* c, Table NT, int64_t new_cap) {
   int err0 = 0, err1 = 0;
   DFX_HIP(hipMemcpyAsync(&err0, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
-  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T.ent,
+  hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T,
                      c->cap, NT, c->ds);
   DFX_HIP(hipGetLastError());
   DFX_HIP(hipMemcpyAsync(&err1, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   if ((err1 & ~err0) & kErrTableFull) {
     (void)hipFree(NT.ent);
+    if (NT.es) (void)hipFree(NT.V);
     DFX_HIP(hipMemcpy(&c->ds->err, &err0, sizeof(int), hipMemcpyHostToDevice));
     set_error("table rebuild: the new table cannot hold every key; the old table is kept");
     return DFX_ERR_CAPACITY;
   }
   (void)hipFree(T.ent);
+  if (T.es) (void)hipFree(T.V);
   T = NT;
   c->cap = new_cap;
   return DFX_OK;
@@ -355,9 +375,11 @@ int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
   while (cap < 2 * n_keys) cap <<= 1;
   Table& T = c->T;
   T.d = c->P.V_dim;
+  T.es = c->slot_es;
   DFX_TRY(table_alloc_entries(&T, cap, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   c->cap = cap;
+  if (T.es) return DFX_OK;  // the Vaux pool came with the slots
   T.vcap = T.d > 0 ? (n_vrows > 0 ? n_vrows : 1) : 0;
   if (T.d > 0) DFX_HIP(hipMalloc(&T.V, T.vcap * 2 * T.d * sizeof(float)));
   return DFX_OK;
@@ -396,7 +418,7 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows) {
     while (cap < 2 * n_keys) cap <<= 1;
     DFX_TRY(table_rebuild(c, T, cap));
   }
-  if (T.d > 0 && n_vrows > T.vcap) {
+  if (T.d > 0 && !T.es && n_vrows > T.vcap) {  // fat slots: V grows with the slots
     HostCounters h;
     DFX_TRY(read_counters(c, &h));
     float* nV;
@@ -520,8 +542,10 @@ int store_maybe_grow(Context* c) {
 
 // load: host-parsed entries uploaded and inserted (SGDEntry::LoadEntry keeps fea_cnt, and
 // keeps sqrt_g/z when the file has no aux data)
+// vr: the entry's V row in the split layout (uploaded to the pool beforehand), or with fat
+// slots its row of VV ([V | Vaux] per loaded V row, vr - vbase), copied into the slot here
 __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const int32_t* vr,
-                       int has_aux, Table T, DevState* ds) {
+                       int has_aux, Table T, DevState* ds, const float* VV, int64_t vbase) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int ins = 0;
   if (i < n) {
@@ -531,12 +555,23 @@ __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const 
     if (s < 0) {
       atomicOr(&ds->err, insert_error(s));
     } else {
-      Entry* en = &T.ent[s];
+      Entry* en = ent_at(T, s);
       float4 e = ent_state(en);
       e.x = st[i].x;
       if (has_aux) { e.y = st[i].y; e.z = st[i].z; }
       ent_set_state(en, e);
-      if (vr[i] >= 0) en->vrow = vr[i];
+      if (vr[i] >= 0 && T.es) {
+        const float* src = VV + (vr[i] - vbase) * 2 * (int64_t)T.d;
+        float* V = row_V(T, s);
+        float* C = row_C(T, s);
+        for (int k = 0; k < T.d; ++k) {
+          V[k] = src[k];
+          C[k] = src[T.d + k];
+        }
+        en->vrow = (int32_t)s;
+      } else if (vr[i] >= 0) {
+        en->vrow = vr[i];
+      }
     }
   }
   block_count_add(ins, &ds->n_keys);
@@ -545,11 +580,11 @@ __global__ void k_load(int64_t n, const uint64_t* keys, const float4* st, const 
 __global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double objv = 0, nnz = 0;
-  if (i < cap && T.ent[i].key != kEmptyKey) {
-    const float w = T.ent[i].w;
+  if (i < cap && ent_at(T, i)->key != kEmptyKey) {
+    const float w = ent_at(T, i)->w;
     if (w != 0.f) nnz += 1;
     objv += P.l1 * fabs(w) + .5 * P.l2 * w * w;
-    const int vr = T.ent[i].vrow;
+    const int vr = ent_at(T, i)->vrow;
     if (vr >= 0) {
       nnz += T.d;
       const float* V = row_V(T, vr);
@@ -570,8 +605,8 @@ __global__ void k_penalty(Table T, int64_t cap, Params P, double* acc) {
 __global__ void k_probe_stats(Table T, int64_t cap, unsigned long long* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long dist = 0, occ = 0, mx = 0;
-  if (i < cap && T.ent[i].key != kEmptyKey) {
-    const uint64_t h = tbl_hash(T.ent[i].key, T);
+  if (i < cap && ent_at(T, i)->key != kEmptyKey) {
+    const uint64_t h = tbl_hash(ent_at(T, i)->key, T);
     dist = ((uint64_t)i - h) & T.mask;
     occ = 1;
     mx = dist;
@@ -590,12 +625,19 @@ __global__ void k_probe_stats(Table T, int64_t cap, unsigned long long* out) {
 }
 
 // host copy of the table for save / dump
+// host copy of the table for save / dump: entries (one per slot), and [V | Vaux] by V row
 struct HostTable {
   std::vector<Entry> ent;
-  std::vector<float> VV;  // n_vrows rows of [V(d) | Vaux(d)]
-  int d = 0;
-  const float* V(int vr) const { return VV.data() + (size_t)vr * 2 * d; }
-  const float* C(int vr) const { return VV.data() + (size_t)vr * 2 * d + d; }
+  std::vector<float> VV;  // split: n_vrows rows of [V(d) | Vaux(d)]; fat: cap rows of Vaux(d)
+  std::vector<Entry> raw;  // fat slots: the slots as stored (32 << es bytes each)
+  int d = 0, es = 0;
+  const float* V(int vr) const {
+    return es ? reinterpret_cast<const float*>(raw.data() + ((size_t)vr << es) + 1)
+              : VV.data() + (size_t)vr * 2 * d;
+  }
+  const float* C(int vr) const {
+    return es ? VV.data() + (size_t)vr * d : VV.data() + (size_t)vr * 2 * d + d;
+  }
 };
 
 static int copy_table_to_host(Context* c, HostTable* h) {
@@ -603,9 +645,17 @@ static int copy_table_to_host(Context* c, HostTable* h) {
   HostCounters hc;
   DFX_TRY(read_counters(c, &hc));
   h->d = T.d;
+  h->es = T.es;
   h->ent.resize(c->cap);
-  h->VV.resize((size_t)hc.n_vrows * 2 * T.d);
-  DFX_HIP(hipMemcpy(h->ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
+  if (T.es) {
+    h->raw.resize((size_t)c->cap << T.es);
+    h->VV.resize((size_t)c->cap * T.d);
+    DFX_HIP(hipMemcpy(h->raw.data(), T.ent, h->raw.size() * sizeof(Entry), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < c->cap; ++i) h->ent[i] = h->raw[(size_t)i << T.es];
+  } else {
+    h->VV.resize((size_t)hc.n_vrows * 2 * T.d);
+    DFX_HIP(hipMemcpy(h->ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
+  }
   if (!h->VV.empty())
     DFX_HIP(hipMemcpy(h->VV.data(), T.V, h->VV.size() * 4, hipMemcpyDeviceToHost));
   return DFX_OK;
@@ -770,7 +820,7 @@ int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has
   *found = 0;
   for (uint64_t probe = 0; probe <= T.mask; ++probe) {
     Entry e;
-    DFX_HIP(hipMemcpy(&e, T.ent + h, sizeof(Entry), hipMemcpyDeviceToHost));
+    DFX_HIP(hipMemcpy(&e, ent_at(T, h), sizeof(Entry), hipMemcpyDeviceToHost));
     if (e.key == kEmptyKey) return DFX_OK;
     if (e.key == key) {
       state[0] = e.w; state[1] = e.sqrt_g; state[2] = e.z; state[3] = e.fea_cnt;
@@ -886,17 +936,23 @@ int dfx_store_load_part(dfx_ctx* ctx, const char* path, int rank, int nranks) {
   uint64_t* dk;
   float4* dst;
   int32_t* dvr;
+  float* dVV = nullptr;
   DFX_HIP(hipMalloc(&dk, n * 8));
   DFX_HIP(hipMalloc(&dst, n * sizeof(float4)));
   DFX_HIP(hipMalloc(&dvr, n * 4));
   DFX_HIP(hipMemcpy(dk, keys.data(), n * 8, hipMemcpyHostToDevice));
   DFX_HIP(hipMemcpy(dst, st.data(), n * sizeof(float4), hipMemcpyHostToDevice));
   DFX_HIP(hipMemcpy(dvr, vr.data(), n * 4, hipMemcpyHostToDevice));
-  if (!VV.empty())
+  if (!VV.empty() && T.es) {  // fat slots: k_load copies each row into its key's slot
+    DFX_HIP(hipMalloc(&dVV, VV.size() * 4));
+    DFX_HIP(hipMemcpy(dVV, VV.data(), VV.size() * 4, hipMemcpyHostToDevice));
+  } else if (!VV.empty()) {
     DFX_HIP(hipMemcpy(row_V(T, hc.n_vrows), VV.data(), VV.size() * 4, hipMemcpyHostToDevice));
+  }
   hipLaunchKernelGGL(k_load, dim3((n + 255) / 256), dim3(256), 0, c->stream, n, dk, dst, dvr,
-                     aux ? 1 : 0, T, c->ds);
+                     aux ? 1 : 0, T, c->ds, dVV, (int64_t)hc.n_vrows);
   DFX_HIP(hipStreamSynchronize(c->stream));
+  if (dVV) (void)hipFree(dVV);
   unsigned long long nv = (unsigned long long)vnext;
   DFX_HIP(hipMemcpy(&c->ds->n_vrows, &nv, 8, hipMemcpyHostToDevice));
   // new_w = model_.size() (sgd_updater.h:91)

@@ -108,6 +108,83 @@ __global__ void bwd_fat(float4* slots, const unsigned* idx, int n) {
     p[0] = e;
   }
 }
+// fat 128 B: slot = [entry (2 float4) | V (4 float4) | pad (2)]; Vaux in a pool of 64-B rows,
+// indexed by the slot (AUXSLOT) or by the entry's vrow (a permutation: allocation order)
+template <bool AUXSLOT>
+__global__ void bwd_fat128(float4* slots, float4* aux, const unsigned* idx, int n) {
+  int g = (blockIdx.x * blockDim.x + threadIdx.x) / 4, l = threadIdx.x & 3;
+  if (g >= n) return;
+  unsigned s = idx[g];
+  float4* p = slots + (size_t)s * 8;
+  float4 e = p[0];
+  float4 v = p[2 + l];
+  float4* q = aux + (AUXSLOT ? (size_t)s : (size_t)__float_as_uint(e.y)) * 4;
+  float4 c = q[l];
+  v.x += e.x;
+  c.y += 1.f;
+  p[2 + l] = v;
+  q[l] = c;
+  if (l == 0) {
+    e.x += 1.f;
+    p[0] = e;
+  }
+}
+// fat 128 B, V first: slot = [V (4 float4) | entry (2 float4) | pad (2)] — V is one whole 64-B
+// sector; E32: the entry is written back whole (32 B) instead of its 16-B hot half
+template <bool E32>
+__global__ void bwd_fatv(float4* slots, float4* aux, const unsigned* idx, int n) {
+  int g = (blockIdx.x * blockDim.x + threadIdx.x) / 4, l = threadIdx.x & 3;
+  if (g >= n) return;
+  unsigned s = idx[g];
+  float4* p = slots + (size_t)s * 8;
+  float4 e = p[4], e1 = p[5];
+  float4 v = p[l];
+  float4* q = aux + (size_t)s * 4;
+  float4 c = q[l];
+  v.x += e.x;
+  c.y += 1.f;
+  p[l] = v;
+  q[l] = c;
+  if (l == 0) {
+    e.x += 1.f;
+    p[4] = e;
+    if (E32) p[5] = e1;
+  }
+}
+__global__ void fwd_fatv(const float4* slots, const unsigned* idx, int n, float* out) {
+  int g = (blockIdx.x * blockDim.x + threadIdx.x) / 4, l = threadIdx.x & 3;
+  if (g >= n) return;
+  unsigned s = idx[g];
+  const float4* p = slots + (size_t)s * 8;
+  const float2 wv = *reinterpret_cast<const float2*>(p + 4);
+  const float2 kk = *reinterpret_cast<const float2*>(p + 5) ;
+  float4 v = p[l];
+  float acc = wv.x + kk.y + v.x + v.y + v.z + v.w;
+  if (acc == 12345.f) out[g] = acc;
+}
+// current layout, the entry written back whole (32 B)
+__global__ void bwd_split32(float4* ent, float4* rows, const unsigned* idx, int n) {
+  int g = (blockIdx.x * blockDim.x + threadIdx.x) / 4, l = threadIdx.x & 3;
+  if (g >= n) return;
+  unsigned s = idx[g];
+  float4 e = ent[(size_t)s * 2], e1 = ent[(size_t)s * 2 + 1];
+  unsigned vr = __float_as_uint(e.y);
+  float4* p = rows + (size_t)vr * 8;
+  float4 v = p[l], c = p[4 + l];
+  v.x += 1.f;
+  c.y += 1.f;
+  p[l] = v;
+  p[4 + l] = c;
+  if (l == 0) {
+    e.x += 1.f;
+    ent[(size_t)s * 2] = e;
+    ent[(size_t)s * 2 + 1] = e1;
+  }
+}
+__global__ void init_fat128(float4* slots, const unsigned* perm, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) slots[i * 8] = make_float4(0.f, __uint_as_float(perm[i]), 0.f, 0.f);
+}
 __global__ void init_split(float4* ent, const unsigned* perm, long n) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) ent[i * 2] = make_float4(0.f, __uint_as_float(perm[i]), 0.f, 0.f);
@@ -122,6 +199,11 @@ int main() {
   CK(hipMalloc(&ent, CAP * 32));
   CK(hipMalloc(&rows, CAP * 128));
   CK(hipMalloc(&fat, CAP * 256));
+  float4 *fat128, *aux;
+  CK(hipMalloc(&fat128, CAP * 128));
+  CK(hipMalloc(&aux, CAP * 64));
+  CK(hipMemset(fat128, 0, CAP * 128));
+  CK(hipMemset(aux, 0, CAP * 64));
   CK(hipMalloc(&ifwd, nfwd * 4));
   CK(hipMalloc(&ibwd, nbwd * 4));
   CK(hipMalloc(&perm, CAP * 4));
@@ -137,6 +219,7 @@ int main() {
     CK(hipMemcpy(perm, p.data(), CAP * 4, hipMemcpyHostToDevice));
   }
   init_split<<<(CAP + 255) / 256, 256>>>(ent, perm, CAP);
+  init_fat128<<<(CAP + 255) / 256, 256>>>(fat128, perm, CAP);
   std::vector<unsigned> h(nfwd);
   for (int i = 0; i < nfwd; ++i) h[i] = (unsigned)(((long)rand() << 16 ^ rand()) % CAP);
   CK(hipMemcpy(ifwd, h.data(), nfwd * 4, hipMemcpyHostToDevice));
@@ -168,6 +251,13 @@ int main() {
   timeit("fwd fat 192 B", [&] { fwd_fat<12><<<gf, 256>>>(fat, ifwd, nfwd, out); });
   timeit("fwd fat 160 B", [&] { fwd_fat<10><<<gf, 256>>>(fat, ifwd, nfwd, out); });
   timeit("fwd fat 256 B", [&] { fwd_fat<16><<<gf, 256>>>(fat, ifwd, nfwd, out); });
+  timeit("fwd fat 128 B", [&] { fwd_fat<8><<<gf, 256>>>(fat128, ifwd, nfwd, out); });
+  timeit("bwd fat 128 B, aux by slot", [&] { bwd_fat128<true><<<gb, 256>>>(fat128, aux, ibwd, nb); });
+  timeit("bwd fat 128 B, aux by vrow", [&] { bwd_fat128<false><<<gb, 256>>>(fat128, aux, ibwd, nb); });
+  timeit("fwd fat 128 B, V first", [&] { fwd_fatv<<<gf, 256>>>(fat128, ifwd, nfwd, out); });
+  timeit("bwd fat 128 B V first, 16-B entry", [&] { bwd_fatv<false><<<gb, 256>>>(fat128, aux, ibwd, nb); });
+  timeit("bwd fat 128 B V first, 32-B entry", [&] { bwd_fatv<true><<<gb, 256>>>(fat128, aux, ibwd, nb); });
+  timeit("bwd split, 32-B entry", [&] { bwd_split32<<<gb, 256>>>(ent, rows, ibwd, nb); });
   timeit("bwd split (sorted slots)", [&] { bwd_split<<<gb, 256>>>(ent, rows, ibwd, nb); });
   timeit("bwd split, row = slot (sorted)", [&] { bwd_split_slot<<<gb, 256>>>(ent, rows, ibwd, nb); });
   timeit("bwd fat 160 B (sorted slots)", [&] { bwd_fat<10><<<gb, 256>>>(fat, ibwd, nb); });

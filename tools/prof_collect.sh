@@ -1,0 +1,29 @@
+#!/bin/bash
+# profiles/<TAG>/ from the gpurun_out/ of `tools/profile.sh TAG` (run on the GPU box): kernel
+# trace summaries of the four bench runs and the PMC JSON files bench.py reads (PMC_ROUND).
+# The sharded traces end with the bench's secondary schedules (short bulk-synchronous runs of
+# the other exchange designs): their step markers are skipped.
+set -e
+TAG=${1:?tag}
+cd "$(dirname "$0")/.."
+O=gpurun_out
+P=profiles/$TAG
+mkdir -p $P
+F=$O/pmc_${TAG}_fetch/pmc_counter_collection.csv
+W=$O/pmc_${TAG}_write/pmc_counter_collection.csv
+python3 tools/prof_summary.py $O/prof_${TAG}_fused/trace_kernel_trace.csv 20 $F $W \
+  > $P/kernel_summary_pipelined.md
+python3 tools/prof_summary.py $O/prof_${TAG}_serial/trace_kernel_trace.csv 20 $F $W \
+  > $P/kernel_summary_serial.md
+DFX_STEP_MARKER=k_split_worker_finalize DFX_STEP_SKIP=44 python3 tools/prof_summary.py \
+  $O/prof_${TAG}_split/trace_kernel_trace.csv 20 $O/pmc_${TAG}_fetch_split/pmc_counter_collection.csv \
+  $O/pmc_${TAG}_write_split/pmc_counter_collection.csv > $P/kernel_summary_split_pipelined.md
+DFX_STEP_MARKER=k_dist_worker_finalize DFX_STEP_SKIP=44 python3 tools/prof_summary.py \
+  $O/prof_${TAG}_a2a/trace_kernel_trace.csv 20 > $P/kernel_summary_a2a_pipelined.md
+python3 tools/pmc_json.py $F $W $P/pmc_hbm.json 3 $TAG
+python3 tools/pmc_json.py $O/pmc_${TAG}_fetch_split/pmc_counter_collection.csv \
+  $O/pmc_${TAG}_write_split/pmc_counter_collection.csv $P/pmc_hbm_split.json 3 $TAG
+U=$(grep -o '"mean_unique_keys": [0-9.]*' $O/pmc_${TAG}_req.log | head -1 | awk '{print $2}')
+python3 tools/pmc_requests.py $O/pmc_${TAG}_req/pmc_counter_collection.csv "$U" 3900000 \
+  $P/pmc_requests.json $TAG
+ls $P
