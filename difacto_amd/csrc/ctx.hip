@@ -62,6 +62,8 @@ struct Kw {
   // slot_layout=auto (default): fat slots (entry + V in one 64/128-byte slot, common.h Table)
   // when V_dim allows them (4 <= d <= 24, d % 4 == 0), else the split layout; split | fat force
   int slot_layout = -1;
+  int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
+  int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -111,6 +113,8 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
         return DFX_ERR_ARG;
       }
     }
+    else if (k == "fat_fwd") kw->fat_fwd = atoi(cv) != 0;
+    else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
       else if (v == "split") kw->slot_layout = 0;
@@ -223,6 +227,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->sort_items = kw.sort_items;
   c->sort_lookback = kw.sort_lookback;
   c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);
+  c->fat_fwd = kw.fat_fwd;
+  c->fat_bwd = kw.fat_bwd;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

@@ -284,8 +284,15 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 // ids, one for the entries and pipelined V trips — where the UNR loop of k_fm_fwd paid three
 // dependent trips per 8 nnz.  Sums run in exactly the same (row, nnz) order, so predictions
 // are bit-identical to k_fm_fwd's (and the reference's).
-template <int G>
-__global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
+//
+// FAT (fat slots, common.h Table::es > 0, d == 4*G): a key's entry and V share one slot, so the
+// group reads nnz t's home slot whole in ONE trip — lane l its V coordinates [4l, 4l+4), even
+// lanes {w, vrow}, odd lanes the key — for 8 nnz at a time, and checks the key afterwards (a
+// key away from home, rare at load <= 0.5, walks its chain then).  Reading the slot's two
+// halves together keeps them one DRAM access; read a chain step apart, the entry's line was
+// often evicted before its V was read (the split walk above, applied to fat slots: 185 us).
+template <int G, bool FAT>
+__device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
   constexpr int MA = CH / G;      // lookups per lane per chunk
@@ -302,7 +309,71 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
     float acc = 0.f;
     float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};
     const bool valued = a.val != nullptr;
-    for (uint64_t j0 = o0; j0 < o1; j0 += CH) {
+    if constexpr (FAT) {
+      constexpr int NB = 8;  // nnz per trip
+      for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
+        const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
+        uint64_t key[NB];
+        float xm[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const uint64_t jj = j0 + t < o1 ? j0 + t : o1 - 1;
+          const uint64_t id = a.index[jj];
+          const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+          key[t] = a.keys_ready ? id : reverse_bytes(mm);
+          xm[t] = valued ? a.val[jj] : 1.f;
+        }
+        float4 v[NB];
+        float2 eh[NB];  // even lanes {w, vrow}, odd lanes the key
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
+          eh[t] = *reinterpret_cast<const float2*>(sl + ((l & 1) ? 6 : 0));
+          v[t] = *reinterpret_cast<const float4*>(sl + 8 + 4 * l);
+        }
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
+          uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
+          float w = __shfl(eh[t].x, gbase, kWave);
+          int vr = __float_as_int(__shfl(eh[t].y, gbase, kWave));
+          float4 vv = v[t];
+          if (ek != key[t] && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
+            uint64_t h = tbl_hash(key[t], a.T);
+            for (uint64_t probe = 0; ek != key[t] && ek != kEmptyKey && probe < a.T.mask; ++probe) {
+              h = (h + 1) & a.T.mask;
+              ek = ent_at(a.T, h)->key;
+            }
+            if (ek == key[t]) {
+              const Entry* e = ent_at(a.T, h);
+              w = e->w;
+              vr = e->vrow;
+              vv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e) + 8 + 4 * l);
+            }
+          }
+          // absent (inserted by this training step's backward): w = 0, no V
+          if (ek != key[t]) { w = 0.f; vr = -1; }
+          // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
+          const bool vok = vr >= 0 && !(a.l1_shrk && w == 0.f);
+          if (t < nin) {
+            const float x = xm[t];
+            // SpMV::Times skips w == 0 (spmv.h:124-125)
+            if (w != 0.f) acc = valued ? acc + w * x : acc + w;
+            if (vok) {
+              const float xx = x * x;  // XX_ (fm_loss.h:86-92)
+              const float vk[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                xv[k] = valued ? xv[k] + vk[k] * x : xv[k] + vk[k];
+                const float q = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
+                xxvv[k] = valued ? xxvv[k] + q * xx : xxvv[k] + q;
+              }
+            }
+          }
+        }
+      }
+    }
+    for (uint64_t j0 = o0; !FAT && j0 < o1; j0 += CH) {
       // ---- the chunk's lookups, MA per lane: nnz j0 + l + G*m
       uint64_t key[MA], hs[MA];
       float xm[MA];
@@ -444,6 +515,18 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
   }
 }
 
+template <int G>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
+  fwd_probe_body<G, false>(a);
+}
+
+// 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
+template <int G>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(
+    FwdArgs a) {
+  fwd_probe_body<G, true>(a);
+}
+
 // Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
 // multiple of 4); otherwise scalar coordinates (the pulled interleaved layout is unaligned).
 void lanes_for(int d, bool vec, int* G, int* CPL, bool* use_vec) {
@@ -503,6 +586,17 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   lanes_for(a.d, true, &G, &CPL, &vec);
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
+  // fat slots: one trip per nnz (G lanes x float4 = d exactly; even / odd lanes hold the
+  // entry's halves, so G >= 2)
+  const bool fat = a.T.es != 0 && !a.no_fat_fwd && vec && CPL == 4 && 4 * G == a.d && G >= 2;
+  if (a.index && a.B > 0 && spread && fat) {
+    const dim3 grid((unsigned)*nblk);
+    if (G == 2) hipLaunchKernelGGL(k_fm_fwd_fat<2>, grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4) hipLaunchKernelGGL(k_fm_fwd_fat<4>, grid, dim3(kFmNT), 0, st, a);
+    else if (G == 8) hipLaunchKernelGGL(k_fm_fwd_fat<8>, grid, dim3(kFmNT), 0, st, a);
+    DFX_HIP(hipGetLastError());
+    if (G == 2 || G == 4 || G == 8) return DFX_OK;
+  }
   if (a.index && spread && vec && CPL == 4 && G >= 4 && G <= 32 && a.B > 0) {
     const dim3 grid((unsigned)*nblk);
 #define DFX_FWDP(GG)                                                                     \
@@ -557,6 +651,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     float fc = 0.f;
     bool home = false;  // the key's entry was read at its home slot already
     bool dead = false;  // the key has no slot (failed insert): nothing is written for it
+    bool spec = false;  // fat slots: V / Vaux of the home slot loaded beside the entry
+    float vcur[CPL], ccur[CPL];
     if (FUSED) {
       if (a.insert_keys) {
         // Get's find-or-insert (model_[key]) here instead of a separate pass: the home slot
@@ -567,6 +663,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         // {fea_cnt, pad, key}; a key found at home (the common case) needs no second trip
         const float4* eh = reinterpret_cast<const float4*>(ent_at(a.T, hh));
         const float4 h0 = eh[0], h1 = eh[1];
+        if (a.T.es && !a.no_fat_spec) {  // a key at home has V there: one trip for the key
+          load_coords<CPL, VEC>(row_V(a.T, (int64_t)hh), l, d, vcur);
+          load_coords<CPL, VEC>(row_C(a.T, (int64_t)hh), l, d, ccur);
+          spec = true;
+        }
         const uint64_t ek =
             ((uint64_t)__float_as_uint(h1.w) << 32) | (uint64_t)__float_as_uint(h1.z);
         home = ek == key;
@@ -616,15 +717,17 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
     // ---- level 3: V / Vaux (or grad / W) of the key, p and XV*p of the occurrences' rows
     float gw = 0.f;
     float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-    float vcur[CPL], ccur[CPL], g0[CPL];
+    float g0[CPL];
     const float* zp = a.zpad + ((cidx & 255u) << 4);
     if (FUSED) {
       e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
       vrow = __float_as_int(h.y);
       // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
       vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
-      load_coords<CPL, VEC>(vq >= 0 ? row_V(a.T, vq) : zp, l, d, vcur);
-      load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur);
+      if (!(spec && home && vq >= 0)) {  // (fat slots: at home, vrow == the home slot)
+        load_coords<CPL, VEC>(vq >= 0 ? row_V(a.T, vq) : zp, l, d, vcur);
+        load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur);
+      }
 #pragma unroll
       for (int k = 0; k < CPL; ++k) g0[k] = 0.f;
     } else if (a.rec_S) {

@@ -57,6 +57,7 @@ struct FwdArgs {
   // and the forward writes per row its partial [XV(d) | XXVV(d) | sum w x | 0 0 0]
   // (split_part_floats(d) floats) instead of pred / p / XV*p / loss
   int keys_ready;
+  int no_fat_fwd;  // fat slots: the split forward walk instead of the one-trip read (A/B)
   float* part;
 };
 
@@ -65,6 +66,7 @@ __host__ __device__ inline int split_part_floats(int d) { return 2 * d + 4; }
 __host__ __device__ inline int split_pxv_floats(int d) { return d + 4; }
 
 struct BwdArgs {
+  int no_fat_spec;           // fat slots: no V / Vaux loads beside the home entry (A/B)
   const uint32_t* segstart;  // nseg+1
   const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
   int64_t nseg_host;

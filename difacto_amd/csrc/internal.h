@@ -185,6 +185,8 @@ struct Context {
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
   int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
   int slot_es = 0;    // Table::es of this context's store (kwarg slot_layout)
+  int fat_fwd = 1;    // kwarg fat_fwd
+  int fat_bwd = 1;    // kwarg fat_bwd
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
   int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)

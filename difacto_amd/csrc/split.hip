@@ -391,6 +391,7 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   a.B = R; a.offs = ows.rowid.as<uint64_t>(); a.val = c->split_x[slot];
   a.index = c->split_keys[slot]; a.max_index = ~0ull; a.keys_ready = 1;
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
+  a.no_fat_fwd = !c->fat_fwd;
   a.part = part_out;
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
@@ -452,7 +453,7 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.occ_row = ows.occ_row.as<uint32_t>();
     g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d); g.d = d;
-    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P;
+    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd;
     g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
     g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();

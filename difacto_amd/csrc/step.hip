@@ -286,6 +286,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     a.col = col; a.wv_rank = pulled;
   }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
+  a.no_fat_fwd = !c->fat_fwd;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -314,7 +315,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
-    g.T = c->T; g.Pm = c->P;
+    g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd;
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
