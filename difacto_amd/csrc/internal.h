@@ -66,6 +66,8 @@ struct DevState {
   double sum_u;                // sum of U over dfx_train_step calls (roofline bytes)
   double n_steps;
   double scratch[8];
+  unsigned int iv_ticket;      // the one-launch InitV's tile tickets (reset by k_step_finalize)
+  unsigned int iv_epoch;       // its look-back words' tag (advanced by k_step_finalize)
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
@@ -86,6 +88,7 @@ struct Workspace {
   DevBuf p, pred, XVp, rowtmp;
   DevBuf ak0, ak1, av0, av1;  // AUC sort buffers (keys, labels; double-buffered)
   DevBuf dscratch;  // double partials
+  DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
   DevBuf os;
@@ -187,6 +190,7 @@ struct Context {
   int slot_es = 0;    // Table::es of this context's store (kwarg slot_layout)
   int fat_fwd = 1;    // kwarg fat_fwd
   int fat_bwd = 1;    // kwarg fat_bwd
+  int initv_onepass = 1;  // kwarg initv_onepass
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
   int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)

@@ -184,6 +184,8 @@ __global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B,
   ds->sum_u += (double)bds->u_count;
   ds->n_steps += 1;
   ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
+  ds->iv_ticket = 0u;  // the next step's one-launch InitV takes its tiles from 0 again
+  ds->iv_epoch += 1u;
   if (initv_total) {  // the InitV pass's rand_r advance and V rows (k_initv_finalize's work)
     const uint32_t n = *initv_total;
     ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * n);

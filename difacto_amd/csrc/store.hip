@@ -83,11 +83,122 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
 }
 
+// The fused step's InitV in ONE launch (it replaced the scan's three launches + k_initv: in the
+// steady state, where no key needs V, all four only found the device gate closed).  A block
+// takes the next tile of kIvTile flags by ticket, counts them, publishes the count and finds
+// its prefix by decoupled look-back over the lower tiles' tagged words (tiles start in ticket
+// order, so a block only waits on running ones), then draws its keys' V exactly as k_initv.
+// The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
+constexpr int kIvItems = 16, kIvTile = kStNT * kIvItems;
+
+__global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, uint32_t* total,
+                                                         const uint32_t* slot, Table T,
+                                                         float scale, DevState* ds,
+                                                         const DevState* nds,
+                                                         const uint32_t* gate,
+                                                         unsigned long long* status) {
+  __shared__ uint32_t lds[kStNT / kWave + 1];
+  __shared__ int64_t s_tile;
+  __shared__ uint32_t s_pre;
+  if (*gate == 0u) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0u;
+    return;
+  }
+  if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(&ds->iv_ticket, 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t n = (int64_t)nds->u_count;
+  const int64_t base = tile * kIvTile;
+  if (base >= n) return;  // every later tile exits too: no waiter is left behind
+  const uint32_t tag = ds->iv_epoch & 0x3FFFFFFFu;
+  // this thread's kIvItems consecutive flags
+  const int64_t i0 = base + (int64_t)threadIdx.x * kIvItems;
+  uint32_t f[kIvItems], cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kIvItems; ++k) {
+    f[k] = i0 + k < n ? flags[i0 + k] : 0u;
+    cnt += f[k];
+  }
+  uint32_t tot;
+  uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
+  if (threadIdx.x == 0) {
+    unsigned long long* st = status + tile;
+    uint32_t pre = 0;
+    if (tile == 0) {
+      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 2u) << 32) | tot,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 1u) << 32) | tot,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t k = tile - 1;
+      uint32_t spins = 0;
+      while (k >= 0) {
+        const unsigned long long v =
+            __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = (uint32_t)(v >> 32);
+        if ((hi >> 2) != tag || (hi & 3u) == 0) {  // not published yet
+          if (++spins > (1u << 24)) {  // a predecessor never published: give up loudly
+            atomicOr(&ds->err, kErrSort);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        pre += (uint32_t)v;
+        if ((hi & 3u) == 2u) break;
+        --k;
+      }
+      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 2u) << 32) | (pre + tot),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_pre = pre;
+    if (base + kIvTile >= n) *total = pre + tot;  // the last tile
+  }
+  __syncthreads();
+  if (cnt == 0) return;
+  uint32_t e = s_pre + ex;
+  const int d = T.d;
+#pragma unroll 1
+  for (int k = 0; k < kIvItems; ++k) {
+    if (!f[k]) continue;
+    const int64_t u = i0 + k;
+    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+    const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
+    ++e;
+    if (vr >= T.vcap) {
+      atomicOr(&ds->err, kErrPoolFull);
+      continue;
+    }
+    float* V = row_V(T, vr);
+    float* C = row_C(T, vr);
+    for (int q = 0; q < d; ++q) {
+      V[q] = initv_value(rand_r_dev(&s), scale);
+      C[q] = 0.f;
+    }
+    ent_at(T, slot[u])->vrow = (int32_t)vr;
+  }
+}
+
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
               const uint32_t* slot, const DevState* nds, const uint32_t* gate, bool finalize) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
+  if (gate && n_host < 0 && !finalize && c->initv_onepass) {  // the fused step
+    const int64_t ntiles = (n_bound + kIvTile - 1) / kIvTile;
+    Workspace& ws = c->ws;
+    void* before = ws.ivstat.p;
+    DFX_TRY(ws.ivstat.ensure((size_t)ntiles * 8));
+    if (ws.ivstat.p != before) {  // fresh words read as unpublished (tag 0, flag 0)
+      DFX_HIP(hipMemset(ws.ivstat.p, 0, ws.ivstat.bytes));
+      DFX_HIP(hipStreamSynchronize(nullptr));
+    }
+    hipLaunchKernelGGL(k_initv_onepass, dim3((unsigned)ntiles), dim3(kStNT), 0, c->stream, flags,
+                       total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate,
+                       ws.ivstat.as<unsigned long long>());
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
+  }
   DFX_TRY(scan_u32(c, flags, n_bound, total_dev, n_host >= 0 ? nullptr : &nds->u_count, gate));
   const int64_t nb = (n_bound + kStNT - 1) / kStNT;
   hipLaunchKernelGGL(k_initv, dim3((unsigned)(gate && nb > 1024 ? 1024 : nb)), dim3(kStNT), 0,

@@ -79,8 +79,14 @@ typedef struct dfx_progress {
  * kwargs: the reference .conf keys, "k=v" separated by ',', ';', ' ' or newlines:
  *   loss (fm|logit), V_dim, lr, lr_beta, l1, l2, V_lr, V_lr_beta, V_l2, V_init_scale,
  *   V_threshold, l1_shrk, seed          (sgd_param.h:79-123, fm_loss.h:19-27)
- * plus device-store sizing: max_keys (hash table keys, default 1<<22), max_vrows
- * (V pool rows, default max_keys).  Unknown keys are ignored (InitAllowUnknown). */
+ * plus device-store sizing: max_keys (hash table keys, default 1<<22; the table grows by
+ * itself at sync points, autogrow=0 turns that off), max_vrows (V pool rows of the split
+ * layout, default max_keys); the store's slot layout: slot_layout=auto|split|fat (auto: a key's
+ * entry and V share one 64/128-byte slot when 4 <= V_dim <= 24 and V_dim % 4 == 0); the
+ * sharded store's push_agg=sum|ranks and hash=ordered|mixed; and execution choices that do
+ * not change results (A/B switches, measured in DESIGN.md): fwd_probe, xvp_row, bwd_lds,
+ * sort_pack, sort_items, sort_lookback, auc_sort=radix|merge, fat_fwd, fat_bwd,
+ * initv_onepass.  Unknown keys are ignored (InitAllowUnknown). */
 const char* dfx_last_error(void);
 int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out);
 int dfx_ctx_destroy(dfx_ctx* ctx);
