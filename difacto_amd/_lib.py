@@ -104,7 +104,7 @@ _SIGS = {
     "dfx_dist_union": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]),
     "dfx_dist_union_rows": (ctypes.c_int, [vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int,
                                            ctypes.c_int64, ctypes.c_int, ctypes.c_int, vp, vp]),
-    "dfx_split_part_floats": (ctypes.c_int, [vp]),
+    "dfx_split_part_floats": (ctypes.c_int, [vp, ctypes.c_int]),
     "dfx_split_pxv_floats": (ctypes.c_int, [vp]),
     "dfx_split_partition": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), c_u64,
                                            ctypes.c_int, vp, vp, vp]),

@@ -206,15 +206,33 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
     if (PROBE && a.part) {
       // owner-computes split: this owner's share of the row; the worker sums the owners'
       // shares and finishes the row (split.hip k_split_combine)
-      const int PS = split_part_floats(d);
+      const int PS = split_part_floats(d, a.part_n);
       float* pr_row = a.part + r * PS;
-      if (d > 0) {
-        store_coords<CPL, VEC>(pr_row, l, d, xv);
-        store_coords<CPL, VEC>(pr_row + d, l, d, xxvv);
-      }
-      if (l == 0) {
-        pr_row[2 * d] = acc;
-        pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+      if (a.part_n > 1) {  // [XV | sum w x | sum_l XXVV_l (serial over l) | 0 0]
+        float sx = 0.f;
+        const int gbase = (threadIdx.x % kWave) - l;
+        for (int q = 0; q < G; ++q) {
+#pragma unroll
+          for (int k = 0; k < CPL; ++k) {
+            const float tk = __shfl(xxvv[k], gbase + q, kWave);
+            if (q * CPL + k < d) sx += tk;
+          }
+        }
+        if (d > 0) store_coords<CPL, VEC>(pr_row, l, d, xv);
+        if (l == 0) {
+          pr_row[d] = acc;
+          pr_row[d + 1] = sx;
+          pr_row[d + 2] = pr_row[d + 3] = 0.f;
+        }
+      } else {
+        if (d > 0) {
+          store_coords<CPL, VEC>(pr_row, l, d, xv);
+          store_coords<CPL, VEC>(pr_row + d, l, d, xxvv);
+        }
+        if (l == 0) {
+          pr_row[2 * d] = acc;
+          pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+        }
       }
     } else if (MODE != kGradPrep && d > 0) {
       // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
@@ -455,15 +473,33 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
     }
     if (a.part) {
       // owner-computes split: this owner's share of the row (split.hip k_split_combine)
-      float* pr_row = a.part + r * split_part_floats(d);
-      if (l * 4 < d) {
-        *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-        *reinterpret_cast<float4*>(pr_row + d + l * 4) =
-            make_float4(xxvv[0], xxvv[1], xxvv[2], xxvv[3]);
-      }
-      if (l == 0) {
-        pr_row[2 * d] = acc;
-        pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+      float* pr_row = a.part + r * split_part_floats(d, a.part_n);
+      if (a.part_n > 1) {  // [XV | sum w x | sum_l XXVV_l (serial over l) | 0 0]
+        float sx = 0.f;
+        for (int q = 0; q < G; ++q) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float tk = __shfl(xxvv[k], gbase + q, kWave);
+            if (q * 4 + k < d) sx += tk;
+          }
+        }
+        if (l * 4 < d)
+          *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+        if (l == 0) {
+          pr_row[d] = acc;
+          pr_row[d + 1] = sx;
+          pr_row[d + 2] = pr_row[d + 3] = 0.f;
+        }
+      } else {
+        if (l * 4 < d) {
+          *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+          *reinterpret_cast<float4*>(pr_row + d + l * 4) =
+              make_float4(xxvv[0], xxvv[1], xxvv[2], xxvv[3]);
+        }
+        if (l == 0) {
+          pr_row[2 * d] = acc;
+          pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+        }
       }
     }
     float pr = acc;

@@ -57,12 +57,17 @@ struct FwdArgs {
   // and the forward writes per row its partial [XV(d) | XXVV(d) | sum w x | 0 0 0]
   // (split_part_floats(d) floats) instead of pred / p / XV*p / loss
   int keys_ready;
+  int part_n;      // owners of the split step (the partial's layout, split_part_floats)
   int no_fat_fwd;  // fat slots: the split forward walk instead of the one-trip read (A/B)
   float* part;
 };
 
 // the owner-computes split's per-row forward partial and its per-row [XV*p | p] record
-__host__ __device__ inline int split_part_floats(int d) { return 2 * d + 4; }
+// the owner's partial per row: one owner (N = 1) [XV(d) | XXVV(d) | sum w x | 0 0 0], so the
+// worker finishes the row exactly as the fused forward; N > 1 owners [XV(d) | sum w x |
+// sum_l XXVV_l | 0 0] (d + 4 floats: the partial exchange is ~half as large, and the regrouped
+// sums are within the tolerance either way)
+__host__ __device__ inline int split_part_floats(int d, int n) { return n > 1 ? d + 4 : 2 * d + 4; }
 __host__ __device__ inline int split_pxv_floats(int d) { return d + 4; }
 
 struct BwdArgs {

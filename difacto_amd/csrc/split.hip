@@ -160,13 +160,27 @@ __global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, i
                                                          uint32_t* auc_lab) {
   __shared__ double red[kSpNT / kWave];
   const int64_t r = (int64_t)blockIdx.x * kSpNT + threadIdx.x;
-  const int PS = split_part_floats(d), PX = split_pxv_floats(d);
+  const int PS = split_part_floats(d, n), PX = split_pxv_floats(d);
+  const bool compact = n > 1;  // [XV | sum w x | sum_l XXVV_l | 0 0] per owner
   double loss = 0;
   if (r < B) {
     float acc = 0.f;
-    for (int o = 0; o < n; ++o) acc += parts[((int64_t)o * M + r) * PS + 2 * d];
+    for (int o = 0; o < n; ++o) acc += parts[((int64_t)o * M + r) * PS + (compact ? d : 2 * d)];
     float pr = acc;
-    if (d > 0) {
+    if (d > 0 && compact) {
+      // s = sum_l XV_l^2 - sum_owners sum_l XXVV_l (the owners' serial sums, in rank order)
+      float s = 0.f, xx = 0.f;
+      for (int l = 0; l < d; ++l) {
+        float xv = 0.f;
+        for (int o = 0; o < n; ++o) xv += parts[((int64_t)o * M + r) * PS + l];
+        s += xv * xv;
+      }
+      for (int o = 0; o < n; ++o) xx += parts[((int64_t)o * M + r) * PS + d + 1];
+      s -= xx;
+      const double y = (double)acc + .5 * (double)s;
+      pr = (float)y;
+      pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);
+    } else if (d > 0) {
       float s = 0.f;
       for (int l = 0; l < d; ++l) {
         float xv = 0.f, xx = 0.f;
@@ -231,8 +245,8 @@ extern "C" {
 
 #define DFX_SPLIT_SLOT(slot) DFX_CHECK_ARG((slot) == 0 || (slot) == 1, "split: slot must be 0 or 1")
 
-int dfx_split_part_floats(dfx_ctx* ctx) {
-  return ctx ? split_part_floats(ctx->c.P.V_dim) : -1;
+int dfx_split_part_floats(dfx_ctx* ctx, int nranks) {
+  return ctx && nranks >= 1 ? split_part_floats(ctx->c.P.V_dim, nranks) : -1;
 }
 
 int dfx_split_pxv_floats(dfx_ctx* ctx) { return ctx ? split_pxv_floats(ctx->c.P.V_dim) : -1; }
@@ -405,6 +419,7 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
   a.no_fat_fwd = !c->fat_fwd;
   a.part = part_out;
+  a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
   // a step without a backward is done with the slot (and the table) here

@@ -206,7 +206,7 @@ class Shard:
 
     def split_owner_forward(self, slot=0):
         R = self._split_R[slot]
-        PS = _lib.lib().dfx_split_part_floats(self.ctx.h)
+        PS = _lib.lib().dfx_split_part_floats(self.ctx.h, self.nranks)
         part = torch.empty(max(R * PS, 1), dtype=torch.float32, device=self.ctx.device)
         check(_lib.lib().dfx_split_owner_forward(self.ctx.h, slot, _p(part)))
         return part[:R * PS]
@@ -782,7 +782,7 @@ def split_step(shards, dblks, comm, job_type=kTraining, push_cnt=False, max_inde
     if want_cnt:
         _split_initv(shards, comm, 0)
     mark(2)
-    PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h)
+    PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h, shards[0].nranks)
     parts = [sh.split_owner_forward(0) for sh in shards]
     mark(3)
     rparts = comm.alltoallv(parts, [[M] * N] * n, [[M] * N] * n, PS)
@@ -906,7 +906,7 @@ class SplitPipeline:
         shards, comm = self.shards, self.comm
         n, N = len(shards), shards[0].nranks
         mark(-1)
-        PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h)
+        PS = _lib.lib().dfx_split_part_floats(shards[0].ctx.h, shards[0].nranks)
         parts = [sh.split_owner_forward(s) for sh in shards]
         mark(0)
         rparts = comm.alltoallv(parts, [[M] * N] * n, [[M] * N] * n, PS)

@@ -304,7 +304,7 @@ struct GpuSplitStore::Impl {
     N = t->nranks();
     L = t->nlocal();
     d = dfx_ctx_vdim(t->ctx(0));
-    PS = dfx_split_part_floats(t->ctx(0));
+    PS = dfx_split_part_floats(t->ctx(0), N);
     PX = dfx_split_pxv_floats(t->ctx(0));
     for (int s = 0; s < 2; ++s) {
       buf[s].resize(L);

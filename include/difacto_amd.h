@@ -323,8 +323,9 @@ int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos
  *                            owner_forward / owner_backward on the context stream
  * dfx_split_partition runs on a stream of its own, after the batch's producer (the input
  * stream, dfx_ctx_set_input_stream, else the context stream).
- *   dfx_split_owner_forward  owner: part_out[R][dfx_split_part_floats()] per received row
- *                            [XV(d) | XXVV(d) | sum w x | 0 0 0] over this owner's keys
+ *   dfx_split_owner_forward  owner: part_out[R][dfx_split_part_floats(ctx, nranks)] per
+ *                            received row over this owner's keys: one owner [XV(d) | XXVV(d) |
+ *                            sum w x | 0 0 0]; N > 1 owners [XV(d) | sum w x | sum_l XXVV_l | 0 0]
  *   -> alltoallv partials back to the workers (rank-major: owner o's rows at o * part_rows)
  *   dfx_split_combine        worker: pred / p / logloss / AUC of its rows from the owners'
  *                            partials (summed in rank order), progress on the device,
@@ -338,7 +339,7 @@ int dfx_dist_union_rows(dfx_ctx* ctx, const uint64_t* keys, const uint32_t* upos
  *   (device int64[nranks]) and dfx_split_initv_draw draws this owner's keys after the lower
  *   owners', so the rand_r stream is the single updater's.  Owner calls run on the context
  *   stream in call order.  Arrays are device pointers unless noted. */
-int dfx_split_part_floats(dfx_ctx* ctx);
+int dfx_split_part_floats(dfx_ctx* ctx, int nranks);
 int dfx_split_pxv_floats(dfx_ctx* ctx);
 int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* batch, uint64_t max_index,
                         int nranks, uint64_t* keys_out, float* x_out, uint32_t* row_cnt_out);
