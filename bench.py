@@ -129,7 +129,7 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r2b"  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
+PMC_ROUND = "r2c"  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
 
 
 def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
