@@ -64,7 +64,8 @@ struct Kw {
   int slot_layout = -1;
   int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
   int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
-  int initv_onepass = 1;  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
+  int initv_onepass = 1;
+  int fat_nb = 8;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B)  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -117,6 +118,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "fat_fwd") kw->fat_fwd = atoi(cv) != 0;
     else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
     else if (k == "initv_onepass") kw->initv_onepass = atoi(cv) != 0;
+    else if (k == "fat_nb") kw->fat_nb = atoi(cv);
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
       else if (v == "split") kw->slot_layout = 0;
@@ -232,6 +234,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_fwd = kw.fat_fwd;
   c->fat_bwd = kw.fat_bwd;
   c->initv_onepass = kw.initv_onepass;
+  c->fat_nb = kw.fat_nb;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

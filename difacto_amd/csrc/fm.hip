@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 // key away from home, rare at load <= 0.5, walks its chain then).  Reading the slot's two
 // halves together keeps them one DRAM access; read a chain step apart, the entry's line was
 // often evicted before its V was read (the split walk above, applied to fat slots: 185 us).
-template <int G, bool FAT>
+template <int G, bool FAT, int NB = 8>
 __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
@@ -328,7 +328,6 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
     float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};
     const bool valued = a.val != nullptr;
     if constexpr (FAT) {
-      constexpr int NB = 8;  // nnz per trip
       for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
         const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
         uint64_t key[NB];
@@ -557,10 +556,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
 }
 
 // 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
-template <int G>
-__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(
-    FwdArgs a) {
-  fwd_probe_body<G, true>(a);
+template <int G, int NB>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
+  fwd_probe_body<G, true, NB>(a);
 }
 
 // Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
@@ -627,9 +625,15 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   const bool fat = a.T.es != 0 && !a.no_fat_fwd && vec && CPL == 4 && 4 * G == a.d && G >= 2;
   if (a.index && a.B > 0 && spread && fat) {
     const dim3 grid((unsigned)*nblk);
-    if (G == 2) hipLaunchKernelGGL(k_fm_fwd_fat<2>, grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4) hipLaunchKernelGGL(k_fm_fwd_fat<4>, grid, dim3(kFmNT), 0, st, a);
-    else if (G == 8) hipLaunchKernelGGL(k_fm_fwd_fat<8>, grid, dim3(kFmNT), 0, st, a);
+    if (G == 2) hipLaunchKernelGGL((k_fm_fwd_fat<2, 8>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 4)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 4>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 6)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 6>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 12)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 12>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4) hipLaunchKernelGGL((k_fm_fwd_fat<4, 8>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 8) hipLaunchKernelGGL((k_fm_fwd_fat<8, 8>), grid, dim3(kFmNT), 0, st, a);
     DFX_HIP(hipGetLastError());
     if (G == 2 || G == 4 || G == 8) return DFX_OK;
   }

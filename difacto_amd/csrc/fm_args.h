@@ -58,7 +58,8 @@ struct FwdArgs {
   // (split_part_floats(d) floats) instead of pred / p / XV*p / loss
   int keys_ready;
   int part_n;      // owners of the split step (the partial's layout, split_part_floats)
-  int no_fat_fwd;  // fat slots: the split forward walk instead of the one-trip read (A/B)
+  int no_fat_fwd;
+  int fat_nb;      // fat forward: nnz per trip (kwarg fat_nb = 4 | 6 | 8 | 12, default 8)  // fat slots: the split forward walk instead of the one-trip read (A/B)
   float* part;
 };
 
