@@ -168,3 +168,25 @@ def test_reserved_key_is_rejected(H):
     st.push(keys, H.kFeaCount, c.tensor(np.ones(2, np.float32), torch.float32))
     with pytest.raises(H._lib.DfxError):
         c.sync()
+
+
+@pytest.mark.parametrize("d", [4, 12, 20, 24])
+def test_fused_fat_layout_other_vdims(H, d):
+    """fat slots at V_dims whose forward is not the one-trip kernel (d = 4: one lane per row;
+    12, 20, 24: lane groups wider than d / 4) walk the fat layout through the generic probe
+    forward; each step equals the reference's"""
+    cfg = dict(V_dim=d, V_threshold=1, l1=0.01, lr=.1, V_lr=.02)
+    c = H.Context(0, max_keys=1 << 16, slot_layout="fat", **cfg)
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(1500, 25, 1 << 14, seed=700 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 1), want_pred=True)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 1), pred=pred)
+        p = H.progress(c)
+        a, b = pred.cpu().numpy().astype(np.float64), opred.astype(np.float64)
+        assert np.all(np.abs(a - b) <= 1e-5 * np.maximum(np.abs(a), np.abs(b)) + 1e-6)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss)
+    s = H.Store(c).stats()
+    assert s["seed"] == up.seed and s["n_keys"] == up.size()
