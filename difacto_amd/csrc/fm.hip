@@ -621,7 +621,7 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   const int64_t rpb = kFmNT / G;
   *nblk = (int)((a.B + rpb - 1) / rpb);
   // fat slots: one trip per nnz (G lanes x float4 = d exactly; even / odd lanes hold the
-  // entry's halves, so G >= 2)
+  // entry's halves, so G >= 2: d = 8 and 16 — other fat V_dims take the probe walk below)
   const bool fat = a.T.es != 0 && !a.no_fat_fwd && vec && CPL == 4 && 4 * G == a.d && G >= 2;
   if (a.index && a.B > 0 && spread && fat) {
     const dim3 grid((unsigned)*nblk);
@@ -633,9 +633,8 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
     else if (G == 4 && a.fat_nb == 12)
       hipLaunchKernelGGL((k_fm_fwd_fat<4, 12>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4) hipLaunchKernelGGL((k_fm_fwd_fat<4, 8>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 8) hipLaunchKernelGGL((k_fm_fwd_fat<8, 8>), grid, dim3(kFmNT), 0, st, a);
     DFX_HIP(hipGetLastError());
-    if (G == 2 || G == 4 || G == 8) return DFX_OK;
+    if (G == 2 || G == 4) return DFX_OK;
   }
   if (a.index && spread && vec && CPL == 4 && G >= 4 && G <= 32 && a.B > 0) {
     const dim3 grid((unsigned)*nblk);
