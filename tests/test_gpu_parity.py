@@ -437,6 +437,28 @@ def test_fused_empty_and_tiny(H):
         assert p["auc"] == pytest.approx(_auc_expect(blk.labels, opred, auc))
 
 
+@pytest.mark.parametrize("ids", [[7, 7, 7, 7, 7], [11]])
+def test_fused_one_distinct_key(H, ids):
+    """every nnz has the same key (no digit varies: the Localizer's sort still runs one pass,
+    which writes the keys its first pass reads from the batch), and a single nnz"""
+    n = len(ids)
+    offs = np.array([0] + [min(i + 2, n) for i in range(0, n, 2)], np.uint64)
+    blk = D.RowBlock(offs, np.array(ids, np.uint64), None,
+                     np.array([1 if i % 2 == 0 else -1 for i in range(len(offs) - 1)], np.float32))
+    for d in (0, 8, 16):
+        c = H.Context(0, V_dim=d, V_threshold=0, l1=0, max_keys=1 << 12)
+        up = O.Updater(V_dim=d, V_threshold=0, l1=0)
+        for ep in range(3):
+            loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                             push_cnt=(ep == 0), want_pred=True)
+            H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(ep == 0))
+            p = H.progress(c)
+            assert abs(p["loss"] - loss) <= 1e-5 * abs(loss)
+            assert p["auc"] == pytest.approx(_auc_expect(blk.labels, opred, auc))
+        assert H.Store(c).stats()["n_keys"] == up.size() == 1
+        c.close()
+
+
 def test_fused_async_batches_released(H):
     """Batches created, handed to the device and dropped without any host sync (the bench's
     pattern): the library must run on torch's stream so freed blocks are not recycled
