@@ -735,40 +735,47 @@ __global__ void k_probe_stats(Table T, int64_t cap, unsigned long long* out) {
   }
 }
 
-// host copy of the table for save / dump
-// host copy of the table for save / dump: entries (one per slot), and [V | Vaux] by V row
-struct HostTable {
-  std::vector<Entry> ent;
-  std::vector<float> VV;  // split: n_vrows rows of [V(d) | Vaux(d)]; fat: cap rows of Vaux(d)
-  std::vector<Entry> raw;  // fat slots: the slots as stored (32 << es bytes each)
-  int d = 0, es = 0;
-  const float* V(int vr) const {
-    return es ? reinterpret_cast<const float*>(raw.data() + ((size_t)vr << es) + 1)
-              : VV.data() + (size_t)vr * 2 * d;
-  }
-  const float* C(int vr) const {
-    return es ? VV.data() + (size_t)vr * d : VV.data() + (size_t)vr * 2 * d + d;
-  }
-};
+// Every stored entry with its V and Vaux rows (null without V), in slot order, for save /
+// dump.  Fat slots stream the table in chunks of kHostChunk slots (a key's V and Vaux rows are
+// its slot's, so a chunk carries them); the split layout copies the entries and the used V pool
+// rows once (V rows are in allocation order, not slot order).
+constexpr int64_t kHostChunk = 1 << 20;
 
-static int copy_table_to_host(Context* c, HostTable* h) {
+template <typename F>
+static int for_each_entry(Context* c, F fn) {
   const Table& T = c->T;
+  const int d = T.d;
   HostCounters hc;
   DFX_TRY(read_counters(c, &hc));
-  h->d = T.d;
-  h->es = T.es;
-  h->ent.resize(c->cap);
   if (T.es) {
-    h->raw.resize((size_t)c->cap << T.es);
-    h->VV.resize((size_t)c->cap * T.d);
-    DFX_HIP(hipMemcpy(h->raw.data(), T.ent, h->raw.size() * sizeof(Entry), hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < c->cap; ++i) h->ent[i] = h->raw[(size_t)i << T.es];
-  } else {
-    h->VV.resize((size_t)hc.n_vrows * 2 * T.d);
-    DFX_HIP(hipMemcpy(h->ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
+    std::vector<Entry> raw((size_t)std::min<int64_t>(c->cap, kHostChunk) << T.es);
+    std::vector<float> aux((size_t)std::min<int64_t>(c->cap, kHostChunk) * d);
+    for (int64_t i0 = 0; i0 < c->cap; i0 += kHostChunk) {
+      const int64_t n = std::min<int64_t>(kHostChunk, c->cap - i0);
+      DFX_HIP(hipMemcpy(raw.data(), ent_at(T, i0), ((size_t)n << T.es) * sizeof(Entry),
+                        hipMemcpyDeviceToHost));
+      if (d > 0)
+        DFX_HIP(hipMemcpy(aux.data(), T.V + i0 * d, (size_t)n * d * 4, hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < n; ++i) {
+        const Entry& e = raw[(size_t)i << T.es];
+        if (e.key == kEmptyKey) continue;
+        const bool v = e.vrow >= 0;
+        fn(e, v ? reinterpret_cast<const float*>(&raw[(size_t)i << T.es] + 1) : nullptr,
+           v ? aux.data() + (size_t)i * d : nullptr);
+      }
+    }
+    return DFX_OK;
   }
-  if (!h->VV.empty())
-    DFX_HIP(hipMemcpy(h->VV.data(), T.V, h->VV.size() * 4, hipMemcpyDeviceToHost));
+  std::vector<Entry> ent((size_t)c->cap);
+  std::vector<float> VV((size_t)hc.n_vrows * 2 * d);  // [V(d) | Vaux(d)] per V row
+  DFX_HIP(hipMemcpy(ent.data(), T.ent, c->cap * sizeof(Entry), hipMemcpyDeviceToHost));
+  if (!VV.empty()) DFX_HIP(hipMemcpy(VV.data(), T.V, VV.size() * 4, hipMemcpyDeviceToHost));
+  for (const Entry& e : ent) {
+    if (e.key == kEmptyKey) continue;
+    const bool v = e.vrow >= 0;
+    fn(e, v ? VV.data() + (size_t)e.vrow * 2 * d : nullptr,
+       v ? VV.data() + (size_t)e.vrow * 2 * d + d : nullptr);
+  }
   return DFX_OK;
 }
 
@@ -954,24 +961,25 @@ int dfx_store_save(dfx_ctx* ctx, const char* path, int save_aux) {
   DFX_CHECK_ARG(ctx && path, "null argument");
   Context* c = &ctx->c;
   const int d = c->T.d;
-  HostTable ht;
-  DFX_TRY(copy_table_to_host(c, &ht));
   FILE* f = fopen(path, "wb");
   if (!f) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
   bool aux = save_aux != 0;
   fwrite(&aux, sizeof(bool), 1, f);
-  for (const Entry& e : ht.ent) {
-    if (e.key == kEmptyKey) continue;
-    const int size = e.vrow >= 0 ? 1 + d : 1;
-    if (e.w == 0.f && size == 1) continue;  // SGDEntry::empty()
+  const int rc = for_each_entry(c, [&](const Entry& e, const float* V, const float* C) {
+    const int size = V ? 1 + d : 1;
+    if (e.w == 0.f && size == 1) return;  // SGDEntry::empty()
     const uint64_t key = e.key;
     fwrite(&key, 8, 1, f);
     fwrite(&size, sizeof(int), 1, f);
     fwrite(&e.w, 4, 1, f);
     if (aux) { fwrite(&e.sqrt_g, 4, 1, f); fwrite(&e.z, 4, 1, f); }
-    if (size == 1) continue;
-    fwrite(ht.V(e.vrow), 4, d, f);
-    if (aux) fwrite(ht.C(e.vrow), 4, d, f);
+    if (size == 1) return;
+    fwrite(V, 4, d, f);
+    if (aux) fwrite(C, 4, d, f);
+  });
+  if (rc != DFX_OK) {
+    fclose(f);
+    return rc;
   }
   fclose(f);
   return DFX_OK;
@@ -1082,28 +1090,21 @@ int dfx_store_dump(dfx_ctx* ctx, const char* path, int dump_aux, int need_revers
   DFX_CHECK_ARG(ctx && path, "null argument");
   Context* c = &ctx->c;
   const int d = c->T.d;
-  HostTable ht;
-  DFX_TRY(copy_table_to_host(c, &ht));
   std::ofstream os(path);
   if (!os) { set_error(std::string("cannot open ") + path); return DFX_ERR_IO; }
-  for (const Entry& e : ht.ent) {
-    if (e.key == kEmptyKey) continue;
-    const int size = e.vrow >= 0 ? 1 + d : 1;
-    if (e.w == 0.f && size == 1) continue;
+  return for_each_entry(c, [&](const Entry& e, const float* V, const float* C) {
+    const int size = V ? 1 + d : 1;
+    if (e.w == 0.f && size == 1) return;
     os << (need_reverse ? reverse_bytes(e.key) : (uint64_t)e.key);
     os << '\t' << size << '\t' << e.w;
     if (dump_aux) os << '\t' << e.sqrt_g << '\t' << e.z;
     if (size > 1) {
-      const float* v = ht.V(e.vrow);
-      for (int k = 0; k < d; ++k) os << '\t' << v[k];
-      if (dump_aux) {
-        const float* cc = ht.C(e.vrow);
-        for (int k = 0; k < d; ++k) os << '\t' << cc[k];
-      }
+      for (int k = 0; k < d; ++k) os << '\t' << V[k];
+      if (dump_aux)
+        for (int k = 0; k < d; ++k) os << '\t' << C[k];
     }
     os << '\n';
-  }
-  return DFX_OK;
+  });
 }
 
 }  // extern "C"
