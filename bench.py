@@ -129,7 +129,24 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r2c"  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
+PMC_ROUND = "r2c"
+
+# Random 128-byte chunks per second on MI355X, measured in isolation (tools/membench/pmccal,
+# DESIGN.md (d)): reads of distinct random rows, and read-modify-writes of them
+CHUNK_READS_PER_S = 45.5e9
+CHUNK_RMW_PER_S = 17.9e9
+STREAM_BYTES_PER_S = 5.0e12  # the Localizer lane's sequential passes (~0.4 GB per C3 step)
+LOC_BYTES_PER_NNZ = 104.0    # its traffic per nnz (profiles/r2c: transform, 3 sort passes, write)
+
+
+def chunk_model(nnz, U, ms_per_step):
+    """The step's floor in random 128-B chunks: the forward reads one fat slot
+    per nnz, the backward read-modify-writes two chunks per unique key (its slot and its Vaux
+    row), the Localizer streams; the measured step against that floor"""
+    floor_ms = (nnz / CHUNK_READS_PER_S + 2 * U / CHUNK_RMW_PER_S
+                + nnz * LOC_BYTES_PER_NNZ / STREAM_BYTES_PER_S) * 1e3
+    return {"floor_ms": round(floor_ms, 4), "frac": round(floor_ms / ms_per_step, 3),
+            "source": "tools/membench/pmccal rates; DESIGN.md (d)"}  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
 
 
 def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
@@ -359,6 +376,7 @@ def main():
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
+        "chunk_model": chunk_model(B * k, mean_u, elapsed / args.steps * 1e3),
         "train_loss_per_row": round(prog["loss"] / max(prog["nrows"], 1), 6),
         "train_auc": round(prog["auc"] / max(prog["nrows"], 1), 6),
         "model_keys": st["n_keys"], "model_vrows": st["n_vrows"],
