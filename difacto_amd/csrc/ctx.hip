@@ -65,7 +65,8 @@ struct Kw {
   int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
   int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
   int initv_onepass = 1;
-  int fat_nb = 8;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B)  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
+  int fat_nb = 8;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B)
+  int lane_prio = 1;  // lane_prio=normal: the Localizer / AUC lanes at normal priority (A/B)  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -119,6 +120,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
     else if (k == "initv_onepass") kw->initv_onepass = atoi(cv) != 0;
     else if (k == "fat_nb") kw->fat_nb = atoi(cv);
+    else if (k == "lane_prio") kw->lane_prio = v != "normal";
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
       else if (v == "split") kw->slot_layout = 0;
@@ -179,9 +181,10 @@ int pipeline_init(Context* c) {
   // normal-priority side lane cost 9 % of the sharded step)
   int lo = 0, hi = 0;
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, hi));
+  const int lp = c->lane_prio ? hi : 0;  // kwarg lane_prio=normal: the default priority (0)
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, lp));
   c->own_loc_stream = c->loc_stream;
-  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, lp));
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
@@ -235,6 +238,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_bwd = kw.fat_bwd;
   c->initv_onepass = kw.initv_onepass;
   c->fat_nb = kw.fat_nb;
+  c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");
