@@ -382,7 +382,7 @@ int dfx_sync(dfx_ctx* ctx) {
     if (err & kErrPoolFull) m += " V pool full (raise max_vrows);";
     if (err & kErrLens) m += " CHECK_EQ(lens[i], V_dim+1) failed (sgd_updater.cc:83);";
     if (err & kErrNoV) m += " CHECK(e.V != nullptr) failed (sgd_updater.cc:84);";
-    if (err & kErrSort) m += " radix sort look-back never completed;";
+    if (err & kErrSort) m += " a look-back (radix sort or InitV ranking) never completed;";
     if (err & kErrBadKey) m += " key 0xffffffffffffffff is reserved (the empty-slot marker);";
     set_error(m);
     return (err & (kErrTableFull | kErrPoolFull)) ? DFX_ERR_CAPACITY : DFX_ERR_CHECK;
