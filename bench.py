@@ -403,8 +403,10 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     # max_keys sizes the table (cap = pow2 >= 2 * max_keys; a soft bound): the owner's share
     # of the key space, so its table runs at the single-GPU bench's load factor (~0.5);
     # max_vrows (a hard bound) has headroom for an uneven share
+    extra = dict(kv.split("=", 1) for kv in args.ctx.split(",") if kv)
     ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
-                    max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg)
+                    max_keys=max(keyspace // world, 1), max_vrows=per, push_agg=args.push_agg,
+                    **extra)
     shard = DI.Shard(ctx, world)
     comm = DI.TorchComm(device=dev, stage_cpu=args.backend == "gloo",
                         force_collectives=args.force_collectives, comm_priority=args.comm_prio)

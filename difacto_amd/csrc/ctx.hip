@@ -66,7 +66,12 @@ struct Kw {
   int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
   int initv_onepass = 1;
   int fat_nb = 8;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B)
-  int lane_prio = 1;  // lane_prio=normal: the Localizer / AUC lanes at normal priority (A/B)  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
+  // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
+  // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
+  // auc_high: the AUC lane's short latency-bound chain at high priority, the Localizer lane at
+  // the context stream's (fused step: it then ends about when the next step needs it, and the
+  // backward keeps more of the machine: +1.5 %)
+  int lane_prio = 2;  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -120,7 +125,13 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
     else if (k == "initv_onepass") kw->initv_onepass = atoi(cv) != 0;
     else if (k == "fat_nb") kw->fat_nb = atoi(cv);
-    else if (k == "lane_prio") kw->lane_prio = v != "normal";
+    else if (k == "lane_prio") {
+      if (v == "high") kw->lane_prio = 3;
+      else if (v == "normal") kw->lane_prio = 0;
+      else if (v == "loc_high") kw->lane_prio = 1;
+      else if (v == "auc_high") kw->lane_prio = 2;
+      else { set_error("unknown lane_prio: " + v + " (high|normal|loc_high|auc_high)"); return DFX_ERR_ARG; }
+    }
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
       else if (v == "split") kw->slot_layout = 0;
@@ -177,14 +188,21 @@ static void release_ws(Workspace& w) {
 int pipeline_init(Context* c) {
   if (c->loc_stream) return DFX_OK;
   // the side lanes run latency-bound chains of small launches beside a full-occupancy
-  // backward: give them priority so their workgroups are not queued behind its tail (a
-  // normal-priority side lane cost 9 % of the sharded step)
+  // backward: the AUC lane gets priority so its workgroups are not queued behind its tail;
+  // the Localizer lane, which has a step of slack, runs at the main stream's priority by default
+  // (kwarg lane_prio; DESIGN.md (d) has the sweep)
   int lo = 0, hi = 0;
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const int lp = c->lane_prio ? hi : 0;  // kwarg lane_prio=normal: the default priority (0)
-  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, lp));
+  // kwarg lane_prio: bit 0 the Localizer lane high, else at the context stream's priority (the
+  // sharded bench runs its compute on a high-priority stream: a Localizer lane below it
+  // starved, 108 -> 70 M ex/s); bit 1 the AUC lane high, else priority 0
+  int main_prio = 0;
+  if (hipStreamGetPriority(c->stream, &main_prio) != hipSuccess) main_prio = 0;
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
+                                      (c->lane_prio & 1) ? hi : main_prio));
   c->own_loc_stream = c->loc_stream;
-  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, lp));
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
+                                      (c->lane_prio & 2) ? hi : 0));
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
