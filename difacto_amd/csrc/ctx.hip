@@ -180,7 +180,8 @@ static void release_ws(Workspace& w) {
                     &w.uniq, &w.cnt, &w.segstart, &w.col, &w.slot, &w.flags, &w.wb, &w.Vb,
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
-                    &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted};
+                    &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
+                    &w.ivstat};
   for (DevBuf* b : bufs) b->release();
 }
 

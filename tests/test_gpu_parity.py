@@ -85,6 +85,20 @@ def test_localizer_synthetic(H, kind, items, lookback):
         _check_localize(H, c, blk, max_index=1000)
 
 
+def test_localizer_sort_hint_changes(H):
+    """one context sorting narrow keys (3 active digit passes: the next sorts launch the other
+    passes on a small looping grid) then 64-bit ids (every pass active, on that small grid the
+    first time) then narrow keys again: bit-exact every time"""
+    c = H.Context(0)
+    rng = np.random.default_rng(9)
+    for i, wide in enumerate([False, False, True, True, False, True]):
+        blk = D.synthetic(30000, 39, 1 << 24, seed=60 + i)  # many tiles
+        if wide:
+            blk.ids = rng.integers(0, np.iinfo(np.uint64).max, size=blk.nnz, dtype=np.uint64,
+                                   endpoint=True)
+        _check_localize(H, c, blk)
+
+
 def test_localizer_empty(H):
     c = H.Context(0)
     blk = D.RowBlock(np.zeros(5, np.uint64), np.zeros(0, np.uint64), None, np.ones(4, np.float32))
