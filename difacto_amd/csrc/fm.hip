@@ -725,7 +725,6 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
           s = __shfl(s0, (int)(threadIdx.x % kWave) - l, kWave);
         }
         sl = (uint32_t)s;
-        if (l == 0) a.slot[cidx] = sl;  // InitV's slot
       } else {
         sl = a.slot[cidx];
       }
@@ -934,6 +933,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         const bool need =
             !dead && tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
         a.flags[u] = need ? 1u : 0u;
+        // InitV's slot: it reads the slots of flagged keys only (in the steady state none)
+        if (need && a.insert_keys) a.slot[cidx] = sl;
         ninit = need ? 1 : 0;
       }
     }
