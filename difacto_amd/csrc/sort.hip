@@ -13,7 +13,7 @@
 // stores leave in runs of consecutive addresses: keys first, then the payloads through the same
 // LDS buffer (half the LDS, more blocks per CU).  Digits that are constant over all keys (an
 // OR/AND reduction of the keys) get no pass: the active digits run first and the trailing
-// launches exit on the device — no host round trip, graph-capturable.  An optional
+// launches exit on the device — no host round trip.  An optional
 // device-side count (n_dev) bounds the items when only the device knows it.
 #include <cstdlib>
 

@@ -11,8 +11,10 @@
 //                                                                   sgd_updater.cc:76-142
 //   InitV for keys whose w left zero      sgd_updater.cc:118-121,144-152
 //
-// Every grid is sized from host-known B and nnz; U lives on the device, so the sequence is
-// capturable into a hipGraph once dfx_reserve has sized the workspace.
+// Every grid is sized from host-known B and nnz; U lives on the device, so a step needs no
+// host round trip.  It is not captured into a hipGraph: the host enqueues a step in ~0.16 ms
+// against a ~0.8 ms GPU step, and a replayed graph would serialise the
+// Localizer lane of step t + 1 behind step t.
 
 #include "fm_args.h"
 

@@ -115,7 +115,7 @@ int dfx_free(dfx_ctx* ctx, void* ptr);
  * behind a busy stream by tools/pageable_probe.hip); a pinned one only after the copy ran.
  * Device->host returns once the data are on the host. */
 int dfx_memcpy(dfx_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
-/* pre-size the fused-path workspace so dfx_train_step allocates nothing (graph capture) */
+/* pre-size the fused-path workspace so dfx_train_step allocates nothing */
 int dfx_reserve(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz);
 
 /* ---- batch feeder (SGDLearner::IterateData's producer loop, sgd_learner.cc:289-314) -----
@@ -202,7 +202,7 @@ int dfx_store_entry(dfx_ctx* ctx, uint64_t key, float* state, float* V, int* has
 
 /* ---- fused minibatch (SGDLearner::IterateData executor, sgd_learner.cc:203-269) --------
  * localize -> [push kFeaCount] -> pull -> predict -> evaluate -> AUC -> calcgrad -> push,
- * all on the device with no host round trip (graph-capturable after dfx_reserve).
+ * all on the device with no host round trip.
  * job_type: DFX_JOB_TRAINING updates the model; validation/prediction stop after AUC.
  * push_cnt: push occurrence counts first (epoch 0 with V_dim > 0, sgd_learner.cc:272).
  * pred_out: optional device B floats.  Progress accumulates on the device. */
