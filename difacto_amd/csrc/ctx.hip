@@ -65,7 +65,7 @@ struct Kw {
   int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
   int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
   int initv_onepass = 1;
-  int fat_nb = 8;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B)
+  int fat_nb = 6;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B; 6: DESIGN.md (d))
   // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
   // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
   // auc_high: the AUC lane's short latency-bound chain at high priority, the Localizer lane at

@@ -59,7 +59,7 @@ struct FwdArgs {
   int keys_ready;
   int part_n;      // owners of the split step (the partial's layout, split_part_floats)
   int no_fat_fwd;
-  int fat_nb;      // fat forward: nnz per trip (kwarg fat_nb = 4 | 6 | 8 | 12, default 8)  // fat slots: the split forward walk instead of the one-trip read (A/B)
+  int fat_nb;      // fat forward: nnz per trip (kwarg fat_nb = 4 | 6 | 8 | 12, default 6)  // fat slots: the split forward walk instead of the one-trip read (A/B)
   float* part;
 };
 

@@ -191,7 +191,7 @@ struct Context {
   int fat_fwd = 1;    // kwarg fat_fwd
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
-  int fat_nb = 8;         // kwarg fat_nb
+  int fat_nb = 6;         // kwarg fat_nb
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
