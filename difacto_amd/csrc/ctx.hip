@@ -65,6 +65,11 @@ struct Kw {
   int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
   int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
   int initv_onepass = 1;
+  // diag=noauc|noloc|noauc_noloc: MEASUREMENT ONLY (the headroom of the side lanes): no AUC
+  // lane, or each Localizer parity run once and its output reused (results are then wrong
+  // unless the batches repeat); never set by the product path
+  int diag = 0;
+  int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
   int fat_nb = 6;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B; 6: DESIGN.md (d))
   // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
   // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
@@ -124,7 +129,27 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "fat_fwd") kw->fat_fwd = atoi(cv) != 0;
     else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
     else if (k == "initv_onepass") kw->initv_onepass = atoi(cv) != 0;
-    else if (k == "fat_nb") kw->fat_nb = atoi(cv);
+    else if (k == "diag") {
+      if (v == "noauc") kw->diag = 1;
+      else if (v == "noloc") kw->diag = 2;
+      else if (v == "noauc_noloc") kw->diag = 3;
+      else { set_error("unknown diag: " + v + " (noauc|noloc|noauc_noloc)"); return DFX_ERR_ARG; }
+    }
+    else if (k == "fwd_lanes") {
+      kw->fwd_lanes = atoi(cv);
+      if (kw->fwd_lanes != 0 && kw->fwd_lanes != 2 && kw->fwd_lanes != 4) {
+        set_error("fwd_lanes must be 0, 2 or 4");
+        return DFX_ERR_ARG;
+      }
+    }
+    else if (k == "fat_nb") {
+      // the fat forward's nnz per trip at V_dim 16 (V_dim 8 always takes 8)
+      kw->fat_nb = atoi(cv);
+      if (kw->fat_nb != 4 && kw->fat_nb != 6 && kw->fat_nb != 8 && kw->fat_nb != 12) {
+        set_error("fat_nb must be 4, 6, 8 or 12");
+        return DFX_ERR_ARG;
+      }
+    }
     else if (k == "lane_prio") {
       if (v == "high") kw->lane_prio = 3;
       else if (v == "normal") kw->lane_prio = 0;
@@ -211,10 +236,10 @@ int pipeline_init(Context* c) {
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads, &c->ods[0], &c->ods[1]}) {
     DFX_HIP(hipMalloc(d, sizeof(DevState)));
-    DFX_HIP(hipMemset(*d, 0, sizeof(DevState)));
+    DFX_HIP(hipMemsetAsync(*d, 0, sizeof(DevState), c->stream));
   }
-  // null-stream memsets are not ordered against the (non-blocking) lanes: complete them here
-  DFX_HIP(hipStreamSynchronize(nullptr));
+  // complete the zeroing before any lane (a non-blocking stream) can run
+  DFX_HIP(hipStreamSynchronize(c->stream));
   for (auto& h : c->dist_host)
     DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), (kMaxDistRanks + 2) * 8,
                           hipHostMallocDefault));
@@ -257,6 +282,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_bwd = kw.fat_bwd;
   c->initv_onepass = kw.initv_onepass;
   c->fat_nb = kw.fat_nb;
+  c->fwd_lanes = kw.fwd_lanes;
+  c->diag = kw.diag;
   c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
@@ -271,7 +298,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
     return DFX_ERR_HIP;
   }
   if (hipMalloc(&c->zpad, kZpadFloats * sizeof(float)) != hipSuccess ||
-      hipMemset(c->zpad, 0, kZpadFloats * sizeof(float)) != hipSuccess) {
+      hipMemsetAsync(c->zpad, 0, kZpadFloats * sizeof(float), c->stream) != hipSuccess) {
     set_error("hipMalloc(zpad) failed");
     dfx_ctx_destroy(ctx);
     return DFX_ERR_HIP;
@@ -289,7 +316,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
     dfx_ctx_destroy(ctx);
     return rc;
   }
-  // the zpad memset (null stream) and the table's initialisation done before any stream runs
+  // the zpad memset and the table's initialisation done before any other stream runs
   if (hipDeviceSynchronize() != hipSuccess) {
     set_error("dfx_ctx_create: device synchronisation failed");
     dfx_ctx_destroy(ctx);

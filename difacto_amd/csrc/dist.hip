@@ -792,7 +792,7 @@ int dfx_dist_localize(dfx_ctx* ctx, const dfx_batch* b, uint64_t max_index, int 
   const int64_t B = b->size, nnz = b->nnz;
   DFX_TRY(ws_reserve(c, B, nnz));
   Workspace& bw = c->bws[slot];
-  DFX_TRY(loc_reserve(bw, nnz));
+  DFX_TRY(loc_reserve(bw, nnz, c->loc_stream));
   DFX_TRY(bw.ofrank.ensure((kMaxRanks + 2) * 8));
   const Lane LL{c->loc_stream, &bw, c->bds[slot], &c->ds->err};
   // the batch is ready on the caller's (input) stream; the slot's buffers are free once the
@@ -866,7 +866,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   // AUC on its own lane beside the backward (as in the fused step): the forward writes the
   // snapshot of (pred, label) once the previous AUC released the lane's buffers
   const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
-  DFX_TRY(auc_reserve(c->aws, B));
+  DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
   a.auc_key = c->aws.ak0.as<uint32_t>();
   a.auc_lab = c->aws.av0.as<uint32_t>();
   DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));

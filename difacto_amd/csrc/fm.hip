@@ -561,6 +561,157 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
   fwd_probe_body<G, true, NB>(a);
 }
 
+// Fat-slot forward, second form (kwarg fwd_lanes = 2 | 4; V_dim 16, 128-byte slots): G lanes
+// per row, lane l holding V coordinates [CPL*l, CPL*l + CPL) with CPL = 16 / G, NB nnz per
+// trip, and the NEXT trip's ids (and values) loaded while this trip's slots are in flight, so
+// a trip costs one memory round trip instead of two (id, then slot).  At G = 2 a 256-thread
+// block holds 128 rows: B = 100 k rows is 782 blocks, all resident at once on 256 CUs (at G = 4
+// the 1563 blocks ran as 1.5 waves of blocks, the second half-empty).  Sums in the reference's
+// (row, nnz) order exactly as fwd_probe_body's, so predictions are bit-identical to it.
+template <int G, int NB, bool VALUED>
+__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat_pf(FwdArgs a) {
+  constexpr int RPB = kFmNT / G;  // rows per block
+  constexpr int CPL = 16 / G;     // V coordinates per lane
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int gbase = (threadIdx.x % kWave) - l;
+  const int64_t r = (int64_t)blockIdx.x * RPB + g;
+  __shared__ double red[kFmNT / kWave];
+  double loss = 0;
+  if (r < a.B) {
+    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
+    constexpr bool valued = VALUED;
+    float acc = 0.f;
+    float xv[CPL], xxvv[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
+    uint64_t idn[NB];
+    float xn[NB];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const uint64_t jj = o0 + t < o1 ? o0 + t : (o1 > o0 ? o1 - 1 : o0);
+      idn[t] = o1 > o0 ? a.index[jj] : 0ull;
+      xn[t] = (valued && o1 > o0) ? a.val[jj] : 1.f;
+    }
+    for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
+      const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
+      uint64_t key[NB];
+      float xm[NB];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const uint64_t id = idn[t];
+        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+        key[t] = a.keys_ready ? id : reverse_bytes(mm);
+        xm[t] = xn[t];
+      }
+      // this trip's slots: even lanes {w, vrow}, odd lanes the key, every lane its V share
+      float2 eh[NB];
+      float4 v[NB][CPL / 4];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
+        eh[t] = *reinterpret_cast<const float2*>(sl + ((l & 1) ? 6 : 0));
+#pragma unroll
+        for (int m = 0; m < CPL / 4; ++m)
+          v[t][m] = *reinterpret_cast<const float4*>(sl + 8 + CPL * l + 4 * m);
+      }
+      // the next trip's ids, in flight beside the slots
+      const uint64_t jn = j0 + NB;
+      if (jn < o1) {
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const uint64_t jj = jn + t < o1 ? jn + t : o1 - 1;
+          idn[t] = a.index[jj];
+          if (valued) xn[t] = a.val[jj];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) {
+        const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
+        uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
+        float w = __shfl(eh[t].x, gbase, kWave);
+        int vr = __float_as_int(__shfl(eh[t].y, gbase, kWave));
+        float vk[CPL];
+#pragma unroll
+        for (int m = 0; m < CPL / 4; ++m) {
+          vk[4 * m] = v[t][m].x; vk[4 * m + 1] = v[t][m].y;
+          vk[4 * m + 2] = v[t][m].z; vk[4 * m + 3] = v[t][m].w;
+        }
+        if (ek != key[t] && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
+          uint64_t h = tbl_hash(key[t], a.T);
+          for (uint64_t probe = 0; ek != key[t] && ek != kEmptyKey && probe < a.T.mask; ++probe) {
+            h = (h + 1) & a.T.mask;
+            ek = ent_at(a.T, h)->key;
+          }
+          if (ek == key[t]) {
+            const Entry* e = ent_at(a.T, h);
+            w = e->w;
+            vr = e->vrow;
+            load_coords<CPL, true>(reinterpret_cast<const float*>(e) + 8, l, 16, vk);
+          }
+        }
+        // absent (inserted by this training step's backward): w = 0, no V
+        if (ek != key[t]) { w = 0.f; vr = -1; }
+        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
+        const bool vok = vr >= 0 && !(a.l1_shrk && w == 0.f);
+        if (t < nin) {
+          const float x = xm[t];
+          // SpMV::Times skips w == 0 (spmv.h:124-125)
+          if (w != 0.f) acc = valued ? acc + w * x : acc + w;
+          if (vok) {
+            const float xx = x * x;  // XX_ (fm_loss.h:86-92)
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+              xv[k] = valued ? xv[k] + vk[k] * x : xv[k] + vk[k];
+              const float q = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
+              xxvv[k] = valued ? xxvv[k] + q * xx : xxvv[k] + q;
+            }
+          }
+        }
+      }
+    }
+    // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..15 (fm_loss.h:110-113)
+    float tt[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) tt[k] = xv[k] * xv[k] - xxvv[k];
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) s += __shfl(tt[k], gbase + q, kWave);
+    }
+    double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
+    float pr = (float)y;
+    pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
+    const float p = logit_p(a.label[r], pr, a.rw, r);
+    const int64_t xs = a.xs > 16 ? a.xs : 16;
+    if (l == 0) {
+      a.p_out[r] = p;
+      if (xs > 16) a.XVp[r * xs + 16] = p;
+      a.pred[r] = pr;
+      double yy = a.label[r] > 0 ? 1.0 : -1.0;
+      loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+      if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
+        uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
+        a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < CPL / 4; ++m)  // XV_ *= p (fm_loss.h:196-199)
+      *reinterpret_cast<float4*>(a.XVp + r * xs + CPL * l + 4 * m) =
+          make_float4(xv[4 * m] * p, xv[4 * m + 1] * p, xv[4 * m + 2] * p, xv[4 * m + 3] * p);
+  }
+  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0;
+    for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+    a.loss_part[blockIdx.x] = s;
+  }
+}
+
 // Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
 // multiple of 4); otherwise scalar coordinates (the pulled interleaved layout is unaligned).
 void lanes_for(int d, bool vec, int* G, int* CPL, bool* use_vec) {
@@ -623,6 +774,26 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   // fat slots: one trip per nnz (G lanes x float4 = d exactly; even / odd lanes hold the
   // entry's halves, so G >= 2: d = 8 and 16 — other fat V_dims take the probe walk below)
   const bool fat = a.T.es != 0 && !a.no_fat_fwd && vec && CPL == 4 && 4 * G == a.d && G >= 2;
+  if (a.index && a.B > 0 && spread && fat && G == 4 && !a.part && a.fwd_lanes) {
+    // the prefetching form (kwarg fwd_lanes): G' lanes per row
+    const int G2 = a.fwd_lanes;
+    *nblk = (int)((a.B + kFmNT / G2 - 1) / (kFmNT / G2));
+    const dim3 grid((unsigned)*nblk);
+#define DFX_FWDPF(GG, NN)                                                              \
+    if (G2 == GG && a.fat_nb == NN) {                                                  \
+      if (a.val)                                                                       \
+        hipLaunchKernelGGL((k_fm_fwd_fat_pf<GG, NN, true>), grid, dim3(kFmNT), 0, st, a); \
+      else                                                                             \
+        hipLaunchKernelGGL((k_fm_fwd_fat_pf<GG, NN, false>), grid, dim3(kFmNT), 0, st, a); \
+      DFX_HIP(hipGetLastError());                                                      \
+      return DFX_OK;                                                                   \
+    }
+    DFX_FWDPF(2, 4) DFX_FWDPF(2, 6) DFX_FWDPF(2, 8) DFX_FWDPF(4, 4) DFX_FWDPF(4, 6)
+    DFX_FWDPF(4, 8)
+#undef DFX_FWDPF
+    set_error("fwd_lanes 2 | 4 with fat_nb 4 | 6 | 8");
+    return DFX_ERR_ARG;
+  }
   if (a.index && a.B > 0 && spread && fat) {
     const dim3 grid((unsigned)*nblk);
     if (G == 2) hipLaunchKernelGGL((k_fm_fwd_fat<2, 8>), grid, dim3(kFmNT), 0, st, a);

@@ -58,8 +58,9 @@ struct FwdArgs {
   // (split_part_floats(d) floats) instead of pred / p / XV*p / loss
   int keys_ready;
   int part_n;      // owners of the split step (the partial's layout, split_part_floats)
-  int no_fat_fwd;
-  int fat_nb;      // fat forward: nnz per trip (kwarg fat_nb = 4 | 6 | 8 | 12, default 6)  // fat slots: the split forward walk instead of the one-trip read (A/B)
+  int no_fat_fwd;  // fat slots: the split forward walk instead of the one-trip read (A/B)
+  int fat_nb;      // fat forward: nnz per trip at V_dim 16 (kwarg fat_nb = 4 | 6 | 8 | 12)
+  int fwd_lanes;   // V_dim 16 fat slots: k_fm_fwd_fat_pf with this many lanes per row (0: off)
   float* part;
 };
 

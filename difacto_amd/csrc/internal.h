@@ -93,7 +93,9 @@ struct Workspace {
   // look-back words [tiles][256] (u64)
   DevBuf os;
   int64_t os_tiles = 0;
-  int os_reserve(int64_t ntiles);
+  // grows the radix sort's counters / look-back words; fresh ones are zeroed on st, the
+  // stream whose sorts use them (stream order, no host wait)
+  int os_reserve(int64_t ntiles, hipStream_t st);
   uint32_t* os_parts() const { return os.as<uint32_t>(); }
   uint32_t* os_counts() const { return os.as<uint32_t>() + kOsParts * kOsDigits * 256; }
   unsigned long long* os_status() const {
@@ -192,6 +194,9 @@ struct Context {
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
   int fat_nb = 6;         // kwarg fat_nb
+  int fwd_lanes = 0;      // kwarg fwd_lanes
+  int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
+  bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
@@ -336,8 +341,10 @@ int pipeline_init(Context* c);
 int table_unclump(Context* c);
 int table_set_ranges(Context* c, int nranks);
 int step_reserve(Context* c, int64_t rows, int64_t nnz);  // ws_reserve + the step's lanes
-int loc_reserve(Workspace& w, int64_t nnz);              // a Localizer's buffers
-int auc_reserve(Workspace& w, int64_t rows);             // the AUC lane's buffers
+// a Localizer's / the AUC lane's buffers; st: the stream that uses them (fresh sort counters
+// are zeroed there)
+int loc_reserve(Workspace& w, int64_t nnz, hipStream_t st);
+int auc_reserve(Workspace& w, int64_t rows, hipStream_t st);
 
 // store phases (store.hip).  n_host < 0: the count is ds->u_count; n_bound sizes the grid.
 // nds: the device state whose u_count holds the count when n_host < 0

@@ -296,7 +296,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   uint64_t* k1 = ws.keys1.as<uint64_t>();
   uint64_t* p0 = ws.vals0.as<uint64_t>();
   uint64_t* p1 = ws.vals1.as<uint64_t>();
-  DFX_TRY(ws.os_reserve((nnz + 2047) / 2048));
+  DFX_TRY(ws.os_reserve((nnz + 2047) / 2048, L.stream));
   hipLaunchKernelGGL(k_loc_init, dim3(1), dim3(1), 0, L.stream, ds);
   // nothing but the row travels with a key when there is no col to scatter and no value to
   // gather (the fused step on binary data): a 4-byte payload, 12 instead of 16 bytes per item

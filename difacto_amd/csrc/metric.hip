@@ -108,7 +108,7 @@ int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred) {
   Workspace& ws = *L.ws;
   if (B <= 0) return DFX_OK;
-  DFX_TRY(auc_reserve(ws, B));
+  DFX_TRY(auc_reserve(ws, B, L.stream));
   hipLaunchKernelGGL(k_auc_keys, dim3((B + 255) / 256), dim3(256), 0, st, B, label, pred,
                      ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>());
   DFX_HIP(hipGetLastError());
@@ -216,7 +216,7 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool 
     if (!accumulate) DFX_HIP(hipMemsetAsync(out_dev, 0, sizeof(double), L.stream));
     return DFX_OK;
   }
-  DFX_TRY(auc_reserve(ws, B));
+  DFX_TRY(auc_reserve(ws, B, L.stream));
   const int64_t ntiles = (B + kArTile - 1) / kArTile;
   const uint32_t* V0 = nullptr;
   const uint32_t* V1 = nullptr;

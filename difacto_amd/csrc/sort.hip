@@ -324,16 +324,16 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   }
 }
 
-int Workspace::os_reserve(int64_t ntiles) {
+int Workspace::os_reserve(int64_t ntiles, hipStream_t st) {
   if (ntiles < 1) ntiles = 1;
   void* before = os.p;
   const size_t want = kOsCountBytes + (size_t)ntiles * 256 * sizeof(unsigned long long);
   DFX_TRY(os.ensure(want));
   if (os.p != before) {
-    // zero the parts and the look-back words, complete before the host goes on: the lanes are
-    // non-blocking streams, which a memset on the null stream does not order against
-    DFX_HIP(hipMemset(os.p, 0, os.bytes));
-    DFX_HIP(hipStreamSynchronize(nullptr));
+    // zero the parts and the look-back words on the stream that sorts with them: stream order
+    // puts the zeroing before the first sort (a null-stream memset is not ordered against the
+    // non-blocking lanes; round 2's illegal address)
+    DFX_HIP(hipMemsetAsync(os.p, 0, os.bytes, st));
   }
   os_tiles = ntiles;
   return DFX_OK;
@@ -356,7 +356,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   }
   const int64_t tile = (int64_t)kOsNT * it;
   const int64_t ntiles = n > 0 ? (n + tile - 1) / tile : 1;
-  DFX_TRY(ws.os_reserve(n > 0 ? (n + 2047) / 2048 : 1));  // look-back words for tiles >= 2048
+  DFX_TRY(ws.os_reserve(n > 0 ? (n + 2047) / 2048 : 1, L.stream));  // look-back words for tiles >= 2048
   uint32_t* parts = ws.os_parts();
   uint32_t* counts = ws.os_counts();
   unsigned int* epoch = &L.ds->sort_epoch;

@@ -355,7 +355,7 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
     DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[slot], 0));
   }
   Workspace& ows = c->ows[slot];
-  DFX_TRY(loc_reserve(ows, nnz));
+  DFX_TRY(loc_reserve(ows, nnz, OL.stream));
   DFX_TRY(ows.rowid.ensure((size_t)(R + 1) * 8));
   DFX_TRY(ows.oflags.ensure((size_t)(nnz + 1) * 4));
   uint64_t* offs = ows.rowid.as<uint64_t>();
@@ -447,7 +447,7 @@ int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* p
   const int64_t nb = (B + kSpNT - 1) / kSpNT;
   // the AUC lane's snapshot buffers are free once its previous AUC is done
   const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
-  DFX_TRY(auc_reserve(c->aws, B));
+  DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
   DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   if (B > 0) {
     hipLaunchKernelGGL(k_split_combine, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, B,

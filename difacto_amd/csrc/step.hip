@@ -52,13 +52,13 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
 }
 
 // a Localizer lane: its sort buffers and per-nnz / per-key outputs
-int loc_reserve(Workspace& w, int64_t nnz) {
+int loc_reserve(Workspace& w, int64_t nnz, hipStream_t st) {
   if (nnz < 1) nnz = 1;
   DFX_TRY(w.keys0.ensure(nnz * 8));
   DFX_TRY(w.keys1.ensure(nnz * 8));
   DFX_TRY(w.vals0.ensure(nnz * 8));
   DFX_TRY(w.vals1.ensure(nnz * 8));
-  DFX_TRY(w.os_reserve((nnz + 2047) / 2048));
+  DFX_TRY(w.os_reserve((nnz + 2047) / 2048, st));
   DFX_TRY(w.tiles.ensure(sizeof(uint32_t) * ((nnz + 2047) / 2048 + 1)));
   DFX_TRY(w.segstart.ensure((nnz + 1) * 4));
   DFX_TRY(w.col.ensure(nnz * 4));
@@ -74,7 +74,7 @@ int loc_reserve(Workspace& w, int64_t nnz) {
 
 // the AUC lane (metric.hip auc_finish): the snapshot (keys ak0, labels av0) and the merge
 // ping-pong buffers (u64 keys, u32 labels)
-int auc_reserve(Workspace& w, int64_t rows) {
+int auc_reserve(Workspace& w, int64_t rows, hipStream_t st) {
   if (rows < 1) rows = 1;
   if (w.rows >= rows && w.ak0.p) return DFX_OK;
   DFX_TRY(w.ak0.ensure(rows * 4));
@@ -83,7 +83,7 @@ int auc_reserve(Workspace& w, int64_t rows) {
   DFX_TRY(w.keys1.ensure(rows * 8));
   DFX_TRY(w.vals0.ensure(rows * 4));
   DFX_TRY(w.vals1.ensure(rows * 4));
-  DFX_TRY(w.os_reserve((rows + 2047) / 2048));  // the radix-sort fallback's look-back words
+  DFX_TRY(w.os_reserve((rows + 2047) / 2048, st));  // the radix sort's look-back words
   w.rows = rows;
   return DFX_OK;
 }
@@ -91,9 +91,9 @@ int auc_reserve(Workspace& w, int64_t rows) {
 int step_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(pipeline_init(c));
   DFX_TRY(ws_reserve(c, rows, nnz));
-  DFX_TRY(loc_reserve(c->bws[0], nnz));
-  DFX_TRY(loc_reserve(c->bws[1], nnz));
-  return auc_reserve(c->aws, rows);
+  DFX_TRY(loc_reserve(c->bws[0], nnz, c->loc_stream));
+  DFX_TRY(loc_reserve(c->bws[1], nnz, c->loc_stream));
+  return auc_reserve(c->aws, rows, c->aux_stream);
 }
 
 // SGDUpdater::Get (sgd_updater.cc:34-58) over the batch's sorted unique keys, as the
@@ -250,12 +250,15 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   o.col = c->fwd_probe ? nullptr : col;  // probe mode: the forward finds keys itself
   o.uniq = uniq;
   lane_mark(c, 0, c->loc_stream);
-  DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
-  // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
   uint32_t* choff = bw.flags.as<uint32_t>();
   uint32_t* chunk_seg = bw.rowtmp.as<uint32_t>();
   uint32_t* nchunks = &bds->totals[1];
-  DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
+  if (!((c->diag & 2) && c->loc_done[k])) {  // (diag: measurement only)
+    DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+    // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
+    DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
+    c->loc_done[k] = true;
+  }
   lane_mark(c, 1, c->loc_stream);
   DFX_HIP(hipEventRecord(c->ev_loc[k], c->loc_stream));
 
@@ -292,6 +295,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.no_fat_fwd = !c->fat_fwd;
   a.fat_nb = c->fat_nb;
+  a.fwd_lanes = c->fwd_lanes;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
@@ -310,7 +314,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   lane_mark(c, 2, c->aux_stream);
-  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
+  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
   lane_mark(c, 3, c->aux_stream);
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   prof_mark(c, 5);
@@ -426,7 +430,8 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
   double h[2];
   DFX_HIP(hipMemcpy(h, &c->ds->sum_u, sizeof(h), hipMemcpyDeviceToHost));
   if (mean_u) *mean_u = h[1] > 0 ? h[0] / h[1] : 0;
-  DFX_HIP(hipMemset(&c->ds->sum_u, 0, sizeof(h)));
-  DFX_HIP(hipStreamSynchronize(nullptr));  // before any lane's next kernel
+  // the counters are the context stream's (k_step_finalize): zeroed in its order
+  DFX_HIP(hipMemsetAsync(&c->ds->sum_u, 0, sizeof(h), c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;
 }

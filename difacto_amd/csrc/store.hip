@@ -189,10 +189,8 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
     Workspace& ws = c->ws;
     void* before = ws.ivstat.p;
     DFX_TRY(ws.ivstat.ensure((size_t)ntiles * 8));
-    if (ws.ivstat.p != before) {  // fresh words read as unpublished (tag 0, flag 0)
-      DFX_HIP(hipMemset(ws.ivstat.p, 0, ws.ivstat.bytes));
-      DFX_HIP(hipStreamSynchronize(nullptr));
-    }
+    if (ws.ivstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
+      DFX_HIP(hipMemsetAsync(ws.ivstat.p, 0, ws.ivstat.bytes, c->stream));
     hipLaunchKernelGGL(k_initv_onepass, dim3((unsigned)ntiles), dim3(kStNT), 0, c->stream, flags,
                        total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate,
                        ws.ivstat.as<unsigned long long>());

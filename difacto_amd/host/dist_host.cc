@@ -138,26 +138,37 @@ class RcclExchange : public ShardExchange {
   RcclExchange(dfx_ctx* ctx, int rank, int nranks, const std::string& id_file)
       : ctx_(ctx), rank_(rank), n_(nranks) {
     ncclUniqueId id[2];
+    // the file carries the launch's nonce (TORCHELASTIC_RUN_ID, the same on every rank of a
+    // torchrun launch, or DFX_RUN_ID): a reader rejects a file left by an earlier launch
+    char nonce[64] = {0};
+    const char* rid = std::getenv("DFX_RUN_ID");
+    if (!rid) rid = std::getenv("TORCHELASTIC_RUN_ID");
+    if (rid) std::snprintf(nonce, sizeof(nonce), "%s", rid);
     if (rank == 0) {
       NcclCheck(ncclGetUniqueId(&id[0]), "ncclGetUniqueId");
       NcclCheck(ncclGetUniqueId(&id[1]), "ncclGetUniqueId");
       const std::string tmp = id_file + ".tmp" + std::to_string(getpid());
       FILE* f = std::fopen(tmp.c_str(), "wb");
-      if (!f || std::fwrite(id, sizeof(id), 1, f) != 1) Fail("cannot write " + tmp);
+      if (!f || std::fwrite(nonce, sizeof(nonce), 1, f) != 1 ||
+          std::fwrite(id, sizeof(id), 1, f) != 1)
+        Fail("cannot write " + tmp);
       std::fclose(f);
       if (std::rename(tmp.c_str(), id_file.c_str()) != 0) Fail("cannot publish " + id_file);
     } else {
-      // node-local rendezvous: wait for rank 0's ids (60 s)
+      // node-local rendezvous: wait for rank 0's ids of this launch (60 s)
       bool ok = false;
       for (int i = 0; i < 6000 && !ok; ++i) {
         FILE* f = std::fopen(id_file.c_str(), "rb");
         if (f) {
-          ok = std::fread(id, sizeof(id), 1, f) == 1;
+          char got[64];
+          ok = std::fread(got, sizeof(got), 1, f) == 1 &&
+               std::memcmp(got, nonce, sizeof(nonce)) == 0 &&
+               std::fread(id, sizeof(id), 1, f) == 1;
           std::fclose(f);
         }
         if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(10));
       }
-      if (!ok) Fail("no communicator id in " + id_file);
+      if (!ok) Fail("no communicator id of this launch in " + id_file);
     }
     // the compute stream at high priority: HIP maps the streams of one priority onto that
     // priority's hardware queues, which run their packets in order, so this keeps the step's
@@ -195,6 +206,7 @@ class RcclExchange : public ShardExchange {
     (void)hipEventDestroy(in_);
     (void)hipHostFree(hcnt_);
     (void)hipFree(dcnt_);
+    if (ar_) (void)hipFree(ar_);
     (void)dfx_ctx_use_own_stream(ctx_);
     for (auto s : cs_) (void)hipStreamDestroy(s);
     (void)hipStreamDestroy(stream_);
@@ -277,16 +289,21 @@ class RcclExchange : public ShardExchange {
     return h;
   }
 
+  // (GpuDistStore's progress thread polls with it: a grow-only device buffer, no malloc per call)
   void AllReduceSum(std::vector<double>* v) override {
     const size_t n = v->size();
+    if (n == 0) return;
+    if (n > ar_cap_) {
+      HipCheck(hipStreamSynchronize(cs_[0]), "sync");
+      if (ar_) (void)hipFree(ar_);
+      HipCheck(hipMalloc(reinterpret_cast<void**>(&ar_), 8 * n), "malloc");
+      ar_cap_ = n;
+    }
     std::vector<double> buf(*v);
-    double* d = nullptr;
-    HipCheck(hipMalloc(reinterpret_cast<void**>(&d), 8 * (n ? n : 1)), "malloc");
-    HipCheck(hipMemcpyAsync(d, buf.data(), 8 * n, hipMemcpyHostToDevice, cs_[0]), "H2D");
-    NcclCheck(ncclAllReduce(d, d, n, ncclFloat64, ncclSum, comm_[0], cs_[0]), "allreduce");
-    HipCheck(hipMemcpyAsync(v->data(), d, 8 * n, hipMemcpyDeviceToHost, cs_[0]), "D2H");
+    HipCheck(hipMemcpyAsync(ar_, buf.data(), 8 * n, hipMemcpyHostToDevice, cs_[0]), "H2D");
+    NcclCheck(ncclAllReduce(ar_, ar_, n, ncclFloat64, ncclSum, comm_[0], cs_[0]), "allreduce");
+    HipCheck(hipMemcpyAsync(v->data(), ar_, 8 * n, hipMemcpyDeviceToHost, cs_[0]), "D2H");
     HipCheck(hipStreamSynchronize(cs_[0]), "sync");
-    (void)hipFree(d);
   }
 
  private:
@@ -306,6 +323,8 @@ class RcclExchange : public ShardExchange {
   int next_ = 0;
   int64_t* hcnt_ = nullptr;
   int64_t* dcnt_ = nullptr;
+  double* ar_ = nullptr;  // AllReduceSum's device buffer
+  size_t ar_cap_ = 0;
 };
 
 // grow-only device buffer of one context

@@ -2,8 +2,14 @@
 // interface (no HIP headers).
 #include "dist_store.h"
 
+#include <chrono>
 #include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <functional>
 #include <mutex>
+#include <set>
+#include <thread>
 
 #include "gpu_adapters.h"
 
@@ -11,16 +17,21 @@ namespace difacto {
 
 namespace {
 
-enum Op { kOpCount = 1, kOpPull = 2, kOpGrad = 3, kOpBarrier = 4 };
+enum Op { kOpNone = 0, kOpCount = 1, kOpPull = 2, kOpGrad = 3, kOpBarrier = 4 };
+constexpr int kFlagStop = 5, kFlags = 6;  // per rank: its head ops (one-hot) and "stopping"
 
-// one worker's call of a round
+// one request of a worker, queued until a round serves it.  The SArrays are shared handles:
+// the request keeps the caller's buffers alive (ps-lite's KVWorker holds them the same way)
 struct Req {
-  int op = 0;
-  const SArray<feaid_t>* keys = nullptr;
-  const SArray<real_t>* vals = nullptr;
-  const SArray<int>* lens = nullptr;
+  int op = kOpNone;
+  int ts = -1;
+  bool from_cb = false;  // issued by a callback of its worker
+  SArray<feaid_t> keys;
+  SArray<real_t> vals;
+  SArray<int> lens;
   SArray<real_t>* out_vals = nullptr;
   SArray<int>* out_lens = nullptr;
+  std::function<void()> cb;
 };
 
 std::string CtxKw(const KWArgs& kw) {
@@ -30,6 +41,17 @@ std::string CtxKw(const KWArgs& kw) {
     s += p.first + "=" + p.second;
   }
   return s;
+}
+
+// kwarg store_sync=lockstep|async (GpuDistStore::Core::lockstep)
+bool LockstepOf(const KWArgs& kw) {
+  for (const auto& p : kw) {
+    if (p.first != "store_sync") continue;
+    DFX_HOST_CHECK(p.second == "lockstep" || p.second == "async",
+                   "store_sync must be lockstep or async");
+    return p.second == "lockstep";
+  }
+  return true;
 }
 
 std::vector<int64_t> Offsets(const std::vector<int64_t>& rows) {
@@ -43,8 +65,29 @@ inline int OwnerOf(feaid_t k, int n) {
   return (int)(((unsigned __int128)k * (unsigned)n) >> 64);
 }
 
+// the worker whose callback the current thread is running (requests it issues are that
+// worker's next ones: they go to the front of its queue, see Core::Enqueue)
+thread_local int t_in_callback_of = -1;
+
 }  // namespace
 
+// KVStoreDist's request flow (kvstore_dist.h:90-175) for GPU shards: Push / Pull enqueue a
+// request and return a timestamp; ONE progress thread per process serves the queues in
+// rounds, all processes together, and runs each request's callback when it is done (ps-lite
+// runs them on its receiving thread the same way).  So the reference's IterateData drives it
+// unchanged: the reader thread's Push(kFeaCount) of batch k+1 and the executor's Pull /
+// Push(kGradient) of batch k may overlap, and workers may hold different numbers of batches.
+//
+// A round: every process reports which kinds each local worker can have served (a host
+// all-reduce — RCCL, or nothing at loopback); every process then serves the same ONE kind, the
+// first servable of gradient push, pull, count push, barrier — lockstep (store_sync=lockstep,
+// the default): when every worker has one; async: for the workers that have one at their head —
+// as one exchange among all shards, in which the workers without a request send no keys.
+// Order within a worker: FIFO, except that requests issued from a callback of its own go first
+// (the pull's callback pushes the gradient: served before a count push of the next batch that
+// the reader queued meanwhile), and in lockstep a pull or gradient push may overtake count
+// pushes (the reader's look-ahead) — the sequential order count(k), pull(k), grad(k),
+// count(k+1), ...  A barrier is served when it heads every worker's queue.
 struct GpuDistStore::Core {
   std::vector<dfx_ctx*> ctxs;  // owned
   std::unique_ptr<ShardExchange> ex;
@@ -52,12 +95,21 @@ struct GpuDistStore::Core {
   bool agg_sum = false;
   std::vector<std::unique_ptr<Store>> workers;
 
-  // the round's rendezvous: the last of the L workers to call runs the round for all
   std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0;
-  uint64_t gen = 0;
-  std::vector<Req> reqs;
+  std::condition_variable cv_done;
+  std::vector<std::deque<Req>> q;      // per local worker
+  std::vector<int> next_ts;            // per local worker
+  std::vector<std::set<int>> done;     // completed timestamps >= done_low
+  std::vector<int> done_low;           // every timestamp below it is complete
+  bool stopping = false;
+  // store_sync=lockstep (default): a sub-round of a kind runs when every worker has a request
+  // of that kind (the synchronous step of push_agg=sum: every worker issues the same calls, an
+  // idle worker empty ones); async: each worker's head request is served as it comes, as
+  // ps-lite's server handles pushes in arrival order (workers may hold different numbers of
+  // batches; which requests share a round depends on timing)
+  bool lockstep = true;
+  std::thread progress;
+  std::string failure;                 // a round failed: every later call reports it
 
   struct Bufs {
     explicit Bufs(dfx_ctx* c)
@@ -70,27 +122,53 @@ struct GpuDistStore::Core {
   std::vector<float> host;
 
   void Setup();
+  void Stop() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!progress.joinable()) return;
+      stopping = true;
+    }
+    progress.join();
+  }
   ~Core() {
+    Stop();
     workers.clear();
     for (dfx_ctx* c : ctxs) (void)dfx_sync(c);
     ex.reset();
     for (dfx_ctx* c : ctxs) (void)dfx_ctx_destroy(c);
   }
 
-  void Round(int l, const Req& r) {
-    std::unique_lock<std::mutex> lk(mu);
-    reqs[l] = r;
-    const uint64_t g = gen;
-    if (++arrived < L) {
-      cv.wait(lk, [&]() { return gen != g; });
-      return;
+  int Enqueue(int l, Req r) {
+    std::lock_guard<std::mutex> lk(mu);
+    DFX_HOST_CHECK(failure.empty(), "GpuDistStore: " + failure);
+    DFX_HOST_CHECK(!stopping, "GpuDistStore: a request after the store began to stop");
+    r.ts = next_ts[l]++;
+    const int ts = r.ts;
+    if (t_in_callback_of == l) {
+      // issued by a callback of this worker: ahead of what was queued meanwhile, after any
+      // request the same callback issued before it
+      r.from_cb = true;
+      size_t pos = 0;
+      while (pos < q[l].size() && q[l][pos].from_cb && q[l][pos].ts >= cb_first_ts_) ++pos;
+      q[l].insert(q[l].begin() + pos, std::move(r));
+    } else {
+      q[l].push_back(std::move(r));
     }
-    arrived = 0;
-    lk.unlock();  // the other workers wait for gen to move
-    Exec();
-    lk.lock();
-    ++gen;
-    cv.notify_all();
+    return ts;
+  }
+  int cb_first_ts_ = 1 << 30;  // requests of the running callback have ts >= this
+
+  bool IsDone(int l, int ts) {
+    return ts < done_low[l] || done[l].count(ts) != 0;
+  }
+  void MarkDone(int l, int ts) {
+    done[l].insert(ts);
+    while (done[l].count(done_low[l])) done[l].erase(done_low[l]++);
+  }
+  void Wait(int l, int ts) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&]() { return IsDone(l, ts) || !failure.empty(); });
+    DFX_HOST_CHECK(failure.empty(), "GpuDistStore: " + failure);
   }
 
   void Sync() {
@@ -115,7 +193,10 @@ struct GpuDistStore::Core {
                "dfx_dist_initv_draw");
   }
 
-  void Exec();
+  void Loop();
+  // one sub-round of kind op among all shards: reqs[l] is local worker l's request, or null
+  // (it takes part with no keys)
+  void Exec(int op, const std::vector<Req*>& reqs);
 };
 
 void GpuDistStore::Core::Setup() {
@@ -124,44 +205,159 @@ void GpuDistStore::Core::Setup() {
   S = dfx_dist_record_floats(ctxs[0]);
   d = dfx_ctx_vdim(ctxs[0]);
   agg_sum = dfx_dist_push_agg_sum(ctxs[0]) == 1;
-  reqs.resize(L);
+  q.resize(L);
+  next_ts.assign(L, 0);
+  done.resize(L);
+  done_low.assign(L, 0);
   for (int l = 0; l < L; ++l) {
     bufs.emplace_back(new Bufs(ctxs[l]));
     bufs.back()->icnt.ensure(1);
     bufs.back()->iall.ensure(N);
   }
+  progress = std::thread([this]() { Loop(); });
 }
 
-void GpuDistStore::Core::Exec() {
-  const int op = reqs[0].op;
-  for (int l = 1; l < L; ++l)
-    DFX_HOST_CHECK(reqs[l].op == op, "GpuDistStore: the workers' calls of a round differ");
-  if (op == kOpBarrier) {
-    std::vector<double> one(1, 1.0);
-    ex->AllReduceSum(&one);
-    return;
+void GpuDistStore::Core::Loop() {
+  int idle_us = 0;
+  // the request of kind op worker l can have served now, or -1.  Its queue is FIFO, except
+  // that (lockstep) a pull or a gradient push may overtake count pushes queued ahead of it: a
+  // count push is the reader thread's look-ahead to the next batch (IterateData issues it
+  // while the executor still works on the previous batch), so the others run first
+  auto find = [&](int l, int op) -> int {
+    if (q[l].empty()) return -1;
+    if (!lockstep || op == kOpCount || op == kOpBarrier) return q[l].front().op == op ? 0 : -1;
+    for (size_t i = 0; i < q[l].size(); ++i)
+      if (q[l][i].op != kOpCount) return q[l][i].op == op ? (int)i : -1;
+    return -1;
+  };
+  while (true) {
+    // what every rank can serve this round, by a host all-reduce
+    std::vector<double> flags((size_t)N * kFlags, 0.0);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (int l = 0; l < L; ++l) {
+        const size_t r = (size_t)ex->rank(l);
+        for (int o : {kOpCount, kOpPull, kOpGrad, kOpBarrier})
+          if (find(l, o) >= 0) flags[r * kFlags + o] = 1.0;
+        if (stopping) flags[r * kFlags + kFlagStop] = 1.0;
+      }
+    }
+    try {
+      ex->AllReduceSum(&flags);
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu);
+      failure = e.what();
+      cv_done.notify_all();
+      return;
+    }
+    int nop[kFlags] = {0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < N; ++r)
+      for (int o = 1; o < kFlags; ++o) nop[o] += flags[(size_t)r * kFlags + o] != 0 ? 1 : 0;
+    // one kind per round, the first servable of gradient push, pull, count push, barrier:
+    // lockstep, when every worker has one; async, for whoever has one at its head.  A barrier
+    // needs everyone
+    int kind = kOpNone;
+    for (int o : {kOpGrad, kOpPull, kOpCount, kOpBarrier}) {
+      if (lockstep || o == kOpBarrier ? nop[o] == N : nop[o] > 0) {
+        kind = o;
+        break;
+      }
+    }
+    const bool work = kind != kOpNone;
+    if (!work) {
+      const bool pending = nop[kOpCount] || nop[kOpPull] || nop[kOpGrad] || nop[kOpBarrier];
+      if (nop[kFlagStop] == N) {
+        // every process is stopping: the store is done.  Requests still queued can never be
+        // served (lockstep: a worker issued calls the others did not)
+        if (pending) {
+          std::lock_guard<std::mutex> lk(mu);
+          failure = "requests left at shutdown: in lockstep (store_sync=lockstep) every worker "
+                    "must issue the same sequence of calls";
+          cv_done.notify_all();
+        }
+        return;
+      }
+      idle_us = idle_us == 0 ? 20 : std::min(idle_us * 2, 1000);
+      std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+      continue;
+    }
+    idle_us = 0;
+    {
+      const int op = kind;
+      std::vector<Req> served(L);
+      std::vector<Req*> reqs(L, nullptr);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int l = 0; l < L; ++l) {
+          // what was reported at the start of the round is still there: only this thread
+          // takes requests, and a callback of this thread adds them at the front
+          const int i = find(l, op);
+          if (i >= 0) {
+            served[l] = std::move(q[l][i]);
+            q[l].erase(q[l].begin() + i);
+            reqs[l] = &served[l];
+          }
+        }
+      }
+      try {
+        if (op == kOpBarrier) {
+          std::vector<double> one(1, 1.0);
+          ex->AllReduceSum(&one);
+        } else {
+          Exec(op, reqs);
+        }
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> lk(mu);
+        failure = e.what();
+        cv_done.notify_all();
+        return;
+      }
+      for (int l = 0; l < L; ++l) {
+        if (!reqs[l]) continue;
+        if (served[l].cb) {
+          // requests the callback issues are this worker's next ones
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            cb_first_ts_ = next_ts[l];
+          }
+          t_in_callback_of = l;
+          served[l].cb();
+          t_in_callback_of = -1;
+          std::lock_guard<std::mutex> lk(mu);
+          cb_first_ts_ = 1 << 30;
+        }
+        std::lock_guard<std::mutex> lk(mu);
+        MarkDone(l, served[l].ts);
+        cv_done.notify_all();
+      }
+    }
   }
+}
+
+void GpuDistStore::Core::Exec(int op, const std::vector<Req*>& reqs) {
   // split every worker's keys by owner (sorted keys: contiguous runs, kvstore_dist.h:101,111)
   std::vector<std::vector<int64_t>> send(L, std::vector<int64_t>(N, 0)), recv;
   std::vector<int64_t> U(L), R(L);
   std::vector<const void*> ks(L), cs(L), ps(L);
   std::vector<void*> kr(L), cr(L), pr(L);
   for (int l = 0; l < L; ++l) {
-    const SArray<feaid_t>& k = *reqs[l].keys;
-    U[l] = (int64_t)k.size();
-    for (size_t i = 0; i < k.size(); ++i) {
-      DFX_HOST_CHECK(i == 0 || k[i - 1] <= k[i], "fea_ids must in non-decreasing order");
-      ++send[l][OwnerOf(k[i], N)];
+    const Req* rq = reqs[l];
+    U[l] = rq ? (int64_t)rq->keys.size() : 0;
+    for (int64_t i = 0; i < U[l]; ++i) {
+      DFX_HOST_CHECK(i == 0 || rq->keys[i - 1] <= rq->keys[i],
+                     "fea_ids must in non-decreasing order");
+      ++send[l][OwnerOf(rq->keys[i], N)];
     }
     Bufs& b = *bufs[l];
     b.keys.ensure(U[l]);
-    if (U[l]) DfxCheck(dfx_memcpy(ctxs[l], b.keys.get(), k.data(), U[l] * 8, 0), "upload keys");
+    if (U[l])
+      DfxCheck(dfx_memcpy(ctxs[l], b.keys.get(), rq->keys.data(), U[l] * 8, 0), "upload keys");
     ks[l] = b.keys.get();
     if (op == kOpCount) {
-      const SArray<real_t>& c = *reqs[l].vals;
-      DFX_HOST_CHECK((int64_t)c.size() == U[l], "kFeaCount: one count per key");
+      DFX_HOST_CHECK(!rq || (int64_t)rq->vals.size() == U[l], "kFeaCount: one count per key");
       b.cnt.ensure(U[l]);
-      if (U[l]) DfxCheck(dfx_memcpy(ctxs[l], b.cnt.get(), c.data(), U[l] * 4, 0), "upload counts");
+      if (U[l])
+        DfxCheck(dfx_memcpy(ctxs[l], b.cnt.get(), rq->vals.data(), U[l] * 4, 0), "upload counts");
       cs[l] = b.cnt.get();
     }
   }
@@ -180,7 +376,7 @@ void GpuDistStore::Core::Exec() {
   const int hc = op == kOpCount ? ex->Start(0, cs, send, cr, recv, 4, true) : -1;
   ex->Wait(hk);
   if (hc >= 0) ex->Wait(hc);
-  // every call begins its own owner step: table slots may move at a sync point in between
+  // every sub-round begins its own owner step: table slots may move at a sync point in between
   for (int l = 0; l < L; ++l) {
     const std::vector<int64_t> offs = Offsets(recv[l]);
     DfxCheck(dfx_dist_owner_begin(ctxs[l], 0, bufs[l]->rkeys.get(), offs.data(), N,
@@ -204,7 +400,8 @@ void GpuDistStore::Core::Exec() {
     ex->Wait(ex->Start(1, ps, recv, pr, send, (size_t)S * 4, true));
     // records [V(d) | w | live | 0 0] -> Get layout (sgd_updater.cc:34-58): w, then V when live
     for (int l = 0; l < L; ++l) {
-      const Req& q = reqs[l];
+      const Req* rq = reqs[l];
+      if (!rq) continue;
       host.resize((size_t)U[l] * S);
       bufs[l]->rrecs.download(host.data(), host.size());
       std::vector<real_t> vals;
@@ -219,12 +416,12 @@ void GpuDistStore::Core::Exec() {
           lens.push_back(live ? d + 1 : 1);
         }
       }
-      q.out_vals->CopyFrom(vals.data(), vals.size());
-      if (q.out_lens) {
+      rq->out_vals->CopyFrom(vals.data(), vals.size());
+      if (rq->out_lens) {
         if (d > 0) {
-          q.out_lens->CopyFrom(lens.data(), lens.size());
+          rq->out_lens->CopyFrom(lens.data(), lens.size());
         } else {
-          q.out_lens->clear();
+          rq->out_lens->clear();
         }
       }
     }
@@ -233,25 +430,28 @@ void GpuDistStore::Core::Exec() {
   }
   // kGradient: Get-layout gradients (the lens of the pull) -> records [gV | gw | live | 0 0]
   for (int l = 0; l < L; ++l) {
-    const Req& q = reqs[l];
-    const SArray<real_t>& g = *q.vals;
-    const SArray<int>& lens = *q.lens;
-    DFX_HOST_CHECK(d == 0 || (int64_t)lens.size() == U[l], "kGradient: one length per key");
+    const Req* rq = reqs[l];
     host.assign((size_t)U[l] * S, 0.f);
-    size_t p = 0;
-    for (int64_t i = 0; i < U[l]; ++i) {
-      const int len = d > 0 ? lens[i] : 1;
-      DFX_HOST_CHECK(len == 1 || len == d + 1, "kGradient: lengths must be 1 or 1 + V_dim");
-      DFX_HOST_CHECK(p + len <= g.size(), "kGradient: fewer values than the lengths say");
-      float* r = host.data() + i * S;
-      r[d] = g[p];
-      if (len > 1) {
-        std::memcpy(r, g.data() + p + 1, d * sizeof(float));
-        r[d + 1] = 1.f;
+    if (rq) {
+      const SArray<real_t>& g = rq->vals;
+      const SArray<int>& lens = rq->lens;
+      DFX_HOST_CHECK(d == 0 || U[l] == 0 || (int64_t)lens.size() == U[l],
+                     "kGradient: one length per key");
+      size_t p = 0;
+      for (int64_t i = 0; i < U[l]; ++i) {
+        const int len = d > 0 ? lens[i] : 1;
+        DFX_HOST_CHECK(len == 1 || len == d + 1, "kGradient: lengths must be 1 or 1 + V_dim");
+        DFX_HOST_CHECK(p + len <= g.size(), "kGradient: fewer values than the lengths say");
+        float* r = host.data() + i * S;
+        r[d] = g[p];
+        if (len > 1) {
+          std::memcpy(r, g.data() + p + 1, d * sizeof(float));
+          r[d + 1] = 1.f;
+        }
+        p += len;
       }
-      p += len;
+      DFX_HOST_CHECK(p == g.size(), "kGradient: more values than the lengths say");
     }
-    DFX_HOST_CHECK(p == g.size(), "kGradient: more values than the lengths say");
     Bufs& b = *bufs[l];
     b.recs.ensure(host.size());
     if (!host.empty())
@@ -281,12 +481,11 @@ class DistWorker : public Store {
                    "GpuDistStore::Push: kFeaCount or kGradient");
     Req r;
     r.op = val_type == kFeaCount ? kOpCount : kOpGrad;
-    r.keys = &fea_ids;
-    r.vals = &vals;
-    r.lens = &lens;
-    core_->Round(l_, r);
-    if (on_complete) on_complete();
-    return time_++;
+    r.keys = fea_ids;
+    r.vals = vals;
+    r.lens = lens;
+    r.cb = on_complete;
+    return core_->Enqueue(l_, std::move(r));
   }
   int Pull(const SArray<feaid_t>& fea_ids, int val_type, SArray<real_t>* vals, SArray<int>* lens,
            const std::function<void()>& on_complete) override {
@@ -294,14 +493,13 @@ class DistWorker : public Store {
     DFX_HOST_CHECK(vals != nullptr, "GpuDistStore::Pull: null vals");
     Req r;
     r.op = kOpPull;
-    r.keys = &fea_ids;
+    r.keys = fea_ids;
     r.out_vals = vals;
     r.out_lens = lens;
-    core_->Round(l_, r);
-    if (on_complete) on_complete();
-    return time_++;
+    r.cb = on_complete;
+    return core_->Enqueue(l_, std::move(r));
   }
-  void Wait(int) override {}  // every call completed before it returned
+  void Wait(int ts) override { core_->Wait(l_, ts); }
   int NumWorkers() override { return core_->N; }
   int NumServers() override { return core_->N; }
   int Rank() override { return core_->ex->rank(l_); }
@@ -310,13 +508,12 @@ class DistWorker : public Store {
   void Barrier() override {
     Req r;
     r.op = kOpBarrier;
-    core_->Round(l_, r);
+    core_->Wait(l_, core_->Enqueue(l_, std::move(r)));
   }
 
  private:
   GpuDistStore::Core* core_;
   int l_;
-  int time_ = 0;
 };
 
 // Store::Create's product under a distributed launch: worker 0 of a GpuDistStore it owns
@@ -351,12 +548,13 @@ GpuDistStore::GpuDistStore(std::unique_ptr<Core> core) : core_(std::move(core)) 
   for (int l = 0; l < core_->L; ++l) core_->workers.emplace_back(new DistWorker(core_.get(), l));
 }
 
-GpuDistStore::~GpuDistStore() {}
+GpuDistStore::~GpuDistStore() { core_->Stop(); }
 
 std::shared_ptr<GpuDistStore> GpuDistStore::CreateLoopback(int nshards, const KWArgs& kwargs) {
   DFX_HOST_CHECK(nshards >= 1, "GpuDistStore: nshards >= 1");
   std::unique_ptr<Core> c(new Core());
   const std::string kw = CtxKw(kwargs);
+  c->lockstep = LockstepOf(kwargs);
   c->ctxs.assign(nshards, nullptr);
   for (auto& h : c->ctxs) DfxCheck(dfx_ctx_create(0, kw.c_str(), &h), "dfx_ctx_create");
   c->ex = MakeLoopbackExchange(c->ctxs);
@@ -376,6 +574,7 @@ std::shared_ptr<GpuDistStore> GpuDistStore::CreateRccl(const KWArgs& kwargs) {
     id_file = std::string("/tmp/dfx_comm_") + (port ? port : "0");
   }
   std::unique_ptr<Core> c(new Core());
+  c->lockstep = LockstepOf(kwargs);
   c->ctxs.assign(1, nullptr);
   DfxCheck(dfx_ctx_create(local, CtxKw(kwargs).c_str(), &c->ctxs[0]), "dfx_ctx_create");
   c->ex = MakeRcclExchange(c->ctxs[0], rank, world, id_file);

@@ -2,23 +2,33 @@
 // interface (include/difacto/store.h:55-83), over the sharded store's device phases
 // (dfx_dist_*, include/difacto_amd.h) and a ShardExchange (dist_host.h).
 //
-// A worker calls Push / Pull exactly as SGDLearner::IterateData does (sgd_learner.cc:201-317):
-// Push(kFeaCount) + Wait, Pull(kWeight), Push(kGradient).  Each call is one exchange round among
-// all workers, so the workers issue the same sequence of calls (an idle worker passes an empty
-// key list).  Every call completes before it returns (on_complete runs inline; Wait is a no-op):
+// Push / Pull enqueue a request and return a timestamp (KVWorker semantics): one progress
+// thread per process serves the queues in rounds among all processes and then runs the
+// request's callback (on_complete); Wait(ts) blocks until the request is done.  A round serves
+// one kind of request, as one exchange among all shards:
 //   Push(kFeaCount)  keys + counts all-to-all-v to their owners, owner_begin with the counts
 //                    (HandlePush -> Update(kFeaCount), kvstore_dist.h:158-165)
 //   Pull(kWeight)    keys to their owners, owner_begin + owner_pull, records back, the worker's
 //                    vals / lens in Get layout (HandlePull -> Get, kvstore_dist.h:167-175)
 //   Push(kGradient)  keys and gradient records to their owners, owner_push
+// A worker's requests are served in the order it issued them, except that a request issued
+// by a callback of its own goes first (the pull's callback pushes the gradient: the sequential
+// order count(k), pull(k), grad(k), count(k+1) even when the reader thread queued count(k+1)
+// meanwhile) — so SGDLearner::IterateData (sgd_learner.cc:201-317) drives it unchanged, reader
+// and executor threads included.
+// kwarg store_sync:
+//   lockstep (default)  a kind is served when every worker has one queued (the synchronous
+//                       step): every worker issues the same sequence of calls,
+//                       an idle worker empty ones
+//   async               each worker's next request is served as it comes (ps-lite's arrival
+//                       order): workers may hold different numbers of batches
 // The update aggregation follows the contexts' push_agg kwarg: sum (one Update per key on the
-// workers' summed gradients, InitV ranked over all owners) or ranks (KVStoreDist: one Update per
-// pushing worker, in rank order).
+// served workers' summed gradients, InitV ranked over all owners) or ranks (KVStoreDist: one
+// Update per pushing worker, in rank order).
 //
 // One process per GPU (RCCL, Store::Create under a distributed launch) holds one worker; a
-// loopback store holds N workers in one process (tests on one GPU): each worker is used by
-// its own thread, and the last of the N calls of a round runs the round for all of them.
-// The worker's arrays are host SArrays (the reference's), so this path is PCIe-inclusive.
+// loopback store holds N workers in one process (tests on one GPU).  The worker's arrays are
+// host SArrays (the reference's), so this path is PCIe-inclusive.
 #ifndef DIFACTO_AMD_HOST_DIST_STORE_H_
 #define DIFACTO_AMD_HOST_DIST_STORE_H_
 

@@ -1,6 +1,8 @@
 // gpu_adapters.cc — see gpu_adapters.h.
 #include "gpu_adapters.h"
 
+#include <cstdlib>
+
 #include <iterator>
 
 #include "reader.h"
@@ -376,11 +378,17 @@ GpuSGDLearner::GpuSGDLearner(const KWArgs& kwargs, std::shared_ptr<Store> store)
   KWArgs mine;
   KWArgs rest = Consume(kwargs, {"fused", "loss", "device"}, &mine);
   std::string loss = "fm";
-  int device = 0;
+  int device = -1;
   for (const auto& p : mine) {
     if (p.first == "fused") fused_ = std::stoi(p.second) != 0;
     if (p.first == "loss") loss = p.second;
     if (p.first == "device") device = std::stoi(p.second);
+  }
+  if (device < 0) {
+    // under a distributed launch the store's shard is on LOCAL_RANK (CreateStore /
+    // GpuDistStore::CreateRccl): the learner's Localizer and loss default to the same GPU
+    const char* lr = std::getenv("LOCAL_RANK");
+    device = (store && lr) ? std::atoi(lr) : 0;
   }
   DFX_HOST_CHECK(loss == "fm" || loss == "logit", "unknown loss type " + loss);
   if (store) {
@@ -468,7 +476,8 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   if (push_cnt) store_->Wait(store_->Push(keys, Store::kFeaCount, SArray<real_t>(feacnt), {}));
   SArray<real_t> values;
   SArray<int> lengths;
-  store_->Pull(keys, Store::kWeight, &values, V_dim_ > 0 ? &lengths : nullptr);
+  // (a StoreGPU pull completes inline; a GpuDistStore pull when its round has run)
+  store_->Wait(store_->Pull(keys, Store::kWeight, &values, V_dim_ > 0 ? &lengths : nullptr));
   dmlc::RowBlock<unsigned> blk = data.GetBlock();
   if (blk.size == 0) {
     // a worker with no rows this round (the sharded store's workers call in step): it takes

@@ -17,7 +17,11 @@
 // workers stepping together (an idle worker passes empty batches).  Prints one line per epoch,
 // "epoch E loss L auc A nrows R" summed over the workers, which tests/test_host_cpp.py compares
 // with oracle/dist_oracle.py; model_out: each server saves its part (with aux) to P_part-<rank>.
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 
@@ -271,8 +275,176 @@ static int RunDist(int argc, char** argv) {
   return g_fail ? 1 : 0;
 }
 
+// SGDLearner::IterateData (sgd_learner.cc:201-317) restated over the adapters and a Store, with
+// its threads: this thread is the reader — it localizes each batch, pushes the batch's counts
+// (+ Wait) and issues it; an executor thread pulls with a callback, and the callback (run by the
+// store) predicts, evaluates, computes the AUC and the gradient and pushes it, the batch done
+// when that push completes; at most two batches in flight (batch_tracker.NumRemains() > 1).
+// One deviation: Issue returns once the executor has issued the batch's Pull (the reference's
+// AsyncLocalTracker returns at once), so the count push of the next batch always queues after
+// that pull and a one-worker run is deterministic.
+static Progress IterateDataAsync(Store* store, GpuLocalizer& lc, GpuFMLoss& loss, int V_dim,
+                                 const std::vector<RowSlice>& batches, bool push_cnt) {
+  struct Job {
+    RowBlockContainer<unsigned> data;
+    SArray<feaid_t> feaids;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<Job>> queue;
+  int remains = 0;        // issued, not yet complete
+  bool issued_pull = false, end = false;
+  Progress prog;
+  std::thread executor([&]() {
+    while (true) {
+      std::shared_ptr<Job> job;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&]() { return !queue.empty() || end; });
+        if (queue.empty()) return;
+        job = queue.front();
+        queue.pop_front();
+      }
+      auto values = std::make_shared<SArray<real_t>>();
+      auto lengths = V_dim > 0 ? std::make_shared<SArray<int>>() : nullptr;
+      auto pull_callback = [&, job, values, lengths]() {
+        dmlc::RowBlock<unsigned> data = job->data.GetBlock();
+        SArray<real_t> pred(data.size);
+        SArray<int> w_pos, V_pos;
+        if (lengths) GetPos(*lengths, &w_pos, &V_pos);
+        std::vector<SArray<char>> inputs = {SArray<char>(*values), SArray<char>(w_pos),
+                                            SArray<char>(V_pos)};
+        if (data.size) loss.Predict(data, inputs, &pred);
+        const double l = data.size ? loss.Evaluate(data.label, pred) : 0.0;
+        const double auc = data.size ? loss.AUC(data.label, pred) : 0.0;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          prog.nrows += data.size;
+          prog.loss += l;
+          prog.auc += auc;
+        }
+        SArray<real_t> grads(values->size());
+        inputs.push_back(SArray<char>(pred));
+        if (data.size) loss.CalcGrad(data, inputs, &grads);
+        store->Push(job->feaids, Store::kGradient, grads, lengths ? *lengths : SArray<int>(),
+                    [&]() {
+                      std::lock_guard<std::mutex> lk(mu);
+                      --remains;
+                      cv.notify_all();
+                    });
+      };
+      store->Pull(job->feaids, Store::kWeight, values.get(), lengths.get(), pull_callback);
+      std::lock_guard<std::mutex> lk(mu);
+      issued_pull = true;
+      cv.notify_all();
+    }
+  });
+  for (const RowSlice& b : batches) {
+    auto job = std::make_shared<Job>();
+    auto feaids = std::make_shared<std::vector<feaid_t>>();
+    auto feacnt = std::make_shared<std::vector<real_t>>();
+    lc.Compact(b.blk, &job->data, feaids.get(), push_cnt ? feacnt.get() : nullptr);
+    job->feaids = SArray<feaid_t>(feaids);
+    if (push_cnt)
+      store->Wait(store->Push(job->feaids, Store::kFeaCount, SArray<real_t>(feacnt), {}));
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&]() { return remains <= 1; });  // while (NumRemains() > 1) sleep
+    ++remains;
+    issued_pull = false;
+    queue.push_back(job);
+    cv.notify_all();
+    cv.wait(lk, [&]() { return issued_pull; });
+  }
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&]() { return remains == 0; });  // batch_tracker.Wait()
+    end = true;
+    cv.notify_all();
+  }
+  executor.join();
+  return prog;
+}
+
+// host_tests dist_async <data> shards=N|-1 epochs=E batch_size=B uneven=0|1 [dfx_ctx kwargs,
+// store_sync]: N workers, each running IterateDataAsync (reader + executor threads) over its
+// share of the rows: rows [r n / N, (r + 1) n / N), or (uneven=1) r + 1 parts of N (N + 1) / 2,
+// so the workers hold different numbers of batches (store_sync=async).  Prints
+// "epoch E loss L auc A nrows R" summed over the workers.
+static int RunDistAsync(int argc, char** argv) {
+  RowBlockContainer<feaid_t> data;
+  if (argc < 3 || !ReadLibSVM(argv[2], &data)) return 2;
+  int shards = 1, epochs = 1;
+  bool uneven = false;
+  size_t bs = 10;
+  std::string vdim = "0";
+  KWArgs kw;
+  for (int i = 3; i < argc; ++i) {
+    const std::string a = argv[i];
+    const size_t eq = a.find('=');
+    if (eq == std::string::npos) return 2;
+    const std::string k = a.substr(0, eq), v = a.substr(eq + 1);
+    if (k == "uneven") uneven = std::stoi(v) != 0;
+    else if (k == "shards") shards = std::stoi(v);
+    else if (k == "epochs") epochs = std::stoi(v);
+    else if (k == "batch_size") bs = std::stoul(v);
+    else {
+      if (k == "V_dim") vdim = v;
+      kw.push_back({k, v});
+    }
+  }
+  const char* lr_env = std::getenv("LOCAL_RANK");
+  const int device = shards < 0 && lr_env ? std::atoi(lr_env) : 0;
+  std::shared_ptr<GpuDistStore> ds =
+      shards > 0 ? GpuDistStore::CreateLoopback(shards, kw) : GpuDistStore::CreateRccl(kw);
+  ShardExchange* ex = ds->exchange();
+  const int L = ds->nlocal(), N = ex->nranks();
+  const size_t n = data.Size(), tri = (size_t)N * (N + 1) / 2;
+  const int d = std::stoi(vdim);
+  std::vector<std::unique_ptr<GpuLocalizer>> lcs;
+  std::vector<std::unique_ptr<GpuFMLoss>> losses;
+  for (int l = 0; l < L; ++l) {
+    lcs.emplace_back(new GpuLocalizer(std::make_shared<GpuContext>(
+        device, KWArgs{{"V_dim", vdim}, {"max_keys", "16"}, {"max_vrows", "1"}})));
+    losses.emplace_back(new GpuFMLoss(d == 0));
+    losses.back()->Init({{"V_dim", vdim}, {"device", std::to_string(device)}});
+  }
+  for (int ep = 0; ep < epochs; ++ep) {
+    std::vector<Progress> prog(L);
+    std::vector<std::thread> th;
+    for (int l = 0; l < L; ++l) {
+      th.emplace_back([&, l]() {
+        const size_t r = (size_t)ex->rank(l);
+        const size_t lo = uneven ? n * (r * (r + 1) / 2) / tri : r * n / N;
+        const size_t hi = uneven ? n * ((r + 1) * (r + 2) / 2) / tri : (r + 1) * n / N;
+        std::vector<RowSlice> batches;
+        for (size_t b = lo; b < hi; b += bs) batches.push_back(Slice(data, b, std::min(hi, b + bs)));
+        prog[l] = IterateDataAsync(ds->worker(l), *lcs[l], *losses[l], d, batches,
+                                   ep == 0 && d > 0);
+      });
+    }
+    for (auto& t : th) t.join();
+    std::vector<double> sum(3, 0.0);
+    for (const Progress& p : prog) {
+      sum[0] += p.loss;
+      sum[1] += p.auc;
+      sum[2] += p.nrows;
+    }
+    ex->AllReduceSum(&sum);
+    EXPECT(sum[2] == (double)n, "epoch %d nrows %.0f want %zu", ep, sum[2], n);
+    if (ex->rank(0) == 0)
+      std::printf("epoch %d loss %.9e auc %.9e nrows %.0f\n", ep, sum[0], sum[1], sum[2]);
+    std::fflush(stdout);
+  }
+  losses.clear();
+  lcs.clear();
+  ds.reset();
+  std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+  return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "dist") return RunDist(argc, argv);
+  if (argc >= 2 && std::string(argv[1]) == "dist_async") return RunDistAsync(argc, argv);
   if (argc < 2) {
     std::fprintf(stderr, "usage: %s rcv1_100.libsvm\n", argv[0]);
     return 2;

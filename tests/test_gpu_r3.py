@@ -1,0 +1,202 @@
+"""Round-3 GPU tests: the kernel variants added this round against the previous kernels and
+the oracle, and the regression test for round 2's workspace-growth fault.
+
+* k_fm_fwd_fat_pf (context kwarg fwd_lanes = 2 | 4, fat_nb = 4 | 6 | 8): the prefetching fat
+  forward at V_dim 16 must produce predictions BIT-identical to k_fm_fwd_fat's (both sum in
+  the reference's (row, nnz) order, fm_loss.h:67-119) and the same trained model.
+* Workspace growth (DESIGN.md (e), round 2's illegal address): every batch larger than the
+  last regrows the Localizer lane's radix-sort counters; the zeroing must be ordered before
+  the lane's first sort.  Each step is compared with the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from difacto_amd import data as D
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    from difacto_amd import hotpath
+    return hotpath
+
+
+def close(a, b, rtol=1e-5):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    floor = 1e-6 * max(1.0, float(np.max(np.abs(b))) if b.size else 1.0)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(a), np.abs(b)) + floor)
+
+
+def _auc_expect(label, opred, oauc):
+    return O.auc_stable_ties(label, opred) if O.has_ties(opred) else oauc
+
+
+@pytest.mark.parametrize("lanes,nb", [(2, 4), (2, 6), (2, 8), (4, 4), (4, 6), (4, 8)])
+@pytest.mark.parametrize("binary", [True, False])
+def test_prefetch_forward_bit_identical(H, lanes, nb, binary):
+    """Two contexts step the same batches: the default forward and the prefetching one.
+    Ragged rows (empty rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    ca = H.Context(0, max_keys=1 << 16, **cfg)
+    cb = H.Context(0, max_keys=1 << 16, fwd_lanes=lanes, fat_nb=nb, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(3001, 39, 1 << 15, binary=binary, ragged=True, seed=40 + step)
+        if step == 3:  # one long row
+            ids = np.concatenate([blk.ids, np.arange(700, dtype=np.uint64) * 7919])
+            offs = np.concatenate([blk.offs, [blk.offs[-1] + 700]]).astype(np.uint64)
+            vals = None if binary else np.concatenate([blk.vals, np.full(700, .5, np.float32)])
+            blk = D.RowBlock(offs, ids, vals, np.concatenate([blk.labels, [1.0]]))
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=(step < 2), pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=(step < 2), pred=pb)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        qa, qb = H.progress(ca), H.progress(cb)
+        assert np.array_equal(pa.cpu().numpy().view(np.uint32), pb.cpu().numpy().view(np.uint32))
+        assert qa["loss"] == qb["loss"] and qa["auc"] == qb["auc"]
+        assert close(pb.cpu().numpy(), opred, rtol=1e-4)
+        assert abs(qb["loss"] - loss) <= 1e-4 * abs(loss)
+        assert abs(qb["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    va, la = H.Store(ca).pull(ca.tensor(uniq, torch.int64))
+    vb, lb = H.Store(cb).pull(cb.tensor(uniq, torch.int64))
+    assert np.array_equal(la.cpu().numpy(), lb.cpu().numpy())
+    assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
+    ca.close()
+    cb.close()
+
+
+def test_workspace_growth_then_lane_localize(H):
+    """Each batch is ~1.6x the previous one, so every step regrows the Localizer lane's sort
+    counters / look-back words right before the lane sorts with them (round 2's fault: a
+    null-stream memset not ordered against the lane).  Loss, AUC, model size and rand_r state
+    follow the oracle at every step."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    c = H.Context(0, max_keys=1 << 18, **cfg)
+    up = O.Updater(**cfg)
+    rows = 300
+    for step in range(7):
+        blk = D.synthetic(rows, 39, 1 << 17, seed=700 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 3), want_pred=True)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 3))
+        p = H.progress(c)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
+        assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+        rows = rows * 8 // 5
+    s = H.Store(c).stats()
+    assert s["n_keys"] == up.size() and s["seed"] == up.seed
+    c.close()
+
+
+def test_bad_kwargs_rejected(H):
+    from difacto_amd._lib import DfxError
+    for kw in (dict(fat_nb=5), dict(fwd_lanes=3), dict(diag="bogus")):
+        with pytest.raises(DfxError):
+            H.Context(0, V_dim=16, **kw)
+
+
+# ---------------------------------------------------------------- C1 as SURVEY §8(d) pins it
+def test_c1_rcv1_pinned_config(H):
+    """C1 (BASELINE configs[0]): rcv1-100, FM V_dim=2, lr=.02, V_lr=.001,
+    B=100 (the whole file, shuffle=0), 20 epochs, every other key at its default (l1=1, l2=0,
+    V_l2=.01, V_threshold=10, l1_shrk=1, V_init_scale=.01, seed=0).  Per-epoch loss and AUC
+    within 1e-4 of the oracle; the final model within 1e-5 (lens exact)."""
+    rcv1 = D.read_libsvm(_golden("rcv1_100.libsvm")).drop_binary_values()
+    cfg = dict(V_dim=2, lr=.02, V_lr=.001)
+    c = H.Context(0, max_keys=1 << 14, **cfg)
+    up = O.Updater(**cfg)
+    db = H.DeviceRowBlock(c, rcv1)
+    for ep in range(20):
+        loss, auc, opred = up.train_step(rcv1.offs, rcv1.ids, rcv1.vals, rcv1.labels,
+                                         push_cnt=(ep == 0), want_pred=True)
+        H.train_step(c, db, H.kTraining, push_cnt=(ep == 0))
+        p = H.progress(c)
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (ep, p["loss"], loss)
+        assert abs(p["auc"] - _auc_expect(rcv1.labels, opred, auc)) <= 1e-4 * rcv1.size, ep
+    uniq, _, _ = O.localize(rcv1.offs, rcv1.ids)
+    v, l = H.Store(c).pull(c.tensor(uniq, torch.int64))
+    ov, ol = up.get(uniq)
+    assert np.array_equal(l.cpu().numpy(), ol)
+    assert close(v.cpu().numpy(), ov, rtol=1e-5)
+    s = H.Store(c).stats()
+    assert s["seed"] == up.seed and s["n_keys"] == up.size()
+    c.close()
+
+
+def _golden(name):
+    import os
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name)
+
+
+def _gisette_like(rows, seed, lo=200, hi=3000, feats=5000):
+    """gisette_scale-shaped (C1's dataset, not in the container): dense-ish valued rows of
+    hundreds to thousands of nnz over 5000 feature ids, ids ascending inside a row"""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(lo, hi + 1, size=rows)
+    offs = np.zeros(rows + 1, np.uint64)
+    offs[1:] = np.cumsum(lens)
+    ids = np.concatenate([np.sort(rng.choice(feats, size=int(n), replace=False))
+                          for n in lens]).astype(np.uint64)
+    vals = (rng.random(int(offs[-1])) * 2 - 1).astype(np.float32)
+    labels = np.where(rng.random(rows) < .5, 1.0, -1.0).astype(np.float32)
+    return D.RowBlock(offs, ids, vals, labels)
+
+
+def test_gisette_long_rows_predict_calcgrad(H):
+    """Long valued rows (200-3000 nnz, ~9.6 M nnz over 5000 ids), FM V_dim=2 through the
+    interface calls (dfx_fm_predict / dfx_fm_calcgrad): predictions bit-exact, gradients within
+    1e-5 of oracle.fm_predict / fm_calcgrad (spmv.h:107-171, fm_loss.h:67-203)."""
+    blk = _gisette_like(6000, 11)
+    d = 2
+    ou, _, ocol = O.localize(blk.offs, blk.ids)
+    U = len(ou)
+    rng = np.random.default_rng(3)
+    lens = np.where(rng.random(U) < 0.2, 1, d + 1).astype(np.int32)
+    wp, vp = O.get_pos(lens)
+    W = (rng.standard_normal(int(lens.sum())) * 0.01).astype(np.float32)
+    c = H.Context(0)
+    db = H.DeviceRowBlock(c, blk)
+    col, uniq, _ = H.Localizer(c).compact(db)
+    assert np.array_equal(H.u32(col), ocol)
+    loss = H.FMLoss(c, d)
+    tW, twp, tvp = c.tensor(W, torch.float32), c.tensor(wp, torch.int32), c.tensor(vp, torch.int32)
+    pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+    loss.predict(db, col, tW, twp, tvp, pred, U)
+    grad = torch.zeros(len(W), dtype=torch.float32, device=c.device)
+    loss.calc_grad(db, col, tW, twp, tvp, pred, grad, U)
+    opred = O.fm_predict(blk.offs, ocol, blk.vals, W, wp, vp, d)
+    assert np.array_equal(pred.cpu().numpy(), opred)
+    og = O.fm_calcgrad(blk.offs, ocol, blk.vals, blk.labels, None, W, wp, vp, U, d, opred)
+    assert close(grad.cpu().numpy(), og)
+    c.close()
+
+
+def test_gisette_long_rows_fused_steps(H):
+    """The same shape through the fused step (C1's settings, lazy V at V_threshold=10): per-step
+    predictions bit-exact with the oracle's, loss / AUC within 1e-4, model within 1e-5."""
+    cfg = dict(V_dim=2, lr=.02, V_lr=.001)
+    c = H.Context(0, max_keys=1 << 14, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(3):
+        blk = _gisette_like(2000, 20 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step == 0), want_pred=True)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step == 0), pred=pred)
+        p = H.progress(c)
+        assert close(pred.cpu().numpy(), opred, rtol=1e-5), step
+        assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
+        assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    v, l = H.Store(c).pull(c.tensor(uniq, torch.int64))
+    ov, ol = up.get(uniq)
+    assert np.array_equal(l.cpu().numpy(), ol)
+    assert close(v.cpu().numpy(), ov, rtol=1e-5)
+    c.close()

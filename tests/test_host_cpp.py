@@ -368,3 +368,62 @@ def test_dist_store_iterate_data_matches_oracle(tmp_path, shards, agg):
                 assert np.allclose(a[1], b[1], rtol=1e-5, atol=1e-6)
         assert cnt == up.size() > 0
     assert not os.path.exists(str(tmp_path / "id"))
+
+
+def _dist_oracle_epochs(blk, N, bs, epochs, agg, kw):
+    """per-epoch (loss, auc) of the lockstep sharded oracle: worker p trains rows
+    [p n / N, (p + 1) n / N) in batches of bs, the workers stepping together"""
+    from oracle import dist_oracle as DO
+    n = blk.size
+    parts = [list(range(p * n // N, (p + 1) * n // N)) for p in range(N)]
+    nsteps = max((len(p) + bs - 1) // bs for p in parts)
+    so = DO.AggOracle(N, **kw) if agg == "sum" else DO.ShardedOracle(N, **kw)
+    out = []
+    for ep in range(epochs):
+        loss = auc = 0.0
+        for t in range(nsteps):
+            res = so.step([_slice(blk, parts[p][t * bs:(t + 1) * bs]) for p in range(N)],
+                          push_cnt=ep == 0)
+            loss += sum(o[0] for o in res)
+            auc += sum(o[1] for o in res)
+        out.append((loss, auc))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,sync,uneven", [(1, "lockstep", 0), (3, "lockstep", 0),
+                                                (-1, "lockstep", 0), (3, "async", 1)])
+def test_dist_store_async_iterate_data(tmp_path, shards, sync, uneven):
+    """SGDLearner::IterateData with its own threads (host_tests.cc IterateDataAsync: a reader
+    thread that localizes and pushes counts ahead, an executor whose pull callback computes and
+    pushes the gradient, two batches in flight) over GpuDistStore workers:
+    requests queue per worker and one progress thread per process serves them.
+    * lockstep, even parts: the result equals the lockstep oracle (one step per batch index);
+    * async, uneven parts (worker r holds r + 1 sixths of the rows): no worker waits for the
+      others, every row is trained once per epoch, and the loss stays near the lockstep run's
+      (which requests share an update depends on timing, as on ps-lite's server)."""
+    from difacto_amd import data as D
+    N = shards if shards > 0 else 1
+    bs, epochs = 10, 3
+    kw = dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1, seed=7)
+    env = dict(os.environ, DFX_COMM_ID_FILE=str(tmp_path / "id"))
+    r = subprocess.run([BIN, "dist_async", DATA, "shards=%d" % shards, "epochs=%d" % epochs,
+                        "batch_size=%d" % bs, "uneven=%d" % uneven, "max_keys=65536",
+                        "store_sync=" + sync, "push_agg=sum"]
+                       + ["%s=%s" % kv for kv in kw.items()],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL PASSED" in r.stdout, r.stdout
+    got = [l.split() for l in r.stdout.splitlines() if l.startswith("epoch ")]
+    assert len(got) == epochs, r.stdout
+    blk = D.read_libsvm(DATA)
+    want = _dist_oracle_epochs(blk, N, bs, epochs, "sum", kw)
+    for ep in range(epochs):
+        g_loss, g_auc, g_rows = float(got[ep][3]), float(got[ep][5]), float(got[ep][7])
+        assert g_rows == blk.size
+        loss, auc = want[ep]
+        if uneven:
+            assert abs(g_loss - loss) <= 0.05 * abs(loss), (ep, g_loss, loss)
+        else:
+            assert abs(g_loss - loss) <= 1e-5 * abs(loss), (ep, g_loss, loss)
+            assert abs(g_auc - auc) <= 1e-4 * blk.size, (ep, g_auc, auc)
