@@ -34,14 +34,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload: c3 (the metric's, default), c2 (LR V_dim=0, "
+                         "40 valued nnz, 2^20 keys, FTRL L1), c5 (Zipf(1.1) keys, V_dim=128, "
+                         "lazy V), c4shard (one GPU's share of C4: 2^27 keys, V_dim=64)")
     # 100 timed steps: the first step's Localizer (not yet overlapped) and the pipeline's
     # drain are amortised (+2 % over 20 steps, same box); still well under a second of GPU
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=100_000, help="rows per GPU per step")
-    ap.add_argument("--nnz", type=int, default=39)
-    ap.add_argument("--key-bits", type=int, default=24)
-    ap.add_argument("--vdim", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=None, help="rows per GPU per step")
+    ap.add_argument("--nnz", type=int, default=None)
+    ap.add_argument("--key-bits", type=int, default=None)
+    ap.add_argument("--vdim", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sharded", action="store_true",
                     help="use the key-range-sharded store even at N=1 (default for N>1)")
@@ -82,38 +86,81 @@ def parse():
                          "sort_pack=0)")
     ap.add_argument("--cpu-rows", type=int, default=200_000)
     ap.add_argument("--cpu-batch", type=int, default=10_000)
-    return ap.parse_args()
+    args = ap.parse_args()
+    cf = CONFIGS[args.config]
+    for k in ("batch", "nnz", "key_bits", "vdim"):
+        if getattr(args, k) is None:
+            setattr(args, k, cf[k])
+    return args
+
+
+# BASELINE.json configs (SURVEY.md §8(d) shapes).  keys: rows per step, nnz per row, key space
+# bits, V_dim, valued data, Zipf exponent (None: uniform ids), the updater's .conf keys
+CONFIGS = {
+    "c3": dict(batch=100_000, nnz=39, key_bits=24, vdim=16, valued=False, zipf=None,
+               upd=dict(V_threshold=0, l1=0, lr=.1, V_lr=.01),
+               name="C3 Criteo-shaped FM V_dim=%(vdim)d, %(nnz)d binary nnz/row, 2^%(key_bits)d "
+                    "keys, l1=0 V_threshold=0"),
+    "c2": dict(batch=100_000, nnz=40, key_bits=20, vdim=0, valued=True, zipf=None,
+               upd=dict(l1=1, l2=0, lr=.1),
+               name="C2 LR-only (V_dim=0) FTRL L1 (l1=1), %(nnz)d valued nnz/row, 2^%(key_bits)d "
+                    "keys"),
+    "c5": dict(batch=100_000, nnz=39, key_bits=24, vdim=128, valued=False, zipf=1.1,
+               upd=dict(lr=.05, V_lr=.01),
+               name="C5 Zipf(1.1) keys over [1, 2^%(key_bits)d], FM V_dim=%(vdim)d, %(nnz)d binary "
+                    "nnz/row, defaults (V_threshold=10, l1=1, l1_shrk): lazy V for hot keys"),
+    "c4shard": dict(batch=100_000, nnz=39, key_bits=27, vdim=64, valued=False, zipf=None,
+                    upd=dict(V_threshold=0, l1=0, lr=.1, V_lr=.01),
+                    name="C4 one GPU's share: 2^%(key_bits)d keys (2^30 over 8 GPUs), FM "
+                         "V_dim=%(vdim)d, %(nnz)d binary nnz/row, l1=0 V_threshold=0, fused step"),
+}
 
 
 class DevBatch:
-    """A synthetic RowBlock generated directly in HBM (torch is only the allocator/RNG)."""
+    """A synthetic RowBlock generated directly in HBM (torch is only the allocator/RNG).
+    Uniform ids ~ U[0, 2^key_bits) on the device; Zipf(s) ids over [1, 2^key_bits] drawn on the
+    host (difacto_amd.data.zipf_keys) and copied once, before timing.  valued: x ~ U(0, 1]."""
 
-    def __init__(self, torch, dev, B, k, key_bits, seed):
+    def __init__(self, torch, dev, B, k, key_bits, seed, valued=False, zipf=None):
         g = torch.Generator(device=dev)
         g.manual_seed(seed)
         self.size = B
         self.nnz = B * k
-        self.ids = torch.randint(0, 1 << key_bits, (self.nnz,), device=dev, generator=g,
-                                 dtype=torch.int64)
+        if zipf is None:
+            self.ids = torch.randint(0, 1 << key_bits, (self.nnz,), device=dev, generator=g,
+                                     dtype=torch.int64)
+        else:
+            from difacto_amd import data as D
+            ids = D.zipf_keys(np.random.default_rng(seed), self.nnz, zipf, 1 << key_bits)
+            self.ids = torch.from_numpy(ids.view(np.int64)).to(dev)
         self.offs = torch.arange(0, self.nnz + 1, k, device=dev, dtype=torch.int64)
         r = torch.rand(B, device=dev, generator=g)
         self.labels = torch.where(r < 0.25, 1.0, -1.0).to(torch.float32)
-        self.vals = None
+        self.vals = (1.0 - torch.rand(self.nnz, device=dev, generator=g)) if valued else None
         self.weights = None
 
     def as_batch(self):
         from difacto_amd import _lib
         import ctypes
         return _lib.Batch(self.size, self.nnz, ctypes.c_void_p(self.offs.data_ptr()),
-                          ctypes.c_void_p(self.ids.data_ptr()), None,
+                          ctypes.c_void_p(self.ids.data_ptr()),
+                          ctypes.c_void_p(self.vals.data_ptr()) if self.vals is not None else None,
                           ctypes.c_void_p(self.labels.data_ptr()), None)
 
 
-def algorithmic_bytes(B, nnz, U, d):
-    """Essential HBM bytes per launch, binary data, all V live."""
-    # forward (probe mode): per nnz its id and its key's {w, vrow} entry bytes, then V
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + 4 * d)
-    bwd = U * (8 + 4 + 8 + 32 + 16 * d + 4) + nnz * (4 + 4 + 4 + 4 * d)
+def algorithmic_bytes(B, nnz, U, d, valued=False, U_V=None, occ_V=None):
+    """Essential HBM bytes per launch.  U_V: keys with live V, occ_V:
+    their occurrences (dfx_prof_counts; default: every key has V); valued: + the value per nnz
+    in the forward and per occurrence in the backward"""
+    if U_V is None or occ_V is None:
+        U_V, occ_V = U, nnz
+    x = 4 if valued else 0
+    # forward (probe mode): per row offset / label / pred / p / XV*p, per nnz its id and its
+    # key's {w, vrow} entry bytes (+ value), per nnz of a key with V its V row
+    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + x) + occ_V * 4 * d
+    # backward: per key its segment start, key, entry read + written, slot; per key with V its
+    # V and Vaux read + written; per occurrence its row, p (+ value), and XV*p row when V
+    bwd = U * (8 + 4 + 8 + 32 + 4) + U_V * 16 * d + nnz * (4 + 4 + 4 + x) + occ_V * 4 * d
     return {"forward": fwd, "backward_update": bwd}
 
 
@@ -165,6 +212,21 @@ def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
     return None
 
 
+def pmc_requests(kernel_prefix, fname="pmc_requests.json"):
+    """the L2's memory-side read / write requests per launch of a kernel (a separate --pmc pass,
+    profiles/<PMC_ROUND>/pmc_requests.json), or None"""
+    path = os.path.join(ROOT, "profiles", PMC_ROUND, fname)
+    try:
+        with open(path) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, v in ks.items():
+        if name.startswith(kernel_prefix):
+            return v
+    return None
+
+
 def sharded_traffic():
     """the a2a sharded worker's forward + backward (record mode) HBM bytes per step (round 1's
     passes: the a2a schedule is unchanged since)"""
@@ -180,6 +242,31 @@ def sharded_traffic():
             return None
         tot += int((v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]) * 1024)
     return tot
+
+
+def forward_roofline(fwd_bytes, fwd_ms, config):
+    """The forward's fraction of the byte peak (its phase time from the diagnostic pass, which
+    runs beside the Localizer lane as the timed steps do) and its HBM traffic.  FETCH_SIZE counts
+    a 128-byte memory request at 64 B on gfx950 (MI355X_MICROARCH.md §HBM); the fat forward reads
+    its slots as 128-B requests, so the corrected read traffic is the L2's memory-side read
+    requests x 128 B (an upper bound: some requests are 64 B)"""
+    achieved = fwd_bytes / (max(fwd_ms, 1e-9) * 1e-3) / 1e9
+    out = {"bound": "hbm", "kernel": "forward", "achieved": round(achieved, 1),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_launch": int(fwd_bytes), "launch_ms": round(fwd_ms, 4),
+           "traffic": None}
+    if config != "c3":
+        return out
+    raw = pmc_traffic("k_fm_fwd")
+    req = pmc_requests("k_fm_fwd")
+    if raw is not None:
+        out["traffic_fetch_write_raw"] = raw
+    if req is not None:
+        out["traffic"] = int(req["rdreq_per_launch"] * 128 + req["wrreq_per_launch"] * 64)
+        out["traffic_source"] = ("profiles/%s/pmc_requests.json: TCC_EA0_RDREQ x 128 B + "
+                                 "TCC_EA0_WRREQ x 64 B per launch (the guide's 128-B request "
+                                 "correction)" % PMC_ROUND)
+    return out
 
 
 def cpu_baseline(args):
@@ -258,10 +345,13 @@ def main():
         return
 
     B, k, kb, d = args.batch, args.nnz, args.key_bits, args.vdim
+    cf = CONFIGS[args.config]
     keyspace = 1 << kb
     extra = dict(kv.split("=", 1) for kv in args.ctx.split(",") if kv)
-    ctx = H.Context(local, V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01,
-                    max_keys=keyspace, max_vrows=keyspace, **extra)
+    upd = dict(cf["upd"], **{kk: v for kk, v in extra.items() if kk in cf["upd"]})
+    extra = {kk: v for kk, v in extra.items() if kk not in upd}
+    ctx = H.Context(local, V_dim=d, max_keys=keyspace, max_vrows=keyspace if d > 0 else 0,
+                    **upd, **extra)
     ctx.reserve(B, B * k)
     lib = H._lib.lib()
 
@@ -277,9 +367,19 @@ def main():
     if not os.environ.get("DFX_SERIAL"):
         ctx.set_input_stream(loader)
 
+    zipf_pool = {}
+
     def make(seed):
+        if cf["zipf"] is not None:
+            # host-drawn Zipf ids: a pool of 8 batches, reused (drawing takes ~0.3 s each)
+            seed = seed % 8
+            if seed not in zipf_pool:
+                with torch.cuda.stream(loader):
+                    zipf_pool[seed] = DevBatch(torch, dev, B, k, kb, seed, cf["valued"],
+                                               cf["zipf"])
+            return zipf_pool[seed]
         with torch.cuda.stream(loader):
-            return DevBatch(torch, dev, B, k, kb, seed=seed)
+            return DevBatch(torch, dev, B, k, kb, seed, cf["valued"])
 
     # untimed epoch 0: touch the key space with count pushes (all keys end up with V)
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (B * k)))
@@ -321,6 +421,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    counts = H.prof_counts(ctx)
     phases, nrec, mean_u = H.prof_read(ctx)
     bwd_ms = phases["backward_update"]
     prog = H.progress(ctx)
@@ -339,7 +440,7 @@ def main():
 
     value = world * B * args.steps / elapsed
     per_launch_ms = {p: phases[p] / max(nrec, 1) for p in phases}
-    ab = algorithmic_bytes(B, B * k, mean_u, d)
+    ab = algorithmic_bytes(B, B * k, mean_u, d, cf["valued"], counts["U_V"], counts["occ_V"])
     dom = max(ab, key=lambda p: per_launch_ms[p])
     achieved = ab[dom] / (max(per_launch_ms[dom], 1e-9) * 1e-3) / 1e9
     out = {
@@ -355,15 +456,18 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (device-generated, resident in HBM before timing)",
-        "config": {"workload": "C3 Criteo-shaped FM V_dim=%d, %d binary nnz/row, 2^%d keys, "
-                               "l1=0 V_threshold=0, fused dfx_train_step" % (d, k, kb),
+        "config": {"workload": (cf["name"] % dict(vdim=d, nnz=k, key_bits=kb))
+                               + ", fused dfx_train_step",
+                   "config": args.config,
                    "rows_per_gpu_step": B, "global_batch": B * world,
                    "parallelism": "single GPU"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic("k_fm_bwd" if dom == "backward_update"
-                                            else "k_fm_fwd"),
+                                            else "k_fm_fwd",
+                                            "pmc_hbm.json" if args.config == "c3"
+                                            else "pmc_hbm_%s.json" % args.config),
                      "traffic_source": "profiles/%s/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
                                        "WRITE_SIZE per launch; request counts per key / nnz "
                                        "in profiles/%s/pmc_requests.json); counters "
@@ -372,16 +476,21 @@ def main():
                                        "counted exactly, factor 1.00)" % (PMC_ROUND, PMC_ROUND),
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
+        "roofline_forward": forward_roofline(ab["forward"], per_launch_ms["forward"],
+                                             args.config),
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
-        "chunk_model": chunk_model(B * k, mean_u, elapsed / args.steps * 1e3),
+        "mean_live_v_keys": round(counts["U_V"], 1),
+        "mean_live_v_occurrences": round(counts["occ_V"], 1),
+        "chunk_model": (chunk_model(B * k, mean_u, elapsed / args.steps * 1e3)
+                        if args.config == "c3" else None),
         "train_loss_per_row": round(prog["loss"] / max(prog["nrows"], 1), 6),
         "train_auc": round(prog["auc"] / max(prog["nrows"], 1), 6),
         "model_keys": st["n_keys"], "model_vrows": st["n_vrows"],
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -416,9 +525,19 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     loader = torch.cuda.Stream(device=dev)
     ctx.set_input_stream(loader)
 
+    zipf_pool = {}
+
     def make(seed):
+        if cf["zipf"] is not None:
+            # host-drawn Zipf ids: a pool of 8 batches, reused (drawing takes ~0.3 s each)
+            seed = seed % 8
+            if seed not in zipf_pool:
+                with torch.cuda.stream(loader):
+                    zipf_pool[seed] = DevBatch(torch, dev, B, k, kb, seed, cf["valued"],
+                                               cf["zipf"])
+            return zipf_pool[seed]
         with torch.cuda.stream(loader):
-            return DevBatch(torch, dev, B, k, kb, seed=seed)
+            return DevBatch(torch, dev, B, k, kb, seed, cf["valued"])
 
     host_t = None
     if os.environ.get("DFX_HOSTTIME"):  # host seconds per call of each shard / comm method

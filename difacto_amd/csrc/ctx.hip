@@ -166,7 +166,8 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "auc_sort") {
       if (v == "radix") kw->auc_radix = 1;
       else if (v == "merge") kw->auc_radix = 0;
-      else { set_error("unknown auc_sort: " + v + " (radix|merge)"); return DFX_ERR_ARG; }
+      else if (v == "block") kw->auc_radix = 2;
+      else { set_error("unknown auc_sort: " + v + " (radix|merge|block)"); return DFX_ERR_ARG; }
     }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
@@ -275,6 +276,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->dist_sum = kw.dist_sum;
   c->sort_pack = kw.sort_pack;
   c->auc_radix = kw.auc_radix != 0;
+  c->auc_block = kw.auc_radix == 2;
   c->sort_items = kw.sort_items;
   c->sort_lookback = kw.sort_lookback;
   c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);

@@ -845,7 +845,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   __shared__ int red[kFmNT / kWave];
   __shared__ int redn[kFmNT / kWave];
   __shared__ int redi[kFmNT / kWave];
+  __shared__ unsigned redl[kFmNT / kWave], redo[kFmNT / kWave];
   int dnew = 0, ninit = 0, nins = 0;
+  unsigned nlive = 0, nlocc = 0;  // keys with V in this step, and their occurrences (roofline)
   if (u < nseg) {
     const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
@@ -1107,6 +1109,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         // InitV's slot: it reads the slots of flagged keys only (in the steady state none)
         if (need && a.insert_keys) a.slot[cidx] = sl;
         ninit = need ? 1 : 0;
+        nlive = vq >= 0 ? 1u : 0u;
+        nlocc = vq >= 0 ? len : 0u;
       }
     }
   }
@@ -1116,23 +1120,32 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       dnew += __shfl_xor(dnew, off, kWave);
       ninit += __shfl_xor(ninit, off, kWave);
       nins += __shfl_xor(nins, off, kWave);
+      nlive += __shfl_xor(nlive, off, kWave);
+      nlocc += __shfl_xor(nlocc, off, kWave);
     }
     if (lane_id() == 0) {
       red[threadIdx.x / kWave] = dnew;
       redn[threadIdx.x / kWave] = ninit;
       redi[threadIdx.x / kWave] = nins;
+      redl[threadIdx.x / kWave] = nlive;
+      redo[threadIdx.x / kWave] = nlocc;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
       int s = 0, q = 0, i2 = 0;
+      unsigned long long lv = 0, lo = 0;
       for (int i = 0; i < kFmNT / kWave; ++i) {
         s += red[i];
         q += redn[i];
         i2 += redi[i];
+        lv += redl[i];
+        lo += redo[i];
       }
       if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
       if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
       if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
+      if (lv) atomicAdd(&a.dsw->live_keys, lv);
+      if (lo) atomicAdd(&a.dsw->live_occ, lo);
     }
   }
 }

@@ -65,6 +65,8 @@ struct DevState {
   double auc_n;                // AUC * n of the current step
   double sum_u;                // sum of U over dfx_train_step calls (roofline bytes)
   double n_steps;
+  unsigned long long live_keys;  // fused backward: keys with live V, summed over steps
+  unsigned long long live_occ;   // ... and their occurrences (the forward's V gathers)
   double scratch[8];
   unsigned int iv_ticket;      // the one-launch InitV's tile tickets (reset by k_step_finalize)
   unsigned int iv_epoch;       // its look-back words' tag (advanced by k_step_finalize)
@@ -200,6 +202,7 @@ struct Context {
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
+  bool auc_block = false;  // auc_sort=block: the AUC lane in one workgroup
   int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)
   int sort_lookback = 4;  // the Localizer sort's look-back step width (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
@@ -385,11 +388,14 @@ int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_
 int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uniq,
                    uint32_t* segslot);
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
-            bool radix);
+            bool radix, bool block = false);
 // the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream
 int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred);
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix);
+// the same, auc_sort=block: the whole AUC in one 1024-thread workgroup (metric.hip k_auc_block)
+int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix,
+               bool block);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

@@ -314,7 +314,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   lane_mark(c, 2, c->aux_stream);
-  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
+  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix, c->auc_block));
   lane_mark(c, 3, c->aux_stream);
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   prof_mark(c, 5);
@@ -389,6 +389,26 @@ extern "C" int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask)
 // after dfx_prof_read: out[4] = mean ms of the Localizer lane per batch, of its start after
 // the context stream reached that batch (negative: it ran ahead), of its end after that point
 // (positive: the exposed wait), and of the AUC lane
+// out[3]: per dfx_train_step since the last call, the mean number of unique keys, of keys with
+// live V (their V is read and updated) and of those keys' occurrences; resets the counters
+extern "C" int dfx_prof_counts(dfx_ctx* ctx, double* out) {
+  DFX_CHECK_ARG(ctx && out, "bad argument");
+  Context* c = &ctx->c;
+  double h[2];
+  unsigned long long lv[2];
+  DFX_HIP(hipMemcpyAsync(h, &c->ds->sum_u, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipMemcpyAsync(lv, &c->ds->live_keys, sizeof(lv), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  const double n = h[1] > 0 ? h[1] : 1;
+  out[0] = h[0] / n;
+  out[1] = (double)lv[0] / n;
+  out[2] = (double)lv[1] / n;
+  DFX_HIP(hipMemsetAsync(&c->ds->sum_u, 0, sizeof(h), c->stream));
+  DFX_HIP(hipMemsetAsync(&c->ds->live_keys, 0, sizeof(lv), c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
+  return DFX_OK;
+}
+
 extern "C" int dfx_prof_lanes(dfx_ctx* ctx, double* out) {
   DFX_CHECK_ARG(ctx && out, "bad argument");
   for (int i = 0; i < 4; ++i) out[i] = ctx->c.lane_stats[i];
@@ -428,10 +448,12 @@ extern "C" int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mea
   if (n_steps) *n_steps = c->prof_n;
   c->prof_n = 0;
   double h[2];
-  DFX_HIP(hipMemcpy(h, &c->ds->sum_u, sizeof(h), hipMemcpyDeviceToHost));
+  DFX_HIP(hipMemcpyAsync(h, &c->ds->sum_u, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  DFX_HIP(hipStreamSynchronize(c->stream));
   if (mean_u) *mean_u = h[1] > 0 ? h[0] / h[1] : 0;
   // the counters are the context stream's (k_step_finalize): zeroed in its order
   DFX_HIP(hipMemsetAsync(&c->ds->sum_u, 0, sizeof(h), c->stream));
+  DFX_HIP(hipMemsetAsync(&c->ds->live_keys, 0, 2 * sizeof(unsigned long long), c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;
 }

@@ -283,6 +283,14 @@ def prof_read(ctx):
     return dict(zip(PHASES, list(ms))), n.value, mu.value
 
 
+def prof_counts(ctx):
+    """per step since the last call (or prof_read): mean unique keys, keys with live V and
+    their occurrences; resets"""
+    out = (ctypes.c_double * 3)()
+    check(_lib.lib().dfx_prof_counts(ctx.h, out))
+    return dict(zip(("U", "U_V", "occ_V"), list(out)))
+
+
 def prof_lanes(ctx):
     """after prof_read: mean ms per batch of the Localizer lane, its start / end relative to
     the main stream reaching the batch, and the AUC lane"""

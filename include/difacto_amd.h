@@ -227,6 +227,9 @@ int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
  * end relative to the context stream reaching that batch (start < 0: it ran ahead; end > 0:
  * the exposed wait), and of the AUC lane */
 int dfx_prof_lanes(dfx_ctx* ctx, double* out);
+/* out[3] = per dfx_train_step since the last call (or dfx_prof_read): the mean number of
+ * unique keys, of keys with live V and of their occurrences (the roofline's bytes); resets */
+int dfx_prof_counts(dfx_ctx* ctx, double* out);
 
 /* ---- key-range-sharded store over N GPUs (KVStoreDist, src/store/kvstore_dist.h) --------
  * Every rank is a worker (its own batch) and the server of the keys with

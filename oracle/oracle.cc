@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <fstream>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
@@ -475,6 +476,29 @@ int orc_updater_save(void* h, const char* path, int save_aux) {
   }
   fclose(f);
   return 0;
+}
+
+// SGDUpdater::Dump (sgd_updater.h:108-139): one text line per non-empty entry, fields
+// tab-separated, floats through an ostream's default formatting (as dmlc::ostream does)
+int orc_updater_dump(void* h, const char* path, int dump_aux, int need_reverse) {
+  Updater* up = static_cast<Updater*>(h);
+  std::ofstream os(path);
+  if (!os) { g_err = "cannot open file"; return -1; }
+  for (const auto& it : up->model) {
+    const Entry& e = it.second;
+    if (e.empty()) continue;
+    os << (need_reverse ? ReverseBytes(it.first) : it.first);
+    os << '\t' << e.size << '\t' << e.w;
+    if (dump_aux) os << '\t' << e.sqrt_g << '\t' << e.z;
+    if (e.size > 1) {
+      const int n = e.size - 1;
+      for (int i = 0; i < n; ++i) os << '\t' << e.V[i];
+      if (dump_aux)
+        for (int i = n; i < 2 * n; ++i) os << '\t' << e.V[i];
+    }
+    os << '\n';
+  }
+  return os.good() ? 0 : -1;
 }
 
 // SGDUpdater::Load (sgd_updater.h:84-96 + SGDEntry::LoadEntry :50-68).

@@ -67,6 +67,9 @@ def lib():
         L.orc_updater_entry.restype = ctypes.c_int
         L.orc_updater_entry.argtypes = [ctypes.c_void_p, ctypes.c_uint64, f32p, f32p,
                                         ctypes.POINTER(ctypes.c_int)]
+        L.orc_updater_dump.restype = ctypes.c_int
+        L.orc_updater_dump.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int,
+                                       ctypes.c_int]
         L.orc_updater_save.restype = ctypes.c_int
         L.orc_updater_save.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.orc_updater_load.restype = ctypes.c_int
@@ -247,6 +250,11 @@ class Updater:
 
     def save(self, path, save_aux=True):
         if lib().orc_updater_save(self.h, path.encode(), int(save_aux)) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+
+    def dump(self, path, dump_aux=False, need_reverse=False):
+        """SGDUpdater::Dump (sgd_updater.h:108-139): text, one line per non-empty entry"""
+        if lib().orc_updater_dump(self.h, path.encode(), int(dump_aux), int(need_reverse)) != 0:
             raise RuntimeError(lib().orc_last_error().decode())
 
     def load(self, path):
