@@ -408,10 +408,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    H.prof_host(ctx)
     t0 = time.perf_counter()
     for bt in batches:
         step(bt, False)
     t_enq = time.perf_counter() - t0
+    host_wait = H.prof_host(ctx)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -421,7 +423,6 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    counts = H.prof_counts(ctx)
     phases, nrec, mean_u = H.prof_read(ctx)
     bwd_ms = phases["backward_update"]
     prog = H.progress(ctx)
@@ -430,6 +431,7 @@ def main():
     for bt in batches:
         step(bt, False)
     torch.cuda.synchronize()
+    counts = H.prof_counts(ctx)  # live-V keys / occurrences, counted in the diagnostic pass
     phases, nrec_diag, _ = H.prof_read(ctx)
     phases = {p: v * nrec / max(nrec_diag, 1) for p, v in phases.items()}  # per timed step
     phases["backward_update"] = bwd_ms
@@ -480,6 +482,10 @@ def main():
                                              args.config),
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
+        # the host's own work per step: the calls' time less their waits on the capacity guard
+        # (which lets the host run a few steps ahead of the device, then blocks it)
+        "host_busy_ms_per_step": round((t_enq - host_wait["wait_s"]) / args.steps * 1e3, 4),
+        "host_waits": host_wait["waits"],
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
         "mean_live_v_keys": round(counts["U_V"], 1),

@@ -52,6 +52,7 @@ _SIGS = {
     "dfx_ctx_set_input_stream": (ctypes.c_int, [vp, vp]),
     "dfx_prof_lanes": (ctypes.c_int, [vp, f64p]),
     "dfx_prof_counts": (ctypes.c_int, [vp, f64p]),
+    "dfx_prof_host": (ctypes.c_int, [vp, f64p]),
     "dfx_ctx_vdim": (ctypes.c_int, [vp]),
     "dfx_sync": (ctypes.c_int, [vp]),
     "dfx_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),

@@ -1144,8 +1144,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
       if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
       if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
-      if (lv) atomicAdd(&a.dsw->live_keys, lv);
-      if (lo) atomicAdd(&a.dsw->live_occ, lo);
+      if (a.live_part) a.live_part[blockIdx.x] = make_uint2((unsigned)lv, (unsigned)lo);
     }
   }
 }
@@ -1260,6 +1259,48 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
 
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds) {
   return launch_bwd<true>(a, nseg_bound, st, true, lds);
+}
+
+// blocks of the fused backward over nseg_bound keys (the size of BwdArgs::live_part)
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound) {
+  int G, CPL;
+  bool vec;
+  lanes_for(d, true, &G, &CPL, &vec);
+  const int64_t spb = kFmNT / G;
+  return (nseg_bound + spb - 1) / spb;
+}
+
+// the diagnostic live-V counts of one backward: its blocks' partials into the counters
+__global__ void k_sum_live(const uint2* part, int64_t n, DevState* ds) {
+  __shared__ unsigned long long r0[1024 / kWave], r1[1024 / kWave];
+  unsigned long long a = 0, b = 0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    a += part[i].x;
+    b += part[i].y;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off, kWave);
+    b += __shfl_xor(b, off, kWave);
+  }
+  if (lane_id() == 0) {
+    r0[threadIdx.x / kWave] = a;
+    r1[threadIdx.x / kWave] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x / kWave); ++i) {
+      a += r0[i];
+      b += r1[i];
+    }
+    ds->live_keys += a;
+    ds->live_occ += b;
+  }
+}
+
+int sum_live(const uint2* part, int64_t n, DevState* ds, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_live, dim3(1), dim3(1024), 0, st, part, n, ds);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
 }
 
 // sharded store: per-key gradient records in the pulled-record layout (aligned rows)

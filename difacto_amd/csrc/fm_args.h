@@ -104,6 +104,10 @@ struct BwdArgs {
   Params Pm;
   uint32_t* flags;  // InitV request per key
   DevState* dsw;
+  // (diagnostic) per block {keys with live V, their occurrences}: plain stores, summed by
+  // k_sum_live only when dfx_prof_counts is being fed (same-address atomics from every block
+  // serialise at one L2 channel: they tripled the backward)
+  uint2* live_part;
   // long segments (chunk_plan): first chunk of each segment, segment of each chunk, the
   // chunk count (device) and the chunks' partials [g_w, XXp, sum (XV p) x (d)] in double
   const uint32_t* choff;
@@ -119,6 +123,8 @@ int xvp_stride(const Context* c);
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread = true);
 // fused backward + FTRL/AdaGrad update over at most nseg_bound segments; lds: bytes of LDS
 // reserved per block (-1: the default cap)
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound);
+int sum_live(const uint2* part, int64_t n, DevState* ds, hipStream_t st);
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds = -1);
 // the chunk partials of long segments (before the backward reads them)
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st);

@@ -91,6 +91,7 @@ struct Workspace {
   DevBuf ak0, ak1, av0, av1;  // AUC sort buffers (keys, labels; double-buffered)
   DevBuf dscratch;  // double partials
   DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
+  DevBuf live;      // (diagnostic) the fused backward's per-block live-V counts
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
   DevBuf os;
@@ -208,6 +209,9 @@ struct Context {
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
   // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
   CapGuard capg;
+  // host seconds the step calls spent blocked in cap_check (dfx_prof_host), and how many waits
+  double host_wait_s = 0;
+  int64_t host_waits = 0;
 
   bool dist_used = false;  // a key-range server: its slots hold table slots across steps
   // push_agg=sum (default): one Update per key per step on the workers' summed gradients, InitV

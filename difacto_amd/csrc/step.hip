@@ -328,8 +328,16 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
+    // (diagnostic, dfx_prof_enable_marks bit 9) the live-V key / occurrence counts
+    const bool count_live = c->prof_n < c->prof_max && (c->prof_mask >> 9 & 1u);
+    const int64_t nbb = bwd_fused_blocks(d, nnz);
+    if (count_live) {
+      DFX_TRY(ws.live.ensure((size_t)nbb * sizeof(uint2)));
+      g.live_part = ws.live.as<uint2>();
+    }
     DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
+    if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);
     DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false));
   } else {
@@ -406,6 +414,18 @@ extern "C" int dfx_prof_counts(dfx_ctx* ctx, double* out) {
   DFX_HIP(hipMemsetAsync(&c->ds->sum_u, 0, sizeof(h), c->stream));
   DFX_HIP(hipMemsetAsync(&c->ds->live_keys, 0, sizeof(lv), c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
+  return DFX_OK;
+}
+
+// out[2]: host seconds dfx_train_step calls spent waiting (the capacity guard's waits on
+// earlier steps' counts, store.hip cap_check) since the last call, and the number of waits;
+// resets.  The rest of a call's time is the host's own work of enqueueing the step.
+extern "C" int dfx_prof_host(dfx_ctx* ctx, double* out) {
+  DFX_CHECK_ARG(ctx && out, "bad argument");
+  out[0] = ctx->c.host_wait_s;
+  out[1] = (double)ctx->c.host_waits;
+  ctx->c.host_wait_s = 0;
+  ctx->c.host_waits = 0;
   return DFX_OK;
 }
 

@@ -21,6 +21,8 @@
 #include <sstream>
 #include <vector>
 
+#include <chrono>
+
 #include "internal.h"
 
 namespace dfx {
@@ -612,12 +614,17 @@ int cap_check(Context* c, int64_t add) {
     const bool keys_ok = 10 * (g.known_keys + pend) <= 9 * c->cap;
     const bool vrows_ok = !has_v || g.known_vrows + pend <= c->T.vcap;
     if (keys_ok && vrows_ok) break;
+    const auto t0 = std::chrono::steady_clock::now();
     if (g.count > 0) {  // an older step's counts may show room: wait for it, not the stream
       DFX_TRY(cap_pop_oldest(c, true, &popped));
+      c->host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      c->host_waits += 1;
       continue;
     }
     // exact counts at a sync point; grow so that this step fits below 0.9 load
     DFX_HIP(hipStreamSynchronize(c->stream));
+    c->host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    c->host_waits += 1;
     HostCounters h;
     DFX_TRY(read_counters(c, &h));
     g.known_keys = (int64_t)h.n_keys;

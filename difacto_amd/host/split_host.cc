@@ -42,16 +42,35 @@ std::vector<int64_t> Offsets(const std::vector<int64_t>& v) {
   return o;
 }
 
+// buffers a DBuf outgrew: queued work (this step's other phases, the previous step on the
+// side streams) may still use them, so they are freed only when the driver is at a sync point
+// (its destructor) — a growing batch costs memory for a while, not a device-wide wait that
+// would drain the pipelined step's lanes
+struct Graveyard {
+  std::vector<std::pair<dfx_ctx*, void*>> bufs;
+  void Reap() {
+    for (auto& b : bufs) (void)dfx_free(b.first, b.second);
+    bufs.clear();
+  }
+};
+
 // grow-only device buffer of one context
 struct DBuf {
   dfx_ctx* c = nullptr;
+  Graveyard* grave = nullptr;
   void* p = nullptr;
   size_t cap = 0;
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes <= cap) return p;
-    HipCheck(hipDeviceSynchronize(), "sync");  // queued work may still use the old buffer
-    if (p) DfxOk(dfx_free(c, p), "dfx_free");
+    if (p) {
+      if (grave) {
+        grave->bufs.push_back({c, p});
+      } else {
+        HipCheck(hipDeviceSynchronize(), "sync");  // queued work may still use the old buffer
+        DfxOk(dfx_free(c, p), "dfx_free");
+      }
+    }
     p = nullptr;
     cap = bytes + bytes / 8;
     DfxOk(dfx_malloc(c, &p, cap), "dfx_malloc");
@@ -292,6 +311,7 @@ struct GpuSplitStore::Impl {
   std::vector<Buf> buf[2];  // [slot][local]
   std::vector<DBuf> icnt, iall;
   std::vector<hipEvent_t> slot_done[2];  // [slot][local]: the main streams are done with it
+  Graveyard grave;  // outgrown step buffers, freed after the device is idle
   std::deque<std::vector<hipEvent_t>> inflight;
   std::vector<std::vector<hipEvent_t>> spare;
   bool have_pending = false;
@@ -310,7 +330,10 @@ struct GpuSplitStore::Impl {
       buf[s].resize(L);
       slot_done[s].resize(L);
       for (int l = 0; l < L; ++l) {
-        for (DBuf* b : buf[s][l].all()) b->c = t->ctx(l);
+        for (DBuf* b : buf[s][l].all()) {
+          b->c = t->ctx(l);
+          b->grave = &grave;
+        }
         HipCheck(hipEventCreateWithFlags(&slot_done[s][l], hipEventDisableTiming), "event");
         // a slot nobody used yet is free
         HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
@@ -593,6 +616,8 @@ GpuSplitStore::~GpuSplitStore() {
   } catch (...) {
   }
   for (int l = 0; l < impl_->L; ++l) (void)dfx_sync(impl_->t->ctx(l));
+  (void)hipDeviceSynchronize();  // the side streams too: the outgrown buffers are free now
+  impl_->grave.Reap();
 }
 
 void GpuSplitStore::Submit(const std::vector<dfx_batch>& batches, int job_type, bool push_cnt,

@@ -291,6 +291,13 @@ def prof_counts(ctx):
     return dict(zip(("U", "U_V", "occ_V"), list(out)))
 
 
+def prof_host(ctx):
+    """host seconds dfx_train_step calls waited (capacity guard) since the last call, waits"""
+    out = (ctypes.c_double * 2)()
+    check(_lib.lib().dfx_prof_host(ctx.h, out))
+    return {"wait_s": out[0], "waits": int(out[1])}
+
+
 def prof_lanes(ctx):
     """after prof_read: mean ms per batch of the Localizer lane, its start / end relative to
     the main stream reaching the batch, and the AUC lane"""

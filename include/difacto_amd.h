@@ -218,7 +218,8 @@ int dfx_progress_read(dfx_ctx* ctx, dfx_progress* out, int reset);
  * and the mean unique-key count U per step (for algorithmic-byte accounting); it resets. */
 int dfx_prof_enable(dfx_ctx* ctx, int max_steps);
 /* dfx_prof_enable recording only the marks in mask: bit m (0..7) = the event at the start of
- * phase m (bit 7: the step's end), bit 8 = the lanes' events.  A phase is timed when both its
+ * phase m (bit 7: the step's end), bit 8 = the lanes' events, bit 9 = the live-V counts of
+ * dfx_prof_counts (one extra launch per step).  A phase is timed when both its
  * marks are recorded (0 otherwise); each timing event costs the step a little latency, so a
  * throughput run records only the phase it reports (the backward: bits 5 and 6). */
 int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask);
@@ -228,8 +229,12 @@ int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
  * the exposed wait), and of the AUC lane */
 int dfx_prof_lanes(dfx_ctx* ctx, double* out);
 /* out[3] = per dfx_train_step since the last call (or dfx_prof_read): the mean number of
- * unique keys, of keys with live V and of their occurrences (the roofline's bytes); resets */
+ * unique keys, of keys with live V and of their occurrences (the roofline's bytes; the live-V
+ * counts are taken only in steps recorded with mark bit 9, dfx_prof_enable_marks); resets */
 int dfx_prof_counts(dfx_ctx* ctx, double* out);
+/* out[2] = host seconds dfx_train_step calls spent blocked (the capacity guard waiting for
+ * earlier steps' counts) since the last call, and the number of such waits; resets */
+int dfx_prof_host(dfx_ctx* ctx, double* out);
 
 /* ---- key-range-sharded store over N GPUs (KVStoreDist, src/store/kvstore_dist.h) --------
  * Every rank is a worker (its own batch) and the server of the keys with

@@ -176,13 +176,29 @@ def test_gisette_long_rows_predict_calcgrad(H):
     opred = O.fm_predict(blk.offs, ocol, blk.vals, W, wp, vp, d)
     assert np.array_equal(pred.cpu().numpy(), opred)
     og = O.fm_calcgrad(blk.offs, ocol, blk.vals, blk.labels, None, W, wp, vp, U, d, opred)
-    assert close(grad.cpu().numpy(), og)
+    # every key has ~1900 occurrences: the device sums them in 256-occurrence chunks combined
+    # in double, the reference in one float run.  As for C5 (test_gpu_fullsize.py
+    # test_calcgrad_c5_chunked): the device is within 1e-6 of the float64 sums of the
+    # reference's own terms, measured on each element's condition scale (sum of |terms|), so its
+    # distance from the reference is the reference's own rounding plus at most that
+    from tests.exact_sums import exact_calcgrad
+    g = grad.cpu().numpy().astype(np.float64)
+    ex, sc = exact_calcgrad(blk, ocol, W, wp, vp, d, opred, U)
+    sc = np.maximum(sc, 1e-30)
+    dev_exact = np.abs(g - ex) / sc
+    ref_exact = np.abs(og - ex) / sc
+    print("gisette calcgrad: device vs f64 %.3g of scale, reference vs f64 %.3g"
+          % (dev_exact.max(), ref_exact.max()))
+    assert dev_exact.max() <= 1e-6
+    assert np.all(np.abs(g - og) <= ref_exact * sc + 1e-6 * sc)
     c.close()
 
 
 def test_gisette_long_rows_fused_steps(H):
-    """The same shape through the fused step (C1's settings, lazy V at V_threshold=10): per-step
-    predictions bit-exact with the oracle's, loss / AUC within 1e-4, model within 1e-5."""
+    """The same shape through the fused step (C1's settings, lazy V at V_threshold=10): loss /
+    AUC within 1e-4 of the oracle and predictions within 1e-4 every step; the model within
+    1e-4 — its gradients are chunked sums (see above), the reference's one float run differs
+    from them by its own rounding, which the FTRL / AdaGrad state carries on."""
     cfg = dict(V_dim=2, lr=.02, V_lr=.001)
     c = H.Context(0, max_keys=1 << 14, **cfg)
     up = O.Updater(**cfg)
@@ -193,14 +209,17 @@ def test_gisette_long_rows_fused_steps(H):
         pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
         H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step == 0), pred=pred)
         p = H.progress(c)
-        assert close(pred.cpu().numpy(), opred, rtol=1e-5), step
+        assert close(pred.cpu().numpy(), opred, rtol=1e-4), step
         assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
         assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     uniq, _, _ = O.localize(blk.offs, blk.ids)
     v, l = H.Store(c).pull(c.tensor(uniq, torch.int64))
     ov, ol = up.get(uniq)
     assert np.array_equal(l.cpu().numpy(), ol)
-    assert close(v.cpu().numpy(), ov, rtol=1e-5)
+    a, b = v.cpu().numpy().astype(np.float64), ov.astype(np.float64)
+    print("gisette fused: model max relative difference %.3g"
+          % float((np.abs(a - b) / (np.maximum(np.abs(a), np.abs(b)) + 1e-7)).max()))
+    assert close(a, b, rtol=1e-4)
     c.close()
 
 
