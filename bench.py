@@ -509,6 +509,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     """N > 1: data parallel over N GPUs with the model sharded by key range
     (difacto_amd/dist.py; keys / records exchanged with RCCL all-to-all-v over xGMI).
     Weak scaling: B rows per GPU per step."""
+    cf = CONFIGS[args.config]
     from difacto_amd import hotpath as H
     from difacto_amd import dist as DI
 

@@ -166,8 +166,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "auc_sort") {
       if (v == "radix") kw->auc_radix = 1;
       else if (v == "merge") kw->auc_radix = 0;
-      else if (v == "block") kw->auc_radix = 2;
-      else { set_error("unknown auc_sort: " + v + " (radix|merge|block)"); return DFX_ERR_ARG; }
+      else { set_error("unknown auc_sort: " + v + " (radix|merge)"); return DFX_ERR_ARG; }
     }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
@@ -207,7 +206,7 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live};
+                    &w.ivstat, &w.live, &w.hstat};
   for (DevBuf* b : bufs) b->release();
 }
 
@@ -276,7 +275,6 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->dist_sum = kw.dist_sum;
   c->sort_pack = kw.sort_pack;
   c->auc_radix = kw.auc_radix != 0;
-  c->auc_block = kw.auc_radix == 2;
   c->sort_items = kw.sort_items;
   c->sort_lookback = kw.sort_lookback;
   c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);

@@ -1003,15 +1003,32 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       double gwd = 0, xxpd = 0, accp[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) accp[k] = 0;
-      for (uint32_t c = 0; c < nc; ++c) {
-        const double* pc = a.part + (int64_t)(c0 + c) * P;
-        gwd += pc[0];
-        xxpd += pc[1];
-        if (vq >= 0) {
+      // kCU chunks' partials loaded together, then added in chunk order: the same sums as one
+      // chunk at a time, a hot key's thousands of chunks in a tenth of the round trips (C5: the
+      // hottest Zipf key's ~1.4 k chunks were the backward's tail)
+      constexpr int kCU = 16;
+      for (uint32_t cb = 0; cb < nc; cb += kCU) {
+        double pg[kCU][2], pv[kCU][CPL];
+#pragma unroll
+        for (int t = 0; t < kCU; ++t) {
+          const uint32_t c = cb + t < nc ? cb + t : nc - 1;
+          const double* pc = a.part + (int64_t)(c0 + c) * P;
+          pg[t][0] = pc[0];
+          pg[t][1] = pc[1];
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             const int cd = l * CPL + k;
-            accp[k] += cd < d ? pc[2 + cd] : 0.0;
+            pv[t][k] = (vq >= 0 && cd < d) ? pc[2 + cd] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < kCU; ++t) {
+          if (cb + t >= nc) break;
+          gwd += pg[t][0];
+          xxpd += pg[t][1];
+          if (vq >= 0) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) accp[k] += pv[t][k];
           }
         }
       }
@@ -1403,8 +1420,8 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   DFX_TRY(ws.occ_x.ensure(nnz * 4));
   DFX_TRY(ws.cnt.ensure(4 * 4));
   DFX_TRY(ws.col.ensure((nnz + 1) * 4));                                      // chunk offsets
-  DFX_TRY(ws.vpos.ensure((nnz / kChunkOcc + 2) * 4));                         // chunk -> segment
-  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (V_dim + 2) * 8));    // chunk partials
+  DFX_TRY(ws.vpos.ensure(max_chunks(nnz) * 4));                         // chunk -> segment
+  DFX_TRY(ws.Vb.ensure((size_t)max_chunks(nnz) * (V_dim + 2) * 8));    // chunk partials
   // 1) p and XV*p per row
   FwdArgs a{};
   a.B = B; a.offs = offset; a.col = col; a.val = value; a.W = weights; a.wpos = w_pos;
@@ -1432,7 +1449,8 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   // 3) long segments (skewed keys) in chunks, combined in double (as in the fused step)
   DFX_HIP(hipMemcpyAsync(&c->ds->u_count, total, sizeof(uint32_t), hipMemcpyDeviceToDevice,
                          c->stream));
-  DFX_HIP(hipMemsetAsync(&c->ds->n_init, 0, sizeof(uint32_t), c->stream));
+  // the plan's gate open: it counts every segment's chunks (k_chunk_plan), none is skipped
+  DFX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&c->ds->n_init), 1, 1, c->stream));
   uint32_t* choff = ws.col.as<uint32_t>();
   uint32_t* chunk_seg = ws.vpos.as<uint32_t>();
   uint32_t* nchunks = total + 1;
@@ -1450,7 +1468,7 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   b.wpos = w_pos; b.vpos = V_pos; b.W = weights; b.grad = grad;
   b.choff = choff; b.chunk_seg = chunk_seg; b.nchunks = nchunks; b.part = ws.Vb.as<double>();
   // the number of segments is device-side (ds->u_count, set above), where k_fm_bwd reads it
-  DFX_TRY(launch_bwd_chunks(b, nnz / kChunkOcc + 1, c->stream));
+  DFX_TRY(launch_bwd_chunks(b, max_chunks(nnz), c->stream));
   DFX_TRY(launch_bwd<false>(b, nnz, c->stream));
   // n_init served as the chunk plan's gate; it counts the fused step's InitV requests
   DFX_HIP(hipMemsetAsync(&c->ds->n_init, 0, sizeof(uint32_t), c->stream));

@@ -92,6 +92,7 @@ struct Workspace {
   DevBuf dscratch;  // double partials
   DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
   DevBuf live;      // (diagnostic) the fused backward's per-block live-V counts
+  DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
   DevBuf os;
@@ -203,7 +204,6 @@ struct Context {
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   bool auc_radix = true;  // the AUC lane sorts by onesweep radix (kwarg auc_sort=radix|merge)
-  bool auc_block = false;  // auc_sort=block: the AUC lane in one workgroup
   int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)
   int sort_lookback = 4;  // the Localizer sort's look-back step width (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
@@ -271,6 +271,10 @@ inline constexpr int kSortItems(int it) { return it << 16; }
 // flags |= kSortLookback(lb): predecessor words a look-back step reads (4 = default, 16, 32)
 inline constexpr int kSortLookback(int lb) { return lb << 24; }
 constexpr int kSortMetaPack = 25;
+// sortmeta[24]: the sort's launch epoch (tags its look-back words); [26] / [27]: the tile
+// tickets of the Localizer's heads / write pass and of the chunk plan (localize.hip k_loc_hw,
+// k_chunk_plan), reset by each sort's plan
+constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
 // the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
 __device__ inline void sort_unpack(const unsigned* meta, uint64_t and_mask, uint64_t w,
@@ -315,6 +319,10 @@ int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
 // of its chunk count, 0 for short segments), chunk_seg[c] = segment of chunk c, total in
 // *nchunks_dev.  Arrays sized for nnz + 1 (choff) and nnz / kChunkOcc + 1 (chunk_seg).
 constexpr int kChunkOcc = 256;
+// chunks of a batch, at most: a long segment of len > kChunkOcc occurrences has
+// ceil(len / kChunkOcc) <= len / kChunkOcc + 1 of them, and there are at most
+// nnz / (kChunkOcc + 1) long segments (the chunk partials and the chunk -> segment table)
+inline int64_t max_chunks(int64_t nnz) { return nnz / kChunkOcc + nnz / (kChunkOcc + 1) + 2; }
 int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
                uint32_t* chunk_seg, uint32_t* nchunks_dev);
 
@@ -392,14 +400,11 @@ int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_
 int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uniq,
                    uint32_t* segslot);
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
-            bool radix, bool block = false);
+            bool radix);
 // the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream
 int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred);
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix);
-// the same, auc_sort=block: the whole AUC in one 1024-thread workgroup (metric.hip k_auc_block)
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix,
-               bool block);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

@@ -110,27 +110,6 @@ __global__ void k_loc_init(DevState* ds) {
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
 }
 
-// heads per tile
-__global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const uint64_t* k1,
-                                                      int64_t n, const DevState* ds,
-                                                      uint32_t* tilesum) {
-  __shared__ uint32_t lds[kLocNT / kWave + 1];
-  const uint64_t* K = ds->sortmeta[31] ? k1 : k0;
-  const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
-  uint32_t s = 0;
-#pragma unroll
-  for (int i = 0; i < kLocItems; ++i) {
-    int64_t idx = base + i;
-    if (idx < n)
-      s += (idx == 0 || sort_key_bits(ds->sortmeta, K[idx]) !=
-                            sort_key_bits(ds->sortmeta, K[idx - 1]))
-               ? 1u : 0u;
-  }
-  uint32_t tot;
-  block_excl_scan<kLocNT>(s, lds, &tot);
-  if (threadIdx.x == 0) tilesum[blockIdx.x] = tot;
-}
-
 struct LocWriteArgs {
   const uint64_t* k0;
   const uint64_t* k1;
@@ -140,7 +119,7 @@ struct LocWriteArgs {
   const uint32_t* q1;
   int64_t n;
   DevState* ds;
-  const uint32_t* tilebase;
+  unsigned long long* hstat;  // per tile: its tagged look-back word (Workspace::hstat)
   uint64_t* uniq;
   uint32_t* col;
   int col_heads;     // col[pos] = rank | (pos is its segment's head) << 31
@@ -150,37 +129,127 @@ struct LocWriteArgs {
   float* occ_x;
 };
 
-__global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
+__device__ inline unsigned long long hw_word(uint32_t tag, uint32_t flag, uint32_t v) {
+  return ((unsigned long long)((tag << 2) | flag) << 32) | v;
+}
+
+// Decoupled look-back over one word per tile (tiles taken in ticket order), by the block's
+// first wave: publishes this tile's aggregate, sums the predecessors' words 64 at a time back to
+// the nearest one that knows its inclusive prefix, publishes its own inclusive prefix and
+// returns the exclusive one to every thread.  tag (29 bits + a kind bit): the launch's, so stale
+// words of earlier launches never match.
+__device__ inline uint32_t tile_lookback(unsigned long long* stat, int64_t tile, uint32_t tag,
+                                         uint32_t tot, int* err, uint32_t* s_pre) {
+  if (threadIdx.x < kWave) {
+    const int l = lane_id();
+    unsigned long long* st = stat + tile;
+    if (l == 0)
+      __hip_atomic_store(st, hw_word(tag, tile == 0 ? 2u : 1u, tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t pre = 0;
+    int64_t kk = tile - 1;
+    uint32_t spins = 0;
+    while (kk >= 0) {
+      const int64_t j = kk - l;
+      uint32_t flag = 2, v = 0;
+      if (j >= 0) {
+        const unsigned long long wv =
+            __hip_atomic_load(stat + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = (uint32_t)(wv >> 32);
+        flag = (hi >> 2) == tag ? (hi & 3u) : 0u;
+        v = (uint32_t)wv;
+      }
+      const uint64_t inc = __ballot(flag == 2u);
+      const uint64_t none = __ballot(flag == 0u);
+      // lanes up to the first inclusive word (the nearest predecessor that knows its prefix)
+      const int lim = inc ? __ffsll((long long)inc) - 1 : kWave - 1;
+      const uint64_t upto = lim == kWave - 1 ? ~0ull : ((1ull << (lim + 1)) - 1);
+      if (none & upto) {  // a predecessor has not published yet: read again
+        if (++spins > (1u << 24)) {
+          if (l == 0) atomicOr(err, kErrSort);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint32_t add = l <= lim ? v : 0u;
+      for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, kWave);
+      pre += add;
+      if (inc) break;
+      kk -= kWave;
+    }
+    if (l == 0) {
+      if (tile > 0)
+        __hip_atomic_store(st, hw_word(tag, 2u, pre + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      *s_pre = pre;
+    }
+  }
+  __syncthreads();
+  return *s_pre;
+}
+// tag spaces of the two users of Workspace::hstat on a lane (the same sort epoch)
+__device__ inline uint32_t hw_tag(const unsigned* meta) { return meta[kSortMetaEpoch] & 0x1FFFFFFFu; }
+__device__ inline uint32_t cp_tag(const unsigned* meta) {
+  return (meta[kSortMetaEpoch] & 0x1FFFFFFFu) | 0x20000000u;
+}
+
+// Run heads -> ranks -> outputs in ONE pass over the sorted items (CountUniqIndex's run-length
+// pass + RemapIndex, localizer.cc:31-107): tiles of 2048 sorted items, taken in order by a
+// ticket; each tile counts its heads (a key differing from the item before it), publishes the
+// count, and finds the heads of every tile before it by decoupled look-back (a wave reads 64
+// predecessors' words at a time) — so the keys are read once and no separate count / scan pass
+// runs.  Per unique key (rank): uniq, segment start; per nnz: col[pos] = rank; per occurrence in
+// sorted order: its row (and value).  A segment longer than kChunkOcc (a skewed key: the item
+// kChunkOcc before an item has its key) raises ds->n_init, the chunk plan's gate.
+__global__ __launch_bounds__(kLocNT) void k_loc_hw(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
-  const bool s1 = a.ds->sortmeta[31] != 0;
+  __shared__ uint32_t s_tile, s_pre;
+  unsigned* meta = a.ds->sortmeta;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaHwTile], 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t n = a.n;
+  if (tile * kLocTile >= n) return;  // every later ticket exits too: no waiter is left behind
+  const bool s1 = meta[31] != 0;
   const uint64_t* K = s1 ? a.k1 : a.k0;
   const uint64_t* P = s1 ? a.p1 : a.p0;
   const uint32_t* Q = s1 ? a.q1 : a.q0;
   // packed items (sort.hip, kSortPackRows): one u64 holds the key window and the row
-  const bool packed = sort_packed(a.ds->sortmeta);
+  const bool packed = sort_packed(meta);
   const uint64_t andm = a.ds->and_mask;
-  const int64_t n = a.n;
-  const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
+  const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint64_t k[kLocItems];
   uint32_t h[kLocItems];
   uint32_t s = 0;
+  bool longseg = false;
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
     h[i] = 0;
     if (idx < n) {
       k[i] = K[idx];
-      h[i] = (idx == 0 || sort_key_bits(a.ds->sortmeta, k[i]) !=
-                              sort_key_bits(a.ds->sortmeta, K[idx - 1]))
-                 ? 1u : 0u;
+      const uint64_t kb = sort_key_bits(meta, k[i]);
+      h[i] = (idx == 0 || kb != sort_key_bits(meta, K[idx - 1])) ? 1u : 0u;
+      if (idx >= kChunkOcc && kb == sort_key_bits(meta, K[idx - kChunkOcc])) longseg = true;
       if (packed) {
         uint32_t row;
-        sort_unpack(a.ds->sortmeta, andm, k[i], &k[i], &row);
+        sort_unpack(meta, andm, k[i], &k[i], &row);
       }
     }
     s += h[i];
   }
-  uint32_t incl = block_excl_scan<kLocNT>(s, lds, nullptr) + a.tilebase[blockIdx.x];
+  // one flag per block at most, and only while it is still clear: a skewed batch has long
+  // segments in most blocks, and same-address atomics from all of them serialise at one L2
+  // channel beside the previous step's backward
+  if (__syncthreads_or(longseg) && threadIdx.x == 0 &&
+      __hip_atomic_load(&a.ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&a.ds->n_init, 1u);
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
+  // decoupled look-back over the tiles before this one: their heads
+  const uint32_t pre = tile_lookback(a.hstat, tile, hw_tag(meta), tot, &a.ds->err, &s_pre);
+  uint32_t incl = ex + pre;
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
@@ -200,13 +269,13 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   }
   // per-occurrence outputs need no rank: write them striped (coalesced stores)
   if (a.occ_row) {
-    const int64_t tb = (int64_t)blockIdx.x * kLocTile;
+    const int64_t tb = tile * kLocTile;
 #pragma unroll
     for (int i = 0; i < kLocItems; ++i) {
       const int64_t idx = tb + (int64_t)i * kLocNT + threadIdx.x;
       if (idx < n) {
         if (packed) {
-          a.occ_row[idx] = (uint32_t)(K[idx] & ((1ull << ((a.ds->sortmeta[kSortMetaPack] >> 16) &
+          a.occ_row[idx] = (uint32_t)(K[idx] & ((1ull << ((meta[kSortMetaPack] >> 16) &
                                                              0xFFu)) - 1));
         } else if (Q) {
           a.occ_row[idx] = Q[idx];
@@ -229,31 +298,50 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
-// ds->n_init counts the long segments (reset by k_loc_init): when there are none (uniform
-// keys) the scan and the table exit at once on the device
-__global__ void k_seg_chunks(int64_t bound, DevState* ds, const uint32_t* segstart,
-                             uint32_t* nch) {
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= bound) return;
-  uint32_t c = 0;
-  if (u < (int64_t)ds->u_count) {
-    const uint32_t len = segstart[u + 1] - segstart[u];
-    c = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
+// ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
+// k_loc_hw).  One launch: tiles of 2048 segments in ticket order; per segment its chunk count
+// (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
+// (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
+// writes the total 0 and exits.
+__global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart, DevState* ds,
+                                                       unsigned long long* stat, uint32_t* choff,
+                                                       uint32_t* chunk_seg, uint32_t* nchunks) {
+  __shared__ uint32_t lds[kLocNT / kWave + 1];
+  __shared__ uint32_t s_tile, s_pre;
+  if (ds->n_init == 0u) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *nchunks = 0u;
+    return;
   }
-  nch[u] = c;
-  if (c) atomicAdd(&ds->n_init, 1u);
-}
-
-// choff now holds the exclusive scan; a long segment lists its chunks
-__global__ void k_chunk_table(int64_t bound, const DevState* ds, const uint32_t* segstart,
-                              const uint32_t* choff, uint32_t* chunk_seg) {
-  if (ds->n_init == 0u) return;
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= bound || u >= (int64_t)ds->u_count) return;
-  const uint32_t len = segstart[u + 1] - segstart[u];
-  if (len <= (uint32_t)kChunkOcc) return;
-  const uint32_t n = (len + kChunkOcc - 1) / kChunkOcc;
-  for (uint32_t c = 0; c < n; ++c) chunk_seg[choff[u] + c] = (uint32_t)u;
+  unsigned* meta = ds->sortmeta;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaCpTile], 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t U = (int64_t)ds->u_count;
+  if (tile * kLocTile >= U) return;  // later tickets exit too
+  const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;
+  uint32_t cnt[kLocItems];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kLocItems; ++i) {
+    cnt[i] = 0;
+    if (base + i < U) {
+      const uint32_t len = segstart[base + i + 1] - segstart[base + i];
+      cnt[i] = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
+    }
+    s += cnt[i];
+  }
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
+  uint32_t incl = ex + tile_lookback(stat, tile, cp_tag(meta), tot, &ds->err, &s_pre);
+#pragma unroll
+  for (int i = 0; i < kLocItems; ++i) {
+    const int64_t u = base + i;
+    if (u >= U) break;
+    choff[u] = incl;
+    for (uint32_t c = 0; c < cnt[i]; ++c) chunk_seg[incl + c] = (uint32_t)u;
+    incl += cnt[i];
+    if (u == U - 1) *nchunks = incl;
+  }
 }
 
 int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
@@ -262,11 +350,14 @@ int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* c
     DFX_HIP(hipMemsetAsync(nchunks_dev, 0, sizeof(uint32_t), L.stream));
     return DFX_OK;
   }
-  const dim3 g((unsigned)((nnz + 255) / 256));
-  hipLaunchKernelGGL(k_seg_chunks, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff);
-  DFX_TRY(scan_u32(L, choff, nnz, nchunks_dev, &L.ds->u_count, &L.ds->n_init));
-  hipLaunchKernelGGL(k_chunk_table, g, dim3(256), 0, L.stream, nnz, L.ds, segstart, choff,
-                     chunk_seg);
+  const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
+  Workspace& ws = *L.ws;
+  void* before = ws.hstat.p;
+  DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * ntiles));
+  if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
+    DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
+  hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, segstart,
+                     L.ds, ws.hstat.as<unsigned long long>(), choff, chunk_seg, nchunks_dev);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -328,18 +419,21 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback))));
   }
+  // heads -> ranks -> outputs in one pass (tiles in ticket order, look-back for the ranks)
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
-  DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
-  uint32_t* ts = ws.tiles.as<uint32_t>();
-  hipLaunchKernelGGL(k_loc_heads, dim3(ntiles), dim3(kLocNT), 0, L.stream, k0, k1, nnz, ds, ts);
-  scan_tiles_top(L, ts, ntiles, nullptr);
+  {
+    void* before = ws.hstat.p;
+    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * ntiles));
+    if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
+      DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
+  }
   LocWriteArgs a{};
   a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1; a.q0 = q0; a.q1 = q1;
-  a.n = nnz; a.ds = ds; a.tilebase = ts;
+  a.n = nnz; a.ds = ds; a.hstat = ws.hstat.as<unsigned long long>();
   a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
-  hipLaunchKernelGGL(k_loc_write, dim3(ntiles), dim3(kLocNT), 0, L.stream, a);
+  hipLaunchKernelGGL(k_loc_hw, dim3(ntiles), dim3(kLocNT), 0, L.stream, a);
   if (o.cnt) {
     hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, L.stream, ds, segs,
                        o.cnt, nnz);

@@ -209,158 +209,6 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
   }
 }
 
-// ---- the AUC lane in ONE workgroup (context kwarg auc_sort=block) ---------------------------
-// The whole AUC of a snapshot in one 1024-thread block: the digit counts of the four 8-bit
-// digits of the orderable pred in one read, then one stable LSD pass per digit that varies —
-// the items in chunks of 8192 in input order, ranked by wave ballots, every digit's running
-// global offset kept in LDS — and a last sweep that counts, for every negative, the positives
-// before it (exact, double).  No look-back chains between blocks and no launches beyond one:
-// beside the backward it holds a single CU, where the multi-block radix lane took 25 blocks per
-// pass and ~9 launches.  The order is the same stable sort by pred (ties in input order), so the
-// result equals the radix and merge lanes'.
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix);
-constexpr int kAbNT = 1024, kAbWaves = kAbNT / kWave, kAbIT = 8, kAbChunk = kAbNT * kAbIT;
-
-__global__ __launch_bounds__(kAbNT) void k_auc_block(int64_t n, uint32_t* k0, uint32_t* v0,
-                                                      uint32_t* k1, uint32_t* v1, double* out,
-                                                      int accumulate) {
-  __shared__ uint32_t hist[4][256];
-  __shared__ uint32_t wcnt[kAbWaves][256];
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t lds[kAbWaves + 1];
-  __shared__ double dred[kAbWaves];
-  const int t = threadIdx.x, w = t / kWave, l = lane_id();
-  for (int i = t; i < 4 * 256; i += kAbNT) (&hist[0][0])[i] = 0;
-  __syncthreads();
-  for (int64_t i = t; i < n; i += kAbNT) {
-    const uint32_t k = k0[i];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) atomicAdd(&hist[p][(k >> (8 * p)) & 255u], 1u);
-  }
-  __syncthreads();
-  uint32_t* kin = k0;
-  uint32_t* vin = v0;
-  uint32_t* kout = k1;
-  uint32_t* vout = v1;
-  for (int p = 0; p < 4; ++p) {
-    // a digit every key shares needs no pass (block-uniform: all threads read the same hist)
-    bool constant = false;
-    for (int d = 0; d < 256; ++d) constant |= hist[p][d] == (uint32_t)n;
-    if (constant) continue;
-    {
-      const uint32_t c = t < 256 ? hist[p][t] : 0u;
-      const uint32_t ex = block_excl_scan<kAbNT>(c, lds, nullptr);
-      if (t < 256) base[t] = ex;
-    }
-    const int shift = 8 * p;
-    for (int64_t c0 = 0; c0 < n; c0 += kAbChunk) {
-      for (int i = t; i < kAbWaves * 256; i += kAbNT) (&wcnt[0][0])[i] = 0;
-      __syncthreads();
-      uint32_t key[kAbIT], lab[kAbIT], dr[kAbIT];
-      const int64_t wb = c0 + (int64_t)w * kWave * kAbIT;
-#pragma unroll
-      for (int j = 0; j < kAbIT; ++j) {
-        const int64_t idx = wb + j * kWave + l;
-        const bool valid = idx < n;
-        key[j] = valid ? kin[idx] : 0u;
-        lab[j] = valid ? vin[idx] : 0u;
-        const uint32_t d = (key[j] >> shift) & 255u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          const bool bit = (d >> b) & 1u;
-          const uint64_t mb = __ballot(valid && bit);
-          peers &= bit ? mb : ~mb;
-        }
-        if (!valid) peers = 0;
-        const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
-        const uint32_t old = valid ? wcnt[w][d] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && r == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[j] = valid ? (d | ((old + r) << 8)) : 0xFFFFFFFFu;
-      }
-      __syncthreads();
-      // per digit: the waves' exclusive offsets inside the chunk, folded onto the running base
-      if (t < 256) {
-        uint32_t run = base[t];
-        for (int i = 0; i < kAbWaves; ++i) {
-          const uint32_t x = wcnt[i][t];
-          wcnt[i][t] = run;
-          run += x;
-        }
-        base[t] = run;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kAbIT; ++j) {
-        if (dr[j] == 0xFFFFFFFFu) continue;
-        const uint32_t d = dr[j] & 255u;
-        const uint32_t pos = wcnt[w][d] + (dr[j] >> 8);
-        kout[pos] = key[j];
-        vout[pos] = lab[j];
-      }
-      __syncthreads();
-    }
-    // the pass's writes are visible to the whole block before the next pass reads them
-    __threadfence_block();
-    __syncthreads();
-    uint32_t* tk = kin; kin = kout; kout = tk;
-    uint32_t* tv = vin; vin = vout; vout = tv;
-  }
-  // area: every negative adds the positives before it in the sorted order
-  double area = 0;
-  uint32_t run = 0;  // positives before the current chunk (block-uniform)
-  for (int64_t c0 = 0; c0 < n; c0 += kAbChunk) {
-    uint32_t lab[kAbIT], s = 0;
-    const int64_t tb = c0 + (int64_t)t * kAbIT;
-#pragma unroll
-    for (int j = 0; j < kAbIT; ++j) {
-      lab[j] = tb + j < n ? vin[tb + j] : 0u;
-      s += lab[j];
-    }
-    uint32_t tot;
-    uint32_t cum = block_excl_scan<kAbNT>(s, lds, &tot) + run;
-#pragma unroll
-    for (int j = 0; j < kAbIT; ++j) {
-      if (tb + j >= n) break;
-      if (lab[j]) cum += 1; else area += (double)cum;
-    }
-    run += tot;
-  }
-  for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
-  if (l == 0) dred[w] = area;
-  __syncthreads();
-  if (t == 0) {
-    double a = 0;
-    for (int i = 0; i < kAbWaves; ++i) a += dred[i];
-    const double P = (double)run;
-    double r;
-    if (P == 0 || P == (double)n) {
-      r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
-    } else {
-      a /= P * ((double)n - P);
-      r = (a < 0.5 ? 1 - a : a) * (double)n;
-    }
-    *out = accumulate ? *out + r : r;
-  }
-}
-
-// AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix,
-               bool block) {
-  if (block && B > 0) {
-    Workspace& ws = *L.ws;
-    DFX_TRY(auc_reserve(ws, B, L.stream));
-    hipLaunchKernelGGL(k_auc_block, dim3(1), dim3(kAbNT), 0, L.stream, B, ws.ak0.as<uint32_t>(),
-                       ws.av0.as<uint32_t>(), ws.keys0.as<uint32_t>(), ws.vals0.as<uint32_t>(),
-                       out_dev, accumulate ? 1 : 0);
-    DFX_HIP(hipGetLastError());
-    return DFX_OK;
-  }
-  return auc_finish(L, B, out_dev, accumulate, radix);
-}
-
 // AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix) {
   Workspace& ws = *L.ws;
@@ -418,9 +266,9 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool 
 }
 
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
-            bool radix, bool block) {
+            bool radix) {
   DFX_TRY(auc_snapshot(L, L.stream, B, label, pred));
-  return auc_finish(L, B, out_dev, false, radix, block);
+  return auc_finish(L, B, out_dev, false, radix);
 }
 
 __global__ void k_eval_part(int64_t B, const float* label, const float* pred, double* part) {
@@ -494,7 +342,7 @@ extern "C" int dfx_auc(dfx_ctx* ctx, int64_t B, const float* label, const float*
   DFX_CHECK_ARG(ctx && auc_n, "null argument");
   Context* c = &ctx->c;
   double* o = &c->ds->scratch[2];
-  DFX_TRY(auc_run(main_lane(c), B, label, pred, o, c->auc_radix, c->auc_block));
+  DFX_TRY(auc_run(main_lane(c), B, label, pred, o, c->auc_radix));
   DFX_HIP(hipMemcpyAsync(auc_n, o, 8, hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;

@@ -38,7 +38,7 @@ constexpr unsigned kOsNone = 0xFFFFFFFFu;
 // sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
 // The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
-constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = 24;
+constexpr int kMetaSrc = 8, kMetaTile = 16, kMetaEpoch = kSortMetaEpoch;
 // [25]: packed mode (kSortPackRows): 1 | lo8 << 8 | rb8 << 16 — the items travel as one u64
 // ((key >> lo8) << rb8 | row), see k_os_plan; 0: (key, payload) pairs
 constexpr int kMetaPack = 25;
@@ -88,6 +88,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
       meta[kMetaSrc + r] = (unsigned)(r & 1);
       meta[kMetaTile + r] = 0;
     }
+    meta[kSortMetaHwTile] = 0;
+    meta[kSortMetaCpTile] = 0;
     meta[kMetaPack] = (pack && q > 0) ? (1u | ((unsigned)lo8 << 8) | ((unsigned)pack_rb8 << 16))
                                       : 0u;
     meta[31] = (unsigned)(q & 1);

@@ -457,7 +457,7 @@ int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* p
   sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
-  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix, c->auc_block));
+  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   DFX_HIP(hipGetLastError());
@@ -486,9 +486,9 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
     g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();
     g.nchunks = &ods->totals[1];
-    DFX_TRY(ows.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 8));
+    DFX_TRY(ows.Vb.ensure((size_t)max_chunks(nnz) * (d + 2) * 8));
     g.part = ows.Vb.as<double>();
-    DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
+    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
   }
   (void)R;

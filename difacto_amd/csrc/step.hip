@@ -45,7 +45,7 @@ int ws_reserve(Context* c, int64_t rows, int64_t nnz) {
   if (d > 0) DFX_TRY(ws.XVp.ensure((size_t)rows * xvp_stride(c) * 4));
   DFX_TRY(ws.dscratch.ensure((rows / 4 + 64) * 8));
   DFX_TRY(ws.wv.ensure(nnz * 8));
-  DFX_TRY(ws.Vb.ensure((size_t)(nnz / kChunkOcc + 2) * (d + 2) * 8));  // chunk partials (f64)
+  DFX_TRY(ws.Vb.ensure((size_t)max_chunks(nnz) * (d + 2) * 8));  // chunk partials (f64)
   ws.rows = rows;
   ws.nnz = nnz;
   return DFX_OK;
@@ -64,7 +64,7 @@ int loc_reserve(Workspace& w, int64_t nnz, hipStream_t st) {
   DFX_TRY(w.col.ensure(nnz * 4));
   DFX_TRY(w.uniq.ensure(nnz * 8));
   DFX_TRY(w.flags.ensure((nnz + 1) * 4));                   // chunk plan: choff
-  DFX_TRY(w.rowtmp.ensure((nnz / kChunkOcc + 2) * 4));      // chunk plan: chunk_seg
+  DFX_TRY(w.rowtmp.ensure(max_chunks(nnz) * 4));      // chunk plan: chunk_seg
   DFX_TRY(w.slot.ensure((nnz + 1) * 4));
   DFX_TRY(w.occ_row.ensure(nnz * 4));
   DFX_TRY(w.occ_x.ensure(nnz * 4));
@@ -314,7 +314,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   lane_mark(c, 2, c->aux_stream);
-  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix, c->auc_block));
+  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
   lane_mark(c, 3, c->aux_stream);
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   prof_mark(c, 5);
@@ -335,7 +335,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
       DFX_TRY(ws.live.ensure((size_t)nbb * sizeof(uint2)));
       g.live_part = ws.live.as<uint2>();
     }
-    DFX_TRY(launch_bwd_chunks(g, nnz / kChunkOcc + 1, c->stream));
+    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);

@@ -287,6 +287,8 @@ def prof_counts(ctx):
     """per step since the last call (or prof_read): mean unique keys, keys with live V and
     their occurrences; resets"""
     out = (ctypes.c_double * 3)()
+    if not hasattr(_lib.lib(), "dfx_prof_counts"):  # an older library under A/B (DFX_LIB_PATH)
+        return {"U": 0.0, "U_V": None, "occ_V": None}
     check(_lib.lib().dfx_prof_counts(ctx.h, out))
     return dict(zip(("U", "U_V", "occ_V"), list(out)))
 
@@ -294,6 +296,8 @@ def prof_counts(ctx):
 def prof_host(ctx):
     """host seconds dfx_train_step calls waited (capacity guard) since the last call, waits"""
     out = (ctypes.c_double * 2)()
+    if not hasattr(_lib.lib(), "dfx_prof_host"):  # an older library under A/B (DFX_LIB_PATH)
+        return {"wait_s": 0.0, "waits": 0}
     check(_lib.lib().dfx_prof_host(ctx.h, out))
     return {"wait_s": out[0], "waits": int(out[1])}
 

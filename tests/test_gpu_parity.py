@@ -218,7 +218,7 @@ def test_auc_and_evaluate(H):
 
 @pytest.mark.parametrize("n", [1, 4095, 4097, 100000, 1000003])
 def test_auc_radix_and_merge_sorts_agree(H, n):
-    """the AUC lane's three stable sorts (auc_sort=radix | merge | block): the same AUC*n, equal to the
+    """the AUC lane's two stable sorts (auc_sort=radix | merge): the same AUC*n, equal to the
     input-order tie break of the oracle, with heavy ties (quantised predictions, one constant
     digit pattern) and with all predictions equal (epoch 0, w = 0)"""
     rng = np.random.default_rng(n)
@@ -227,10 +227,10 @@ def test_auc_radix_and_merge_sorts_agree(H, n):
                  np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32)]:
         want = O.auc_stable_ties(label, pred) if O.has_ties(pred) else O.auc(label, pred)
         got = []
-        for mode in ["radix", "merge", "block"]:
+        for mode in ["radix", "merge"]:
             c = H.Context(0, auc_sort=mode)
             got.append(H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32)))
-        assert got[0] == got[1] == got[2], got
+        assert got[0] == got[1], got
         assert abs(got[0] - want) <= 1e-4 * n, (got, want)
 
 
