@@ -488,8 +488,8 @@ def main():
         "host_waits": host_wait["waits"],
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
-        "mean_live_v_keys": round(counts["U_V"], 1),
-        "mean_live_v_occurrences": round(counts["occ_V"], 1),
+        "mean_live_v_keys": counts["U_V"] and round(counts["U_V"], 1),
+        "mean_live_v_occurrences": counts["occ_V"] and round(counts["occ_V"], 1),
         "chunk_model": (chunk_model(B * k, mean_u, elapsed / args.steps * 1e3)
                         if args.config == "c3" else None),
         "train_loss_per_row": round(prog["loss"] / max(prog["nrows"], 1), 6),

@@ -70,6 +70,14 @@ struct Kw {
   // unless the batches repeat); never set by the product path
   int diag = 0;
   int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
+  // loc_bucket=1|2: the fused step's Localizer sorts one global pass over the top varying digit
+  // and then each bucket by one block of 256 | 1024 threads (localize.hip k_loc_bucket); 0: LSD
+  // passes over every digit.  A/B at C3 (round 3, same box): 0 128.0, 1 115.0, 2 121.0 M ex/s —
+  // the bucket blocks run long beside the backward and the next forward waits for them
+  int loc_bucket = 0;
+  // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
+  // heads + scan + write)
+  int loc_onepass = 0;
   int fat_nb = 6;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B; 6: DESIGN.md (d))
   // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
   // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
@@ -134,6 +142,14 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else if (v == "noloc") kw->diag = 2;
       else if (v == "noauc_noloc") kw->diag = 3;
       else { set_error("unknown diag: " + v + " (noauc|noloc|noauc_noloc)"); return DFX_ERR_ARG; }
+    }
+    else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
+    else if (k == "loc_bucket") {
+      kw->loc_bucket = atoi(cv);
+      if (kw->loc_bucket < 0 || kw->loc_bucket > 2) {
+        set_error("loc_bucket must be 0, 1 (256-thread buckets) or 2 (1024)");
+        return DFX_ERR_ARG;
+      }
     }
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
@@ -284,6 +300,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_nb = kw.fat_nb;
   c->fwd_lanes = kw.fwd_lanes;
   c->diag = kw.diag;
+  c->loc_bucket = kw.loc_bucket;
+  c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;

@@ -1003,32 +1003,15 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       double gwd = 0, xxpd = 0, accp[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) accp[k] = 0;
-      // kCU chunks' partials loaded together, then added in chunk order: the same sums as one
-      // chunk at a time, a hot key's thousands of chunks in a tenth of the round trips (C5: the
-      // hottest Zipf key's ~1.4 k chunks were the backward's tail)
-      constexpr int kCU = 16;
-      for (uint32_t cb = 0; cb < nc; cb += kCU) {
-        double pg[kCU][2], pv[kCU][CPL];
-#pragma unroll
-        for (int t = 0; t < kCU; ++t) {
-          const uint32_t c = cb + t < nc ? cb + t : nc - 1;
-          const double* pc = a.part + (int64_t)(c0 + c) * P;
-          pg[t][0] = pc[0];
-          pg[t][1] = pc[1];
+      for (uint32_t c = 0; c < nc; ++c) {
+        const double* pc = a.part + (int64_t)(c0 + c) * P;
+        gwd += pc[0];
+        xxpd += pc[1];
+        if (vq >= 0) {
 #pragma unroll
           for (int k = 0; k < CPL; ++k) {
             const int cd = l * CPL + k;
-            pv[t][k] = (vq >= 0 && cd < d) ? pc[2 + cd] : 0.0;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < kCU; ++t) {
-          if (cb + t >= nc) break;
-          gwd += pg[t][0];
-          xxpd += pg[t][1];
-          if (vq >= 0) {
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) accp[k] += pv[t][k];
+            accp[k] += cd < d ? pc[2 + cd] : 0.0;
           }
         }
       }

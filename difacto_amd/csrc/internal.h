@@ -199,6 +199,8 @@ struct Context {
   int initv_onepass = 1;  // kwarg initv_onepass
   int fat_nb = 6;         // kwarg fat_nb
   int fwd_lanes = 0;      // kwarg fwd_lanes
+  int loc_bucket = 0;     // kwarg loc_bucket (localize.hip k_loc_bucket)
+  int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
@@ -272,9 +274,16 @@ inline constexpr int kSortItems(int it) { return it << 16; }
 inline constexpr int kSortLookback(int lb) { return lb << 24; }
 constexpr int kSortMetaPack = 25;
 // sortmeta[24]: the sort's launch epoch (tags its look-back words); [26] / [27]: the tile
-// tickets of the Localizer's heads / write pass and of the chunk plan (localize.hip k_loc_hw,
+// tickets of the Localizer's one-pass write and of the chunk plan (localize.hip k_loc_write,
 // k_chunk_plan), reset by each sort's plan
 constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
+// flags |= kSortBucket (packed items only): the plan may turn the sort into one pass over the top
+// varying digit plus the Localizer's per-bucket sort (sort.hip k_os_plan, localize.hip
+// k_loc_bucket) when no bucket exceeds kSortBucketMax items; sortmeta[30] says so,
+// [28..29] hold the shifts of the digits below the top one
+constexpr int kSortBucket = 4;
+constexpr uint32_t kSortBucketMax = 1u << 18;
+constexpr int kSortMetaRest = 28, kSortMetaBucket = 30;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
 // the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
 __device__ inline void sort_unpack(const unsigned* meta, uint64_t and_mask, uint64_t w,

@@ -119,7 +119,8 @@ struct LocWriteArgs {
   const uint32_t* q1;
   int64_t n;
   DevState* ds;
-  unsigned long long* hstat;  // per tile: its tagged look-back word (Workspace::hstat)
+  const uint32_t* tilebase;   // two-pass mode: per tile the heads before it (k_loc_heads + scan)
+  unsigned long long* hstat;  // one-pass mode: per tile its tagged look-back word
   uint64_t* uniq;
   uint32_t* col;
   int col_heads;     // col[pos] = rank | (pos is its segment's head) << 31
@@ -194,21 +195,63 @@ __device__ inline uint32_t cp_tag(const unsigned* meta) {
   return (meta[kSortMetaEpoch] & 0x1FFFFFFFu) | 0x20000000u;
 }
 
-// Run heads -> ranks -> outputs in ONE pass over the sorted items (CountUniqIndex's run-length
-// pass + RemapIndex, localizer.cc:31-107): tiles of 2048 sorted items, taken in order by a
-// ticket; each tile counts its heads (a key differing from the item before it), publishes the
-// count, and finds the heads of every tile before it by decoupled look-back (a wave reads 64
-// predecessors' words at a time) — so the keys are read once and no separate count / scan pass
-// runs.  Per unique key (rank): uniq, segment start; per nnz: col[pos] = rank; per occurrence in
-// sorted order: its row (and value).  A segment longer than kChunkOcc (a skewed key: the item
-// kChunkOcc before an item has its key) raises ds->n_init, the chunk plan's gate.
-__global__ __launch_bounds__(kLocNT) void k_loc_hw(LocWriteArgs a) {
+// A segment longer than kChunkOcc (a skewed key: the item kChunkOcc before an item has its key)
+// raises ds->n_init, the chunk plan's gate: one flag per block at most, and only while it is
+// still clear — a skewed batch has long segments in most blocks, and same-address atomics from
+// all of them serialise at one L2 channel beside the previous step's backward.
+__device__ inline void flag_longseg(bool longseg, DevState* ds) {
+  if (__syncthreads_or(longseg) && threadIdx.x == 0 &&
+      __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&ds->n_init, 1u);
+}
+
+// Two-pass heads -> ranks (CountUniqIndex's run-length pass, localizer.cc:31-60): per tile of
+// 2048 sorted items the number of heads (a key differing from the item before it) into
+// tilesum, and the long-segment flag; k_scan_top turns the counts into every tile's base rank.
+__global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const uint64_t* k1,
+                                                      int64_t n, DevState* ds,
+                                                      uint32_t* tilesum) {
+  __shared__ uint32_t lds[kLocNT / kWave + 1];
+  const unsigned* meta = ds->sortmeta;
+  if (meta[kSortMetaBucket] & 1u) return;  // bucket mode: k_loc_bucket wrote the outputs
+  const uint64_t* K = meta[31] ? k1 : k0;
+  const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
+  uint32_t s = 0;
+  bool longseg = false;
+#pragma unroll
+  for (int i = 0; i < kLocItems; ++i) {
+    const int64_t idx = base + i;
+    if (idx < n) {
+      const uint64_t kb = sort_key_bits(meta, K[idx]);
+      s += (idx == 0 || kb != sort_key_bits(meta, K[idx - 1])) ? 1u : 0u;
+      if (idx >= kChunkOcc && kb == sort_key_bits(meta, K[idx - kChunkOcc])) longseg = true;
+    }
+  }
+  flag_longseg(longseg, ds);
+  uint32_t tot;
+  block_excl_scan<kLocNT>(s, lds, &tot);
+  if (threadIdx.x == 0) tilesum[blockIdx.x] = tot;
+}
+
+// Ranks -> outputs (RemapIndex, localizer.cc:62-107) over tiles of 2048 sorted items: per
+// unique key (rank) uniq and segment start; per nnz col[pos] = rank; per occurrence in sorted
+// order its row (and value).  A tile's base rank comes from the two-pass scan (a.tilebase), or
+// — one-pass mode (kwarg loc_onepass), no heads launch — tiles are taken in order by a ticket,
+// count their own heads and find the heads before them by decoupled look-back (a wave reads 64
+// predecessors' words at a time).  The one-pass form reads the keys once, but its blocks sit
+// spinning on the look-back beside the backward (measured: 100 us against 60 us for heads +
+// scan + write, and a slower backward), so two passes are the default.
+__global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   __shared__ uint32_t s_tile, s_pre;
   unsigned* meta = a.ds->sortmeta;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaHwTile], 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
+  if (meta[kSortMetaBucket] & 1u) return;  // bucket mode: k_loc_bucket wrote the outputs
+  const bool onepass = a.tilebase == nullptr;
+  if (onepass) {
+    if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaHwTile], 1u);
+    __syncthreads();
+  }
+  const int64_t tile = onepass ? (int64_t)s_tile : (int64_t)blockIdx.x;
   const int64_t n = a.n;
   if (tile * kLocTile >= n) return;  // every later ticket exits too: no waiter is left behind
   const bool s1 = meta[31] != 0;
@@ -231,7 +274,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_hw(LocWriteArgs a) {
       k[i] = K[idx];
       const uint64_t kb = sort_key_bits(meta, k[i]);
       h[i] = (idx == 0 || kb != sort_key_bits(meta, K[idx - 1])) ? 1u : 0u;
-      if (idx >= kChunkOcc && kb == sort_key_bits(meta, K[idx - kChunkOcc])) longseg = true;
+      if (onepass && idx >= kChunkOcc && kb == sort_key_bits(meta, K[idx - kChunkOcc]))
+        longseg = true;
       if (packed) {
         uint32_t row;
         sort_unpack(meta, andm, k[i], &k[i], &row);
@@ -239,17 +283,16 @@ __global__ __launch_bounds__(kLocNT) void k_loc_hw(LocWriteArgs a) {
     }
     s += h[i];
   }
-  // one flag per block at most, and only while it is still clear: a skewed batch has long
-  // segments in most blocks, and same-address atomics from all of them serialise at one L2
-  // channel beside the previous step's backward
-  if (__syncthreads_or(longseg) && threadIdx.x == 0 &&
-      __hip_atomic_load(&a.ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    atomicOr(&a.ds->n_init, 1u);
-  uint32_t tot;
-  const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
-  // decoupled look-back over the tiles before this one: their heads
-  const uint32_t pre = tile_lookback(a.hstat, tile, hw_tag(meta), tot, &a.ds->err, &s_pre);
-  uint32_t incl = ex + pre;
+  uint32_t incl;
+  if (onepass) {
+    flag_longseg(longseg, a.ds);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
+    // decoupled look-back over the tiles before this one: their heads
+    incl = ex + tile_lookback(a.hstat, tile, hw_tag(meta), tot, &a.ds->err, &s_pre);
+  } else {
+    incl = block_excl_scan<kLocNT>(s, lds, nullptr) + a.tilebase[tile];
+  }
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
@@ -289,6 +332,179 @@ __global__ __launch_bounds__(kLocNT) void k_loc_hw(LocWriteArgs a) {
   }
 }
 
+// ---- bucket mode (sort.hip k_os_plan, kSortBucket): the per-bucket sort + heads / outputs ----
+// After ONE pass over the top varying digit (its buckets in key order, each stable in input
+// order) a block per bucket, taken in bucket order by a ticket, sorts its bucket by the digits
+// below (stable LSD through global memory: the bucket, ~15 k items at B = 100 k, stays in L2),
+// counts its heads, finds the heads of the buckets before it by decoupled look-back, and writes
+// uniq / segstart / occ_row as k_loc_write does — in place of two more global passes and the heads / write pass.
+constexpr int kBkIT = 8;
+
+struct BucketArgs {
+  uint64_t* k0;  // ping-pong buffer (the pass's source)
+  uint64_t* k1;  // the top-digit pass's result (packed items)
+  const uint32_t* counts;  // counts[0..256): items per bucket
+  int64_t n;
+  DevState* ds;
+  unsigned long long* stat;  // per bucket: its tagged look-back word (Workspace::hstat)
+  uint64_t* uniq;
+  uint32_t* segstart;
+  uint32_t* occ_row;
+};
+
+// NT threads per bucket (kwarg loc_bucket: 1 -> 256, a block that fits beside the backward's;
+// 2 -> 1024)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_loc_bucket(BucketArgs a) {
+  constexpr int kBkNT = NT, kBkWaves = NT / kWave, kBkChunk = NT * kBkIT;
+  unsigned* meta = a.ds->sortmeta;
+  const unsigned mode = meta[kSortMetaBucket];
+  if (!(mode & 1u)) return;  // the LSD passes ran instead (k_loc_write writes the outputs)
+  __shared__ uint32_t wcnt[kBkWaves][256];
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t lds[kBkWaves + 1];
+  __shared__ uint32_t s_b, s_start, s_pre;
+  const int t = threadIdx.x, w = t / kWave, l = lane_id();
+  if (t == 0) s_b = atomicAdd(&meta[kSortMetaHwTile], 1u);
+  __syncthreads();
+  const uint32_t b = s_b;
+  if (b >= 256u) return;
+  {  // the bucket's start: the counts of the buckets before it
+    uint32_t c = 0;
+    for (int i = t; i < (int)b; i += kBkNT) c += a.counts[i];
+    uint32_t tot;
+    (void)block_excl_scan<kBkNT>(c, lds, &tot);
+    if (t == 0) s_start = tot;
+  }
+  __syncthreads();
+  const int64_t start = s_start;
+  const int64_t nb = a.counts[b];
+  uint64_t* X = a.k1 + start;
+  uint64_t* Y = a.k0 + start;
+  const int nrest = (int)((mode >> 8) & 0xFFu);
+  // ---- stable LSD over the digits below the top one (ascending), through global memory
+  for (int r = 0; r < nrest && nb > 1; ++r) {
+    const int shift = (int)((meta[kSortMetaRest + (r >> 2)] >> (8 * (r & 3))) & 0xFFu);
+    if (t < 256) base[t] = 0;
+    __syncthreads();
+    for (int64_t i = t; i < nb; i += kBkNT) atomicAdd(&base[(uint32_t)(X[i] >> shift) & 255u], 1u);
+    __syncthreads();
+    {
+      const uint32_t c = t < 256 ? base[t] : 0u;
+      __syncthreads();
+      const uint32_t ex = block_excl_scan<kBkNT>(c, lds, nullptr);
+      if (t < 256) base[t] = ex;
+    }
+    static_assert(NT >= 256, "one thread per digit");
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
+      for (int i = t; i < kBkWaves * 256; i += kBkNT) (&wcnt[0][0])[i] = 0;
+      __syncthreads();
+      uint64_t key[kBkIT];
+      uint32_t dr[kBkIT];
+      const int64_t wb = c0 + (int64_t)w * kWave * kBkIT;
+#pragma unroll
+      for (int j = 0; j < kBkIT; ++j) {
+        const int64_t idx = wb + j * kWave + l;
+        const bool valid = idx < nb;
+        key[j] = valid ? X[idx] : 0ull;
+        const uint32_t d = (uint32_t)(key[j] >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bt = 0; bt < 8; ++bt) {
+          const bool bit = (d >> bt) & 1u;
+          const uint64_t mb = __ballot(valid && bit);
+          peers &= bit ? mb : ~mb;
+        }
+        if (!valid) peers = 0;
+        const uint32_t rk = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t old = valid ? wcnt[w][d] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && rk == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        dr[j] = valid ? (d | ((old + rk) << 8)) : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      if (t < 256) {  // the waves' offsets inside the chunk, on the digit's running base
+        uint32_t run = base[t];
+        for (int i = 0; i < kBkWaves; ++i) {
+          const uint32_t x = wcnt[i][t];
+          wcnt[i][t] = run;
+          run += x;
+        }
+        base[t] = run;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kBkIT; ++j)
+        if (dr[j] != 0xFFFFFFFFu) Y[wcnt[w][dr[j] & 255u] + (dr[j] >> 8)] = key[j];
+      __syncthreads();
+    }
+    __threadfence_block();  // this pass's stores, seen by the whole block in the next
+    __syncthreads();
+    uint64_t* tmp = X; X = Y; Y = tmp;
+  }
+  // ---- heads: a key differing from the item before it (the first item of a bucket always)
+  const uint64_t andm = a.ds->and_mask;
+  uint32_t mine = 0;
+  bool longseg = false;
+  for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
+    const int64_t ib = c0 + (int64_t)t * kBkIT;
+#pragma unroll
+    for (int j = 0; j < kBkIT; ++j) {
+      const int64_t i = ib + j;
+      if (i >= nb) break;
+      const uint64_t kb = sort_key_bits(meta, X[i]);
+      mine += (i == 0 || kb != sort_key_bits(meta, X[i - 1])) ? 1u : 0u;
+      if (i >= kChunkOcc && kb == sort_key_bits(meta, X[i - kChunkOcc])) longseg = true;
+    }
+  }
+  if (__syncthreads_or(longseg) && t == 0 &&
+      __hip_atomic_load(&a.ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&a.ds->n_init, 1u);
+  uint32_t tot;
+  (void)block_excl_scan<kBkNT>(mine, lds, &tot);
+  uint32_t rank0 = tile_lookback(a.stat, (int64_t)b, hw_tag(meta), tot, &a.ds->err, &s_pre);
+  // ---- outputs, in position order: per head its key and segment start, per item its row
+  const int rb8 = (int)((meta[kSortMetaPack] >> 16) & 0xFFu);
+  for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
+    const int64_t ib = c0 + (int64_t)t * kBkIT;
+    uint64_t it[kBkIT];
+    uint32_t h[kBkIT], s = 0;
+#pragma unroll
+    for (int j = 0; j < kBkIT; ++j) {
+      const int64_t i = ib + j;
+      h[j] = 0;
+      if (i < nb) {
+        it[j] = X[i];
+        h[j] = (i == 0 || sort_key_bits(meta, it[j]) != sort_key_bits(meta, X[i - 1])) ? 1u : 0u;
+      }
+      s += h[j];
+    }
+    uint32_t ctot;
+    uint32_t incl = block_excl_scan<kBkNT>(s, lds, &ctot) + rank0;
+#pragma unroll
+    for (int j = 0; j < kBkIT; ++j) {
+      const int64_t i = ib + j;
+      if (i >= nb) break;
+      incl += h[j];
+      uint64_t key;
+      uint32_t row;
+      sort_unpack(meta, andm, it[j], &key, &row);
+      if (h[j]) {
+        if (a.uniq) a.uniq[incl - 1] = key;
+        if (a.segstart) a.segstart[incl - 1] = (uint32_t)(start + i);
+      }
+      if (a.occ_row) a.occ_row[start + i] = (uint32_t)(it[j] & ((1ull << rb8) - 1));
+    }
+    rank0 += ctot;
+  }
+  if (b == 255u && t == 0) {  // the last bucket closes the segments
+    a.ds->u_count = rank0;
+    if (a.segstart) a.segstart[rank0] = (uint32_t)a.n;
+  }
+}
+
 __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* cnt, int64_t cap) {
   int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= cap || u >= ds->u_count) return;
@@ -299,7 +515,7 @@ __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
 // ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
-// k_loc_hw).  One launch: tiles of 2048 segments in ticket order; per segment its chunk count
+// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments in ticket order; per segment its chunk count
 // (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
 // (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
 // writes the total 0 and exits.
@@ -411,7 +627,8 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                   kSortDiffIsOrAnd | kSortCountsReady |
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
-                                                      (c->sort_pack ? kSortPackRows(rb8) : 0))));
+                                                      (c->sort_pack ? kSortPackRows(rb8) : 0) |
+                                                      (c->loc_bucket ? kSortBucket : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
@@ -419,21 +636,44 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback))));
   }
-  // heads -> ranks -> outputs in one pass (tiles in ticket order, look-back for the ranks)
+  // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
+  // k_loc_write with look-back; in bucket mode (the plan's choice) k_loc_bucket does it per
+  // bucket and these exit
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
-  {
+  uint32_t* ts = nullptr;
+  if (!c->loc_onepass) {
+    DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+    ts = ws.tiles.as<uint32_t>();
+  }
+  if (c->loc_onepass || (narrow && c->sort_pack && c->loc_bucket)) {
     void* before = ws.hstat.p;
-    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * ntiles));
+    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * (ntiles > 256 ? ntiles : 256)));
     if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
       DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
   }
+  if (narrow && c->sort_pack && c->loc_bucket) {
+    BucketArgs ba{};
+    ba.k0 = k0; ba.k1 = k1; ba.counts = ws.os_counts(); ba.n = nnz; ba.ds = ds;
+    ba.stat = ws.hstat.as<unsigned long long>();
+    ba.uniq = o.uniq; ba.segstart = segs; ba.occ_row = o.occ_row;
+    if (c->loc_bucket == 2)
+      hipLaunchKernelGGL(k_loc_bucket<1024>, dim3(256), dim3(1024), 0, L.stream, ba);
+    else
+      hipLaunchKernelGGL(k_loc_bucket<256>, dim3(256), dim3(256), 0, L.stream, ba);
+  }
+  if (ts) {
+    hipLaunchKernelGGL(k_loc_heads, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, k0, k1,
+                       nnz, ds, ts);
+    scan_tiles_top(L, ts, ntiles, nullptr);
+  }
   LocWriteArgs a{};
   a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1; a.q0 = q0; a.q1 = q1;
-  a.n = nnz; a.ds = ds; a.hstat = ws.hstat.as<unsigned long long>();
+  a.n = nnz; a.ds = ds; a.tilebase = ts;
+  a.hstat = ts ? nullptr : ws.hstat.as<unsigned long long>();
   a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
-  hipLaunchKernelGGL(k_loc_hw, dim3(ntiles), dim3(kLocNT), 0, L.stream, a);
+  hipLaunchKernelGGL(k_loc_write, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, a);
   if (o.cnt) {
     hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, L.stream, ds, segs,
                        o.cnt, nnz);

@@ -267,9 +267,12 @@ def test_c5_model_drift_bound(H):
     in 256-occurrence chunks (double partials in chunk order) where the reference sums one float
     run, so the two trajectories drift apart a little every step.  After every step the model
     entries of the batch's keys (w, V; lens exact) are compared; the largest relative difference
-    per step is printed (DESIGN.md (c) quotes it) and bounded by DRIFT, and loss / AUC stay
+    per step is printed (DESIGN.md (c) quotes it).  Elementwise it is no bound: FTRL's L1
+    threshold turns a last-bit difference of z into w = 0 against a small w (round 3: max
+    1e-1, 99.9th percentile 1.4e-3 by step 5), so the bound is on the model as a vector —
+    ||a - b|| / ||b|| <= DRIFT every step (round 3: 1.9e-6 by step 5) — and loss / AUC stay
     within 1e-4."""
-    DRIFT = 5e-3
+    DRIFT = 1e-5
     cfg = dict(V_dim=128, lr=.05, V_lr=.01)
     c = H.Context(0, max_keys=1 << 18, **cfg)
     up = O.Updater(**cfg)
@@ -287,8 +290,67 @@ def test_c5_model_drift_bound(H):
         ov, ol = up.get(uniq)
         assert np.array_equal(l.cpu().numpy(), ol)
         a, b = v.cpu().numpy().astype(np.float64), ov.astype(np.float64)
-        rel = np.abs(a - b) / (np.maximum(np.abs(a), np.abs(b)) + 1e-6)
-        worst.append(float(rel.max()))
-        assert rel.max() <= DRIFT, (step, rel.max())
-    print("C5 per-step max relative model drift:", ["%.2e" % w for w in worst])
+        # relative to each value, with close()'s absolute floor (1e-6 of the largest value)
+        rel = np.abs(a - b) / (np.maximum(np.abs(a), np.abs(b)) + 1e-6 * np.abs(b).max())
+        worst.append((float(np.linalg.norm(a - b) / np.linalg.norm(b)), float(rel.max()),
+                      float(np.quantile(rel, 0.999))))
+    print("C5 per-step model drift (norm, max, 99.9th pct of elementwise relative):",
+          ["%.2e/%.2e/%.2e" % w for w in worst])
+    assert max(w[0] for w in worst) <= DRIFT, worst
     c.close()
+
+
+# ---------------------------------------------------------------- bucket-mode Localizer
+def _ids_of(kind, rng, n):
+    if kind == "uniform":
+        return rng.integers(0, 1 << 22, n, dtype=np.uint64)
+    if kind == "narrow":       # 2^12 ids: two key digits vary
+        return rng.integers(0, 1 << 12, n, dtype=np.uint64)
+    if kind == "wide":         # every key bit varies: packing fails, LSD passes
+        return rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    if kind == "zipf":         # hot keys: a bucket beyond kSortBucketMax falls back to LSD
+        return D.zipf_keys(rng, n, 1.1, 1 << 20)
+    if kind == "fields":       # criteo-parser ids (hash << 12 | field): 39 top-digit values
+        return (rng.integers(0, 1 << 40, n, dtype=np.uint64) << np.uint64(12)) | \
+            rng.integers(0, 39, n, dtype=np.uint64)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "narrow", "wide", "zipf", "fields"])
+def test_bucket_localizer_equals_lsd(H, kind):
+    """The fused step's Localizer in bucket mode (one global pass over the top varying digit,
+    then one block per bucket: loc_bucket=1 with 256 threads, 2 with 1024) against the LSD
+    passes over every digit (loc_bucket=0): predictions, loss and AUC identical every step, the
+    model identical at the end, and both equal to the oracle within the usual tolerances.
+    Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=m, **cfg) for m in (0, 1, 2)]
+    up = O.Updater(**cfg)
+    rng = np.random.default_rng(9)
+    for step in range(4):
+        rows = 3000 if step == 3 else 60000
+        blk = D.synthetic(rows, 39, 2, ragged=(step == 3), seed=80 + step)
+        blk = D.RowBlock(blk.offs, _ids_of(kind, rng, blk.nnz), None, blk.labels)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        preds, progs = [], []
+        for c in cs:
+            pr = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+            H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pr)
+            preds.append(pr.cpu().numpy().view(np.uint32))
+            progs.append(H.progress(c))
+        assert np.array_equal(preds[0], preds[1]) and np.array_equal(preds[0], preds[2]), step
+        assert progs[0]["loss"] == progs[1]["loss"] == progs[2]["loss"], step
+        assert progs[0]["auc"] == progs[1]["auc"] == progs[2]["auc"], step
+        assert abs(progs[1]["loss"] - loss) <= 1e-4 * abs(loss), (step, progs[1]["loss"], loss)
+        assert abs(progs[1]["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    vs = [H.Store(c).pull(c.tensor(uniq, torch.int64)) for c in cs]
+    for v, l in vs[1:]:
+        assert np.array_equal(l.cpu().numpy(), vs[0][1].cpu().numpy())
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), vs[0][0].cpu().numpy().view(np.uint32))
+    st = [H.Store(c).stats() for c in cs]
+    assert st[0]["n_keys"] == st[1]["n_keys"] == st[2]["n_keys"] == up.size()
+    assert st[0]["seed"] == st[1]["seed"] == st[2]["seed"] == up.seed
+    for c in cs:
+        c.close()
