@@ -1,9 +1,11 @@
 // Context lifecycle, .conf-key parsing, device memory helpers and error plumbing.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
+#include <vector>
 
 #include "internal.h"
 

@@ -57,6 +57,10 @@ struct UpdaterParam {
   int V_dim = 0, V_threshold = 10;
   bool l1_shrk = true;
   unsigned seed = 0;
+  // not a reference parameter: sum64=1 makes orc_train_step sum every gradient column in
+  // double and round once (the exact trajectory the C5 drift test measures both the device
+  // and the reference against)
+  bool sum64 = false;
 };
 
 bool ParseKW(const char* kwargs, UpdaterParam* p) {
@@ -82,6 +86,7 @@ bool ParseKW(const char* kwargs, UpdaterParam* p) {
     else if (k == "V_threshold") vs >> p->V_threshold;
     else if (k == "l1_shrk") p->l1_shrk = !(v == "0" || v == "false");
     else if (k == "seed") vs >> p->seed;
+    else if (k == "sum64") p->sum64 = !(v == "0" || v == "false");
   }
   return true;
 }
@@ -250,10 +255,15 @@ void orc_fm_predict(int64_t B, const uint64_t* offs, const uint32_t* col, const 
 // partitioned SpMV/SpMM::TransTimes (spmv.h:139-171, spmm.h:127-159) produce for any
 // thread count.
 // ---------------------------------------------------------------------------------
-void orc_fm_calcgrad(int64_t B, const uint64_t* offs, const uint32_t* col, const float* val,
+}  // extern "C"
+
+// A = float: the reference's arithmetic.  A = double (sum64): the same float terms, every
+// column sum in double (the caller rounds once) — test infrastructure, not a reference mode.
+template <typename A>
+static void CalcGrad(int64_t B, const uint64_t* offs, const uint32_t* col, const float* val,
                      const float* label, const float* rweight, const float* weights,
                      const int32_t* w_pos, const int32_t* V_pos, int64_t ncol, int V_dim,
-                     const float* pred, float* grad) {
+                     const float* pred, A* grad) {
   std::vector<real_t> p(B);
   for (int64_t i = 0; i < B; ++i) {                 // fm_loss.h:155-165
     real_t y = label[i] > 0 ? 1 : -1;
@@ -267,14 +277,14 @@ void orc_fm_calcgrad(int64_t B, const uint64_t* offs, const uint32_t* col, const
     for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
       uint32_t c = col[j];
       if ((int64_t)c >= ncol) continue;
-      float* g;
+      A* g;
       if (w_pos) { int q = w_pos[c]; if (q == -1) continue; g = grad + q; } else { g = grad + c; }
       if (val) *g += pr * val[j]; else *g += pr;
     }
   }
   if (V_dim == 0) return;
   // XXp = (X.*X)' p  (fm_loss.h:176-182)
-  std::vector<real_t> XXp(ncol, 0.f);
+  std::vector<A> XXp(ncol, 0.f);
   for (int64_t r = 0; r < B; ++r) {
     real_t pr = p[r];
     if (pr == 0) continue;
@@ -311,11 +321,21 @@ void orc_fm_calcgrad(int64_t B, const uint64_t* offs, const uint32_t* col, const
       if ((int64_t)c >= ncol) continue;
       int q = V_pos[c];
       if (q == -1) continue;
-      float* g = grad + q;
+      A* g = grad + q;
       if (val) { real_t x = val[j]; for (int l = 0; l < V_dim; ++l) g[l] += t[l] * x; }
       else { for (int l = 0; l < V_dim; ++l) g[l] += t[l]; }
     }
   }
+}
+
+extern "C" {
+
+void orc_fm_calcgrad(int64_t B, const uint64_t* offs, const uint32_t* col, const float* val,
+                     const float* label, const float* rweight, const float* weights,
+                     const int32_t* w_pos, const int32_t* V_pos, int64_t ncol, int V_dim,
+                     const float* pred, float* grad) {
+  CalcGrad<float>(B, offs, col, val, label, rweight, weights, w_pos, V_pos, ncol, V_dim, pred,
+                  grad);
 }
 
 // Loss::Evaluate (loss.h:57-66): sum log(1+exp(-y pred)), y = label>0 ? 1 : -1.
@@ -563,9 +583,17 @@ int orc_train_step(void* h, int64_t B, const uint64_t* offs, const uint64_t* ids
   if (pred_out) memcpy(pred_out, pred.data(), B * sizeof(float));
   if (!train) return 0;
   std::vector<float> grad(nv, 0.f);
-  orc_fm_calcgrad(B, offs, col.data(), val, label, rweight, vals.data(),
-                  d > 0 ? w_pos.data() : nullptr, d > 0 ? V_pos.data() : nullptr, U, d,
-                  pred.data(), grad.data());
+  if (up->param.sum64) {
+    std::vector<double> g64(nv, 0.);
+    CalcGrad<double>(B, offs, col.data(), val, label, rweight, vals.data(),
+                     d > 0 ? w_pos.data() : nullptr, d > 0 ? V_pos.data() : nullptr, U, d,
+                     pred.data(), g64.data());
+    for (int64_t i = 0; i < nv; ++i) grad[i] = (float)g64[i];
+  } else {
+    orc_fm_calcgrad(B, offs, col.data(), val, label, rweight, vals.data(),
+                    d > 0 ? w_pos.data() : nullptr, d > 0 ? V_pos.data() : nullptr, U, d,
+                    pred.data(), grad.data());
+  }
   return orc_updater_update(h, uniq.data(), U, 3, grad.data(), nv, d > 0 ? lens.data() : nullptr);
 }
 
