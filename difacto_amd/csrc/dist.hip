@@ -905,7 +905,6 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_TRY(pipeline_init(c));
   DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1],
                 "dist_owner_begin: finish the pending InitV first (dfx_dist_initv_local / _draw)");
-  c->dist_used = true;  // slots now carry table slots across steps: no growth at sync points
   // this table serves one of nranks key ranges: hash keys by their position in the range
   DFX_TRY(table_set_ranges(c, nranks));
   const Lane OL = owner_lane(c, slot);
@@ -916,6 +915,14 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   const int64_t R = recv_offsets[nranks];
   DFX_CHECK_ARG(R < 0x7FFFFFFFll, "dist_owner_begin: too many keys");
   DFX_CHECK_ARG(R == 0 || recv_keys, "dist_owner_begin: null keys");
+  // this begin ends the slot's previous step; it inserts at most R keys and draws at most R V
+  // rows: the table grows here first if they might not fit (the reference's model is an
+  // unbounded map, sgd_updater.h:178).  Growth rehashes; a pipelined schedule's other step,
+  // which holds table positions until its push, gets them moved (table_rebuild)
+  c->dist_live[slot] = false;
+  DFX_TRY(cap_check(c, R));
+  c->dist_live[slot] = true;
+  c->dist_pushed[slot] = false;
   c->dist_R[slot] = R;
   c->dist_offs[slot].assign(recv_offsets, recv_offsets + nranks + 1);
   DFX_HIP(hipMemsetAsync(&OL.ds->totals[1], 0, 12, OL.stream));
@@ -1013,7 +1020,10 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1],
                 "dist_owner_push: finish the pending InitV first (dfx_dist_initv_local / _draw)");
   const int64_t R = c->dist_R[slot];
-  if (R == 0 && !c->dist_sum) return DFX_OK;
+  if (R == 0 && !c->dist_sum) {
+    c->dist_live[slot] = false;
+    return DFX_OK;
+  }
   DFX_CHECK_ARG(R == 0 || recv_grads, "dist_owner_push: null buffer");
   owner_segs(c, slot);  // a push with no pull before it
   const Lane OL = owner_lane(c, slot);
@@ -1041,7 +1051,13 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
                            &OL.ds->totals[3]);
     }
     // every owner takes part in the InitV ranking, with or without keys this step
-    if (c->P.V_dim > 0) c->dist_initv_pending[slot] = true;
+    c->dist_pushed[slot] = true;
+    if (c->P.V_dim > 0) {
+      c->dist_initv_pending[slot] = true;
+    } else {
+      c->dist_live[slot] = false;  // the step is done with its table positions
+      DFX_TRY(cap_record(c));
+    }
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
@@ -1064,6 +1080,8 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
                        &OL.ds->totals[1], ws.oflags.as<uint32_t>(), ws.ofrank.as<uint32_t>(),
                        c->ds, &OL.ds->totals[3]);
   if (c->P.V_dim > 0) DFX_TRY(owner_initv(c, slot, (int)c->dist_offs[slot].size() - 1));
+  c->dist_live[slot] = false;  // the step is done with its table positions
+  DFX_TRY(cap_record(c));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -1112,6 +1130,8 @@ int dfx_dist_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, i
   hipLaunchKernelGGL(k_dist_initv_sum_finalize, dim3(1), dim3(1), 0, OL.stream, ftotal,
                      counts_all_dev, nranks, c->P.V_dim, c->T.vcap, c->ds, &OL.ds->totals[3]);
   c->dist_initv_pending[slot] = false;
+  if (c->dist_pushed[slot]) c->dist_live[slot] = false;  // the step is done with the table
+  DFX_TRY(cap_record(c));
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

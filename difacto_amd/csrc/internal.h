@@ -215,7 +215,10 @@ struct Context {
   double host_wait_s = 0;
   int64_t host_waits = 0;
 
-  bool dist_used = false;  // a key-range server: its slots hold table slots across steps
+  // a key-range server's slot holds table positions (segment slots) from its owner_begin to the
+  // end of its step (the push, or its InitV draws): a table rebuild moves them with the keys
+  bool dist_live[2] = {false, false};
+  bool dist_pushed[2] = {false, false};  // the slot's gradient push ran (its InitV ends the step)
   // push_agg=sum (default): one Update per key per step on the workers' summed gradients, InitV
   // ranked over all owners (dfx_dist_initv_local / _draw); push_agg=ranks: one Update per
   // pushing worker in rank order, InitV per server (KVStoreDist's HandlePush)

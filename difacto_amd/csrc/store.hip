@@ -379,14 +379,18 @@ __global__ void k_tbl_init(Table T, int64_t cap) {
 }
 
 // re-insert every key of table O into T; with fat slots a key's V and Vaux rows move with it
-// (its vrow is its slot)
-__global__ void k_rehash(Table O, int64_t ocap, Table T, DevState* ds) {
+// (its vrow is its slot).  map (optional): map[old slot] = its new slot
+__global__ void k_rehash(Table O, int64_t ocap, Table T, DevState* ds, uint32_t* map) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ocap) return;
   Entry e = *ent_at(O, i);
-  if (e.key == kEmptyKey) return;
+  if (e.key == kEmptyKey) {
+    if (map) map[i] = kNoSlot;
+    return;
+  }
   bool ins;
   int64_t s = tbl_insert(T, e.key, &ins);
+  if (map) map[i] = s < 0 ? kNoSlot : (uint32_t)s;
   if (s < 0) { atomicOr(&ds->err, kErrTableFull); return; }
   if (T.es && e.vrow >= 0) {
     const float* V0 = row_V(O, e.vrow);
@@ -418,26 +422,54 @@ static int table_alloc_entries(Table* T, int64_t cap, hipStream_t st) {
   return DFX_OK;
 }
 
+// a live key-range server step's segment slots, moved to the rebuilt table
+__global__ void k_remap_segslots(uint32_t* segslot, const uint32_t* nseg, int64_t bound,
+                                 const uint32_t* map) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= bound || u >= (int64_t)*nseg) return;
+  const uint32_t s = segslot[u];
+  if (s != kNoSlot) segslot[u] = map[s];
+}
+
 // Rebuild the table as NT (new hash parameters and/or capacity): every entry of the old
 // table is re-inserted.  The old table is freed only once every entry landed; on a failure
-// (a full new table) the old one stays and the error is returned.
+// (a full new table) the old one stays and the error is returned.  A key-range server's step
+// slots that hold table positions across calls (dfx_dist_owner_begin to its push / InitV: a
+// pipelined schedule's other step) get their positions moved with the keys.
 static int table_rebuild(Context* c, Table NT, int64_t new_cap) {
   Table& T = c->T;
   DFX_TRY(table_alloc_entries(&NT, new_cap, c->stream));
   int err0 = 0, err1 = 0;
   DFX_HIP(hipMemcpyAsync(&err0, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
+  const bool remap = (c->dist_live[0] && !c->dist_segs_pending[0] && c->dist_R[0] > 0) ||
+                     (c->dist_live[1] && !c->dist_segs_pending[1] && c->dist_R[1] > 0);
+  uint32_t* map = nullptr;
+  if (remap) DFX_HIP(hipMalloc(&map, (size_t)c->cap * sizeof(uint32_t)));
   hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T,
-                     c->cap, NT, c->ds);
+                     c->cap, NT, c->ds, map);
   DFX_HIP(hipGetLastError());
   DFX_HIP(hipMemcpyAsync(&err1, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   if ((err1 & ~err0) & kErrTableFull) {
     (void)hipFree(NT.ent);
     if (NT.es) (void)hipFree(NT.V);
+    if (map) (void)hipFree(map);
     DFX_HIP(hipMemcpy(&c->ds->err, &err0, sizeof(int), hipMemcpyHostToDevice));
     set_error("table rebuild: the new table cannot hold every key; the old table is kept");
     return DFX_ERR_CAPACITY;
+  }
+  for (int s = 0; s < 2 && map; ++s) {
+    const int64_t R = c->dist_R[s];
+    if (!c->dist_live[s] || c->dist_segs_pending[s] || R <= 0) continue;
+    hipLaunchKernelGGL(k_remap_segslots, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,
+                       c->stream, c->ows[s].osegslot.as<uint32_t>(), &c->ods[s]->totals[1], R,
+                       map);
+    DFX_HIP(hipGetLastError());
+  }
+  if (map) {
+    DFX_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(map);
   }
   (void)hipFree(T.ent);
   if (T.es) (void)hipFree(T.V);
@@ -481,7 +513,7 @@ int table_set_ranges(Context* c, int nranks) {
 }
 
 int table_alloc(Context* c, int64_t n_keys, int64_t n_vrows) {
-  if (n_keys < 1024) n_keys = 1024;
+  if (n_keys < 64) n_keys = 64;
   int64_t cap = 1;
   while (cap < 2 * n_keys) cap <<= 1;
   Table& T = c->T;
@@ -645,7 +677,7 @@ int store_maybe_grow(Context* c) {
   if (!c->T.ent) return DFX_OK;
   HostCounters h;
   DFX_TRY(read_counters(c, &h));
-  if (c->autogrow && !c->dist_used && 2 * (int64_t)h.n_keys > c->cap)
+  if (c->autogrow && 2 * (int64_t)h.n_keys > c->cap)
     DFX_TRY(grow_to(c, (int64_t)h.n_keys, 0));
   // the stream is idle: every recorded count is complete, and the exact ones are at hand
   CapGuard& g = c->capg;

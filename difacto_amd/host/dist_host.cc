@@ -29,6 +29,14 @@ void NcclCheck(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) Fail(std::string(what) + ": " + ncclGetErrorString(r));
 }
 void DfxOk(int status, const char* what) {
+  if (status == DFX_ERR_CAPACITY) {
+    // a clean stop before a step could overflow the model (no step was issued): the queued
+    // work drains and the process exits with an error status rather than aborting
+    std::fprintf(stderr, "[FATAL] %s: %s\n", what, dfx_last_error());
+    std::fflush(stderr);
+    (void)hipDeviceSynchronize();
+    std::_Exit(3);
+  }
   if (status != DFX_OK) Fail(std::string(what) + ": " + dfx_last_error());
 }
 

@@ -17,8 +17,8 @@ namespace difacto {
 
 namespace {
 
-enum Op { kOpNone = 0, kOpCount = 1, kOpPull = 2, kOpGrad = 3, kOpBarrier = 4 };
-constexpr int kFlagStop = 5, kFlags = 6;  // per rank: its head ops (one-hot) and "stopping"
+enum Op { kOpNone = 0, kOpCount = 1, kOpPull = 2, kOpGrad = 3, kOpBarrier = 4, kOpReduce = 5 };
+constexpr int kFlagStop = 6, kFlags = 7;  // per rank: its head ops (one-hot) and "stopping"
 
 // one request of a worker, queued until a round serves it.  The SArrays are shared handles:
 // the request keeps the caller's buffers alive (ps-lite's KVWorker holds them the same way)
@@ -31,6 +31,7 @@ struct Req {
   SArray<int> lens;
   SArray<real_t>* out_vals = nullptr;
   SArray<int>* out_lens = nullptr;
+  std::vector<double>* red = nullptr;  // kOpReduce: the process's values (one local worker's)
   std::function<void()> cb;
 };
 
@@ -225,7 +226,8 @@ void GpuDistStore::Core::Loop() {
   // while the executor still works on the previous batch), so the others run first
   auto find = [&](int l, int op) -> int {
     if (q[l].empty()) return -1;
-    if (!lockstep || op == kOpCount || op == kOpBarrier) return q[l].front().op == op ? 0 : -1;
+    if (!lockstep || op == kOpCount || op == kOpBarrier || op == kOpReduce)
+      return q[l].front().op == op ? 0 : -1;
     for (size_t i = 0; i < q[l].size(); ++i)
       if (q[l][i].op != kOpCount) return q[l][i].op == op ? (int)i : -1;
     return -1;
@@ -237,7 +239,7 @@ void GpuDistStore::Core::Loop() {
       std::lock_guard<std::mutex> lk(mu);
       for (int l = 0; l < L; ++l) {
         const size_t r = (size_t)ex->rank(l);
-        for (int o : {kOpCount, kOpPull, kOpGrad, kOpBarrier})
+        for (int o : {kOpCount, kOpPull, kOpGrad, kOpBarrier, kOpReduce})
           if (find(l, o) >= 0) flags[r * kFlags + o] = 1.0;
         if (stopping) flags[r * kFlags + kFlagStop] = 1.0;
       }
@@ -250,22 +252,23 @@ void GpuDistStore::Core::Loop() {
       cv_done.notify_all();
       return;
     }
-    int nop[kFlags] = {0, 0, 0, 0, 0, 0};
+    int nop[kFlags] = {0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < N; ++r)
       for (int o = 1; o < kFlags; ++o) nop[o] += flags[(size_t)r * kFlags + o] != 0 ? 1 : 0;
-    // one kind per round, the first servable of gradient push, pull, count push, barrier:
-    // lockstep, when every worker has one; async, for whoever has one at its head.  A barrier
-    // needs everyone
+    // one kind per round, the first servable of gradient push, pull, count push, barrier,
+    // reduce: lockstep, when every worker has one; async, for whoever has one at its head.  A
+    // barrier or a reduce needs everyone
     int kind = kOpNone;
-    for (int o : {kOpGrad, kOpPull, kOpCount, kOpBarrier}) {
-      if (lockstep || o == kOpBarrier ? nop[o] == N : nop[o] > 0) {
+    for (int o : {kOpGrad, kOpPull, kOpCount, kOpBarrier, kOpReduce}) {
+      if (lockstep || o == kOpBarrier || o == kOpReduce ? nop[o] == N : nop[o] > 0) {
         kind = o;
         break;
       }
     }
     const bool work = kind != kOpNone;
     if (!work) {
-      const bool pending = nop[kOpCount] || nop[kOpPull] || nop[kOpGrad] || nop[kOpBarrier];
+      const bool pending = nop[kOpCount] || nop[kOpPull] || nop[kOpGrad] || nop[kOpBarrier] ||
+                           nop[kOpReduce];
       if (nop[kFlagStop] == N) {
         // every process is stopping: the store is done.  Requests still queued can never be
         // served (lockstep: a worker issued calls the others did not)
@@ -303,6 +306,13 @@ void GpuDistStore::Core::Loop() {
         if (op == kOpBarrier) {
           std::vector<double> one(1, 1.0);
           ex->AllReduceSum(&one);
+        } else if (op == kOpReduce) {
+          // the process's values ride on one local worker's request; the exchange's own
+          // collectives are issued by this thread only, so every rank issues them in one order
+          std::vector<double>* v = nullptr;
+          for (int l = 0; l < L; ++l)
+            if (reqs[l] && reqs[l]->red) v = reqs[l]->red;
+          if (v) ex->AllReduceSum(v);
         } else {
           Exec(op, reqs);
         }
@@ -549,6 +559,18 @@ GpuDistStore::GpuDistStore(std::unique_ptr<Core> core) : core_(std::move(core)) 
 }
 
 GpuDistStore::~GpuDistStore() { core_->Stop(); }
+
+void GpuDistStore::AllReduceSum(std::vector<double>* v) {
+  DFX_HOST_CHECK(t_in_callback_of < 0, "GpuDistStore::AllReduceSum from a request callback");
+  std::vector<int> ts(core_->L);
+  for (int l = 0; l < core_->L; ++l) {
+    Req r;
+    r.op = kOpReduce;
+    r.red = l == 0 ? v : nullptr;
+    ts[l] = core_->Enqueue(l, std::move(r));
+  }
+  for (int l = 0; l < core_->L; ++l) core_->Wait(l, ts[l]);
+}
 
 std::shared_ptr<GpuDistStore> GpuDistStore::CreateLoopback(int nshards, const KWArgs& kwargs) {
   DFX_HOST_CHECK(nshards >= 1, "GpuDistStore: nshards >= 1");

@@ -57,6 +57,11 @@ class GpuDistStore {
   /** the server context of local shard l (model save / load / stats) */
   dfx_ctx* shard(int local) const;
   ShardExchange* exchange() const;
+  /** element-wise sum of v over the processes (every process calls it once, its local workers
+   * having summed into v): served by the progress thread in a round of its own, in the same
+   * order as the store's exchanges on every rank.  While the store lives, use this, not
+   * exchange()->AllReduceSum, whose collectives the progress thread also issues */
+  void AllReduceSum(std::vector<double>* v);
 
   struct Core;
 

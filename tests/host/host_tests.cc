@@ -260,7 +260,7 @@ static int RunDist(int argc, char** argv) {
       sum[1] += p.auc;
       sum[2] += p.nrows;
     }
-    ex->AllReduceSum(&sum);
+    ds->AllReduceSum(&sum);
     if (ex->rank(0) == 0)
       std::printf("epoch %d loss %.9e auc %.9e nrows %.0f\n", ep, sum[0], sum[1], sum[2]);
     std::fflush(stdout);
@@ -429,7 +429,7 @@ static int RunDistAsync(int argc, char** argv) {
       sum[1] += p.auc;
       sum[2] += p.nrows;
     }
-    ex->AllReduceSum(&sum);
+    ds->AllReduceSum(&sum);
     EXPECT(sum[2] == (double)n, "epoch %d nrows %.0f want %zu", ep, sum[2], n);
     if (ex->rank(0) == 0)
       std::printf("epoch %d loss %.9e auc %.9e nrows %.0f\n", ep, sum[0], sum[1], sum[2]);

@@ -224,13 +224,18 @@ def _slice(blk, rows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("agg", ["sum", "ranks"])
+@pytest.mark.parametrize("agg,max_keys", [("sum", 65536), ("ranks", 65536), ("sum", 256),
+                                          ("ranks", 256)])
 @pytest.mark.parametrize("pipelined", [1, 0])
-def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined, agg):
+def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined, agg, max_keys):
     """dfx_train shards=3: the C++ sharded store (dist_host.cc, loopback exchange) against the
     sharded oracle of the same schedule, on the batches the driver forms (shard r reads part
     r of 3, batches of 10 rows, shards step together with empty batches once done): per-epoch
-    loss, and every server's saved part against the oracle's server state"""
+    loss, and every server's saved part against the oracle's server state.
+    max_keys=256: each server's table starts below its ~900 keys and grows at the owner
+    steps' begins (the reference's model is an unbounded map, sgd_updater.h:178); in the
+    pipelined schedule the other step, which holds table positions until its push, gets them
+    moved by the rebuild"""
     import numpy as np
     from oracle import dist_oracle as DO
     from oracle import oracle as O
@@ -241,7 +246,7 @@ def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined, agg):
     args = [TRAIN_BIN, "data_in=" + DATA, "shards=%d" % N, "pipelined=%d" % pipelined,
             "num_jobs_per_epoch=1", "shuffle=0", "batch_size=%d" % bs,
             "max_num_epochs=%d" % epochs, "stop_rel_objv=0", "model_out=" + model, "has_aux=1",
-            "max_keys=65536", "push_agg=" + agg] + ["%s=%s" % kv for kv in kw.items()]
+            "max_keys=%d" % max_keys, "push_agg=" + agg] + ["%s=%s" % kv for kv in kw.items()]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
@@ -312,13 +317,16 @@ def test_train_driver_sharded_rccl_world1(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shards,agg", [(3, "sum"), (3, "ranks"), (-1, "sum")])
-def test_dist_store_iterate_data_matches_oracle(tmp_path, shards, agg):
+@pytest.mark.parametrize("shards,agg,max_keys", [(3, "sum", 65536), (3, "ranks", 65536),
+                                                 (-1, "sum", 65536), (3, "sum", 256),
+                                                 (-1, "sum", 256)])
+def test_dist_store_iterate_data_matches_oracle(tmp_path, shards, agg, max_keys):
     """GpuDistStore behind the reference's Store interface (dist_store.h): IterateData's
     executor (Compact -> Push(kFeaCount) + Wait -> Pull -> Predict / Evaluate / AUC -> CalcGrad
     -> Push(kGradient), through GpuSGDLearner's interface path) with N=3 loopback workers on
     their own threads, or one RCCL worker (world 1), against the synchronous sharded oracle of
-    the same aggregation: per-epoch loss and AUC, and every server's saved part"""
+    the same aggregation: per-epoch loss and AUC, and every server's saved part.  max_keys=256:
+    the servers' tables start far below the model and grow mid-run (sgd_updater.h:178)"""
     import numpy as np
     from oracle import dist_oracle as DO
     from oracle import oracle as O
@@ -329,7 +337,7 @@ def test_dist_store_iterate_data_matches_oracle(tmp_path, shards, agg):
     model = str(tmp_path / "m")
     env = dict(os.environ, DFX_COMM_ID_FILE=str(tmp_path / "id"))
     r = subprocess.run([BIN, "dist", DATA, "shards=%d" % shards, "epochs=%d" % epochs,
-                        "batch_size=%d" % bs, "model_out=" + model, "max_keys=65536",
+                        "batch_size=%d" % bs, "model_out=" + model, "max_keys=%d" % max_keys,
                         "push_agg=" + agg] + ["%s=%s" % kv for kv in kw.items()],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
