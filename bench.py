@@ -176,7 +176,7 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r2e"
+PMC_ROUND = "r3"
 
 # Random 128-byte chunks per second on MI355X, measured in isolation (tools/membench/pmccal,
 # DESIGN.md (d)): reads of distinct random rows, and read-modify-writes of them
