@@ -436,6 +436,18 @@ def main():
     phases = {p: v * nrec / max(nrec_diag, 1) for p, v in phases.items()}  # per timed step
     phases["backward_update"] = bwd_ms
     lanes = H.prof_lanes(ctx)
+    # the host's own cost of a step call, measured on an idle device (a sync before each call:
+    # no capacity-guard wait, no full hardware queue to block a launch) — in the timed loop the
+    # call time also holds the blocks of a host running ahead of the device
+    H.prof_enable(ctx, 0)
+    host_idle = []
+    for bt in batches[:20]:
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        step(bt, False)
+        host_idle.append(time.perf_counter() - t)
+    torch.cuda.synchronize()
+    host_idle.sort()
     H.progress(ctx)
     ctx.sync()
     st = H.Store(ctx).stats()
@@ -486,6 +498,7 @@ def main():
         # (which lets the host run a few steps ahead of the device, then blocks it)
         "host_busy_ms_per_step": round((t_enq - host_wait["wait_s"]) / args.steps * 1e3, 4),
         "host_waits": host_wait["waits"],
+        "host_call_ms_idle_device": round(host_idle[len(host_idle) // 2] * 1e3, 4),
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
         "mean_unique_keys": round(mean_u, 1),
         "mean_live_v_keys": counts["U_V"] and round(counts["U_V"], 1),

@@ -390,6 +390,10 @@ int store_reserve(Context* c, int64_t n_keys, int64_t n_vrows);
 // point when needed (kwarg autogrow=0: no-op).  cap_record after that work is enqueued.
 int cap_check(Context* c, int64_t add);
 int cap_record(Context* c);
+// cap_record in two halves: the pinned ring entry for {n_keys, n_vrows} (NULL: no guard), to be
+// written by the caller's last kernel on the context stream, then the entry's event
+int cap_record_slot(Context* c, unsigned long long** slot);
+int cap_record_commit(Context* c);
 void cap_release(Context* c);
 // at a sync point (the stream is idle): grow the table once its load passes 0.5
 int store_maybe_grow(Context* c);

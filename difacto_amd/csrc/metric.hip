@@ -209,6 +209,119 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
   }
 }
 
+// Small snapshots (B <= kAbMax, e.g. B = 10^4 rows per GPU): ONE 1024-thread block sorts
+// (orderable pred, input index << 1 | label) in LDS — four stable 8-bit LSD passes ranked by
+// wave ballots as in k_auc_runs — then scans the sorted labels and adds, per negative, the
+// positives ranked below it, and writes AUC*n (k_auc_final's rules): one launch, where the
+// radix lane takes ~14 latency-bound launches (~0.12 ms of lane time at B = 10^4,
+// profiles/r3/kernel_summary_b1e4_pipelined.md).  Same stable order, so the same AUC exactly.
+constexpr int kAbNT = 1024, kAbItems = 12, kAbMax = kAbNT * kAbItems;  // 12288 rows, 152 KiB
+
+__global__ __launch_bounds__(kAbNT) void k_auc_block(int64_t n, const uint32_t* __restrict__ key,
+                                                     const uint32_t* __restrict__ lab,
+                                                     double* out, int accumulate) {
+  __shared__ uint32_t lk[2][kAbMax];
+  __shared__ uint16_t ll[2][kAbMax];  // (input index << 1) | label
+  __shared__ uint16_t wcnt[kAbNT / kWave][256];
+  __shared__ uint32_t lds[kAbNT / kWave + 1];
+  __shared__ double red[kAbNT / kWave];
+  const int t = threadIdx.x, w = t / kWave, l = lane_id();
+  const int m = (int)n;
+  for (int i = t; i < m; i += kAbNT) {
+    lk[0][i] = key[i];
+    ll[0][i] = (uint16_t)((i << 1) | (lab[i] & 1u));
+  }
+  __syncthreads();
+  int src = 0;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 8 * pass;
+    for (int i = t; i < (kAbNT / kWave) * 256; i += kAbNT) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t dr[kAbItems];
+    const int wb = w * kWave * kAbItems;  // wave w ranks items [wb, wb + 64 * kAbItems) in order
+#pragma unroll
+    for (int c = 0; c < kAbItems; ++c) {
+      const int idx = wb + c * kWave + l;
+      const bool valid = idx < m;
+      const uint32_t d = valid ? (lk[src][idx] >> shift) & 255u : 0u;
+      uint64_t peers = __ballot(valid);
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t mb = __ballot(valid && bit);
+        peers &= bit ? mb : ~mb;
+      }
+      if (!valid) peers = 0;
+      const uint32_t r = (uint32_t)__popcll(peers & lanemask_lt());
+      const uint32_t old = valid ? wcnt[w][d] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && r == 0) wcnt[w][d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+      __builtin_amdgcn_wave_barrier();
+      dr[c] = d | ((old + r) << 8);
+    }
+    __syncthreads();
+    // per digit (threads 0..255): the waves' exclusive offsets, then the digits' starts
+    uint32_t cnt = 0;
+    if (t < 256) {
+#pragma unroll
+      for (int i = 0; i < kAbNT / kWave; ++i) {
+        const uint32_t x = wcnt[i][t];
+        wcnt[i][t] = (uint16_t)cnt;
+        cnt += x;
+      }
+    }
+    const uint32_t start = block_excl_scan<kAbNT>(cnt, lds, nullptr);
+    if (t < 256) {
+#pragma unroll
+      for (int i = 0; i < kAbNT / kWave; ++i) wcnt[i][t] = (uint16_t)(wcnt[i][t] + start);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kAbItems; ++c) {
+      const int idx = wb + c * kWave + l;
+      if (idx < m) {
+        const uint32_t d = dr[c] & 255u;
+        const uint32_t pos = wcnt[w][d] + (dr[c] >> 8);
+        lk[src ^ 1][pos] = lk[src][idx];
+        ll[src ^ 1][pos] = ll[src][idx];
+      }
+    }
+    __syncthreads();
+    src ^= 1;
+  }
+  // the sorted labels: thread t holds items [t * kAbItems, ...); positives below each negative
+  const int base = t * kAbItems;
+  uint32_t lb[kAbItems], s = 0;
+#pragma unroll
+  for (int c = 0; c < kAbItems; ++c) {
+    lb[c] = base + c < m ? (uint32_t)(ll[src][base + c] & 1u) : 0u;
+    s += lb[c];
+  }
+  uint32_t npos = 0;
+  uint32_t cum = block_excl_scan<kAbNT>(s, lds, &npos);
+  double area = 0;
+#pragma unroll
+  for (int c = 0; c < kAbItems; ++c) {
+    if (lb[c]) cum += 1;
+    else if (base + c < m) area += (double)cum;
+  }
+  for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
+  if (l == 0) red[w] = area;
+  __syncthreads();
+  if (t == 0) {
+    double a = 0;
+    for (int i = 0; i < kAbNT / kWave; ++i) a += red[i];
+    const double P = (double)npos;
+    double r;
+    if (P == 0 || P == (double)n) {
+      r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
+    } else {
+      a /= P * ((double)n - P);
+      r = (a < 0.5 ? 1 - a : a) * (double)n;
+    }
+    *out = accumulate ? *out + r : r;
+  }
+}
+
 // AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix) {
   Workspace& ws = *L.ws;
@@ -217,6 +330,13 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool 
     return DFX_OK;
   }
   DFX_TRY(auc_reserve(ws, B, L.stream));
+  if (B <= kAbMax) {  // one block in LDS (both auc_sort modes: the same stable order)
+    hipLaunchKernelGGL(k_auc_block, dim3(1), dim3(kAbNT), 0, L.stream, B,
+                       ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), out_dev,
+                       accumulate ? 1 : 0);
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
+  }
   const int64_t ntiles = (B + kArTile - 1) / kArTile;
   const uint32_t* V0 = nullptr;
   const uint32_t* V1 = nullptr;

@@ -178,11 +178,28 @@ __global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ 
   pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent_at(T, s));
 }
 
-__global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B,
-                                const uint32_t* initv_total, int d, int64_t vcap) {
+// the step's last kernel: the forward's loss partials summed (k_sum_parts' order exactly),
+// the progress counters, the InitV pass's seed advance, and the capacity guard's counts into
+// its pinned ring entry (cap_host, or NULL)
+constexpr int kFinNT = 1024;
+__global__ __launch_bounds__(kFinNT) void k_step_finalize(DevState* ds, const DevState* bds,
+                                                          int64_t B, const uint32_t* initv_total,
+                                                          int d, int64_t vcap,
+                                                          const double* loss_part, int64_t nparts,
+                                                          unsigned long long* cap_host) {
+  __shared__ double red[kFinNT / kWave];
+  double a = 0;
+  for (int64_t i = threadIdx.x; i < nparts; i += kFinNT) a += loss_part[i];
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double loss = 0;
+  for (int k = 0; k < kFinNT / kWave; ++k) loss += red[k];
+  ds->scratch[3] = loss;
   // sgd::Progress: nrows, loss (sgd_learner.cc:213-229); the AUC lane adds its own
   ds->prog[0] += (double)B;
-  ds->prog[1] += ds->scratch[3];
+  ds->prog[1] += loss;
   ds->sum_u += (double)bds->u_count;
   ds->n_steps += 1;
   ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
@@ -193,6 +210,10 @@ __global__ void k_step_finalize(DevState* ds, const DevState* bds, int64_t B,
     ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * n);
     const unsigned long long nv = ds->n_vrows + n;
     ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+  }
+  if (cap_host) {
+    cap_host[0] = ds->n_keys;
+    cap_host[1] = ds->n_vrows;
   }
 }
 
@@ -308,7 +329,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
   prof_mark(c, 4);
-  sum_parts(c, a.loss_part, nblk, &c->ds->scratch[3], false);
+  // (the forward's loss partials are summed by k_step_finalize, the step's last kernel)
 
   // ---- aux lane: AUC of this batch's predictions, beside the backward
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
@@ -344,10 +365,12 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     prof_mark(c, 6);
   }
   const bool initv = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 && d > 0;
-  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, bds, B,
-                     initv ? total : nullptr, d, c->T.vcap);
+  unsigned long long* cap_host = nullptr;
+  DFX_TRY(cap_record_slot(c, &cap_host));
+  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(kFinNT), 0, c->stream, c->ds, bds, B,
+                     initv ? total : nullptr, d, c->T.vcap, a.loss_part, (int64_t)nblk, cap_host);
   DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
-  DFX_TRY(cap_record(c));
+  DFX_TRY(cap_record_commit(c));
   prof_mark(c, 7);
   if (c->prof_n < c->prof_max) ++c->prof_n;
   DFX_HIP(hipGetLastError());

@@ -598,7 +598,10 @@ static int cap_pop_oldest(Context* c, bool wait, bool* popped) {
   return DFX_OK;
 }
 
-int cap_record(Context* c) {
+// the ring entry the next recorded counts go to: the step's last kernel may write them there
+// itself (k_step_finalize: one launch less than a copy), then cap_record_commit
+int cap_record_slot(Context* c, unsigned long long** slot) {
+  *slot = nullptr;
   if (!c->autogrow) return DFX_OK;
   CapGuard& g = c->capg;
   if (!g.host) {
@@ -608,14 +611,29 @@ int cap_record(Context* c) {
   }
   bool popped;
   if (g.count == kCapRing) DFX_TRY(cap_pop_oldest(c, true, &popped));
+  *slot = g.host + 2 * g.head;
+  return DFX_OK;
+}
+
+// the counts of the slot cap_record_slot returned are written by work already on the stream
+int cap_record_commit(Context* c) {
+  if (!c->autogrow) return DFX_OK;
+  CapGuard& g = c->capg;
   const int i = g.head;
-  static_assert(offsetof(DevState, n_vrows) == offsetof(DevState, n_keys) + 8, "layout");
-  DFX_HIP(hipMemcpyAsync(g.host + 2 * i, &c->ds->n_keys, 16, hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipEventRecord(g.ev[i], c->stream));
   g.enq_at[i] = g.enq_total;
   g.head = (g.head + 1) % kCapRing;
   ++g.count;
   return DFX_OK;
+}
+
+int cap_record(Context* c) {
+  unsigned long long* slot = nullptr;
+  DFX_TRY(cap_record_slot(c, &slot));
+  if (!slot) return DFX_OK;
+  static_assert(offsetof(DevState, n_vrows) == offsetof(DevState, n_keys) + 8, "layout");
+  DFX_HIP(hipMemcpyAsync(slot, &c->ds->n_keys, 16, hipMemcpyDeviceToHost, c->stream));
+  return cap_record_commit(c);
 }
 
 void cap_release(Context* c) {

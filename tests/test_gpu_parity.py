@@ -216,15 +216,19 @@ def test_auc_and_evaluate(H):
     assert H.auc(c, c.tensor(np.ones(n, np.float32), torch.float32), tp) == 1.0
 
 
-@pytest.mark.parametrize("n", [1, 4095, 4097, 100000, 1000003])
+@pytest.mark.parametrize("n", [1, 2, 4095, 4097, 10000, 12288, 12289, 100000, 1000003])
 def test_auc_radix_and_merge_sorts_agree(H, n):
-    """the AUC lane's two stable sorts (auc_sort=radix | merge): the same AUC*n, equal to the
-    input-order tie break of the oracle, with heavy ties (quantised predictions, one constant
-    digit pattern) and with all predictions equal (epoch 0, w = 0)"""
+    """the AUC lane's two stable sorts (auc_sort=radix | merge; up to 12288 rows both take the
+    one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie break of
+    the oracle, with heavy ties (quantised predictions, one constant digit pattern), with all
+    predictions equal (epoch 0, w = 0) and with signed zeros (-0 == +0)"""
     rng = np.random.default_rng(n)
     label = np.where(rng.random(n) < 0.25, 1.0, -1.0).astype(np.float32)
+    signed0 = np.where(rng.random(n) < 0.5, np.float32(-0.0), np.float32(0.0)).astype(np.float32)
+    signed0[rng.random(n) < 0.3] = -1.5
     for pred in [np.round(rng.standard_normal(n) * 8).astype(np.float32) / 8,
-                 np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32)]:
+                 np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32),
+                 signed0]:
         want = O.auc_stable_ties(label, pred) if O.has_ties(pred) else O.auc(label, pred)
         got = []
         for mode in ["radix", "merge"]:

@@ -9,9 +9,9 @@ run() {  # name, then bench arguments
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r, f = d["roofline"], d.get("roofline_forward", {})
-print("%-10s %8.2f M ex/s  %.4f ms/step  bwd frac %.3f  fwd frac %.3f  host busy %.4f ms  U %.0f U_V %s"
+print("%-10s %8.2f M ex/s  %.4f ms/step  bwd frac %.3f  fwd frac %.3f  host call %.4f ms  U %.0f U_V %s"
       % (sys.argv[1].split("cfg_")[1][:-4], d["value"] / 1e6, d["ms_per_step"], r["frac"],
-         f.get("frac", 0), d.get("host_busy_ms_per_step", -1), d["mean_unique_keys"],
+         f.get("frac", 0), d.get("host_call_ms_idle_device", -1), d["mean_unique_keys"],
          d.get("mean_live_v_keys")))
 PY
 }
