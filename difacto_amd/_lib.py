@@ -154,7 +154,9 @@ def check(rc):
 
 
 # ---- libdfx_dist.so: the multi-GPU split driver (include/difacto_amd_dist.h) ----------------
-DIST_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libdfx_dist.so")
+# beside the core library it links (an A/B build's DFX_LIB_PATH brings its own driver: a
+# driver from another directory would load a second, different copy of the core library)
+DIST_PATH = os.path.join(os.path.dirname(os.path.abspath(LIB_PATH)), "libdfx_dist.so")
 _dist = None
 u32 = ctypes.c_uint32
 

@@ -70,7 +70,12 @@ struct FwdArgs {
 // sum_l XXVV_l | 0 0] (d + 4 floats: the partial exchange is ~half as large, and the regrouped
 // sums are within the tolerance either way)
 __host__ __device__ inline int split_part_floats(int d, int n) { return n > 1 ? d + 4 : 2 * d + 4; }
-__host__ __device__ inline int split_pxv_floats(int d) { return d + 4; }
+// [XV*p (d) | p | pad] rows of the split's all-gather: wide = whole 128-byte lines (the fused
+// step's xvp_row layout: one line per occurrence in the backward), else d + 4 floats
+__host__ __device__ inline int split_pxv_floats(int d, int wide = 0) {
+  const int w = (d + 1 + 31) / 32 * 32;
+  return (wide && d > 0 && w > d + 4) ? w : d + 4;
+}
 
 struct BwdArgs {
   int no_fat_spec;           // fat slots: no V / Vaux loads beside the home entry (A/B)

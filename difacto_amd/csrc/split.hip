@@ -153,14 +153,14 @@ __global__ void k_split_offsets(const uint32_t* excl, const uint32_t* total, int
 // (fm_loss.h:110-119), Evaluate, the AUC snapshot and CalcGrad's per-row factors
 // (fm_loss.h:155-199): pxv row [XV*p (d) | p | 0 0 0]
 __global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, int n, int d,
-                                                         const float* __restrict__ parts,
+                                                         int PX, const float* __restrict__ parts,
                                                          const float* label, const float* rw,
                                                          float* pred_out, float* pxv,
                                                          double* loss_part, uint32_t* auc_key,
                                                          uint32_t* auc_lab) {
   __shared__ double red[kSpNT / kWave];
   const int64_t r = (int64_t)blockIdx.x * kSpNT + threadIdx.x;
-  const int PS = split_part_floats(d, n), PX = split_pxv_floats(d);
+  const int PS = split_part_floats(d, n);
   const bool compact = n > 1;  // [XV | sum w x | sum_l XXVV_l | 0 0] per owner
   double loss = 0;
   if (r < B) {
@@ -223,6 +223,82 @@ __global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, i
   }
 }
 
+// k_split_combine with G lanes per row (V_dim % 4 == 0, G = pow2 >= V_dim / 4): lane l sums
+// coordinates [4l, 4l + 4) of the owners' partials with float4 loads, in rank order; the serial
+// sum over l of the reference (fm_loss.h:110-113) is taken by every lane through shuffles in l
+// order, so results are bit-identical to k_split_combine's, with coalesced row reads
+template <int G>
+__global__ __launch_bounds__(kSpNT) void k_split_combine_vec(int64_t B, int64_t M, int n, int d,
+                                                             int PX,
+                                                             const float* __restrict__ parts,
+                                                             const float* label, const float* rw,
+                                                             float* pred_out, float* pxv,
+                                                             double* loss_part, uint32_t* auc_key,
+                                                             uint32_t* auc_lab) {
+  __shared__ double red[kSpNT / kWave];
+  constexpr int RPB = kSpNT / G;
+  const int l = threadIdx.x % G;
+  const int gbase = (threadIdx.x % kWave) - l;
+  const int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / G;
+  const int PS = split_part_floats(d, n);
+  const bool compact = n > 1;
+  const bool mine = 4 * l < d;
+  double loss = 0;
+  if (r < B) {
+    float acc = 0.f, xx1 = 0.f;
+    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), xx = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int o = 0; o < n; ++o) {
+      const float* q = parts + ((int64_t)o * M + r) * PS;
+      acc += q[compact ? d : 2 * d];
+      if (compact) xx1 += q[d + 1];
+      if (mine) {
+        const float4 v = *reinterpret_cast<const float4*>(q + 4 * l);
+        xv.x += v.x; xv.y += v.y; xv.z += v.z; xv.w += v.w;
+        if (!compact) xx = *reinterpret_cast<const float4*>(q + d + 4 * l);  // one owner
+      }
+    }
+    float t4[4];
+    const float xk[4] = {xv.x, xv.y, xv.z, xv.w}, yk[4] = {xx.x, xx.y, xx.z, xx.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t4[k] = compact ? xk[k] * xk[k] : xk[k] * xk[k] - yk[k];
+    float s = 0.f;
+    for (int q = 0; q < G; ++q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float tk = __shfl(t4[k], gbase + q, kWave);
+        if (4 * q + k < d) s += tk;
+      }
+    }
+    if (compact) s -= xx1;
+    const double y = (double)acc + .5 * (double)s;
+    float pr = (float)y;
+    pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);
+    const float p = logit_p(label[r], pr, rw, r);
+    float* x = pxv + r * PX;
+    if (mine)  // XV_ *= p (fm_loss.h:196-199)
+      *reinterpret_cast<float4*>(x + 4 * l) = make_float4(xv.x * p, xv.y * p, xv.z * p, xv.w * p);
+    if (l == 0) {
+      if (pred_out) pred_out[r] = pr;
+      *reinterpret_cast<float4*>(x + d) = make_float4(p, 0.f, 0.f, 0.f);
+      const double yy = label[r] > 0 ? 1.0 : -1.0;
+      loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+      if (auc_key) {
+        const uint32_t u = __float_as_uint(pr + 0.0f);
+        auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        auc_lab[r] = label[r] > 0 ? 1u : 0u;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0;
+    for (int i = 0; i < kSpNT / kWave; ++i) t += red[i];
+    loss_part[blockIdx.x] = t;
+  }
+}
+
 __global__ void k_split_worker_finalize(DevState* ds, int64_t B) {
   ds->prog[0] += (double)B;       // sgd::Progress of this worker (sgd_learner.cc:213-229)
   ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
@@ -249,7 +325,9 @@ int dfx_split_part_floats(dfx_ctx* ctx, int nranks) {
   return ctx && nranks >= 1 ? split_part_floats(ctx->c.P.V_dim, nranks) : -1;
 }
 
-int dfx_split_pxv_floats(dfx_ctx* ctx) { return ctx ? split_pxv_floats(ctx->c.P.V_dim) : -1; }
+int dfx_split_pxv_floats(dfx_ctx* ctx) {
+  return ctx ? split_pxv_floats(ctx->c.P.V_dim, ctx->c.xvp_row) : -1;
+}
 
 int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* b, uint64_t max_index,
                         int nranks, uint64_t* keys_out, float* x_out, uint32_t* row_cnt_out) {
@@ -442,17 +520,38 @@ int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* p
   DFX_CHECK_ARG(part_rows >= B, "split_combine: part_rows < the batch's rows");
   const int d = c->P.V_dim;
   Workspace& ws = c->ws;
-  DFX_TRY(ws.dscratch.ensure((size_t)(B / kSpNT + 64) * 8));
+  // V_dim % 4 == 0: G lanes per row, coalesced float4 rows (else one thread per row)
+  int G = 0;
+  if (d > 0 && d % 4 == 0 && d <= 256) {
+    G = 1;
+    while (4 * G < d) G <<= 1;
+  }
+  const int64_t rpb = G ? kSpNT / G : kSpNT;
+  const int64_t nb = (B + rpb - 1) / rpb;
+  const int PX = split_pxv_floats(d, c->xvp_row);
+  // one loss partial per block, after the 8 doubles the scratch keeps in front
+  DFX_TRY(ws.dscratch.ensure((size_t)(nb + 16) * 8));
   double* loss_part = ws.dscratch.as<double>() + 8;
-  const int64_t nb = (B + kSpNT - 1) / kSpNT;
   // the AUC lane's snapshot buffers are free once its previous AUC is done
   const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
   DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
   DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   if (B > 0) {
-    hipLaunchKernelGGL(k_split_combine, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, B,
-                       part_rows, nranks, d, parts, b->label, b->weight, pred_out, pxv_out, loss_part,
-                       c->aws.ak0.as<uint32_t>(), c->aws.av0.as<uint32_t>());
+    uint32_t* ak = c->aws.ak0.as<uint32_t>();
+    uint32_t* al = c->aws.av0.as<uint32_t>();
+#define DFX_COMBINE(GG)                                                                        \
+    if (G == GG)                                                                               \
+      hipLaunchKernelGGL(k_split_combine_vec<GG>, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, \
+                         B, part_rows, nranks, d, PX, parts, b->label, b->weight, pred_out,   \
+                         pxv_out,                                                            \
+                         loss_part, ak, al);
+    DFX_COMBINE(1) DFX_COMBINE(2) DFX_COMBINE(4) DFX_COMBINE(8) DFX_COMBINE(16) DFX_COMBINE(32)
+    DFX_COMBINE(64)
+#undef DFX_COMBINE
+    if (G == 0)
+      hipLaunchKernelGGL(k_split_combine, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, B,
+                         part_rows, nranks, d, PX, parts, b->label, b->weight, pred_out, pxv_out,
+                         loss_part, ak, al);
   }
   sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
@@ -480,7 +579,7 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.segstart = ows.segstart.as<uint32_t>(); g.ds = ods; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = ows.occ_row.as<uint32_t>();
     g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
-    g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d); g.d = d;
+    g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d, c->xvp_row); g.d = d;
     g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd;
     g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
