@@ -64,6 +64,10 @@ def parse():
                          "records / gradients all-to-all-v (pipelined unless --sync).  The "
                          "other schedules, and the north_star's literal union all-gather / "
                          "reduce-scatter (rsag), are measured beside it on short runs")
+    ap.add_argument("--slices", type=int, default=0,
+                    help="split C++ driver: rows of a step in this many slices, each slice's "
+                         "exchanges beside the next slice's compute (0: the driver's default, "
+                         "one slice)")
     ap.add_argument("--force-collectives", action="store_true",
                     help="sharded store: run every exchange as an RCCL collective even at N=1 "
                          "(tests the multi-GPU code paths on one GPU)")
@@ -596,12 +600,14 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
     cpp = split and args.driver == "cpp" and args.backend == "nccl"
     store = None
     if cpp:
-        ids = torch.zeros(3 * 128, dtype=torch.uint8)
+        ids = torch.zeros(DI.SplitStore.rccl_ids_size(), dtype=torch.uint8)
         if rank == 0:
             ids = torch.frombuffer(bytearray(DI.SplitStore.rccl_ids()), dtype=torch.uint8)
         dist.broadcast(ids, src=0, group=comm.cgroup)
         store = DI.SplitStore([shard], pipelined=not args.sync,
                               rccl=(rank, world, ids.numpy().tobytes(), args.force_collectives))
+        if args.slices:
+            store.set_slices(args.slices)
         pipe = None
     elif args.sync:
         pipe = None
@@ -741,17 +747,28 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
             py_pipe[0] = DI.SplitPipeline(shards, comm_)
         py_pipe[0].submit(dblks, job)
 
+    def cpp_other_slices(shards, dblks, comm_, job):
+        store.submit(dblks, job)
+
     sched = [("split_sync", DI.split_step), ("a2a_sync", DI.sharded_step),
              ("rsag_sync", DI.rsag_step)]
     if store is not None and not args.sync:  # the same schedule driven from Python
         sched.insert(0, ("split_pipelined_py", py_split_pipelined))
+        # the C++ driver with the other slicing (rows in 2 slices, each slice's exchanges
+        # beside the next slice's compute; or unsliced if the main run was sliced)
+        other_k = 1 if args.slices > 1 else 2
+        sched.insert(1, ("split_pipelined_cpp_slices%d" % other_k, cpp_other_slices))
     for cname, fn in sched:
         if cname == main_name or (cname != "a2a_sync" and args.push_agg != "sum"):
             continue
+        if fn is cpp_other_slices:
+            store.set_slices(other_k)
         for bt in batches[:2]:
             fn([shard], [bt], comm, H.kTraining)
         if py_pipe[0] is not None:
             py_pipe[0].flush()
+        if fn is cpp_other_slices:
+            store.flush()
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
@@ -760,6 +777,9 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         if py_pipe[0] is not None:
             py_pipe[0].flush()
             py_pipe[0] = None
+        if fn is cpp_other_slices:
+            store.flush()
+            store.set_slices(args.slices)
         torch.cuda.synchronize()
         dist.barrier()
         dt = time.perf_counter() - t1

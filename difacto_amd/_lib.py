@@ -117,6 +117,10 @@ _SIGS = {
     "dfx_ctx_lane_stream": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp)]),
     "dfx_ctx_set_lane_stream": (ctypes.c_int, [vp, ctypes.c_int, vp]),
     "dfx_split_owner_forward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "dfx_split_owner_forward_rows": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, c_i64,
+                                                    c_i64, c_i64]),
+    "dfx_split_combine_rows": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp, c_i64,
+                                              ctypes.c_int, vp, vp, c_i64, c_i64]),
     "dfx_split_combine": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(Batch), vp, c_i64,
                                          ctypes.c_int, vp, vp]),
     "dfx_split_owner_backward": (ctypes.c_int, [vp, ctypes.c_int, vp]),
@@ -164,6 +168,8 @@ _DIST_SIGS = {
     "dfx_dist_last_error": (ctypes.c_char_p, []),
     "dfx_dist_rccl_id_bytes": (ctypes.c_int, []),
     "dfx_dist_rccl_ids": (ctypes.c_int, [ctypes.c_int, vp]),
+    "dfx_dist_rccl_comms": (ctypes.c_int, []),
+    "dfx_split_store_set_slices": (ctypes.c_int, [vp, ctypes.c_int]),
     "dfx_split_store_create_rccl": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp,
                                                    ctypes.c_int, ctypes.c_int, c_u64,
                                                    ctypes.POINTER(vp)]),

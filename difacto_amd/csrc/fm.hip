@@ -77,11 +77,12 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   constexpr int UNR = PROBE ? (CPL <= 4 ? 8 : 2) : (CPL <= 4 ? 8 : (CPL <= 8 ? 4 : 2));
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
-  const int64_t r = (int64_t)blockIdx.x * RPB + g;
+  const int64_t i = (int64_t)blockIdx.x * RPB + g;
+  const int64_t r = fwd_row(a, i);
   const int d = a.d;
   __shared__ double red[kFmNT / kWave];
   double loss = 0;
-  if (r < a.B) {
+  if (i < a.B) {
     const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = (MODE == kPredict) ? a.pred[r] : 0.f;
     float xv[CPL], xxvv[CPL];
@@ -318,11 +319,12 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int gbase = (threadIdx.x % kWave) - l;
-  const int64_t r = (int64_t)blockIdx.x * RPB + g;
+  const int64_t ri = (int64_t)blockIdx.x * RPB + g;
+  const int64_t r = fwd_row(a, ri);
   const int d = a.d;
   __shared__ double red[kFmNT / kWave];
   double loss = 0;
-  if (r < a.B) {
+  if (ri < a.B) {
     const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = 0.f;
     float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};

@@ -62,7 +62,15 @@ struct FwdArgs {
   int fat_nb;      // fat forward: nnz per trip at V_dim 16 (kwarg fat_nb = 4 | 6 | 8 | 12)
   int fwd_lanes;   // V_dim 16 fat slots: k_fm_fwd_fat_pf with this many lanes per row (0: off)
   float* part;
+  // the split's sliced owner forward (slice_len > 0): B = workers * slice_len logical rows,
+  // logical row i being the owner's row (i / slice_len) * slice_m + slice_lo + i % slice_len
+  int64_t slice_m, slice_lo, slice_len;
 };
+
+__device__ inline int64_t fwd_row(const FwdArgs& a, int64_t i) {
+  if (a.slice_len <= 0) return i;
+  return (i / a.slice_len) * a.slice_m + a.slice_lo + i % a.slice_len;
+}
 
 // the owner-computes split's per-row forward partial and its per-row [XV*p | p] record
 // the owner's partial per row: one owner (N = 1) [XV(d) | XXVV(d) | sum w x | 0 0 0], so the

@@ -152,14 +152,15 @@ __global__ void k_split_offsets(const uint32_t* excl, const uint32_t* total, int
 // worker: the owners' partials of each row summed in rank order, then FMLoss::Predict's tail
 // (fm_loss.h:110-119), Evaluate, the AUC snapshot and CalcGrad's per-row factors
 // (fm_loss.h:155-199): pxv row [XV*p (d) | p | 0 0 0]
-__global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, int n, int d,
+__global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t row0, int64_t B, int64_t M,
+                                                         int n, int d,
                                                          int PX, const float* __restrict__ parts,
                                                          const float* label, const float* rw,
                                                          float* pred_out, float* pxv,
                                                          double* loss_part, uint32_t* auc_key,
                                                          uint32_t* auc_lab) {
   __shared__ double red[kSpNT / kWave];
-  const int64_t r = (int64_t)blockIdx.x * kSpNT + threadIdx.x;
+  const int64_t r = row0 + (int64_t)blockIdx.x * kSpNT + threadIdx.x;
   const int PS = split_part_floats(d, n);
   const bool compact = n > 1;  // [XV | sum w x | sum_l XXVV_l | 0 0] per owner
   double loss = 0;
@@ -228,8 +229,8 @@ __global__ __launch_bounds__(kSpNT) void k_split_combine(int64_t B, int64_t M, i
 // sum over l of the reference (fm_loss.h:110-113) is taken by every lane through shuffles in l
 // order, so results are bit-identical to k_split_combine's, with coalesced row reads
 template <int G>
-__global__ __launch_bounds__(kSpNT) void k_split_combine_vec(int64_t B, int64_t M, int n, int d,
-                                                             int PX,
+__global__ __launch_bounds__(kSpNT) void k_split_combine_vec(int64_t row0, int64_t B,
+                                                             int64_t M, int n, int d, int PX,
                                                              const float* __restrict__ parts,
                                                              const float* label, const float* rw,
                                                              float* pred_out, float* pxv,
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(kSpNT) void k_split_combine_vec(int64_t B, int64_t 
   constexpr int RPB = kSpNT / G;
   const int l = threadIdx.x % G;
   const int gbase = (threadIdx.x % kWave) - l;
-  const int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / G;
+  const int64_t r = row0 + (int64_t)blockIdx.x * RPB + threadIdx.x / G;
   const int PS = split_part_floats(d, n);
   const bool compact = n > 1;
   const bool mine = 4 * l < d;
@@ -480,27 +481,42 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   return DFX_OK;
 }
 
-int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
+// rows [lo, lo + len) of every source worker's M-row block (len = 0: every row, M unused)
+int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nranks, int64_t M,
+                                 int64_t lo, int64_t len) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_SPLIT_SLOT(slot);
   Context* c = &ctx->c;
   DFX_CHECK_ARG(!c->split_initv_pending[slot],
                 "split_owner_forward: the count push's InitV is pending (dfx_split_initv_*)");
   const int64_t R = c->split_rows[slot];
+  const bool sliced = len > 0;
+  DFX_CHECK_ARG(!sliced || (nranks >= 1 && M >= 1 && lo >= 0 && lo + len <= M &&
+                            R == (int64_t)nranks * M),
+                "split_owner_forward_rows: rows [lo, lo + len) of nranks blocks of M rows");
   if (c->split_lane[slot]) DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_loc[slot], 0));
-  if (R == 0) return DFX_OK;
-  DFX_CHECK_ARG(part_out, "split_owner_forward: null buffer");
-  Workspace& ows = c->ows[slot];
-  FwdArgs a{};
-  a.B = R; a.offs = ows.rowid.as<uint64_t>(); a.val = c->split_x[slot];
-  a.index = c->split_keys[slot]; a.max_index = ~0ull; a.keys_ready = 1;
-  a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
-  a.no_fat_fwd = !c->fat_fwd;
-  a.fat_nb = c->fat_nb;
-  a.part = part_out;
-  a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
-  int nblk = 0;
-  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+  const bool last = !sliced || lo + len == M;
+  if (R > 0) {
+    DFX_CHECK_ARG(part_out, "split_owner_forward: null buffer");
+    Workspace& ows = c->ows[slot];
+    FwdArgs a{};
+    a.B = sliced ? (int64_t)nranks * len : R;
+    a.offs = ows.rowid.as<uint64_t>(); a.val = c->split_x[slot];
+    a.index = c->split_keys[slot]; a.max_index = ~0ull; a.keys_ready = 1;
+    a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
+    a.no_fat_fwd = !c->fat_fwd;
+    a.fat_nb = c->fat_nb;
+    a.part = part_out;
+    a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
+    if (sliced) {
+      a.slice_m = M;
+      a.slice_lo = lo;
+      a.slice_len = len;
+    }
+    int nblk = 0;
+    DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+  }
+  if (!last) return DFX_OK;
   // a step without a backward is done with the slot (and the table) here
   DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
   if (c->split_job[slot] != DFX_JOB_TRAINING) DFX_TRY(cap_record(c));
@@ -508,11 +524,20 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
   return DFX_OK;
 }
 
-int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* parts,
-                      int64_t part_rows, int nranks, float* pxv_out, float* pred_out) {
+int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out) {
+  return dfx_split_owner_forward_rows(ctx, slot, part_out, 1, 0, 0, 0);
+}
+
+// rows [lo, lo + len) of this worker's batch (lo a multiple of 256); the call whose rows end
+// at part_rows (or beyond) finishes the step: the loss of every row, the AUC lane, progress
+int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* parts,
+                           int64_t part_rows, int nranks, float* pxv_out, float* pred_out,
+                           int64_t lo, int64_t len) {
   DFX_CHECK_ARG(ctx && b, "null argument");
   DFX_SPLIT_SLOT(slot);
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
+  DFX_CHECK_ARG(lo >= 0 && len >= 1 && lo % 256 == 0,
+                "split_combine_rows: rows [lo, lo + len), lo a multiple of 256");
   Context* c = &ctx->c;
   const int64_t B = b->size;
   DFX_CHECK_ARG(B == c->split_B[slot], "split_combine: batch differs from split_partition's");
@@ -529,29 +554,39 @@ int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* p
   const int64_t rpb = G ? kSpNT / G : kSpNT;
   const int64_t nb = (B + rpb - 1) / rpb;
   const int PX = split_pxv_floats(d, c->xvp_row);
-  // one loss partial per block, after the 8 doubles the scratch keeps in front
-  DFX_TRY(ws.dscratch.ensure((size_t)(nb + 16) * 8));
+  const bool first = lo == 0, last = lo + len >= part_rows;
+  // one loss partial per block (the blocks of every call tile the batch), after the 8 doubles
+  // the scratch keeps in front
+  if (first) DFX_TRY(ws.dscratch.ensure((size_t)(nb + 16) * 8));
   double* loss_part = ws.dscratch.as<double>() + 8;
   // the AUC lane's snapshot buffers are free once its previous AUC is done
   const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
-  DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
-  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
-  if (B > 0) {
+  if (first) {
+    DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
+    DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+  }
+  const int64_t r1 = lo + len < B ? lo + len : B;
+  if (r1 > lo) {
     uint32_t* ak = c->aws.ak0.as<uint32_t>();
     uint32_t* al = c->aws.av0.as<uint32_t>();
+    const dim3 grid((unsigned)((r1 - lo + rpb - 1) / rpb));
+    double* lp = loss_part + lo / rpb;
 #define DFX_COMBINE(GG)                                                                        \
     if (G == GG)                                                                               \
-      hipLaunchKernelGGL(k_split_combine_vec<GG>, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, \
-                         B, part_rows, nranks, d, PX, parts, b->label, b->weight, pred_out,   \
-                         pxv_out,                                                            \
-                         loss_part, ak, al);
+      hipLaunchKernelGGL(k_split_combine_vec<GG>, grid, dim3(kSpNT), 0, c->stream, lo, r1,     \
+                         part_rows, nranks, d, PX, parts, b->label, b->weight, pred_out,       \
+                         pxv_out, lp, ak, al);
     DFX_COMBINE(1) DFX_COMBINE(2) DFX_COMBINE(4) DFX_COMBINE(8) DFX_COMBINE(16) DFX_COMBINE(32)
     DFX_COMBINE(64)
 #undef DFX_COMBINE
     if (G == 0)
-      hipLaunchKernelGGL(k_split_combine, dim3((unsigned)nb), dim3(kSpNT), 0, c->stream, B,
-                         part_rows, nranks, d, PX, parts, b->label, b->weight, pred_out, pxv_out,
-                         loss_part, ak, al);
+      hipLaunchKernelGGL(k_split_combine, grid, dim3(kSpNT), 0, c->stream, lo, r1, part_rows,
+                         nranks, d, PX, parts, b->label, b->weight, pred_out, pxv_out, lp, ak,
+                         al);
+  }
+  if (!last) {
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
   }
   sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
@@ -561,6 +596,12 @@ int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* p
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
+}
+
+int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* parts,
+                      int64_t part_rows, int nranks, float* pxv_out, float* pred_out) {
+  return dfx_split_combine_rows(ctx, slot, b, parts, part_rows, nranks, pxv_out, pred_out, 0,
+                                part_rows > 0 ? part_rows : 1);
 }
 
 int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {

@@ -1063,10 +1063,21 @@ class SplitStore:
     def rccl_ids():
         """fresh communicator ids (rank 0), as bytes for the caller's rendezvous"""
         D = _lib.dist_lib()
-        n = 3 * D.dfx_dist_rccl_id_bytes()
-        buf = ctypes.create_string_buffer(n)
-        _lib.dist_check(D.dfx_dist_rccl_ids(3, buf))
+        k = D.dfx_dist_rccl_comms()
+        buf = ctypes.create_string_buffer(k * D.dfx_dist_rccl_id_bytes())
+        _lib.dist_check(D.dfx_dist_rccl_ids(k, buf))
         return buf.raw
+
+    @staticmethod
+    def rccl_ids_size():
+        """bytes of rccl_ids() (every rank allocates its receive buffer with it)"""
+        D = _lib.dist_lib()
+        return D.dfx_dist_rccl_comms() * D.dfx_dist_rccl_id_bytes()
+
+    def set_slices(self, k):
+        """rows of a step in k slices (the exchanges of one slice beside the next slice's
+        compute; 0: the driver's default, one slice)"""
+        _lib.dist_check(_lib.dist_lib().dfx_split_store_set_slices(self.h, int(k)))
 
     def submit(self, dblks, job_type=kTraining, push_cnt=False, preds=None):
         D = _lib.dist_lib()

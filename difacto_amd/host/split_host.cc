@@ -148,6 +148,25 @@ class SplitLoopback : public SplitTransport {
     Release(streams);
   }
 
+  void Exchange(int, const std::vector<std::vector<const void*>>& send,
+                const std::vector<std::vector<int64_t>>& send_bytes,
+                const std::vector<std::vector<void*>>& recv,
+                const std::vector<std::vector<int64_t>>& recv_bytes,
+                const std::vector<void*>& streams) override {
+    const int n = nranks();
+    Join(streams);
+    for (int g = 0; g < n; ++g)
+      for (int l = 0; l < n; ++l) {
+        const int64_t bytes = send_bytes[l][g];
+        if (bytes != recv_bytes[g][l]) throw Error(DFX_ERR_ARG, "loopback: size mismatch");
+        if (bytes <= 0) continue;
+        HipCheck(hipMemcpyAsync(recv[g][l], send[l][g], (size_t)bytes, hipMemcpyDeviceToDevice,
+                                S(streams[g])),
+                 "loopback exchange");
+      }
+    Release(streams);
+  }
+
  private:
   void Join(const std::vector<void*>& st) {
     const int n = nranks();
@@ -260,6 +279,31 @@ class SplitRccl : public SplitTransport {
               "ncclAllGather");
   }
 
+  void Exchange(int channel, const std::vector<std::vector<const void*>>& send,
+                const std::vector<std::vector<int64_t>>& send_bytes,
+                const std::vector<std::vector<void*>>& recv,
+                const std::vector<std::vector<int64_t>>& recv_bytes,
+                const std::vector<void*>& streams) override {
+    hipStream_t st = S(streams[0]);
+    // this rank's own rows: a device copy
+    if (send_bytes[0][rank_] > 0)
+      HipCheck(hipMemcpyAsync(recv[0][rank_], send[0][rank_], (size_t)send_bytes[0][rank_],
+                              hipMemcpyDeviceToDevice, st),
+               "self copy");
+    if (n_ == 1) return;
+    NcclCheck(ncclGroupStart(), "group");
+    for (int p = 0; p < n_; ++p) {
+      if (p == rank_) continue;
+      if (send_bytes[0][p] > 0)
+        NcclCheck(ncclSend(send[0][p], (size_t)send_bytes[0][p], ncclUint8, p, comm_[channel], st),
+                  "ncclSend");
+      if (recv_bytes[0][p] > 0)
+        NcclCheck(ncclRecv(recv[0][p], (size_t)recv_bytes[0][p], ncclUint8, p, comm_[channel], st),
+                  "ncclRecv");
+    }
+    NcclCheck(ncclGroupEnd(), "group");
+  }
+
  private:
   static constexpr int kMaxCounts = 64 * 4;
   dfx_ctx* ctx_;
@@ -302,6 +346,10 @@ struct GpuSplitStore::Impl {
   };
 
   static constexpr int kAhead = 2;  // steps the host may run ahead of the context streams
+  // rows per step in one slice unless asked (SetSlices): at N = 1 with every exchange forced
+  // through the transport, 2 slices cost 9 % (each slice's owner forward fills under one wave of
+  // blocks); what they hide at N > 1 is measured by bench.py's secondary schedule
+  static constexpr int kDefaultSlices = 1;
 
   SplitTransport* t;
   bool pipelined;
@@ -319,6 +367,11 @@ struct GpuSplitStore::Impl {
   double throttle_s = 0;
   uint32_t mark_mask = 0;
   std::vector<Marks> marks;
+  int slices = 0;  // 0: the default (2 with an exchange, 1 without)
+  // sliced steps: per local shard a partial-exchange stream and a row-gather stream, and per
+  // (slice, local) the hand-off events: forward done, partials in, combine done, rows in
+  std::vector<hipStream_t> xst, yst;
+  std::vector<std::vector<hipEvent_t>> evf, evx, evc, evy;
 
   Impl(SplitTransport* tr, bool pipe, uint64_t mi) : t(tr), pipelined(pipe), max_index(mi) {
     N = t->nranks();
@@ -348,6 +401,17 @@ struct GpuSplitStore::Impl {
     }
   }
   ~Impl() {
+    for (auto st : xst) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+    for (auto st : yst) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+    for (auto* ev : {&evf, &evx, &evc, &evy})
+      for (auto& v : *ev)
+        for (auto e : v) (void)hipEventDestroy(e);
     for (auto& v : inflight)
       for (auto e : v) (void)hipEventDestroy(e);
     for (auto& v : spare)
@@ -514,13 +578,115 @@ struct GpuSplitStore::Impl {
     return q;
   }
 
-  // the step's main-stream work: owner forward, partials to the workers, combine, rows to the
-  // owners, backward + update, InitV
-  void Run(const Step& q) {
+  int Slices() const { return t->solo() ? 1 : (slices > 0 ? slices : kDefaultSlices); }
+
+  // streams and events of the sliced step, made on first use
+  void SliceRes(int K) {
+    int least = 0, greatest = 0;
+    HipCheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "priority range");
+    while ((int)xst.size() < L) {
+      hipStream_t a, b;
+      HipCheck(hipStreamCreateWithPriority(&a, hipStreamNonBlocking, greatest), "stream");
+      HipCheck(hipStreamCreateWithPriority(&b, hipStreamNonBlocking, greatest), "stream");
+      xst.push_back(a);
+      yst.push_back(b);
+    }
+    for (auto* ev : {&evf, &evx, &evc, &evy})
+      while ((int)ev->size() < K) {
+        std::vector<hipEvent_t> v(L);
+        for (auto& e : v) HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+        ev->push_back(v);
+      }
+  }
+
+  // the main-stream part of a step with an exchange, in K row slices: forward(h) -> partials
+  // of slice h on the exchange streams (beside forward(h + 1)) -> combine(h) -> rows of slice h
+  // on the gather streams (beside combine(h + 1)) -> the backward waits for every slice
+  void RunSliced(const Step& q, int K) {
     const int s = q.slot;
     const int64_t M = q.M;
-    if (mark_mask) marks.emplace_back();
-    Mark(0);
+    const bool train = q.job == DFX_JOB_TRAINING;
+    SliceRes(K);
+    // slice bounds: multiples of 256 rows (dfx_split_combine_rows)
+    const int64_t per = ((M + K - 1) / K + 255) / 256 * 256;
+    std::vector<int64_t> lo, len;
+    for (int64_t a = 0; a < M; a += per) {
+      lo.push_back(a);
+      len.push_back(std::min(per, M - a));
+    }
+    const int H = (int)lo.size();
+    std::vector<float*> parts(L), rparts(L), pxv(L), allp(L);
+    std::vector<void*> xs(L), ys(L);
+    for (int l = 0; l < L; ++l) {
+      Buf& u = buf[s][l];
+      parts[l] = static_cast<float*>(u.parts.ensure((size_t)N * M * PS * 4));
+      rparts[l] = static_cast<float*>(u.rparts.ensure((size_t)N * M * PS * 4));
+      pxv[l] = static_cast<float*>(u.pxv.ensure((size_t)M * PX * 4));
+      allp[l] = train ? static_cast<float*>(u.allp.ensure((size_t)N * M * PX * 4)) : nullptr;
+      xs[l] = xst[l];
+      ys[l] = yst[l];
+    }
+    std::vector<std::vector<const void*>> sp(L, std::vector<const void*>(N));
+    std::vector<std::vector<void*>> rp(L, std::vector<void*>(N));
+    std::vector<std::vector<int64_t>> nb(L, std::vector<int64_t>(N));
+    for (int h = 0; h < H; ++h) {
+      for (int l = 0; l < L; ++l) {
+        DfxOk(dfx_split_owner_forward_rows(t->ctx(l), s, parts[l], N, M, lo[h], len[h]),
+              "dfx_split_owner_forward_rows");
+        HipCheck(hipEventRecord(evf[h][l], Main(l)), "record");
+        HipCheck(hipStreamWaitEvent(xst[l], evf[h][l], 0), "wait");
+        // to worker g: its slice rows of this owner's partial; from owner o: o's block
+        for (int g = 0; g < N; ++g) {
+          sp[l][g] = parts[l] + ((size_t)g * M + lo[h]) * PS;
+          rp[l][g] = rparts[l] + ((size_t)g * M + lo[h]) * PS;
+          nb[l][g] = len[h] * PS * 4;
+        }
+      }
+      t->Exchange(3, sp, nb, rp, nb, xs);
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(evx[h][l], xst[l]), "record");
+    }
+    Mark(1);
+    Mark(2);
+    for (int h = 0; h < H; ++h) {
+      for (int l = 0; l < L; ++l) {
+        HipCheck(hipStreamWaitEvent(Main(l), evx[h][l], 0), "wait");
+        DfxOk(dfx_split_combine_rows(t->ctx(l), s, &q.batches[l], rparts[l], M, N, pxv[l],
+                                     q.preds.empty() ? nullptr : q.preds[l], lo[h], len[h]),
+              "dfx_split_combine_rows");
+        if (!train) continue;
+        HipCheck(hipEventRecord(evc[h][l], Main(l)), "record");
+        HipCheck(hipStreamWaitEvent(yst[l], evc[h][l], 0), "wait");
+        // this worker's slice rows to every owner; from worker g into g's block
+        for (int g = 0; g < N; ++g) {
+          sp[l][g] = pxv[l] + (size_t)lo[h] * PX;
+          rp[l][g] = allp[l] + ((size_t)g * M + lo[h]) * PX;
+          nb[l][g] = len[h] * PX * 4;
+        }
+      }
+      if (!train) continue;
+      t->Exchange(4, sp, nb, rp, nb, ys);
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(evy[h][l], yst[l]), "record");
+    }
+    Mark(3);
+    if (train) {
+      for (int h = 0; h < H; ++h)
+        for (int l = 0; l < L; ++l) HipCheck(hipStreamWaitEvent(Main(l), evy[h][l], 0), "wait");
+      Mark(4);
+      for (int l = 0; l < L; ++l)
+        DfxOk(dfx_split_owner_backward(t->ctx(l), s, allp[l]), "dfx_split_owner_backward");
+      Mark(5);
+      InitV(s);
+    } else {
+      Mark(4);
+      Mark(5);
+    }
+  }
+
+  // the unsliced step (no exchange, or K = 1): owner forward, partials to the workers, combine,
+  // rows to the owners, backward + update, InitV — every exchange on the context streams
+  void RunWhole(const Step& q) {
+    const int s = q.slot;
+    const int64_t M = q.M;
     std::vector<const void*> ps(L), xs(L);
     std::vector<void*> pr(L), xr(L), st(L);
     for (int l = 0; l < L; ++l) {
@@ -556,6 +722,19 @@ struct GpuSplitStore::Impl {
     } else {
       Mark(4);
       Mark(5);
+    }
+  }
+
+  // the step's main-stream work (sliced with an exchange), then the run-ahead bound
+  void Run(const Step& q) {
+    const int s = q.slot;
+    if (mark_mask) marks.emplace_back();
+    Mark(0);
+    const int K = Slices();
+    if (K > 1) {
+      RunSliced(q, K);
+    } else {
+      RunWhole(q);
     }
     Mark(6);
     for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
@@ -626,6 +805,11 @@ void GpuSplitStore::Submit(const std::vector<dfx_batch>& batches, int job_type, 
 }
 
 void GpuSplitStore::Flush() { impl_->Flush(); }
+
+void GpuSplitStore::SetSlices(int K) {
+  if (K < 0 || K > 64) throw Error(DFX_ERR_ARG, "split store: 0 <= slices <= 64");
+  impl_->slices = K;  // 0: the default
+}
 
 double GpuSplitStore::TakeThrottleSeconds() {
   const double v = impl_->throttle_s;
@@ -743,6 +927,15 @@ int dfx_split_store_flush(dfx_split_store* s) {
     s->s->Flush();
   });
 }
+
+int dfx_split_store_set_slices(dfx_split_store* s, int slices) {
+  return Guard([&] {
+    if (!s) throw difacto::Error(DFX_ERR_ARG, "null argument");
+    s->s->SetSlices(slices);
+  });
+}
+
+int dfx_dist_rccl_comms(void) { return difacto::kSplitComms; }
 
 int dfx_split_store_throttle_seconds(dfx_split_store* s, double* out) {
   return Guard([&] {

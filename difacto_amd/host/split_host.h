@@ -12,6 +12,11 @@
 //   main    worker combine: pred, p, loss, AUC     (dfx_split_combine)
 //   main    [XV*p | p] rows -> every owner         (AllGather channel 1)
 //   main    owner backward + FTRL / AdaGrad, InitV (owner_backward, initv_local/gather/draw)
+// With an exchange the rows may go in K slices (SetSlices): the owner forwards of every
+// slice queue on the main stream, slice h's partials travel on an exchange stream as soon as
+// its forward is done (channel 3) while slice h+1 computes, slice h's combine waits only for
+// them, and its [XV*p | p] rows travel on a gather stream (channel 4) beside the next
+// combine; the backward waits for every slice's rows.
 // Pipelined, step t+1's partition, key exchange and owner Localizer run on the side streams
 // beside step t's main-stream work (every forward still reads the model after the previous
 // update: results equal the synchronous schedule bit for bit).
@@ -58,13 +63,23 @@ class SplitTransport {
   virtual void AllGather(int channel, const std::vector<const void*>& send,
                          const std::vector<void*>& recv, size_t bytes,
                          const std::vector<void*>& streams) = 0;
+  /** point-to-point form, ordered like AllToAllV: local l sends send_bytes[l][g] bytes from
+   * send[l][g] to global shard g and receives recv_bytes[l][g] bytes from g into recv[l][g]
+   * (the sliced exchanges: one slice's rows sit apart in every shard's buffer).  channel 3 is
+   * issued from the partial-exchange streams, channel 4 from the row-gather streams */
+  virtual void Exchange(int channel, const std::vector<std::vector<const void*>>& send,
+                        const std::vector<std::vector<int64_t>>& send_bytes,
+                        const std::vector<std::vector<void*>>& recv,
+                        const std::vector<std::vector<int64_t>>& recv_bytes,
+                        const std::vector<void*>& streams) = 0;
 };
 
 /** N shards on this process's GPU, exchanging by device copies */
 std::unique_ptr<SplitTransport> MakeSplitLoopback(const std::vector<dfx_ctx*>& ctxs);
 
-/** communicators the RCCL transport needs (keys, rows, split counts) */
-constexpr int kSplitComms = 3;
+/** communicators the RCCL transport needs (keys, rows, split counts, sliced partials, sliced
+ * row gathers): one per issuing stream */
+constexpr int kSplitComms = 5;
 
 /** one shard per process over RCCL.  ids: kSplitComms ncclUniqueIds made by rank 0
  * (dfx_dist_rccl_ids) and handed to every rank by the caller's own rendezvous.
@@ -89,6 +104,10 @@ class GpuSplitStore {
               const std::vector<float*>& preds = {});
   /** run the queued step */
   void Flush();
+  /** rows of a step in K slices (K >= 1; 0: the default, 1): slice h's
+   * partial exchange runs beside slice h+1's owner forward, and its row gather beside the
+   * next slice's combine, on streams of their own.  Same results for every K */
+  void SetSlices(int K);
   /** host seconds spent waiting on the run-ahead bound (pipelined) since the last call */
   double TakeThrottleSeconds();
   /** timing events on local shard 0's context stream at the main-stream phase boundaries

@@ -360,6 +360,19 @@ int dfx_split_owner_forward(dfx_ctx* ctx, int slot, float* part_out);
 int dfx_split_combine(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* parts,
                       int64_t part_rows, int nranks, float* pxv_out, float* pred_out);
 int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv);
+/* sliced forms, so a driver can exchange one slice's rows while the next slice computes:
+ * dfx_split_owner_forward_rows  rows [lo, lo + len) of each of the nranks source workers'
+ *                               M-row blocks (the received rows must be nranks * M), written
+ *                               at their place in part_out; the call ending at M finishes the
+ *                               owner's forward (len = 0: all rows, as dfx_split_owner_forward)
+ * dfx_split_combine_rows        this worker's rows [lo, lo + len), lo a multiple of 256; the
+ *                               call whose rows reach part_rows finishes the step's combine
+ *                               (loss, AUC, progress) — as dfx_split_combine over all rows */
+int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nranks, int64_t M,
+                                 int64_t lo, int64_t len);
+int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* batch, const float* parts,
+                           int64_t part_rows, int nranks, float* pxv_out, float* pred_out,
+                           int64_t lo, int64_t len);
 /* the owner's last begin: received rows, keys and unique keys (synchronises the stream) */
 int dfx_split_owner_stats(dfx_ctx* ctx, int slot, int64_t* rows, int64_t* nnz,
                           int64_t* n_uniq);

@@ -31,8 +31,9 @@ extern "C" {
 typedef struct dfx_split_store dfx_split_store;
 
 const char* dfx_dist_last_error(void);
-/* bytes of one communicator id; the RCCL store needs 3 of them */
+/* bytes of one communicator id; the RCCL store needs dfx_dist_rccl_comms() of them */
 int dfx_dist_rccl_id_bytes(void);
+int dfx_dist_rccl_comms(void);
 /* n fresh communicator ids into out[n * dfx_dist_rccl_id_bytes()] (rank 0 only) */
 int dfx_dist_rccl_ids(int n, void* out);
 /* one shard per process: this context (its stream, lanes and store) is rank `rank` of
@@ -51,6 +52,10 @@ int dfx_split_store_create_loopback(dfx_ctx* const* ctxs, int n, int pipelined,
 int dfx_split_store_submit(dfx_split_store* s, const dfx_batch* batches, int job_type,
                            int push_cnt, float* const* preds);
 int dfx_split_store_flush(dfx_split_store* s);
+/* a step's rows in `slices` slices (>= 1; 0: the default, one slice):
+ * slice h's partials travel while slice h + 1's owner forward runs, and its [XV*p | p] rows
+ * while the next slice combines (streams of the driver's own); results do not change */
+int dfx_split_store_set_slices(dfx_split_store* s, int slices);
 /* host seconds spent waiting on the pipelined run-ahead bound since the last call */
 int dfx_split_store_throttle_seconds(dfx_split_store* s, double* out);
 /* timing events at the main-stream phase boundaries of the following steps (bit i of mask:

@@ -310,3 +310,51 @@ def test_split_store_marks(pipelined):
     store.close()
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("name", ["fm_v16", "fm_v5_odd"])
+def test_split_store_slices_equal(name):
+    """the C++ driver's sliced step (SetSlices: slice h's partial exchange beside slice h+1's
+    owner forward, its row gather beside the next combine, on streams of their own) gives the
+    unsliced step's results bit for bit, for slice counts that do and do not divide the padded
+    rows, over count-push / training / validation steps and ragged, uneven workers"""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    N = 3
+    kw = CFGS[name]
+    jobs = [(H.kTraining, True), (H.kTraining, False), (H.kValidation, False),
+            (H.kTraining, False), (H.kTraining, False)]
+    outs = []
+    for K in (1, 2, 5):
+        ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(N)]
+        shards = [DI.Shard(c, N) for c in ctxs]
+        store = DI.SplitStore(shards, pipelined=True)
+        store.set_slices(K)
+        preds_all = []
+        for s, (job, cnt) in enumerate(jobs):
+            rows = [1300, 700 if s != 3 else 0, 1299]
+            step = [D.synthetic(rows[r], 12, 20000, binary=(r % 2 == 0), seed=900 + 31 * s + r,
+                                ragged=(s == 1)) for r in range(N)]
+            dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+            preds = [torch.zeros(1300, dtype=torch.float32, device=ctxs[r].device)
+                     for r in range(N)]
+            store.submit(dbs, job, push_cnt=cnt, preds=preds)
+            preds_all.append(preds)
+        store.flush()
+        for c in ctxs:
+            c.sync()
+        outs.append({"preds": [[p.cpu().numpy() for p in ps] for ps in preds_all],
+                     "prog": [H.progress(c) for c in ctxs],
+                     "stats": [H.Store(c).stats() for c in ctxs]})
+        store.close()
+        for c in ctxs:
+            c.close()
+    a = outs[0]
+    for b in outs[1:]:
+        for s in range(len(jobs)):
+            for r in range(N):
+                assert np.array_equal(a["preds"][s][r], b["preds"][s][r]), (name, s, r)
+        assert a["stats"] == b["stats"]
+        for pa, pb in zip(a["prog"], b["prog"]):
+            assert pa["nrows"] == pb["nrows"] and pa["auc"] == pb["auc"]
+            assert pa["loss"] == pb["loss"]
