@@ -14,9 +14,11 @@ LIB = difacto_amd/libdifacto_amd.so
 HOSTBIN = build/host_tests
 TRAINBIN = build/dfx_train
 HOSTLIB = difacto_amd/host/gpu_adapters.cc difacto_amd/host/reader.cc
-HOSTSRC = $(HOSTLIB) difacto_amd/host/dist_store.cc tests/host/host_tests.cc
+HOSTSRC = $(HOSTLIB) difacto_amd/host/dist_store.cc difacto_amd/host/split_learner.cc \
+  tests/host/host_tests.cc
 HOSTHDR = difacto_amd/host/iface.h difacto_amd/host/gpu_adapters.h difacto_amd/host/reader.h \
-  difacto_amd/host/dist_host.h difacto_amd/host/dist_store.h include/difacto_amd.h
+  difacto_amd/host/dist_host.h difacto_amd/host/dist_store.h difacto_amd/host/split_learner.h \
+  include/difacto_amd.h include/difacto_amd_dist.h
 HOSTFLAGS = -std=c++14 -O2 -Wall -pthread
 
 READERBIN = build/reader_tests
@@ -50,9 +52,9 @@ $(READERBIN): difacto_amd/host/reader.cc tests/host/reader_tests.cc difacto_amd/
 
 # C++ host adapters (the reference's Loss/Updater/Store over the C-ABI) + their test driver;
 # plain g++ against the C-ABI (the sharded store's exchange, dist_host.o, links RCCL)
-$(HOSTBIN): $(HOSTSRC) $(HOSTHDR) build/obj/dist_host.o $(LIB)
+$(HOSTBIN): $(HOSTSRC) $(HOSTHDR) build/obj/dist_host.o $(LIB) $(DISTLIB)
 	@mkdir -p build
-	g++ $(HOSTFLAGS) -o $@ $(HOSTSRC) build/obj/dist_host.o -Ldifacto_amd -ldifacto_amd \
+	g++ $(HOSTFLAGS) -o $@ $(HOSTSRC) build/obj/dist_host.o -Ldifacto_amd -ldifacto_amd -ldfx_dist \
 	  -L/opt/rocm/lib -lrccl -lamdhip64 \
 	  -Wl,-rpath,'$$ORIGIN/../difacto_amd' -Wl,-rpath,/opt/rocm/lib
 

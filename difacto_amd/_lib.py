@@ -90,6 +90,9 @@ _SIGS = {
     "dfx_feeder_submit": (ctypes.c_int, [vp, c_i64, c_i64, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(Batch)]),
     "dfx_feeder_consumed": (ctypes.c_int, [vp]),
+    "dfx_feeder_create_slots": (ctypes.c_int, [vp, c_i64, c_i64, ctypes.c_int,
+                                               ctypes.POINTER(vp)]),
+    "dfx_feeder_consumed_back": (ctypes.c_int, [vp, ctypes.c_int]),
     "dfx_dist_record_floats": (ctypes.c_int, [vp]),
     "dfx_dist_localize": (ctypes.c_int, [vp, ctypes.POINTER(Batch), c_u64, ctypes.c_int,
                                          ctypes.c_int, vp, vp]),
@@ -170,6 +173,7 @@ _DIST_SIGS = {
     "dfx_dist_rccl_ids": (ctypes.c_int, [ctypes.c_int, vp]),
     "dfx_dist_rccl_comms": (ctypes.c_int, []),
     "dfx_split_store_set_slices": (ctypes.c_int, [vp, ctypes.c_int]),
+    "dfx_split_store_allreduce_sum": (ctypes.c_int, [vp, f64p, ctypes.c_int]),
     "dfx_split_store_create_rccl": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp,
                                                    ctypes.c_int, ctypes.c_int, c_u64,
                                                    ctypes.POINTER(vp)]),

@@ -1,10 +1,12 @@
 // Batch feeder: host RowBlocks -> device batches through pinned staging buffers and a loader
-// stream, double-buffered.  The reader fills a slot's pinned arrays (parsing straight into
+// stream, double-buffered (or more slots: dfx_feeder_create_slots).  The reader fills a slot's pinned arrays (parsing straight into
 // them), dfx_feeder_submit enqueues the host->device copies on the loader stream, which is the
 // context's input stream, so the Localizer lane of dfx_train_step waits only for the copy of
 // its own batch — batch t+1's upload runs while the GPU trains on batch t.  A slot is reused
 // only after the context stream passed the step that consumed it (dfx_feeder_consumed).
 // This is the host side of SGDLearner::IterateData's producer loop (sgd_learner.cc:289-314).
+#include <vector>
+
 #include "internal.h"
 
 struct dfx_feeder {
@@ -17,8 +19,9 @@ struct dfx_feeder {
     uint64_t *d_off = nullptr, *d_idx = nullptr;
     float *d_val = nullptr, *d_lab = nullptr, *d_wt = nullptr;
     hipEvent_t consumed = nullptr;
-  } slot[2];
-  int cur = 1;
+  };
+  std::vector<Slot> slot;
+  int cur = -1;
 };
 
 using namespace dfx;
@@ -42,10 +45,12 @@ extern "C" int dfx_feeder_destroy(dfx_feeder* f) {
   return DFX_OK;
 }
 
-extern "C" int dfx_feeder_create(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz,
-                                 dfx_feeder** out) {
-  DFX_CHECK_ARG(ctx && out && max_rows > 0 && max_nnz >= 0, "feeder_create: bad argument");
+extern "C" int dfx_feeder_create_slots(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz,
+                                       int nslots, dfx_feeder** out) {
+  DFX_CHECK_ARG(ctx && out && max_rows > 0 && max_nnz >= 0 && nslots >= 2 && nslots <= 8,
+                "feeder_create: bad argument");
   dfx_feeder* f = new dfx_feeder();
+  f->slot.resize((size_t)nslots);
   f->ctx = ctx;
   f->max_rows = max_rows;
   f->max_nnz = max_nnz > 0 ? max_nnz : 1;
@@ -80,11 +85,16 @@ extern "C" int dfx_feeder_create(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz
   return DFX_OK;
 }
 
+extern "C" int dfx_feeder_create(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz,
+                                 dfx_feeder** out) {
+  return dfx_feeder_create_slots(ctx, max_rows, max_nnz, 2, out);
+}
+
 extern "C" int dfx_feeder_slot(dfx_feeder* f, dfx_host_batch* hb) {
   DFX_CHECK_ARG(f && hb, "feeder_slot: null argument");
-  f->cur ^= 1;
+  f->cur = (f->cur + 1) % (int)f->slot.size();
   auto& s = f->slot[f->cur];
-  // the step that consumed this slot two batches ago must be past the device
+  // the step that consumed this slot a round of slots ago must be past the device
   DFX_HIP(hipEventSynchronize(s.consumed));
   hb->offset = s.h_off;
   hb->index = s.h_idx;
@@ -121,8 +131,11 @@ extern "C" int dfx_feeder_submit(dfx_feeder* f, int64_t B, int64_t nnz, int has_
   return DFX_OK;
 }
 
-extern "C" int dfx_feeder_consumed(dfx_feeder* f) {
-  DFX_CHECK_ARG(f, "feeder_consumed: null argument");
-  DFX_HIP(hipEventRecord(f->slot[f->cur].consumed, f->ctx->c.stream));
+extern "C" int dfx_feeder_consumed(dfx_feeder* f) { return dfx_feeder_consumed_back(f, 0); }
+
+extern "C" int dfx_feeder_consumed_back(dfx_feeder* f, int back) {
+  const int n = f ? (int)f->slot.size() : 0;
+  DFX_CHECK_ARG(f && back >= 0 && back < n && f->cur >= 0, "feeder_consumed: bad argument");
+  DFX_HIP(hipEventRecord(f->slot[(f->cur - back + n) % n].consumed, f->ctx->c.stream));
   return DFX_OK;
 }

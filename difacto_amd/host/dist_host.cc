@@ -141,43 +141,57 @@ class LoopbackExchange : public ShardExchange {
 };
 
 // ---- RCCL: one shard per process --------------------------------------------------------
+}  // namespace
+
+void ShareIdsThroughFile(int rank, void* ids, size_t bytes, const std::string& id_file) {
+  // the file carries the launch's nonce (TORCHELASTIC_RUN_ID, the same on every rank of a
+  // torchrun launch, or DFX_RUN_ID): a reader rejects a file left by an earlier launch
+  char nonce[64] = {0};
+  const char* rid = std::getenv("DFX_RUN_ID");
+  if (!rid) rid = std::getenv("TORCHELASTIC_RUN_ID");
+  if (rid) std::snprintf(nonce, sizeof(nonce), "%s", rid);
+  if (rank == 0) {
+    const std::string tmp = id_file + ".tmp" + std::to_string(getpid());
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f || std::fwrite(nonce, sizeof(nonce), 1, f) != 1 || std::fwrite(ids, bytes, 1, f) != 1)
+      Fail("cannot write " + tmp);
+    std::fclose(f);
+    if (std::rename(tmp.c_str(), id_file.c_str()) != 0) Fail("cannot publish " + id_file);
+    return;
+  }
+  // node-local rendezvous: wait for rank 0's ids of this launch (60 s)
+  bool ok = false;
+  for (int i = 0; i < 6000 && !ok; ++i) {
+    FILE* f = std::fopen(id_file.c_str(), "rb");
+    if (f) {
+      char got[64];
+      ok = std::fread(got, sizeof(got), 1, f) == 1 && std::memcmp(got, nonce, sizeof(nonce)) == 0 &&
+           std::fread(ids, bytes, 1, f) == 1;
+      std::fclose(f);
+    }
+    if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  if (!ok) Fail("no communicator id of this launch in " + id_file);
+}
+
+std::string CommIdFile() {
+  if (const char* f = std::getenv("DFX_COMM_ID_FILE")) return f;
+  const char* port = std::getenv("MASTER_PORT");
+  return std::string("/tmp/dfx_comm_") + (port ? port : "0");
+}
+
+namespace {
+
 class RcclExchange : public ShardExchange {
  public:
   RcclExchange(dfx_ctx* ctx, int rank, int nranks, const std::string& id_file)
       : ctx_(ctx), rank_(rank), n_(nranks) {
     ncclUniqueId id[2];
-    // the file carries the launch's nonce (TORCHELASTIC_RUN_ID, the same on every rank of a
-    // torchrun launch, or DFX_RUN_ID): a reader rejects a file left by an earlier launch
-    char nonce[64] = {0};
-    const char* rid = std::getenv("DFX_RUN_ID");
-    if (!rid) rid = std::getenv("TORCHELASTIC_RUN_ID");
-    if (rid) std::snprintf(nonce, sizeof(nonce), "%s", rid);
     if (rank == 0) {
       NcclCheck(ncclGetUniqueId(&id[0]), "ncclGetUniqueId");
       NcclCheck(ncclGetUniqueId(&id[1]), "ncclGetUniqueId");
-      const std::string tmp = id_file + ".tmp" + std::to_string(getpid());
-      FILE* f = std::fopen(tmp.c_str(), "wb");
-      if (!f || std::fwrite(nonce, sizeof(nonce), 1, f) != 1 ||
-          std::fwrite(id, sizeof(id), 1, f) != 1)
-        Fail("cannot write " + tmp);
-      std::fclose(f);
-      if (std::rename(tmp.c_str(), id_file.c_str()) != 0) Fail("cannot publish " + id_file);
-    } else {
-      // node-local rendezvous: wait for rank 0's ids of this launch (60 s)
-      bool ok = false;
-      for (int i = 0; i < 6000 && !ok; ++i) {
-        FILE* f = std::fopen(id_file.c_str(), "rb");
-        if (f) {
-          char got[64];
-          ok = std::fread(got, sizeof(got), 1, f) == 1 &&
-               std::memcmp(got, nonce, sizeof(nonce)) == 0 &&
-               std::fread(id, sizeof(id), 1, f) == 1;
-          std::fclose(f);
-        }
-        if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(10));
-      }
-      if (!ok) Fail("no communicator id of this launch in " + id_file);
     }
+    ShareIdsThroughFile(rank, id, sizeof(id), id_file);
     // the compute stream at high priority: HIP maps the streams of one priority onto that
     // priority's hardware queues, which run their packets in order, so this keeps the step's
     // kernels (and the library's high-priority side lanes) off the queues of the

@@ -65,6 +65,13 @@ std::unique_ptr<ShardExchange> MakeLoopbackExchange(const std::vector<dfx_ctx*>&
 std::unique_ptr<ShardExchange> MakeRcclExchange(dfx_ctx* ctx, int rank, int nranks,
                                                 const std::string& id_file);
 
+/** the node-local rendezvous of communicator ids: rank 0 publishes `bytes` of ids (with the
+ * launch's nonce, DFX_RUN_ID or TORCHELASTIC_RUN_ID) in id_file, the other ranks wait for
+ * them (60 s); rank 0 removes the file once every rank holds its communicators */
+void ShareIdsThroughFile(int rank, void* ids, size_t bytes, const std::string& id_file);
+/** DFX_COMM_ID_FILE, else /tmp/dfx_comm_<MASTER_PORT> */
+std::string CommIdFile();
+
 /** KVStoreDist over the exchange: every local shard is a worker and the server of its key
  * range.  Pipelined (1-step-stale, dist.py ShardedPipeline / StaleOracle) or synchronous
  * (dist.sharded_step / ShardedOracle, AggOracle).  The update aggregation follows the

@@ -588,13 +588,7 @@ std::shared_ptr<GpuDistStore> GpuDistStore::CreateRccl(const KWArgs& kwargs) {
   const int world = ws ? std::atoi(ws) : 1;
   const int rank = std::getenv("RANK") ? std::atoi(std::getenv("RANK")) : 0;
   const int local = std::getenv("LOCAL_RANK") ? std::atoi(std::getenv("LOCAL_RANK")) : 0;
-  std::string id_file;
-  if (const char* f = std::getenv("DFX_COMM_ID_FILE")) {
-    id_file = f;
-  } else {
-    const char* port = std::getenv("MASTER_PORT");
-    id_file = std::string("/tmp/dfx_comm_") + (port ? port : "0");
-  }
+  const std::string id_file = CommIdFile();
   std::unique_ptr<Core> c(new Core());
   c->lockstep = LockstepOf(kwargs);
   c->ctxs.assign(1, nullptr);

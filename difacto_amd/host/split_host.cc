@@ -148,6 +148,8 @@ class SplitLoopback : public SplitTransport {
     Release(streams);
   }
 
+  void AllReduceSum(std::vector<double>*) override {}
+
   void Exchange(int, const std::vector<std::vector<const void*>>& send,
                 const std::vector<std::vector<int64_t>>& send_bytes,
                 const std::vector<std::vector<void*>>& recv,
@@ -277,6 +279,21 @@ class SplitRccl : public SplitTransport {
                  const std::vector<void*>& streams) override {
     NcclCheck(ncclAllGather(send[0], recv[0], bytes, ncclUint8, comm_[channel], S(streams[0])),
               "ncclAllGather");
+  }
+
+  void AllReduceSum(std::vector<double>* v) override {
+    const size_t m = v->size();
+    if (m == 0 || n_ == 1) return;
+    if (m * 8 > (size_t)kMaxCounts * 8) throw Error(DFX_ERR_ARG, "rccl: too many values");
+    double* hs = reinterpret_cast<double*>(hcnt_);
+    double* ds = reinterpret_cast<double*>(dcnt_);
+    std::memcpy(hs, v->data(), m * 8);
+    HipCheck(hipMemcpyAsync(ds, hs, m * 8, hipMemcpyHostToDevice, cnt_stream_), "H2D");
+    NcclCheck(ncclAllReduce(ds, ds, m, ncclFloat64, ncclSum, comm_[2], cnt_stream_),
+              "ncclAllReduce");
+    HipCheck(hipMemcpyAsync(hs, ds, m * 8, hipMemcpyDeviceToHost, cnt_stream_), "D2H");
+    HipCheck(hipStreamSynchronize(cnt_stream_), "sync");
+    std::memcpy(v->data(), hs, m * 8);
   }
 
   void Exchange(int channel, const std::vector<std::vector<const void*>>& send,
@@ -806,6 +823,8 @@ void GpuSplitStore::Submit(const std::vector<dfx_batch>& batches, int job_type, 
 
 void GpuSplitStore::Flush() { impl_->Flush(); }
 
+void GpuSplitStore::AllReduceSum(std::vector<double>* v) { impl_->t->AllReduceSum(v); }
+
 void GpuSplitStore::SetSlices(int K) {
   if (K < 0 || K > 64) throw Error(DFX_ERR_ARG, "split store: 0 <= slices <= 64");
   impl_->slices = K;  // 0: the default
@@ -936,6 +955,15 @@ int dfx_split_store_set_slices(dfx_split_store* s, int slices) {
 }
 
 int dfx_dist_rccl_comms(void) { return difacto::kSplitComms; }
+
+int dfx_split_store_allreduce_sum(dfx_split_store* s, double* v, int n) {
+  return Guard([&] {
+    if (!s || (n > 0 && !v) || n < 0) throw difacto::Error(DFX_ERR_ARG, "bad argument");
+    std::vector<double> x(v, v + n);
+    s->s->AllReduceSum(&x);
+    std::copy(x.begin(), x.end(), v);
+  });
+}
 
 int dfx_split_store_throttle_seconds(dfx_split_store* s, double* out) {
   return Guard([&] {

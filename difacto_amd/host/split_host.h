@@ -72,6 +72,9 @@ class SplitTransport {
                         const std::vector<std::vector<void*>>& recv,
                         const std::vector<std::vector<int64_t>>& recv_bytes,
                         const std::vector<void*>& streams) = 0;
+  /** host: v summed element-wise over the processes (loopback: one process, unchanged); issued
+   * on the split-count communicator, so call it from the thread that submits steps */
+  virtual void AllReduceSum(std::vector<double>* v) = 0;
 };
 
 /** N shards on this process's GPU, exchanging by device copies */
@@ -104,6 +107,8 @@ class GpuSplitStore {
               const std::vector<float*>& preds = {});
   /** run the queued step */
   void Flush();
+  /** host sum of v over the processes (after Flush: a collective of every rank) */
+  void AllReduceSum(std::vector<double>* v);
   /** rows of a step in K slices (K >= 1; 0: the default, 1): slice h's
    * partial exchange runs beside slice h+1's owner forward, and its row gather beside the
    * next slice's combine, on streams of their own.  Same results for every K */

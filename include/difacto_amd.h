@@ -141,6 +141,12 @@ int dfx_feeder_slot(dfx_feeder* f, dfx_host_batch* hb);
 int dfx_feeder_submit(dfx_feeder* f, int64_t B, int64_t nnz, int has_value, int has_weight,
                       dfx_batch* out);
 int dfx_feeder_consumed(dfx_feeder* f);
+/* nslots (2..8) staging slots; dfx_feeder_consumed_back(f, k) marks the slot of the batch
+ * submitted k submits ago — a pipelined consumer (the split driver runs step t when step t+1
+ * is submitted) marks batch t after the call that queued its last reader */
+int dfx_feeder_create_slots(dfx_ctx* ctx, int64_t max_rows, int64_t max_nnz, int nslots,
+                            dfx_feeder** out);
+int dfx_feeder_consumed_back(dfx_feeder* f, int back);
 
 /* ---- Localizer::Compact (localizer.h:41-51) -------------------------------------------
  * keys = ReverseBytes(index % max_index); uniq[U] ascending, cnt[U] occurrence counts

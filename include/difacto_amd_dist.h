@@ -56,6 +56,9 @@ int dfx_split_store_flush(dfx_split_store* s);
  * slice h's partials travel while slice h + 1's owner forward runs, and its [XV*p | p] rows
  * while the next slice combines (streams of the driver's own); results do not change */
 int dfx_split_store_set_slices(dfx_split_store* s, int slices);
+/* host: v[n] summed over the processes (a collective of every rank, on the split-count
+ * communicator; loopback: unchanged) */
+int dfx_split_store_allreduce_sum(dfx_split_store* s, double* v, int n);
 /* host seconds spent waiting on the pipelined run-ahead bound since the last call */
 int dfx_split_store_throttle_seconds(dfx_split_store* s, double* out);
 /* timing events at the main-stream phase boundaries of the following steps (bit i of mask:

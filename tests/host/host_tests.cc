@@ -27,6 +27,7 @@
 
 #include "../../difacto_amd/host/dist_store.h"
 #include "../../difacto_amd/host/gpu_adapters.h"
+#include "../../difacto_amd/host/split_learner.h"
 
 using namespace difacto;
 
@@ -442,7 +443,81 @@ static int RunDistAsync(int argc, char** argv) {
   return g_fail ? 1 : 0;
 }
 
+// host_tests split <data> shards=N|-1 epochs=E batch_size=B [model_out=P] [kwargs]: the
+// owner-computes split behind GpuSplitLearner (split_learner.h) — IterateData's executor fed
+// the raw minibatches of N loopback workers (one thread each) or one RCCL worker per process
+// (shards=-1): rows [r n / N, (r + 1) n / N) for worker r in batches of B, the workers stepping
+// together (an idle worker gives an empty batch).  Prints "epoch E loss L auc A nrows R" summed
+// over the workers; saves every server's model part.
+static int RunSplit(int argc, char** argv) {
+  RowBlockContainer<feaid_t> data;
+  if (argc < 3 || !ReadLibSVM(argv[2], &data)) return 2;
+  int shards = 1, epochs = 1;
+  size_t bs = 10;
+  std::string model_out, vdim = "0";
+  KWArgs kw;
+  for (int i = 3; i < argc; ++i) {
+    const std::string a = argv[i];
+    const size_t eq = a.find('=');
+    if (eq == std::string::npos) return 2;
+    const std::string k = a.substr(0, eq), v = a.substr(eq + 1);
+    if (k == "shards") shards = std::stoi(v);
+    else if (k == "epochs") epochs = std::stoi(v);
+    else if (k == "batch_size") bs = std::stoul(v);
+    else if (k == "model_out") model_out = v;
+    else {
+      if (k == "V_dim") vdim = v;
+      kw.push_back({k, v});
+    }
+  }
+  std::shared_ptr<GpuSplitLearner> sl =
+      shards > 0 ? GpuSplitLearner::CreateLoopback(shards, kw) : GpuSplitLearner::CreateRccl(kw);
+  const int L = sl->nlocal(), N = sl->nranks();
+  const size_t n = data.Size();
+  size_t nsteps = 0;
+  for (int r = 0; r < N; ++r) {
+    const size_t rows = (size_t)(r + 1) * n / N - (size_t)r * n / N;
+    nsteps = std::max(nsteps, (rows + bs - 1) / bs);
+  }
+  for (int ep = 0; ep < epochs; ++ep) {
+    std::vector<std::thread> th;
+    for (int l = 0; l < L; ++l) {
+      th.emplace_back([&, l]() {
+        const int r = sl->rank(l);
+        const size_t lo = (size_t)r * n / N, hi = (size_t)(r + 1) * n / N;
+        for (size_t t = 0; t < nsteps; ++t) {
+          const size_t b = std::min(hi, lo + t * bs), e = std::min(hi, lo + (t + 1) * bs);
+          RowSlice s = Slice(data, b, e);
+          sl->ProcessBatch(l, s.blk, GpuSplitLearner::kTraining, ep == 0 && vdim != "0");
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    std::vector<double> sum(3, 0.0);
+    for (int l = 0; l < L; ++l) {
+      const Progress p = sl->TakeProgress(l);
+      sum[0] += p.loss;
+      sum[1] += p.auc;
+      sum[2] += p.nrows;
+    }
+    sl->AllReduceSum(&sum);
+    EXPECT(sum[2] == (double)n, "epoch %d nrows %.0f want %zu", ep, sum[2], n);
+    if (sl->rank(0) == 0)
+      std::printf("epoch %d loss %.9e auc %.9e nrows %.0f\n", ep, sum[0], sum[1], sum[2]);
+    std::fflush(stdout);
+  }
+  if (!model_out.empty())
+    for (int l = 0; l < L; ++l)
+      DfxCheck(dfx_store_save(sl->shard(l), (model_out + "_part-" + std::to_string(sl->rank(l))).c_str(),
+                              1),
+               "dfx_store_save");
+  sl.reset();
+  std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+  return g_fail ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc >= 2 && std::string(argv[1]) == "split") return RunSplit(argc, argv);
   if (argc >= 2 && std::string(argv[1]) == "dist") return RunDist(argc, argv);
   if (argc >= 2 && std::string(argv[1]) == "dist_async") return RunDistAsync(argc, argv);
   if (argc < 2) {

@@ -378,6 +378,69 @@ def test_dist_store_iterate_data_matches_oracle(tmp_path, shards, agg, max_keys)
     assert not os.path.exists(str(tmp_path / "id"))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards,max_keys,extra", [(3, 65536, []), (-1, 65536, []),
+                                                   (3, 256, []), (-1, 256, []),
+                                                   (3, 65536, ["slices=2"]),
+                                                   (3, 256, ["pipelined=0"])])
+def test_split_learner_iterate_data_matches_oracle(tmp_path, shards, max_keys, extra):
+    """GpuSplitLearner (split_learner.h): IterateData's executor fed raw minibatches, the
+    owner-computes split behind it (libdfx_dist.so) — N=3 loopback workers on their own
+    threads, or one RCCL worker (world 1) — against the synchronous sum oracle (one reference
+    step on the concatenated batches): per-epoch loss and AUC, and every server's saved part.
+    max_keys=256: each server's table starts below its share of the model and grows mid-run
+    (sgd_updater.h:178); slices=2: the sliced exchange schedule; pipelined=0: synchronous"""
+    import numpy as np
+    from oracle import dist_oracle as DO
+    from oracle import oracle as O
+    from difacto_amd import data as D
+    N = shards if shards > 0 else 1
+    bs, epochs = 10, 3
+    kw = dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1, seed=7)
+    model = str(tmp_path / "m")
+    env = dict(os.environ, DFX_COMM_ID_FILE=str(tmp_path / "id"))
+    r = subprocess.run([BIN, "split", DATA, "shards=%d" % shards, "epochs=%d" % epochs,
+                        "batch_size=%d" % bs, "model_out=" + model, "max_keys=%d" % max_keys]
+                       + extra + ["%s=%s" % kv for kv in kw.items()],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL PASSED" in r.stdout, r.stdout
+    got = [l.split() for l in r.stdout.splitlines() if l.startswith("epoch ")]
+    assert len(got) == epochs, r.stdout
+    blk = D.read_libsvm(DATA)
+    n = blk.size
+    parts = [list(range(p * n // N, (p + 1) * n // N)) for p in range(N)]
+    nsteps = max((len(p) + bs - 1) // bs for p in parts)
+    so = DO.AggOracle(N, **kw)
+    for ep in range(epochs):
+        loss = auc = 0.0
+        for t in range(nsteps):
+            out = so.step([_slice(blk, parts[p][t * bs:(t + 1) * bs]) for p in range(N)],
+                          push_cnt=ep == 0)
+            loss += sum(o[0] for o in out)
+            auc += sum(o[1] for o in out)
+        g_loss, g_auc, g_rows = float(got[ep][3]), float(got[ep][5]), float(got[ep][7])
+        assert g_rows == n
+        assert abs(g_loss - loss) <= 1e-5 * abs(loss), (ep, g_loss, loss)
+        assert abs(g_auc - auc) <= 1e-4 * n, (ep, g_auc, auc)
+    for g in range(N):
+        up = O.Updater(**kw)
+        up.load(model + "_part-%d" % g)
+        cnt = 0
+        for k in O.localize(blk.offs, blk.ids)[0]:
+            a, b = up.entry(k), so.up[0].entry(k)
+            if a is None:
+                continue
+            cnt += 1
+            assert b is not None
+            assert np.allclose(a[0][:3], b[0][:3], rtol=1e-5, atol=1e-6), (g, k)
+            assert (a[1] is None) == (b[1] is None)
+            if a[1] is not None:
+                assert np.allclose(a[1], b[1], rtol=1e-5, atol=1e-6)
+        assert cnt == up.size() > 0
+    assert not os.path.exists(str(tmp_path / "id"))
+
+
 def _dist_oracle_epochs(blk, N, bs, epochs, agg, kw):
     """per-epoch (loss, auc) of the lockstep sharded oracle: worker p trains rows
     [p n / N, (p + 1) n / N) in batches of bs, the workers stepping together"""
