@@ -65,11 +65,12 @@ build/obj/dist_host.o: difacto_amd/host/dist_host.cc difacto_amd/host/dist_host.
 
 # the training driver (src/main.cc + SGDLearner::RunScheduler): reader -> feeder -> fused step,
 # or the sharded store over RCCL / loopback
-$(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc $(HOSTHDR) difacto_amd/host/dist_host.h \
-  build/obj/dist_host.o $(LIB)
+$(TRAINBIN): $(HOSTLIB) difacto_amd/host/train_main.cc difacto_amd/host/split_learner.cc \
+  $(HOSTHDR) difacto_amd/host/dist_host.h build/obj/dist_host.o $(LIB) $(DISTLIB)
 	@mkdir -p build
-	g++ $(HOSTFLAGS) -o $@ $(HOSTLIB) difacto_amd/host/train_main.cc build/obj/dist_host.o \
-	  -Ldifacto_amd -ldifacto_amd -L/opt/rocm/lib -lrccl -lamdhip64 \
+	g++ $(HOSTFLAGS) -o $@ $(HOSTLIB) difacto_amd/host/train_main.cc \
+	  difacto_amd/host/split_learner.cc build/obj/dist_host.o \
+	  -Ldifacto_amd -ldifacto_amd -ldfx_dist -L/opt/rocm/lib -lrccl -lamdhip64 \
 	  -Wl,-rpath,'$$ORIGIN/../difacto_amd' -Wl,-rpath,/opt/rocm/lib
 
 # the multi-GPU split driver's C-ABI (include/difacto_amd_dist.h): host code (HIP runtime

@@ -238,6 +238,19 @@ void GpuSplitLearner::ProcessBatch(int local, const dmlc::RowBlock<feaid_t>& bat
   DFX_HOST_CHECK(m.failure.empty(), "GpuSplitLearner: " + m.failure);
 }
 
+void GpuSplitLearner::ProcessBatches(const std::vector<const dmlc::RowBlock<feaid_t>*>& batches,
+                                     int job_type, bool push_cnt) {
+  Impl& m = *impl_;
+  DFX_HOST_CHECK((int)batches.size() == m.L, "GpuSplitLearner: one batch per local worker");
+  DFX_HOST_CHECK(job_type == kTraining || job_type == kValidation || job_type == kPrediction,
+                 "GpuSplitLearner: bad job type");
+  std::lock_guard<std::mutex> lk(m.mu);
+  DFX_HOST_CHECK(m.arrived == 0, "GpuSplitLearner: ProcessBatches beside ProcessBatch calls");
+  for (int l = 0; l < m.L; ++l) m.pend[l] = batches[l];
+  m.Submit(job_type, push_cnt && job_type == kTraining);
+  for (auto& p : m.pend) p = nullptr;
+}
+
 void GpuSplitLearner::Flush() {
   Impl& m = *impl_;
   std::lock_guard<std::mutex> lk(m.mu);
@@ -259,7 +272,6 @@ Progress GpuSplitLearner::TakeProgress(int local) {
 }
 
 void GpuSplitLearner::AllReduceSum(std::vector<double>* v) {
-  Flush();
   DistCheck(dfx_split_store_allreduce_sum(impl_->store, v->data(), (int)v->size()),
             "dfx_split_store_allreduce_sum");
 }

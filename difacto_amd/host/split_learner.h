@@ -49,11 +49,15 @@ class GpuSplitLearner {
    * is submitted when the last of them gave its batch; the others wait for that) */
   void ProcessBatch(int local, const dmlc::RowBlock<feaid_t>& batch, int job_type,
                     bool push_cnt);
+  /** one step from a single caller thread: batches[l] is local worker l's minibatch */
+  void ProcessBatches(const std::vector<const dmlc::RowBlock<feaid_t>*>& batches, int job_type,
+                      bool push_cnt);
   /** run the queued step (one thread, every local worker idle) */
   void Flush();
   /** sgd::Progress of worker `local` since the last call (Flush first) */
   Progress TakeProgress(int local);
-  /** v summed over the processes (one thread; a collective of every rank) */
+  /** v summed over the processes (the thread that submits steps; a collective of every rank,
+   * ordered with the steps' own exchanges, so it needs no flush) */
   void AllReduceSum(std::vector<double>* v);
 
   struct Impl;

@@ -15,7 +15,8 @@
 // step together (an exhausted shard submits empty batches until all are done), and
 // `pipelined=1` (default) selects the 1-step-stale schedule.  Each server saves
 // <model_out>_part-<rank>; `model_in_parts=K` loads a model K servers saved into this run's
-// shards (each keeps the keys it owns).
+// shards (each keeps the keys it owns).  `exchange=split` runs the sharded epochs through the
+// owner-computes split (GpuSplitLearner, split_learner.h) instead of KVStoreDist's exchanges.
 //
 // Model files are named like SGDLearner::ModelName (sgd_learner.h:65-69):
 // <prefix>[_iter-<epoch>]_part-0, in SGDUpdater::Save's format; task=2 predicts data_val with
@@ -38,6 +39,7 @@
 #include "dist_host.h"
 #include "gpu_adapters.h"
 #include "reader.h"
+#include "split_learner.h"
 
 using namespace difacto;
 
@@ -51,6 +53,7 @@ struct Param {
   int shards = 0;  // > 0: that many loopback shards in this process; -1: one shard, RCCL
   int model_in_parts = 0;  // servers that saved model_in, when not this run's shard count
   bool pipelined = true;
+  std::string exchange = "a2a";  // a2a: GpuShardedStore (KVStoreDist); split: GpuSplitLearner
   bool has_aux = false, pred_prob = true;
   double stop_rel_objv = 1e-5;
 };
@@ -153,7 +156,103 @@ std::string KwString(const KWArgs& kw) {
   return s;
 }
 
+// exchange=split: the owner-computes split behind GpuSplitLearner (split_learner.h): the same
+// readers, parts and stop rule, one synchronous reference step per batch index on the
+// concatenation of the shards' batches (push_agg=sum); pipelined=1 only overlaps model-free
+// work, so the results equal the synchronous schedule
+int RunShardedSplit(const Param& P, const KWArgs& rest) {
+  const char* ws = std::getenv("WORLD_SIZE");
+  const int world = ws ? std::atoi(ws) : 1;
+  const bool rccl = world > 1 || P.shards < 0;
+  KWArgs kw = rest;
+  kw.push_back({"pipelined", P.pipelined ? "1" : "0"});
+  std::shared_ptr<GpuSplitLearner> sl =
+      rccl ? GpuSplitLearner::CreateRccl(kw) : GpuSplitLearner::CreateLoopback(P.shards, kw);
+  const int nlocal = sl->nlocal(), nshards = sl->nranks(), rank = sl->rank(0);
+  if (!P.model_in.empty()) {
+    const int it = P.load_epoch > 0 ? P.load_epoch : -1;
+    for (int l = 0; l < nlocal; ++l) {
+      if (P.model_in_parts <= 0 || P.model_in_parts == nshards) {
+        DfxCheck(dfx_store_load(sl->shard(l), ModelNamePart(P.model_in, it, sl->rank(l)).c_str()),
+                 "dfx_store_load");
+      } else {
+        for (int r = 0; r < P.model_in_parts; ++r)
+          DfxCheck(dfx_store_load_part(sl->shard(l), ModelNamePart(P.model_in, it, r).c_str(),
+                                       sl->rank(l), nshards),
+                   "dfx_store_load_part");
+      }
+    }
+  }
+  static const size_t kZeroOff = 0;
+  dmlc::RowBlock<feaid_t> empty;
+  empty.size = 0;
+  empty.offset = &kZeroOff;
+  const double t0 = Now();
+  double pre_loss = 0;
+  for (int k = std::max(0, P.load_epoch > 0 ? P.load_epoch + 1 : 0); k < P.max_num_epochs; ++k) {
+    const double te = Now();
+    for (int job = 0; job < P.num_jobs_per_epoch; ++job) {
+      const int nparts = P.num_jobs_per_epoch * nshards;
+      std::vector<std::unique_ptr<ThreadedBatchReader>> rd(nlocal);
+      for (int l = 0; l < nlocal; ++l)
+        rd[l].reset(new ThreadedBatchReader(P.data_in, P.data_format,
+                                            job * nshards + sl->rank(l), nparts, P.batch_size,
+                                            P.batch_size * P.shuffle, P.neg_sampling,
+                                            P.nthreads));
+      std::vector<bool> more(nlocal, true);
+      std::vector<dmlc::RowBlock<feaid_t>> blk(nlocal);
+      for (;;) {
+        std::vector<double> any(1, 0.0);
+        for (int l = 0; l < nlocal; ++l) {
+          if (more[l]) more[l] = rd[l]->Next();
+          if (more[l]) any[0] += 1;
+        }
+        sl->AllReduceSum(&any);
+        if (any[0] == 0) break;
+        std::vector<const dmlc::RowBlock<feaid_t>*> ptrs(nlocal);
+        for (int l = 0; l < nlocal; ++l) {
+          blk[l] = more[l] ? rd[l]->Value().GetBlock() : empty;
+          ptrs[l] = &blk[l];
+        }
+        sl->ProcessBatches(ptrs, GpuSplitLearner::kTraining, k == 0);
+      }
+    }
+    std::vector<double> pr(3, 0.0);
+    for (int l = 0; l < nlocal; ++l) {
+      const Progress p = sl->TakeProgress(l);
+      pr[0] += p.nrows;
+      pr[1] += p.loss;
+      pr[2] += p.auc;
+    }
+    sl->AllReduceSum(&pr);
+    Progress tr;
+    tr.nrows = pr[0];
+    tr.loss = pr[1];
+    tr.auc = pr[2];
+    const double dt = Now() - te;
+    if (rank == 0)
+      std::printf("Epoch[%d] Training: %s  (%.0f ex/s incl. parse+PCIe, %d shards, split, %.2f s)\n",
+                  k, Text(tr).c_str(), tr.nrows / dt, nshards, Now() - t0);
+    std::fflush(stdout);
+    const double eps = std::fabs(tr.loss - pre_loss) / pre_loss;
+    if (eps < P.stop_rel_objv) break;
+    pre_loss = tr.loss;
+  }
+  sl->Flush();
+  if (!P.model_out.empty())
+    for (int l = 0; l < nlocal; ++l)
+      DfxCheck(dfx_store_save(sl->shard(l), ModelNamePart(P.model_out, -1, sl->rank(l)).c_str(),
+                              P.has_aux ? 1 : 0),
+               "dfx_store_save");
+  return 0;
+}
+
 int RunSharded(const Param& P, const KWArgs& rest) {
+  if (P.exchange == "split") return RunShardedSplit(P, rest);
+  if (P.exchange != "a2a") {
+    std::fprintf(stderr, "exchange must be a2a or split\n");
+    return 2;
+  }
   const char* ws = std::getenv("WORLD_SIZE");
   const int world = ws ? std::atoi(ws) : 1;
   const bool rccl = world > 1 || P.shards < 0;
@@ -300,6 +399,7 @@ int main(int argc, char** argv) {
     else if (k == "has_aux") P.has_aux = std::stoi(v) != 0;
     else if (k == "shards") P.shards = std::stoi(v);
     else if (k == "pipelined") P.pipelined = std::stoi(v) != 0;
+    else if (k == "exchange") P.exchange = v;
     else if (k == "model_in_parts") P.model_in_parts = std::stoi(v);
     else {
       fused_given = fused_given || k == "fused";

@@ -289,6 +289,58 @@ def test_train_driver_sharded_loopback_matches_oracle(tmp_path, pipelined, agg, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pipelined,max_keys", [(1, 65536), (0, 65536), (1, 256)])
+def test_train_driver_split_loopback_matches_oracle(tmp_path, pipelined, max_keys):
+    """dfx_train shards=3 exchange=split: the sharded epochs through GpuSplitLearner (the
+    owner-computes split) on the batches the driver forms, against the synchronous sum oracle
+    (one reference step per batch index on the concatenated batches; the pipelined schedule
+    only overlaps model-free work): per-epoch loss and every server's saved part; max_keys=256
+    grows the servers' tables mid-run"""
+    import numpy as np
+    from oracle import dist_oracle as DO
+    from oracle import oracle as O
+    from difacto_amd import data as D
+    N, bs, epochs = 3, 10, 3
+    kw = dict(V_dim=4, V_threshold=1, lr=0.1, V_lr=0.05, l1=0.1, seed=7)
+    model = str(tmp_path / "m")
+    args = [TRAIN_BIN, "data_in=" + DATA, "shards=%d" % N, "pipelined=%d" % pipelined,
+            "exchange=split", "num_jobs_per_epoch=1", "shuffle=0", "batch_size=%d" % bs,
+            "max_num_epochs=%d" % epochs, "stop_rel_objv=0", "model_out=" + model, "has_aux=1",
+            "max_keys=%d" % max_keys] + ["%s=%s" % kv for kv in kw.items()]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = [float(l.split("loss = ")[1].split(",")[0]) for l in r.stdout.splitlines()
+           if "Training:" in l]
+    assert len(got) == epochs, r.stdout
+    blk = D.read_libsvm(DATA)
+    parts = [_part_rows(DATA, p, N) for p in range(N)]
+    nsteps = max((len(p) + bs - 1) // bs for p in parts)
+    so = DO.AggOracle(N, **kw)
+    for ep in range(epochs):
+        loss = 0.0
+        for t in range(nsteps):
+            out = so.step([_slice(blk, parts[p][t * bs:(t + 1) * bs]) for p in range(N)],
+                          push_cnt=ep == 0)
+            loss += sum(o[0] for o in out)
+        assert abs(got[ep] - loss / blk.size) <= 1e-5 * abs(loss / blk.size), (ep, got[ep])
+    for g in range(N):
+        up = O.Updater(**kw)
+        up.load(model + "_part-%d" % g)
+        n = 0
+        for k in O.localize(blk.offs, blk.ids)[0]:
+            a, b = up.entry(k), so.up[0].entry(k)
+            if a is None:
+                continue
+            n += 1
+            assert b is not None
+            assert np.allclose(a[0][:3], b[0][:3], rtol=1e-5, atol=1e-6), (g, k)
+            assert (a[1] is None) == (b[1] is None)
+            if a[1] is not None:
+                assert np.allclose(a[1], b[1], rtol=1e-5, atol=1e-6)
+        assert n == up.size() > 0
+
+
+@pytest.mark.gpu
 def test_train_driver_sharded_rccl_world1(tmp_path):
     """shards=-1: one shard per process over RCCL (communicators from a node-local id file);
     at world size 1 it trains like the single-context store: the same batches (one part),
