@@ -7,6 +7,46 @@
 namespace dfx {
 
 constexpr int kWave = 64;
+
+// Loads / stores with the streaming (non-temporal) cache policy when nt is set: traffic that
+// is touched once per step (the Localizer's sort passes, the model table's random lines) need
+// not displace what is re-read within the step from the Infinity Cache / L2 (the [XV*p | p]
+// rows the backward reads once per occurrence).  Context kwarg nt (a mask, store.hip).
+typedef float dfx_f4v __attribute__((ext_vector_type(4)));
+typedef float dfx_f2v __attribute__((ext_vector_type(2)));
+__device__ inline float4 ld4(const float* p, bool nt) {
+  if (nt) {
+    const dfx_f4v v = __builtin_nontemporal_load(reinterpret_cast<const dfx_f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ inline float2 ld2(const float* p, bool nt) {
+  if (nt) {
+    const dfx_f2v v = __builtin_nontemporal_load(reinterpret_cast<const dfx_f2v*>(p));
+    return make_float2(v.x, v.y);
+  }
+  return *reinterpret_cast<const float2*>(p);
+}
+__device__ inline void st4(float* p, float4 v, bool nt) {
+  if (nt) {
+    const dfx_f4v x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<dfx_f4v*>(p));
+  } else {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+}
+template <typename T>
+__device__ inline T ldnt(const T* p, bool nt) {
+  return nt ? __builtin_nontemporal_load(p) : *p;
+}
+template <typename T>
+__device__ inline void stnt(T* p, T v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+// the context kwarg nt's bits
+constexpr int kNtLane = 1, kNtBwdTable = 2, kNtFwdTable = 4, kNtBwdOcc = 8;
 constexpr uint64_t kEmptyKey = ~0ull;  // never produced by the Localizer
 // the slot of a key whose insert failed (table full, or the reserved key ~0): every consumer
 // skips it — no update ever lands in another key's entry
@@ -164,8 +204,8 @@ __device__ inline float4 ent_state(const Entry* e) {
 }
 // a gradient update's write-back: {w, vrow, sqrt_g, z} as one 16-byte store (fea_cnt does not
 // change in Update(kGradient); vrow is written back as read — InitV sets it later, in order)
-__device__ inline void ent_store_hot(Entry* e, float4 s, int vrow) {
-  *reinterpret_cast<float4*>(e) = make_float4(s.x, __int_as_float(vrow), s.y, s.z);
+__device__ inline void ent_store_hot(Entry* e, float4 s, int vrow, bool nt = false) {
+  st4(reinterpret_cast<float*>(e), make_float4(s.x, __int_as_float(vrow), s.y, s.z), nt);
 }
 
 // writes back {w, sqrt_g, z, fea_cnt}; vrow is untouched

@@ -81,6 +81,17 @@ struct Kw {
   // heads + scan + write)
   int loc_onepass = 0;
   int fat_nb = 6;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B; 6: DESIGN.md (d))
+  // nt=<mask>: streaming (non-temporal) cache policy for 1 the Localizer lane's sort passes and
+  // transform, 2 the backward's model-table lines, 4 the forward's, 8 the backward's
+  // per-occurrence arrays (common.h ld4 / st4)
+  int nt = 0;
+  // bwd_two_pass=1: the wide-V_dim (>= 32 lanes per key) fused backward in two passes (fm.hip
+  // k_fm_bwd_w / _v, bit-identical; A/B: C5 50.4 -> 43.2 M ex/s, so off by default)
+  int bwd_two_pass = 0;
+  // lane_cus=<n>: the Localizer and AUC lanes on n CUs only (a CU-masked stream; lane_cu_stride=1
+  // every (CUs / n)-th CU, else the highest n); main_excl=1: the main stream on the other CUs
+  // (the context's own stream, kept by dfx_ctx_set_stream).  A/B of the lanes' interference.
+  int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;
   // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
   // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
   // auc_high: the AUC lane's short latency-bound chain at high priority, the Localizer lane at
@@ -160,6 +171,17 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
         return DFX_ERR_ARG;
       }
     }
+    else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
+    else if (k == "lane_cus") kw->lane_cus = atoi(cv);
+    else if (k == "lane_cu_stride") kw->lane_cu_stride = atoi(cv);
+    else if (k == "main_excl") kw->main_excl = atoi(cv);
+    else if (k == "nt") {
+      kw->nt = atoi(cv);
+      if (kw->nt < 0 || kw->nt > 15) {
+        set_error("nt must be a mask of 1, 2, 4, 8");
+        return DFX_ERR_ARG;
+      }
+    }
     else if (k == "fat_nb") {
       // the fat forward's nnz per trip at V_dim 16 (V_dim 8 always takes 8)
       kw->fat_nb = atoi(cv);
@@ -224,7 +246,7 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live, &w.hstat};
+                    &w.ivstat, &w.live, &w.hstat, &w.vlist};
   for (DevBuf* b : bufs) b->release();
 }
 
@@ -242,11 +264,31 @@ int pipeline_init(Context* c) {
   // starved, 108 -> 70 M ex/s); bit 1 the AUC lane high, else priority 0
   int main_prio = 0;
   if (hipStreamGetPriority(c->stream, &main_prio) != hipSuccess) main_prio = 0;
-  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
-                                      (c->lane_prio & 1) ? hi : main_prio));
+  if (c->lane_cus > 0) {
+    hipDeviceProp_t prop;
+    DFX_HIP(hipGetDeviceProperties(&prop, c->device));
+    const int ncu = prop.multiProcessorCount, n = c->lane_cus < ncu ? c->lane_cus : ncu;
+    std::vector<uint32_t> lane((ncu + 31) / 32, 0u), rest((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i) {
+      const bool on = c->lane_cu_stride ? (i % (ncu / n) == 0 && i / (ncu / n) < n)
+                                        : i >= ncu - n;
+      (on ? lane : rest)[i / 32] |= 1u << (i % 32);
+    }
+    DFX_HIP(hipExtStreamCreateWithCUMask(&c->loc_stream, (uint32_t)lane.size(), lane.data()));
+    DFX_HIP(hipExtStreamCreateWithCUMask(&c->aux_stream, (uint32_t)lane.size(), lane.data()));
+    if (c->main_excl) {
+      hipStream_t m = nullptr;
+      DFX_HIP(hipExtStreamCreateWithCUMask(&m, (uint32_t)rest.size(), rest.data()));
+      c->masked_main = m;
+      c->stream = m;
+    }
+  } else {
+    DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
+                                        (c->lane_prio & 1) ? hi : main_prio));
+    DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
+                                        (c->lane_prio & 2) ? hi : 0));
+  }
   c->own_loc_stream = c->loc_stream;
-  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
-                                      (c->lane_prio & 2) ? hi : 0));
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
   for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
@@ -300,6 +342,11 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_bwd = kw.fat_bwd;
   c->initv_onepass = kw.initv_onepass;
   c->fat_nb = kw.fat_nb;
+  c->nt_mask = kw.nt;
+  c->bwd_two_pass = kw.bwd_two_pass;
+  c->lane_cus = kw.lane_cus;
+  c->lane_cu_stride = kw.lane_cu_stride;
+  c->main_excl = kw.main_excl;
   c->fwd_lanes = kw.fwd_lanes;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;
@@ -377,6 +424,10 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->masked_main) {
+    (void)hipStreamSynchronize(c->masked_main);
+    (void)hipStreamDestroy(c->masked_main);
+  }
   delete ctx;
   return DFX_OK;
 }
@@ -384,7 +435,8 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
 int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream) {
   DFX_CHECK_ARG(ctx, "null ctx");
   // NULL is HIP's null (legacy default) stream, which is also torch's default stream
-  ctx->c.stream = static_cast<hipStream_t>(hip_stream);
+  // (kwarg main_excl keeps its CU-masked main stream)
+  ctx->c.stream = ctx->c.masked_main ? ctx->c.masked_main : static_cast<hipStream_t>(hip_stream);
   return DFX_OK;
 }
 

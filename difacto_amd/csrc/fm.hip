@@ -34,37 +34,39 @@ enum FwdMode { kPredict = 0, kGradPrep = 1, kFused = 2, kFusedProbe = 3 };
 // width and the row 16-byte aligned, so a lane's chunk is wholly inside or wholly outside
 // the row (outside chunks read chunk 0 and are ignored).
 template <int CPL, bool VEC>
-__device__ inline void load_coords(const float* row, int l, int d, float (&v)[CPL]) {
+__device__ inline void load_coords(const float* row, int l, int d, float (&v)[CPL],
+                                   bool nt = false) {
   const int base = l * CPL;
   if constexpr (VEC && CPL % 4 == 0) {
     const int b = base < d ? base : 0;
 #pragma unroll
     for (int m = 0; m < CPL / 4; ++m) {
-      const float4 f = *reinterpret_cast<const float4*>(row + b + 4 * m);
+      const float4 f = ld4(row + b + 4 * m, nt);
       v[4 * m] = f.x; v[4 * m + 1] = f.y; v[4 * m + 2] = f.z; v[4 * m + 3] = f.w;
     }
   } else {
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       const int cd = base + k;
-      v[k] = row[cd < d ? cd : 0];
+      v[k] = ldnt(row + (cd < d ? cd : 0), nt);
     }
   }
 }
 
 template <int CPL, bool VEC>
-__device__ inline void store_coords(float* row, int l, int d, const float (&v)[CPL]) {
+__device__ inline void store_coords(float* row, int l, int d, const float (&v)[CPL],
+                                    bool nt = false) {
   const int base = l * CPL;
   if (base >= d) return;
   if constexpr (VEC && CPL % 4 == 0) {
 #pragma unroll
     for (int m = 0; m < CPL / 4; ++m)
-      *reinterpret_cast<float4*>(row + base + 4 * m) =
-          make_float4(v[4 * m], v[4 * m + 1], v[4 * m + 2], v[4 * m + 3]);
+      st4(row + base + 4 * m, make_float4(v[4 * m], v[4 * m + 1], v[4 * m + 2], v[4 * m + 3]),
+          nt);
   } else {
 #pragma unroll
     for (int k = 0; k < CPL; ++k)
-      if (base + k < d) row[base + k] = v[k];
+      if (base + k < d) stnt(row + base + k, v[k], nt);
   }
 }
 
@@ -329,6 +331,7 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
     float acc = 0.f;
     float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};
     const bool valued = a.val != nullptr;
+    const bool ntf = (a.nt & kNtFwdTable) != 0;
     if constexpr (FAT) {
       for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
         const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
@@ -347,8 +350,8 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
           const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
-          eh[t] = *reinterpret_cast<const float2*>(sl + ((l & 1) ? 6 : 0));
-          v[t] = *reinterpret_cast<const float4*>(sl + 8 + 4 * l);
+          eh[t] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
+          v[t] = ld4(sl + 8 + 4 * l, ntf);
         }
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
@@ -851,7 +854,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   int dnew = 0, ninit = 0, nins = 0;
   unsigned nlive = 0, nlocc = 0;  // keys with V in this step, and their occurrences (roofline)
   if (u < nseg) {
-    const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
+    const bool ntb = (a.nt & kNtBwdTable) != 0, nto = (a.nt & kNtBwdOcc) != 0;
+    const uint32_t s0 = ldnt(a.segstart + u, nto), s1 = ldnt(a.segstart + u + 1, nto);
     const uint32_t cidx = a.segcol ? a.segcol[u] : (uint32_t)u;
     const bool valued = a.occ_x != nullptr;
     const int d = a.d;
@@ -871,15 +875,15 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (a.insert_keys) {
         // Get's find-or-insert (model_[key]) here instead of a separate pass: the home slot
         // first (every lane), a longer chain or an insert by the group's first lane
-        const uint64_t key = a.uniq[cidx];
+        const uint64_t key = ldnt(a.uniq + cidx, nto);
         const uint64_t hh = tbl_hash(key, a.T);
         // the whole home entry in two 16-byte loads issued together: {w, vrow, sqrt_g, z} and
         // {fea_cnt, pad, key}; a key found at home (the common case) needs no second trip
-        const float4* eh = reinterpret_cast<const float4*>(ent_at(a.T, hh));
-        const float4 h0 = eh[0], h1 = eh[1];
+        const float* eh = reinterpret_cast<const float*>(ent_at(a.T, hh));
+        const float4 h0 = ld4(eh, ntb), h1 = ld4(eh + 4, ntb);
         if (a.T.es && !a.no_fat_spec) {  // a key at home has V there: one trip for the key
-          load_coords<CPL, VEC>(row_V(a.T, (int64_t)hh), l, d, vcur);
-          load_coords<CPL, VEC>(row_C(a.T, (int64_t)hh), l, d, ccur);
+          load_coords<CPL, VEC>(row_V(a.T, (int64_t)hh), l, d, vcur, ntb);
+          load_coords<CPL, VEC>(row_C(a.T, (int64_t)hh), l, d, ccur, ntb);
           spec = true;
         }
         const uint64_t ek =
@@ -924,8 +928,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
       const uint32_t i = s0 + ((uint32_t)t < len ? (uint32_t)t : 0u);
-      row[t] = a.occ_row[i];
-      x[t] = valued ? a.occ_x[i] : 1.f;
+      row[t] = ldnt(a.occ_row + i, nto);
+      x[t] = valued ? ldnt(a.occ_x + i, nto) : 1.f;
     }
     // ---- level 3: V / Vaux (or grad / W) of the key, p and XV*p of the occurrences' rows
     float gw = 0.f;
@@ -938,8 +942,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       // V was pulled iff present and not (l1_shrk && w == 0) (SGDUpdater::Get, :40-43)
       vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
       if (!(spec && home && vq >= 0)) {  // (fat slots: at home, vrow == the home slot)
-        load_coords<CPL, VEC>(vq >= 0 ? row_V(a.T, vq) : zp, l, d, vcur);
-        load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur);
+        load_coords<CPL, VEC>(vq >= 0 ? row_V(a.T, vq) : zp, l, d, vcur, ntb);
+        load_coords<CPL, VEC>(vq >= 0 ? row_C(a.T, vq) : zp, l, d, ccur, ntb);
       }
 #pragma unroll
       for (int k = 0; k < CPL; ++k) g0[k] = 0.f;
@@ -1098,11 +1102,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (vq >= 0) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
-        store_coords<CPL, VEC>(row_V(a.T, vq), l, d, vcur);
-        store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur);
+        store_coords<CPL, VEC>(row_V(a.T, vq), l, d, vcur, ntb);
+        store_coords<CPL, VEC>(row_C(a.T, vq), l, d, ccur, ntb);
       }
       if (l == 0) {
-        if (!dead) ent_store_hot(ent_at(a.T, sl), e, vrow);
+        if (!dead) ent_store_hot(ent_at(a.T, sl), e, vrow, ntb);
         dnew = dead ? 0 : dw;
         // InitV on a 0 -> nonzero transition (sgd_updater.cc:118-121); e.w is fea_cnt
         const bool need =
@@ -1148,6 +1152,243 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
       if (a.live_part) a.live_part[blockIdx.x] = make_uint2((unsigned)lv, (unsigned)lo);
     }
+  }
+}
+
+// ---- the fused backward in two passes, for wide V_dim (G >= 32 lanes per key) ------------
+// With d = 128 a key's group is 32 lanes, and under lazy V (C5: V_threshold, Zipf keys) most
+// keys carry no V: their group does a w-only update on lane 0 while 31 lanes wait, two keys per
+// wave, a latency-bound walk (profiles/r3/kernel_summary_c5.md).  Pass W takes one lane per key
+// — the entry's find-or-insert, g_w and XXp over the key's occurrences in order, FTRL, the InitV
+// flag — and lists each key whose V was pulled with its XXp; pass V takes G lanes per listed key
+// for the sum of (XV*p) x in occurrence order and AdaGrad.  Every term and its order are
+// k_fm_bwd's, so the model is bit-identical; the list's order (wave-aggregated appends) changes
+// only which group updates which key.  Both passes loop over a resident grid.  Measured on C5
+// (same box, kwarg bwd_two_pass=1): backward 1.53 -> 1.85 ms — under Zipf keys a wave of pass W
+// runs as long as its longest key's serial walk, which the one-kernel form spreads over two
+// keys per wave; kept as an A/B.
+constexpr int kBwdWNT = 256;
+
+__global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
+  __shared__ int red[kBwdWNT / kWave], redn[kBwdWNT / kWave], redi[kBwdWNT / kWave];
+  __shared__ unsigned redl[kBwdWNT / kWave], redo[kBwdWNT / kWave];
+  const int64_t nseg = a.nseg_host >= 0 ? a.nseg_host : (int64_t)a.ds->u_count;
+  const int d = a.d;
+  const int64_t xs = a.xs > d ? a.xs : d;
+  const bool valued = a.occ_x != nullptr;
+  int dnew = 0, ninit = 0, nins = 0;
+  unsigned nlive = 0, nlocc = 0;
+  const int64_t stride = (int64_t)gridDim.x * kBwdWNT;
+  // every lane runs the same number of rounds (the list append is wave-aggregated)
+  const int64_t rounds = (nseg + stride - 1) / stride;
+  for (int64_t rd = 0; rd < rounds; ++rd) {
+    const int64_t u = rd * stride + (int64_t)blockIdx.x * kBwdWNT + threadIdx.x;
+    bool listed = false;
+    uint4 item = make_uint4(0u, 0u, 0u, 0u);
+    if (u < nseg) {
+      const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
+      const uint32_t len = s1 - s0;
+      const uint32_t cidx = (uint32_t)u;
+      uint32_t sl = 0;
+      bool home = false;
+      float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+      float fc = 0.f;
+      if (a.insert_keys) {
+        const uint64_t key = a.uniq[cidx];
+        const uint64_t hh = tbl_hash(key, a.T);
+        const float4* eh = reinterpret_cast<const float4*>(ent_at(a.T, hh));
+        const float4 h0 = eh[0], h1 = eh[1];
+        const uint64_t ek =
+            ((uint64_t)__float_as_uint(h1.w) << 32) | (uint64_t)__float_as_uint(h1.z);
+        home = ek == key;
+        h = h0;
+        fc = h1.x;
+        int64_t s = (int64_t)hh;
+        if (!home) {
+          bool inserted;
+          s = tbl_insert(a.T, key, &inserted);
+          if (s < 0) atomicOr(&a.dsw->err, insert_error(s));
+          nins += inserted ? 1 : 0;
+        }
+        sl = s < 0 ? kNoSlot : (uint32_t)s;
+      } else {
+        sl = a.slot[cidx];
+      }
+      const bool dead = sl == kNoSlot;
+      if (dead) {
+        h = make_float4(0.f, __int_as_float(-1), 0.f, 0.f);
+        fc = 0.f;
+      } else if (!home) {
+        const Entry* en = ent_at(a.T, sl);
+        h = *reinterpret_cast<const float4*>(en);
+        fc = en->fea_cnt;
+      }
+      float4 e = make_float4(h.x, h.z, h.w, fc);  // {w, sqrt_g, z, fea_cnt}
+      const int vrow = __float_as_int(h.y);
+      const int vq = (vrow >= 0 && !(a.Pm.l1_shrk && e.x == 0.f)) ? vrow : -1;
+      float gw = 0.f, xxp = 0.f;
+      if (a.choff && len > (uint32_t)kChunkOcc) {
+        const uint32_t c0 = a.choff[u];
+        const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+        double gwd = 0, xxpd = 0;
+        for (uint32_t c = 0; c < nc; ++c) {
+          const double* pc = a.part + (int64_t)(c0 + c) * (d + 2);
+          gwd += pc[0];
+          xxpd += pc[1];
+        }
+        gw = (float)gwd;
+        xxp = (float)xxpd;
+      } else {
+        for (uint32_t i0 = s0; i0 < s1; i0 += 4) {
+          uint32_t rw[4];
+          float xw[4], pw[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
+            rw[t] = a.occ_row[i];
+            xw[t] = valued ? a.occ_x[i] : 1.f;
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (i0 + t < s1 && pw[t] != 0.f) {
+              if (valued) {
+                gw += pw[t] * xw[t];
+                xxp += pw[t] * (xw[t] * xw[t]);
+              } else {
+                gw += pw[t];
+                xxp += pw[t];
+              }
+            }
+          }
+        }
+      }
+      // Update(kGradient): UpdateW (FTRL); UpdateV by pass V if V was pulled
+      bool tr;
+      const int dw = ftrl_update(a.Pm, gw, &e, &tr);
+      if (!dead) ent_store_hot(ent_at(a.T, sl), e, vrow);
+      dnew += dead ? 0 : dw;
+      const bool need = !dead && tr && d > 0 && vrow < 0 && e.w > (float)a.Pm.V_threshold;
+      a.flags[u] = need ? 1u : 0u;
+      if (need && a.insert_keys) a.slot[cidx] = sl;
+      ninit += need ? 1 : 0;
+      if (vq >= 0) {
+        listed = true;
+        item = make_uint4((uint32_t)u, (uint32_t)vq, __float_as_uint(xxp), 0u);
+        nlive += 1u;
+        nlocc += len;
+      }
+    }
+    // the listed keys of this wave: one append
+    const uint64_t m = __ballot(listed);
+    if (m) {
+      uint32_t base = 0;
+      if (lane_id() == 0) base = atomicAdd(a.vcount, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, 0, kWave);
+      if (listed) a.vlist[base + (uint32_t)__popcll(m & lanemask_lt())] = item;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    dnew += __shfl_xor(dnew, off, kWave);
+    ninit += __shfl_xor(ninit, off, kWave);
+    nins += __shfl_xor(nins, off, kWave);
+    nlive += __shfl_xor(nlive, off, kWave);
+    nlocc += __shfl_xor(nlocc, off, kWave);
+  }
+  if (lane_id() == 0) {
+    red[threadIdx.x / kWave] = dnew;
+    redn[threadIdx.x / kWave] = ninit;
+    redi[threadIdx.x / kWave] = nins;
+    redl[threadIdx.x / kWave] = nlive;
+    redo[threadIdx.x / kWave] = nlocc;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0, q = 0, i2 = 0;
+    unsigned long long lv = 0, lo = 0;
+    for (int i = 0; i < kBwdWNT / kWave; ++i) {
+      s += red[i];
+      q += redn[i];
+      i2 += redi[i];
+      lv += redl[i];
+      lo += redo[i];
+    }
+    if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
+    if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
+    if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
+    if (a.live_part) a.live_part[blockIdx.x] = make_uint2((unsigned)lv, (unsigned)lo);
+  }
+}
+
+template <int G, int CPL>
+__global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
+  constexpr int EPB = kFmNT / G;
+  constexpr int UNR = CPL <= 4 ? 4 : 2;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t n = (int64_t)*a.vcount;
+  const int d = a.d;
+  const int64_t xs = a.xs > d ? a.xs : d;
+  const bool valued = a.occ_x != nullptr;
+  for (int64_t j = (int64_t)blockIdx.x * EPB + g; j < n; j += (int64_t)gridDim.x * EPB) {
+    const uint4 it = a.vlist[j];
+    const uint32_t u = it.x;
+    const int vq = (int)it.y;
+    const float xxp = __uint_as_float(it.z);
+    const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
+    const uint32_t len = s1 - s0;
+    float vcur[CPL], ccur[CPL], acc[CPL];
+    load_coords<CPL, true>(row_V(a.T, vq), l, d, vcur);
+    load_coords<CPL, true>(row_C(a.T, vq), l, d, ccur);
+    // grad_u = (g0 - V*XXp) + sum (XV_ p) x, g0 = 0 (fm_loss.h:185-202, spmm.h:127-159)
+    if (a.choff && len > (uint32_t)kChunkOcc) {
+      const uint32_t c0 = a.choff[u];
+      const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+      double accp[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) accp[k] = 0;
+      for (uint32_t c = 0; c < nc; ++c) {
+        const double* pc = a.part + (int64_t)(c0 + c) * (d + 2);
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const int cd = l * CPL + k;
+          accp[k] += cd < d ? pc[2 + cd] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < CPL; ++k)
+        acc[k] = (float)((double)(0.f - vcur[k] * xxp) + accp[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) acc[k] = 0.f - vcur[k] * xxp;
+      for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+        uint32_t rw[UNR];
+        float xw[UNR], xrw[UNR][CPL];
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
+          rw[t] = a.occ_row[i];
+          xw[t] = valued ? a.occ_x[i] : 1.f;
+        }
+#pragma unroll
+        for (int t = 0; t < UNR; ++t)
+          load_coords<CPL, true>(a.XVp + (int64_t)rw[t] * xs, l, d, xrw[t]);
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          if (i0 + t < s1) {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+              acc[k] = valued ? acc[k] + xrw[t][k] * xw[t] : acc[k] + xrw[t][k];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) adagrad_update(a.Pm, acc[k], &vcur[k], &ccur[k]);
+    store_coords<CPL, true>(row_V(a.T, vq), l, d, vcur);
+    store_coords<CPL, true>(row_C(a.T, vq), l, d, ccur);
   }
 }
 
@@ -1259,12 +1500,54 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   return DFX_ERR_ARG;
 }
 
+// the two-pass backward's resident grid (blocks per pass)
+constexpr int64_t kBwdPassBlocks = 4096;
+
+// V_dim whose backward runs in two passes (k_fm_bwd_w + k_fm_bwd_v): G >= 32 lanes per key
+bool bwd_two_pass(int d) {
+  int G, CPL;
+  bool vec;
+  lanes_for(d, true, &G, &CPL, &vec);
+  return vec && CPL == 4 && G >= 32;
+}
+
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds) {
-  return launch_bwd<true>(a, nseg_bound, st, true, lds);
+  if (!a.vlist) return launch_bwd<true>(a, nseg_bound, st, true, lds);
+  if (nseg_bound <= 0) return DFX_OK;
+  int G, CPL;
+  bool vec;
+  lanes_for(a.d, true, &G, &CPL, &vec);
+  if (!(vec && CPL == 4 && (G == 32 || G == 64))) {
+    set_error("two-pass backward: V_dim a multiple of 4, 32 or 64 lanes per key");
+    return DFX_ERR_ARG;
+  }
+  const size_t lds_bytes = lds >= 0 ? (size_t)lds : kBwdLdsCap;
+  DFX_HIP(hipMemsetAsync(a.vcount, 0, sizeof(uint32_t), st));
+  const int64_t gw = std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);
+  hipLaunchKernelGGL(k_fm_bwd_w, dim3((unsigned)gw), dim3(kBwdWNT), 0, st, a);
+  const int64_t epb = kFmNT / G;
+  const int64_t gv = std::min<int64_t>((nseg_bound + epb - 1) / epb, kBwdPassBlocks);
+  if (G == 32)
+    hipLaunchKernelGGL((k_fm_bwd_v<32, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, a);
+  else
+    hipLaunchKernelGGL((k_fm_bwd_v<64, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, a);
+  DFX_HIP(hipGetLastError());
+  return DFX_OK;
+}
+
+int bwd_two_pass_reserve(Context* c, Workspace& ws, int64_t nseg_bound, BwdArgs* g) {
+  g->vlist = nullptr;
+  g->vcount = nullptr;
+  if (c->bwd_two_pass == 0 || !bwd_two_pass(c->P.V_dim) || nseg_bound <= 0) return DFX_OK;
+  DFX_TRY(ws.vlist.ensure((size_t)(nseg_bound + 1) * sizeof(uint4)));
+  g->vlist = ws.vlist.as<uint4>();
+  g->vcount = reinterpret_cast<uint32_t*>(g->vlist + nseg_bound);
+  return DFX_OK;
 }
 
 // blocks of the fused backward over nseg_bound keys (the size of BwdArgs::live_part)
-int64_t bwd_fused_blocks(int d, int64_t nseg_bound) {
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass) {
+  if (two_pass) return std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);
   int G, CPL;
   bool vec;
   lanes_for(d, true, &G, &CPL, &vec);

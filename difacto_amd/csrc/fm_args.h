@@ -62,6 +62,7 @@ struct FwdArgs {
   int fat_nb;      // fat forward: nnz per trip at V_dim 16 (kwarg fat_nb = 4 | 6 | 8 | 12)
   int fwd_lanes;   // V_dim 16 fat slots: k_fm_fwd_fat_pf with this many lanes per row (0: off)
   float* part;
+  int nt;  // kwarg nt: kNtFwdTable = the slots with the streaming policy
   // the split's sliced owner forward (slice_len > 0): B = workers * slice_len logical rows,
   // logical row i being the owner's row (i / slice_len) * slice_m + slice_lo + i % slice_len
   int64_t slice_m, slice_lo, slice_len;
@@ -87,6 +88,7 @@ __host__ __device__ inline int split_pxv_floats(int d, int wide = 0) {
 
 struct BwdArgs {
   int no_fat_spec;           // fat slots: no V / Vaux loads beside the home entry (A/B)
+  int nt;                    // kwarg nt: kNtBwdTable / kNtBwdOcc with the streaming policy
   const uint32_t* segstart;  // nseg+1
   const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
   int64_t nseg_host;
@@ -127,6 +129,11 @@ struct BwdArgs {
   const uint32_t* chunk_seg;
   const uint32_t* nchunks;
   double* part;
+  // wide V_dim, two passes (launch_bwd_fused with wsplit): a pass with one lane per key (entry,
+  // g_w, FTRL) lists the keys whose V it must update {segment, V row, XXp}; a pass with G lanes
+  // per listed key does the V sums and AdaGrad
+  uint4* vlist;
+  uint32_t* vcount;
 };
 
 // the XVp row stride the workspace is sized for (step.hip): p rides in each row
@@ -136,7 +143,11 @@ int xvp_stride(const Context* c);
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread = true);
 // fused backward + FTRL/AdaGrad update over at most nseg_bound segments; lds: bytes of LDS
 // reserved per block (-1: the default cap)
-int64_t bwd_fused_blocks(int d, int64_t nseg_bound);
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass = false);
+// V_dim whose fused backward may run in two passes (>= 32 lanes per key)
+bool bwd_two_pass(int d);
+// the two-pass backward's list for nseg_bound keys, when the context runs it (else vlist NULL)
+int bwd_two_pass_reserve(Context* c, Workspace& ws, int64_t nseg_bound, BwdArgs* g);
 int sum_live(const uint2* part, int64_t n, DevState* ds, hipStream_t st);
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds = -1);
 // the chunk partials of long segments (before the backward reads them)

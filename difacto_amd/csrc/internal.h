@@ -92,6 +92,7 @@ struct Workspace {
   DevBuf dscratch;  // double partials
   DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
   DevBuf live;      // (diagnostic) the fused backward's per-block live-V counts
+  DevBuf vlist;     // the two-pass backward's listed keys {segment, V row, XXp, 0} + a counter
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
@@ -198,6 +199,10 @@ struct Context {
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
   int fat_nb = 6;         // kwarg fat_nb
+  int nt_mask = 0;        // kwarg nt (common.h kNt*)
+  int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
+  int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
+  hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
   int loc_bucket = 0;     // kwarg loc_bucket (localize.hip k_loc_bucket)
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
@@ -285,6 +290,8 @@ constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
 // k_loc_bucket) when no bucket exceeds kSortBucketMax items; sortmeta[30] says so,
 // [28..29] hold the shifts of the digits below the top one
 constexpr int kSortBucket = 4;
+// flags |= kSortNT: the scatter passes load and store their items with the streaming policy
+constexpr int kSortNT = 8;
 constexpr uint32_t kSortBucketMax = 1u << 18;
 constexpr int kSortMetaRest = 28, kSortMetaBucket = 30;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }

@@ -34,6 +34,7 @@ struct TransformArgs {
   uint32_t* parts;  // radix-sort digit counts of every 8-bit position (ws.os_parts())
   DevState* ds;     // the lane's state: OR / AND of the keys
   int keys_ready;   // index holds the final keys (no ReverseBytes / max_index)
+  int nt;           // streaming policy for the ids read and the items written (kwarg nt & 1)
 };
 
 __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
@@ -49,7 +50,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
   const uint64_t j0 = offs[0], j1 = offs[nr];
   unsigned long long vor = 0, vand = ~0ull;
   for (uint64_t j = j0 + threadIdx.x; j < j1; j += kLocNT) {
-    const uint64_t id = a.index[j];
+    const uint64_t id = ldnt(a.index + j, a.nt != 0);
     const uint64_t m = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
     const uint64_t k = a.keys_ready ? id : reverse_bytes(m);
     vor |= k;
@@ -73,11 +74,11 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
       const int mid = (lo + hi) >> 1;
       if (offs[mid] <= j) lo = mid; else hi = mid;
     }
-    a.keys[j] = k;
+    stnt(a.keys + j, k, a.nt != 0);
     if (a.pay32)
-      a.pay32[j] = (uint32_t)(r0 + lo);
+      stnt(a.pay32 + j, (uint32_t)(r0 + lo), a.nt != 0);
     else
-      a.pay[j] = (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32);
+      stnt(a.pay + j, (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32), a.nt != 0);
   }
   for (int off = 32; off > 0; off >>= 1) {
     vor |= __shfl_xor(vor, off, kWave);
@@ -615,6 +616,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
   t.keys = k0; t.pay = p0; t.pay32 = q0; t.parts = ws.os_parts(); t.ds = ds;
   t.keys_ready = o.keys_ready ? 1 : 0;
+  t.nt = (c->nt_mask & kNtLane) ? 1 : 0;
   hipLaunchKernelGGL(k_loc_transform, dim3((unsigned)((B + kLocRows - 1) / kLocRows)),
                      dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits
@@ -628,13 +630,15 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0) |
-                                                      (c->loc_bucket ? kSortBucket : 0))));
+                                                      (c->loc_bucket ? kSortBucket : 0) |
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
                                                       kSortItems(c->sort_items) |
-                                                      kSortLookback(c->sort_lookback))));
+                                                      kSortLookback(c->sort_lookback) |
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
   }
   // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
   // k_loc_write with look-back; in bucket mode (the plan's choice) k_loc_bucket does it per

@@ -182,7 +182,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
                                                       const uint32_t* n_dev, unsigned int* meta,
                                                       int q, const uint32_t* counts,
                                                       unsigned long long* status,
-                                                      int* err) {
+                                                      int* err, int nt) {
   const unsigned m = meta[q];
   if (m == kOsNone) return;
   const int shift = (int)(m & 0xFFFFu);
@@ -228,14 +228,15 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
 #pragma unroll
   for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
-    key[c] = idx < n ? kin[idx] : (K)0;
+    key[c] = idx < n ? ldnt(kin + idx, nt != 0) : (K)0;
   }
   if (pack_now) {
 #pragma unroll
     for (int c = 0; c < IT; ++c) {
       const int64_t idx = wbase + c * kWave + l;
       if (idx < n)
-        key[c] = (K)((((uint64_t)key[c] >> lo8) << rb8) | (uint64_t)(uint32_t)vin[idx]);
+        key[c] = (K)((((uint64_t)key[c] >> lo8) << rb8) |
+                     (uint64_t)(uint32_t)ldnt(vin + idx, nt != 0));
     }
   }
 #pragma unroll
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
       const K kk = lk[qi];
       const uint32_t d = (uint32_t)(kk >> shift) & dmask;
       ldig[qi] = (uint8_t)d;
-      kout[gdig[d] + ((uint32_t)qi - lstart[d])] = kk;
+      stnt(kout + gdig[d] + ((uint32_t)qi - lstart[d]), kk, nt != 0);
     }
   }
   if (packed) return;  // the payload rides in the key
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
 #pragma unroll
   for (int c = 0; c < IT; ++c) {
     const int64_t idx = wbase + c * kWave + l;
-    if (idx < n) lv[dr[c]] = vin[idx];
+    if (idx < n) lv[dr[c]] = ldnt(vin + idx, nt != 0);
   }
   __syncthreads();
 #pragma unroll
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
     const int qi = i * kOsNT + t;
     if (qi < nvalid) {
       const uint32_t d = ldig[qi];
-      vout[gdig[d] + ((uint32_t)qi - lstart[d])] = lv[qi];
+      stnt(vout + gdig[d] + ((uint32_t)qi - lstart[d]), lv[qi], nt != 0);
     }
   }
 }
@@ -412,7 +413,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
     if (it == IT && lb == LB)                                                                \
       hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)ntiles), dim3(kOsNT), 0, \
                          L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status,     \
-                         L.err);
+                         L.err, (flags & kSortNT) ? 1 : 0);
     DFX_OS_SCATTER(8, 4)
     DFX_OS_SCATTER(16, 4)
     DFX_OS_SCATTER(32, 4)

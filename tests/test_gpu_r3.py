@@ -357,3 +357,44 @@ def test_bucket_localizer_equals_lsd(H, kind):
     assert st[0]["seed"] == st[1]["seed"] == st[2]["seed"] == up.seed
     for c in cs:
         c.close()
+
+
+@pytest.mark.parametrize("d", [128, 200])
+def test_two_pass_backward_bit_identical(H, d):
+    """The wide-V_dim fused backward in two passes (k_fm_bwd_w: one lane per key — entry, g_w,
+    FTRL — listing the keys with V; k_fm_bwd_v: G lanes per listed key — the V sums, AdaGrad)
+    (kwarg bwd_two_pass=1) against the one-kernel backward: every term in the same order, so the
+    predictions, the progress and the model are bit-identical.  Zipf(1.1) keys with lazy V
+    (C5's shape): most keys carry no V, hot keys take the chunked sums."""
+    cfg = dict(V_dim=d, lr=.05, V_lr=.01, V_threshold=4)
+    ca = H.Context(0, max_keys=1 << 17, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, bwd_two_pass=1, **cfg)
+    blocks = []
+    for step in range(5):
+        blk = D.synthetic(3000, 39, 1 << 18, zipf=1.1, seed=500 + step)
+        blocks.append(blk)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step < 2, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step < 2, pred=pb)
+        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
+        a, b = H.progress(ca), H.progress(cb)
+        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
+    ca.sync()
+    cb.sync()
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0] for b in blocks]))
+    nv = 0
+    for k in keys[::3]:
+        ea, eb = H.Store(ca).entry(k), H.Store(cb).entry(k)
+        assert (ea is None) == (eb is None)
+        if ea is None:
+            continue
+        assert np.array_equal(ea[0], eb[0]), k
+        assert (ea[1] is None) == (eb[1] is None)
+        if ea[1] is not None:
+            nv += 1
+            assert np.array_equal(ea[1], eb[1]), k
+    assert nv > 0
+    ca.close()
+    cb.close()
