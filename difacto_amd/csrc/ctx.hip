@@ -88,6 +88,9 @@ struct Kw {
   // bwd_two_pass=1: the wide-V_dim (>= 32 lanes per key) fused backward in two passes (fm.hip
   // k_fm_bwd_w / _v, bit-identical; A/B: C5 50.4 -> 43.2 M ex/s, so off by default)
   int bwd_two_pass = 0;
+  // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
+  // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
+  int loc_pos = 0;
   // lane_cus=<n>: the Localizer and AUC lanes on n CUs only (a CU-masked stream; lane_cu_stride=1
   // every (CUs / n)-th CU, else the highest n); main_excl=1: the main stream on the other CUs
   // (the context's own stream, kept by dfx_ctx_set_stream).  A/B of the lanes' interference.
@@ -172,6 +175,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       }
     }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
+    else if (k == "loc_pos") kw->loc_pos = atoi(cv) != 0;
     else if (k == "lane_cus") kw->lane_cus = atoi(cv);
     else if (k == "lane_cu_stride") kw->lane_cu_stride = atoi(cv);
     else if (k == "main_excl") kw->main_excl = atoi(cv);
@@ -246,7 +250,7 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live, &w.hstat, &w.vlist};
+                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.rowtmp2};
   for (DevBuf* b : bufs) b->release();
 }
 
@@ -344,6 +348,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_nb = kw.fat_nb;
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
+  c->loc_pos_payload = kw.loc_pos;
   c->lane_cus = kw.lane_cus;
   c->lane_cu_stride = kw.lane_cu_stride;
   c->main_excl = kw.main_excl;

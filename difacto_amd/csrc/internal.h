@@ -93,6 +93,7 @@ struct Workspace {
   DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
   DevBuf live;      // (diagnostic) the fused backward's per-block live-V counts
   DevBuf vlist;     // the two-pass backward's listed keys {segment, V row, XXp, 0} + a counter
+  DevBuf rowtmp2;   // the Localizer's row of each position (valued data, position payloads)
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
@@ -201,6 +202,7 @@ struct Context {
   int fat_nb = 6;         // kwarg fat_nb
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
+  int loc_pos_payload = 0;  // kwarg loc_pos: valued data sorts packed (key | position) items
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes

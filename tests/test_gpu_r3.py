@@ -398,3 +398,39 @@ def test_two_pass_backward_bit_identical(H, d):
     assert nv > 0
     ca.close()
     cb.close()
+
+
+@pytest.mark.parametrize("d", [0, 16, 5])
+def test_position_payload_localizer_bit_identical(H, d):
+    """Valued batches: the Localizer sorts packed (key | position) items and gathers each
+    occurrence's row and value by position (loc_pos=1, a measured A/B kwarg) against the
+    16-byte (key, {pos, row}) items (loc_pos=0, the default): the same occurrence order, so predictions, progress
+    and the model are bit-identical; ragged rows, a count-push step, C2's shape at d = 0"""
+    cfg = dict(V_dim=d, lr=.1, V_lr=.02, l1=.5, V_threshold=1) if d else dict(V_dim=0, lr=.1, l1=1)
+    ca = H.Context(0, max_keys=1 << 17, loc_pos=1, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, **cfg)
+    blocks = []
+    for step in range(4):
+        blk = D.synthetic(5000, 40, 1 << 16, binary=False, ragged=(step == 1), seed=90 + step)
+        blocks.append(blk)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step == 0, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step == 0, pred=pb)
+        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
+        a, b = H.progress(ca), H.progress(cb)
+        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
+    ca.sync()
+    cb.sync()
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0] for b in blocks]))
+    for k in keys[::5]:
+        ea, eb = H.Store(ca).entry(k), H.Store(cb).entry(k)
+        assert (ea is None) == (eb is None)
+        if ea is not None:
+            assert np.array_equal(ea[0], eb[0]), k
+            assert (ea[1] is None) == (eb[1] is None)
+            if ea[1] is not None:
+                assert np.array_equal(ea[1], eb[1]), k
+    ca.close()
+    cb.close()
