@@ -91,6 +91,9 @@ struct Kw {
   // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
   // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
   int loc_pos = 0;
+  // loc_xpay=0: valued 16-byte items carry the position and the write pass gathers the value
+  // (A/B; 1: the value's bits ride in the payload, read by the transform in input order)
+  int loc_xpay = 1;
   // lane_cus=<n>: the Localizer and AUC lanes on n CUs only (a CU-masked stream; lane_cu_stride=1
   // every (CUs / n)-th CU, else the highest n); main_excl=1: the main stream on the other CUs
   // (the context's own stream, kept by dfx_ctx_set_stream).  A/B of the lanes' interference.
@@ -176,6 +179,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
     else if (k == "loc_pos") kw->loc_pos = atoi(cv) != 0;
+    else if (k == "loc_xpay") kw->loc_xpay = atoi(cv) != 0;
     else if (k == "lane_cus") kw->lane_cus = atoi(cv);
     else if (k == "lane_cu_stride") kw->lane_cu_stride = atoi(cv);
     else if (k == "main_excl") kw->main_excl = atoi(cv);
@@ -349,6 +353,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
   c->loc_pos_payload = kw.loc_pos;
+  c->loc_x_payload = kw.loc_xpay;
   c->lane_cus = kw.lane_cus;
   c->lane_cu_stride = kw.lane_cu_stride;
   c->main_excl = kw.main_excl;

@@ -203,6 +203,7 @@ struct Context {
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int loc_pos_payload = 0;  // kwarg loc_pos: valued data sorts packed (key | position) items
+  int loc_x_payload = 1;    // kwarg loc_xpay: valued data carries x, not the position
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes

@@ -38,6 +38,9 @@ struct TransformArgs {
   // valued data, narrow payload: pay32 carries the position (the value gather needs it) and
   // row_of[pos] the row
   uint32_t* row_of;
+  // valued data, 8-byte payload, no col: the payload's low word is the value's bits (read here,
+  // coalesced) instead of the position, so the write pass gathers nothing
+  const float* value;
 };
 
 __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
@@ -83,8 +86,10 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
       stnt(a.row_of + j, (uint32_t)(r0 + lo), a.nt != 0);
     } else if (a.pay32)
       stnt(a.pay32 + j, (uint32_t)(r0 + lo), a.nt != 0);
-    else
-      stnt(a.pay + j, (uint64_t)(uint32_t)j | ((uint64_t)(uint32_t)(r0 + lo) << 32), a.nt != 0);
+    else {
+      const uint32_t lo32 = a.value ? __float_as_uint(ldnt(a.value + j, a.nt != 0)) : (uint32_t)j;
+      stnt(a.pay + j, (uint64_t)lo32 | ((uint64_t)(uint32_t)(r0 + lo) << 32), a.nt != 0);
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     vor |= __shfl_xor(vor, off, kWave);
@@ -137,6 +142,7 @@ struct LocWriteArgs {
   float* occ_x;
   // narrow payload holding positions (valued data): occ_row = row_of[pos], occ_x = value[pos]
   const uint32_t* row_of;
+  int x_in_pay;  // the 8-byte payload's low word is the value's bits (TransformArgs::value)
 };
 
 __device__ inline unsigned long long hw_word(uint32_t tag, uint32_t flag, uint32_t v) {
@@ -339,7 +345,8 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
         } else {
           const uint64_t p = P[idx];
           a.occ_row[idx] = (uint32_t)(p >> 32);
-          if (a.occ_x) a.occ_x[idx] = a.value[(uint32_t)p];
+          if (a.occ_x)
+            a.occ_x[idx] = a.x_in_pay ? __uint_as_float((uint32_t)p) : a.value[(uint32_t)p];
         }
       }
     }
@@ -637,6 +644,10 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   t.keys_ready = o.keys_ready ? 1 : 0;
   t.nt = (c->nt_mask & kNtLane) ? 1 : 0;
   t.row_of = row_of;
+  // valued occurrences without col (the fused step, the split owner): the value rides in the
+  // payload in place of the position (kwarg loc_xpay=0: the position, and a gather)
+  const bool x_pay = !narrow && !o.col && o.value && o.occ_row && o.occ_x && c->loc_x_payload;
+  t.value = x_pay ? o.value : nullptr;
   hipLaunchKernelGGL(k_loc_transform, dim3((unsigned)((B + kLocRows - 1) / kLocRows)),
                      dim3(kLocNT), 0, L.stream, t);
   // the varying bits are OR ^ AND of the keys; the transform already counted the digits
@@ -701,6 +712,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
   a.row_of = row_of;
+  a.x_in_pay = x_pay ? 1 : 0;
   hipLaunchKernelGGL(k_loc_write, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, a);
   if (o.cnt) {
     hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, L.stream, ds, segs,

@@ -434,3 +434,27 @@ def test_position_payload_localizer_bit_identical(H, d):
                 assert np.array_equal(ea[1], eb[1]), k
     ca.close()
     cb.close()
+
+
+@pytest.mark.parametrize("d", [0, 5])
+def test_value_payload_localizer_bit_identical(H, d):
+    """Valued batches: the Localizer's 16-byte items carry each occurrence's value bits (the
+    default, loc_xpay=1) against its position with the value gathered by the write pass
+    (loc_xpay=0): predictions, progress and the model bit-identical; ragged rows, a count push"""
+    cfg = dict(V_dim=d, lr=.1, V_lr=.02, l1=.5, V_threshold=1) if d else dict(V_dim=0, lr=.1, l1=1)
+    ca = H.Context(0, max_keys=1 << 17, loc_xpay=0, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, **cfg)
+    for step in range(4):
+        blk = D.synthetic(5000, 40, 1 << 16, binary=False, ragged=(step == 1), seed=190 + step)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step == 0, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step == 0, pred=pb)
+        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
+        a, b = H.progress(ca), H.progress(cb)
+        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
+    ca.sync()
+    cb.sync()
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    ca.close()
+    cb.close()
