@@ -94,6 +94,10 @@ struct Kw {
   // loc_xpay=0: valued 16-byte items carry the position and the write pass gathers the value
   // (A/B; 1: the value's bits ride in the payload, read by the transform in input order)
   int loc_xpay = 1;
+  // sort_hint=1: the Localizer sort's passes beyond the previous sort's active count on a
+  // 64-block looping grid (sort.hip kSortHint; bit-identical).  A/B: C3 lane 0.83 -> 0.63 ms but
+  // the backward 0.50 -> 0.55, 125.8 -> 124.4 M ex/s; C2 a tie — so off by default
+  int sort_hint = 0;
   // lane_cus=<n>: the Localizer and AUC lanes on n CUs only (a CU-masked stream; lane_cu_stride=1
   // every (CUs / n)-th CU, else the highest n); main_excl=1: the main stream on the other CUs
   // (the context's own stream, kept by dfx_ctx_set_stream).  A/B of the lanes' interference.
@@ -180,6 +184,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
     else if (k == "loc_pos") kw->loc_pos = atoi(cv) != 0;
     else if (k == "loc_xpay") kw->loc_xpay = atoi(cv) != 0;
+    else if (k == "sort_hint") kw->sort_hint = atoi(cv) != 0;
     else if (k == "lane_cus") kw->lane_cus = atoi(cv);
     else if (k == "lane_cu_stride") kw->lane_cu_stride = atoi(cv);
     else if (k == "main_excl") kw->main_excl = atoi(cv);
@@ -256,6 +261,8 @@ static void release_ws(Workspace& w) {
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
                     &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.rowtmp2};
   for (DevBuf* b : bufs) b->release();
+  if (w.os_hint) (void)hipHostFree(w.os_hint);
+  w.os_hint = nullptr;
 }
 
 // streams, events and lane states of the fused step's pipeline, created on first use
@@ -354,6 +361,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->bwd_two_pass = kw.bwd_two_pass;
   c->loc_pos_payload = kw.loc_pos;
   c->loc_x_payload = kw.loc_xpay;
+  c->sort_hint = kw.sort_hint;
   c->lane_cus = kw.lane_cus;
   c->lane_cu_stride = kw.lane_cu_stride;
   c->main_excl = kw.main_excl;

@@ -99,6 +99,10 @@ struct Workspace {
   // look-back words [tiles][256] (u64)
   DevBuf os;
   int64_t os_tiles = 0;
+  // per item type (u64/u32, u64/u64, u32/u32) the active pass count of the last sort's plan,
+  // written by the device into pinned memory (kSortHint)
+  unsigned int* os_hint = nullptr;
+  int os_hint_reserve();
   // grows the radix sort's counters / look-back words; fresh ones are zeroed on st, the
   // stream whose sorts use them (stream order, no host wait)
   int os_reserve(int64_t ntiles, hipStream_t st);
@@ -204,6 +208,7 @@ struct Context {
   int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int loc_pos_payload = 0;  // kwarg loc_pos: valued data sorts packed (key | position) items
   int loc_x_payload = 1;    // kwarg loc_xpay: valued data carries x, not the position
+  int sort_hint = 0;        // kwarg sort_hint: the Localizer sort's kSortHint
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
@@ -295,6 +300,8 @@ constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
 constexpr int kSortBucket = 4;
 // flags |= kSortNT: the scatter passes load and store their items with the streaming policy
 constexpr int kSortNT = 8;
+// flags |= kSortHint: passes beyond the previous sort's active count run on a small looping grid
+constexpr int kSortHint = 16;
 constexpr uint32_t kSortBucketMax = 1u << 18;
 constexpr int kSortMetaRest = 28, kSortMetaBucket = 30;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }

@@ -665,14 +665,16 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0) |
                                                       (c->loc_bucket && !narrow_pos ? kSortBucket
                                                                                     : 0) |
-                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0) |
+                                                      (c->sort_hint ? kSortHint : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
-                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0) |
+                                                      (c->sort_hint ? kSortHint : 0))));
   }
   // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
   // k_loc_write with look-back; in bucket mode (the plan's choice) k_loc_bucket does it per

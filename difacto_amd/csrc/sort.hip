@@ -35,6 +35,7 @@ static_assert(kOsTile <= 4096, "rank packing below assumes < 2^12 items per wave
 constexpr int kOsMaxPasses = kOsDigits;
 constexpr int kOsLookback = 4;  // predecessor words read per look-back step (default)
 constexpr unsigned kOsNone = 0xFFFFFFFFu;
+constexpr int64_t kOsLoopGrid = 64;  // blocks of a pass expected to be constant (kSortHint)
 // sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
 // The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
@@ -62,7 +63,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
                                                    int npasses, int begin_bit, int end_bit,
                                                    unsigned int* meta, uint32_t* parts,
                                                    uint32_t* counts, unsigned int* epoch,
-                                                   int pack_rb8, uint32_t bucket_max) {
+                                                   int pack_rb8, uint32_t bucket_max,
+                                                   unsigned int* host_nq) {
   __shared__ int s_pos[kOsMaxPasses];
   __shared__ int s_nq;
   __shared__ uint32_t s_max;
@@ -101,6 +103,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
                                       : 0u;
     meta[31] = (unsigned)(q & 1);
     meta[kSortMetaBucket] = 0;
+    if (host_nq) *host_nq = (unsigned)q;  // the next sort's launch hint (pinned, vector store)
     s_nq = q;
     s_max = 0;
   }
@@ -133,6 +136,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
     for (int r = 1; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
     meta[31] = 1u;
     meta[kSortMetaBucket] = 1u | ((unsigned)(nq - 1) << 8);
+    if (host_nq) *host_nq = 1u;
   }
 }
 
@@ -211,12 +215,18 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   const int t = threadIdx.x;
   const int w = t / kWave;
   const int l = lane_id();
+  const int64_t n = os_count(n0, n_dev);
+  // a grid smaller than the tile count (a pass the host expects to find constant, below) takes
+  // tiles until they run out: tickets are taken in order and a block takes its next one only
+  // after publishing its tile, so every tile a block looks back on is done or held by a
+  // running block
+  const bool looping = (int64_t)gridDim.x * (kOsNT * IT) < n;
+  for (;;) {
   if (t == 0) s_tile = (int64_t)atomicAdd(&meta[kMetaTile + q], 1u);
 #pragma unroll
   for (int i = 0; i < kOsWaves; ++i) wcnt[i][t] = 0;
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t n = os_count(n0, n_dev);
   const int64_t tbase = tile * (kOsNT * IT);
   if (tbase >= n) return;  // every later tile exits too: no waiter is left behind
 
@@ -336,23 +346,35 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
       stnt(kout + gdig[d] + ((uint32_t)qi - lstart[d]), kk, nt != 0);
     }
   }
-  if (packed) return;  // the payload rides in the key
-  __syncthreads();
-  // ---- payloads: the same permutation through the same LDS buffer
+  if (!packed) {  // else the payload rides in the key
+    __syncthreads();
+    // ---- payloads: the same permutation through the same LDS buffer
 #pragma unroll
-  for (int c = 0; c < IT; ++c) {
-    const int64_t idx = wbase + c * kWave + l;
-    if (idx < n) lv[dr[c]] = ldnt(vin + idx, nt != 0);
-  }
-  __syncthreads();
+    for (int c = 0; c < IT; ++c) {
+      const int64_t idx = wbase + c * kWave + l;
+      if (idx < n) lv[dr[c]] = ldnt(vin + idx, nt != 0);
+    }
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int qi = i * kOsNT + t;
-    if (qi < nvalid) {
-      const uint32_t d = ldig[qi];
-      stnt(vout + gdig[d] + ((uint32_t)qi - lstart[d]), lv[qi], nt != 0);
+    for (int i = 0; i < IT; ++i) {
+      const int qi = i * kOsNT + t;
+      if (qi < nvalid) {
+        const uint32_t d = ldig[qi];
+        stnt(vout + gdig[d] + ((uint32_t)qi - lstart[d]), lv[qi], nt != 0);
+      }
     }
   }
+  if (!looping) return;
+  __syncthreads();  // the tile's LDS is read out before the next ticket reuses it
+  }
+}
+
+int Workspace::os_hint_reserve() {
+  if (os_hint) return DFX_OK;
+  DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&os_hint), 4 * sizeof(unsigned int),
+                        hipHostMallocDefault));
+  for (int i = 0; i < 4; ++i) os_hint[i] = kOsNone;  // unknown: every pass on a full grid
+  return DFX_OK;
 }
 
 int Workspace::os_reserve(int64_t ntiles, hipStream_t st) {
@@ -395,7 +417,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   const int pack_rb8 = (sizeof(K) == 8 && sizeof(P) == 4) ? (flags >> 8) & 0xFF : 0;
   if (n <= 0 || end_bit <= begin_bit) {
     hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, 0,
-                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0, 0u);
+                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0, 0u, nullptr);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
@@ -406,12 +428,28 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                        0, L.stream, k0, n, n_dev, begin_bit, npasses, parts);
   }
   const uint32_t bucket_max = (flags & kSortBucket) && pack_rb8 > 0 ? kSortBucketMax : 0u;
+  // kSortHint: the passes beyond the active count of this workspace's previous sort of the same
+  // item type (k_os_plan writes it to pinned memory; read here without a wait, so it may be a
+  // step old) run on a small looping grid: they are almost always constant digits, whose
+  // full-grid launches only queue for CU slots behind the other streams to find nothing to do.
+  // A wrong hint costs time, never correctness.
+  const int site = sizeof(K) == 8 ? (sizeof(P) == 8 ? 1 : 0) : 2;
+  unsigned int* host_nq = nullptr;
+  int hint = npasses;
+  if (flags & kSortHint) {
+    DFX_TRY(ws.os_hint_reserve());
+    host_nq = ws.os_hint + site;
+    const unsigned h = __atomic_load_n(host_nq, __ATOMIC_RELAXED);
+    if (h <= (unsigned)npasses) hint = (int)h;
+  }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
-                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8, bucket_max);
+                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8, bucket_max,
+                     host_nq);
   for (int q = 0; q < npasses; ++q) {
+    const int64_t grid = q < hint ? ntiles : std::min<int64_t>(ntiles, kOsLoopGrid);
 #define DFX_OS_SCATTER(IT, LB)                                                               \
     if (it == IT && lb == LB)                                                                \
-      hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)ntiles), dim3(kOsNT), 0, \
+      hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)grid), dim3(kOsNT), 0,   \
                          L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status,     \
                          L.err, (flags & kSortNT) ? 1 : 0);
     DFX_OS_SCATTER(8, 4)

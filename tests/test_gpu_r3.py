@@ -458,3 +458,30 @@ def test_value_payload_localizer_bit_identical(H, d):
     assert H.Store(ca).stats() == H.Store(cb).stats()
     ca.close()
     cb.close()
+
+
+@pytest.mark.parametrize("binary", [True, False])
+def test_sort_hint_wrong_hint_bit_identical(H, binary):
+    """kSortHint runs the Localizer sort's passes beyond the previous sort's active count on a
+    64-block looping grid.  A batch over 2^8 ids (one varying digit) sets the hint to 1; the
+    next batches, over 2^40 ids (five varying digits, 420 k nnz: 103 tiles > 64 blocks), then
+    sort four real passes on the looping grid and back: predictions, progress and the model
+    bit-identical to sort_hint=0 (every pass on a full grid)"""
+    cfg = dict(V_dim=4, lr=.1, V_lr=.02, l1=.5, V_threshold=1)
+    ca = H.Context(0, max_keys=1 << 20, sort_hint=0, **cfg)
+    cb = H.Context(0, max_keys=1 << 20, sort_hint=1, **cfg)
+    spaces = [1 << 8, 1 << 40, 1 << 40, 1 << 8, 1 << 40]
+    for step, ks in enumerate(spaces):
+        blk = D.synthetic(10500, 40, ks, binary=binary, ragged=(step == 2), seed=290 + step)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step < 2, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step < 2, pred=pb)
+        ca.sync()
+        cb.sync()  # the hint of the next step is this step's plan
+        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
+        a, b = H.progress(ca), H.progress(cb)
+        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    ca.close()
+    cb.close()
