@@ -88,6 +88,10 @@ struct Kw {
   // bwd_two_pass=1: the wide-V_dim (>= 32 lanes per key) fused backward in two passes (fm.hip
   // k_fm_bwd_w / _v, bit-identical; A/B: C5 50.4 -> 43.2 M ex/s, so off by default)
   int bwd_two_pass = 0;
+  // bwd_cpl=8: the fused backward at V_dim >= 64 with 8 coordinates per lane (half the lanes
+  // per key: G = d / 8), bit-identical (every coordinate's terms and order are a lane's own);
+  // 4: one float4 per lane (d / 4 lanes per key, capped at 64)
+  int bwd_cpl = 8;
   // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
   // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
   int loc_pos = 0;
@@ -182,6 +186,13 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       }
     }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
+    else if (k == "bwd_cpl") {
+      kw->bwd_cpl = atoi(cv);
+      if (kw->bwd_cpl != 4 && kw->bwd_cpl != 8) {
+        set_error("bwd_cpl must be 4 or 8");
+        return DFX_ERR_ARG;
+      }
+    }
     else if (k == "loc_pos") kw->loc_pos = atoi(cv) != 0;
     else if (k == "loc_xpay") kw->loc_xpay = atoi(cv) != 0;
     else if (k == "sort_hint") kw->sort_hint = atoi(cv) != 0;
@@ -359,6 +370,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_nb = kw.fat_nb;
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
+  c->bwd_cpl = kw.bwd_cpl;
   c->loc_pos_payload = kw.loc_pos;
   c->loc_x_payload = kw.loc_xpay;
   c->sort_hint = kw.sort_hint;

@@ -963,10 +963,19 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       for (int k = 0; k < CPL; ++k) ccur[k] = 0.f;
     }
     float pr[UNR], xr[UNR][CPL];
+    // A key without V (lazy V: most keys of a Zipf batch) needs only p of its rows, not their
+    // XV*p.  Outside fat slots vq is known here from the entry the V / Vaux loads above already
+    // waited for, so the condition adds no memory round trip and saves d floats per occurrence
+    // of such a key; with fat slots (kernel-uniform) V came with the entry and the rows load
+    // beside it, unconditionally, as before.
+    const bool xv_spec = !FUSED || (a.T.es && !a.no_fat_spec);
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
       pr[t] = xs > d ? a.XVp[(int64_t)row[t] * xs + d] : a.p[row[t]];
-      load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)row[t] * xs : zp, l, d, xr[t]);
+      if (xv_spec)
+        load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)row[t] * xs : zp, l, d, xr[t]);
+      else
+        load_coords<CPL, VEC>(d > 0 && vq >= 0 ? a.XVp + (int64_t)row[t] * xs : zp, l, d, xr[t]);
     }
     float xxp = 0.f;
     float acc[CPL];
@@ -1028,18 +1037,30 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         for (int k = 0; k < CPL; ++k) acc[k] = (float)((double)(g0[k] - vcur[k] * xxp) + accp[k]);
       }
     } else {
-      for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
-        uint32_t rw[UNR];
-        float xw[UNR], pw[UNR];
+      // Both walks keep the next trip's rows in flight beside this trip's row reads (the
+      // segment's occ_row / occ_x are contiguous; the p / XV*p reads are the random ones), so a
+      // trip costs one memory round trip instead of two.  Same terms, same order.
+      uint32_t rw[UNR];
+      float xw[UNR];
 #pragma unroll
-        for (int t = 0; t < UNR; ++t) {
-          const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-          rw[t] = a.occ_row[i];
-          xw[t] = valued ? a.occ_x[i] : 1.f;
-        }
+      for (int t = 0; t < UNR; ++t) {  // the first trip's rows: already loaded (level 2)
+        rw[t] = row[t];
+        xw[t] = x[t];
+      }
+      for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+        float pw[UNR];
 #pragma unroll
         for (int t = 0; t < UNR; ++t)
           pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+        const uint32_t in = i0 + UNR;
+        uint32_t rn[UNR];
+        float xn[UNR];
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          const uint32_t i = in + t < s1 ? in + t : s1 - 1;
+          rn[t] = in < s1 ? a.occ_row[i] : 0u;
+          xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
+        }
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
           if (i0 + t < s1 && pw[t] != 0.f) {
@@ -1052,22 +1073,35 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
             }
           }
         }
+#pragma unroll
+        for (int t = 0; t < UNR; ++t) {
+          rw[t] = rn[t];
+          xw[t] = xn[t];
+        }
       }
       if (vq >= 0) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
-        for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
-          uint32_t rw[UNR];
-          float xw[UNR], xrw[UNR][CPL];
 #pragma unroll
-          for (int t = 0; t < UNR; ++t) {
-            const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-            rw[t] = a.occ_row[i];
-            xw[t] = valued ? a.occ_x[i] : 1.f;
-          }
+        for (int t = 0; t < UNR; ++t) {
+          rw[t] = row[t];
+          xw[t] = x[t];
+        }
+        for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+          float xrw[UNR][CPL];
 #pragma unroll
           for (int t = 0; t < UNR; ++t)
             load_coords<CPL, VEC>(a.XVp + (int64_t)rw[t] * xs, l, d, xrw[t]);
+          // the next trip's rows, in flight beside this trip's XV*p rows
+          const uint32_t in = i0 + UNR;
+          uint32_t rn[UNR];
+          float xn[UNR];
+#pragma unroll
+          for (int t = 0; t < UNR; ++t) {
+            const uint32_t i = in + t < s1 ? in + t : s1 - 1;
+            rn[t] = in < s1 ? a.occ_row[i] : 0u;
+            xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
+          }
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
             if (i0 + t < s1) {
@@ -1075,6 +1109,11 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
               for (int k = 0; k < CPL; ++k)
                 acc[k] = valued ? acc[k] + xrw[t][k] * xw[t] : acc[k] + xrw[t][k];
             }
+          }
+#pragma unroll
+          for (int t = 0; t < UNR; ++t) {
+            rw[t] = rn[t];
+            xw[t] = xn[t];
           }
         }
       }
@@ -1477,6 +1516,19 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
 // random-line traffic).  The context kwarg bwd_lds overrides (bytes, 0 = no cap).
 constexpr size_t kBwdLdsCap = 32768;
 
+// Lane layout of a fused backward.  kwarg bwd_cpl = 8 at V_dim >= 64 (float4-aligned rows):
+// two float4 per lane, half the lanes per key — a key's walk (entry, rows, update) is latency
+// bound, and the keys of a batch that carry no V (lazy V) keep only lane 0 busy, so fewer lanes
+// per key are more keys in flight per wave.  Every coordinate's terms stay one lane's, in the
+// same order: bit-identical to the 4-per-lane layout.
+static void bwd_lanes(const BwdArgs& a, bool aligned, int* G, int* CPL, bool* vec) {
+  lanes_for(a.d, aligned, G, CPL, vec);
+  if (a.cpl == 8 && *vec && *CPL == 4 && *G >= 16 && a.d % 8 == 0 && a.d <= 512) {
+    *G /= 2;
+    *CPL = 8;
+  }
+}
+
 template <bool FUSED>
 int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligned = FUSED,
                long lds = -1) {
@@ -1484,7 +1536,7 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;
   bool vec;
-  lanes_for(a.d, aligned, &G, &CPL, &vec);
+  bwd_lanes(a, aligned, &G, &CPL, &vec);
   const int64_t spb = kFmNT / G;
   dim3 grid((unsigned)((nseg_bound + spb - 1) / spb));
 #define DFX_BWD(GG, CC, VV)                                                              \
@@ -1495,6 +1547,7 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   }
   DFX_SCALAR_SET(DFX_BWD)
   DFX_VEC_SET(DFX_BWD)
+  if constexpr (FUSED) { DFX_BWD(8, 8, true) DFX_BWD(16, 8, true) DFX_BWD(32, 8, true) DFX_BWD(64, 8, true) }
 #undef DFX_BWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -1546,11 +1599,14 @@ int bwd_two_pass_reserve(Context* c, Workspace& ws, int64_t nseg_bound, BwdArgs*
 }
 
 // blocks of the fused backward over nseg_bound keys (the size of BwdArgs::live_part)
-int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass) {
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass, int cpl) {
   if (two_pass) return std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);
   int G, CPL;
   bool vec;
-  lanes_for(d, true, &G, &CPL, &vec);
+  BwdArgs a{};
+  a.d = d;
+  a.cpl = cpl;
+  bwd_lanes(a, true, &G, &CPL, &vec);
   const int64_t spb = kFmNT / G;
   return (nseg_bound + spb - 1) / spb;
 }

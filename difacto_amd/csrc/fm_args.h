@@ -89,6 +89,7 @@ __host__ __device__ inline int split_pxv_floats(int d, int wide = 0) {
 struct BwdArgs {
   int no_fat_spec;           // fat slots: no V / Vaux loads beside the home entry (A/B)
   int nt;                    // kwarg nt: kNtBwdTable / kNtBwdOcc with the streaming policy
+  int cpl;                   // kwarg bwd_cpl (fused launches; 0 = 4)
   const uint32_t* segstart;  // nseg+1
   const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
   int64_t nseg_host;
@@ -143,7 +144,7 @@ int xvp_stride(const Context* c);
 int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread = true);
 // fused backward + FTRL/AdaGrad update over at most nseg_bound segments; lds: bytes of LDS
 // reserved per block (-1: the default cap)
-int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass = false);
+int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass, int cpl);
 // V_dim whose fused backward may run in two passes (>= 32 lanes per key)
 bool bwd_two_pass(int d);
 // the two-pass backward's list for nseg_bound keys, when the context runs it (else vlist NULL)

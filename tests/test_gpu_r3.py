@@ -400,6 +400,53 @@ def test_two_pass_backward_bit_identical(H, d):
     cb.close()
 
 
+@pytest.mark.parametrize("d,zipf,binary", [(64, 1.1, True), (128, 1.1, True), (200, 1.1, False),
+                                            (64, None, False), (72, None, True)])
+def test_backward_eight_coords_per_lane_bit_identical(H, d, zipf, binary):
+    """The fused backward at V_dim >= 64 with 8 coordinates per lane (kwarg bwd_cpl=8, the
+    default: half the lanes per key) against 4 per lane (bwd_cpl=4): each coordinate's terms
+    are one lane's in the same order, so predictions, progress and the model are bit-identical.
+    Zipf keys with lazy V (cold V-less keys, chunked hot keys) and a small uniform key space
+    with every key carrying V (segments walked over several trips); binary and valued data;
+    V_dim 72 takes 16 lanes of 8 over a 128-float lane span."""
+    vt = 4 if zipf else 0
+    cfg = dict(V_dim=d, lr=.05, V_lr=.01, V_threshold=vt, l1=1 if zipf else 0)
+    ca = H.Context(0, max_keys=1 << 17, bwd_cpl=4, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, **cfg)
+    blocks = []
+    for step in range(5):
+        if zipf:
+            blk = D.synthetic(3000, 39, 1 << 18, zipf=zipf, seed=700 + step, binary=binary)
+        else:
+            blk = D.synthetic(3000, 20, 1 << 10, seed=700 + step, binary=binary, ragged=True)
+        blocks.append(blk)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step < 2, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step < 2, pred=pb)
+        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
+        a, b = H.progress(ca), H.progress(cb)
+        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
+    ca.sync()
+    cb.sync()
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0] for b in blocks]))
+    nv = 0
+    for k in keys[::3]:
+        ea, eb = H.Store(ca).entry(k), H.Store(cb).entry(k)
+        assert (ea is None) == (eb is None)
+        if ea is None:
+            continue
+        assert np.array_equal(ea[0], eb[0]), k
+        assert (ea[1] is None) == (eb[1] is None)
+        if ea[1] is not None:
+            nv += 1
+            assert np.array_equal(ea[1], eb[1]), k
+    assert nv > 0
+    ca.close()
+    cb.close()
+
+
 @pytest.mark.parametrize("d", [0, 16, 5])
 def test_position_payload_localizer_bit_identical(H, d):
     """Valued batches: the Localizer sorts packed (key | position) items and gathers each
