@@ -92,6 +92,7 @@ struct Kw {
   // per key: G = d / 8), bit-identical (every coordinate's terms and order are a lane's own);
   // 4: one float4 per lane (d / 4 lanes per key, capped at 64)
   int bwd_cpl = 8;
+  int bwd_cpl_from = 64;  // bwd_cpl_from=<V_dim>: the least V_dim (multiple of 8) bwd_cpl=8 takes
   // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
   // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
   int loc_pos = 0;
@@ -186,10 +187,11 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       }
     }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
+    else if (k == "bwd_cpl_from") kw->bwd_cpl_from = atoi(cv);
     else if (k == "bwd_cpl") {
       kw->bwd_cpl = atoi(cv);
-      if (kw->bwd_cpl != 4 && kw->bwd_cpl != 8) {
-        set_error("bwd_cpl must be 4 or 8");
+      if (kw->bwd_cpl != 4 && kw->bwd_cpl != 8 && kw->bwd_cpl != 16) {
+        set_error("bwd_cpl must be 4, 8 or 16");
         return DFX_ERR_ARG;
       }
     }
@@ -371,6 +373,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
   c->bwd_cpl = kw.bwd_cpl;
+  c->bwd_cpl_from = kw.bwd_cpl_from;
   c->loc_pos_payload = kw.loc_pos;
   c->loc_x_payload = kw.loc_xpay;
   c->sort_hint = kw.sort_hint;

@@ -1523,9 +1523,15 @@ constexpr size_t kBwdLdsCap = 32768;
 // same order: bit-identical to the 4-per-lane layout.
 static void bwd_lanes(const BwdArgs& a, bool aligned, int* G, int* CPL, bool* vec) {
   lanes_for(a.d, aligned, G, CPL, vec);
-  if (a.cpl == 8 && *vec && *CPL == 4 && *G >= 16 && a.d % 8 == 0 && a.d <= 512) {
-    *G /= 2;
-    *CPL = 8;
+  const int from = a.cpl_from > 0 ? a.cpl_from : 64;
+  if (!(*vec && *CPL == 4 && a.d >= from && a.d <= 512)) return;
+  for (int c = a.cpl; c >= 8; c /= 2) {  // 16 -> 8 when d is not a multiple of 16
+    const int g = *G * 4 / c;
+    if (g >= 2 && a.d % c == 0) {
+      *G = g;
+      *CPL = c;
+      return;
+    }
   }
 }
 
@@ -1547,7 +1553,11 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
   }
   DFX_SCALAR_SET(DFX_BWD)
   DFX_VEC_SET(DFX_BWD)
-  if constexpr (FUSED) { DFX_BWD(8, 8, true) DFX_BWD(16, 8, true) DFX_BWD(32, 8, true) DFX_BWD(64, 8, true) }
+  if constexpr (FUSED) {
+    DFX_BWD(2, 8, true) DFX_BWD(4, 8, true) DFX_BWD(8, 8, true) DFX_BWD(16, 8, true)
+    DFX_BWD(32, 8, true) DFX_BWD(64, 8, true)
+    DFX_BWD(4, 16, true) DFX_BWD(8, 16, true) DFX_BWD(16, 16, true)
+  }
 #undef DFX_BWD
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -1605,7 +1615,8 @@ int64_t bwd_fused_blocks(int d, int64_t nseg_bound, bool two_pass, int cpl) {
   bool vec;
   BwdArgs a{};
   a.d = d;
-  a.cpl = cpl;
+  a.cpl = cpl & 0xFF;
+  a.cpl_from = cpl >> 8;
   bwd_lanes(a, true, &G, &CPL, &vec);
   const int64_t spb = kFmNT / G;
   return (nseg_bound + spb - 1) / spb;

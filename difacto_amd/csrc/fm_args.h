@@ -90,6 +90,7 @@ struct BwdArgs {
   int no_fat_spec;           // fat slots: no V / Vaux loads beside the home entry (A/B)
   int nt;                    // kwarg nt: kNtBwdTable / kNtBwdOcc with the streaming policy
   int cpl;                   // kwarg bwd_cpl (fused launches; 0 = 4)
+  int cpl_from;              // kwarg bwd_cpl_from: the least V_dim bwd_cpl applies to (0 = 64)
   const uint32_t* segstart;  // nseg+1
   const DevState* ds;        // nseg = ds->u_count when nseg_host < 0
   int64_t nseg_host;

@@ -621,7 +621,7 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.occ_row = ows.occ_row.as<uint32_t>();
     g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d, c->xvp_row); g.d = d;
-    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl;
+    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from;
     g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
     g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();

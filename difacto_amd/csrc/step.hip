@@ -346,14 +346,14 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
-    g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.nt = c->nt_mask;
+    g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from; g.nt = c->nt_mask;
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
     // (diagnostic, dfx_prof_enable_marks bit 9) the live-V key / occurrence counts
     const bool count_live = c->prof_n < c->prof_max && (c->prof_mask >> 9 & 1u);
     DFX_TRY(bwd_two_pass_reserve(c, ws, nnz, &g));
-    const int64_t nbb = bwd_fused_blocks(d, nnz, g.vlist != nullptr, g.cpl);
+    const int64_t nbb = bwd_fused_blocks(d, nnz, g.vlist != nullptr, g.cpl | g.cpl_from << 8);
     if (count_live) {
       DFX_TRY(ws.live.ensure((size_t)nbb * sizeof(uint2)));
       g.live_part = ws.live.as<uint2>();

@@ -99,7 +99,7 @@ def test_workspace_growth_then_lane_localize(H):
 
 def test_bad_kwargs_rejected(H):
     from difacto_amd._lib import DfxError
-    for kw in (dict(fat_nb=5), dict(fwd_lanes=3), dict(diag="bogus")):
+    for kw in (dict(fat_nb=5), dict(fwd_lanes=3), dict(diag="bogus"), dict(bwd_cpl=32)):
         with pytest.raises(DfxError):
             H.Context(0, V_dim=16, **kw)
 
@@ -400,19 +400,23 @@ def test_two_pass_backward_bit_identical(H, d):
     cb.close()
 
 
-@pytest.mark.parametrize("d,zipf,binary", [(64, 1.1, True), (128, 1.1, True), (200, 1.1, False),
-                                            (64, None, False), (72, None, True)])
-def test_backward_eight_coords_per_lane_bit_identical(H, d, zipf, binary):
+@pytest.mark.parametrize("d,zipf,binary,cpl", [
+    (64, 1.1, True, 8), (128, 1.1, True, 8), (200, 1.1, False, 8), (64, None, False, 8),
+    (72, None, True, 8), (16, None, True, 8), (16, 1.1, False, 8), (32, None, False, 8),
+    (128, 1.1, False, 16), (64, None, True, 16), (200, None, True, 16)])
+def test_backward_eight_coords_per_lane_bit_identical(H, d, zipf, binary, cpl):
     """The fused backward at V_dim >= 64 with 8 coordinates per lane (kwarg bwd_cpl=8, the
     default: half the lanes per key) against 4 per lane (bwd_cpl=4): each coordinate's terms
     are one lane's in the same order, so predictions, progress and the model are bit-identical.
     Zipf keys with lazy V (cold V-less keys, chunked hot keys) and a small uniform key space
     with every key carrying V (segments walked over several trips); binary and valued data;
-    V_dim 72 takes 16 lanes of 8 over a 128-float lane span."""
+    V_dim 72 takes 16 lanes of 8 over a 128-float lane span; V_dim 16 and 32 (kwarg
+    bwd_cpl_from, fat slots at 16) take 2 and 4 lanes; bwd_cpl=16 (V_dim 200: not a multiple
+    of 16, so 8)."""
     vt = 4 if zipf else 0
     cfg = dict(V_dim=d, lr=.05, V_lr=.01, V_threshold=vt, l1=1 if zipf else 0)
     ca = H.Context(0, max_keys=1 << 17, bwd_cpl=4, **cfg)
-    cb = H.Context(0, max_keys=1 << 17, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, bwd_cpl=cpl, bwd_cpl_from=min(d, 64), **cfg)
     blocks = []
     for step in range(5):
         if zipf:
