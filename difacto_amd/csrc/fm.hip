@@ -1036,6 +1036,65 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
         for (int k = 0; k < CPL; ++k) acc[k] = (float)((double)(g0[k] - vcur[k] * xxp) + accp[k]);
       }
+    } else if (G >= 8) {
+      // Wide groups (V_dim >= 64): the group walks G occurrences per trip — lane l reads
+      // occurrence i0 + l's row, value and p, so G of the random p reads are in flight at once
+      // — and the sums take the terms from the lanes by shuffles in occurrence order: the same
+      // terms in the same order as the per-lane walk below (bit-identical), G / UNR times fewer
+      // round trips on a skewed key's long segment.  The V sums then read WU XV*p rows per
+      // sub-trip, their row ids shuffled from the lanes that loaded them.
+      constexpr int WU = CPL <= 4 ? 4 : 2;
+      const int gb = (int)(threadIdx.x % kWave) - l;
+      for (uint32_t i0 = s0; i0 < s1; i0 += G) {
+        const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
+        const uint32_t rl = a.occ_row[i];
+        const float xl = valued ? a.occ_x[i] : 1.f;
+        const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
+        const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
+#pragma unroll
+        for (int t = 0; t < G; ++t) {
+          const float pt = __shfl(pl, gb + t, kWave);
+          const float xt = __shfl(xl, gb + t, kWave);
+          if ((uint32_t)t < n && pt != 0.f) {
+            if (valued) {
+              gw += pt * xt;
+              xxp += pt * (xt * xt);
+            } else {
+              gw += pt;
+              xxp += pt;
+            }
+          }
+        }
+      }
+      if (vq >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
+        for (uint32_t i0 = s0; i0 < s1; i0 += G) {
+          const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
+          const uint32_t rl = a.occ_row[i];
+          const float xl = valued ? a.occ_x[i] : 1.f;
+          const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
+#pragma unroll
+          for (int t0 = 0; t0 < G; t0 += WU) {
+            if ((uint32_t)t0 >= n) break;  // group-uniform: the segment's last trip
+            float xrw[WU][CPL], xw[WU];
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+              const uint32_t r = (uint32_t)__shfl((int)rl, gb + t0 + u, kWave);
+              xw[u] = __shfl(xl, gb + t0 + u, kWave);
+              load_coords<CPL, VEC>(a.XVp + (int64_t)r * xs, l, d, xrw[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < WU; ++u) {
+              if ((uint32_t)(t0 + u) < n) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k)
+                  acc[k] = valued ? acc[k] + xrw[u][k] * xw[u] : acc[k] + xrw[u][k];
+              }
+            }
+          }
+        }
+      }
     } else {
       // Both walks keep the next trip's rows in flight beside this trip's row reads (the
       // segment's occ_row / occ_x are contiguous; the p / XV*p reads are the random ones), so a
