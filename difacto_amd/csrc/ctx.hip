@@ -92,6 +92,9 @@ struct Kw {
   // per key: G = d / 8), bit-identical (every coordinate's terms and order are a lane's own);
   // 4: one float4 per lane (d / 4 lanes per key, capped at 64)
   int bwd_cpl = 8;
+  // fwd_cpl=8: the probe forward at V_dim >= 64 with two float4 of V per lane (bit-identical;
+  // same-box A/B: C5 63.5 -> 65.7 M ex/s, forward 0.30 -> 0.23 ms; C4 shard a tie); 4: one
+  int fwd_cpl = 8;
   int bwd_cpl_from = 64;  // bwd_cpl_from=<V_dim>: the least V_dim (multiple of 8) bwd_cpl=8 takes
   // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
   // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
@@ -188,6 +191,13 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
     else if (k == "bwd_cpl_from") kw->bwd_cpl_from = atoi(cv);
+    else if (k == "fwd_cpl") {
+      kw->fwd_cpl = atoi(cv);
+      if (kw->fwd_cpl != 4 && kw->fwd_cpl != 8) {
+        set_error("fwd_cpl must be 4 or 8");
+        return DFX_ERR_ARG;
+      }
+    }
     else if (k == "bwd_cpl") {
       kw->bwd_cpl = atoi(cv);
       if (kw->bwd_cpl != 4 && kw->bwd_cpl != 8 && kw->bwd_cpl != 16) {
@@ -374,6 +384,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->bwd_two_pass = kw.bwd_two_pass;
   c->bwd_cpl = kw.bwd_cpl;
   c->bwd_cpl_from = kw.bwd_cpl_from;
+  c->fwd_cpl = kw.fwd_cpl;
   c->loc_pos_payload = kw.loc_pos;
   c->loc_x_payload = kw.loc_xpay;
   c->sort_hint = kw.sort_hint;

@@ -312,12 +312,17 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 // key away from home, rare at load <= 0.5, walks its chain then).  Reading the slot's two
 // halves together keeps them one DRAM access; read a chain step apart, the entry's line was
 // often evicted before its V was read (the split walk above, applied to fat slots: 185 us).
-template <int G, bool FAT, int NB = 8>
+//
+// CPL = 8 (kwarg fwd_cpl, V_dim a multiple of 8, not FAT): two float4 of V per lane, half the
+// lanes per row; each coordinate's sums are still one lane's in nnz order and s is summed over
+// l = 0..d-1 in order, so predictions are bit-identical to CPL = 4.
+template <int G, bool FAT, int NB = 8, int CPL = 4>
 __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
+  static_assert(CPL == 4 || (CPL == 8 && !FAT), "fat slots: one float4 per lane");
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
   constexpr int MA = CH / G;      // lookups per lane per chunk
-  constexpr int VB = 8;           // V rows in flight per batch
+  constexpr int VB = CPL == 4 ? 8 : 4;  // V rows in flight per batch
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int gbase = (threadIdx.x % kWave) - l;
@@ -329,7 +334,9 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   if (ri < a.B) {
     const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = 0.f;
-    float xv[4] = {0.f, 0.f, 0.f, 0.f}, xxvv[4] = {0.f, 0.f, 0.f, 0.f};
+    float xv[CPL], xxvv[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
     const bool valued = a.val != nullptr;
     const bool ntf = (a.nt & kNtFwdTable) != 0;
     if constexpr (FAT) {
@@ -443,7 +450,7 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
         if (b * VB >= nin) break;
         float w[VB], x[VB];
         int vp[VB];
-        float4 v[VB];
+        float v[VB][CPL];
 #pragma unroll
         for (int t = 0; t < VB; ++t) {
           const int tt = b * VB + t;  // the chunk's nnz tt sits with lane tt % G, slot tt / G
@@ -454,8 +461,12 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
 #pragma unroll
         for (int t = 0; t < VB; ++t) {
           const float* Vr = vp[t] < 0 ? a.zpad + (((uint32_t)t & 255u) << 4) : row_V(a.T, vp[t]);
-          const int base = l * 4 < d ? l * 4 : 0;
-          v[t] = *reinterpret_cast<const float4*>(Vr + base);
+          const int base = l * CPL < d ? l * CPL : 0;
+#pragma unroll
+          for (int m = 0; m < CPL / 4; ++m) {
+            const float4 f = *reinterpret_cast<const float4*>(Vr + base + 4 * m);
+            v[t][4 * m] = f.x; v[t][4 * m + 1] = f.y; v[t][4 * m + 2] = f.z; v[t][4 * m + 3] = f.w;
+          }
         }
 #pragma unroll
         for (int t = 0; t < VB; ++t) {
@@ -464,9 +475,9 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
           if (w[t] != 0.f) acc = valued ? acc + w[t] * x[t] : acc + w[t];
           if (vp[t] >= 0) {
             const float xx = x[t] * x[t];  // XX_ (fm_loss.h:86-92)
-            const float vk[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
+            const float (&vk)[CPL] = v[t];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < CPL; ++k) {
               xv[k] = valued ? xv[k] + vk[k] * x[t] : xv[k] + vk[k];
               const float vv = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
               xxvv[k] = valued ? xxvv[k] + vv * xx : xxvv[k] + vv;
@@ -482,23 +493,30 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
         float sx = 0.f;
         for (int q = 0; q < G; ++q) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < CPL; ++k) {
             const float tk = __shfl(xxvv[k], gbase + q, kWave);
-            if (q * 4 + k < d) sx += tk;
+            if (q * CPL + k < d) sx += tk;
           }
         }
-        if (l * 4 < d)
-          *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+#pragma unroll
+        for (int m = 0; m < CPL / 4; ++m)
+          if (l * CPL + 4 * m < d)
+            *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
+                make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
         if (l == 0) {
           pr_row[d] = acc;
           pr_row[d + 1] = sx;
           pr_row[d + 2] = pr_row[d + 3] = 0.f;
         }
       } else {
-        if (l * 4 < d) {
-          *reinterpret_cast<float4*>(pr_row + l * 4) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-          *reinterpret_cast<float4*>(pr_row + d + l * 4) =
-              make_float4(xxvv[0], xxvv[1], xxvv[2], xxvv[3]);
+#pragma unroll
+        for (int m = 0; m < CPL / 4; ++m) {
+          if (l * CPL + 4 * m < d) {
+            *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
+                make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
+            *reinterpret_cast<float4*>(pr_row + d + l * CPL + 4 * m) =
+                make_float4(xxvv[4 * m], xxvv[4 * m + 1], xxvv[4 * m + 2], xxvv[4 * m + 3]);
+          }
         }
         if (l == 0) {
           pr_row[2 * d] = acc;
@@ -509,15 +527,15 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
     float pr = acc;
     if (d > 0 && !a.part) {
       // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
-      float t4[4];
+      float t4[CPL];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t4[k] = xv[k] * xv[k] - xxvv[k];
+      for (int k = 0; k < CPL; ++k) t4[k] = xv[k] * xv[k] - xxvv[k];
       float s = 0.f;
       for (int q = 0; q < G; ++q) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < CPL; ++k) {
           const float tk = __shfl(t4[k], gbase + q, kWave);
-          if (q * 4 + k < d) s += tk;
+          if (q * CPL + k < d) s += tk;
         }
       }
       double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
@@ -540,9 +558,11 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
         a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
       }
     }
-    if (d > 0 && l * 4 < d && !a.part)  // XV_ *= p (fm_loss.h:196-199)
-      *reinterpret_cast<float4*>(a.XVp + r * xs + l * 4) =
-          make_float4(xv[0] * p, xv[1] * p, xv[2] * p, xv[3] * p);
+#pragma unroll
+    for (int m = 0; m < CPL / 4; ++m)  // XV_ *= p (fm_loss.h:196-199)
+      if (d > 0 && l * CPL + 4 * m < d && !a.part)
+        *reinterpret_cast<float4*>(a.XVp + r * xs + l * CPL + 4 * m) =
+            make_float4(xv[4 * m] * p, xv[4 * m + 1] * p, xv[4 * m + 2] * p, xv[4 * m + 3] * p);
   }
   if (a.part) return;  // block-uniform: no loss partial in split mode
   for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
@@ -555,9 +575,9 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   }
 }
 
-template <int G>
+template <int G, int CPL>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
-  fwd_probe_body<G, false>(a);
+  fwd_probe_body<G, false, 8, CPL>(a);
 }
 
 // 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
@@ -813,14 +833,22 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
     if (G == 2 || G == 4) return DFX_OK;
   }
   if (a.index && spread && vec && CPL == 4 && G >= 4 && G <= 32 && a.B > 0) {
+    // kwarg fwd_cpl = 8 at V_dim >= 64 (a multiple of 8): two float4 per lane, half the lanes
+    int C = 4;
+    if (a.cpl == 8 && a.d >= 64 && a.d % 8 == 0 && G >= 8) {
+      G /= 2;
+      C = 8;
+      *nblk = (int)((a.B + kFmNT / G - 1) / (kFmNT / G));
+    }
     const dim3 grid((unsigned)*nblk);
-#define DFX_FWDP(GG)                                                                     \
-    if (G == GG) {                                                                       \
-      hipLaunchKernelGGL(k_fm_fwd_probe<GG>, grid, dim3(kFmNT), 0, st, a);                \
+#define DFX_FWDP(GG, CC)                                                                 \
+    if (G == GG && C == CC) {                                                            \
+      hipLaunchKernelGGL((k_fm_fwd_probe<GG, CC>), grid, dim3(kFmNT), 0, st, a);          \
       DFX_HIP(hipGetLastError());                                                        \
       return DFX_OK;                                                                     \
     }
-    DFX_FWDP(4) DFX_FWDP(8) DFX_FWDP(16) DFX_FWDP(32)
+    DFX_FWDP(4, 4) DFX_FWDP(8, 4) DFX_FWDP(16, 4) DFX_FWDP(32, 4)
+    DFX_FWDP(4, 8) DFX_FWDP(8, 8) DFX_FWDP(16, 8)
 #undef DFX_FWDP
   }
   if (a.index) return launch_fwd_gc<kFusedProbe, true>(a, G, CPL, vec, st);
@@ -1013,7 +1041,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       // chunk order, all in double and rounded once — the sums differ from the reference's
       // sequential float sums only by that float rounding (reordering error)
       const uint32_t c0 = a.choff[u];
-      const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+      const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
       const int P = d + 2;
       double gwd = 0, xxpd = 0, accp[CPL];
 #pragma unroll
@@ -1327,7 +1355,7 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
       float gw = 0.f, xxp = 0.f;
       if (a.choff && len > (uint32_t)kChunkOcc) {
         const uint32_t c0 = a.choff[u];
-        const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+        const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
         double gwd = 0, xxpd = 0;
         for (uint32_t c = 0; c < nc; ++c) {
           const double* pc = a.part + (int64_t)(c0 + c) * (d + 2);
@@ -1443,7 +1471,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
     // grad_u = (g0 - V*XXp) + sum (XV_ p) x, g0 = 0 (fm_loss.h:185-202, spmm.h:127-159)
     if (a.choff && len > (uint32_t)kChunkOcc) {
       const uint32_t c0 = a.choff[u];
-      const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+      const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
       double accp[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) accp[k] = 0;
@@ -1510,7 +1538,44 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   double gw = 0, xxp = 0, acc[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) acc[k] = 0;
-  for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
+  if constexpr (G >= 8) {
+    // G occurrences per trip, lane l reading occurrence i0 + l's row, value and p; the terms
+    // shuffled from the lanes in occurrence order (bit-identical to the walk below), WU XV*p
+    // rows in flight per sub-trip
+    constexpr int WU = 8;
+    const int gb = (int)(threadIdx.x % kWave) - l;
+    for (uint32_t i0 = s0; i0 < s1; i0 += G) {
+      const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
+      const uint32_t rl = a.occ_row[i];
+      const float xl = valued ? a.occ_x[i] : 1.f;
+      const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
+      const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
+#pragma unroll
+      for (int t0 = 0; t0 < G; t0 += WU) {
+        if ((uint32_t)t0 >= n) break;  // group-uniform
+        float xw[WU], pw[WU], xr[WU][CPL];
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+          const uint32_t r = (uint32_t)__shfl((int)rl, gb + t0 + u, kWave);
+          pw[u] = __shfl(pl, gb + t0 + u, kWave);
+          xw[u] = __shfl(xl, gb + t0 + u, kWave);
+          load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)r * xs : a.zpad, l, d, xr[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+          if ((uint32_t)(t0 + u) >= n) continue;
+          if (pw[u] != 0.f) {  // SpMV::TransTimes skips p == 0
+            gw += valued ? (double)(pw[u] * xw[u]) : (double)pw[u];
+            xxp += valued ? (double)(pw[u] * (xw[u] * xw[u])) : (double)pw[u];
+          }
+#pragma unroll
+          for (int k = 0; k < CPL; ++k)
+            acc[k] += valued ? (double)(xr[u][k] * xw[u]) : (double)xr[u][k];
+        }
+      }
+    }
+  }
+  for (uint32_t i0 = s0; G < 8 && i0 < s1; i0 += UNR) {
     uint32_t rw[UNR];
     float xw[UNR], pw[UNR], xr[UNR][CPL];
 #pragma unroll
@@ -1549,6 +1614,39 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   }
 }
 
+// A key of >= kHotChunks chunks (the hottest keys of a skewed batch: C5's top key has ~1750)
+// gets its chunk partials summed by a block of its own, one thread per partial value, in chunk
+// order in double — exactly the sequence the backward's per-key combine would add — and the
+// total written over its first chunk's partial; the backward then reads that one partial
+// (0 + total = total: bit-identical).  Without it one group walked all of a hot key's chunks
+// serially, a memory round trip per chunk, the backward's longest chain.
+__global__ __launch_bounds__(256) void k_chunk_hotsum(BwdArgs a) {
+  const int64_t ch = blockIdx.x;
+  if (ch >= (int64_t)*a.nchunks) return;
+  const uint32_t u = a.chunk_seg[ch];
+  const uint32_t c0 = a.choff[u];
+  if ((uint32_t)ch != c0) return;
+  const uint32_t len = a.segstart[u + 1] - a.segstart[u];
+  const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+  if (nc < kHotChunks) return;
+  const int P = a.d + 2;
+  constexpr int U = 16;
+  for (int j = threadIdx.x; j < P; j += blockDim.x) {
+    const double* pj = a.part + (int64_t)c0 * P + j;
+    double s = 0;
+    uint32_t c = 0;
+    for (; c + U <= nc; c += U) {
+      double v[U];
+#pragma unroll
+      for (int t = 0; t < U; ++t) v[t] = pj[(int64_t)(c + t) * P];
+#pragma unroll
+      for (int t = 0; t < U; ++t) s += v[t];
+    }
+    for (; c < nc; ++c) s += pj[(int64_t)c * P];
+    a.part[(int64_t)c0 * P + j] = s;
+  }
+}
+
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
   if (chunk_bound <= 0 || !a.choff) return DFX_OK;
   int G, CPL;
@@ -1560,6 +1658,10 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
   if (G == GG && CPL == CC) {                                                             \
     hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC>), grid, dim3(kFmNT), 0, st, a);          \
     DFX_HIP(hipGetLastError());                                                           \
+    if (chunk_bound >= (int64_t)kHotChunks) {                                             \
+      hipLaunchKernelGGL(k_chunk_hotsum, dim3((unsigned)chunk_bound), dim3(256), 0, st, a); \
+      DFX_HIP(hipGetLastError());                                                         \
+    }                                                                                     \
     return DFX_OK;                                                                        \
   }
   DFX_SCALAR_SET(DFX_BWDC)

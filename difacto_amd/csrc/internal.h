@@ -204,6 +204,7 @@ struct Context {
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
   int fat_nb = 6;         // kwarg fat_nb
+  int fwd_cpl = 8;        // kwarg fwd_cpl: V coordinates per lane of the probe forward
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int bwd_cpl = 8;        // kwarg bwd_cpl: coordinates per lane of the fused backward, d >= 64
@@ -350,6 +351,12 @@ int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
 // of its chunk count, 0 for short segments), chunk_seg[c] = segment of chunk c, total in
 // *nchunks_dev.  Arrays sized for nnz + 1 (choff) and nnz / kChunkOcc + 1 (chunk_seg).
 constexpr int kChunkOcc = 256;
+// keys of at least this many chunks have their chunk partials pre-summed (fm.hip
+// k_chunk_hotsum): the per-key combines read one partial for them
+constexpr uint32_t kHotChunks = 8;
+__host__ __device__ inline uint32_t hot_chunks_read(uint32_t nc) {
+  return nc >= kHotChunks ? 1u : nc;
+}
 // chunks of a batch, at most: a long segment of len > kChunkOcc occurrences has
 // ceil(len / kChunkOcc) <= len / kChunkOcc + 1 of them, and there are at most
 // nnz / (kChunkOcc + 1) long segments (the chunk partials and the chunk -> segment table)

@@ -315,7 +315,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.no_fat_fwd = !c->fat_fwd;
-  a.fat_nb = c->fat_nb;
+  a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
   a.fwd_lanes = c->fwd_lanes;
   a.nt = c->nt_mask;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();

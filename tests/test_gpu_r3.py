@@ -99,7 +99,7 @@ def test_workspace_growth_then_lane_localize(H):
 
 def test_bad_kwargs_rejected(H):
     from difacto_amd._lib import DfxError
-    for kw in (dict(fat_nb=5), dict(fwd_lanes=3), dict(diag="bogus"), dict(bwd_cpl=32)):
+    for kw in (dict(fat_nb=5), dict(fwd_lanes=3), dict(diag="bogus"), dict(bwd_cpl=32), dict(fwd_cpl=16)):
         with pytest.raises(DfxError):
             H.Context(0, V_dim=16, **kw)
 
@@ -447,6 +447,40 @@ def test_backward_eight_coords_per_lane_bit_identical(H, d, zipf, binary, cpl):
             nv += 1
             assert np.array_equal(ea[1], eb[1]), k
     assert nv > 0
+    ca.close()
+    cb.close()
+
+
+@pytest.mark.parametrize("d,zipf,binary", [(64, None, True), (128, 1.1, False), (96, 1.1, True)])
+def test_forward_eight_coords_per_lane_bit_identical(H, d, zipf, binary):
+    """The probe forward at V_dim >= 64 with two float4 of V per lane (kwarg fwd_cpl=8, the
+    default) against one (fwd_cpl=4): every coordinate's sums are one lane's in nnz order and s is summed over
+    l = 0..d-1 in order, so predictions, progress and the trained model are bit-identical;
+    ragged rows (empty rows, partial chunks), Zipf keys with lazy V."""
+    cfg = dict(V_dim=d, lr=.05, V_lr=.01, V_threshold=2 if zipf else 0, l1=1 if zipf else 0)
+    ca = H.Context(0, max_keys=1 << 17, fwd_cpl=4, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, **cfg)
+    for step in range(4):
+        if zipf:
+            blk = D.synthetic(2500, 39, 1 << 18, zipf=zipf, seed=900 + step, binary=binary,
+                              ragged=True)
+        else:
+            blk = D.synthetic(2500, 39, 1 << 14, seed=900 + step, binary=binary, ragged=True)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step < 2, pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step < 2, pred=pb)
+        assert np.array_equal(pa.cpu().numpy().view(np.uint32), pb.cpu().numpy().view(np.uint32))
+        a, b = H.progress(ca), H.progress(cb)
+        assert abs(a["loss"] - b["loss"]) <= 1e-12 * abs(a["loss"]) and a["auc"] == b["auc"]
+    ca.sync()
+    cb.sync()
+    assert H.Store(ca).stats() == H.Store(cb).stats()
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    va, la = H.Store(ca).pull(ca.tensor(uniq, torch.int64))
+    vb, lb = H.Store(cb).pull(cb.tensor(uniq, torch.int64))
+    assert np.array_equal(la.cpu().numpy(), lb.cpu().numpy())
+    assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
     ca.close()
     cb.close()
 
