@@ -85,9 +85,10 @@ struct Kw {
   // transform, 2 the backward's model-table lines, 4 the forward's, 8 the backward's
   // per-occurrence arrays (common.h ld4 / st4)
   int nt = 0;
-  // bwd_two_pass=1: the wide-V_dim (>= 32 lanes per key) fused backward in two passes (fm.hip
-  // k_fm_bwd_w / _v, bit-identical; A/B: C5 50.4 -> 43.2 M ex/s, so off by default)
-  int bwd_two_pass = 0;
+  // bwd_two_pass=1: the wide-V_dim (V_dim >= 128) fused backward in two passes (fm.hip
+  // k_fm_bwd_w / _v, bit-identical; A/B with the hot keys' chunk sums: C5 65.7 -> 92.3 M ex/s,
+  // the default); 0: one kernel
+  int bwd_two_pass = 1;
   // bwd_cpl=8: the fused backward at V_dim >= 64 with 8 coordinates per lane (half the lanes
   // per key: G = d / 8), bit-identical (every coordinate's terms and order are a lane's own);
   // 4: one float4 per lane (d / 4 lanes per key, capped at 64)

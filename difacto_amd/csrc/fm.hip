@@ -1290,9 +1290,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 // for the sum of (XV*p) x in occurrence order and AdaGrad.  Every term and its order are
 // k_fm_bwd's, so the model is bit-identical; the list's order (wave-aggregated appends) changes
 // only which group updates which key.  Both passes loop over a resident grid.  Measured on C5
-// (same box, kwarg bwd_two_pass=1): backward 1.53 -> 1.85 ms — under Zipf keys a wave of pass W
-// runs as long as its longest key's serial walk, which the one-kernel form spreads over two
-// keys per wave; kept as an A/B.
+// (same box, kwarg bwd_two_pass): first 1.53 -> 1.85 ms — a wave of pass W ran as long as its
+// longest key's serial walk, a hot key's ~1750 chunk partials one round trip each; with those
+// pre-summed (k_chunk_hotsum) the two passes take 0.74 ms against the one kernel's 1.17
+// (C5 65.7 -> 92.3 M ex/s): the default at >= 32 lanes per key (V_dim >= 128).
 constexpr int kBwdWNT = 256;
 
 __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
@@ -1745,6 +1746,8 @@ int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long 
     set_error("two-pass backward: V_dim a multiple of 4, 32 or 64 lanes per key");
     return DFX_ERR_ARG;
   }
+  // pass V keeps one float4 per lane: two per lane measured worse (C5 92.2 -> 87.1 M ex/s,
+  // pass V holds only the keys with V, whose walks fill its lanes)
   const size_t lds_bytes = lds >= 0 ? (size_t)lds : kBwdLdsCap;
   DFX_HIP(hipMemsetAsync(a.vcount, 0, sizeof(uint32_t), st));
   const int64_t gw = std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);

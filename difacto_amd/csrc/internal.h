@@ -206,7 +206,7 @@ struct Context {
   int fat_nb = 6;         // kwarg fat_nb
   int fwd_cpl = 8;        // kwarg fwd_cpl: V coordinates per lane of the probe forward
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
-  int bwd_two_pass = 0;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
+  int bwd_two_pass = 1;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int bwd_cpl = 8;        // kwarg bwd_cpl: coordinates per lane of the fused backward, d >= 64
   int bwd_cpl_from = 64;  // kwarg bwd_cpl_from: the least V_dim bwd_cpl = 8 applies to
   int loc_pos_payload = 0;  // kwarg loc_pos: valued data sorts packed (key | position) items

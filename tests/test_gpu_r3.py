@@ -363,12 +363,12 @@ def test_bucket_localizer_equals_lsd(H, kind):
 def test_two_pass_backward_bit_identical(H, d):
     """The wide-V_dim fused backward in two passes (k_fm_bwd_w: one lane per key — entry, g_w,
     FTRL — listing the keys with V; k_fm_bwd_v: G lanes per listed key — the V sums, AdaGrad)
-    (kwarg bwd_two_pass=1) against the one-kernel backward: every term in the same order, so the
+    (kwarg bwd_two_pass=1, the default) against the one-kernel backward (bwd_two_pass=0): every term in the same order, so the
     predictions, the progress and the model are bit-identical.  Zipf(1.1) keys with lazy V
     (C5's shape): most keys carry no V, hot keys take the chunked sums."""
     cfg = dict(V_dim=d, lr=.05, V_lr=.01, V_threshold=4)
-    ca = H.Context(0, max_keys=1 << 17, **cfg)
-    cb = H.Context(0, max_keys=1 << 17, bwd_two_pass=1, **cfg)
+    ca = H.Context(0, max_keys=1 << 17, bwd_two_pass=0, **cfg)
+    cb = H.Context(0, max_keys=1 << 17, **cfg)
     blocks = []
     for step in range(5):
         blk = D.synthetic(3000, 39, 1 << 18, zipf=1.1, seed=500 + step)
