@@ -1366,20 +1366,33 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
         gw = (float)gwd;
         xxp = (float)xxpd;
       } else {
-        for (uint32_t i0 = s0; i0 < s1; i0 += 4) {
-          uint32_t rw[4];
-          float xw[4], pw[4];
+        // WU occurrences per trip, the next trip's rows in flight beside this trip's p reads
+        // (one lane per key: a warm key's walk is this pass's longest chain); same order
+        constexpr int WU = 8;
+        uint32_t rw[WU];
+        float xw[WU];
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-            rw[t] = a.occ_row[i];
-            xw[t] = valued ? a.occ_x[i] : 1.f;
+        for (int t = 0; t < WU; ++t) {
+          const uint32_t i = s0 + t < s1 ? s0 + t : s1 - 1;
+          rw[t] = a.occ_row[i];
+          xw[t] = valued ? a.occ_x[i] : 1.f;
+        }
+        for (uint32_t i0 = s0; i0 < s1; i0 += WU) {
+          float pw[WU];
+#pragma unroll
+          for (int t = 0; t < WU; ++t)
+            pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+          const uint32_t in = i0 + WU;
+          uint32_t rn[WU];
+          float xn[WU];
+#pragma unroll
+          for (int t = 0; t < WU; ++t) {
+            const uint32_t i = in + t < s1 ? in + t : s1 - 1;
+            rn[t] = in < s1 ? a.occ_row[i] : 0u;
+            xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
           }
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
-            pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
+          for (int t = 0; t < WU; ++t) {
             if (i0 + t < s1 && pw[t] != 0.f) {
               if (valued) {
                 gw += pw[t] * xw[t];
@@ -1389,6 +1402,11 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
                 xxp += pw[t];
               }
             }
+          }
+#pragma unroll
+          for (int t = 0; t < WU; ++t) {
+            rw[t] = rn[t];
+            xw[t] = xn[t];
           }
         }
       }
@@ -1490,24 +1508,31 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
     } else {
 #pragma unroll
       for (int k = 0; k < CPL; ++k) acc[k] = 0.f - vcur[k] * xxp;
-      for (uint32_t i0 = s0; i0 < s1; i0 += UNR) {
-        uint32_t rw[UNR];
-        float xw[UNR], xrw[UNR][CPL];
+      // G occurrences per trip: lane l reads occurrence i0 + l's row and value, UNR XV*p rows
+      // in flight per sub-trip with their row ids shuffled from those lanes (occurrence order)
+      const int gb = (int)(threadIdx.x % kWave) - l;
+      for (uint32_t i0 = s0; i0 < s1; i0 += G) {
+        const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
+        const uint32_t rl = a.occ_row[i];
+        const float xl = valued ? a.occ_x[i] : 1.f;
+        const uint32_t nt = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
-        for (int t = 0; t < UNR; ++t) {
-          const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-          rw[t] = a.occ_row[i];
-          xw[t] = valued ? a.occ_x[i] : 1.f;
-        }
+        for (int t0 = 0; t0 < G; t0 += UNR) {
+          if ((uint32_t)t0 >= nt) break;  // group-uniform
+          float xw[UNR], xrw[UNR][CPL];
 #pragma unroll
-        for (int t = 0; t < UNR; ++t)
-          load_coords<CPL, true>(a.XVp + (int64_t)rw[t] * xs, l, d, xrw[t]);
+          for (int t = 0; t < UNR; ++t) {
+            const uint32_t r = (uint32_t)__shfl((int)rl, gb + t0 + t, kWave);
+            xw[t] = __shfl(xl, gb + t0 + t, kWave);
+            load_coords<CPL, true>(a.XVp + (int64_t)r * xs, l, d, xrw[t]);
+          }
 #pragma unroll
-        for (int t = 0; t < UNR; ++t) {
-          if (i0 + t < s1) {
+          for (int t = 0; t < UNR; ++t) {
+            if ((uint32_t)(t0 + t) < nt) {
 #pragma unroll
-            for (int k = 0; k < CPL; ++k)
-              acc[k] = valued ? acc[k] + xrw[t][k] * xw[t] : acc[k] + xrw[t][k];
+              for (int k = 0; k < CPL; ++k)
+                acc[k] = valued ? acc[k] + xrw[t][k] * xw[t] : acc[k] + xrw[t][k];
+            }
           }
         }
       }
