@@ -1546,7 +1546,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
 
 // one group per chunk of a long segment: partial {g_w, XXp, sum (XV p) x} over its
 // kChunkOcc occurrences in order (the same terms as k_fm_bwd's walk)
-template <int G, int CPL>
+template <int G, int CPL, bool VEC = false>
 __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   constexpr int CPB = kFmNT / G;
   constexpr int UNR = 4;
@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
           const uint32_t r = (uint32_t)__shfl((int)rl, gb + t0 + u, kWave);
           pw[u] = __shfl(pl, gb + t0 + u, kWave);
           xw[u] = __shfl(xl, gb + t0 + u, kWave);
-          load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)r * xs : a.zpad, l, d, xr[u]);
+          load_coords<CPL, VEC>(d > 0 ? a.XVp + (int64_t)r * xs : a.zpad, l, d, xr[u]);
         }
 #pragma unroll
         for (int u = 0; u < WU; ++u) {
@@ -1673,16 +1673,18 @@ __global__ __launch_bounds__(256) void k_chunk_hotsum(BwdArgs a) {
   }
 }
 
-int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
+int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, bool aligned) {
   if (chunk_bound <= 0 || !a.choff) return DFX_OK;
   int G, CPL;
   bool vec;
-  lanes_for(a.d, false, &G, &CPL, &vec);
+  // aligned (the fused steps' 16-byte XV*p rows, V_dim a multiple of 4): float4 per lane, a
+  // chunk on d / 4 lanes (same per-coordinate sums: the partials are bit-identical)
+  lanes_for(a.d, aligned && a.d >= 64, &G, &CPL, &vec);
   const int64_t cpb = kFmNT / G;
   dim3 grid((unsigned)((chunk_bound + cpb - 1) / cpb));
 #define DFX_BWDC(GG, CC, VV)                                                              \
-  if (G == GG && CPL == CC) {                                                             \
-    hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC>), grid, dim3(kFmNT), 0, st, a);          \
+  if (G == GG && CPL == CC && vec == VV) {                                                \
+    hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC, VV>), grid, dim3(kFmNT), 0, st, a);      \
     DFX_HIP(hipGetLastError());                                                           \
     if (chunk_bound >= (int64_t)kHotChunks) {                                             \
       hipLaunchKernelGGL(k_chunk_hotsum, dim3((unsigned)chunk_bound), dim3(256), 0, st, a); \
@@ -1691,6 +1693,7 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st) {
     return DFX_OK;                                                                        \
   }
   DFX_SCALAR_SET(DFX_BWDC)
+  DFX_BWDC(16, 4, true) DFX_BWDC(32, 4, true) DFX_BWDC(64, 4, true)
 #undef DFX_BWDC
   set_error("unsupported V_dim");
   return DFX_ERR_ARG;
@@ -1992,7 +1995,7 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   b.wpos = w_pos; b.vpos = V_pos; b.W = weights; b.grad = grad;
   b.choff = choff; b.chunk_seg = chunk_seg; b.nchunks = nchunks; b.part = ws.Vb.as<double>();
   // the number of segments is device-side (ds->u_count, set above), where k_fm_bwd reads it
-  DFX_TRY(launch_bwd_chunks(b, max_chunks(nnz), c->stream));
+  DFX_TRY(launch_bwd_chunks(b, max_chunks(nnz), c->stream, false));
   DFX_TRY(launch_bwd<false>(b, nnz, c->stream));
   // n_init served as the chunk plan's gate; it counts the fused step's InitV requests
   DFX_HIP(hipMemsetAsync(&c->ds->n_init, 0, sizeof(uint32_t), c->stream));

@@ -154,6 +154,6 @@ int bwd_two_pass_reserve(Context* c, Workspace& ws, int64_t nseg_bound, BwdArgs*
 int sum_live(const uint2* part, int64_t n, DevState* ds, hipStream_t st);
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds = -1);
 // the chunk partials of long segments (before the backward reads them)
-int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st);
+int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, bool aligned);
 
 }  // namespace dfx

@@ -629,7 +629,7 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     DFX_TRY(ows.Vb.ensure((size_t)max_chunks(nnz) * (d + 2) * 8));
     g.part = ows.Vb.as<double>();
     DFX_TRY(bwd_two_pass_reserve(c, ows, nnz, &g));
-    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream));
+    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream, true));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
   }
   (void)R;

@@ -358,7 +358,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
       DFX_TRY(ws.live.ensure((size_t)nbb * sizeof(uint2)));
       g.live_part = ws.live.as<uint2>();
     }
-    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream));
+    DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream, true));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);
