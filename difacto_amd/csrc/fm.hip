@@ -1470,7 +1470,7 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
 template <int G, int CPL>
 __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
   constexpr int EPB = kFmNT / G;
-  constexpr int UNR = CPL <= 4 ? 4 : 2;
+  constexpr int UNR = CPL <= 4 ? 8 : 2;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int64_t n = (int64_t)*a.vcount;
@@ -1755,6 +1755,7 @@ int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligne
 
 // the two-pass backward's resident grid (blocks per pass)
 constexpr int64_t kBwdPassBlocks = 4096;
+constexpr int64_t kBwdPassVBlocks = 32768;
 
 // V_dim whose backward runs in two passes (k_fm_bwd_w + k_fm_bwd_v): G >= 32 lanes per key
 bool bwd_two_pass(int d) {
@@ -1781,7 +1782,10 @@ int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long 
   const int64_t gw = std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);
   hipLaunchKernelGGL(k_fm_bwd_w, dim3((unsigned)gw), dim3(kBwdWNT), 0, st, a);
   const int64_t epb = kFmNT / G;
-  const int64_t gv = std::min<int64_t>((nseg_bound + epb - 1) / epb, kBwdPassBlocks);
+  // pass V: enough blocks that a group takes about one listed key (blocks past the list exit
+  // at once) — the list's keys differ widely in walk length, and a resident grid's stride
+  // loop stacked several long walks on one group
+  const int64_t gv = std::min<int64_t>((nseg_bound + epb - 1) / epb, kBwdPassVBlocks);
   if (G == 32)
     hipLaunchKernelGGL((k_fm_bwd_v<32, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, a);
   else
