@@ -28,7 +28,8 @@ RBENCH = build/reader_bench
 
 DISTLIB = difacto_amd/libdfx_dist.so
 
-all: $(LIB) $(DISTLIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH)
+all: $(LIB) $(DISTLIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH) \
+  build/expf_check
 
 $(RBENCH): difacto_amd/host/reader.cc tools/reader_bench.cc difacto_amd/host/reader.h
 	@mkdir -p build
@@ -90,6 +91,11 @@ $(LIB): $(OBJS)
 
 oracle:
 	$(MAKE) -s -C oracle
+
+# test infrastructure: the device's expf (csrc/expf.h) against the host's glibc expf
+build/expf_check: tools/expf_check.hip $(CSRC)/expf.h
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -ffp-contract=off -o $@ $<
 
 clean:
 	rm -rf build $(LIB) $(DISTLIB)

@@ -33,7 +33,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without a launcher bench.py starts them")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="BASELINE.json workload: c3 (the metric's, default), c2 (LR V_dim=0, "
                          "40 valued nnz, 2^20 keys, FTRL L1), c5 (Zipf(1.1) keys, V_dim=128, "
@@ -153,30 +154,35 @@ class DevBatch:
 
 
 def algorithmic_bytes(B, nnz, U, d, valued=False, U_V=None, occ_V=None):
-    """Essential HBM bytes per launch.  U_V: keys with live V, occ_V:
-    their occurrences (dfx_prof_counts; default: every key has V); valued: + the value per nnz
-    in the forward and per occurrence in the backward"""
-    if U_V is None or occ_V is None:
-        U_V, occ_V = U, nnz
+    """Essential HBM bytes per launch, every datum counted once per step: a
+    key's entry and V row once however many of the batch's nnz read it (hot Zipf keys are read
+    from cache, not HBM), a row's [XV*p | p] once however many occurrences read it.  U_V: keys
+    with live V (dfx_prof_counts; default: every key); valued: + the value per nnz.  occ_V is
+    accepted for the callers' sake and no longer priced (per-occurrence gathers of one key's V
+    are reuse, not traffic)"""
+    if U_V is None:
+        U_V = U
     x = 4 if valued else 0
-    # forward (probe mode): per row offset / label / pred / p / XV*p, per nnz its id and its
-    # key's {w, vrow} entry bytes (+ value), per nnz of a key with V its V row
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + x) + occ_V * 4 * d
-    # backward: per key its segment start, key, entry read + written, slot; per key with V its
-    # V and Vaux read + written; per occurrence its row, p (+ value), and XV*p row when V
-    bwd = U * (8 + 4 + 8 + 32 + 4) + U_V * 16 * d + nnz * (4 + 4 + 4 + x) + occ_V * 4 * d
+    row = 4 * (d + 1) if d > 0 else 4  # a row's [XV*p | p] (p alone at V_dim 0)
+    # forward: per row its offset, label, pred and the [XV*p | p] row it writes; per nnz its
+    # id (+ value); per unique key its entry {key, w, vrow} and, when live, its V row
+    fwd = B * (8 + 4 + 4 + row) + nnz * (8 + x) + U * 16 + U_V * 4 * d
+    # backward: per unique key its segment start, key, slot, entry read + written; V and Vaux
+    # read + written when live; per occurrence its row index (+ value); per row its [XV*p | p]
+    bwd = U * (8 + 4 + 8 + 32 + 4) + U_V * 16 * d + nnz * (4 + x) + B * row
     return {"forward": fwd, "backward_update": bwd}
 
 
 def algorithmic_bytes_sharded(B, nnz, U, d):
     """Essential HBM bytes of the worker's dfx_dist_fwd_bwd (forward + backward over pulled
-    records of S = d + 4 floats, binary data, all V live): forward per row offs / label / pred /
-    p / XVp, per nnz col + the record's {w, live} + V; backward per key segstart + {w, live} +
-    V + the whole gradient record written, per occurrence occ_row / p / XVp."""
+    records of S = d + 4 floats, binary data, all V live), each datum once per step: forward
+    per row offs / label / pred / [XV*p | p], per nnz its col, per unique key its record;
+    backward per key its segment start and the whole gradient record written, per occurrence
+    its row index, per row its [XV*p | p]."""
     S = d + 4
-    # forward (probe mode): per nnz its id and its key's {w, vrow} entry bytes, then V
-    fwd = B * (8 + 4 + 4 + 4 + 4 * d) + nnz * (8 + 8 + 4 * d)
-    bwd = U * (4 + 8 + 4 * d + 4 * S) + nnz * (4 + 4 + 4 * d)
+    row = 4 * (d + 1)
+    fwd = B * (8 + 4 + 4 + row) + nnz * 4 + U * 4 * S
+    bwd = U * (4 + 4 * S) + nnz * 4 + B * row
     return fwd + bwd
 
 
@@ -312,8 +318,34 @@ def cpu_baseline(args):
                       % (nb * args.cpu_batch, nb, args.cpu_batch)}
 
 
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: run this script as N ranks, one process per GPU, with the
+    environment torch.distributed.run gives them (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), and
+    exit with the worst rank's status.  Called before anything touches the GPU; rank 0 prints
+    the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc != 0), 0)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%s (launch with --nproc-per-node %d, or "
+                 "without a launcher)" % (args.gpus, os.environ.get("WORLD_SIZE"), args.gpus))
     import torch
     import torch.distributed as dist
 

@@ -72,11 +72,10 @@ struct Kw {
   // unless the batches repeat); never set by the product path
   int diag = 0;
   int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
-  // loc_bucket=1|2: the fused step's Localizer sorts one global pass over the top varying digit
-  // and then each bucket by one block of 256 | 1024 threads (localize.hip k_loc_bucket); 0: LSD
-  // passes over every digit.  A/B at C3 (round 3, same box): 0 128.0, 1 115.0, 2 121.0 M ex/s —
-  // the bucket blocks run long beside the backward and the next forward waits for them
-  int loc_bucket = 0;
+  // loc_bucket=1 (default): the Localizer of the fused step and of the split owner (no col) as a
+  // bucket sort — histogram, scatter into key-range buckets, one LDS sort per bucket
+  // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
+  int loc_bucket = 1;
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -176,13 +175,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else { set_error("unknown diag: " + v + " (noauc|noloc|noauc_noloc)"); return DFX_ERR_ARG; }
     }
     else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
-    else if (k == "loc_bucket") {
-      kw->loc_bucket = atoi(cv);
-      if (kw->loc_bucket < 0 || kw->loc_bucket > 2) {
-        set_error("loc_bucket must be 0, 1 (256-thread buckets) or 2 (1024)");
-        return DFX_ERR_ARG;
-      }
-    }
+    else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
       if (kw->fwd_lanes != 0 && kw->fwd_lanes != 2 && kw->fwd_lanes != 4) {
@@ -283,10 +276,12 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.rowtmp2};
+                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.rowtmp2, &w.lbcnt, &w.lbq};
   for (DevBuf* b : bufs) b->release();
   if (w.os_hint) (void)hipHostFree(w.os_hint);
   w.os_hint = nullptr;
+  if (w.lb_hint) (void)hipHostFree(w.lb_hint);
+  w.lb_hint = nullptr;
 }
 
 // streams, events and lane states of the fused step's pipeline, created on first use

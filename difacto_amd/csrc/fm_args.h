@@ -1,15 +1,21 @@
 // Argument blocks of the FM forward/backward kernels (fm.hip), shared with step.hip.
 #pragma once
+#include "expf.h"
 #include "internal.h"
 
 namespace dfx {
 
-// p = -y / (1 + exp(y * pred)) [* weight]   (fm_loss.h:155-165).  exp in double, rounded:
-// correctly rounded like glibc's expf in all but rare ties (within the 1e-5 tolerance).
+// the exp2 table of glibc's expf (expf.h), one copy per translation unit in constant memory
+static __constant__ const uint64_t kExp2fTab[32] = DFX_EXP2F_TAB;
+__device__ inline float dfx_expf(float x) {
+  return expf_glibc(x, [](int i) { return kExp2fTab[i]; });
+}
+
+// CalcGrad's p = -y / (1 + expf(y * pred)) [* weight] (fm_loss.h:159-164), expf as glibc's
 __device__ inline float logit_p(float label, float pred, const float* rw, int64_t r) {
   float y = label > 0 ? 1.f : -1.f;
   float t = y * pred;
-  float e = (float)exp((double)t);
+  float e = dfx_expf(t);
   float den = 1.f + e;
   float p = -y / den;
   if (rw) p = p * rw[r];

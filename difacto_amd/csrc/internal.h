@@ -70,6 +70,10 @@ struct DevState {
   double scratch[8];
   unsigned int iv_ticket;      // the one-launch InitV's tile tickets (reset by k_step_finalize)
   unsigned int iv_epoch;       // its look-back words' tag (advanced by k_step_finalize)
+  // the bucket Localizer (locbucket.hip): min / max of the batch's keys, and the key range its
+  // bucket map was fitted to (the previous batch on this lane; pk_valid == 0: none yet)
+  unsigned long long kmin, kmax, pk_min, pk_max;
+  unsigned int pk_valid;
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
@@ -95,6 +99,12 @@ struct Workspace {
   DevBuf vlist;     // the two-pass backward's listed keys {segment, V row, XXp, 0} + a counter
   DevBuf rowtmp2;   // the Localizer's row of each position (valued data, position payloads)
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
+  // the bucket Localizer (locbucket.hip): per (tile, bucket) counts / prefixes, per bucket its
+  // total and start; per item its row / position when the items are not packed (and scratch)
+  DevBuf lbcnt, lbq;
+  // pinned, written by the device: [0] buckets over the LDS capacity in the last bucket
+  // Localizer of this workspace, [1] radix Localizers run since, [2] 1 packed / 2 not
+  unsigned int* lb_hint = nullptr;
   // radix sort: partial digit counts [kOsParts][8][256], per-pass counts [8][256] (u32), then
   // look-back words [tiles][256] (u64)
   DevBuf os;
@@ -215,7 +225,7 @@ struct Context {
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
-  int loc_bucket = 0;     // kwarg loc_bucket (localize.hip k_loc_bucket)
+  int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
@@ -296,17 +306,10 @@ constexpr int kSortMetaPack = 25;
 // tickets of the Localizer's one-pass write and of the chunk plan (localize.hip k_loc_write,
 // k_chunk_plan), reset by each sort's plan
 constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
-// flags |= kSortBucket (packed items only): the plan may turn the sort into one pass over the top
-// varying digit plus the Localizer's per-bucket sort (sort.hip k_os_plan, localize.hip
-// k_loc_bucket) when no bucket exceeds kSortBucketMax items; sortmeta[30] says so,
-// [28..29] hold the shifts of the digits below the top one
-constexpr int kSortBucket = 4;
 // flags |= kSortNT: the scatter passes load and store their items with the streaming policy
 constexpr int kSortNT = 8;
 // flags |= kSortHint: passes beyond the previous sort's active count run on a small looping grid
 constexpr int kSortHint = 16;
-constexpr uint32_t kSortBucketMax = 1u << 18;
-constexpr int kSortMetaRest = 28, kSortMetaBucket = 30;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
 // the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
 __device__ inline void sort_unpack(const unsigned* meta, uint64_t and_mask, uint64_t w,
@@ -386,6 +389,10 @@ struct LocOut {
 };
 int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o);
+// the same by the bucket sort (locbucket.hip), for outputs without col; *used = false when the
+// workspace's hint sent this batch to the radix sort instead (nothing was enqueued)
+int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
+                    const uint64_t* index, uint64_t max_index, const LocOut& o, bool* used);
 
 int ws_reserve(Context* c, int64_t rows, int64_t nnz);
 int pipeline_init(Context* c);

@@ -12,7 +12,7 @@
 // Every index of the block is in its own dictionary, so the compacted block keeps all nnz:
 // its offsets/values/labels are the input's and only `col` is new.  Bit-exact by
 // construction (ranks depend only on keys).
-#include "internal.h"
+#include "lookback.h"
 
 namespace dfx {
 
@@ -145,71 +145,6 @@ struct LocWriteArgs {
   int x_in_pay;  // the 8-byte payload's low word is the value's bits (TransformArgs::value)
 };
 
-__device__ inline unsigned long long hw_word(uint32_t tag, uint32_t flag, uint32_t v) {
-  return ((unsigned long long)((tag << 2) | flag) << 32) | v;
-}
-
-// Decoupled look-back over one word per tile (tiles taken in ticket order), by the block's
-// first wave: publishes this tile's aggregate, sums the predecessors' words 64 at a time back to
-// the nearest one that knows its inclusive prefix, publishes its own inclusive prefix and
-// returns the exclusive one to every thread.  tag (29 bits + a kind bit): the launch's, so stale
-// words of earlier launches never match.
-__device__ inline uint32_t tile_lookback(unsigned long long* stat, int64_t tile, uint32_t tag,
-                                         uint32_t tot, int* err, uint32_t* s_pre) {
-  if (threadIdx.x < kWave) {
-    const int l = lane_id();
-    unsigned long long* st = stat + tile;
-    if (l == 0)
-      __hip_atomic_store(st, hw_word(tag, tile == 0 ? 2u : 1u, tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t pre = 0;
-    int64_t kk = tile - 1;
-    uint32_t spins = 0;
-    while (kk >= 0) {
-      const int64_t j = kk - l;
-      uint32_t flag = 2, v = 0;
-      if (j >= 0) {
-        const unsigned long long wv =
-            __hip_atomic_load(stat + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hi = (uint32_t)(wv >> 32);
-        flag = (hi >> 2) == tag ? (hi & 3u) : 0u;
-        v = (uint32_t)wv;
-      }
-      const uint64_t inc = __ballot(flag == 2u);
-      const uint64_t none = __ballot(flag == 0u);
-      // lanes up to the first inclusive word (the nearest predecessor that knows its prefix)
-      const int lim = inc ? __ffsll((long long)inc) - 1 : kWave - 1;
-      const uint64_t upto = lim == kWave - 1 ? ~0ull : ((1ull << (lim + 1)) - 1);
-      if (none & upto) {  // a predecessor has not published yet: read again
-        if (++spins > (1u << 24)) {
-          if (l == 0) atomicOr(err, kErrSort);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      uint32_t add = l <= lim ? v : 0u;
-      for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, kWave);
-      pre += add;
-      if (inc) break;
-      kk -= kWave;
-    }
-    if (l == 0) {
-      if (tile > 0)
-        __hip_atomic_store(st, hw_word(tag, 2u, pre + tot), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      *s_pre = pre;
-    }
-  }
-  __syncthreads();
-  return *s_pre;
-}
-// tag spaces of the two users of Workspace::hstat on a lane (the same sort epoch)
-__device__ inline uint32_t hw_tag(const unsigned* meta) { return meta[kSortMetaEpoch] & 0x1FFFFFFFu; }
-__device__ inline uint32_t cp_tag(const unsigned* meta) {
-  return (meta[kSortMetaEpoch] & 0x1FFFFFFFu) | 0x20000000u;
-}
-
 // A segment longer than kChunkOcc (a skewed key: the item kChunkOcc before an item has its key)
 // raises ds->n_init, the chunk plan's gate: one flag per block at most, and only while it is
 // still clear — a skewed batch has long segments in most blocks, and same-address atomics from
@@ -228,7 +163,6 @@ __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const 
                                                       uint32_t* tilesum) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   const unsigned* meta = ds->sortmeta;
-  if (meta[kSortMetaBucket] & 1u) return;  // bucket mode: k_loc_bucket wrote the outputs
   const uint64_t* K = meta[31] ? k1 : k0;
   const int64_t base = (int64_t)blockIdx.x * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint32_t s = 0;
@@ -260,7 +194,6 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   __shared__ uint32_t s_tile, s_pre;
   unsigned* meta = a.ds->sortmeta;
-  if (meta[kSortMetaBucket] & 1u) return;  // bucket mode: k_loc_bucket wrote the outputs
   const bool onepass = a.tilebase == nullptr;
   if (onepass) {
     if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaHwTile], 1u);
@@ -353,179 +286,6 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   }
 }
 
-// ---- bucket mode (sort.hip k_os_plan, kSortBucket): the per-bucket sort + heads / outputs ----
-// After ONE pass over the top varying digit (its buckets in key order, each stable in input
-// order) a block per bucket, taken in bucket order by a ticket, sorts its bucket by the digits
-// below (stable LSD through global memory: the bucket, ~15 k items at B = 100 k, stays in L2),
-// counts its heads, finds the heads of the buckets before it by decoupled look-back, and writes
-// uniq / segstart / occ_row as k_loc_write does — in place of two more global passes and the heads / write pass.
-constexpr int kBkIT = 8;
-
-struct BucketArgs {
-  uint64_t* k0;  // ping-pong buffer (the pass's source)
-  uint64_t* k1;  // the top-digit pass's result (packed items)
-  const uint32_t* counts;  // counts[0..256): items per bucket
-  int64_t n;
-  DevState* ds;
-  unsigned long long* stat;  // per bucket: its tagged look-back word (Workspace::hstat)
-  uint64_t* uniq;
-  uint32_t* segstart;
-  uint32_t* occ_row;
-};
-
-// NT threads per bucket (kwarg loc_bucket: 1 -> 256, a block that fits beside the backward's;
-// 2 -> 1024)
-template <int NT>
-__global__ __launch_bounds__(NT) void k_loc_bucket(BucketArgs a) {
-  constexpr int kBkNT = NT, kBkWaves = NT / kWave, kBkChunk = NT * kBkIT;
-  unsigned* meta = a.ds->sortmeta;
-  const unsigned mode = meta[kSortMetaBucket];
-  if (!(mode & 1u)) return;  // the LSD passes ran instead (k_loc_write writes the outputs)
-  __shared__ uint32_t wcnt[kBkWaves][256];
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t lds[kBkWaves + 1];
-  __shared__ uint32_t s_b, s_start, s_pre;
-  const int t = threadIdx.x, w = t / kWave, l = lane_id();
-  if (t == 0) s_b = atomicAdd(&meta[kSortMetaHwTile], 1u);
-  __syncthreads();
-  const uint32_t b = s_b;
-  if (b >= 256u) return;
-  {  // the bucket's start: the counts of the buckets before it
-    uint32_t c = 0;
-    for (int i = t; i < (int)b; i += kBkNT) c += a.counts[i];
-    uint32_t tot;
-    (void)block_excl_scan<kBkNT>(c, lds, &tot);
-    if (t == 0) s_start = tot;
-  }
-  __syncthreads();
-  const int64_t start = s_start;
-  const int64_t nb = a.counts[b];
-  uint64_t* X = a.k1 + start;
-  uint64_t* Y = a.k0 + start;
-  const int nrest = (int)((mode >> 8) & 0xFFu);
-  // ---- stable LSD over the digits below the top one (ascending), through global memory
-  for (int r = 0; r < nrest && nb > 1; ++r) {
-    const int shift = (int)((meta[kSortMetaRest + (r >> 2)] >> (8 * (r & 3))) & 0xFFu);
-    if (t < 256) base[t] = 0;
-    __syncthreads();
-    for (int64_t i = t; i < nb; i += kBkNT) atomicAdd(&base[(uint32_t)(X[i] >> shift) & 255u], 1u);
-    __syncthreads();
-    {
-      const uint32_t c = t < 256 ? base[t] : 0u;
-      __syncthreads();
-      const uint32_t ex = block_excl_scan<kBkNT>(c, lds, nullptr);
-      if (t < 256) base[t] = ex;
-    }
-    static_assert(NT >= 256, "one thread per digit");
-    __syncthreads();
-    for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
-      for (int i = t; i < kBkWaves * 256; i += kBkNT) (&wcnt[0][0])[i] = 0;
-      __syncthreads();
-      uint64_t key[kBkIT];
-      uint32_t dr[kBkIT];
-      const int64_t wb = c0 + (int64_t)w * kWave * kBkIT;
-#pragma unroll
-      for (int j = 0; j < kBkIT; ++j) {
-        const int64_t idx = wb + j * kWave + l;
-        const bool valid = idx < nb;
-        key[j] = valid ? X[idx] : 0ull;
-        const uint32_t d = (uint32_t)(key[j] >> shift) & 255u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bt = 0; bt < 8; ++bt) {
-          const bool bit = (d >> bt) & 1u;
-          const uint64_t mb = __ballot(valid && bit);
-          peers &= bit ? mb : ~mb;
-        }
-        if (!valid) peers = 0;
-        const uint32_t rk = (uint32_t)__popcll(peers & lanemask_lt());
-        const uint32_t old = valid ? wcnt[w][d] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && rk == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        dr[j] = valid ? (d | ((old + rk) << 8)) : 0xFFFFFFFFu;
-      }
-      __syncthreads();
-      if (t < 256) {  // the waves' offsets inside the chunk, on the digit's running base
-        uint32_t run = base[t];
-        for (int i = 0; i < kBkWaves; ++i) {
-          const uint32_t x = wcnt[i][t];
-          wcnt[i][t] = run;
-          run += x;
-        }
-        base[t] = run;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < kBkIT; ++j)
-        if (dr[j] != 0xFFFFFFFFu) Y[wcnt[w][dr[j] & 255u] + (dr[j] >> 8)] = key[j];
-      __syncthreads();
-    }
-    __threadfence_block();  // this pass's stores, seen by the whole block in the next
-    __syncthreads();
-    uint64_t* tmp = X; X = Y; Y = tmp;
-  }
-  // ---- heads: a key differing from the item before it (the first item of a bucket always)
-  const uint64_t andm = a.ds->and_mask;
-  uint32_t mine = 0;
-  bool longseg = false;
-  for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
-    const int64_t ib = c0 + (int64_t)t * kBkIT;
-#pragma unroll
-    for (int j = 0; j < kBkIT; ++j) {
-      const int64_t i = ib + j;
-      if (i >= nb) break;
-      const uint64_t kb = sort_key_bits(meta, X[i]);
-      mine += (i == 0 || kb != sort_key_bits(meta, X[i - 1])) ? 1u : 0u;
-      if (i >= kChunkOcc && kb == sort_key_bits(meta, X[i - kChunkOcc])) longseg = true;
-    }
-  }
-  if (__syncthreads_or(longseg) && t == 0 &&
-      __hip_atomic_load(&a.ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    atomicOr(&a.ds->n_init, 1u);
-  uint32_t tot;
-  (void)block_excl_scan<kBkNT>(mine, lds, &tot);
-  uint32_t rank0 = tile_lookback(a.stat, (int64_t)b, hw_tag(meta), tot, &a.ds->err, &s_pre);
-  // ---- outputs, in position order: per head its key and segment start, per item its row
-  const int rb8 = (int)((meta[kSortMetaPack] >> 16) & 0xFFu);
-  for (int64_t c0 = 0; c0 < nb; c0 += kBkChunk) {
-    const int64_t ib = c0 + (int64_t)t * kBkIT;
-    uint64_t it[kBkIT];
-    uint32_t h[kBkIT], s = 0;
-#pragma unroll
-    for (int j = 0; j < kBkIT; ++j) {
-      const int64_t i = ib + j;
-      h[j] = 0;
-      if (i < nb) {
-        it[j] = X[i];
-        h[j] = (i == 0 || sort_key_bits(meta, it[j]) != sort_key_bits(meta, X[i - 1])) ? 1u : 0u;
-      }
-      s += h[j];
-    }
-    uint32_t ctot;
-    uint32_t incl = block_excl_scan<kBkNT>(s, lds, &ctot) + rank0;
-#pragma unroll
-    for (int j = 0; j < kBkIT; ++j) {
-      const int64_t i = ib + j;
-      if (i >= nb) break;
-      incl += h[j];
-      uint64_t key;
-      uint32_t row;
-      sort_unpack(meta, andm, it[j], &key, &row);
-      if (h[j]) {
-        if (a.uniq) a.uniq[incl - 1] = key;
-        if (a.segstart) a.segstart[incl - 1] = (uint32_t)(start + i);
-      }
-      if (a.occ_row) a.occ_row[start + i] = (uint32_t)(it[j] & ((1ull << rb8) - 1));
-    }
-    rank0 += ctot;
-  }
-  if (b == 255u && t == 0) {  // the last bucket closes the segments
-    a.ds->u_count = rank0;
-    if (a.segstart) a.segstart[rank0] = (uint32_t)a.n;
-  }
-}
-
 __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* cnt, int64_t cap) {
   int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= cap || u >= ds->u_count) return;
@@ -611,15 +371,28 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
-  DFX_TRY(ws.keys0.ensure(nnz * 8));
-  DFX_TRY(ws.keys1.ensure(nnz * 8));
-  DFX_TRY(ws.vals0.ensure(nnz * 8));
-  DFX_TRY(ws.vals1.ensure(nnz * 8));
   uint32_t* segs = o.segstart;
   if (o.cnt && !segs) {
     DFX_TRY(ws.segstart.ensure((nnz + 1) * 4));
     segs = ws.segstart.as<uint32_t>();
   }
+  if (c->loc_bucket && !o.col && o.occ_row) {  // no col wanted: the bucket sort (locbucket.hip)
+    LocOut ob = o;
+    ob.segstart = segs;
+    bool used = false;
+    DFX_TRY(localize_bucket(c, L, B, nnz, offset, index, max_index, ob, &used));
+    if (used) {
+      if (o.cnt)
+        hipLaunchKernelGGL(k_loc_cnt, dim3((nnz + 255) / 256), dim3(256), 0, L.stream, ds, segs,
+                           o.cnt, nnz);
+      DFX_HIP(hipGetLastError());
+      return DFX_OK;
+    }
+  }
+  DFX_TRY(ws.keys0.ensure(nnz * 8));
+  DFX_TRY(ws.keys1.ensure(nnz * 8));
+  DFX_TRY(ws.vals0.ensure(nnz * 8));
+  DFX_TRY(ws.vals1.ensure(nnz * 8));
   uint64_t* k0 = ws.keys0.as<uint64_t>();
   uint64_t* k1 = ws.keys1.as<uint64_t>();
   uint64_t* p0 = ws.vals0.as<uint64_t>();
@@ -663,8 +436,6 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0) |
-                                                      (c->loc_bucket && !narrow_pos ? kSortBucket
-                                                                                    : 0) |
                                                       (c->nt_mask & kNtLane ? kSortNT : 0) |
                                                       (c->sort_hint ? kSortHint : 0))));
   } else {
@@ -677,29 +448,18 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       (c->sort_hint ? kSortHint : 0))));
   }
   // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
-  // k_loc_write with look-back; in bucket mode (the plan's choice) k_loc_bucket does it per
-  // bucket and these exit
+  // k_loc_write with look-back
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
   uint32_t* ts = nullptr;
   if (!c->loc_onepass) {
     DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
     ts = ws.tiles.as<uint32_t>();
   }
-  if (c->loc_onepass || (narrow && !narrow_pos && c->sort_pack && c->loc_bucket)) {
+  if (c->loc_onepass) {
     void* before = ws.hstat.p;
     DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * (ntiles > 256 ? ntiles : 256)));
     if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
       DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  }
-  if (narrow && !narrow_pos && c->sort_pack && c->loc_bucket) {
-    BucketArgs ba{};
-    ba.k0 = k0; ba.k1 = k1; ba.counts = ws.os_counts(); ba.n = nnz; ba.ds = ds;
-    ba.stat = ws.hstat.as<unsigned long long>();
-    ba.uniq = o.uniq; ba.segstart = segs; ba.occ_row = o.occ_row;
-    if (c->loc_bucket == 2)
-      hipLaunchKernelGGL(k_loc_bucket<1024>, dim3(256), dim3(1024), 0, L.stream, ba);
-    else
-      hipLaunchKernelGGL(k_loc_bucket<256>, dim3(256), dim3(256), 0, L.stream, ba);
   }
   if (ts) {
     hipLaunchKernelGGL(k_loc_heads, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, k0, k1,

@@ -53,21 +53,14 @@ constexpr int kMetaPack = 25;
 // row — (key >> lo8) << rb8 | row.  Digit boundaries are kept (lo8, rb8 multiples of 8), so the
 // counts of key digit p serve packed digit p - lo8/8 + rb8/8; the first active pass packs as it
 // loads, later passes and the consumers read 8 bytes per item instead of 12.
-//
-// bucket_max > 0 (the fused step's Localizer, packed items): when at least two digits vary and
-// no value of the top one holds more than bucket_max items, the sort becomes ONE pass over the
-// top digit — its buckets in key order, each stable in input order — and the Localizer's
-// k_loc_bucket sorts every bucket by the digits below, one block per bucket (sortmeta[30]: 1 |
-// (digits below) << 8, their shifts in [28..29]; the top digit's counts move to counts[0])
+
 __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* diff, int or_and,
                                                    int npasses, int begin_bit, int end_bit,
                                                    unsigned int* meta, uint32_t* parts,
                                                    uint32_t* counts, unsigned int* epoch,
-                                                   int pack_rb8, uint32_t bucket_max,
-                                                   unsigned int* host_nq) {
+                                                   int pack_rb8, unsigned int* host_nq) {
   __shared__ int s_pos[kOsMaxPasses];
   __shared__ int s_nq;
-  __shared__ uint32_t s_max;
   const int t = threadIdx.x;
   if (t == 0) {
     // one epoch counter per lane (which owns the look-back words): tags never repeat
@@ -102,10 +95,8 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
     meta[kMetaPack] = (pack && q > 0) ? (1u | ((unsigned)lo8 << 8) | ((unsigned)pack_rb8 << 16))
                                       : 0u;
     meta[31] = (unsigned)(q & 1);
-    meta[kSortMetaBucket] = 0;
     if (host_nq) *host_nq = (unsigned)q;  // the next sort's launch hint (pinned, vector store)
     s_nq = q;
-    s_max = 0;
   }
   __syncthreads();
   const int nq = s_nq;
@@ -118,26 +109,6 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
   }
   for (int c = 0; c < kOsParts; ++c)
     for (int p = 0; p < kOsDigits; ++p) parts[(c * kOsDigits + p) * 256 + t] = 0;
-  if (bucket_max == 0 || nq < 2 || meta[kMetaPack] == 0u) return;  // block-uniform
-  const uint32_t ct = counts[(nq - 1) * 256 + t];
-  atomicMax(&s_max, ct);
-  __syncthreads();
-  if (s_max > bucket_max) return;  // block-uniform: the LSD passes as planned
-  counts[t] = ct;  // the top digit's counts first (this thread's entry only)
-  if (t == 0) {
-    uint32_t r0 = 0, r1 = 0;
-    for (int r = 0; r < nq - 1; ++r) {
-      const uint32_t sh = meta[r] & 0xFFu;
-      if (r < 4) r0 |= sh << (8 * r); else r1 |= sh << (8 * (r - 4));
-    }
-    meta[kSortMetaRest] = r0;
-    meta[kSortMetaRest + 1] = r1;
-    meta[0] = meta[nq - 1];
-    for (int r = 1; r < kOsMaxPasses; ++r) meta[r] = kOsNone;
-    meta[31] = 1u;
-    meta[kSortMetaBucket] = 1u | ((unsigned)(nq - 1) << 8);
-    if (host_nq) *host_nq = 1u;
-  }
 }
 
 __device__ inline int64_t os_count(int64_t n, const uint32_t* n_dev) {
@@ -417,7 +388,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   const int pack_rb8 = (sizeof(K) == 8 && sizeof(P) == 4) ? (flags >> 8) & 0xFF : 0;
   if (n <= 0 || end_bit <= begin_bit) {
     hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, 0,
-                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0, 0u, nullptr);
+                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0, nullptr);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
@@ -427,7 +398,6 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
     hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)((n + kOsTile - 1) / kOsTile)), dim3(kOsNT),
                        0, L.stream, k0, n, n_dev, begin_bit, npasses, parts);
   }
-  const uint32_t bucket_max = (flags & kSortBucket) && pack_rb8 > 0 ? kSortBucketMax : 0u;
   // kSortHint: the passes beyond the active count of this workspace's previous sort of the same
   // item type (k_os_plan writes it to pinned memory; read here without a wait, so it may be a
   // step old) run on a small looping grid: they are almost always constant digits, whose
@@ -443,8 +413,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
     if (h <= (unsigned)npasses) hint = (int)h;
   }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
-                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8, bucket_max,
-                     host_nq);
+                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8, host_nq);
   for (int q = 0; q < npasses; ++q) {
     const int64_t grid = q < hint ? ntiles : std::min<int64_t>(ntiles, kOsLoopGrid);
 #define DFX_OS_SCATTER(IT, LB)                                                               \

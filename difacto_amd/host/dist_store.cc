@@ -168,6 +168,10 @@ struct GpuDistStore::Core {
   }
   void Wait(int l, int ts) {
     std::unique_lock<std::mutex> lk(mu);
+    // a callback runs on the progress thread, the only thread that completes requests: waiting
+    // there for an unfinished one would hang
+    DFX_HOST_CHECK(t_in_callback_of < 0 || IsDone(l, ts),
+                   "GpuDistStore: Wait on an unfinished request from a request callback");
     cv_done.wait(lk, [&]() { return IsDone(l, ts) || !failure.empty(); });
     DFX_HOST_CHECK(failure.empty(), "GpuDistStore: " + failure);
   }

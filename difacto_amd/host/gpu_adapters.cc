@@ -482,7 +482,8 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
   if (blk.size == 0) {
     // a worker with no rows this round (the sharded store's workers call in step): it takes
     // part in the exchanges with no keys
-    if (job_type == kTraining) store_->Push(keys, Store::kGradient, SArray<real_t>(), SArray<int>());
+    if (job_type == kTraining)
+      store_->Wait(store_->Push(keys, Store::kGradient, SArray<real_t>(), SArray<int>()));
     return;
   }
   prog_.nrows += blk.size;
@@ -499,7 +500,9 @@ void GpuSGDLearner::ProcessBatch(const dmlc::RowBlock<feaid_t>& batch, int job_t
     SArray<real_t> grads(values.size());
     inputs.push_back(SArray<char>(pred));
     loss_->CalcGrad(blk, inputs, &grads);
-    store_->Push(keys, Store::kGradient, grads, V_dim_ > 0 ? lengths : SArray<int>());
+    // the batch is done once its update is applied (sgd_learner.cc:255-259, on_complete): a
+    // caller may read the store's shards (save, progress) right after ProcessBatch returns
+    store_->Wait(store_->Push(keys, Store::kGradient, grads, V_dim_ > 0 ? lengths : SArray<int>()));
   }
 }
 

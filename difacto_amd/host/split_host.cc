@@ -43,9 +43,9 @@ std::vector<int64_t> Offsets(const std::vector<int64_t>& v) {
 }
 
 // buffers a DBuf outgrew: queued work (this step's other phases, the previous step on the
-// side streams) may still use them, so they are freed only when the driver is at a sync point
-// (its destructor) — a growing batch costs memory for a while, not a device-wide wait that
-// would drain the pipelined step's lanes
+// side streams) may still use them, so they are freed only at a point where the driver knows
+// the device idle (GpuSplitStore::Sync, its destructor) — a growing batch costs memory for a
+// while, never a device-wide wait that would drain the pipelined step's lanes
 struct Graveyard {
   std::vector<std::pair<dfx_ctx*, void*>> bufs;
   void Reap() {
@@ -54,7 +54,8 @@ struct Graveyard {
   }
 };
 
-// grow-only device buffer of one context
+// grow-only device buffer of one context; an outgrown buffer goes to the graveyard.  Growth is
+// geometric (at least 2x), so a run whose batches grow retires few buffers
 struct DBuf {
   dfx_ctx* c = nullptr;
   Graveyard* grave = nullptr;
@@ -63,16 +64,9 @@ struct DBuf {
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes <= cap) return p;
-    if (p) {
-      if (grave) {
-        grave->bufs.push_back({c, p});
-      } else {
-        HipCheck(hipDeviceSynchronize(), "sync");  // queued work may still use the old buffer
-        DfxOk(dfx_free(c, p), "dfx_free");
-      }
-    }
+    if (p) grave->bufs.push_back({c, p});
     p = nullptr;
-    cap = bytes + bytes / 8;
+    cap = std::max(bytes + bytes / 8, 2 * cap);
     DfxOk(dfx_malloc(c, &p, cap), "dfx_malloc");
     return p;
   }
@@ -413,6 +407,7 @@ struct GpuSplitStore::Impl {
     iall.resize(L);
     for (int l = 0; l < L; ++l) {
       icnt[l].c = iall[l].c = t->ctx(l);
+      icnt[l].grave = iall[l].grave = &grave;
       icnt[l].ensure(8);
       iall[l].ensure((size_t)8 * N);
     }
@@ -801,6 +796,16 @@ struct GpuSplitStore::Impl {
       Run(pending);
     }
   }
+
+  // the queued step run and every stream the driver uses drained: the outgrown buffers are
+  // free then
+  void Sync() {
+    Flush();
+    for (int l = 0; l < L; ++l) DfxOk(dfx_sync(t->ctx(l)), "dfx_sync");
+    for (auto st : xst) HipCheck(hipStreamSynchronize(st), "sync");
+    for (auto st : yst) HipCheck(hipStreamSynchronize(st), "sync");
+    grave.Reap();
+  }
 };
 
 GpuSplitStore::GpuSplitStore(SplitTransport* t, bool pipelined, uint64_t max_index)
@@ -822,6 +827,8 @@ void GpuSplitStore::Submit(const std::vector<dfx_batch>& batches, int job_type, 
 }
 
 void GpuSplitStore::Flush() { impl_->Flush(); }
+
+void GpuSplitStore::Sync() { impl_->Sync(); }
 
 void GpuSplitStore::AllReduceSum(std::vector<double>* v) { impl_->t->AllReduceSum(v); }
 
@@ -944,6 +951,13 @@ int dfx_split_store_flush(dfx_split_store* s) {
   return Guard([&] {
     if (!s) throw difacto::Error(DFX_ERR_ARG, "null argument");
     s->s->Flush();
+  });
+}
+
+int dfx_split_store_sync(dfx_split_store* s) {
+  return Guard([&] {
+    if (!s) throw difacto::Error(DFX_ERR_ARG, "null argument");
+    s->s->Sync();
   });
 }
 

@@ -107,6 +107,9 @@ class GpuSplitStore {
               const std::vector<float*>& preds = {});
   /** run the queued step */
   void Flush();
+  /** run the queued step and wait for it (every context and stream of the driver); buffers
+   * the driver outgrew are freed here */
+  void Sync();
   /** host sum of v over the processes (after Flush: a collective of every rank) */
   void AllReduceSum(std::vector<double>* v);
   /** rows of a step in K slices (K >= 1; 0: the default, 1): slice h's

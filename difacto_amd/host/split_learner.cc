@@ -57,11 +57,10 @@ struct GpuSplitLearner::Impl {
       nnz = std::max<int64_t>(nnz, b->size ? (int64_t)b->offset[b->size] : 0);
     }
     if (!feeders.empty() && rows <= cap_rows && nnz <= cap_nnz) return;
-    // grow: every queued step must be done with the old staging buffers first
-    if (queued) {
-      DistCheck(dfx_split_store_flush(store), "dfx_split_store_flush");
-      queued = false;
-    }
+    // grow: every queued step must be done with the old staging buffers first (the store's
+    // sync also frees the step buffers it outgrew)
+    if (store) DistCheck(dfx_split_store_sync(store), "dfx_split_store_sync");
+    queued = false;
     for (dfx_ctx* c : ctxs) DfxCheck(dfx_sync(c), "dfx_sync");
     for (dfx_feeder* f : feeders) DfxCheck(dfx_feeder_destroy(f), "dfx_feeder_destroy");
     feeders.assign(L, nullptr);
@@ -79,6 +78,7 @@ struct GpuSplitLearner::Impl {
     for (int l = 0; l < L; ++l) {
       const dmlc::RowBlock<feaid_t>& x = *pend[l];
       const int64_t B = (int64_t)x.size, nnz = B ? (int64_t)x.offset[B] : 0;
+      DFX_HOST_CHECK(B == 0 || x.offset[0] == 0, "split learner: offset[0] must be 0");
       dfx_host_batch hb;
       DfxCheck(dfx_feeder_slot(feeders[l], &hb), "dfx_feeder_slot");
       static_assert(sizeof(size_t) == sizeof(uint64_t), "size_t offsets");

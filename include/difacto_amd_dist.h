@@ -52,6 +52,9 @@ int dfx_split_store_create_loopback(dfx_ctx* const* ctxs, int n, int pipelined,
 int dfx_split_store_submit(dfx_split_store* s, const dfx_batch* batches, int job_type,
                            int push_cnt, float* const* preds);
 int dfx_split_store_flush(dfx_split_store* s);
+/* flush, then wait until every context and stream of the store is idle; buffers the store
+ * outgrew (growing batches) are freed here.  No reference counterpart (a device-memory point) */
+int dfx_split_store_sync(dfx_split_store* s);
 /* a step's rows in `slices` slices (>= 1; 0: the default, one slice):
  * slice h's partials travel while slice h + 1's owner forward runs, and its [XV*p | p] rows
  * while the next slice combines (streams of the driver's own); results do not change */

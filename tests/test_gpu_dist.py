@@ -544,6 +544,31 @@ def test_rsag_step_matches_agg_oracle(name):
         c.close()
 
 
+def test_bench_spawns_its_ranks():
+    """`bench.py --gpus 2` without a launcher starts its two ranks itself (one process per GPU;
+    gloo here, as both share the test box's GPU) and reports them: n_gpus 2, whole-job
+    throughput over both; a launcher whose WORLD_SIZE disagrees with --gpus is refused"""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--batch", "20000", "--key-bits", "20", "--backend", "gloo", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 40000 and out["value"] > 0
+    bad = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1"], cwd=root,
+                         capture_output=True, text=True, timeout=120,
+                         env=dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
 @pytest.mark.parametrize("collective", ["split", "a2a"])
 def test_bench_rccl_collectives_at_world_one(collective):
     """bench.py's sharded path with every exchange forced through RCCL at world size 1 (the

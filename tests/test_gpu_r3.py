@@ -303,37 +303,41 @@ def test_c5_model_drift_bound(H):
     c.close()
 
 
-# ---------------------------------------------------------------- bucket-mode Localizer
-def _ids_of(kind, rng, n):
-    if kind == "uniform":
+# ---------------------------------------------------------------- bucket Localizer
+def _ids_of(kind, rng, n, step):
+    if kind in ("uniform", "valued"):
         return rng.integers(0, 1 << 22, n, dtype=np.uint64)
-    if kind == "narrow":       # 2^12 ids: two key digits vary
+    if kind == "narrow":       # 2^12 ids: few distinct keys, long segments
         return rng.integers(0, 1 << 12, n, dtype=np.uint64)
-    if kind == "wide":         # every key bit varies: packing fails, LSD passes
+    if kind == "wide":         # every key bit varies: items do not pack (key and row apart)
         return rng.integers(0, 1 << 63, n, dtype=np.uint64)
-    if kind == "zipf":         # hot keys: a bucket beyond kSortBucketMax falls back to LSD
+    if kind == "zipf":         # hot keys: buckets beyond the LDS capacity (global-memory passes)
         return D.zipf_keys(rng, n, 1.1, 1 << 20)
     if kind == "fields":       # criteo-parser ids (hash << 12 | field): 39 top-digit values
         return (rng.integers(0, 1 << 40, n, dtype=np.uint64) << np.uint64(12)) | \
             rng.integers(0, 39, n, dtype=np.uint64)
+    if kind == "shift":        # the key range moves every step: the bucket map's hint is stale
+        return rng.integers(0, 1 << (10 + 4 * step), n, dtype=np.uint64)
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("kind", ["uniform", "narrow", "wide", "zipf", "fields"])
+@pytest.mark.parametrize("kind", ["uniform", "valued", "narrow", "wide", "zipf", "fields",
+                                  "shift"])
 def test_bucket_localizer_equals_lsd(H, kind):
-    """The fused step's Localizer in bucket mode (one global pass over the top varying digit,
-    then one block per bucket: loc_bucket=1 with 256 threads, 2 with 1024) against the LSD
-    passes over every digit (loc_bucket=0): predictions, loss and AUC identical every step, the
-    model identical at the end, and both equal to the oracle within the usual tolerances.
-    Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one."""
+    """The fused step's Localizer as a bucket sort (locbucket.hip, loc_bucket=1, the default)
+    against the onesweep radix sort (loc_bucket=0): predictions, loss and AUC identical every
+    step, the model identical at the end, and both equal to the oracle within the usual
+    tolerances.  Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one; skewed and moving
+    key ranges exercise the global-memory bucket passes and the radix fallback."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=m, **cfg) for m in (0, 1, 2)]
+    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=m, **cfg) for m in (0, 1)]
     up = O.Updater(**cfg)
     rng = np.random.default_rng(9)
-    for step in range(4):
+    for step in range(5):
         rows = 3000 if step == 3 else 60000
-        blk = D.synthetic(rows, 39, 2, ragged=(step == 3), seed=80 + step)
-        blk = D.RowBlock(blk.offs, _ids_of(kind, rng, blk.nnz), None, blk.labels)
+        blk = D.synthetic(rows, 39, 2, ragged=(step == 3), binary=(kind != "valued"),
+                          seed=80 + step)
+        blk = D.RowBlock(blk.offs, _ids_of(kind, rng, blk.nnz, step), blk.vals, blk.labels)
         loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
                                          push_cnt=(step < 2), want_pred=True)
         preds, progs = [], []
@@ -342,9 +346,9 @@ def test_bucket_localizer_equals_lsd(H, kind):
             H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pr)
             preds.append(pr.cpu().numpy().view(np.uint32))
             progs.append(H.progress(c))
-        assert np.array_equal(preds[0], preds[1]) and np.array_equal(preds[0], preds[2]), step
-        assert progs[0]["loss"] == progs[1]["loss"] == progs[2]["loss"], step
-        assert progs[0]["auc"] == progs[1]["auc"] == progs[2]["auc"], step
+        assert np.array_equal(preds[0], preds[1]), step
+        assert progs[0]["loss"] == progs[1]["loss"], step
+        assert progs[0]["auc"] == progs[1]["auc"], step
         assert abs(progs[1]["loss"] - loss) <= 1e-4 * abs(loss), (step, progs[1]["loss"], loss)
         assert abs(progs[1]["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     uniq, _, _ = O.localize(blk.offs, blk.ids)
@@ -353,8 +357,8 @@ def test_bucket_localizer_equals_lsd(H, kind):
         assert np.array_equal(l.cpu().numpy(), vs[0][1].cpu().numpy())
         assert np.array_equal(v.cpu().numpy().view(np.uint32), vs[0][0].cpu().numpy().view(np.uint32))
     st = [H.Store(c).stats() for c in cs]
-    assert st[0]["n_keys"] == st[1]["n_keys"] == st[2]["n_keys"] == up.size()
-    assert st[0]["seed"] == st[1]["seed"] == st[2]["seed"] == up.seed
+    assert st[0]["n_keys"] == st[1]["n_keys"] == up.size()
+    assert st[0]["seed"] == st[1]["seed"] == up.seed
     for c in cs:
         c.close()
 

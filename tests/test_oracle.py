@@ -3,6 +3,8 @@
 Every expected value below is read from tests/golden/reference_known_answers.json, which
 transcribes the reference's gtest assertions (file:line in that JSON).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -148,3 +150,17 @@ def test_cpu_ref_matches_oracle(nt):
     assert n == 4000 and dt > 0 and abs(loss - tot) <= 1e-4 * abs(tot)
     assert up.size() == ref.size() and up.seed == ref.seed
     ref.close()
+
+
+def test_device_expf_equals_glibc():
+    """csrc/expf.h (glibc's expf restated for the device: CalcGrad's p, fm_loss.h:159-164)
+    equals the host's expf bit for bit on a sample of every 97th float bit pattern (the full
+    2^32 sweep: `build/expf_check 1`, 0 differences)"""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "build", "expf_check")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "build/expf_check"], cwd=root)
+    r = subprocess.run([exe, "97"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("0 of "), r.stdout
