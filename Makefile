@@ -29,7 +29,7 @@ RBENCH = build/reader_bench
 DISTLIB = difacto_amd/libdfx_dist.so
 
 all: $(LIB) $(DISTLIB) oracle $(HOSTBIN) $(TRAINBIN) $(READERBIN) $(GENBIN) $(CONVBIN) $(RBENCH) \
-  build/expf_check
+  build/expf_check build/locbench
 
 $(RBENCH): difacto_amd/host/reader.cc tools/reader_bench.cc difacto_amd/host/reader.h
 	@mkdir -p build
@@ -91,6 +91,12 @@ $(LIB): $(OBJS)
 
 oracle:
 	$(MAKE) -s -C oracle
+
+# measurement: the fused step's Localizer alone (links the library's internals)
+build/locbench: tools/locbench.hip $(LIB) $(HDRS)
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -Wno-unused-result -o $@ $< -Ldifacto_amd \
+	  -ldifacto_amd -Wl,-rpath,'$$ORIGIN/../difacto_amd'
 
 # test infrastructure: the device's expf (csrc/expf.h) against the host's glibc expf
 build/expf_check: tools/expf_check.hip $(CSRC)/expf.h

@@ -58,7 +58,9 @@ struct Kw {
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
   int sort_pack = 1;    // sort_pack=0: the Localizer sorts 12-byte (key, row) pairs
-  int auc_radix = 1;    // auc_sort=merge: the AUC lane's tile sorts + merge rounds
+  // auc_sort=bucket (default): the AUC lane's bucket sort (locbucket.hip); radix: onesweep
+  // passes; merge: tile sorts + merge rounds
+  int auc_sort = 2;
   int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
   int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
   // slot_layout=auto (default): fat slots (entry + V in one 64/128-byte slot, common.h Table)
@@ -76,6 +78,9 @@ struct Kw {
   // bucket sort — histogram, scatter into key-range buckets, one LDS sort per bucket
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
   int loc_bucket = 1;
+  // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_bucket skipped — 1 the LDS
+  // sort, 2 the look-back, 4 the outputs; the Localizer's results are then wrong
+  int lb_diag = 0;
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -176,6 +181,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     }
     else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
+    else if (k == "lb_diag") kw->lb_diag = atoi(cv);
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
       if (kw->fwd_lanes != 0 && kw->fwd_lanes != 2 && kw->fwd_lanes != 4) {
@@ -234,9 +240,10 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else { set_error("unknown slot_layout: " + v + " (auto|split|fat)"); return DFX_ERR_ARG; }
     }
     else if (k == "auc_sort") {
-      if (v == "radix") kw->auc_radix = 1;
-      else if (v == "merge") kw->auc_radix = 0;
-      else { set_error("unknown auc_sort: " + v + " (radix|merge)"); return DFX_ERR_ARG; }
+      if (v == "bucket") kw->auc_sort = 2;
+      else if (v == "radix") kw->auc_sort = 1;
+      else if (v == "merge") kw->auc_sort = 0;
+      else { set_error("unknown auc_sort: " + v + " (bucket|radix|merge)"); return DFX_ERR_ARG; }
     }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
@@ -368,7 +375,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->autogrow = kw.autogrow;
   c->dist_sum = kw.dist_sum;
   c->sort_pack = kw.sort_pack;
-  c->auc_radix = kw.auc_radix != 0;
+  c->auc_sort = kw.auc_sort;
   c->sort_items = kw.sort_items;
   c->sort_lookback = kw.sort_lookback;
   c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);
@@ -390,6 +397,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fwd_lanes = kw.fwd_lanes;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;
+  c->lb_diag = kw.lb_diag;
   c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {

@@ -16,10 +16,10 @@
 //                 key's varying bits above the row (binary data) or the position (valued data,
 //                 {value, row} beside it) in one u64 when they fit; else the key and the row /
 //                 position travel apart
-//   k_lb_bucket   one block per bucket, in bucket order (tickets): the bucket sorted in LDS —
-//                 bitonic, on the whole item: (key, row) resp. (key, position) is a total order
-//                 and equal items are the same occurrence data, so the scatter's order inside a
-//                 bucket never shows — then its heads (CountUniqIndex's run-length pass), the
+//   k_lb_bucket   one block per bucket, in bucket order: the bucket sorted in LDS — LSD radix
+//                 over the digits that vary inside it, on the whole item: (key, row) resp.
+//                 (key, position) is a total order and equal items are the same occurrence
+//                 data, so the scatter's order inside a bucket never shows — then its heads (CountUniqIndex's run-length pass), the
 //                 heads of the buckets before it by decoupled look-back (RemapIndex's ranks),
 //                 and the outputs: per rank its key and segment start, per occurrence in sorted
 //                 order its row (and value).  A bucket beyond the LDS capacity (skewed keys, or a
@@ -44,6 +44,7 @@ constexpr int64_t kLbMaxRows = 2048; // rows per hist / scatter tile (their offs
 constexpr int kLbIT = 8;             // items per thread of a chunk (heads, the global-memory passes)
 constexpr unsigned kLbOverRadix = 2; // more buckets than this over kLbCap: radix Localizer next
 constexpr unsigned kLbRetry = 64;    // ... and the bucket Localizer tried again after this many
+constexpr int kLbBigBlocks = 64;     // blocks sorting the oversize buckets through global memory
 
 struct LbArgs {
   int64_t B, nnz;
@@ -71,6 +72,7 @@ struct LbArgs {
   uint32_t* occ_row;
   float* occ_x;
   unsigned int* hint;    // pinned: Workspace::lb_hint
+  int diag;              // Context::lb_diag (measurement only)
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -135,7 +137,6 @@ __global__ void k_lb_init(DevState* ds) {
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
   unsigned* meta = ds->sortmeta;
   meta[kSortMetaEpoch] = ++ds->sort_epoch;  // tags this Localizer's look-back words
-  meta[kSortMetaHwTile] = 0;                // bucket tickets
   meta[kSortMetaCpTile] = 0;                // the chunk plan's tile tickets
 }
 
@@ -162,7 +163,7 @@ __device__ inline unsigned long long lb_wave_max(unsigned long long v) {
   return v;
 }
 
-constexpr int kLbUnr = 4;  // ids in flight per thread
+constexpr int kLbUnr = 8;  // ids in flight per thread
 
 __global__ __launch_bounds__(kLbNT) void k_lb_hist(LbArgs a) {
   extern __shared__ uint32_t lb_dyn[];
@@ -414,88 +415,192 @@ __device__ void lb_global_pass(const uint64_t* Xk, const uint32_t* Xq, const uin
   __syncthreads();
 }
 
+// ---- a bucket's stable LSD radix sort in LDS (n <= kLbCap items) ------------------------------
+// The items stay in registers, kLbIT per thread — thread (wave w, lane l) holds positions
+// w * 64 * kLbIT + c * 64 + l, c < kLbIT — and each pass over an 8-bit digit that varies inside
+// the bucket ranks them with wave ballots (wave w's items before wave w+1's, in order: stable),
+// scatters them through the LDS buffers and reads them back in the new order; the last pass
+// leaves the sorted bucket in the LDS buffers.  q's digits go first when the items are not packed
+// (q is the less significant part of (key, q)).  About 16 bytes of LDS traffic per item and pass,
+// where a bitonic network over 1024 items moved ~880 (LDS-bound at 4096 buckets: ~220 us).
+constexpr int kLbRadixIT = kLbCap / kLbNT;  // 8
+
 template <bool Q, bool S>
-__global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
-  __shared__ uint64_t sk[kLbCap];
-  __shared__ uint32_t sq[Q ? kLbCap : 1];
-  __shared__ uint64_t ss[S ? kLbCap : 1];
-  __shared__ uint32_t wcnt[kLbWaves][256];
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t lds[kLbWaves + 1];
-  __shared__ uint32_t s_b, s_pre;
-  __shared__ unsigned long long s_red[4][kLbWaves];
-  static_assert(kLbNT == 256, "one thread per 8-bit digit in the global-memory passes");
-  DevState* ds = a.ds;
-  unsigned* meta = ds->sortmeta;
-  const int t = threadIdx.x;
-  if (t == 0) s_b = atomicAdd(&meta[kSortMetaHwTile], 1u);
+__device__ inline void lb_lds_sort(uint64_t (&k)[kLbRadixIT], uint32_t (&q)[kLbRadixIT],
+                                   uint64_t (&sv)[kLbRadixIT], int n, bool hasq,
+                                   uint64_t* sk, uint32_t* sq, uint64_t* ss,
+                                   uint32_t (*wcnt)[256], uint32_t* lds,
+                                   unsigned long long (*red)[kLbWaves]) {
+  const int t = threadIdx.x, w = t / kWave, l = lane_id();
+  const int wb = w * kWave * kLbRadixIT;
+  // the digits that vary inside the bucket
+  unsigned long long kor = 0, kand = ~0ull, qor = 0, qand = ~0ull;
+#pragma unroll
+  for (int c = 0; c < kLbRadixIT; ++c) {
+    if (wb + c * kWave + l < n) {
+      kor |= k[c];
+      kand &= k[c];
+      if (Q && hasq) {
+        qor |= q[c];
+        qand &= q[c];
+      }
+    }
+  }
+  kor = lb_wave_or(kor);
+  kand = lb_wave_and(kand);
+  if (Q) {
+    qor = lb_wave_or(qor);
+    qand = lb_wave_and(qand);
+  }
+  if (l == 0) {
+    red[0][w] = kor;
+    red[1][w] = kand;
+    red[2][w] = qor;
+    red[3][w] = qand;
+  }
   __syncthreads();
-  const uint32_t b = s_b;
-  const uint32_t nbk = 1u << a.wbits;
-  if (b >= nbk) return;  // every later ticket exits too: no waiter is left behind
-  const int64_t start = a.bstart[b];
-  const int64_t n = (int64_t)a.bstart[b + 1] - start;
-  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
-  const LbPack p = lb_pack(ds, qmax);
-  const bool hasq = !p.packed;
-  const bool fast = n <= kLbCap && (p.packed || Q);
-  // where the sorted bucket is read from by the heads / outputs below
-  const uint64_t* gk = a.kbuf + start;
-  const uint32_t* gq = a.qbuf + start;
-  const uint64_t* gs = a.sbuf + start;
-  if (fast) {
-    int n2 = 2;
-    while (n2 < n) n2 <<= 1;
-    for (int i = t; i < n2; i += kLbNT) {
-      if (i < n) {
-        sk[i] = ldnt(gk + i, a.nt != 0);
-        if (Q && hasq) sq[i] = gq[i];
-        if (S) ss[i] = gs[i];
-      } else {  // padding sorts last: no real item is ~0 (lb_pack)
-        sk[i] = ~0ull;
-        if (Q && hasq) sq[i] = ~0u;
+  for (int i = 0; i < kLbWaves; ++i) {
+    kor |= red[0][i];
+    kand &= red[1][i];
+    qor |= red[2][i];
+    qand &= red[3][i];
+  }
+  const unsigned long long kvary = kor ^ kand, qvary = (Q && hasq) ? (qor ^ qand) : 0ull;
+  int last = -1;  // the last active pass (0..3: q's digits, 4..11: the key's)
+  for (int pass = 0; pass < 12; ++pass) {
+    const unsigned long long vary = pass < 4 ? qvary : kvary;
+    const int shift = 8 * (pass < 4 ? pass : pass - 4);
+    if ((vary >> shift) & 255ull) last = pass;
+  }
+  if (last < 0) {  // one item value (or none): in place
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {
+      const int idx = wb + c * kWave + l;
+      if (idx < n) {
+        sk[idx] = k[c];
+        if (Q && hasq) sq[idx] = q[c];
+        if (S) ss[idx] = sv[c];
       }
     }
     __syncthreads();
-    for (int size = 2; size <= n2; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int i = t; i < (n2 >> 1); i += kLbNT) {
-          const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
-          const int hi = lo + stride;
-          const int x = (lo & size) == 0 ? lo : hi;  // x must not exceed y
-          const int y = x == lo ? hi : lo;
-          const uint64_t kx = sk[x], ky = sk[y];
-          bool sw = kx > ky;
-          if (Q && hasq && kx == ky) sw = sq[x] > sq[y];
-          if (sw) {
-            sk[x] = ky;
-            sk[y] = kx;
-            if (Q && hasq) {
-              const uint32_t qx = sq[x];
-              sq[x] = sq[y];
-              sq[y] = qx;
-            }
-            if (S) {
-              const uint64_t sx = ss[x];
-              ss[x] = ss[y];
-              ss[y] = sx;
-            }
-          }
-        }
-        __syncthreads();
+    return;
+  }
+  for (int pass = 0; pass <= last; ++pass) {
+    const bool on_q = pass < 4;
+    const unsigned long long vary = on_q ? qvary : kvary;
+    const int shift = 8 * (on_q ? pass : pass - 4);
+    if (((vary >> shift) & 255ull) == 0) continue;
+#pragma unroll
+    for (int i = 0; i < 256 / kWave; ++i) wcnt[w][i * kWave + l] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t dr[kLbRadixIT];
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {
+      const bool valid = wb + c * kWave + l < n;
+      const uint32_t d = !valid ? 0u : on_q ? (q[c] >> shift) & 255u
+                                            : (uint32_t)(k[c] >> shift) & 255u;
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int bt = 0; bt < 8; ++bt) {
+        const bool bit = (d >> bt) & 1u;
+        const uint64_t mb = __ballot(valid && bit);
+        peers &= bit ? mb : ~mb;
+      }
+      if (!valid) peers = 0;
+      const uint32_t rk = (uint32_t)__popcll(peers & lanemask_lt());
+      const uint32_t old = valid ? wcnt[w][d] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (valid && rk == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+      dr[c] = d | ((old + rk) << 8);
+    }
+    __syncthreads();
+    {  // digit t: the waves' exclusive offsets, then the digit's start in the bucket
+      uint32_t run = 0;
+#pragma unroll
+      for (int i = 0; i < kLbWaves; ++i) {
+        const uint32_t x = wcnt[i][t];
+        wcnt[i][t] = run;
+        run += x;
+      }
+      const uint32_t st = block_excl_scan<kLbNT>(run, lds, nullptr);
+#pragma unroll
+      for (int i = 0; i < kLbWaves; ++i) wcnt[i][t] += st;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {
+      if (wb + c * kWave + l < n) {
+        const uint32_t pos = wcnt[w][dr[c] & 255u] + (dr[c] >> 8);
+        sk[pos] = k[c];
+        if (Q && hasq) sq[pos] = q[c];
+        if (S) ss[pos] = sv[c];
       }
     }
-  } else if (n > 1) {
-    // through global memory: stable 8-bit LSD over the digits that vary inside the bucket — q's
-    // first (the less significant part of an unpacked item), then the key's
+    __syncthreads();
+    if (pass == last) break;  // the sorted bucket stays in LDS
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {
+      const int idx = wb + c * kWave + l;
+      if (idx < n) {
+        k[c] = sk[idx];
+        if (Q && hasq) q[c] = sq[idx];
+        if (S) sv[c] = ss[idx];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Buckets the LDS sort cannot take — beyond kLbCap items (skewed keys, or a key range that
+// moved), or unpacked items while the launch expected packed ones (q_lds = 0) — sorted in place by
+// a few looping blocks, through global memory, before k_lb_bucket reads them: stable 8-bit LSD
+// passes over the digits that vary inside the bucket, q's first (the less significant part of an
+// unpacked item), then the key's; the result copied back when it ends in the scratch buffers.
+// Kept out of k_lb_bucket, whose registers would otherwise be sized for it.
+__device__ inline bool lb_needs_global(int64_t n, bool packed, int q_lds) {
+  return n > kLbCap || (!packed && !q_lds);
+}
+
+template <bool S>
+__global__ __launch_bounds__(kLbNT) void k_lb_big(LbArgs a, int q_lds) {
+  __shared__ uint32_t wcnt[kLbWaves][256];
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t lds[kLbWaves + 1];
+  __shared__ unsigned long long s_red[4][kLbWaves];
+  const int t = threadIdx.x;
+  const uint32_t nbk = 1u << a.wbits;
+  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const LbPack p = lb_pack(a.ds, qmax);
+  const bool hasq = !p.packed;
+  __shared__ uint32_t s_list[kLbNT];
+  __shared__ uint32_t s_nlist;
+  uint32_t listed = 0;  // buckets needing this kernel so far; block i takes the list's i, i + G, ...
+  for (uint32_t b0 = 0; b0 < nbk; b0 += kLbNT) {
+    const uint32_t bb = b0 + t;
+    const int64_t nb = bb < nbk ? (int64_t)a.bstart[bb + 1] - (int64_t)a.bstart[bb] : 0;
+    const uint32_t need = (bb < nbk && nb > 1 && lb_needs_global(nb, p.packed, q_lds)) ? 1u : 0u;
+    uint32_t cnt;
+    const uint32_t ex = block_excl_scan<kLbNT>(need, lds, &cnt);
+    if (t == 0) s_nlist = 0;
+    __syncthreads();
+    if (need && (listed + ex) % gridDim.x == blockIdx.x) s_list[atomicAdd(&s_nlist, 1u)] = bb;
+    __syncthreads();
+    listed += cnt;
+    const uint32_t nl = s_nlist;
+    // (the order of a block's own buckets does not matter: each is sorted on its own)
+    for (uint32_t li = 0; li < nl; ++li) {
+    const uint32_t b = s_list[li];
+    const int64_t start = a.bstart[b];
+    const int64_t n = (int64_t)a.bstart[b + 1] - start;
     unsigned long long kor = 0, kand = ~0ull, qor = 0, qand = ~0ull;
     for (int64_t i = t; i < n; i += kLbNT) {
-      const uint64_t x = gk[i];
+      const uint64_t x = a.kbuf[start + i];
       kor |= x;
       kand &= x;
       if (hasq) {
-        qor |= gq[i];
-        qand &= gq[i];
+        qor |= a.qbuf[start + i];
+        qand &= a.qbuf[start + i];
       }
     }
     kor = lb_wave_or(kor);
@@ -522,6 +627,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
     uint64_t* Yk = a.kscr + start;
     uint32_t* Yq = hasq ? a.qscr + start : nullptr;
     uint64_t* Ys = S ? a.sscr + start : nullptr;
+    int np = 0;
     for (int pass = 0; pass < 12; ++pass) {
       const bool on_q = pass < 4;
       const int shift = 8 * (on_q ? pass : pass - 4);
@@ -531,17 +637,80 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
       uint64_t* tk = Xk; Xk = Yk; Yk = tk;
       uint32_t* tq = Xq; Xq = Yq; Yq = tq;
       uint64_t* ts = Xs; Xs = Ys; Ys = ts;
+      ++np;
     }
-    gk = Xk;
-    gq = Xq;
-    gs = Xs;
+    if (np & 1) {  // the sorted bucket sits in the scratch buffers: back into place
+      for (int64_t i = t; i < n; i += kLbNT) {
+        Yk[i] = Xk[i];
+        if (hasq) Yq[i] = Xq[i];
+        if (S) Ys[i] = Xs[i];
+      }
+    }
+    __syncthreads();
+    }
+    __syncthreads();  // s_list is rewritten by the next chunk
   }
-  auto item = [&](int64_t i) -> uint64_t { return fast ? sk[i] : gk[i]; };
+}
+
+template <bool Q, bool S>
+__global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
+  __shared__ uint64_t sk[kLbCap];
+  __shared__ uint32_t sq[Q ? kLbCap : 1];
+  __shared__ uint64_t ss[S ? kLbCap : 1];
+  __shared__ uint32_t wcnt[kLbWaves][256];
+  __shared__ unsigned long long s_red[4][kLbWaves];
+  __shared__ uint32_t lds[kLbWaves + 1];
+  __shared__ uint32_t s_lb[3 * kLbWaves];
+  DevState* ds = a.ds;
+  unsigned* meta = ds->sortmeta;
+  const int t = threadIdx.x;
+  // bucket = block: workgroups are dispatched in index order, so every bucket a block looks back
+  // on is running or done (a ticket counter would serialise 4096 blocks on one word: ~88
+  // returning atomics per us, MI355X_MICROARCH.md 'dequeue')
+  const uint32_t b = blockIdx.x;
+  const uint32_t nbk = 1u << a.wbits;
+  const int64_t start = a.bstart[b];
+  const int n = (int)((int64_t)a.bstart[b + 1] - start);
+  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const LbPack p = lb_pack(ds, qmax);
+  const bool hasq = !p.packed;
+  // sorted in LDS here, or already in place (k_lb_big)
+  const bool fast = !lb_needs_global(n, p.packed, Q ? 1 : 0);
+  const uint64_t* gk = a.kbuf + start;
+  const uint32_t* gq = a.qbuf + start;
+  const uint64_t* gs = a.sbuf + start;
+  if (fast) {
+    uint64_t kr[kLbRadixIT], sr[kLbRadixIT];
+    uint32_t qr[kLbRadixIT];
+    const int wb = (t / kWave) * kWave * kLbRadixIT + lane_id();
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {  // every load in flight at once
+      const int i = wb + c * kWave;
+      kr[c] = i < n ? ldnt(gk + i, a.nt != 0) : 0ull;
+      qr[c] = (Q && hasq && i < n) ? gq[i] : 0u;
+      sr[c] = (S && i < n) ? gs[i] : 0ull;
+    }
+    if (a.diag & 1) {  // (measurement only) no sort: the items as they came
+#pragma unroll
+      for (int c = 0; c < kLbRadixIT; ++c) {
+        const int i = wb + c * kWave;
+        if (i < n) {
+          sk[i] = kr[c];
+          if (Q && hasq) sq[i] = qr[c];
+          if (S) ss[i] = sr[c];
+        }
+      }
+      __syncthreads();
+    } else {
+      lb_lds_sort<Q, S>(kr, qr, sr, n, hasq, sk, sq, ss, wcnt, lds, s_red);
+    }
+  }
+  auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
   // ---- heads: an item whose key differs from the one before it (the bucket's first always);
   // a segment longer than kChunkOcc raises the chunk plan's gate
   uint32_t mine = 0;
   bool longseg = false;
-  for (int64_t i = t; i < n; i += kLbNT) {
+  for (int i = t; i < n; i += kLbNT) {
     const uint64_t kb = lb_keybits(p, item(i));
     mine += (i == 0 || kb != lb_keybits(p, item(i - 1))) ? 1u : 0u;
     if (i >= kChunkOcc && kb == lb_keybits(p, item(i - kChunkOcc))) longseg = true;
@@ -551,15 +720,18 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
     atomicOr(&ds->n_init, 1u);
   uint32_t tot;
   (void)block_excl_scan<kLbNT>(mine, lds, &tot);
-  uint32_t rank0 = tile_lookback(a.hstat, (int64_t)b, hw_tag(meta), tot, &ds->err, &s_pre);
+  uint32_t rank0 = (a.diag & 2) ? 0u
+                                 : block_lookback<kLbNT>(a.hstat, (int64_t)b, hw_tag(meta), tot,
+                                                         &ds->err, s_lb);
+  if (a.diag & 4) return;
   // ---- outputs, per thread kLbIT consecutive items of a chunk
   const uint64_t qmask = p.rb ? (~0ull >> (64 - p.rb)) : 0ull;
-  for (int64_t c0 = 0; c0 < n; c0 += (int64_t)kLbNT * kLbIT) {
-    const int64_t ib = c0 + (int64_t)t * kLbIT;
+  for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
+    const int ib = c0 + t * kLbIT;
     uint32_t h[kLbIT], s = 0;
 #pragma unroll
     for (int j = 0; j < kLbIT; ++j) {
-      const int64_t i = ib + j;
+      const int i = ib + j;
       h[j] = (i < n && (i == 0 || lb_keybits(p, item(i)) != lb_keybits(p, item(i - 1)))) ? 1u
                                                                                         : 0u;
       s += h[j];
@@ -568,24 +740,25 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
     uint32_t incl = block_excl_scan<kLbNT>(s, lds, &ctot) + rank0;
 #pragma unroll
     for (int j = 0; j < kLbIT; ++j) {
-      const int64_t i = ib + j;
-      if (i >= n) break;
-      incl += h[j];
-      const uint64_t it = item(i);
-      if (h[j]) {
-        const uint64_t key = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
-        if (a.uniq) a.uniq[incl - 1] = key;
-        if (a.segstart) a.segstart[incl - 1] = (uint32_t)(start + i);
+      const int i = ib + j;
+      if (i < n) {
+        incl += h[j];
+        const uint64_t it = item(i);
+        if (h[j]) {
+          const uint64_t key = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
+          if (a.uniq) a.uniq[incl - 1] = key;
+          if (a.segstart) a.segstart[incl - 1] = (uint32_t)(start + i);
+        }
+        uint32_t row;
+        if (S) {
+          const uint64_t sv = fast ? ss[i] : gs[i];
+          row = (uint32_t)(sv >> 32);
+          if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sv);
+        } else {
+          row = p.packed ? (uint32_t)(it & qmask) : (fast ? sq[i] : gq[i]);
+        }
+        a.occ_row[start + i] = row;
       }
-      uint32_t row;
-      if (S) {
-        const uint64_t sv = fast ? ss[i] : gs[i];
-        row = (uint32_t)(sv >> 32);
-        if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sv);
-      } else {
-        row = p.packed ? (uint32_t)(it & qmask) : (fast ? sq[i] : gq[i]);
-      }
-      a.occ_row[start + i] = row;
     }
     rank0 += ctot;
   }
@@ -653,6 +826,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.uniq = o.uniq; a.segstart = o.segstart; a.occ_row = o.occ_row;
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
+  a.diag = c->lb_diag;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
   hipLaunchKernelGGL(k_lb_hist, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
                      L.stream, a);
@@ -669,6 +843,10 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   // do not pack while the launch expected packed ones sorts through global memory: correct)
   const bool q_lds = hint[2] == 2u;
   const dim3 bg(nbk), bb(kLbNT);
+  if (valued)
+    hipLaunchKernelGGL(k_lb_big<true>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_lb_big<false>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   if (valued) {
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, true>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, true>), bg, bb, 0, L.stream, a);
@@ -676,6 +854,371 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, false>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, false>), bg, bb, 0, L.stream, a);
   }
+  DFX_HIP(hipGetLastError());
+  *used = true;
+  return DFX_OK;
+}
+
+// ---- BinClassMetric::AUC (src/loss/bin_class_metric.h:35-57) by the same bucket sort -------
+// The snapshot's items (orderable pred << 32 | row << 1 | label) go to buckets by a monotone map
+// of the prediction's value, linear over the previous snapshot's range (k_ab_hist,
+// k_lb_colscan, k_ab_scatter); one block per bucket in bucket order sorts its items in LDS —
+// the row in the item makes (pred, row) a total order: the stable tie break of the radix AUC —
+// counts its positives, finds the positives of the buckets before it by decoupled look-back,
+// and adds, per negative, the positives ranked below it (k_ab_bucket).  The area is a sum of
+// integers, exact in double in any order; the last block to finish turns it into AUC * n
+// (k_auc_final's rules) and leaves the lane's state ready for the next snapshot.  Four
+// launches (+ k_ab_big for oversize buckets) where the radix lane takes ~10 latency-bound ones.
+constexpr int kAbTileItems = 4096;
+
+struct AbArgs {
+  int64_t B, ntiles;
+  const uint32_t* key;  // orderable pred (metric.hip k_auc_keys' form)
+  const uint32_t* lab;  // label > 0
+  int wbits;
+  uint32_t* tilecnt;
+  uint32_t* totals;
+  uint32_t* bstart;
+  uint64_t* kbuf;
+  uint64_t* kscr;
+  DevState* ds;
+  unsigned long long* hstat;
+  double* out;
+  int accumulate;
+  unsigned int* hint;
+};
+
+__device__ inline float ab_value(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// bucket(key): linear in the prediction's value over the previous snapshot's [kmin, kmax]
+// (clamped outside it: NaN and infinities sit at the ends of the key order), or the key's top
+// bits before any snapshot; monotone in the key either way
+struct AbMap {
+  uint32_t kmin, kmax, nbk;
+  int shift;
+  bool linear;
+  double vmin, scale;
+};
+__device__ inline AbMap ab_map(const DevState* ds, int wbits) {
+  AbMap m;
+  m.nbk = 1u << wbits;
+  m.shift = 32 - wbits;
+  m.linear = false;
+  m.kmin = ds->auc_pk_min;
+  m.kmax = ds->auc_pk_max;
+  if (ds->auc_pk_valid && m.kmax > m.kmin) {
+    const double lo = ab_value(m.kmin), hi = ab_value(m.kmax);
+    if (hi > lo && hi - lo < 1e300) {
+      m.linear = true;
+      m.vmin = lo;
+      m.scale = (double)m.nbk / (hi - lo);
+    }
+  }
+  return m;
+}
+__device__ inline uint32_t ab_bucket(uint32_t k, const AbMap& m) {
+  if (!m.linear) return k >> m.shift;
+  if (k <= m.kmin) return 0u;
+  if (k >= m.kmax) return m.nbk - 1u;
+  const double x = ((double)ab_value(k) - m.vmin) * m.scale;
+  const uint32_t b = x > 0.0 ? (uint32_t)x : 0u;
+  return b < m.nbk ? b : m.nbk - 1u;
+}
+
+__global__ __launch_bounds__(kLbNT) void k_ab_hist(AbArgs a) {
+  extern __shared__ uint32_t lb_dyn[];
+  uint32_t* hist = lb_dyn;
+  __shared__ uint32_t red[2][kLbWaves];
+  const AbMap m = ab_map(a.ds, a.wbits);
+  const int t = threadIdx.x;
+  for (uint32_t d = t; d < m.nbk; d += kLbNT) hist[d] = 0;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kAbTileItems;
+  const int64_t i1 = i0 + kAbTileItems < a.B ? i0 + kAbTileItems : a.B;
+  uint32_t kmax = 0, kmin_inv = 0;
+  for (int64_t i = i0 + t; i < i1; i += kLbNT) {
+    const uint32_t k = a.key[i];
+    kmax = k > kmax ? k : kmax;
+    kmin_inv = ~k > kmin_inv ? ~k : kmin_inv;
+    atomicAdd(&hist[ab_bucket(k, m)], 1u);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t x = __shfl_xor(kmax, off, kWave), y = __shfl_xor(kmin_inv, off, kWave);
+    kmax = x > kmax ? x : kmax;
+    kmin_inv = y > kmin_inv ? y : kmin_inv;
+  }
+  if (lane_id() == 0) {
+    red[0][t / kWave] = kmax;
+    red[1][t / kWave] = kmin_inv;
+  }
+  __syncthreads();
+  uint32_t* dst = a.tilecnt + (size_t)blockIdx.x * m.nbk;
+  for (uint32_t d = t; d < m.nbk; d += kLbNT) dst[d] = hist[d];
+  if (t == 0) {
+    for (int w = 1; w < kLbWaves; ++w) {
+      kmax = red[0][w] > kmax ? red[0][w] : kmax;
+      kmin_inv = red[1][w] > kmin_inv ? red[1][w] : kmin_inv;
+    }
+    atomicMax(&a.ds->auc_kmax, kmax);
+    atomicMax(&a.ds->auc_kmin_inv, kmin_inv);
+  }
+}
+
+__global__ __launch_bounds__(kLbNT) void k_ab_scatter(AbArgs a) {
+  extern __shared__ uint32_t lb_dyn[];
+  __shared__ uint32_t lds[kLbWaves + 1];
+  const AbMap m = ab_map(a.ds, a.wbits);
+  uint32_t* cur = lb_dyn;
+  const int t = threadIdx.x;
+  const uint32_t per = (m.nbk + kLbNT - 1) / kLbNT;
+  uint32_t mine = 0, over = 0;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < m.nbk) {
+      const uint32_t c = a.totals[d];
+      mine += c;
+      over += c > (uint32_t)kLbCap ? 1u : 0u;
+    }
+  }
+  uint32_t total;
+  uint32_t ex = block_excl_scan<kLbNT>(mine, lds, &total);
+  const uint32_t* pre = a.tilecnt + (size_t)blockIdx.x * m.nbk;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < m.nbk) {
+      cur[d] = ex + pre[d];
+      if (blockIdx.x == 0) a.bstart[d] = ex;
+      ex += a.totals[d];
+    }
+  }
+  if (blockIdx.x == 0) {
+    uint32_t nover;
+    (void)block_excl_scan<kLbNT>(over, lds, &nover);
+    if (t == 0) {
+      a.bstart[m.nbk] = total;
+      a.hint[0] = nover;  // pinned host word, vector store
+    }
+  }
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kAbTileItems;
+  const int64_t i1 = i0 + kAbTileItems < a.B ? i0 + kAbTileItems : a.B;
+  for (int64_t i = i0 + t; i < i1; i += kLbNT) {
+    const uint32_t k = a.key[i];
+    const uint32_t pos = atomicAdd(&cur[ab_bucket(k, m)], 1u);
+    a.kbuf[pos] = ((uint64_t)k << 32) | ((uint64_t)i << 1) | (uint64_t)(a.lab[i] & 1u);
+  }
+}
+
+// AUC buckets beyond kLbCap (a skewed or shifted snapshot: all predictions equal at epoch 0)
+// sorted in place through global memory before k_ab_bucket (as k_lb_big)
+__global__ __launch_bounds__(kLbNT) void k_ab_big(AbArgs a) {
+  __shared__ uint32_t wcnt[kLbWaves][256];
+  __shared__ uint32_t base[256];
+  __shared__ uint32_t lds[kLbWaves + 1];
+  __shared__ unsigned long long s_red[2][kLbWaves];
+  __shared__ uint32_t s_list[kLbNT];
+  __shared__ uint32_t s_nlist;
+  const int t = threadIdx.x;
+  const uint32_t nbk = 1u << a.wbits;
+  uint32_t listed = 0;
+  for (uint32_t b0 = 0; b0 < nbk; b0 += kLbNT) {
+    const uint32_t bb = b0 + t;
+    const int64_t nb = bb < nbk ? (int64_t)a.bstart[bb + 1] - (int64_t)a.bstart[bb] : 0;
+    const uint32_t need = nb > kLbCap ? 1u : 0u;
+    uint32_t cnt;
+    const uint32_t ex = block_excl_scan<kLbNT>(need, lds, &cnt);
+    if (t == 0) s_nlist = 0;
+    __syncthreads();
+    if (need && (listed + ex) % gridDim.x == blockIdx.x) s_list[atomicAdd(&s_nlist, 1u)] = bb;
+    __syncthreads();
+    listed += cnt;
+    const uint32_t nl = s_nlist;
+    for (uint32_t li = 0; li < nl; ++li) {
+      const uint32_t b = s_list[li];
+      const int64_t start = a.bstart[b];
+      const int64_t n = (int64_t)a.bstart[b + 1] - start;
+      unsigned long long kor = 0, kand = ~0ull;
+      for (int64_t i = t; i < n; i += kLbNT) {
+        kor |= a.kbuf[start + i];
+        kand &= a.kbuf[start + i];
+      }
+      kor = lb_wave_or(kor);
+      kand = lb_wave_and(kand);
+      if (lane_id() == 0) {
+        s_red[0][t / kWave] = kor;
+        s_red[1][t / kWave] = kand;
+      }
+      __syncthreads();
+      for (int i = 0; i < kLbWaves; ++i) {
+        kor |= s_red[0][i];
+        kand &= s_red[1][i];
+      }
+      __syncthreads();
+      uint64_t* X = a.kbuf + start;
+      uint64_t* Y = a.kscr + start;
+      int np = 0;
+      for (int shift = 0; shift < 64; shift += 8) {
+        if ((((kor ^ kand) >> shift) & 255ull) == 0) continue;
+        lb_global_pass<false>(X, nullptr, nullptr, Y, nullptr, nullptr, n, false, shift, wcnt,
+                              base, lds);
+        uint64_t* tk = X;
+        X = Y;
+        Y = tk;
+        ++np;
+      }
+      if (np & 1)
+        for (int64_t i = t; i < n; i += kLbNT) Y[i] = X[i];
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
+  __shared__ uint64_t sk[kLbCap];
+  __shared__ uint32_t wcnt[kLbWaves][256];
+  __shared__ unsigned long long s_red[4][kLbWaves];
+  __shared__ uint32_t lds[kLbWaves + 1];
+  __shared__ uint32_t s_lb[3 * kLbWaves];
+  __shared__ uint32_t s_tag;
+  __shared__ double s_area[kLbWaves];
+  DevState* ds = a.ds;
+  unsigned* meta = ds->sortmeta;
+  const int t = threadIdx.x;
+  if (t == 0) s_tag = hw_tag(meta);
+  __syncthreads();
+  const uint32_t b = blockIdx.x;  // bucket = block (dispatch order; see k_lb_bucket)
+  const uint32_t nbk = 1u << a.wbits;
+  const int64_t start = a.bstart[b];
+  const int n = (int)((int64_t)a.bstart[b + 1] - start);
+  const bool fast = n <= kLbCap;  // else sorted in place by k_ab_big
+  const uint64_t* gk = a.kbuf + start;
+  if (fast) {
+    uint64_t kr[kLbRadixIT], sr[kLbRadixIT];
+    uint32_t qr[kLbRadixIT];
+    const int wb = (t / kWave) * kWave * kLbRadixIT + lane_id();
+#pragma unroll
+    for (int c = 0; c < kLbRadixIT; ++c) {
+      const int i = wb + c * kWave;
+      kr[c] = i < n ? gk[i] : 0ull;
+      qr[c] = 0u;
+      sr[c] = 0ull;
+    }
+    lb_lds_sort<false, false>(kr, qr, sr, n, false, sk, nullptr, nullptr, wcnt, lds, s_red);
+  }
+  auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
+  // positives of this bucket, then of the buckets before it
+  uint32_t mine = 0;
+  for (int i = t; i < n; i += kLbNT) mine += (uint32_t)(item(i) & 1ull);
+  uint32_t tot;
+  (void)block_excl_scan<kLbNT>(mine, lds, &tot);
+  uint32_t cum0 = block_lookback<kLbNT>(a.hstat, (int64_t)b, s_tag, tot, &ds->err, s_lb);
+  // every negative adds the positives ranked below it (exact integers in double)
+  double area = 0;
+  for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
+    const int ib = c0 + t * kLbIT;
+    uint32_t lb[kLbIT], s = 0;
+#pragma unroll
+    for (int j = 0; j < kLbIT; ++j) {
+      lb[j] = ib + j < n ? (uint32_t)(item(ib + j) & 1ull) : 2u;
+      s += lb[j] & 1u;
+    }
+    uint32_t ctot;
+    uint32_t cum = block_excl_scan<kLbNT>(s, lds, &ctot) + cum0;
+#pragma unroll
+    for (int j = 0; j < kLbIT; ++j) {
+      if (lb[j] == 1u) cum += 1;
+      else if (lb[j] == 0u) area += (double)cum;
+    }
+    cum0 += ctot;
+  }
+  for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
+  if (lane_id() == 0) s_area[t / kWave] = area;
+  __syncthreads();
+  if (t != 0) return;
+  for (int w = 1; w < kLbWaves; ++w) area += s_area[w];
+  atomicAdd(&ds->auc_area, area);
+  if (b == nbk - 1u) ds->auc_npos = cum0;  // every positive of the snapshot
+  const unsigned done =
+      __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (done != nbk - 1u) return;
+  // the last bucket done: AUC * n as k_auc_final computes it, and the lane reset for the next
+  // snapshot (tickets, tag, the bucket map fitted to this snapshot's range)
+  const double tot_area = __hip_atomic_load(&ds->auc_area, __ATOMIC_ACQUIRE,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+  const double P = (double)__hip_atomic_load(&ds->auc_npos, __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+  const double nn = (double)a.B;
+  double r;
+  if (P == 0 || P == nn) {
+    r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
+  } else {
+    const double ar = tot_area / (P * (nn - P));
+    r = (ar < 0.5 ? 1 - ar : ar) * nn;
+  }
+  *a.out = a.accumulate ? *a.out + r : r;
+  ds->auc_area = 0;
+  ds->auc_done = 0;
+  ds->auc_pk_min = ~ds->auc_kmin_inv;
+  ds->auc_pk_max = ds->auc_kmax;
+  ds->auc_pk_valid = 1u;
+  ds->auc_kmin_inv = 0;
+  ds->auc_kmax = 0;
+  meta[kSortMetaEpoch] = ++ds->sort_epoch;
+}
+
+int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
+               double* out_dev, bool accumulate, bool* used) {
+  *used = false;
+  Workspace& ws = *L.ws;
+  if (!ws.lb_hint) {
+    DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws.lb_hint), 4 * sizeof(unsigned int),
+                          hipHostMallocDefault));
+    for (int i = 0; i < 4; ++i) ws.lb_hint[i] = 0;
+  }
+  volatile unsigned int* hint = ws.lb_hint;
+  if (hint[0] > kLbOverRadix) {  // skewed snapshots lately: the radix lane
+    if (++hint[1] < kLbRetry) return DFX_OK;
+    hint[0] = 0;
+    hint[1] = 0;
+  }
+  int wbits = 1;  // ~256 items a bucket
+  while (wbits < 12 && ((int64_t)256 << wbits) < B) ++wbits;
+  const uint32_t nbk = 1u << wbits;
+  const int64_t ntiles = (B + kAbTileItems - 1) / kAbTileItems;
+  DFX_TRY(ws.keys0.ensure(B * 8));
+  DFX_TRY(ws.keys1.ensure(B * 8));
+  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 2 * (nbk + 1))));
+  {
+    void* before = ws.hstat.p;
+    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * std::max<uint32_t>(nbk, 256)));
+    if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
+      DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
+  }
+  AbArgs a{};
+  a.B = B; a.ntiles = ntiles; a.key = key; a.lab = lab; a.wbits = wbits;
+  a.tilecnt = ws.lbcnt.as<uint32_t>();
+  a.totals = a.tilecnt + (size_t)ntiles * nbk;
+  a.bstart = a.totals + nbk + 1;
+  a.kbuf = ws.keys0.as<uint64_t>();
+  a.kscr = ws.keys1.as<uint64_t>();
+  a.ds = L.ds;
+  a.hstat = ws.hstat.as<unsigned long long>();
+  a.out = out_dev;
+  a.accumulate = accumulate ? 1 : 0;
+  a.hint = ws.lb_hint;
+  LbArgs c{};  // the column scan's view
+  c.tilecnt = a.tilecnt; c.totals = a.totals; c.ntiles = ntiles; c.wbits = wbits;
+  hipLaunchKernelGGL(k_ab_hist, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
+                     L.stream, a);
+  hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
+                     L.stream, c);
+  hipLaunchKernelGGL(k_ab_scatter, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
+                     L.stream, a);
+  hipLaunchKernelGGL(k_ab_big, dim3(kLbBigBlocks), dim3(kLbNT), 0, L.stream, a);
+  hipLaunchKernelGGL(k_ab_bucket, dim3(nbk), dim3(kLbNT), 0, L.stream, a);
   DFX_HIP(hipGetLastError());
   *used = true;
   return DFX_OK;

@@ -323,20 +323,27 @@ __global__ __launch_bounds__(kAbNT) void k_auc_block(int64_t n, const uint32_t* 
 }
 
 // AUC*n of the snapshot (keys ak0, labels av0) into *out_dev (accumulate: += ), on the lane
-int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool radix) {
+int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, int mode) {
   Workspace& ws = *L.ws;
   if (B <= 0) {
     if (!accumulate) DFX_HIP(hipMemsetAsync(out_dev, 0, sizeof(double), L.stream));
     return DFX_OK;
   }
   DFX_TRY(auc_reserve(ws, B, L.stream));
-  if (B <= kAbMax) {  // one block in LDS (both auc_sort modes: the same stable order)
+  if (B <= kAbMax) {  // one block in LDS (every auc_sort mode: the same stable order)
     hipLaunchKernelGGL(k_auc_block, dim3(1), dim3(kAbNT), 0, L.stream, B,
                        ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), out_dev,
                        accumulate ? 1 : 0);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
+  if (mode == 2) {  // the bucket sort (locbucket.hip), unless the hint says skewed snapshots
+    bool used = false;
+    DFX_TRY(auc_bucket(L, B, ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), out_dev, accumulate,
+                       &used));
+    if (used) return DFX_OK;
+  }
+  const bool radix = mode != 0;
   const int64_t ntiles = (B + kArTile - 1) / kArTile;
   const uint32_t* V0 = nullptr;
   const uint32_t* V1 = nullptr;
@@ -386,9 +393,9 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, bool 
 }
 
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
-            bool radix) {
+            int mode) {
   DFX_TRY(auc_snapshot(L, L.stream, B, label, pred));
-  return auc_finish(L, B, out_dev, false, radix);
+  return auc_finish(L, B, out_dev, false, mode);
 }
 
 __global__ void k_eval_part(int64_t B, const float* label, const float* pred, double* part) {
@@ -462,7 +469,7 @@ extern "C" int dfx_auc(dfx_ctx* ctx, int64_t B, const float* label, const float*
   DFX_CHECK_ARG(ctx && auc_n, "null argument");
   Context* c = &ctx->c;
   double* o = &c->ds->scratch[2];
-  DFX_TRY(auc_run(main_lane(c), B, label, pred, o, c->auc_radix));
+  DFX_TRY(auc_run(main_lane(c), B, label, pred, o, c->auc_sort));
   DFX_HIP(hipMemcpyAsync(auc_n, o, 8, hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;

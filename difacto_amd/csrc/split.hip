@@ -591,7 +591,7 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
-  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
+  DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   DFX_HIP(hipGetLastError());

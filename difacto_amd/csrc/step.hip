@@ -336,7 +336,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   lane_mark(c, 2, c->aux_stream);
-  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_radix));
+  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   lane_mark(c, 3, c->aux_stream);
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   prof_mark(c, 5);

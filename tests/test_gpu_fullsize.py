@@ -73,7 +73,8 @@ def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=Tr
         pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
         H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=push, pred=pred)
         p = H.progress(c)
-        assert close(pred.cpu().numpy(), opred, rtol=pred_rtol), step
+        rt = pred_rtol[step] if isinstance(pred_rtol, (list, tuple)) else pred_rtol
+        assert close(pred.cpu().numpy(), opred, rtol=rt), step
         assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
         assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size, step
         assert p["nrows"] == blk.size
@@ -115,7 +116,10 @@ def test_fused_full_c5(H):
     test_c5_model_drift_bound; this full-size run keeps close()'s elementwise 1e-3."""
     cfg = dict(V_dim=128, lr=.05, V_lr=.01)
     batches = [D.synthetic(10_000, 39, 1 << 24, zipf=1.1, seed=7000 + s) for s in range(4)]
-    _run(H, cfg, batches, n_cnt=2, max_keys=1 << 20, pred_rtol=1e-4, model_rtol=1e-3)
+    # step 0 reads the oracle's own (empty) model: north_star's 1e-5; after the first chunked
+    # update the models differ by the reference's float rounding of hot keys' sums
+    _run(H, cfg, batches, n_cnt=2, max_keys=1 << 20, pred_rtol=[RTOL, 1e-4, 1e-4, 1e-4],
+         model_rtol=1e-3)
 
 
 def test_calcgrad_c5_chunked(H):

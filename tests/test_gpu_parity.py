@@ -148,7 +148,7 @@ def test_fmloss_nov_known(H, rcv1, known):
     assert np.array_equal(pred, opred)
     og = O.fm_calcgrad(rcv1.offs, ocol, rcv1.vals, rcv1.labels, None, w, None, None, len(ou), 0,
                        opred)
-    assert close(grad, og)
+    assert np.array_equal(grad, og)  # bit-exact (expf included: csrc/expf.h)
 
 
 def test_fmloss_hasv_known(H, rcv1, known):
@@ -163,7 +163,7 @@ def test_fmloss_hasv_known(H, rcv1, known):
     opred = O.fm_predict(rcv1.offs, ocol, rcv1.vals, W, wp, vp, d)
     assert np.array_equal(pred, opred)
     og = O.fm_calcgrad(rcv1.offs, ocol, rcv1.vals, rcv1.labels, None, W, wp, vp, len(ou), d, opred)
-    assert close(grad, og)
+    assert np.array_equal(grad, og)  # bit-exact (expf included: csrc/expf.h)
 
 
 @pytest.mark.parametrize("d", [0, 1, 2, 5, 16, 33, 64, 100, 128, 200])
@@ -189,6 +189,9 @@ def test_fmloss_random(H, d, binary):
     assert np.array_equal(pred, opred), np.max(np.abs(pred - opred))
     og = O.fm_calcgrad(blk.offs, ocol, blk.vals, blk.labels, rw, W, wp, vp, U, d, opred)
     assert close(grad, og)
+    # no key reaches a chunked sum (<= 256 occurrences) and p's expf is glibc's (csrc/expf.h):
+    # the gradients are the reference's bit for bit
+    assert np.array_equal(grad, og), int((grad != og).sum())
     assert abs(objv - O.evaluate(blk.labels, opred)) <= 1e-4 * abs(objv)
 
 
@@ -218,24 +221,28 @@ def test_auc_and_evaluate(H):
 
 @pytest.mark.parametrize("n", [1, 2, 4095, 4097, 10000, 12288, 12289, 100000, 1000003])
 def test_auc_radix_and_merge_sorts_agree(H, n):
-    """the AUC lane's two stable sorts (auc_sort=radix | merge; up to 12288 rows both take the
-    one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie break of
-    the oracle, with heavy ties (quantised predictions, one constant digit pattern), with all
-    predictions equal (epoch 0, w = 0) and with signed zeros (-0 == +0)"""
+    """the AUC lane's three stable sorts (auc_sort=bucket | radix | merge; up to 12288 rows all
+    take the one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie
+    break of the oracle, with heavy ties (quantised predictions, one constant digit pattern),
+    with all predictions equal (epoch 0, w = 0: one bucket far beyond the LDS sort) and with
+    signed zeros (-0 == +0).  Each context sees every snapshot twice, so the bucket sort runs
+    with its map fitted to the previous snapshot's range and to a different one"""
     rng = np.random.default_rng(n)
     label = np.where(rng.random(n) < 0.25, 1.0, -1.0).astype(np.float32)
     signed0 = np.where(rng.random(n) < 0.5, np.float32(-0.0), np.float32(0.0)).astype(np.float32)
     signed0[rng.random(n) < 0.3] = -1.5
+    cs = [H.Context(0, auc_sort=mode) for mode in ["bucket", "radix", "merge"]]
     for pred in [np.round(rng.standard_normal(n) * 8).astype(np.float32) / 8,
                  np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32),
                  signed0]:
         want = O.auc_stable_ties(label, pred) if O.has_ties(pred) else O.auc(label, pred)
-        got = []
-        for mode in ["radix", "merge"]:
-            c = H.Context(0, auc_sort=mode)
-            got.append(H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32)))
-        assert got[0] == got[1], got
-        assert abs(got[0] - want) <= 1e-4 * n, (got, want)
+        for _ in range(2):
+            got = [H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32))
+                   for c in cs]
+            assert got[0] == got[1] == got[2], got
+            assert abs(got[0] - want) <= 1e-4 * n, (got, want)
+    for c in cs:
+        c.close()
 
 
 # ---------------------------------------------------------------- Store / SGDUpdater

@@ -62,7 +62,9 @@ def test_prefetch_forward_bit_identical(H, lanes, nb, binary):
         # the loss partials are summed per block (128 rows at 2 lanes a row, 64 at 4): the
         # double sums differ in the last bits only
         assert abs(qa["loss"] - qb["loss"]) <= 1e-12 * abs(qa["loss"]) and qa["auc"] == qb["auc"]
-        assert close(pb.cpu().numpy(), opred, rtol=1e-4)
+        # no key reaches a chunked sum here: the model stays the oracle's, so predictions are
+        # held to north_star's 1e-5 every step
+        assert close(pb.cpu().numpy(), opred, rtol=1e-5), step
         assert abs(qb["loss"] - loss) <= 1e-4 * abs(loss)
         assert abs(qb["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     uniq, _, _ = O.localize(blk.offs, blk.ids)
@@ -196,9 +198,10 @@ def test_gisette_long_rows_predict_calcgrad(H):
 
 def test_gisette_long_rows_fused_steps(H):
     """The same shape through the fused step (C1's settings, lazy V at V_threshold=10): loss /
-    AUC within 1e-4 of the oracle and predictions within 1e-4 every step; the model within
-    1e-4 — its gradients are chunked sums (see above), the reference's one float run differs
-    from them by its own rounding, which the FTRL / AdaGrad state carries on."""
+    AUC within 1e-4 of the oracle; predictions within 1e-5 at step 0 (the model is still the
+    oracle's) and within 1e-4 after — the gradients are chunked sums (see above), the
+    reference's one float run differs from them by its own rounding, which the FTRL / AdaGrad
+    state carries on; the model within 1e-4."""
     cfg = dict(V_dim=2, lr=.02, V_lr=.001)
     c = H.Context(0, max_keys=1 << 14, **cfg)
     up = O.Updater(**cfg)
@@ -209,7 +212,7 @@ def test_gisette_long_rows_fused_steps(H):
         pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
         H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step == 0), pred=pred)
         p = H.progress(c)
-        assert close(pred.cpu().numpy(), opred, rtol=1e-4), step
+        assert close(pred.cpu().numpy(), opred, rtol=1e-5 if step == 0 else 1e-4), step
         assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
         assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     uniq, _, _ = O.localize(blk.offs, blk.ids)
@@ -246,18 +249,9 @@ def test_dump_text_equals_oracle(H, tmp_path, aux, rev, layout):
     gl = sorted(open(g).read().splitlines(), key=lambda l: int(l.split("\t")[0]))
     ol = sorted(open(o).read().splitlines(), key=lambda l: int(l.split("\t")[0]))
     assert len(gl) == len(ol) > 0
-    # the values follow from float arithmetic in the same order, except expf (the gradient's
-    # p is exp in double, rounded, on the device): lines equal field for field, and a field
-    # that differs must agree within 1e-5 relative
-    diff = 0
-    for a, b in zip(gl, ol):
-        fa, fb = a.split("\t"), b.split("\t")
-        assert fa[:2] == fb[:2] and len(fa) == len(fb), (a, b)
-        for x, y in zip(fa[2:], fb[2:]):
-            if x != y:
-                diff += 1
-                assert abs(float(x) - float(y)) <= 1e-5 * max(abs(float(x)), abs(float(y))) + 1e-7
-    assert diff <= len(gl) // 100, diff  # text-identical for nearly every line
+    # every value follows from float arithmetic in the reference's order — expf included
+    # (csrc/expf.h is glibc's) — and no key here reaches a chunked sum: the text is identical
+    assert gl == ol
     c.close()
 
 

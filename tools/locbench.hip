@@ -1,0 +1,74 @@
+// The fused step's Localizer alone, on the GPU: a C3-shaped batch (B rows of k ids uniform
+// below 2^kbits, generated on the device) localized `iters` times on the context stream, as
+// the fused step's lane does (no col: the bucket Localizer, or the radix one with
+// loc_bucket=0), timed with events; run it under rocprofv3 --kernel-trace for per-kernel
+// times.  Measurement tool (links the library's internals), not a test.
+//   build/locbench [B] [k] [kbits] [iters] [context kwargs]
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "../difacto_amd/csrc/internal.h"
+
+__global__ void k_gen(int64_t B, int k, int kbits, uint64_t* offs, uint64_t* ids, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= B) offs[i] = (uint64_t)i * k;
+  if (i >= B * k) return;
+  uint64_t x = seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;  // splitmix64
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  ids[i] = x >> (64 - kbits);
+}
+
+int main(int argc, char** argv) {
+  const int64_t B = argc > 1 ? atoll(argv[1]) : 100000;
+  const int k = argc > 2 ? atoi(argv[2]) : 39;
+  const int kbits = argc > 3 ? atoi(argv[3]) : 24;
+  const int iters = argc > 4 ? atoi(argv[4]) : 20;
+  const char* kw = argc > 5 ? argv[5] : "";
+  const int64_t nnz = B * k;
+  dfx_ctx* ctx = nullptr;
+  if (dfx_ctx_create(0, kw, &ctx) != DFX_OK) {
+    fprintf(stderr, "ctx: %s\n", dfx_last_error());
+    return 1;
+  }
+  dfx::Context* c = &ctx->c;
+  uint64_t *offs, *ids, *uniq;
+  uint32_t *seg, *occ;
+  hipMalloc(&offs, (B + 1) * 8);
+  hipMalloc(&ids, nnz * 8);
+  hipMalloc(&uniq, nnz * 8);
+  hipMalloc(&seg, (nnz + 1) * 4);
+  hipMalloc(&occ, nnz * 4);
+  hipLaunchKernelGGL(k_gen, dim3((unsigned)((nnz + 256) / 256)), dim3(256), 0, c->stream, B, k,
+                     kbits, offs, ids, 42ull);
+  dfx::Lane L = dfx::main_lane(c);
+  dfx::LocOut o;
+  o.uniq = uniq;
+  o.segstart = seg;
+  o.occ_row = occ;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  double tot = 0;
+  for (int it = 0; it < iters + 2; ++it) {
+    hipEventRecord(e0, c->stream);
+    if (dfx::localize_run(c, L, B, nnz, offs, ids, ~0ull, o) != DFX_OK) {
+      fprintf(stderr, "localize: %s\n", dfx_last_error());
+      return 1;
+    }
+    hipEventRecord(e1, c->stream);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (it >= 2) tot += ms;
+  }
+  unsigned u = 0;
+  hipMemcpy(&u, &c->ds->u_count, 4, hipMemcpyDeviceToHost);
+  int err = 0;
+  hipMemcpy(&err, &c->ds->err, 4, hipMemcpyDeviceToHost);
+  printf("locbench B=%lld k=%d kbits=%d kwargs='%s': %.4f ms per Localizer, U=%u, err=%d\n",
+         (long long)B, k, kbits, kw, tot / iters, u, err);
+  dfx_ctx_destroy(ctx);
+  return 0;
+}

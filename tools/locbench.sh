@@ -1,0 +1,14 @@
+#!/bin/bash
+# tools/locbench on the GPU box: the Localizer alone, radix vs bucket and the bucket kernel's
+# measurement switches (lb_diag), then a kernel trace of the default.  B=${LB_B:-100000}.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+B=${LB_B:-100000}
+for kw in "loc_bucket=0" "" ${LB_VARIANTS:-"lb_diag=1" "lb_diag=2" "lb_diag=3" "lb_diag=7"}; do
+  timeout -k 10 60 ./build/locbench $B 39 24 20 "$kw" || exit $?
+done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_locbench -o trace \
+  --output-format csv -- ./build/locbench $B 39 24 20 "" > gpurun_out/prof_locbench.log 2>&1 || exit $?
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_locbench_lsd -o trace \
+  --output-format csv -- ./build/locbench $B 39 24 20 "loc_bucket=0" > gpurun_out/prof_locbench_lsd.log 2>&1

@@ -11,10 +11,12 @@ P=profiles/$TAG
 mkdir -p $P
 F=$O/pmc_${TAG}_fetch/pmc_counter_collection.csv
 W=$O/pmc_${TAG}_write/pmc_counter_collection.csv
-python3 tools/prof_summary.py $O/prof_${TAG}_fused/trace_kernel_trace.csv 20 $F $W \
-  > $P/kernel_summary_pipelined.md
-python3 tools/prof_summary.py $O/prof_${TAG}_serial/trace_kernel_trace.csv 20 $F $W \
-  > $P/kernel_summary_serial.md
+# the fused bench runs its 20 timed steps, then an untimed diagnostic pass over the same 20
+# batches and 20 host-idle calls (bench.py): the window is the timed steps, 40 markers back
+DFX_STEP_SKIP=40 python3 tools/prof_summary.py $O/prof_${TAG}_fused/trace_kernel_trace.csv 20 \
+  $F $W > $P/kernel_summary_pipelined.md
+DFX_STEP_SKIP=40 python3 tools/prof_summary.py $O/prof_${TAG}_serial/trace_kernel_trace.csv 20 \
+  $F $W > $P/kernel_summary_serial.md
 DFX_STEP_MARKER=k_split_worker_finalize DFX_STEP_SKIP=44 python3 tools/prof_summary.py \
   $O/prof_${TAG}_split/trace_kernel_trace.csv 20 $O/pmc_${TAG}_fetch_split/pmc_counter_collection.csv \
   $O/pmc_${TAG}_write_split/pmc_counter_collection.csv > $P/kernel_summary_split_pipelined.md
