@@ -182,6 +182,7 @@ _DIST_SIGS = {
     "dfx_split_store_submit": (ctypes.c_int, [vp, ctypes.POINTER(Batch), ctypes.c_int,
                                               ctypes.c_int, ctypes.POINTER(vp)]),
     "dfx_split_store_flush": (ctypes.c_int, [vp]),
+    "dfx_split_store_sync": (ctypes.c_int, [vp]),
     "dfx_split_store_throttle_seconds": (ctypes.c_int, [vp, f64p]),
     "dfx_split_store_set_marks": (ctypes.c_int, [vp, u32]),
     "dfx_split_store_take_marks": (ctypes.c_int, [vp, f64p, i64p]),

@@ -79,7 +79,7 @@ struct Kw {
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
   int loc_bucket = 1;
   // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_bucket skipped — 1 the LDS
-  // sort, 2 the look-back, 4 the outputs; the Localizer's results are then wrong
+  // sort, 4 the outputs; the Localizer's results are then wrong
   int lb_diag = 0;
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)

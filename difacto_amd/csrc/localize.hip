@@ -296,7 +296,8 @@ __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
 // ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
-// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments in ticket order; per segment its chunk count
+// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments, tile = block;
+// per segment its chunk count
 // (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
 // (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
 // writes the total 0 and exits.
@@ -304,17 +305,15 @@ __global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart,
                                                        unsigned long long* stat, uint32_t* choff,
                                                        uint32_t* chunk_seg, uint32_t* nchunks) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
-  __shared__ uint32_t s_tile, s_pre;
+  __shared__ uint32_t s_pre;
   if (ds->n_init == 0u) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *nchunks = 0u;
     return;
   }
   unsigned* meta = ds->sortmeta;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaCpTile], 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
+  const int64_t tile = blockIdx.x;  // workgroups start in index order: no ticket needed
   const int64_t U = (int64_t)ds->u_count;
-  if (tile * kLocTile >= U) return;  // later tickets exit too
+  if (tile * kLocTile >= U) return;  // no later tile waits on this one
   const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint32_t cnt[kLocItems];
   uint32_t s = 0;

@@ -59,6 +59,8 @@ struct LbArgs {
   uint32_t* tilecnt;     // [ntiles][nbk]: counts, then exclusive prefixes over the tiles
   uint32_t* totals;      // [nbk]
   uint32_t* bstart;      // [nbk + 1]
+  uint32_t* bheads;      // [nbk]: unique keys per bucket (k_lb_bucket)
+  uint32_t* brank;       // [nbk]: the bucket's first rank (k_lb_bscan)
   uint64_t* kbuf;        // items
   uint32_t* qbuf;        // rows / positions of unpacked items
   uint64_t* sbuf;        // side payloads (valued)
@@ -66,7 +68,6 @@ struct LbArgs {
   uint32_t* qscr;
   uint64_t* sscr;
   DevState* ds;
-  unsigned long long* hstat;  // per bucket its tagged look-back word
   uint64_t* uniq;
   uint32_t* segstart;
   uint32_t* occ_row;
@@ -660,15 +661,9 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
   __shared__ uint32_t wcnt[kLbWaves][256];
   __shared__ unsigned long long s_red[4][kLbWaves];
   __shared__ uint32_t lds[kLbWaves + 1];
-  __shared__ uint32_t s_lb[3 * kLbWaves];
   DevState* ds = a.ds;
-  unsigned* meta = ds->sortmeta;
   const int t = threadIdx.x;
-  // bucket = block: workgroups are dispatched in index order, so every bucket a block looks back
-  // on is running or done (a ticket counter would serialise 4096 blocks on one word: ~88
-  // returning atomics per us, MI355X_MICROARCH.md 'dequeue')
   const uint32_t b = blockIdx.x;
-  const uint32_t nbk = 1u << a.wbits;
   const int64_t start = a.bstart[b];
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
   const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
@@ -706,38 +701,35 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
     }
   }
   auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
-  // ---- heads: an item whose key differs from the one before it (the bucket's first always);
-  // a segment longer than kChunkOcc raises the chunk plan's gate
-  uint32_t mine = 0;
-  bool longseg = false;
-  for (int i = t; i < n; i += kLbNT) {
-    const uint64_t kb = lb_keybits(p, item(i));
-    mine += (i == 0 || kb != lb_keybits(p, item(i - 1))) ? 1u : 0u;
-    if (i >= kChunkOcc && kb == lb_keybits(p, item(i - kChunkOcc))) longseg = true;
-  }
-  if (__syncthreads_or(longseg) && t == 0 &&
-      __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    atomicOr(&ds->n_init, 1u);
-  uint32_t tot;
-  (void)block_excl_scan<kLbNT>(mine, lds, &tot);
-  uint32_t rank0 = (a.diag & 2) ? 0u
-                                 : block_lookback<kLbNT>(a.hstat, (int64_t)b, hw_tag(meta), tot,
-                                                         &ds->err, s_lb);
-  if (a.diag & 4) return;
-  // ---- outputs, per thread kLbIT consecutive items of a chunk
+  // ---- per occurrence its row (and value); per head (an item whose key differs from the one
+  // before it, the bucket's first always) its key and segment start at the bucket's own offset
+  // in the scratch lists (k_lb_out moves them to their ranks); a segment longer than kChunkOcc
+  // raises the chunk plan's gate
   const uint64_t qmask = p.rb ? (~0ull >> (64 - p.rb)) : 0ull;
+  uint32_t* tseg = a.qscr + start;
+  uint64_t* tkey = a.kscr + start;
+  uint32_t run = 0;
+  bool longseg = false;
   for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
     const int ib = c0 + t * kLbIT;
     uint32_t h[kLbIT], s = 0;
 #pragma unroll
     for (int j = 0; j < kLbIT; ++j) {
       const int i = ib + j;
-      h[j] = (i < n && (i == 0 || lb_keybits(p, item(i)) != lb_keybits(p, item(i - 1)))) ? 1u
-                                                                                        : 0u;
+      h[j] = 0u;
+      if (i < n) {
+        const uint64_t kb = lb_keybits(p, item(i));
+        h[j] = (i == 0 || kb != lb_keybits(p, item(i - 1))) ? 1u : 0u;
+        if (i >= kChunkOcc && kb == lb_keybits(p, item(i - kChunkOcc))) longseg = true;
+      }
       s += h[j];
     }
     uint32_t ctot;
-    uint32_t incl = block_excl_scan<kLbNT>(s, lds, &ctot) + rank0;
+    uint32_t incl = block_excl_scan<kLbNT>(s, lds, &ctot) + run;
+    if (a.diag & 4) {
+      run += ctot;
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < kLbIT; ++j) {
       const int i = ib + j;
@@ -745,9 +737,8 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
         incl += h[j];
         const uint64_t it = item(i);
         if (h[j]) {
-          const uint64_t key = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
-          if (a.uniq) a.uniq[incl - 1] = key;
-          if (a.segstart) a.segstart[incl - 1] = (uint32_t)(start + i);
+          tkey[incl - 1] = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
+          tseg[incl - 1] = (uint32_t)(start + i);
         }
         uint32_t row;
         if (S) {
@@ -760,15 +751,54 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
         a.occ_row[start + i] = row;
       }
     }
-    rank0 += ctot;
+    run += ctot;
   }
-  if (b == nbk - 1u && t == 0) {  // the last bucket closes the segments
-    ds->u_count = rank0;
-    if (a.segstart) a.segstart[rank0] = (uint32_t)a.nnz;
-    // the next batch on this lane fits its bucket map to this batch's key range
+  if (__syncthreads_or(longseg) && t == 0 &&
+      __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&ds->n_init, 1u);
+  if (t == 0) a.bheads[b] = run;
+}
+
+// the buckets' first ranks: an exclusive scan of their head counts (one block); U, the closing
+// segment start, and the bucket map of the next batch on this lane
+constexpr int kLbScanNT = 1024;
+__global__ __launch_bounds__(kLbScanNT) void k_lb_bscan(LbArgs a) {
+  __shared__ uint32_t lds[kLbScanNT / kWave + 1];
+  const int t = threadIdx.x;
+  const uint32_t nbk = 1u << a.wbits;
+  const uint32_t per = (nbk + kLbScanNT - 1) / kLbScanNT;
+  uint32_t mine = 0;
+  for (uint32_t i = 0; i < per; ++i)
+    if (t * per + i < nbk) mine += a.bheads[t * per + i];
+  uint32_t U;
+  uint32_t ex = block_excl_scan<kLbScanNT>(mine, lds, &U);
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < nbk) {
+      const uint32_t h = a.bheads[d];
+      a.brank[d] = ex;
+      ex += h;
+    }
+  }
+  if (t == 0) {
+    DevState* ds = a.ds;
+    ds->u_count = U;
+    if (a.segstart) a.segstart[U] = (uint32_t)a.nnz;
     ds->pk_min = ds->kmin;
     ds->pk_max = ds->kmax;
     ds->pk_valid = 1u;
+  }
+}
+
+// every bucket's heads to their ranks: uniq[rank] and segstart[rank] (RemapIndex's ranks,
+// localizer.cc:53-107), a contiguous run per bucket
+__global__ __launch_bounds__(kLbNT) void k_lb_out(LbArgs a) {
+  const uint32_t b = blockIdx.x;
+  const int64_t start = a.bstart[b];
+  const uint32_t h = a.bheads[b], r0 = a.brank[b];
+  for (uint32_t j = threadIdx.x; j < h; j += kLbNT) {
+    if (a.uniq) a.uniq[r0 + j] = a.kscr[start + j];
+    if (a.segstart) a.segstart[r0 + j] = a.qscr[start + j];
   }
 }
 
@@ -799,13 +829,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   DFX_TRY(ws.vals0.ensure(nnz * 8));
   DFX_TRY(ws.vals1.ensure(nnz * 8));
   DFX_TRY(ws.lbq.ensure(nnz * 8));
-  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 2 * (nbk + 1))));
-  {
-    void* before = ws.hstat.p;
-    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * std::max<int64_t>(nbk, 256)));
-    if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
-      DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  }
+  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 4 * (nbk + 1))));
   LbArgs a{};
   a.B = B; a.nnz = nnz; a.offset = offset; a.index = index; a.max_index = max_index;
   a.keys_ready = o.keys_ready ? 1 : 0;
@@ -815,6 +839,8 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.tilecnt = ws.lbcnt.as<uint32_t>();
   a.totals = a.tilecnt + (size_t)ntiles * nbk;
   a.bstart = a.totals + nbk + 1;
+  a.bheads = a.bstart + nbk + 1;
+  a.brank = a.bheads + nbk + 1;
   a.kbuf = ws.keys0.as<uint64_t>();
   a.kscr = ws.keys1.as<uint64_t>();
   a.sbuf = ws.vals0.as<uint64_t>();
@@ -822,7 +848,6 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.qbuf = ws.lbq.as<uint32_t>();
   a.qscr = a.qbuf + nnz;
   a.ds = L.ds;
-  a.hstat = ws.hstat.as<unsigned long long>();
   a.uniq = o.uniq; a.segstart = o.segstart; a.occ_row = o.occ_row;
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
@@ -854,6 +879,8 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, false>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, false>), bg, bb, 0, L.stream, a);
   }
+  hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);
+  hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
   DFX_HIP(hipGetLastError());
   *used = true;
   return DFX_OK;
@@ -881,8 +908,10 @@ struct AbArgs {
   uint32_t* bstart;
   uint64_t* kbuf;
   uint64_t* kscr;
+  uint32_t* bpos;   // per bucket: its positives, negatives, and area within it
+  uint32_t* bneg;
+  double* barea;
   DevState* ds;
-  unsigned long long* hstat;
   double* out;
   int accumulate;
   unsigned int* hint;
@@ -1081,15 +1110,12 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
   __shared__ uint32_t wcnt[kLbWaves][256];
   __shared__ unsigned long long s_red[4][kLbWaves];
   __shared__ uint32_t lds[kLbWaves + 1];
-  __shared__ uint32_t s_lb[3 * kLbWaves];
-  __shared__ uint32_t s_tag;
   __shared__ double s_area[kLbWaves];
+  __shared__ uint32_t s_neg[kLbWaves];
+  __shared__ uint32_t s_last;
   DevState* ds = a.ds;
-  unsigned* meta = ds->sortmeta;
   const int t = threadIdx.x;
-  if (t == 0) s_tag = hw_tag(meta);
-  __syncthreads();
-  const uint32_t b = blockIdx.x;  // bucket = block (dispatch order; see k_lb_bucket)
+  const uint32_t b = blockIdx.x;
   const uint32_t nbk = 1u << a.wbits;
   const int64_t start = a.bstart[b];
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
@@ -1109,14 +1135,10 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
     lb_lds_sort<false, false>(kr, qr, sr, n, false, sk, nullptr, nullptr, wcnt, lds, s_red);
   }
   auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
-  // positives of this bucket, then of the buckets before it
-  uint32_t mine = 0;
-  for (int i = t; i < n; i += kLbNT) mine += (uint32_t)(item(i) & 1ull);
-  uint32_t tot;
-  (void)block_excl_scan<kLbNT>(mine, lds, &tot);
-  uint32_t cum0 = block_lookback<kLbNT>(a.hstat, (int64_t)b, s_tag, tot, &ds->err, s_lb);
-  // every negative adds the positives ranked below it (exact integers in double)
+  // within the bucket: every negative adds the positives ranked below it here (exact integers
+  // in double); the positives of the buckets before it are added by the last block
   double area = 0;
+  uint32_t run = 0, nneg = 0;
   for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
     const int ib = c0 + t * kLbIT;
     uint32_t lb[kLbIT], s = 0;
@@ -1126,47 +1148,83 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
       s += lb[j] & 1u;
     }
     uint32_t ctot;
-    uint32_t cum = block_excl_scan<kLbNT>(s, lds, &ctot) + cum0;
+    uint32_t cum = block_excl_scan<kLbNT>(s, lds, &ctot) + run;
 #pragma unroll
     for (int j = 0; j < kLbIT; ++j) {
-      if (lb[j] == 1u) cum += 1;
-      else if (lb[j] == 0u) area += (double)cum;
+      if (lb[j] == 1u) {
+        cum += 1;
+      } else if (lb[j] == 0u) {
+        area += (double)cum;
+        ++nneg;
+      }
     }
-    cum0 += ctot;
+    run += ctot;
   }
-  for (int off = 32; off > 0; off >>= 1) area += __shfl_xor(area, off, kWave);
-  if (lane_id() == 0) s_area[t / kWave] = area;
+  for (int off = 32; off > 0; off >>= 1) {
+    area += __shfl_xor(area, off, kWave);
+    nneg += __shfl_xor(nneg, off, kWave);
+  }
+  if (lane_id() == 0) {
+    s_area[t / kWave] = area;
+    s_neg[t / kWave] = nneg;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int w = 1; w < kLbWaves; ++w) {
+      area += s_area[w];
+      nneg += s_neg[w];
+    }
+    // write-through (sc1) stores, counted by the agent-scope add; the last adder reads them
+    // with sc1 loads (MI355X_MICROARCH.md, hand-offs without an acquire, first row)
+    __hip_atomic_store(&a.barea[b], area, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.bpos[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.bneg[b], nneg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL,
+                                    __HIP_MEMORY_SCOPE_AGENT) == nbk - 1u ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last bucket done: area = sum over buckets of (its own area + its negatives x the
+  // positives of the buckets before it), then AUC * n as k_auc_final computes it, and the lane
+  // reset for the next snapshot (the bucket map fitted to this snapshot's range)
+  const uint32_t per = (nbk + kLbNT - 1) / kLbNT;
+  uint32_t mpos = 0;
+  for (uint32_t i = 0; i < per; ++i)
+    if (t * per + i < nbk) mpos += __hip_atomic_load(&a.bpos[t * per + i], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t P;
+  uint32_t pb = block_excl_scan<kLbNT>(mpos, lds, &P);
+  double tot_area = 0;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < nbk) {
+      const double ar = __hip_atomic_load(&a.barea[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t ng = __hip_atomic_load(&a.bneg[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot_area += ar + (double)ng * (double)pb;
+      pb += __hip_atomic_load(&a.bpos[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) tot_area += __shfl_xor(tot_area, off, kWave);
+  if (lane_id() == 0) s_area[t / kWave] = tot_area;
   __syncthreads();
   if (t != 0) return;
-  for (int w = 1; w < kLbWaves; ++w) area += s_area[w];
-  atomicAdd(&ds->auc_area, area);
-  if (b == nbk - 1u) ds->auc_npos = cum0;  // every positive of the snapshot
-  const unsigned done =
-      __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (done != nbk - 1u) return;
-  // the last bucket done: AUC * n as k_auc_final computes it, and the lane reset for the next
-  // snapshot (tickets, tag, the bucket map fitted to this snapshot's range)
-  const double tot_area = __hip_atomic_load(&ds->auc_area, __ATOMIC_ACQUIRE,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-  const double P = (double)__hip_atomic_load(&ds->auc_npos, __ATOMIC_ACQUIRE,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+  for (int w = 1; w < kLbWaves; ++w) tot_area += s_area[w];
+  const double Pd = (double)P;
   const double nn = (double)a.B;
   double r;
-  if (P == 0 || P == nn) {
+  if (Pd == 0 || Pd == nn) {
     r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
   } else {
-    const double ar = tot_area / (P * (nn - P));
+    const double ar = tot_area / (Pd * (nn - Pd));
     r = (ar < 0.5 ? 1 - ar : ar) * nn;
   }
   *a.out = a.accumulate ? *a.out + r : r;
-  ds->auc_area = 0;
   ds->auc_done = 0;
   ds->auc_pk_min = ~ds->auc_kmin_inv;
   ds->auc_pk_max = ds->auc_kmax;
   ds->auc_pk_valid = 1u;
   ds->auc_kmin_inv = 0;
   ds->auc_kmax = 0;
-  meta[kSortMetaEpoch] = ++ds->sort_epoch;
 }
 
 int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
@@ -1190,22 +1248,19 @@ int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* la
   const int64_t ntiles = (B + kAbTileItems - 1) / kAbTileItems;
   DFX_TRY(ws.keys0.ensure(B * 8));
   DFX_TRY(ws.keys1.ensure(B * 8));
-  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 2 * (nbk + 1))));
-  {
-    void* before = ws.hstat.p;
-    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * std::max<uint32_t>(nbk, 256)));
-    if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
-      DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  }
+  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 4 * (nbk + 1)) +
+                          sizeof(double) * (nbk + 1)));
   AbArgs a{};
   a.B = B; a.ntiles = ntiles; a.key = key; a.lab = lab; a.wbits = wbits;
-  a.tilecnt = ws.lbcnt.as<uint32_t>();
+  a.barea = ws.lbcnt.as<double>();  // 8-byte aligned first
+  a.tilecnt = reinterpret_cast<uint32_t*>(a.barea + nbk + 1);
   a.totals = a.tilecnt + (size_t)ntiles * nbk;
   a.bstart = a.totals + nbk + 1;
+  a.bpos = a.bstart + nbk + 1;
+  a.bneg = a.bpos + nbk + 1;
   a.kbuf = ws.keys0.as<uint64_t>();
   a.kscr = ws.keys1.as<uint64_t>();
   a.ds = L.ds;
-  a.hstat = ws.hstat.as<unsigned long long>();
   a.out = out_dev;
   a.accumulate = accumulate ? 1 : 0;
   a.hint = ws.lb_hint;

@@ -6,7 +6,7 @@
 // Launches per sort: [k_os_hist: one read of the keys, the digit counts of EVERY pass — or the
 // producer of the keys accumulates them itself, as the Localizer's transform does] ->
 // k_os_plan (1 block: reduce the counts, pick the digits that vary) -> one k_os_scatter per
-// pass.  A scatter block takes its tile id from a counter (so tiles start in order), ranks its
+// pass.  A scatter block takes the tile of its index (tiles start in order), ranks its
 // 4096 items with wave ballots (exact and order preserving), publishes its per-digit counts and
 // finds its global offsets by decoupled look-back over the preceding tiles' published words
 // (several predecessors read per step), then writes the tile through LDS in digit order, so
@@ -191,9 +191,12 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   // tiles until they run out: tickets are taken in order and a block takes its next one only
   // after publishing its tile, so every tile a block looks back on is done or held by a
   // running block
+  // A full grid takes tile = block index: workgroups start in index order, so every tile a block
+  // looks back on is running or done (a ticket counter serialised the ~950 tiles of a pass on one
+  // word: ~88 returning atomics per us, MI355X_MICROARCH.md 'dequeue')
   const bool looping = (int64_t)gridDim.x * (kOsNT * IT) < n;
   for (;;) {
-  if (t == 0) s_tile = (int64_t)atomicAdd(&meta[kMetaTile + q], 1u);
+  if (t == 0) s_tile = looping ? (int64_t)atomicAdd(&meta[kMetaTile + q], 1u) : (int64_t)blockIdx.x;
 #pragma unroll
   for (int i = 0; i < kOsWaves; ++i) wcnt[i][t] = 0;
   __syncthreads();

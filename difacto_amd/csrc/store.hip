@@ -23,7 +23,7 @@
 
 #include <chrono>
 
-#include "internal.h"
+#include "lookback.h"
 
 namespace dfx {
 
@@ -86,10 +86,10 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 }
 
 // The fused step's InitV in ONE launch (it replaced the scan's three launches + k_initv: in the
-// steady state, where no key needs V, all four only found the device gate closed).  A block
-// takes the next tile of kIvTile flags by ticket, counts them, publishes the count and finds
-// its prefix by decoupled look-back over the lower tiles' tagged words (tiles start in ticket
-// order, so a block only waits on running ones), then draws its keys' V exactly as k_initv.
+// steady state, where no key needs V, all four only found the device gate closed).  Block b
+// counts tile b's kIvTile flags, publishes the count and finds its prefix by the block-wide
+// decoupled look-back over the lower tiles' tagged words (lookback.h), then draws its keys' V
+// exactly as k_initv.
 // The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
 constexpr int kIvItems = 16, kIvTile = kStNT * kIvItems;
 
@@ -100,18 +100,18 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
                                                          const uint32_t* gate,
                                                          unsigned long long* status) {
   __shared__ uint32_t lds[kStNT / kWave + 1];
-  __shared__ int64_t s_tile;
-  __shared__ uint32_t s_pre;
+  __shared__ uint32_t s_lb[3 * kStNT / kWave];
   if (*gate == 0u) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0u;
     return;
   }
-  if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(&ds->iv_ticket, 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
+  // tile = block: workgroups start in index order, so a block only waits on running ones (a
+  // ticket counter serialised ~950 blocks on one word, and a one-word-per-step look-back made
+  // the chain ~40 us of the main stream whenever new keys need V)
+  const int64_t tile = blockIdx.x;
   const int64_t n = (int64_t)nds->u_count;
   const int64_t base = tile * kIvTile;
-  if (base >= n) return;  // every later tile exits too: no waiter is left behind
+  if (base >= n) return;  // no later tile waits on this one
   const uint32_t tag = ds->iv_epoch & 0x3FFFFFFFu;
   // this thread's kIvItems consecutive flags
   const int64_t i0 = base + (int64_t)threadIdx.x * kIvItems;
@@ -123,42 +123,10 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   }
   uint32_t tot;
   uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
-  if (threadIdx.x == 0) {
-    unsigned long long* st = status + tile;
-    uint32_t pre = 0;
-    if (tile == 0) {
-      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 2u) << 32) | tot,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 1u) << 32) | tot,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t k = tile - 1;
-      uint32_t spins = 0;
-      while (k >= 0) {
-        const unsigned long long v =
-            __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hi = (uint32_t)(v >> 32);
-        if ((hi >> 2) != tag || (hi & 3u) == 0) {  // not published yet
-          if (++spins > (1u << 24)) {  // a predecessor never published: give up loudly
-            atomicOr(&ds->err, kErrSort);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        pre += (uint32_t)v;
-        if ((hi & 3u) == 2u) break;
-        --k;
-      }
-      __hip_atomic_store(st, ((unsigned long long)((tag << 2) | 2u) << 32) | (pre + tot),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_pre = pre;
-    if (base + kIvTile >= n) *total = pre + tot;  // the last tile
-  }
-  __syncthreads();
+  const uint32_t pre = block_lookback<kStNT>(status, tile, tag, tot, &ds->err, s_lb);
+  if (threadIdx.x == 0 && base + kIvTile >= n) *total = pre + tot;  // the last tile
   if (cnt == 0) return;
-  uint32_t e = s_pre + ex;
+  uint32_t e = pre + ex;
   const int d = T.d;
 #pragma unroll 1
   for (int k = 0; k < kIvItems; ++k) {

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${LB_B:-100000}
-for kw in "loc_bucket=0" "" ${LB_VARIANTS:-"lb_diag=1" "lb_diag=2" "lb_diag=3" "lb_diag=7"}; do
+for kw in "loc_bucket=0" "" ${LB_VARIANTS:-"lb_diag=1" "lb_diag=4" "lb_diag=5"}; do
   timeout -k 10 60 ./build/locbench $B 39 24 20 "$kw" || exit $?
 done
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_locbench -o trace \
