@@ -58,9 +58,12 @@ struct Kw {
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
   int sort_pack = 1;    // sort_pack=0: the Localizer sorts 12-byte (key, row) pairs
-  // auc_sort=bucket (default): the AUC lane's bucket sort (locbucket.hip); radix: onesweep
-  // passes; merge: tile sorts + merge rounds
-  int auc_sort = 2;
+  // auc_sort=radix (default): the AUC lane's onesweep radix passes; wbucket / bucket: the bucket
+  // sort (locbucket.hip: one wave / one block per bucket); merge: tile sorts + merge rounds.
+  // Same-box A/B: the bucket forms make a shorter lane but a slower
+  // step (120.5 / 121.1 vs 123.4 M ex/s): their high-priority, LDS-holding buckets wait for LDS
+  // the backward's blocks hold, and stall the backward's dispatch meanwhile
+  int auc_sort = 1;
   int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
   int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
   // slot_layout=auto (default): fat slots (entry + V in one 64/128-byte slot, common.h Table)
@@ -74,13 +77,16 @@ struct Kw {
   // unless the batches repeat); never set by the product path
   int diag = 0;
   int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
+  int fwd_ids = 0;    // fwd_ids=1: the fat forward stages each row's ids in LDS (one trip)
   // loc_bucket=1 (default): the Localizer of the fused step and of the split owner (no col) as a
   // bucket sort — histogram, scatter into key-range buckets, one LDS sort per bucket
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
   int loc_bucket = 1;
   // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_bucket skipped — 1 the LDS
-  // sort, 4 the outputs; the Localizer's results are then wrong
+  // sort, 4 the outputs, 8 k_lb_scatter's row search; the Localizer's results are then wrong
   int lb_diag = 0;
+  int lb_wave = 1;  // lb_wave=1: the bucket Localizer sorts one bucket per wave (0: per block)
+  int lb_tiles = 256;  // lb_tiles=<n>: the bucket Localizer's row tiles (histogram / scatter blocks)
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -182,6 +188,9 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
+    else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
+    else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 256;
+    else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
       if (kw->fwd_lanes != 0 && kw->fwd_lanes != 2 && kw->fwd_lanes != 4) {
@@ -231,7 +240,8 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else if (v == "normal") kw->lane_prio = 0;
       else if (v == "loc_high") kw->lane_prio = 1;
       else if (v == "auc_high") kw->lane_prio = 2;
-      else { set_error("unknown lane_prio: " + v + " (high|normal|loc_high|auc_high)"); return DFX_ERR_ARG; }
+      else if (v == "loc_low") kw->lane_prio = 6;
+      else { set_error("unknown lane_prio: " + v + " (high|normal|loc_high|auc_high|loc_low)"); return DFX_ERR_ARG; }
     }
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
@@ -240,10 +250,11 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else { set_error("unknown slot_layout: " + v + " (auto|split|fat)"); return DFX_ERR_ARG; }
     }
     else if (k == "auc_sort") {
-      if (v == "bucket") kw->auc_sort = 2;
+      if (v == "wbucket") kw->auc_sort = 3;
+      else if (v == "bucket") kw->auc_sort = 2;
       else if (v == "radix") kw->auc_sort = 1;
       else if (v == "merge") kw->auc_sort = 0;
-      else { set_error("unknown auc_sort: " + v + " (bucket|radix|merge)"); return DFX_ERR_ARG; }
+      else { set_error("unknown auc_sort: " + v + " (wbucket|bucket|radix|merge)"); return DFX_ERR_ARG; }
     }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
@@ -302,7 +313,8 @@ int pipeline_init(Context* c) {
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   // kwarg lane_prio: bit 0 the Localizer lane high, else at the context stream's priority (the
   // sharded bench runs its compute on a high-priority stream: a Localizer lane below it
-  // starved, 108 -> 70 M ex/s); bit 1 the AUC lane high, else priority 0
+  // starved, 108 -> 70 M ex/s); bit 1 the AUC lane high, else priority 0; bit 2 (loc_low) the
+  // Localizer lane at the lowest priority whatever the context stream's
   int main_prio = 0;
   if (hipStreamGetPriority(c->stream, &main_prio) != hipSuccess) main_prio = 0;
   if (c->lane_cus > 0) {
@@ -325,7 +337,8 @@ int pipeline_init(Context* c) {
     }
   } else {
     DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
-                                        (c->lane_prio & 1) ? hi : main_prio));
+                                        (c->lane_prio & 1) ? hi
+                                        : (c->lane_prio & 4) ? lo : main_prio));
     DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
                                         (c->lane_prio & 2) ? hi : 0));
   }
@@ -395,9 +408,12 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lane_cu_stride = kw.lane_cu_stride;
   c->main_excl = kw.main_excl;
   c->fwd_lanes = kw.fwd_lanes;
+  c->fwd_ids = kw.fwd_ids;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;
   c->lb_diag = kw.lb_diag;
+  c->lb_tiles = kw.lb_tiles;
+  c->lb_wave = kw.lb_wave;
   c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {

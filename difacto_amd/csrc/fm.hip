@@ -316,9 +316,17 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 // CPL = 8 (kwarg fwd_cpl, V_dim a multiple of 8, not FAT): two float4 of V per lane, half the
 // lanes per row; each coordinate's sums are still one lane's in nnz order and s is summed over
 // l = 0..d-1 in order, so predictions are bit-identical to CPL = 4.
-template <int G, bool FAT, int NB = 8, int CPL = 4>
+// IDS (FAT, kwarg fwd_ids=1): the group first stages the row's next ~kFwdIds ids (and values; a
+// whole number of trips) in LDS in one trip — G lanes, all loads in flight — and each trip reads
+// its NB ids from LDS: a trip is one memory round trip (the slots) instead of two (ids, then
+// slots).  The same sums in the same order: bit-identical.
+constexpr int kFwdIds = 40;
+
+template <int G, bool FAT, int NB = 8, int CPL = 4, bool IDS = false>
 __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   static_assert(CPL == 4 || (CPL == 8 && !FAT), "fat slots: one float4 per lane");
+  constexpr int CHI = (kFwdIds / NB) * NB;  // ids staged per chunk: whole trips
+  static_assert(!IDS || (FAT && CHI % G == 0), "staged ids: fat slots");
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
   constexpr int MA = CH / G;      // lookups per lane per chunk
@@ -340,17 +348,41 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
     const bool valued = a.val != nullptr;
     const bool ntf = (a.nt & kNtFwdTable) != 0;
     if constexpr (FAT) {
+      __shared__ uint64_t s_id[IDS ? RPB : 1][IDS ? CHI : 1];
+      __shared__ float s_x[IDS ? RPB : 1][IDS ? CHI : 1];
+      uint64_t c_end = o0;  // the staged chunk of ids ends here
       for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
         const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
         uint64_t key[NB];
         float xm[NB];
+        if constexpr (IDS) {
+          if (j0 >= c_end) {  // the next CHI ids of the row, one trip (group-uniform)
+            __builtin_amdgcn_wave_barrier();  // the last chunk's reads are done
+#pragma unroll
+            for (int m = 0; m < CHI / G; ++m) {
+              const uint64_t j = j0 + l + (uint64_t)G * m;
+              if (j < o1) {
+                s_id[g][l + G * m] = a.index[j];
+                if (valued) s_x[g][l + G * m] = a.val[j];
+              }
+            }
+            __builtin_amdgcn_wave_barrier();
+            c_end = j0 + CHI;
+          }
+        }
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
           const uint64_t jj = j0 + t < o1 ? j0 + t : o1 - 1;
-          const uint64_t id = a.index[jj];
+          uint64_t id;
+          if constexpr (IDS) {
+            id = s_id[g][(int)(jj - (c_end - CHI))];
+            xm[t] = valued ? s_x[g][(int)(jj - (c_end - CHI))] : 1.f;
+          } else {
+            id = a.index[jj];
+            xm[t] = valued ? a.val[jj] : 1.f;
+          }
           const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
           key[t] = a.keys_ready ? id : reverse_bytes(mm);
-          xm[t] = valued ? a.val[jj] : 1.f;
         }
         float4 v[NB];
         float2 eh[NB];  // even lanes {w, vrow}, odd lanes the key
@@ -581,9 +613,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
 }
 
 // 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
-template <int G, int NB>
+template <int G, int NB, bool IDS = false>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
-  fwd_probe_body<G, true, NB>(a);
+  fwd_probe_body<G, true, NB, 4, IDS>(a);
 }
 
 // Fat-slot forward, second form (kwarg fwd_lanes = 2 | 4; V_dim 16, 128-byte slots): G lanes
@@ -824,6 +856,12 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
     if (G == 2) hipLaunchKernelGGL((k_fm_fwd_fat<2, 8>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 4)
       hipLaunchKernelGGL((k_fm_fwd_fat<4, 4>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 6 && a.fwd_ids)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 6, true>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 8 && a.fwd_ids)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true>), grid, dim3(kFmNT), 0, st, a);
+    else if (G == 4 && a.fat_nb == 12 && a.fwd_ids)
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 12, true>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 6)
       hipLaunchKernelGGL((k_fm_fwd_fat<4, 6>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 12)
@@ -1705,6 +1743,10 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, boo
 // +3 % step throughput, the backward itself unchanged (5 waves / SIMD already saturate its
 // random-line traffic).  The context kwarg bwd_lds overrides (bytes, 0 = no cap).
 constexpr size_t kBwdLdsCap = 32768;
+// The one-kernel fused backward (V_dim < 128) since round 4's lighter lanes (bucket Localizer,
+// radix AUC): 16 KiB, i.e. up to 10 blocks by LDS (8 by wave slots).  Same-box A/B at C3:
+// 32 KiB 123.4, 20 KiB 126.9, 16 KiB 127.7 M ex/s (backward 0.53 -> 0.42 ms).
+constexpr size_t kBwdLdsCapFused = 16384;
 
 // Lane layout of a fused backward.  kwarg bwd_cpl = 8 at V_dim >= 64 (float4-aligned rows):
 // two float4 per lane, half the lanes per key — a key's walk (entry, rows, update) is latency
@@ -1728,7 +1770,7 @@ static void bwd_lanes(const BwdArgs& a, bool aligned, int* G, int* CPL, bool* ve
 template <bool FUSED>
 int launch_bwd(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, bool aligned = FUSED,
                long lds = -1) {
-  const size_t lds_bytes = lds >= 0 ? (size_t)lds : (FUSED ? kBwdLdsCap : 0);
+  const size_t lds_bytes = lds >= 0 ? (size_t)lds : (FUSED ? kBwdLdsCapFused : 0);
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;
   bool vec;

@@ -74,6 +74,7 @@ struct DevState {
   // bucket map was fitted to (the previous batch on this lane; pk_valid == 0: none yet)
   unsigned long long kmin, kmax, pk_min, pk_max;
   unsigned int pk_valid;
+  unsigned int lb_over;  // buckets of this batch beyond the LDS sort's capacity (k_lb_colscan)
   // the bucket AUC (locbucket.hip): the area summed over buckets, buckets done, and the key
   // range of this snapshot as max(~key) / max(key) (zero when fresh)
   double auc_area;
@@ -230,14 +231,18 @@ struct Context {
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
+  int fwd_ids = 0;        // kwarg fwd_ids (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
+  int lb_wave = 1;        // kwarg lb_wave: one bucket per wave (locbucket.hip k_lb_wbucket)
+  int lb_tiles = 256;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
-  int auc_sort = 2;  // the AUC lane's sort (kwarg auc_sort): 2 bucket, 1 onesweep radix, 0 merge
+  int auc_sort = 1;  // the AUC lane's sort (kwarg auc_sort): 3 wave buckets, 2 block buckets,
+                     // 1 onesweep radix, 0 merge
   int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)
   int sort_lookback = 4;  // the Localizer sort's look-back step width (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
@@ -454,7 +459,7 @@ int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_
 // SGDUpdater::Get's find-or-insert over a lane's sorted unique keys (step.hip k_probe_keys)
 int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uniq,
                    uint32_t* segslot);
-// mode: kwarg auc_sort (2 bucket, 1 radix, 0 merge)
+// mode: kwarg auc_sort (3 wave buckets, 2 block buckets, 1 radix, 0 merge)
 int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, double* out_dev,
             int mode);
 // the same in two parts: the snapshot of (pred, label) on stream st, the rest on L.stream
@@ -464,7 +469,7 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, int m
 // the bucket sort's AUC*n of a snapshot (locbucket.hip); *used = false when the workspace's
 // hint sent it to the radix sort (nothing enqueued)
 int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
-               double* out_dev, bool accumulate, bool* used);
+               double* out_dev, bool accumulate, bool wave, bool* used);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

@@ -1,35 +1,40 @@
 // Localizer::Compact (src/data/localizer.cc:11-107) as a bucket sort, for the callers that need
 // no per-nnz col: the fused step and the split owner, whose forward finds each key in the model
-// table itself and whose backward walks each key's occurrences in sorted order.  Five launches
-// where the radix Localizer (localize.hip + sort.hip) takes ~17, and about half its traffic:
+// table itself and whose backward walks each key's occurrences in sorted order.  Eight short
+// launches where the radix Localizer (localize.hip + sort.hip) takes ~17, and about half its
+// traffic; no look-back chain and no ticket counter (blocks take their tile / bucket by block
+// index — device-scope atomics on one word serialise at ~88 per microsecond on MI355X):
 //
-//   k_lb_init     the batch's key statistics and the bucket tickets reset
+//   k_lb_init     the batch's key statistics reset
 //   k_lb_hist     per tile of rows: every nnz's key (ReverseBytes(id % max_index),
 //                 localizer.cc:24) and its bucket into the tile's histogram (LDS); OR / AND /
 //                 min / max of the keys.  A key's bucket is a monotone map of the key,
 //                 clamp((key - base) >> s), fitted to the key range of the previous batch on this
 //                 lane: buckets are ranges of keys in key order whatever the batch holds, and a
 //                 batch like the previous one spreads evenly over them
-//   k_lb_colscan  per bucket: the exclusive prefix of its counts over the tiles, and its total
+//   k_lb_colscan  per bucket: the exclusive prefix of its counts over the tiles, its total, and
+//                 the count of buckets beyond the LDS sort's capacity
 //   k_lb_scatter  per tile: the buckets' starts (a scan of the totals), then every nnz's item
 //                 into its bucket's range through an LDS cursor per bucket.  An item packs the
 //                 key's varying bits above the row (binary data) or the position (valued data,
 //                 {value, row} beside it) in one u64 when they fit; else the key and the row /
 //                 position travel apart
-//   k_lb_bucket   one block per bucket, in bucket order: the bucket sorted in LDS — LSD radix
-//                 over the digits that vary inside it, on the whole item: (key, row) resp.
-//                 (key, position) is a total order and equal items are the same occurrence
-//                 data, so the scatter's order inside a bucket never shows — then its heads (CountUniqIndex's run-length pass), the
-//                 heads of the buckets before it by decoupled look-back (RemapIndex's ranks),
-//                 and the outputs: per rank its key and segment start, per occurrence in sorted
-//                 order its row (and value).  A bucket beyond the LDS capacity (skewed keys, or a
-//                 key range that moved) is sorted by its block through global memory in stable
-//                 8-bit LSD passes: slower, the same result; the workspace's hint then sends
-//                 the next batches to the radix Localizer and retries every kLbRetry batches.
+//   k_lb_big      (exits at once unless a bucket is oversize: skewed keys, or a key range that
+//                 moved) such buckets sorted in place through global memory by a few looping
+//                 blocks, stable 8-bit LSD passes — slower, the same result; the workspace's hint
+//                 then sends the next batches to the radix Localizer and retries every kLbRetry
+//   k_lb_bucket   one block per bucket: the bucket sorted in LDS — LSD radix over the digits
+//                 that vary inside it, on the whole item: (key, row) resp. (key, position) is a
+//                 total order and equal items are the same occurrence data, so the scatter's
+//                 order inside a bucket never shows — then its heads (CountUniqIndex's run-length
+//                 pass) at the bucket's own offset in scratch lists, per occurrence in sorted
+//                 order its row (and value), and the bucket's head count
+//   k_lb_bscan    one block: the exclusive scan of the head counts (RemapIndex's ranks), U
+//   k_lb_out      per bucket its heads to their ranks: per rank its key and segment start
 //
 // The occurrence order is the radix Localizer's stable (key, position) order: positions ascend
 // with rows, and a binary row's repeats of one key are identical items.  So the outputs are
-// bit-identical to localize.hip's (test_gpu_r4.py compares the two).
+// bit-identical to localize.hip's (test_gpu_r3.py test_bucket_localizer_equals_lsd).
 #include <algorithm>
 
 #include "lookback.h"
@@ -136,6 +141,7 @@ __global__ void k_lb_init(DevState* ds) {
   ds->kmin = ~0ull;
   ds->kmax = 0;
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
+  ds->lb_over = 0;
   unsigned* meta = ds->sortmeta;
   meta[kSortMetaEpoch] = ++ds->sort_epoch;  // tags this Localizer's look-back words
   meta[kSortMetaCpTile] = 0;                // the chunk plan's tile tickets
@@ -166,28 +172,32 @@ __device__ inline unsigned long long lb_wave_max(unsigned long long v) {
 
 constexpr int kLbUnr = 8;  // ids in flight per thread
 
-__global__ __launch_bounds__(kLbNT) void k_lb_hist(LbArgs a) {
+// the histogram and scatter kernels' blocks: 16 waves on a tile, for the loads in flight
+constexpr int kLbHNT = 1024;
+constexpr int kLbHWaves = kLbHNT / kWave;
+
+__global__ __launch_bounds__(kLbHNT) void k_lb_hist(LbArgs a) {
   extern __shared__ uint32_t lb_dyn[];
   uint32_t* hist = lb_dyn;
-  __shared__ unsigned long long red[4][kLbWaves];
+  __shared__ unsigned long long red[4][kLbHWaves];
   const LbMap m = lb_map(a.ds, a.wbits);
   const int t = threadIdx.x;
-  for (uint32_t d = t; d < m.nbk; d += kLbNT) hist[d] = 0;
+  for (uint32_t d = t; d < m.nbk; d += kLbHNT) hist[d] = 0;
   const int64_t r0 = (int64_t)blockIdx.x * a.rt;
   const int64_t r1 = r0 + a.rt < a.B ? r0 + a.rt : a.B;
   const uint64_t j0 = a.offset[r0], j1 = a.offset[r1];
   __syncthreads();
   unsigned long long vor = 0, vand = ~0ull, vmin = ~0ull, vmax = 0;
-  for (uint64_t jb = j0; jb < j1; jb += (uint64_t)kLbUnr * kLbNT) {
+  for (uint64_t jb = j0; jb < j1; jb += (uint64_t)kLbUnr * kLbHNT) {
     uint64_t id[kLbUnr];
 #pragma unroll
     for (int u = 0; u < kLbUnr; ++u) {
-      const uint64_t j = jb + (uint64_t)u * kLbNT + t;
+      const uint64_t j = jb + (uint64_t)u * kLbHNT + t;
       id[u] = j < j1 ? ldnt(a.index + j, a.nt != 0) : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < kLbUnr; ++u) {
-      if (jb + (uint64_t)u * kLbNT + t < j1) {
+      if (jb + (uint64_t)u * kLbHNT + t < j1) {
         const uint64_t k = lb_key(id[u], a.max_index, a.keys_ready);
         vor |= k;
         vand &= k;
@@ -210,9 +220,9 @@ __global__ __launch_bounds__(kLbNT) void k_lb_hist(LbArgs a) {
   }
   __syncthreads();
   uint32_t* dst = a.tilecnt + (size_t)blockIdx.x * m.nbk;
-  for (uint32_t d = t; d < m.nbk; d += kLbNT) dst[d] = hist[d];
+  for (uint32_t d = t; d < m.nbk; d += kLbHNT) dst[d] = hist[d];
   if (t == 0 && j1 > j0) {
-    for (int i = 1; i < kLbWaves; ++i) {
+    for (int i = 1; i < kLbHWaves; ++i) {
       vor |= red[0][i];
       vand &= red[1][i];
       vmin = red[2][i] < vmin ? red[2][i] : vmin;
@@ -248,7 +258,11 @@ __global__ __launch_bounds__(kLbScanWaves * kWave) void k_lb_colscan(LbArgs a) {
       part[i][l] = run;
       run += x;
     }
-    if (ok) a.totals[b] = run;
+    if (ok) {
+      a.totals[b] = run;
+      // (rare) k_lb_big's gate; the AUC's view of this scan has no state
+      if (a.ds && run > (uint32_t)kLbCap) atomicAdd(&a.ds->lb_over, 1u);
+    }
   }
   __syncthreads();
   if (ok) {
@@ -263,9 +277,10 @@ __global__ __launch_bounds__(kLbScanWaves * kWave) void k_lb_colscan(LbArgs a) {
 }
 
 template <bool S>
-__global__ __launch_bounds__(kLbNT) void k_lb_scatter(LbArgs a) {
+__global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
   extern __shared__ uint64_t lb_dyn64[];
-  __shared__ uint32_t lds[kLbWaves + 1];
+  __shared__ uint32_t lds[kLbHWaves + 1];
+  __shared__ uint32_t whist[kLbHWaves][kWave];
   const LbMap m = lb_map(a.ds, a.wbits);
   uint32_t* cur = reinterpret_cast<uint32_t*>(lb_dyn64);  // per bucket: this tile's next slot
   uint64_t* offs = lb_dyn64 + (m.nbk + 1u) / 2;
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_scatter(LbArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
   // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
-  const uint32_t per = (m.nbk + kLbNT - 1) / kLbNT;
+  const uint32_t per = (m.nbk + kLbHNT - 1) / kLbHNT;
   uint32_t mine = 0, over = 0;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
@@ -284,7 +299,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_scatter(LbArgs a) {
     }
   }
   uint32_t total;
-  uint32_t ex = block_excl_scan<kLbNT>(mine, lds, &total);
+  uint32_t ex = block_excl_scan<kLbHNT>(mine, lds, &total);
   const uint32_t* pre = a.tilecnt + (size_t)blockIdx.x * m.nbk;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
@@ -298,7 +313,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_scatter(LbArgs a) {
   const LbPack p = lb_pack(a.ds, qmax);
   if (blockIdx.x == 0) {
     uint32_t nover;
-    (void)block_excl_scan<kLbNT>(over, lds, &nover);
+    (void)block_excl_scan<kLbHNT>(over, lds, &nover);
     if (t == 0) {
       a.bstart[m.nbk] = total;
       // the next batches' choice (pinned host words, vector stores)
@@ -306,30 +321,57 @@ __global__ __launch_bounds__(kLbNT) void k_lb_scatter(LbArgs a) {
       a.hint[2] = p.packed ? 1u : 2u;
     }
   }
-  for (int i = t; i <= nr; i += kLbNT) offs[i] = a.offset[r0 + i];
+  for (int i = t; i <= nr; i += kLbHNT) offs[i] = a.offset[r0 + i];
   __syncthreads();
   const uint64_t j0 = offs[0], j1 = offs[nr];
   const uint64_t qmask = p.rb ? (~0ull >> (64 - p.rb)) : 0ull;
-  for (uint64_t jb = j0; jb < j1; jb += (uint64_t)kLbUnr * kLbNT) {
+  // Each wave takes a contiguous segment of kLbUnr * 64 items per round, 64 per step, and
+  // carries the row of its window's first item from step to step: the rows of a window's
+  // items are that row plus the count of the next 64 rows' starts at or before each item — a
+  // histogram of the starts' offsets in the window (LDS) and a wave scan, one LDS round trip
+  // where a binary search over the tile's offsets took nine.  When all of the next 64 rows
+  // start inside the window (rows of one item, or empty rows) the step searches instead.
+  const int w = t / kWave, l = lane_id();
+  uint32_t* wh = whist[w];
+  auto search = [&](uint64_t j) {  // the row of item j: upper_bound(j) - 1 over offs[0..nr]
+    int lo = 0, hi = (a.diag & 8) ? 0 : nr;  // (diag 8, measurement only: no search)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offs[mid] <= j) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  for (uint64_t jb = j0; jb < j1; jb += (uint64_t)kLbUnr * kLbHNT) {
+    const uint64_t wj = jb + (uint64_t)w * kLbUnr * kWave;
     uint64_t id[kLbUnr];
     float x[kLbUnr];
 #pragma unroll
     for (int u = 0; u < kLbUnr; ++u) {
-      const uint64_t j = jb + (uint64_t)u * kLbNT + t;
+      const uint64_t j = wj + (uint64_t)u * kWave + l;
       id[u] = j < j1 ? ldnt(a.index + j, a.nt != 0) : 0ull;
       if (S) x[u] = j < j1 ? ldnt(a.value + j, a.nt != 0) : 0.f;
     }
+    if (wj >= j1) continue;  // wave-uniform
+    int ra = search(wj);     // the row of the window's first item (wave-uniform)
 #pragma unroll
     for (int u = 0; u < kLbUnr; ++u) {
-      const uint64_t j = jb + (uint64_t)u * kLbNT + t;
+      const uint64_t J = wj + (uint64_t)u * kWave;
+      if (J >= j1) break;  // wave-uniform
+      const int rl = ra + 1 + l;
+      const uint64_t sl = rl <= nr ? offs[rl] : ~0ull;  // > J
+      wh[l] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (sl - J < (uint64_t)kWave) atomicAdd(&wh[sl - J], 1u);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t before = wave_incl_scan(wh[l]);  // the next rows starting at <= J + l
+      __builtin_amdgcn_wave_barrier();
+      const bool full = __shfl(sl, kWave - 1, kWave) <= J + kWave;
+      const uint64_t j = J + l;
+      const int lo = full ? search(j) : ra + (int)before;
+      ra = full ? search(J + kWave)
+                : ra + (int)__popcll(__ballot(sl <= J + kWave));
       if (j >= j1) continue;
       const uint64_t k = lb_key(id[u], a.max_index, a.keys_ready);
-      // row = upper_bound(j) - 1 over the tile's offsets (empty rows skipped)
-      int lo = 0, hi = nr;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (offs[mid] <= j) lo = mid; else hi = mid;
-      }
       const uint32_t row = (uint32_t)(r0 + lo);
       const uint64_t q = S ? j : (uint64_t)row;
       const uint32_t pos = atomicAdd(&cur[lb_bucket(k, m)], 1u);
@@ -574,6 +616,10 @@ __global__ __launch_bounds__(kLbNT) void k_lb_big(LbArgs a, int q_lds) {
   const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
   const LbPack p = lb_pack(a.ds, qmax);
   const bool hasq = !p.packed;
+  // nothing to do unless a bucket is oversize or the items did not pack as the launch expected
+  if (__hip_atomic_load(&a.ds->lb_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+      (p.packed || q_lds))
+    return;
   __shared__ uint32_t s_list[kLbNT];
   __shared__ uint32_t s_nlist;
   uint32_t listed = 0;  // buckets needing this kernel so far; block i takes the list's i, i + G, ...
@@ -700,7 +746,6 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
       lb_lds_sort<Q, S>(kr, qr, sr, n, hasq, sk, sq, ss, wcnt, lds, s_red);
     }
   }
-  auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
   // ---- per occurrence its row (and value); per head (an item whose key differs from the one
   // before it, the bucket's first always) its key and segment start at the bucket's own offset
   // in the scratch lists (k_lb_out moves them to their ranks); a segment longer than kChunkOcc
@@ -710,6 +755,9 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
   uint64_t* tkey = a.kscr + start;
   uint32_t run = 0;
   bool longseg = false;
+  // instantiated for the LDS and the global-memory copy apart (no flat loads)
+  auto heads = [&](const uint64_t* K, const uint32_t* Qs, const uint64_t* Ss) {
+  auto item = [&](int i) -> uint64_t { return K[i]; };
   for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
     const int ib = c0 + t * kLbIT;
     uint32_t h[kLbIT], s = 0;
@@ -742,21 +790,237 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
         }
         uint32_t row;
         if (S) {
-          const uint64_t sv = fast ? ss[i] : gs[i];
+          const uint64_t sv = Ss[i];
           row = (uint32_t)(sv >> 32);
           if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sv);
         } else {
-          row = p.packed ? (uint32_t)(it & qmask) : (fast ? sq[i] : gq[i]);
+          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
         }
         a.occ_row[start + i] = row;
       }
     }
     run += ctot;
   }
+  };
+  if (fast) heads(sk, sq, ss);
+  else heads(gk, gq, gs);
   if (__syncthreads_or(longseg) && t == 0 &&
       __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     atomicOr(&ds->n_init, 1u);
   if (t == 0) a.bheads[b] = run;
+}
+
+// ---- one wave per bucket (kwarg lb_wave=1, the default): k_lb_bucket's sort and outputs with no
+// block barrier.  The wave holds up to kLbCap items, kLbWIT per lane (lane l's slot c is the
+// bucket's position c * 64 + l), ranks each pass's digits with ballots against its own 256
+// counters, scans them across its lanes, scatters through LDS and reads back; the heads' ranks
+// are a ballot prefix per slot.  A 64-thread block per bucket: ~17 KiB of LDS and one wave, so
+// the buckets pack the CUs around the backward's blocks, and no pass waits on other waves.
+constexpr int kLbWIT = kLbCap / kWave;  // 32
+
+// a bucket's n <= kLbCap items (+ rows / positions, side payloads) sorted by one wave into LDS:
+// LSD radix over the digits that vary inside the bucket, q's first when the items are not
+// packed; positions >= n of the last slot hold padding ~0
+template <bool Q, bool S>
+__device__ __attribute__((always_inline)) inline void lb_wave_sort(const uint64_t* gk, const uint32_t* gq, const uint64_t* gs,
+                                    int n, bool hasq, int ntp, int diag, uint64_t* sk,
+                                    uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
+  const int l = threadIdx.x;
+  const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
+    // the last slot's lanes past n hold padding ~0, which sorts after every item (packed items
+    // keep the top bit clear; raw keys are never kEmptyKey): every pass then runs on whole
+    // slots with no lane masks, and the padding ends at positions >= n
+    uint64_t k[kLbWIT], sv[kLbWIT];
+    uint32_t q[kLbWIT];
+#pragma unroll
+    for (int c = 0; c < kLbWIT; ++c) {  // every load in flight at once
+      const int i = c * kWave + l;
+      const bool v = c < nc && i < n;
+      k[c] = v ? ldnt(gk + i, ntp != 0) : ~0ull;
+      q[c] = (Q && hasq) ? (v ? gq[i] : ~0u) : 0u;
+      sv[c] = (S && v) ? gs[i] : 0ull;
+    }
+    unsigned long long kor = 0, kand = ~0ull, qor = 0, qand = ~0ull;
+#pragma unroll
+    for (int c = 0; c < kLbWIT; ++c) {
+      if (c < nc) {
+        const bool v = c * kWave + l < n;
+        kor |= v ? k[c] : 0ull;
+        kand &= k[c];  // (padding is all ones)
+        if (Q && hasq) {
+          qor |= v ? q[c] : 0u;
+          qand &= q[c];
+        }
+      }
+    }
+    kor = lb_wave_or(kor);
+    kand = lb_wave_and(kand);
+    if (Q) {
+      qor = lb_wave_or(qor);
+      qand = lb_wave_and(qand);
+    }
+    const unsigned long long kvary = kor ^ kand, qvary = (Q && hasq) ? (qor ^ qand) : 0ull;
+    int last = -1;  // the last active pass (0..3: q's digits, 4..11: the key's)
+    if (!(diag & 1))
+      for (int pass = 0; pass < 12; ++pass) {
+        const unsigned long long vary = pass < 4 ? qvary : kvary;
+        const int shift = 8 * (pass < 4 ? pass : pass - 4);
+        if ((vary >> shift) & 255ull) last = pass;
+      }
+    if (last < 0) {  // one item value (or none; or diag 1): in place
+#pragma unroll
+      for (int c = 0; c < kLbWIT; ++c) {
+        if (c < nc) {
+          const int i = c * kWave + l;
+          sk[i] = k[c];
+          if (Q && hasq) sq[i] = q[c];
+          if (S) ss[i] = sv[c];
+        }
+      }
+    }
+    for (int pass = 0; pass <= last; ++pass) {
+      const bool on_q = pass < 4;
+      const unsigned long long vary = on_q ? qvary : kvary;
+      const int shift = 8 * (on_q ? pass : pass - 4);
+      if (((vary >> shift) & 255ull) == 0) continue;
+#pragma unroll
+      for (int i = 0; i < 256 / kWave; ++i) cnt[i * kWave + l] = 0;
+      __builtin_amdgcn_wave_barrier();
+      // the digits' counts (LDS adds, no return), their starts, then each slot's items ranked
+      // by ballots on the digit's running start and scattered
+#pragma unroll
+      for (int c = 0; c < kLbWIT; ++c) {
+        if (c < nc) {
+          const uint32_t d = on_q ? (q[c] >> shift) & 255u : (uint32_t)(k[c] >> shift) & 255u;
+          atomicAdd(&cnt[d], 1u);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      {  // lane l holds digits 4l .. 4l + 3
+        const uint32_t c0 = cnt[4 * l], c1 = cnt[4 * l + 1], c2 = cnt[4 * l + 2],
+                       c3 = cnt[4 * l + 3];
+        const uint32_t s4 = c0 + c1 + c2 + c3;
+        const uint32_t ex = wave_incl_scan(s4) - s4;
+        __builtin_amdgcn_wave_barrier();
+        cnt[4 * l] = ex;
+        cnt[4 * l + 1] = ex + c0;
+        cnt[4 * l + 2] = ex + c0 + c1;
+        cnt[4 * l + 3] = ex + c0 + c1 + c2;
+        __builtin_amdgcn_wave_barrier();
+      }
+      uint32_t pos[kLbWIT];
+#pragma unroll
+      for (int c = 0; c < kLbWIT; ++c) {
+        pos[c] = 0;
+        if (c < nc) {
+          const uint32_t d = on_q ? (q[c] >> shift) & 255u : (uint32_t)(k[c] >> shift) & 255u;
+          uint64_t peers = ~0ull;
+#pragma unroll
+          for (int bt = 0; bt < 8; ++bt) {
+            const bool bit = (d >> bt) & 1u;
+            const uint64_t mb = __ballot(bit);
+            peers &= bit ? mb : ~mb;
+          }
+          const uint32_t rk = (uint32_t)__popcll(peers & lanemask_lt());
+          const uint32_t base = cnt[d];
+          __builtin_amdgcn_wave_barrier();
+          if (rk == 0) cnt[d] = base + (uint32_t)__popcll(peers);
+          __builtin_amdgcn_wave_barrier();
+          pos[c] = base + rk;
+        }
+      }
+      // all reads of this pass's items are done (they are in registers): scatter
+#pragma unroll
+      for (int c = 0; c < kLbWIT; ++c) {
+        if (c < nc) {
+          sk[pos[c]] = k[c];
+          if (Q && hasq) sq[pos[c]] = q[c];
+          if (S) ss[pos[c]] = sv[c];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (pass == last) break;  // the sorted bucket stays in LDS
+#pragma unroll
+      for (int c = 0; c < kLbWIT; ++c) {
+        if (c < nc) {
+          const int i = c * kWave + l;
+          k[c] = sk[i];
+          if (Q && hasq) q[c] = sq[i];
+          if (S) sv[c] = ss[i];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <bool Q, bool S>
+__global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
+  __shared__ uint64_t sk[kLbCap];
+  __shared__ uint32_t sq[Q ? kLbCap : 1];
+  __shared__ uint64_t ss[S ? kLbCap : 1];
+  __shared__ uint32_t cnt[256];
+  DevState* ds = a.ds;
+  const int l = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  const int64_t start = a.bstart[b];
+  const int n = (int)((int64_t)a.bstart[b + 1] - start);
+  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const LbPack p = lb_pack(ds, qmax);
+  const bool hasq = !p.packed;
+  // sorted in LDS here, or already in place (k_lb_big)
+  const bool fast = !lb_needs_global(n, p.packed, Q ? 1 : 0);
+  const uint64_t* gk = a.kbuf + start;
+  const uint32_t* gq = a.qbuf + start;
+  const uint64_t* gs = a.sbuf + start;
+  const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
+  if (fast) lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, sk, sq, ss, cnt);
+  // ---- per occurrence its row (and value); per head its key and segment start at the
+  // bucket's own offset in the scratch lists (k_lb_out moves them to their ranks); a segment
+  // longer than kChunkOcc raises the chunk plan's gate.  Instantiated for the LDS and for the
+  // global-memory copy apart: one pointer chosen at run time would make every read a flat load.
+  const uint64_t qmask = p.rb ? (~0ull >> (64 - p.rb)) : 0ull;
+  uint32_t* tseg = a.qscr + start;
+  uint64_t* tkey = a.kscr + start;
+  uint32_t run = 0;
+  bool longseg = false;
+  auto heads = [&](const uint64_t* K, const uint32_t* Qs, const uint64_t* Ss) {
+    uint64_t prev = 0;  // the key bits of the item before this slot's first
+    for (int c = 0; c < nc; ++c) {
+      const int i = c * kWave + l;
+      const bool valid = i < n;
+      const uint64_t it = valid ? K[i] : 0ull;
+      const uint64_t kb = lb_keybits(p, it);
+      const uint64_t up = __shfl_up(kb, 1, kWave);
+      const bool h = valid && (i == 0 || kb != (l == 0 ? prev : up));
+      if (valid && i >= kChunkOcc && kb == lb_keybits(p, K[i - kChunkOcc])) longseg = true;
+      prev = __shfl(kb, kWave - 1, kWave);
+      const uint64_t hb = __ballot(h);
+      if (!(a.diag & 4) && valid) {
+        if (h) {
+          const uint32_t r = run + (uint32_t)__popcll(hb & lanemask_lt());
+          tkey[r] = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
+          tseg[r] = (uint32_t)(start + i);
+        }
+        uint32_t row;
+        if (S) {
+          const uint64_t sw = Ss[i];
+          row = (uint32_t)(sw >> 32);
+          if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sw);
+        } else {
+          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
+        }
+        a.occ_row[start + i] = row;
+      }
+      run += (uint32_t)__popcll(hb);
+    }
+  };
+  if (fast) heads(sk, sq, ss);
+  else heads(gk, gq, gs);
+  if (__ballot(longseg) && l == 0 &&
+      __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&ds->n_init, 1u);
+  if (l == 0) a.bheads[b] = run;
 }
 
 // the buckets' first ranks: an exclusive scan of their head counts (one block); U, the closing
@@ -821,7 +1085,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   int wbits = 1;
   while (wbits < kLbMaxBits && ((int64_t)1024 << wbits) < nnz) ++wbits;
   const uint32_t nbk = 1u << wbits;
-  int64_t ntiles = std::min<int64_t>(256, std::max<int64_t>(1, nnz / 4096));
+  int64_t ntiles = std::min<int64_t>(c->lb_tiles, std::max<int64_t>(1, nnz / 4096));
   int64_t rt = std::min<int64_t>(kLbMaxRows, std::max<int64_t>(1, (B + ntiles - 1) / ntiles));
   ntiles = (B + rt - 1) / rt;
   DFX_TRY(ws.keys0.ensure(nnz * 8));
@@ -853,16 +1117,16 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.hint = ws.lb_hint;
   a.diag = c->lb_diag;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
-  hipLaunchKernelGGL(k_lb_hist, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
+  hipLaunchKernelGGL(k_lb_hist, dim3((unsigned)ntiles), dim3(kLbHNT), nbk * sizeof(uint32_t),
                      L.stream, a);
   hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
                      L.stream, a);
   const size_t scatter_lds = ((nbk + 1) & ~1u) * sizeof(uint32_t) + (rt + 1) * sizeof(uint64_t);
   if (valued)
-    hipLaunchKernelGGL(k_lb_scatter<true>, dim3((unsigned)ntiles), dim3(kLbNT), scatter_lds,
+    hipLaunchKernelGGL(k_lb_scatter<true>, dim3((unsigned)ntiles), dim3(kLbHNT), scatter_lds,
                        L.stream, a);
   else
-    hipLaunchKernelGGL(k_lb_scatter<false>, dim3((unsigned)ntiles), dim3(kLbNT), scatter_lds,
+    hipLaunchKernelGGL(k_lb_scatter<false>, dim3((unsigned)ntiles), dim3(kLbHNT), scatter_lds,
                        L.stream, a);
   // the LDS form of the per-bucket sort follows the last batch's item form (a batch whose items
   // do not pack while the launch expected packed ones sorts through global memory: correct)
@@ -872,7 +1136,16 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     hipLaunchKernelGGL(k_lb_big<true>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   else
     hipLaunchKernelGGL(k_lb_big<false>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
-  if (valued) {
+  if (c->lb_wave) {  // one wave per bucket
+    const dim3 wb(kWave);
+    if (valued) {
+      if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, true>), bg, wb, 0, L.stream, a);
+      else hipLaunchKernelGGL((k_lb_wbucket<false, true>), bg, wb, 0, L.stream, a);
+    } else {
+      if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, false>), bg, wb, 0, L.stream, a);
+      else hipLaunchKernelGGL((k_lb_wbucket<false, false>), bg, wb, 0, L.stream, a);
+    }
+  } else if (valued) {
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, true>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, true>), bg, bb, 0, L.stream, a);
   } else {
@@ -1134,11 +1407,12 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
     }
     lb_lds_sort<false, false>(kr, qr, sr, n, false, sk, nullptr, nullptr, wcnt, lds, s_red);
   }
-  auto item = [&](int i) -> uint64_t { return fast ? sk[i] : gk[i]; };
   // within the bucket: every negative adds the positives ranked below it here (exact integers
   // in double); the positives of the buckets before it are added by the last block
   double area = 0;
   uint32_t run = 0, nneg = 0;
+  auto count = [&](const uint64_t* K) {  // LDS or global instantiation (no flat loads)
+  auto item = [&](int i) -> uint64_t { return K[i]; };
   for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
     const int ib = c0 + t * kLbIT;
     uint32_t lb[kLbIT], s = 0;
@@ -1160,6 +1434,9 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
     }
     run += ctot;
   }
+  };
+  if (fast) count(sk);
+  else count(gk);
   for (int off = 32; off > 0; off >>= 1) {
     area += __shfl_xor(area, off, kWave);
     nneg += __shfl_xor(nneg, off, kWave);
@@ -1227,8 +1504,99 @@ __global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
   ds->auc_kmax = 0;
 }
 
+// one wave per AUC bucket (kwarg lb_wave=1): k_ab_bucket's sort, count and hand-off with no
+// block barrier; the last wave to finish adds the buckets' areas and cross terms
+__global__ __launch_bounds__(kWave) void k_ab_wbucket(AbArgs a) {
+  __shared__ uint64_t sk[kLbCap];
+  __shared__ uint32_t cnt[256];
+  DevState* ds = a.ds;
+  const int l = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  const uint32_t nbk = 1u << a.wbits;
+  const int64_t start = a.bstart[b];
+  const int n = (int)((int64_t)a.bstart[b + 1] - start);
+  const bool fast = n <= kLbCap;  // else sorted in place by k_ab_big
+  const uint64_t* gk = a.kbuf + start;
+  if (fast) lb_wave_sort<false, false>(gk, nullptr, nullptr, n, false, 0, 0, sk, nullptr, nullptr,
+                                       cnt);
+  // within the bucket: every negative adds the positives ranked below it here (exact integers
+  // in double); the positives of the buckets before it are added by the last wave
+  double area = 0;
+  uint32_t run = 0, nneg = 0;
+  const int nc = (n + kWave - 1) / kWave;
+  auto count = [&](const uint64_t* K) {  // LDS or global instantiation (no flat loads)
+    for (int c = 0; c < nc; ++c) {
+      const int i = c * kWave + l;
+      const bool valid = i < n;
+      const uint32_t lb = valid ? (uint32_t)(K[i] & 1ull) : 0u;
+      const uint64_t pm = __ballot(valid && lb == 1u);
+      if (valid && lb == 0u) {
+        area += (double)(run + (uint32_t)__popcll(pm & lanemask_lt()));
+        ++nneg;
+      }
+      run += (uint32_t)__popcll(pm);
+    }
+  };
+  if (fast) count(sk);
+  else count(gk);
+  for (int off = 32; off > 0; off >>= 1) {
+    area += __shfl_xor(area, off, kWave);
+    nneg += __shfl_xor(nneg, off, kWave);
+  }
+  uint32_t last = 0;
+  if (l == 0) {
+    // write-through (sc1) stores, counted by the agent-scope add; the last adder reads them
+    // with sc1 loads (MI355X_MICROARCH.md, hand-offs without an acquire, first row)
+    __hip_atomic_store(&a.barea[b], area, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.bpos[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.bneg[b], nneg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL,
+                                  __HIP_MEMORY_SCOPE_AGENT) == nbk - 1u ? 1u : 0u;
+  }
+  if (!__shfl(last, 0, kWave)) return;
+  // the last bucket done: area = sum over buckets of (its own area + its negatives x the
+  // positives of the buckets before it), then AUC * n as k_auc_final computes it, and the lane
+  // reset for the next snapshot (the bucket map fitted to this snapshot's range)
+  const uint32_t per = (nbk + kWave - 1) / kWave;
+  uint32_t mpos = 0;
+  for (uint32_t i = 0; i < per; ++i)
+    if (l * per + i < nbk) mpos += __hip_atomic_load(&a.bpos[l * per + i], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t incl = wave_incl_scan(mpos);
+  const uint32_t P = __shfl(incl, kWave - 1, kWave);
+  uint32_t pb = incl - mpos;
+  double tot_area = 0;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = l * per + i;
+    if (d < nbk) {
+      const double ar = __hip_atomic_load(&a.barea[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t ng = __hip_atomic_load(&a.bneg[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tot_area += ar + (double)ng * (double)pb;
+      pb += __hip_atomic_load(&a.bpos[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) tot_area += __shfl_xor(tot_area, off, kWave);
+  if (l != 0) return;
+  const double Pd = (double)P;
+  const double nn = (double)a.B;
+  double r;
+  if (Pd == 0 || Pd == nn) {
+    r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
+  } else {
+    const double ar = tot_area / (Pd * (nn - Pd));
+    r = (ar < 0.5 ? 1 - ar : ar) * nn;
+  }
+  *a.out = a.accumulate ? *a.out + r : r;
+  ds->auc_done = 0;
+  ds->auc_pk_min = ~ds->auc_kmin_inv;
+  ds->auc_pk_max = ds->auc_kmax;
+  ds->auc_pk_valid = 1u;
+  ds->auc_kmin_inv = 0;
+  ds->auc_kmax = 0;
+}
+
 int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
-               double* out_dev, bool accumulate, bool* used) {
+               double* out_dev, bool accumulate, bool wave, bool* used) {
   *used = false;
   Workspace& ws = *L.ws;
   if (!ws.lb_hint) {
@@ -1273,7 +1641,8 @@ int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* la
   hipLaunchKernelGGL(k_ab_scatter, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
                      L.stream, a);
   hipLaunchKernelGGL(k_ab_big, dim3(kLbBigBlocks), dim3(kLbNT), 0, L.stream, a);
-  hipLaunchKernelGGL(k_ab_bucket, dim3(nbk), dim3(kLbNT), 0, L.stream, a);
+  if (wave) hipLaunchKernelGGL(k_ab_wbucket, dim3(nbk), dim3(kWave), 0, L.stream, a);
+  else hipLaunchKernelGGL(k_ab_bucket, dim3(nbk), dim3(kLbNT), 0, L.stream, a);
   DFX_HIP(hipGetLastError());
   *used = true;
   return DFX_OK;

@@ -612,13 +612,14 @@ void cap_release(Context* c) {
   g = CapGuard{};
 }
 
-// table capacity >= 2 * need_keys, V pool >= need_vrows (doubling at least)
-static int grow_to(Context* c, int64_t need_keys, int64_t need_vrows) {
+// table capacity >= 2 * need_keys, V pool >= need_vrows (doubling at least, unless exact)
+static int grow_to(Context* c, int64_t need_keys, int64_t need_vrows, bool exact = false) {
   const Table& T = c->T;
   const bool gk = 2 * need_keys > c->cap;
   const bool gv = T.d > 0 && need_vrows > T.vcap;
   if (!gk && !gv) return DFX_OK;
-  return store_reserve(c, gk ? need_keys : 0, gv ? std::max<int64_t>(2 * T.vcap, need_vrows) : 0);
+  return store_reserve(c, gk ? need_keys : 0,
+                       gv ? (exact ? need_vrows : std::max<int64_t>(2 * T.vcap, need_vrows)) : 0);
 }
 
 int cap_check(Context* c, int64_t add) {
@@ -658,9 +659,15 @@ int cap_check(Context* c, int64_t add) {
     g.known_enq = g.enq_total;
     const int64_t need = g.known_keys + kCapRunAhead * add;
     const int64_t need_cap_keys = (10 * need + 8) / 9;  // 0.9 load with that many in flight
-    DFX_TRY(grow_to(c, std::max<int64_t>(need_cap_keys / 2 + 1,
-                                         2 * g.known_keys > c->cap ? g.known_keys : 0),
-                    has_v ? g.known_vrows + kCapRunAhead * add : 0));
+    const int64_t need_keys = std::max<int64_t>(need_cap_keys / 2 + 1,
+                                                2 * g.known_keys > c->cap ? g.known_keys : 0);
+    if (grow_to(c, need_keys, has_v ? g.known_vrows + kCapRunAhead * add : 0) != DFX_OK) {
+      // the V pool's run-ahead is priced at one V row per occurrence (the worst case; lazy V
+      // draws far fewer): when that much does not fit, grow it by one step's worst case only,
+      // exactly — the guard above then waits on older steps' counts instead of running ahead
+      (void)hipGetLastError();
+      DFX_TRY(grow_to(c, need_keys, has_v ? g.known_vrows + add : 0, true));
+    }
     break;
   }
   g.enq_total += add;

@@ -221,8 +221,8 @@ def test_auc_and_evaluate(H):
 
 @pytest.mark.parametrize("n", [1, 2, 4095, 4097, 10000, 12288, 12289, 100000, 1000003])
 def test_auc_radix_and_merge_sorts_agree(H, n):
-    """the AUC lane's three stable sorts (auc_sort=bucket | radix | merge; up to 12288 rows all
-    take the one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie
+    """the AUC lane's four stable sorts (auc_sort=wbucket | bucket | radix | merge; up to 12288
+    rows all take the one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie
     break of the oracle, with heavy ties (quantised predictions, one constant digit pattern),
     with all predictions equal (epoch 0, w = 0: one bucket far beyond the LDS sort) and with
     signed zeros (-0 == +0).  Each context sees every snapshot twice, so the bucket sort runs
@@ -231,7 +231,7 @@ def test_auc_radix_and_merge_sorts_agree(H, n):
     label = np.where(rng.random(n) < 0.25, 1.0, -1.0).astype(np.float32)
     signed0 = np.where(rng.random(n) < 0.5, np.float32(-0.0), np.float32(0.0)).astype(np.float32)
     signed0[rng.random(n) < 0.3] = -1.5
-    cs = [H.Context(0, auc_sort=mode) for mode in ["bucket", "radix", "merge"]]
+    cs = [H.Context(0, auc_sort=mode) for mode in ["bucket", "radix", "merge", "wbucket"]]
     for pred in [np.round(rng.standard_normal(n) * 8).astype(np.float32) / 8,
                  np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32),
                  signed0]:
@@ -239,7 +239,7 @@ def test_auc_radix_and_merge_sorts_agree(H, n):
         for _ in range(2):
             got = [H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32))
                    for c in cs]
-            assert got[0] == got[1] == got[2], got
+            assert got[0] == got[1] == got[2] == got[3], got
             assert abs(got[0] - want) <= 1e-4 * n, (got, want)
     for c in cs:
         c.close()

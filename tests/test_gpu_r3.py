@@ -35,14 +35,17 @@ def _auc_expect(label, opred, oauc):
     return O.auc_stable_ties(label, opred) if O.has_ties(opred) else oauc
 
 
-@pytest.mark.parametrize("lanes,nb", [(2, 4), (2, 6), (2, 8), (4, 4), (4, 6), (4, 8)])
+@pytest.mark.parametrize("lanes,nb", [(2, 4), (2, 6), (2, 8), (4, 4), (4, 6), (4, 8),
+                                      (0, 6), (0, 8), (0, 12)])
 @pytest.mark.parametrize("binary", [True, False])
 def test_prefetch_forward_bit_identical(H, lanes, nb, binary):
-    """Two contexts step the same batches: the default forward and the prefetching one.
-    Ragged rows (empty rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips."""
+    """Two contexts step the same batches: the default forward and the prefetching one
+    (fwd_lanes) or the one staging each row's ids in LDS (lanes 0: fwd_ids=1).  Ragged rows
+    (empty rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips and chunks."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     ca = H.Context(0, max_keys=1 << 16, **cfg)
-    cb = H.Context(0, max_keys=1 << 16, fwd_lanes=lanes, fat_nb=nb, **cfg)
+    kw = dict(fwd_lanes=lanes) if lanes else dict(fwd_ids=1)
+    cb = H.Context(0, max_keys=1 << 16, fat_nb=nb, **kw, **cfg)
     up = O.Updater(**cfg)
     for step in range(4):
         blk = D.synthetic(3001, 39, 1 << 15, binary=binary, ragged=True, seed=40 + step)
@@ -316,7 +319,7 @@ def _ids_of(kind, rng, n, step):
 
 
 @pytest.mark.parametrize("kind", ["uniform", "valued", "narrow", "wide", "zipf", "fields",
-                                  "shift"])
+                                  "shift", "short"])
 def test_bucket_localizer_equals_lsd(H, kind):
     """The fused step's Localizer as a bucket sort (locbucket.hip, loc_bucket=1, the default)
     against the onesweep radix sort (loc_bucket=0): predictions, loss and AUC identical every
@@ -331,7 +334,14 @@ def test_bucket_localizer_equals_lsd(H, kind):
         rows = 3000 if step == 3 else 60000
         blk = D.synthetic(rows, 39, 2, ragged=(step == 3), binary=(kind != "valued"),
                           seed=80 + step)
-        blk = D.RowBlock(blk.offs, _ids_of(kind, rng, blk.nnz, step), blk.vals, blk.labels)
+        if kind == "short":  # rows of 0-3 nnz among long ones: the scatter's row windows
+            lens = rng.choice(np.array([0, 1, 1, 2, 3, 0, 1, 120]), size=rows)
+            offs = np.zeros(rows + 1, np.uint64)
+            offs[1:] = np.cumsum(lens)
+            blk = D.RowBlock(offs, rng.integers(0, 1 << 22, int(offs[-1]), dtype=np.uint64),
+                             None, blk.labels)
+        else:
+            blk = D.RowBlock(blk.offs, _ids_of(kind, rng, blk.nnz, step), blk.vals, blk.labels)
         loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
                                          push_cnt=(step < 2), want_pred=True)
         preds, progs = [], []

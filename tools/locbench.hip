@@ -2,10 +2,14 @@
 // below 2^kbits, generated on the device) localized `iters` times on the context stream, as
 // the fused step's lane does (no col: the bucket Localizer, or the radix one with
 // loc_bucket=0), timed with events; run it under rocprofv3 --kernel-trace for per-kernel
-// times.  Measurement tool (links the library's internals), not a test.
-//   build/locbench [B] [k] [kbits] [iters] [context kwargs]
+// times.  With a sixth argument "auc": the AUC lane's sort + area of a B-row (pred, label)
+// snapshot instead (auc_sort from the kwargs).  Measurement tool (links the library's
+// internals), not a test.
+//   build/locbench [B] [k] [kbits] [iters] [context kwargs] [auc]
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <string>
 
 #include "../difacto_amd/csrc/internal.h"
 
@@ -18,6 +22,50 @@ __global__ void k_gen(int64_t B, int k, int kbits, uint64_t* offs, uint64_t* ids
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   x ^= x >> 31;
   ids[i] = x >> (64 - kbits);
+}
+
+__global__ void k_gen_pred(int64_t B, float* pred, float* lab, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  uint64_t x = seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+  lab[i] = ((x >> 8) & 3) == 0 ? 1.0f : 0.0f;
+  pred[i] = 6.0f * (u - 0.5f) + (lab[i] > 0 ? 0.7f : 0.0f);  // overlapping classes
+}
+
+static int auc_bench(dfx::Context* c, int64_t B, int iters, const char* kw) {
+  float *pred, *lab;
+  double* out;
+  hipMalloc(&pred, B * 4);
+  hipMalloc(&lab, B * 4);
+  hipMalloc(&out, 8);
+  hipLaunchKernelGGL(k_gen_pred, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, c->stream, B,
+                     pred, lab, 7ull);
+  dfx::Lane L = dfx::main_lane(c);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  double tot = 0;
+  for (int it = 0; it < iters + 2; ++it) {
+    hipEventRecord(e0, c->stream);
+    if (dfx::auc_run(L, B, lab, pred, out, c->auc_sort) != DFX_OK) {
+      fprintf(stderr, "auc: %s\n", dfx_last_error());
+      return 1;
+    }
+    hipEventRecord(e1, c->stream);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (it >= 2) tot += ms;
+  }
+  double r = 0;
+  hipMemcpy(&r, out, 8, hipMemcpyDeviceToHost);
+  printf("aucbench B=%lld kwargs='%s': %.4f ms per AUC (snapshot + sort + area), AUC*n=%.1f\n",
+         (long long)B, kw, tot / iters, r);
+  return 0;
 }
 
 int main(int argc, char** argv) {
@@ -33,6 +81,11 @@ int main(int argc, char** argv) {
     return 1;
   }
   dfx::Context* c = &ctx->c;
+  if (argc > 6 && std::string(argv[6]) == "auc") {
+    const int rc = auc_bench(c, B, iters, kw);
+    dfx_ctx_destroy(ctx);
+    return rc;
+  }
   uint64_t *offs, *ids, *uniq;
   uint32_t *seg, *occ;
   hipMalloc(&offs, (B + 1) * 8);
