@@ -77,7 +77,10 @@ struct Kw {
   // unless the batches repeat); never set by the product path
   int diag = 0;
   int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
-  int fwd_ids = 0;    // fwd_ids=1: the fat forward stages each row's ids in LDS (one trip)
+  // fwd_ids=1 (default): the fat forward stages each row's ids in LDS in one trip (fm.hip
+  // fwd_probe_body IDS; same-box A/B at C3 with fat_nb 8: 127.6 -> 130.0 M ex/s, forward
+  // 0.248 -> 0.213 ms in the step); 0: each trip loads its ids
+  int fwd_ids = 1;
   // loc_bucket=1 (default): the Localizer of the fused step and of the split owner (no col) as a
   // bucket sort — histogram, scatter into key-range buckets, one LDS sort per bucket
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
@@ -90,7 +93,9 @@ struct Kw {
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
-  int fat_nb = 6;  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B; 6: DESIGN.md (d))
+  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B, DESIGN.md (d): 8 with the staged ids,
+  // 6 without)
+  int fat_nb = 8;
   // nt=<mask>: streaming (non-temporal) cache policy for 1 the Localizer lane's sort passes and
   // transform, 2 the backward's model-table lines, 4 the forward's, 8 the backward's
   // per-occurrence arrays (common.h ld4 / st4)

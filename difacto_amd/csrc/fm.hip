@@ -334,12 +334,15 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
   const int gbase = (threadIdx.x % kWave) - l;
-  const int64_t ri = (int64_t)blockIdx.x * RPB + g;
-  const int64_t r = fwd_row(a, ri);
   const int d = a.d;
   __shared__ double red[kFmNT / kWave];
   double loss = 0;
-  if (ri < a.B) {
+  // IDS runs on a resident grid (launch_fwd_fused): the block's groups take rows blockIdx.x *
+  // RPB + g, then one grid of rows further on, so no half-empty last round of blocks; else one
+  // row per group
+  for (int64_t ri = (int64_t)blockIdx.x * RPB + g; ri < a.B;
+       ri = IDS ? ri + (int64_t)gridDim.x * RPB : a.B) {
+    const int64_t r = fwd_row(a, ri);
     const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = 0.f;
     float xv[CPL], xxvv[CPL];
@@ -583,7 +586,7 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
       if (xs > d) a.XVp[r * xs + d] = p;
       a.pred[r] = pr;
       double yy = a.label[r] > 0 ? 1.0 : -1.0;
-      loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
+      loss += log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
       if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
         uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
         a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -616,6 +619,21 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
 template <int G, int NB, bool IDS = false>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
   fwd_probe_body<G, true, NB, 4, IDS>(a);
+}
+
+// blocks of kernel K resident at once on this device (at most want): a grid whose blocks loop
+template <auto K>
+static int64_t resident_grid(int64_t want) {
+  static int per_cu = 0;  // per kernel
+  int dev = 0, cus = 0;
+  if (per_cu <= 0 &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, K, kFmNT, 0) != hipSuccess)
+    per_cu = 0;
+  if (per_cu <= 0 || hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return want;
+  return std::min<int64_t>(want, (int64_t)per_cu * cus);
 }
 
 // Fat-slot forward, second form (kwarg fwd_lanes = 2 | 4; V_dim 16, 128-byte slots): G lanes
@@ -853,15 +871,20 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   }
   if (a.index && a.B > 0 && spread && fat) {
     const dim3 grid((unsigned)*nblk);
+    // the staged-ids forms on a resident grid (their groups loop over rows): *nblk loss partials
+#define DFX_FWDIDS(NN)                                                                    \
+    if (G == 4 && a.fat_nb == NN && a.fwd_ids) {                                          \
+      *nblk = (int)resident_grid<k_fm_fwd_fat<4, NN, true>>(*nblk);                       \
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, NN, true>), dim3((unsigned)*nblk), dim3(kFmNT), 0, \
+                         st, a);                                                          \
+      DFX_HIP(hipGetLastError());                                                         \
+      return DFX_OK;                                                                      \
+    }
+    DFX_FWDIDS(6) DFX_FWDIDS(8) DFX_FWDIDS(12)
+#undef DFX_FWDIDS
     if (G == 2) hipLaunchKernelGGL((k_fm_fwd_fat<2, 8>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 4)
       hipLaunchKernelGGL((k_fm_fwd_fat<4, 4>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 6 && a.fwd_ids)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 6, true>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 8 && a.fwd_ids)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 12 && a.fwd_ids)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 12, true>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 6)
       hipLaunchKernelGGL((k_fm_fwd_fat<4, 6>), grid, dim3(kFmNT), 0, st, a);
     else if (G == 4 && a.fat_nb == 12)

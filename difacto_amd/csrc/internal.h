@@ -219,7 +219,7 @@ struct Context {
   int fat_fwd = 1;    // kwarg fat_fwd
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
-  int fat_nb = 6;         // kwarg fat_nb
+  int fat_nb = 8;         // kwarg fat_nb
   int fwd_cpl = 8;        // kwarg fwd_cpl: V coordinates per lane of the probe forward
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 1;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
@@ -231,7 +231,7 @@ struct Context {
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
-  int fwd_ids = 0;        // kwarg fwd_ids (fm.hip fwd_probe_body IDS)
+  int fwd_ids = 1;        // kwarg fwd_ids (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lb_wave = 1;        // kwarg lb_wave: one bucket per wave (locbucket.hip k_lb_wbucket)
   int lb_tiles = 256;     // kwarg lb_tiles: the bucket Localizer's row tiles at most

@@ -43,7 +43,7 @@ def test_prefetch_forward_bit_identical(H, lanes, nb, binary):
     (fwd_lanes) or the one staging each row's ids in LDS (lanes 0: fwd_ids=1).  Ragged rows
     (empty rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips and chunks."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    ca = H.Context(0, max_keys=1 << 16, **cfg)
+    ca = H.Context(0, max_keys=1 << 16, fwd_ids=0, fat_nb=6, **cfg)  # each trip loads its ids
     kw = dict(fwd_lanes=lanes) if lanes else dict(fwd_ids=1)
     cb = H.Context(0, max_keys=1 << 16, fat_nb=nb, **kw, **cfg)
     up = O.Updater(**cfg)
