@@ -81,6 +81,11 @@ def parse():
                          "share that priority's hardware queues, whose packets run in order: "
                          "a high-priority compute stream keeps the step's kernels off the "
                          "queues of RCCL's (normal-priority) streams")
+    ap.add_argument("--stale", action="store_true",
+                    help="sharded split, C++ driver: the 1-step-stale schedule (step t+1's owner "
+                         "forward before step t's backward, each step's partial exchange and "
+                         "row gather beside the other step's compute; oracle: "
+                         "dist_oracle.SplitStaleOracle)")
     ap.add_argument("--driver", default="cpp", choices=("cpp", "py"),
                     help="the split step's driver over RCCL: C++ (libdfx_dist.so, its own "
                          "communicators) or Python (dist.SplitPipeline over torch.distributed)")
@@ -186,7 +191,7 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r3"
+PMC_ROUND = "r4"
 
 # Random 128-byte chunks per second on MI355X, measured in isolation (tools/membench/pmccal,
 # DESIGN.md (d)): reads of distinct random rows, and read-modify-writes of them
@@ -636,7 +641,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         if rank == 0:
             ids = torch.frombuffer(bytearray(DI.SplitStore.rccl_ids()), dtype=torch.uint8)
         dist.broadcast(ids, src=0, group=comm.cgroup)
-        store = DI.SplitStore([shard], pipelined=not args.sync,
+        store = DI.SplitStore([shard], pipelined=not args.sync, stale=args.stale and not args.sync,
                               rccl=(rank, world, ids.numpy().tobytes(), args.force_collectives))
         if args.slices:
             store.set_slices(args.slices)
@@ -772,6 +777,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                  ("a2a_sync" if args.sync else "a2a_pipelined"))
     if store is not None:
         main_name += "_cpp"
+    if store is not None and args.stale and not args.sync:
+        main_name = "split_stale_cpp"
     py_pipe = [None]
 
     def py_split_pipelined(shards, dblks, comm_, job):
@@ -789,7 +796,8 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         # the C++ driver with the other slicing (rows in 2 slices, each slice's exchanges
         # beside the next slice's compute; or unsliced if the main run was sliced)
         other_k = 1 if args.slices > 1 else 2
-        sched.insert(1, ("split_pipelined_cpp_slices%d" % other_k, cpp_other_slices))
+        if not args.stale:  # (the stale schedule runs unsliced)
+            sched.insert(1, ("split_pipelined_cpp_slices%d" % other_k, cpp_other_slices))
     for cname, fn in sched:
         if cname == main_name or (cname != "a2a_sync" and args.push_agg != "sum"):
             continue
@@ -861,9 +869,13 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                                "push_agg=%s"
                                % (d, k, kb, world,
                                   "owner-computes split (RCCL all-to-all of per-row partials "
-                                  "+ all-gather of [XV*p | p] rows), bulk-synchronous%s"
-                                  % ("" if args.sync else " results, next step's partition / "
-                                     "key exchange / owner Localizer on the Localizer lane")
+                                  "+ all-gather of [XV*p | p] rows), %s"
+                                  % ("bulk-synchronous" if args.sync else
+                                     "1-step-stale (step t+1's owner forward before step t's "
+                                     "backward, the exchanges beside the other step's compute)"
+                                     if args.stale and store is not None else
+                                     "bulk-synchronous results, next step's partition / key "
+                                     "exchange / owner Localizer on the Localizer lane")
                                   if split else
                                   "RCCL all-to-all-v of records / gradients, %s schedule"
                                   % ("bulk-synchronous" if args.sync

@@ -89,6 +89,13 @@ struct Kw {
   // sort, 4 the outputs, 8 k_lb_scatter's row search; the Localizer's results are then wrong
   int lb_diag = 0;
   int lb_wave = 1;  // lb_wave=1: the bucket Localizer sorts one bucket per wave (0: per block)
+  // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
+  // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
+  int lb_keyfirst = 0;
+  // lb_gather=1 (default): valued batches sort (key | position) items alone, the row and the
+  // value gathered by position at the outputs (A/B at C2: 126 -> 161 M ex/s); 0: {value, row}
+  // carried beside each item
+  int lb_gather = 1;
   int lb_tiles = 256;  // lb_tiles=<n>: the bucket Localizer's row tiles (histogram / scatter blocks)
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
@@ -194,6 +201,8 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
     else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
+    else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
+    else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 256;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
@@ -419,6 +428,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_diag = kw.lb_diag;
   c->lb_tiles = kw.lb_tiles;
   c->lb_wave = kw.lb_wave;
+  c->lb_keyfirst = kw.lb_keyfirst;
+  c->lb_gather = kw.lb_gather;
   c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {

@@ -68,7 +68,8 @@ struct LbArgs {
   uint32_t* brank;       // [nbk]: the bucket's first rank (k_lb_bscan)
   uint64_t* kbuf;        // items
   uint32_t* qbuf;        // rows / positions of unpacked items
-  uint64_t* sbuf;        // side payloads (valued)
+  uint64_t* sbuf;        // side payloads (valued, carried: kwarg lb_gather=0)
+  uint32_t* rowof;       // valued, gathered (lb_gather=1): each position's row, by k_lb_scatter
   uint64_t* kscr;        // scratch of the global-memory passes
   uint32_t* qscr;
   uint64_t* sscr;
@@ -79,6 +80,7 @@ struct LbArgs {
   float* occ_x;
   unsigned int* hint;    // pinned: Workspace::lb_hint
   int diag;              // Context::lb_diag (measurement only)
+  int keyfirst;          // Context::lb_keyfirst: the wave sort's key-first form (lb_wave_sort)
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
       ex += a.totals[d];
     }
   }
-  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
   const LbPack p = lb_pack(a.ds, qmax);
   if (blockIdx.x == 0) {
     uint32_t nover;
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
     for (int u = 0; u < kLbUnr; ++u) {
       const uint64_t j = wj + (uint64_t)u * kWave + l;
       id[u] = j < j1 ? ldnt(a.index + j, a.nt != 0) : 0ull;
-      if (S) x[u] = j < j1 ? ldnt(a.value + j, a.nt != 0) : 0.f;
+      if (S && !a.rowof) x[u] = j < j1 ? ldnt(a.value + j, a.nt != 0) : 0.f;
     }
     if (wj >= j1) continue;  // wave-uniform
     int ra = search(wj);     // the row of the window's first item (wave-uniform)
@@ -378,7 +380,8 @@ __global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
       stnt(a.kbuf + pos, p.packed ? ((((k - p.kmin) >> p.lo) << p.rb) | (q & qmask)) : k,
            a.nt != 0);
       if (!p.packed) a.qbuf[pos] = (uint32_t)q;
-      if (S) a.sbuf[pos] = (uint64_t)__float_as_uint(x[u]) | ((uint64_t)row << 32);
+      if (S && a.rowof) a.rowof[j] = row;  // in input order (coalesced)
+      else if (S) a.sbuf[pos] = (uint64_t)__float_as_uint(x[u]) | ((uint64_t)row << 32);
     }
   }
 }
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_big(LbArgs a, int q_lds) {
   __shared__ unsigned long long s_red[4][kLbWaves];
   const int t = threadIdx.x;
   const uint32_t nbk = 1u << a.wbits;
-  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
   const LbPack p = lb_pack(a.ds, qmax);
   const bool hasq = !p.packed;
   // nothing to do unless a bucket is oversize or the items did not pack as the launch expected
@@ -712,7 +715,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
   const uint32_t b = blockIdx.x;
   const int64_t start = a.bstart[b];
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
-  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
   const LbPack p = lb_pack(ds, qmax);
   const bool hasq = !p.packed;
   // sorted in LDS here, or already in place (k_lb_big)
@@ -793,6 +796,8 @@ __global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
           const uint64_t sv = Ss[i];
           row = (uint32_t)(sv >> 32);
           if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sv);
+        } else if (a.rowof) {  // valued: the position now, its row and value by k_lb_gather
+          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
         } else {
           row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
         }
@@ -820,52 +825,77 @@ constexpr int kLbWIT = kLbCap / kWave;  // 32
 
 // a bucket's n <= kLbCap items (+ rows / positions, side payloads) sorted by one wave into LDS:
 // LSD radix over the digits that vary inside the bucket, q's first when the items are not
-// packed; positions >= n of the last slot hold padding ~0
+// packed; positions >= n of the last slot hold padding ~0.
+//
+// Key first (packed items, kf): the order wanted is the item's, i.e. (key bits above bit rb,
+// then the row / position below).  Inside a bucket most keys occur once or twice, so only the
+// key bits are sorted by passes (2 of them at C3, where the full item takes 4); then each run of
+// equal keys, in the scatter's order so far, is sorted whole by the lane at its head — runs of
+// up to kLbRun items in registers.  A bucket holding a longer run (hot or few keys) is sorted
+// again from its items in global memory by the full passes.  Either way the LDS holds the
+// bucket in item order.
+constexpr int kLbRun = 8;
+
 template <bool Q, bool S>
-__device__ __attribute__((always_inline)) inline void lb_wave_sort(const uint64_t* gk, const uint32_t* gq, const uint64_t* gs,
-                                    int n, bool hasq, int ntp, int diag, uint64_t* sk,
-                                    uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
+__device__ __attribute__((always_inline)) inline void lb_wave_sort(
+    const uint64_t* gk, const uint32_t* gq, const uint64_t* gs, int n, bool hasq, int ntp,
+    int diag, int rb, bool keyfirst, uint64_t* sk, uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
   const int l = threadIdx.x;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
-    // the last slot's lanes past n hold padding ~0, which sorts after every item (packed items
-    // keep the top bit clear; raw keys are never kEmptyKey): every pass then runs on whole
-    // slots with no lane masks, and the padding ends at positions >= n
-    uint64_t k[kLbWIT], sv[kLbWIT];
-    uint32_t q[kLbWIT];
+  // the last slot's lanes past n hold padding ~0, which sorts after every item (packed items
+  // keep the top bit clear; raw keys are never kEmptyKey): every pass then runs on whole
+  // slots with no lane masks, and the padding ends at positions >= n
+  uint64_t k[kLbWIT], sv[kLbWIT];
+  uint32_t q[kLbWIT];
 #pragma unroll
-    for (int c = 0; c < kLbWIT; ++c) {  // every load in flight at once
-      const int i = c * kWave + l;
-      const bool v = c < nc && i < n;
-      k[c] = v ? ldnt(gk + i, ntp != 0) : ~0ull;
-      q[c] = (Q && hasq) ? (v ? gq[i] : ~0u) : 0u;
-      sv[c] = (S && v) ? gs[i] : 0ull;
-    }
-    unsigned long long kor = 0, kand = ~0ull, qor = 0, qand = ~0ull;
+  for (int c = 0; c < kLbWIT; ++c) {  // every load in flight at once
+    const int i = c * kWave + l;
+    const bool v = c < nc && i < n;
+    k[c] = v ? ldnt(gk + i, ntp != 0) : ~0ull;
+    q[c] = (Q && hasq) ? (v ? gq[i] : ~0u) : 0u;
+    sv[c] = (S && v) ? gs[i] : 0ull;
+  }
+  unsigned long long kor = 0, kand = ~0ull, qor = 0, qand = ~0ull;
 #pragma unroll
-    for (int c = 0; c < kLbWIT; ++c) {
-      if (c < nc) {
-        const bool v = c * kWave + l < n;
-        kor |= v ? k[c] : 0ull;
-        kand &= k[c];  // (padding is all ones)
-        if (Q && hasq) {
-          qor |= v ? q[c] : 0u;
-          qand &= q[c];
-        }
+  for (int c = 0; c < kLbWIT; ++c) {
+    if (c < nc) {  // (no item and no q equals its padding, all ones: no lane masks)
+      kor |= k[c] == ~0ull ? 0ull : k[c];
+      kand &= k[c];
+      if (Q && hasq) {
+        qor |= q[c] == ~0u ? 0u : q[c];
+        qand &= q[c];
       }
     }
-    kor = lb_wave_or(kor);
-    kand = lb_wave_and(kand);
-    if (Q) {
-      qor = lb_wave_or(qor);
-      qand = lb_wave_and(qand);
-    }
-    const unsigned long long kvary = kor ^ kand, qvary = (Q && hasq) ? (qor ^ qand) : 0ull;
-    int last = -1;  // the last active pass (0..3: q's digits, 4..11: the key's)
+  }
+  kor = lb_wave_or(kor);
+  kand = lb_wave_and(kand);
+  if (Q) {
+    qor = lb_wave_or(qor);
+    qand = lb_wave_and(qand);
+  }
+  const unsigned long long kvary = kor ^ kand, qvary = (Q && hasq) ? (qor ^ qand) : 0ull;
+  // key first only for packed items whose key bits vary (one key: a single run)
+  const bool kf = keyfirst && !hasq && !(diag & 1) && rb < 64 && (kvary >> rb) != 0;
+  // the passes of one schedule (wave-uniform): KEYS — the key's digits from bit rb up; else
+  // q's 4 digits, then the item's 8 (an item's low rb bits are its row / position)
+  auto passes = [&](bool keys_only) {
+    auto pass_at = [&](int pass, bool* on_q, int* shift) {
+      if (keys_only) {
+        *on_q = false;
+        *shift = rb + 8 * pass;
+        return *shift < 64;
+      }
+      *on_q = pass < 4;
+      *shift = 8 * (*on_q ? pass : pass - 4);
+      return true;
+    };
+    int last = -1;  // the last active pass
     if (!(diag & 1))
       for (int pass = 0; pass < 12; ++pass) {
-        const unsigned long long vary = pass < 4 ? qvary : kvary;
-        const int shift = 8 * (pass < 4 ? pass : pass - 4);
-        if ((vary >> shift) & 255ull) last = pass;
+        bool on_q;
+        int shift;
+        if (!pass_at(pass, &on_q, &shift)) break;
+        if (((on_q ? qvary : kvary) >> shift) & 255ull) last = pass;
       }
     if (last < 0) {  // one item value (or none; or diag 1): in place
 #pragma unroll
@@ -879,9 +909,10 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(const uint64_
       }
     }
     for (int pass = 0; pass <= last; ++pass) {
-      const bool on_q = pass < 4;
+      bool on_q;
+      int shift;
+      (void)pass_at(pass, &on_q, &shift);
       const unsigned long long vary = on_q ? qvary : kvary;
-      const int shift = 8 * (on_q ? pass : pass - 4);
       if (((vary >> shift) & 255ull) == 0) continue;
 #pragma unroll
       for (int i = 0; i < 256 / kWave; ++i) cnt[i * kWave + l] = 0;
@@ -952,6 +983,75 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(const uint64_
       __builtin_amdgcn_wave_barrier();
     }
     __builtin_amdgcn_wave_barrier();
+  };
+  passes(kf);
+  if (!kf) return;
+  // key first: each run of equal keys sorted whole by the lane at its head (only key bits are
+  // compared while runs are found, and a run's own reordering never changes them)
+  bool longrun = false;
+  for (int c = 0; c < nc; ++c) {
+    const int i = c * kWave + l;
+    if (i >= n) continue;
+    const uint64_t kb = sk[i] >> rb;
+    if (i > 0 && (sk[i - 1] >> rb) == kb) continue;  // not a head
+    int len = 1;
+    while (len <= kLbRun && i + len < n && (sk[i + len] >> rb) == kb) ++len;
+    if (len > kLbRun) {
+      longrun = true;
+      continue;
+    }
+    if (len == 1) continue;
+    if (len == 2) {  // the common case: one compare-exchange
+      const uint64_t x0 = sk[i], x1 = sk[i + 1];
+      if (x0 > x1) {
+        sk[i] = x1;
+        sk[i + 1] = x0;
+        if (S) {
+          const uint64_t y0 = ss[i], y1 = ss[i + 1];
+          ss[i] = y1;
+          ss[i + 1] = y0;
+        }
+      }
+      continue;
+    }
+    uint64_t v[kLbRun], w[kLbRun];
+#pragma unroll
+    for (int t = 0; t < kLbRun; ++t) {
+      v[t] = t < len ? sk[i + t] : ~0ull;
+      w[t] = (S && t < len) ? ss[i + t] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kLbRun; ++r) {  // odd-even transposition: kLbRun rounds sort kLbRun
+#pragma unroll
+      for (int t = r & 1; t + 1 < kLbRun; t += 2) {
+        if (v[t] > v[t + 1]) {
+          const uint64_t x = v[t]; v[t] = v[t + 1]; v[t + 1] = x;
+          if (S) { const uint64_t y = w[t]; w[t] = w[t + 1]; w[t + 1] = y; }
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kLbRun; ++t) {
+      if (t < len) {
+        sk[i + t] = v[t];
+        if (S) ss[i + t] = w[t];
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (!__ballot(longrun)) return;
+  // a run too long for one lane: the full passes (row / position digits, then the key's) from
+  // the key-sorted order in LDS — LSD passes do not depend on the order they start from
+#pragma unroll
+  for (int c = 0; c < kLbWIT; ++c) {
+    if (c < nc) {
+      const int i = c * kWave + l;
+      k[c] = sk[i];
+      if (S) sv[c] = ss[i];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  passes(false);
 }
 
 template <bool Q, bool S>
@@ -965,7 +1065,7 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   const uint32_t b = blockIdx.x;
   const int64_t start = a.bstart[b];
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
-  const uint64_t qmax = S ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
   const LbPack p = lb_pack(ds, qmax);
   const bool hasq = !p.packed;
   // sorted in LDS here, or already in place (k_lb_big)
@@ -974,7 +1074,8 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   const uint32_t* gq = a.qbuf + start;
   const uint64_t* gs = a.sbuf + start;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
-  if (fast) lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, sk, sq, ss, cnt);
+  if (fast)
+    lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, p.rb, a.keyfirst != 0, sk, sq, ss, cnt);
   // ---- per occurrence its row (and value); per head its key and segment start at the
   // bucket's own offset in the scratch lists (k_lb_out moves them to their ranks); a segment
   // longer than kChunkOcc raises the chunk plan's gate.  Instantiated for the LDS and for the
@@ -1007,6 +1108,8 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
           const uint64_t sw = Ss[i];
           row = (uint32_t)(sw >> 32);
           if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sw);
+        } else if (a.rowof) {  // valued: the position now, its row and value by k_lb_gather
+          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
         } else {
           row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
         }
@@ -1066,6 +1169,17 @@ __global__ __launch_bounds__(kLbNT) void k_lb_out(LbArgs a) {
   }
 }
 
+// valued data (lb_gather=1): each occurrence's position (left in occ_row by the bucket kernel)
+// replaced by its row, and its value gathered — one thread per occurrence, so the random reads
+// of rowof / value are all in flight at once (inside the bucket kernel's slot loop each waited)
+__global__ __launch_bounds__(kLbNT) void k_lb_gather(LbArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kLbNT + threadIdx.x;
+  if (i >= a.nnz) return;
+  const uint32_t ps = a.occ_row[i];
+  a.occ_row[i] = a.rowof[ps];
+  if (a.occ_x) a.occ_x[i] = a.value[ps];
+}
+
 int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                     const uint64_t* index, uint64_t max_index, const LocOut& o, bool* used) {
   *used = false;
@@ -1108,6 +1222,10 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.kbuf = ws.keys0.as<uint64_t>();
   a.kscr = ws.keys1.as<uint64_t>();
   a.sbuf = ws.vals0.as<uint64_t>();
+  // valued data: each position's row written in input order, the row and value gathered by
+  // position at the outputs (lb_gather=1), or {value, row} carried beside each item (0)
+  const bool gather = valued && c->lb_gather;
+  a.rowof = gather ? ws.vals0.as<uint32_t>() : nullptr;
   a.sscr = ws.vals1.as<uint64_t>();
   a.qbuf = ws.lbq.as<uint32_t>();
   a.qscr = a.qbuf + nnz;
@@ -1116,6 +1234,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
   a.diag = c->lb_diag;
+  a.keyfirst = c->lb_keyfirst;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
   hipLaunchKernelGGL(k_lb_hist, dim3((unsigned)ntiles), dim3(kLbHNT), nbk * sizeof(uint32_t),
                      L.stream, a);
@@ -1132,26 +1251,30 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   // do not pack while the launch expected packed ones sorts through global memory: correct)
   const bool q_lds = hint[2] == 2u;
   const dim3 bg(nbk), bb(kLbNT);
-  if (valued)
+  const bool carry = valued && !gather;  // side payloads through the sort
+  if (carry)
     hipLaunchKernelGGL(k_lb_big<true>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   else
     hipLaunchKernelGGL(k_lb_big<false>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   if (c->lb_wave) {  // one wave per bucket
     const dim3 wb(kWave);
-    if (valued) {
+    if (carry) {
       if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, true>), bg, wb, 0, L.stream, a);
       else hipLaunchKernelGGL((k_lb_wbucket<false, true>), bg, wb, 0, L.stream, a);
     } else {
       if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, false>), bg, wb, 0, L.stream, a);
       else hipLaunchKernelGGL((k_lb_wbucket<false, false>), bg, wb, 0, L.stream, a);
     }
-  } else if (valued) {
+  } else if (carry) {
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, true>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, true>), bg, bb, 0, L.stream, a);
   } else {
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, false>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, false>), bg, bb, 0, L.stream, a);
   }
+  if (gather && nnz > 0)
+    hipLaunchKernelGGL(k_lb_gather, dim3((unsigned)((nnz + kLbNT - 1) / kLbNT)), bb, 0, L.stream,
+                       a);
   hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);
   hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
   DFX_HIP(hipGetLastError());
@@ -1517,8 +1640,9 @@ __global__ __launch_bounds__(kWave) void k_ab_wbucket(AbArgs a) {
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
   const bool fast = n <= kLbCap;  // else sorted in place by k_ab_big
   const uint64_t* gk = a.kbuf + start;
-  if (fast) lb_wave_sort<false, false>(gk, nullptr, nullptr, n, false, 0, 0, sk, nullptr, nullptr,
-                                       cnt);
+  if (fast)
+    lb_wave_sort<false, false>(gk, nullptr, nullptr, n, false, 0, 0, 32, true, sk, nullptr,
+                               nullptr, cnt);
   // within the bucket: every negative adds the positives ranked below it here (exact integers
   // in double); the positives of the buckets before it are added by the last wave
   double area = 0;

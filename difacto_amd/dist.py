@@ -1032,6 +1032,10 @@ class SplitStore:
     SplitStore([shard], rccl=(rank, nranks, ids, force_exchange)), one shard per process,
     ids = SplitStore.rccl_ids() made on rank 0 and handed to every rank by the caller.
 
+    stale=True (pipelined): the 1-step-stale schedule — step t+1's owner forward runs before
+    step t's backward, so each step's partial exchange and row gather travel beside the other
+    step's compute (oracle: dist_oracle.SplitStaleOracle; push_agg=sum).
+
     Batches must stay alive until the second submit after the one that took them (the store
     keeps them), a pipelined step's predictions / progress are complete after the next submit
     (or flush())."""
@@ -1039,23 +1043,24 @@ class SplitStore:
     MARKS = 7  # main-stream boundaries (dfx_split_store_set_marks)
     PHASES = ("owner_forward", "xchg_parts", "combine", "xchg_pxv", "owner_backward", "initv")
 
-    def __init__(self, shards, pipelined=True, max_index=MAX_INDEX, rccl=None):
+    def __init__(self, shards, pipelined=True, max_index=MAX_INDEX, rccl=None, stale=False):
         D = _lib.dist_lib()
         self.n = len(shards)
+        mode = 2 if stale else int(bool(pipelined))
         self.shards = shards
         h = ctypes.c_void_p()
         if rccl is None:
             arr = (ctypes.c_void_p * self.n)(*[sh.ctx.h for sh in shards])
-            _lib.dist_check(D.dfx_split_store_create_loopback(arr, self.n, int(bool(pipelined)),
-                                                              max_index, ctypes.byref(h)))
+            _lib.dist_check(D.dfx_split_store_create_loopback(arr, self.n, mode, max_index,
+                                                              ctypes.byref(h)))
         else:
             if self.n != 1:
                 raise ValueError("SplitStore over RCCL holds one shard per process")
             rank, nranks, ids, force = rccl
             buf = ctypes.create_string_buffer(bytes(ids), len(ids))
             _lib.dist_check(D.dfx_split_store_create_rccl(
-                shards[0].ctx.h, int(rank), int(nranks), buf, int(bool(force)),
-                int(bool(pipelined)), max_index, ctypes.byref(h)))
+                shards[0].ctx.h, int(rank), int(nranks), buf, int(bool(force)), mode, max_index,
+                ctypes.byref(h)))
         self.h = h
         self._live = []
 

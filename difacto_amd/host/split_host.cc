@@ -364,6 +364,7 @@ struct GpuSplitStore::Impl {
 
   SplitTransport* t;
   bool pipelined;
+  bool stale;  // pipelined == 2: the backward of a step after the next step's forward
   uint64_t max_index;
   int N, L, d, PS, PX;
   int next_slot = 0;
@@ -384,7 +385,15 @@ struct GpuSplitStore::Impl {
   std::vector<hipStream_t> xst, yst;
   std::vector<std::vector<hipEvent_t>> evf, evx, evc, evy;
 
-  Impl(SplitTransport* tr, bool pipe, uint64_t mi) : t(tr), pipelined(pipe), max_index(mi) {
+  // stale schedule: per slot and local shard, the partition buffers free again (after the
+  // step's combine), and the step's partials in / combine done / rows in; the step whose
+  // backward waits for the next Run
+  std::vector<hipEvent_t> part_free[2], sfwd[2], sx[2], sc[2], sy[2];
+  bool have_bwd = false;
+  Step bwd_step;
+
+  Impl(SplitTransport* tr, int pipe, uint64_t mi)
+      : t(tr), pipelined(pipe != 0), stale(pipe == 2), max_index(mi) {
     N = t->nranks();
     L = t->nlocal();
     d = dfx_ctx_vdim(t->ctx(0));
@@ -402,6 +411,11 @@ struct GpuSplitStore::Impl {
         // a slot nobody used yet is free
         HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
       }
+      for (auto* v : {&part_free[s], &sfwd[s], &sx[s], &sc[s], &sy[s]}) {
+        v->resize(L);
+        for (auto& e : *v) HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      }
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(part_free[s][l], Main(l)), "record");
     }
     icnt.resize(L);
     iall.resize(L);
@@ -430,6 +444,9 @@ struct GpuSplitStore::Impl {
       for (auto e : v) (void)hipEventDestroy(e);
     for (auto& s : slot_done)
       for (auto e : s) (void)hipEventDestroy(e);
+    for (int s = 0; s < 2; ++s)
+      for (auto* v : {&part_free[s], &sfwd[s], &sx[s], &sc[s], &sy[s]})
+        for (auto e : *v) (void)hipEventDestroy(e);
     for (auto& m : marks)
       for (auto e : m.ev)
         if (e) (void)hipEventDestroy(e);
@@ -454,7 +471,10 @@ struct GpuSplitStore::Impl {
     for (int l = 0; l < L; ++l) {
       Buf& u = buf[s][l];
       const dfx_batch& x = b[l];
-      HipCheck(hipStreamWaitEvent(Stream(l, 2), slot_done[s][l], 0), "wait");
+      // (stale: the partition buffers are free after the slot's last combine; the slot's
+      // owner state stays in use until its deferred backward)
+      HipCheck(hipStreamWaitEvent(Stream(l, 2), stale ? part_free[s][l] : slot_done[s][l], 0),
+               "wait");
       void* keys = u.keys.ensure((size_t)x.nnz * 8);
       void* xv = x.value ? u.x.ensure((size_t)x.nnz * 4) : nullptr;
       void* rc = u.rc.ensure((size_t)N * x.size * 4);
@@ -737,19 +757,99 @@ struct GpuSplitStore::Impl {
     }
   }
 
+  // the deferred backward of a stale-schedule step: its rows gathered (sy), the backward +
+  // update and InitV on the context streams, then its slot free for the step after next
+  void BackwardOf(const Step& q, bool mark) {
+    const int s = q.slot;
+    for (int l = 0; l < L; ++l) {
+      Buf& u = buf[s][l];
+      HipCheck(hipStreamWaitEvent(Main(l), sy[s][l], 0), "wait");
+      const void* rows = t->solo() ? u.pxv.p : u.allp.p;
+      DfxOk(dfx_split_owner_backward(t->ctx(l), s, static_cast<const float*>(rows)),
+            "dfx_split_owner_backward");
+    }
+    if (mark) Mark(5);
+    InitV(s);
+    for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
+  }
+
+  // the stale schedule's main-stream work for step q: q's owner forward, its partials on the
+  // exchange streams beside the PREVIOUS step's backward (which reads the model after q's
+  // forward did: q is one step stale), q's combine, q's rows to the owners on the gather
+  // streams beside the next step's forward; q's own backward waits for the next Run (or Flush)
+  void RunStale(const Step& q) {
+    const int s = q.slot;
+    const int64_t M = q.M;
+    const bool train = q.job == DFX_JOB_TRAINING;
+    SliceRes(1);
+    std::vector<const void*> ps(L), xs(L);
+    std::vector<void*> pr(L), xr(L), xst_(L), yst_(L);
+    for (int l = 0; l < L; ++l) {
+      Buf& u = buf[s][l];
+      float* parts = static_cast<float*>(u.parts.ensure((size_t)N * M * PS * 4));
+      DfxOk(dfx_split_owner_forward(t->ctx(l), s, parts), "dfx_split_owner_forward");
+      ps[l] = parts;
+      pr[l] = t->solo() ? parts : u.rparts.ensure((size_t)N * M * PS * 4);
+      HipCheck(hipEventRecord(sfwd[s][l], Main(l)), "record");
+      HipCheck(hipStreamWaitEvent(xst[l], sfwd[s][l], 0), "wait");
+      xst_[l] = xst[l];
+      yst_[l] = yst[l];
+    }
+    // marks in main-stream order: the forward (0 -> 1), the previous step's backward (4 -> 5),
+    // its InitV with this step's combine (5 -> 6); the exchanges run beside them (no mark)
+    Mark(1);
+    Mark(2);
+    Mark(3);
+    Mark(4);
+    const std::vector<std::vector<int64_t>> pb(L, std::vector<int64_t>(N, M * PS * 4));
+    // (communicators 3 / 4: the exchange / gather streams' own, as the sliced step's)
+    if (!t->solo()) t->AllToAllV(3, ps, pb, pr, pb, xst_);
+    for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(sx[s][l], xst[l]), "record");
+    if (have_bwd) {  // the previous step's backward, beside q's partial exchange
+      have_bwd = false;
+      BackwardOf(bwd_step, true);
+    } else {
+      Mark(5);
+    }
+    for (int l = 0; l < L; ++l) {
+      Buf& u = buf[s][l];
+      HipCheck(hipStreamWaitEvent(Main(l), sx[s][l], 0), "wait");
+      float* pxv = static_cast<float*>(u.pxv.ensure((size_t)M * PX * 4));
+      DfxOk(dfx_split_combine(t->ctx(l), s, &q.batches[l], static_cast<const float*>(pr[l]), M,
+                              N, pxv, q.preds.empty() ? nullptr : q.preds[l]),
+            "dfx_split_combine");
+      HipCheck(hipEventRecord(part_free[s][l], Main(l)), "record");
+      xs[l] = pxv;
+      xr[l] = t->solo() ? pxv : u.allp.ensure((size_t)N * M * PX * 4);
+      HipCheck(hipEventRecord(sc[s][l], Main(l)), "record");
+      HipCheck(hipStreamWaitEvent(yst[l], sc[s][l], 0), "wait");
+    }
+    if (train) {
+      if (!t->solo()) t->AllGather(4, xs, xr, (size_t)M * PX * 4, yst_);
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(sy[s][l], yst[l]), "record");
+      bwd_step = q;
+      have_bwd = true;
+    } else {
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
+    }
+  }
+
   // the step's main-stream work (sliced with an exchange), then the run-ahead bound
   void Run(const Step& q) {
     const int s = q.slot;
     if (mark_mask) marks.emplace_back();
     Mark(0);
     const int K = Slices();
-    if (K > 1) {
+    if (stale) {
+      RunStale(q);
+    } else if (K > 1) {
       RunSliced(q, K);
     } else {
       RunWhole(q);
     }
     Mark(6);
-    for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
+    if (!stale)
+      for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
     if (!pipelined) return;
     std::vector<hipEvent_t> done;
     if (!spare.empty()) {
@@ -795,6 +895,10 @@ struct GpuSplitStore::Impl {
       have_pending = false;
       Run(pending);
     }
+    if (have_bwd) {  // the stale schedule's last backward
+      have_bwd = false;
+      BackwardOf(bwd_step, false);
+    }
   }
 
   // the queued step run and every stream the driver uses drained: the outgrown buffers are
@@ -808,7 +912,7 @@ struct GpuSplitStore::Impl {
   }
 };
 
-GpuSplitStore::GpuSplitStore(SplitTransport* t, bool pipelined, uint64_t max_index)
+GpuSplitStore::GpuSplitStore(SplitTransport* t, int pipelined, uint64_t max_index)
     : impl_(new Impl(t, pipelined, max_index)) {}
 
 GpuSplitStore::~GpuSplitStore() {
@@ -916,7 +1020,7 @@ int dfx_split_store_create_rccl(dfx_ctx* ctx, int rank, int nranks, const void* 
     if (!ctx || !ids || !out) throw difacto::Error(DFX_ERR_ARG, "null argument");
     std::unique_ptr<dfx_split_store> h(new dfx_split_store);
     h->t = difacto::MakeSplitRccl(ctx, rank, nranks, ids, force_exchange != 0);
-    h->s.reset(new difacto::GpuSplitStore(h->t.get(), pipelined != 0, max_index));
+    h->s.reset(new difacto::GpuSplitStore(h->t.get(), pipelined, max_index));
     *out = h.release();
   });
 }
@@ -930,7 +1034,7 @@ int dfx_split_store_create_loopback(dfx_ctx* const* ctxs, int n, int pipelined,
       if (!c) throw difacto::Error(DFX_ERR_ARG, "null ctx");
     std::unique_ptr<dfx_split_store> h(new dfx_split_store);
     h->t = difacto::MakeSplitLoopback(v);
-    h->s.reset(new difacto::GpuSplitStore(h->t.get(), pipelined != 0, max_index));
+    h->s.reset(new difacto::GpuSplitStore(h->t.get(), pipelined, max_index));
     *out = h.release();
   });
 }

@@ -95,8 +95,11 @@ std::unique_ptr<SplitTransport> MakeSplitRccl(dfx_ctx* ctx, int rank, int nranks
  * its key range (the contexts need push_agg=sum). */
 class GpuSplitStore {
  public:
-  /** pipelined: step t+1's partition / key exchange / owner Localizer beside step t */
-  GpuSplitStore(SplitTransport* t, bool pipelined, uint64_t max_index);
+  /** pipelined 1: step t+1's partition / key exchange / owner Localizer beside step t (same
+   * results as 0); 2 (stale): also step t+1's owner forward before step t's backward, so each
+   * step's partial exchange and row gather travel beside the other step's compute — the
+   * 1-step-stale schedule of oracle/dist_oracle.py SplitStaleOracle */
+  GpuSplitStore(SplitTransport* t, int pipelined, uint64_t max_index);
   ~GpuSplitStore();
   /** one batch per local shard (device arrays, produced on the contexts' input streams);
    * preds: optional, per shard, device floats for the batch's predictions.  Pipelined: runs

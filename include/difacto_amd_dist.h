@@ -37,8 +37,12 @@ int dfx_dist_rccl_comms(void);
 /* n fresh communicator ids into out[n * dfx_dist_rccl_id_bytes()] (rank 0 only) */
 int dfx_dist_rccl_ids(int n, void* out);
 /* one shard per process: this context (its stream, lanes and store) is rank `rank` of
- * `nranks`.  force_exchange: exchange through RCCL even at one rank.  pipelined: step t+1's
- * partition, key exchange and owner Localizer run beside step t (same results). */
+ * `nranks`.  force_exchange: exchange through RCCL even at one rank.  pipelined 1: step t+1's
+ * partition, key exchange and owner Localizer run beside step t (same results as 0);
+ * 2: the 1-step-stale schedule — also step t+1's owner forward before step t's backward, each
+ * step's partial exchange and row gather beside the other step's compute (no reference
+ * counterpart: one of the schedules KVStoreDist's asynchronous pushes allow, kvstore_dist.h:
+ * 137-150) */
 int dfx_split_store_create_rccl(dfx_ctx* ctx, int rank, int nranks, const void* ids,
                                 int force_exchange, int pipelined, uint64_t max_index,
                                 dfx_split_store** out);

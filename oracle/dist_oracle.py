@@ -255,3 +255,69 @@ class StaleOracle:
     def entry(self, key):
         return self.so.entry(key)
 
+
+
+class SplitStaleOracle:
+    """The split store's 1-step-stale schedule (GpuSplitStore pipelined = 2, dist.SplitStore
+    stale=True) on push_agg=sum: on every GPU the owner forward of step t+1
+    runs before the backward of step t, so step t's exchanges travel beside the other step's
+    compute.  Per step:
+        begin(t+1)            count push, as AggOracle (before step t's update)
+        forward(t+1)          predictions from the model after update t-1 (one step stale)
+        update(t)             step t's gradient: p and XV_ from its (stale) forward, the
+                              gradient's layout and the diag(XXp) V term from the model as it
+                              is now (the owner's backward reads V when it runs), summed over
+                              the workers per key and applied once (oracle.fm_calcgrad_stale)
+    flush() applies the last pending update.  Deterministic; one of the schedules the
+    reference's asynchronous KVStoreDist allows with two batches in flight per worker
+    (sgd_learner.cc:310-312, kvstore_dist.h:137-150), with the server's current V in the
+    gradient's V term instead of the worker's pulled copy."""
+
+    def __init__(self, nranks, **kw):
+        self.so = AggOracle(nranks, **kw)
+        self.N, self.one, self.d = self.so.N, self.so.one, self.so.d
+        self.up = self.so.up
+        self.pending = None
+
+    def submit(self, blocks, push_cnt=False, train=True, max_index=(1 << 64) - 1):
+        st = self.so.begin(blocks, push_cnt, max_index)
+        self.so.pull(st)
+        out = []
+        for r in range(self.N):
+            blk = st["blocks"][r]
+            uniq, _, col, _ = st["loc"][r]
+            vals, lens = st["pulled"][r]
+            wp, vp = O.get_pos(lens) if self.d > 0 else (None, None)
+            pred = O.fm_predict(blk.offs, col, blk.vals, vals, wp, vp, self.d)
+            out.append((O.evaluate(blk.labels, pred), O.auc(blk.labels, pred), pred))
+        st["preds"] = [o[2] for o in out]
+        self.flush()
+        if train:
+            self.pending = st
+        return out
+
+    def flush(self):
+        st, self.pending = self.pending, None
+        if st is None:
+            return
+        d = self.d
+        grads, now = [], []
+        for r in range(self.N):
+            blk = st["blocks"][r]
+            uniq, _, col, _ = st["loc"][r]
+            fv, fl = st["pulled"][r]
+            bv, bl = self.one.get(uniq)  # the model as the backward reads it
+            if d > 0:
+                _, fvp = O.get_pos(fl)
+                bwp, bvp = O.get_pos(bl)
+            else:
+                fvp = bwp = bvp = None
+            grads.append(O.fm_calcgrad_stale(blk.offs, col, blk.vals, blk.labels, blk.weights,
+                                             fv, fvp, bv, bwp, bvp, len(uniq), d,
+                                             st["preds"][r]))
+            now.append((bv, bl if d > 0 else None))
+        st["pulled"], st["grads"] = now, grads
+        self.so.push(st)
+
+    def entry(self, key):
+        return self.so.entry(key)

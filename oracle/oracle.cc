@@ -328,7 +328,86 @@ static void CalcGrad(int64_t B, const uint64_t* offs, const uint32_t* col, const
   }
 }
 
+// CalcGrad of a 1-step-stale split step (test infrastructure; DESIGN.md (e), split stale): the
+// forward ran on an older model (fw_weights / fw_V_pos: what it read, so p and XV_ are the stale
+// forward's), the backward reads the model as it is when the update runs (bw_weights / bw_w_pos /
+// bw_V_pos: the gradient's layout and the V of the diag(XXp) V term).  With fw == bw this is
+// CalcGrad<float> term for term.
+static void CalcGradStale(int64_t B, const uint64_t* offs, const uint32_t* col, const float* val,
+                          const float* label, const float* rweight, const float* fw_weights,
+                          const int32_t* fw_V_pos, const float* bw_weights,
+                          const int32_t* bw_w_pos, const int32_t* bw_V_pos, int64_t ncol,
+                          int V_dim, const float* pred, float* grad) {
+  std::vector<real_t> p(B);
+  for (int64_t i = 0; i < B; ++i) {
+    real_t y = label[i] > 0 ? 1 : -1;
+    if (rweight) p[i] = -y / (1 + std::exp(y * pred[i])) * rweight[i];
+    else p[i] = -y / (1 + std::exp(y * pred[i]));
+  }
+  for (int64_t r = 0; r < B; ++r) {
+    real_t pr = p[r];
+    if (pr == 0) continue;
+    for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
+      uint32_t c = col[j];
+      if ((int64_t)c >= ncol) continue;
+      float* g;
+      if (bw_w_pos) { int q = bw_w_pos[c]; if (q == -1) continue; g = grad + q; } else { g = grad + c; }
+      if (val) *g += pr * val[j]; else *g += pr;
+    }
+  }
+  if (V_dim == 0) return;
+  std::vector<float> XXp(ncol, 0.f);
+  for (int64_t r = 0; r < B; ++r) {
+    real_t pr = p[r];
+    if (pr == 0) continue;
+    for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
+      uint32_t c = col[j];
+      if ((int64_t)c >= ncol) continue;
+      if (val) { real_t xx = val[j] * val[j]; XXp[c] += pr * xx; } else { XXp[c] += pr; }
+    }
+  }
+  for (int64_t c = 0; c < ncol; ++c) {
+    int q = bw_V_pos[c];
+    if (q == -1) continue;
+    for (int l = 0; l < V_dim; ++l) grad[q + l] -= bw_weights[q + l] * XXp[c];
+  }
+  std::vector<real_t> XVp((size_t)B * V_dim, 0.f);
+  for (int64_t r = 0; r < B; ++r) {
+    real_t* t = XVp.data() + (size_t)r * V_dim;
+    for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
+      int q = fw_V_pos[col[j]];
+      if (q == -1) continue;
+      const float* V = fw_weights + q;
+      if (val) { real_t x = val[j]; for (int l = 0; l < V_dim; ++l) t[l] += V[l] * x; }
+      else { for (int l = 0; l < V_dim; ++l) t[l] += V[l]; }
+    }
+    for (int l = 0; l < V_dim; ++l) t[l] *= p[r];
+  }
+  for (int64_t r = 0; r < B; ++r) {
+    const real_t* t = XVp.data() + (size_t)r * V_dim;
+    for (uint64_t j = offs[r]; j < offs[r + 1]; ++j) {
+      uint32_t c = col[j];
+      if ((int64_t)c >= ncol) continue;
+      int q = bw_V_pos[c];
+      if (q == -1) continue;
+      float* g = grad + q;
+      if (val) { real_t x = val[j]; for (int l = 0; l < V_dim; ++l) g[l] += t[l] * x; }
+      else { for (int l = 0; l < V_dim; ++l) g[l] += t[l]; }
+    }
+  }
+}
+
 extern "C" {
+
+void orc_fm_calcgrad_stale(int64_t B, const uint64_t* offs, const uint32_t* col,
+                           const float* val, const float* label, const float* rweight,
+                           const float* fw_weights, const int32_t* fw_V_pos,
+                           const float* bw_weights, const int32_t* bw_w_pos,
+                           const int32_t* bw_V_pos, int64_t ncol, int V_dim, const float* pred,
+                           float* grad) {
+  CalcGradStale(B, offs, col, val, label, rweight, fw_weights, fw_V_pos, bw_weights, bw_w_pos,
+                bw_V_pos, ncol, V_dim, pred, grad);
+}
 
 void orc_fm_calcgrad(int64_t B, const uint64_t* offs, const uint32_t* col, const float* val,
                      const float* label, const float* rweight, const float* weights,

@@ -41,6 +41,10 @@ def lib():
         L.orc_fm_calcgrad.restype = None
         L.orc_fm_calcgrad.argtypes = [ctypes.c_int64, u64p, u32p, f32p, f32p, f32p, f32p, i32p,
                                       i32p, ctypes.c_int64, ctypes.c_int, f32p, f32p]
+        L.orc_fm_calcgrad_stale.restype = None
+        L.orc_fm_calcgrad_stale.argtypes = [ctypes.c_int64, u64p, u32p, f32p, f32p, f32p, f32p,
+                                            i32p, f32p, i32p, i32p, ctypes.c_int64, ctypes.c_int,
+                                            f32p, f32p]
         L.orc_evaluate.restype = ctypes.c_double
         L.orc_evaluate.argtypes = [ctypes.c_int64, f32p, f32p]
         L.orc_auc.restype = ctypes.c_float
@@ -142,6 +146,32 @@ def fm_calcgrad(offs, col, val, label, rweight, weights, w_pos, V_pos, ncol, V_d
     lib().orc_fm_calcgrad(B, _p(offs, u64p), _p(col, u32p), _p(val, f32p), _p(label, f32p),
                           _p(rweight, f32p), _p(weights, f32p), _p(w_pos, i32p), _p(V_pos, i32p),
                           int(ncol), int(V_dim), _p(pred, f32p), _p(out, f32p))
+    return out
+
+
+def fm_calcgrad_stale(offs, col, val, label, rweight, fw_weights, fw_V_pos, bw_weights, bw_w_pos,
+                      bw_V_pos, ncol, V_dim, pred):
+    """CalcGrad of a 1-step-stale split step (oracle.cc CalcGradStale): p and XV_ from the
+    forward's (older) model, the gradient's layout and diag(XXp) V from the model the update
+    reads.  Returns the gradient in the bw layout."""
+    offs = _c(offs, np.uint64)
+    col = _c(col, np.uint32)
+    val = _c(val, np.float32)
+    label = _c(label, np.float32)
+    rweight = _c(rweight, np.float32)
+    fw_weights = _c(fw_weights, np.float32)
+    fw_V_pos = _c(fw_V_pos, np.int32)
+    bw_weights = _c(bw_weights, np.float32)
+    bw_w_pos = _c(bw_w_pos, np.int32)
+    bw_V_pos = _c(bw_V_pos, np.int32)
+    pred = _c(pred, np.float32)
+    B = len(offs) - 1
+    out = np.zeros(len(bw_weights), np.float32)
+    lib().orc_fm_calcgrad_stale(B, _p(offs, u64p), _p(col, u32p), _p(val, f32p),
+                                _p(label, f32p), _p(rweight, f32p), _p(fw_weights, f32p),
+                                _p(fw_V_pos, i32p), _p(bw_weights, f32p), _p(bw_w_pos, i32p),
+                                _p(bw_V_pos, i32p), int(ncol), int(V_dim), _p(pred, f32p),
+                                _p(out, f32p))
     return out
 
 

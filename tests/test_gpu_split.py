@@ -289,6 +289,57 @@ def test_split_store_cpp_equals_python_schedule(name, N, pipelined):
         c.close()
 
 
+@pytest.mark.parametrize("N", [1, 3])
+@pytest.mark.parametrize("name", ["fm_v16", "fm_v5_odd", "fm_v8", "logit"])
+def test_split_store_stale_matches_oracle(name, N):
+    """the 1-step-stale schedule of the C++ driver (SplitStore(stale=True): step t+1's owner
+    forward before step t's backward, the exchanges beside the other step's compute) against
+    oracle/dist_oracle.SplitStaleOracle: predictions one step stale, each update's gradient from
+    its stale forward with the V term read at update time; count-push, training and validation
+    steps, mixed binary / valued workers, an empty worker.  Bars as the synchronous split's:
+    predictions, loss and model values within 1e-5; keys, rand_r state and new_w exact."""
+    from difacto_amd import dist as DI
+    from difacto_amd import hotpath as H
+    kw = CFGS[name]
+    jobs = [(H.kTraining, True), (H.kTraining, True), (H.kTraining, False),
+            (H.kValidation, False), (H.kTraining, False), (H.kTraining, False),
+            (H.kTraining, False)]
+    ctxs = [H.Context(0, max_keys=1 << 16, push_agg="sum", **kw) for _ in range(N)]
+    shards = [DI.Shard(c, N) for c in ctxs]
+    store = DI.SplitStore(shards, stale=True)
+    so = DO.SplitStaleOracle(N, **kw)
+    got, want, seen, live = [], [], [], []
+    for s, (job, cnt) in enumerate(jobs):
+        step = [D.synthetic(0 if (s == 5 and r == 1) else 300, 12, 5000,
+                            binary=(r % 2 == 0), seed=500 + 31 * s + r, ragged=(s == 4))
+                for r in range(N)]
+        dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
+        preds = [torch.zeros(300, dtype=torch.float32, device=ctxs[r].device) for r in range(N)]
+        store.submit(dbs, job, push_cnt=cnt, preds=preds)
+        live.append(dbs)
+        got.append(preds)
+        want.append(so.submit(step, push_cnt=cnt, train=job == H.kTraining))
+        seen.append(D.concat(step))
+    store.flush()
+    so.flush()
+    for c in ctxs:
+        c.sync()
+    loss = [0.0] * N
+    for s in range(len(jobs)):
+        for r in range(N):
+            B = len(want[s][r][2])
+            assert close(got[s][r][:B].cpu().numpy(), want[s][r][2]), (name, N, s, r)
+            loss[r] += want[s][r][0]
+    for r in range(N):
+        assert H.progress(ctxs[r])["loss"] == pytest.approx(loss[r], rel=1e-5)
+    n_v = _check_model(ctxs, so.one, seen, N)
+    if kw.get("V_dim", 0) > 0:
+        assert n_v > 0
+    store.close()
+    for c in ctxs:
+        c.close()
+
+
 @pytest.mark.parametrize("pipelined", [False, True])
 def test_split_store_marks(pipelined):
     """the C++ driver's phase events: every marked step times every main-stream phase"""

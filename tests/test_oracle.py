@@ -79,6 +79,26 @@ def test_fmloss_hasv(rcv1, known):
     assert abs(float((g.astype(np.float64) ** 2).sum()) - k["grad_norm2"]) < k["grad_tol"]
 
 
+def test_stale_calcgrad_equals_calcgrad_on_one_model(rcv1, known):
+    """oracle.cc CalcGradStale (the split store's stale schedule) with the forward's and the
+    backward's model the same is CalcGrad term for term; with a different backward model only
+    the diag(XXp) V term moves"""
+    d = known["fmloss_hasv"]["V_dim"]
+    uniq, _, col = O.localize(rcv1.offs, rcv1.ids)
+    W, wp, vp = _fm_weights(_rev(uniq), d)
+    pred = O.fm_predict(rcv1.offs, col, rcv1.vals, W, wp, vp, d)
+    g = O.fm_calcgrad(rcv1.offs, col, rcv1.vals, rcv1.labels, None, W, wp, vp, len(uniq), d, pred)
+    gs = O.fm_calcgrad_stale(rcv1.offs, col, rcv1.vals, rcv1.labels, None, W, vp, W, wp, vp,
+                             len(uniq), d, pred)
+    assert np.array_equal(g.view(np.uint32), gs.view(np.uint32))
+    W2 = W.copy()
+    W2[vp[vp >= 0][:, None] + np.arange(d)] *= 2  # every V doubled, w unchanged
+    g2 = O.fm_calcgrad_stale(rcv1.offs, col, rcv1.vals, rcv1.labels, None, W, vp, W2, wp, vp,
+                             len(uniq), d, pred)
+    assert np.array_equal(g2[wp], g[wp])
+    assert not np.array_equal(g2, g)
+
+
 def test_sgd_learner_basic(rcv1, known):
     k = known["sgd_learner_basic"]
     kw = k["kwargs"]

@@ -5,7 +5,7 @@
 // times.  With a sixth argument "auc": the AUC lane's sort + area of a B-row (pred, label)
 // snapshot instead (auc_sort from the kwargs).  Measurement tool (links the library's
 // internals), not a test.
-//   build/locbench [B] [k] [kbits] [iters] [context kwargs] [auc]
+//   build/locbench [B] [k] [kbits] [iters] [context kwargs] [auc | valued]
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -86,13 +86,20 @@ int main(int argc, char** argv) {
     dfx_ctx_destroy(ctx);
     return rc;
   }
+  const bool valued = argc > 6 && std::string(argv[6]) == "valued";
   uint64_t *offs, *ids, *uniq;
   uint32_t *seg, *occ;
+  float *val = nullptr, *occx = nullptr;
   hipMalloc(&offs, (B + 1) * 8);
   hipMalloc(&ids, nnz * 8);
   hipMalloc(&uniq, nnz * 8);
   hipMalloc(&seg, (nnz + 1) * 4);
   hipMalloc(&occ, nnz * 4);
+  if (valued) {  // values 1.0 (their bits travel as well as any)
+    hipMalloc(&val, nnz * 4);
+    hipMalloc(&occx, nnz * 4);
+    hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(val), 0x3f800000u, nnz);
+  }
   hipLaunchKernelGGL(k_gen, dim3((unsigned)((nnz + 256) / 256)), dim3(256), 0, c->stream, B, k,
                      kbits, offs, ids, 42ull);
   dfx::Lane L = dfx::main_lane(c);
@@ -100,6 +107,8 @@ int main(int argc, char** argv) {
   o.uniq = uniq;
   o.segstart = seg;
   o.occ_row = occ;
+  o.value = val;
+  o.occ_x = occx;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -120,8 +129,8 @@ int main(int argc, char** argv) {
   hipMemcpy(&u, &c->ds->u_count, 4, hipMemcpyDeviceToHost);
   int err = 0;
   hipMemcpy(&err, &c->ds->err, 4, hipMemcpyDeviceToHost);
-  printf("locbench B=%lld k=%d kbits=%d kwargs='%s': %.4f ms per Localizer, U=%u, err=%d\n",
-         (long long)B, k, kbits, kw, tot / iters, u, err);
+  printf("locbench B=%lld k=%d kbits=%d kwargs='%s'%s: %.4f ms per Localizer, U=%u, err=%d\n",
+         (long long)B, k, kbits, kw, valued ? " valued" : "", tot / iters, u, err);
   dfx_ctx_destroy(ctx);
   return 0;
 }

@@ -6,6 +6,14 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${LB_B:-100000}
+if [ -n "$LB_C2" ]; then  # C2's shape: 40 valued nnz per row over 2^20 ids
+  for kw in "loc_bucket=0" "" "lb_gather=0" ${LB_VARIANTS:-}; do
+    timeout -k 10 60 ./build/locbench $B 40 20 20 "$kw" valued || exit $?
+  done
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_locbench_c2 -o trace \
+    --output-format csv -- ./build/locbench $B 40 20 20 "" valued > gpurun_out/prof_locbench_c2.log 2>&1
+  exit $?
+fi
 if [ -n "$LB_AUC" ]; then
   for kw in "auc_sort=bucket" "auc_sort=radix" "auc_sort=merge"; do
     timeout -k 10 60 ./build/locbench $B 39 24 20 "$kw" auc || exit $?
