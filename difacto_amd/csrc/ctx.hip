@@ -359,10 +359,17 @@ int pipeline_init(Context* c) {
   c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
-  for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_loc[0], &c->ev_loc[1],
-                        &c->ev_free[0], &c->ev_free[1], &c->ev_part[0], &c->ev_part[1]})
+  for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  for (DevState** d : {&c->bds[0], &c->bds[1], &c->ads, &c->ods[0], &c->ods[1]}) {
+  for (int s = 0; s < kSlots; ++s)
+    for (hipEvent_t* e : {&c->ev_loc[s], &c->ev_free[s], &c->ev_part[s]})
+      DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  std::vector<DevState**> states{&c->ads};
+  for (int s = 0; s < kSlots; ++s) {
+    states.push_back(&c->bds[s]);
+    states.push_back(&c->ods[s]);
+  }
+  for (DevState** d : states) {
     DFX_HIP(hipMalloc(d, sizeof(DevState)));
     DFX_HIP(hipMemsetAsync(*d, 0, sizeof(DevState), c->stream));
   }
@@ -479,19 +486,23 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   release_ws(c->ws);
-  release_ws(c->bws[0]);
-  release_ws(c->bws[1]);
+  for (int s = 0; s < kSlots; ++s) {
+    release_ws(c->bws[s]);
+    release_ws(c->ows[s]);
+  }
   release_ws(c->aws);
-  release_ws(c->ows[0]);
-  release_ws(c->ows[1]);
   release_ws(c->uws);
   for (auto h : c->dist_host)
     if (h) (void)hipHostFree(h);
-  for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_loc[0], c->ev_loc[1],
-                       c->ev_free[0], c->ev_free[1], c->ev_part[0], c->ev_part[1]})
+  for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc})
     if (e) (void)hipEventDestroy(e);
-  for (DevState* d : {c->bds[0], c->bds[1], c->ads, c->ods[0], c->ods[1]})
-    if (d) (void)hipFree(d);
+  for (int s = 0; s < kSlots; ++s) {
+    for (hipEvent_t e : {c->ev_loc[s], c->ev_free[s], c->ev_part[s]})
+      if (e) (void)hipEventDestroy(e);
+    for (DevState* d : {c->bds[s], c->ods[s]})
+      if (d) (void)hipFree(d);
+  }
+  if (c->ads) (void)hipFree(c->ads);
   if (c->loc_stream) (void)hipStreamSynchronize(c->loc_stream);
   if (c->own_loc_stream) (void)hipStreamDestroy(c->own_loc_stream);
   if (c->part_stream) (void)hipStreamSynchronize(c->part_stream);

@@ -83,6 +83,10 @@ struct DevState {
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
+// step slots of the sharded stores (dist.hip, split.hip): two steps in flight when pipelined,
+// three in the split's 1-step-stale schedule (a step's owner state lives until its backward,
+// after the next step's forward, while the step after that localizes)
+constexpr int kSlots = 3;
 constexpr int kOsSortTile = 4096;  // radix sort tile (sort.hip)
 constexpr int kOsDigits = 8;       // 8-bit digit positions of a u64 key
 constexpr int kOsParts = 16;       // partial digit-count copies (spread the atomics)
@@ -183,17 +187,17 @@ struct Context {
   // received by this owner and each source rank's offset among them (owner buffers ows /
   // state ods), rows and unique keys of this worker's batch (Localizer buffers bws / bds,
   // shared with the fused step), owner split counts + U of the batch in pinned memory
-  Workspace ows[2];
-  DevState* ods[2] = {nullptr, nullptr};
+  Workspace ows[kSlots];
+  DevState* ods[kSlots] = {};
   Workspace uws;  // the union of the workers' keys (dfx_dist_union)
-  int64_t dist_R[2] = {0, 0}, dist_rows[2] = {0, 0}, dist_U[2] = {-1, -1};
-  std::vector<int64_t> dist_offs[2];
+  int64_t dist_R[kSlots] = {}, dist_rows[kSlots] = {}, dist_U[kSlots] = {-1, -1, -1};
+  std::vector<int64_t> dist_offs[kSlots];
   // owner segments of a slot not yet built: owner_begin leaves them to the pull, which
   // builds them and answers the pull in one pass (k_dist_segs_pull)
-  bool dist_segs_pending[2] = {false, false};
-  const uint64_t* dist_K[2] = {nullptr, nullptr};  // the slot's owner keys, merged
-  const uint32_t* dist_P[2] = {nullptr, nullptr};  // their received indices (null: identity)
-  unsigned long long* dist_host[2] = {nullptr, nullptr};
+  bool dist_segs_pending[kSlots] = {};
+  const uint64_t* dist_K[kSlots] = {};  // the slot's owner keys, merged
+  const uint32_t* dist_P[kSlots] = {};  // their received indices (null: identity)
+  unsigned long long* dist_host[kSlots] = {};
   // fused-step pipelining (step.hip): batch t+1's Localizer runs on loc_stream while the main
   // stream runs batch t's forward/backward; the AUC runs on aux_stream beside the backward
   hipStream_t loc_stream = nullptr, aux_stream = nullptr;
@@ -202,12 +206,12 @@ struct Context {
   hipStream_t own_part_stream = nullptr;
   hipStream_t in_stream = nullptr;  // where batches are produced (dfx_ctx_set_input_stream)
   bool has_in_stream = false;
-  Workspace bws[2];
-  DevState* bds[2] = {nullptr, nullptr};
+  Workspace bws[kSlots];  // [0], [1]: also the fused step's Localizer parities
+  DevState* bds[kSlots] = {};
   Workspace aws;
   DevState* ads = nullptr;
   hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
-  hipEvent_t ev_loc[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+  hipEvent_t ev_loc[kSlots] = {}, ev_free[kSlots] = {};
   int parity = 0;
   // the fused forward finds every nnz's key in the table (no Localizer col scatter, no pulled
   // {w, vrow} per key); 0: col + pulled (kwarg fwd_probe=0)
@@ -256,29 +260,29 @@ struct Context {
 
   // a key-range server's slot holds table positions (segment slots) from its owner_begin to the
   // end of its step (the push, or its InitV draws): a table rebuild moves them with the keys
-  bool dist_live[2] = {false, false};
-  bool dist_pushed[2] = {false, false};  // the slot's gradient push ran (its InitV ends the step)
+  bool dist_live[kSlots] = {};
+  bool dist_pushed[kSlots] = {};  // the slot's gradient push ran (its InitV ends the step)
   // push_agg=sum (default): one Update per key per step on the workers' summed gradients, InitV
   // ranked over all owners (dfx_dist_initv_local / _draw); push_agg=ranks: one Update per
   // pushing worker in rank order, InitV per server (KVStoreDist's HandlePush)
   int dist_sum = 1;
-  bool dist_initv_pending[2] = {false, false};
+  bool dist_initv_pending[kSlots] = {};
   // owner-computes split (split.hip), per step slot.  Worker: the batch's rows and its
   // partition's owner-major block offsets.  Owner: the received sub-rows (all workers'
   // concatenated) and their keys / values, localized into ows[slot]; split_resolved: a count
   // push found-or-inserted the slot's keys (the backward then inserts none)
-  int64_t split_B[2] = {0, 0}, split_nblk[2] = {0, 0};
-  int64_t split_rows[2] = {0, 0}, split_nnz[2] = {0, 0};
-  const uint64_t* split_keys[2] = {nullptr, nullptr};
-  const float* split_x[2] = {nullptr, nullptr};
-  bool split_resolved[2] = {false, false};
-  bool split_initv_pending[2] = {false, false};
-  bool split_initv_gated[2] = {false, false};  // the requests came from the backward (n_init)
+  int64_t split_B[kSlots] = {}, split_nblk[kSlots] = {};
+  int64_t split_rows[kSlots] = {}, split_nnz[kSlots] = {};
+  const uint64_t* split_keys[kSlots] = {};
+  const float* split_x[kSlots] = {};
+  bool split_resolved[kSlots] = {};
+  bool split_initv_pending[kSlots] = {};
+  bool split_initv_gated[kSlots] = {};  // the requests came from the backward (n_init)
   // the slot's owner_begin ran on the Localizer lane (the forward waits for ev_loc[slot]);
   // ev_part[slot]: the slot's partition is done (host join)
-  bool split_lane[2] = {false, false};
-  int split_job[2] = {0, 0};  // the slot's job type (the step's last call records its counts)
-  hipEvent_t ev_part[2] = {nullptr, nullptr};
+  bool split_lane[kSlots] = {};
+  int split_job[kSlots] = {};  // the slot's job type (the step's last call records its counts)
+  hipEvent_t ev_part[kSlots] = {};
 };
 
 inline Lane main_lane(Context* c) { return Lane{c->stream, &c->ws, c->ds, &c->ds->err}; }

@@ -410,8 +410,9 @@ static int table_rebuild(Context* c, Table NT, int64_t new_cap) {
   int err0 = 0, err1 = 0;
   DFX_HIP(hipMemcpyAsync(&err0, &c->ds->err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   DFX_HIP(hipStreamSynchronize(c->stream));
-  const bool remap = (c->dist_live[0] && !c->dist_segs_pending[0] && c->dist_R[0] > 0) ||
-                     (c->dist_live[1] && !c->dist_segs_pending[1] && c->dist_R[1] > 0);
+  bool remap = false;
+  for (int s = 0; s < kSlots; ++s)
+    remap = remap || (c->dist_live[s] && !c->dist_segs_pending[s] && c->dist_R[s] > 0);
   uint32_t* map = nullptr;
   if (remap) DFX_HIP(hipMalloc(&map, (size_t)c->cap * sizeof(uint32_t)));
   hipLaunchKernelGGL(k_rehash, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, T,
@@ -427,7 +428,7 @@ static int table_rebuild(Context* c, Table NT, int64_t new_cap) {
     set_error("table rebuild: the new table cannot hold every key; the old table is kept");
     return DFX_ERR_CAPACITY;
   }
-  for (int s = 0; s < 2 && map; ++s) {
+  for (int s = 0; s < kSlots && map; ++s) {
     const int64_t R = c->dist_R[s];
     if (!c->dist_live[s] || c->dist_segs_pending[s] || R <= 0) continue;
     hipLaunchKernelGGL(k_remap_segslots, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,

@@ -368,9 +368,13 @@ struct GpuSplitStore::Impl {
   uint64_t max_index;
   int N, L, d, PS, PX;
   int next_slot = 0;
-  std::vector<Buf> buf[2];  // [slot][local]
+  // step slots: two (pipelined), three (stale: a step's owner state is held until its
+  // deferred backward while the step after next is localized); the library holds three
+  static constexpr int kSlotsMax = 3;
+  int nslots = 2;
+  std::vector<Buf> buf[kSlotsMax];  // [slot][local]
   std::vector<DBuf> icnt, iall;
-  std::vector<hipEvent_t> slot_done[2];  // [slot][local]: the main streams are done with it
+  std::vector<hipEvent_t> slot_done[kSlotsMax];  // [slot][local]: the main streams are done
   Graveyard grave;  // outgrown step buffers, freed after the device is idle
   std::deque<std::vector<hipEvent_t>> inflight;
   std::vector<std::vector<hipEvent_t>> spare;
@@ -388,18 +392,20 @@ struct GpuSplitStore::Impl {
   // stale schedule: per slot and local shard, the partition buffers free again (after the
   // step's combine), and the step's partials in / combine done / rows in; the step whose
   // backward waits for the next Run
-  std::vector<hipEvent_t> part_free[2], sfwd[2], sx[2], sc[2], sy[2];
+  std::vector<hipEvent_t> part_free[kSlotsMax], sfwd[kSlotsMax], sx[kSlotsMax], sc[kSlotsMax],
+      sy[kSlotsMax];
   bool have_bwd = false;
   Step bwd_step;
 
   Impl(SplitTransport* tr, int pipe, uint64_t mi)
       : t(tr), pipelined(pipe != 0), stale(pipe == 2), max_index(mi) {
+    nslots = stale ? 3 : 2;
     N = t->nranks();
     L = t->nlocal();
     d = dfx_ctx_vdim(t->ctx(0));
     PS = dfx_split_part_floats(t->ctx(0), N);
     PX = dfx_split_pxv_floats(t->ctx(0));
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < kSlotsMax; ++s) {
       buf[s].resize(L);
       slot_done[s].resize(L);
       for (int l = 0; l < L; ++l) {
@@ -444,7 +450,7 @@ struct GpuSplitStore::Impl {
       for (auto e : v) (void)hipEventDestroy(e);
     for (auto& s : slot_done)
       for (auto e : s) (void)hipEventDestroy(e);
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < kSlotsMax; ++s)
       for (auto* v : {&part_free[s], &sfwd[s], &sx[s], &sc[s], &sy[s]})
         for (auto e : *v) (void)hipEventDestroy(e);
     for (auto& m : marks)
@@ -879,7 +885,7 @@ struct GpuSplitStore::Impl {
       throw Error(DFX_ERR_ARG, "split store: bad job type");
     const bool want_cnt = push_cnt && job == DFX_JOB_TRAINING && d > 0;
     const int s = next_slot;
-    next_slot ^= 1;
+    next_slot = (next_slot + 1) % nslots;
     Partition(s, b);
     if (!pipelined) {
       Run(Begin(s, b, job, want_cnt, preds, false));
