@@ -96,7 +96,9 @@ struct Kw {
   // value gathered by position at the outputs (A/B at C2: 126 -> 161 M ex/s); 0: {value, row}
   // carried beside each item
   int lb_gather = 1;
-  int lb_tiles = 256;  // lb_tiles=<n>: the bucket Localizer's row tiles (histogram / scatter blocks)
+  // lb_tiles=<n>: the bucket Localizer's row tiles at most (histogram / scatter blocks of 1024
+  // threads).  Same-box A/B at C3: 256 -> 128 tiles 131.5 -> 132.9 M ex/s (two rounds)
+  int lb_tiles = 128;
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -203,7 +205,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
-    else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 256;
+    else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
