@@ -89,6 +89,9 @@ struct Kw {
   // sort, 4 the outputs, 8 k_lb_scatter's row search; the Localizer's results are then wrong
   int lb_diag = 0;
   int lb_wave = 1;  // lb_wave=1: the bucket Localizer sorts one bucket per wave (0: per block)
+  // lane_after_fwd=1: the fused step's Localizer lane starts after the previous step's forward
+  // (A/B of where the lane's traffic lands: beside the backward only)
+  int lane_after_fwd = 0;
   // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
   // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
   int lb_keyfirst = 0;
@@ -203,6 +206,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
     else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
+    else if (k == "lane_after_fwd") kw->lane_after_fwd = atoi(cv) != 0;
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
@@ -437,6 +441,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_diag = kw.lb_diag;
   c->lb_tiles = kw.lb_tiles;
   c->lb_wave = kw.lb_wave;
+  c->lane_after_fwd = kw.lane_after_fwd;
   c->lb_keyfirst = kw.lb_keyfirst;
   c->lb_gather = kw.lb_gather;
   c->loc_onepass = kw.loc_onepass;

@@ -237,6 +237,7 @@ struct Context {
   int fwd_lanes = 0;      // kwarg fwd_lanes
   int fwd_ids = 1;        // kwarg fwd_ids (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
+  int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
   int lb_wave = 1;        // kwarg lb_wave
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 1;      // kwarg lb_gather (locbucket.hip: valued rows / values by position): one bucket per wave (locbucket.hip k_lb_wbucket)

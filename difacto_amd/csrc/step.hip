@@ -261,6 +261,9 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
   DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_in, 0));
   DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[k], 0));
+  // (kwarg lane_after_fwd) the previous step's forward first: this Localizer then runs beside
+  // that step's backward only, and the forward has the memory system to itself
+  if (c->lane_after_fwd) DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_fwd, 0));
   // Localizer::Compact: sorted unique keys (segments in key order, the order Update walks
   // keys in — InitV draws — and, per key, the (row, nnz) order of its gradient sums)
   LocOut o;
