@@ -480,6 +480,15 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
       }
       // ---- V rows 8 nnz at a time, accumulated in nnz order
       const int nin = (int)((o1 - j0) < (uint64_t)CH ? (o1 - j0) : (uint64_t)CH);
+      if (d == 0) {  // LR: the chunk's w x in nnz order (SpMV::Times skips w == 0, spmv.h:124-125)
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+          const float w = __shfl(wm[t / G], gbase + t % G, kWave);
+          const float x = valued ? __shfl(xm[t / G], gbase + t % G, kWave) : 1.f;
+          if (t < nin && w != 0.f) acc = valued ? acc + w * x : acc + w;
+        }
+        continue;
+      }
 #pragma unroll
       for (int b = 0; b < CH / VB; ++b) {
         if (b * VB >= nin) break;
@@ -892,6 +901,15 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
     else if (G == 4) hipLaunchKernelGGL((k_fm_fwd_fat<4, 8>), grid, dim3(kFmNT), 0, st, a);
     DFX_HIP(hipGetLastError());
     if (G == 2 || G == 4) return DFX_OK;
+  }
+  if (a.index && spread && a.d == 0 && a.lr_lanes && a.B > 0 && !a.part) {
+    // LR (V_dim 0): four lanes per row, each finding a quarter of a 32-nnz chunk's entries with
+    // all their loads in flight, the w x summed in nnz order (kwarg lr_lanes; 0: one thread per
+    // row, k_fm_fwd)
+    *nblk = (int)((a.B + kFmNT / 4 - 1) / (kFmNT / 4));
+    hipLaunchKernelGGL((k_fm_fwd_probe<4, 4>), dim3((unsigned)*nblk), dim3(kFmNT), 0, st, a);
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
   }
   if (a.index && spread && vec && CPL == 4 && G >= 4 && G <= 32 && a.B > 0) {
     // kwarg fwd_cpl = 8 at V_dim >= 64 (a multiple of 8): two float4 per lane, half the lanes

@@ -235,7 +235,8 @@ struct Context {
   int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
   hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
-  int fwd_ids = 1;        // kwarg fwd_ids (fm.hip fwd_probe_body IDS)
+  int fwd_ids = 1;        // kwarg fwd_ids
+  int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
   int lb_wave = 1;        // kwarg lb_wave

@@ -367,6 +367,42 @@ def test_bucket_localizer_equals_lsd(H, kind):
         c.close()
 
 
+@pytest.mark.parametrize("binary", [True, False])
+def test_lr_forward_four_lanes_bit_identical(H, binary):
+    """The LR forward (V_dim 0) on four lanes per row (kwarg lr_lanes=1, the default: a 32-nnz
+    chunk's entry loads in flight together, the w x summed in nnz order) against one thread per
+    row (lr_lanes=0): predictions bit-identical every step, the model identical, both equal to
+    the oracle.  Ragged rows (empty rows, rows up to 2k nnz) and a 700-nnz row."""
+    cfg = dict(V_dim=0, lr=.1, l1=.05)
+    ca = H.Context(0, max_keys=1 << 16, lr_lanes=0, **cfg)
+    cb = H.Context(0, max_keys=1 << 16, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(3001, 39, 1 << 15, binary=binary, ragged=True, seed=60 + step)
+        if step == 3:  # one long row
+            ids = np.concatenate([blk.ids, np.arange(700, dtype=np.uint64) * 7919])
+            offs = np.concatenate([blk.offs, [blk.offs[-1] + 700]]).astype(np.uint64)
+            vals = None if binary else np.concatenate([blk.vals, np.full(700, .5, np.float32)])
+            blk = D.RowBlock(offs, ids, vals, np.concatenate([blk.labels, [1.0]]))
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=(step < 2), pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=(step < 2), pred=pb)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        assert np.array_equal(pa.cpu().numpy().view(np.uint32), pb.cpu().numpy().view(np.uint32))
+        assert np.array_equal(pb.cpu().numpy().view(np.uint32),
+                              np.asarray(opred, np.float32).view(np.uint32)), step
+        qa, qb = H.progress(ca), H.progress(cb)
+        assert abs(qa["loss"] - qb["loss"]) <= 1e-12 * abs(qa["loss"]) and qa["auc"] == qb["auc"]
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    va = H.Store(ca).pull(ca.tensor(uniq, torch.int64))[0].cpu().numpy()
+    vb = H.Store(cb).pull(cb.tensor(uniq, torch.int64))[0].cpu().numpy()
+    assert np.array_equal(va.view(np.uint32), vb.view(np.uint32))
+    ca.close()
+    cb.close()
+
+
 @pytest.mark.parametrize("d", [128, 200])
 def test_two_pass_backward_bit_identical(H, d):
     """The wide-V_dim fused backward in two passes (k_fm_bwd_w: one lane per key — entry, g_w,
