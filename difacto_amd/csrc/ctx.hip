@@ -95,6 +95,9 @@ struct Kw {
   // lane_after_fwd=1: the fused step's Localizer lane starts after the previous step's forward
   // (A/B of where the lane's traffic lands: beside the backward only)
   int lane_after_fwd = 0;
+  // auc_db=1 (default): the fused step's AUC snapshot alternates between two buffers, so a
+  // forward waits only for the AUC lane of two steps back (0: of the step before)
+  int auc_db = 1;
   // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
   // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
   int lb_keyfirst = 0;
@@ -210,6 +213,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
     else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
     else if (k == "lane_after_fwd") kw->lane_after_fwd = atoi(cv) != 0;
+    else if (k == "auc_db") kw->auc_db = atoi(cv) != 0;
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
@@ -369,7 +373,7 @@ int pipeline_init(Context* c) {
   c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
-  for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc})
+  for (hipEvent_t* e : {&c->ev_in, &c->ev_fwd, &c->ev_auc, &c->ev_auc_p[0], &c->ev_auc_p[1]})
     DFX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (int s = 0; s < kSlots; ++s)
     for (hipEvent_t* e : {&c->ev_loc[s], &c->ev_free[s], &c->ev_part[s]})
@@ -447,6 +451,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_tiles = kw.lb_tiles;
   c->lb_wave = kw.lb_wave;
   c->lane_after_fwd = kw.lane_after_fwd;
+  c->auc_db = kw.auc_db;
   c->lb_keyfirst = kw.lb_keyfirst;
   c->lb_gather = kw.lb_gather;
   c->loc_onepass = kw.loc_onepass;
@@ -503,10 +508,11 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
     release_ws(c->ows[s]);
   }
   release_ws(c->aws);
+  release_ws(c->aws_alt);
   release_ws(c->uws);
   for (auto h : c->dist_host)
     if (h) (void)hipHostFree(h);
-  for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc})
+  for (hipEvent_t e : {c->ev_in, c->ev_fwd, c->ev_auc, c->ev_auc_p[0], c->ev_auc_p[1]})
     if (e) (void)hipEventDestroy(e);
   for (int s = 0; s < kSlots; ++s) {
     for (hipEvent_t e : {c->ev_loc[s], c->ev_free[s], c->ev_part[s]})

@@ -209,6 +209,9 @@ struct Context {
   Workspace bws[kSlots];  // [0], [1]: also the fused step's Localizer parities
   DevState* bds[kSlots] = {};
   Workspace aws;
+  Workspace aws_alt;  // auc_db: the other parity's AUC snapshot (fused step)
+  int auc_par = 0;
+  hipEvent_t ev_auc_p[2] = {};  // auc_db: the AUC that last read each parity's snapshot
   DevState* ads = nullptr;
   hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
   hipEvent_t ev_loc[kSlots] = {}, ev_free[kSlots] = {};
@@ -239,6 +242,7 @@ struct Context {
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
+  int auc_db = 1;          // kwarg auc_db (step.hip): double-buffered AUC snapshot
   int lb_wave = 1;        // kwarg lb_wave
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 1;      // kwarg lb_gather (locbucket.hip: valued rows / values by position): one bucket per wave (locbucket.hip k_lb_wbucket)

@@ -69,7 +69,8 @@ struct LbArgs {
   uint64_t* kbuf;        // items
   uint32_t* qbuf;        // rows / positions of unpacked items
   uint64_t* sbuf;        // side payloads (valued, carried: kwarg lb_gather=0)
-  uint32_t* rowof;       // valued, gathered (lb_gather=1): each position's row, by k_lb_scatter
+  uint2* rowof;          // valued, gathered (lb_gather=1): each position's {row, value bits},
+                         // written in input order by k_lb_scatter
   uint64_t* kscr;        // scratch of the global-memory passes
   uint32_t* qscr;
   uint64_t* sscr;
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
     for (int u = 0; u < kLbUnr; ++u) {
       const uint64_t j = wj + (uint64_t)u * kWave + l;
       id[u] = j < j1 ? ldnt(a.index + j, a.nt != 0) : 0ull;
-      if (S && !a.rowof) x[u] = j < j1 ? ldnt(a.value + j, a.nt != 0) : 0.f;
+      if (S) x[u] = j < j1 ? ldnt(a.value + j, a.nt != 0) : 0.f;
     }
     if (wj >= j1) continue;  // wave-uniform
     int ra = search(wj);     // the row of the window's first item (wave-uniform)
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
       stnt(a.kbuf + pos, p.packed ? ((((k - p.kmin) >> p.lo) << p.rb) | (q & qmask)) : k,
            a.nt != 0);
       if (!p.packed) a.qbuf[pos] = (uint32_t)q;
-      if (S && a.rowof) a.rowof[j] = row;  // in input order (coalesced)
+      if (S && a.rowof) a.rowof[j] = make_uint2(row, __float_as_uint(x[u]));  // input order
       else if (S) a.sbuf[pos] = (uint64_t)__float_as_uint(x[u]) | ((uint64_t)row << 32);
     }
   }
@@ -1170,14 +1171,15 @@ __global__ __launch_bounds__(kLbNT) void k_lb_out(LbArgs a) {
 }
 
 // valued data (lb_gather=1): each occurrence's position (left in occ_row by the bucket kernel)
-// replaced by its row, and its value gathered — one thread per occurrence, so the random reads
-// of rowof / value are all in flight at once (inside the bucket kernel's slot loop each waited)
+// replaced by its row and its value, one 8-byte {row, value} read per occurrence — one thread
+// per occurrence, so the random reads are all in flight at once (inside the bucket kernel's
+// slot loop each waited)
 __global__ __launch_bounds__(kLbNT) void k_lb_gather(LbArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kLbNT + threadIdx.x;
   if (i >= a.nnz) return;
-  const uint32_t ps = a.occ_row[i];
-  a.occ_row[i] = a.rowof[ps];
-  if (a.occ_x) a.occ_x[i] = a.value[ps];
+  const uint2 rv = a.rowof[a.occ_row[i]];  // one 8-byte read per occurrence
+  a.occ_row[i] = rv.x;
+  if (a.occ_x) a.occ_x[i] = __uint_as_float(rv.y);
 }
 
 int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
@@ -1225,7 +1227,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   // valued data: each position's row written in input order, the row and value gathered by
   // position at the outputs (lb_gather=1), or {value, row} carried beside each item (0)
   const bool gather = valued && c->lb_gather;
-  a.rowof = gather ? ws.vals0.as<uint32_t>() : nullptr;
+  a.rowof = gather ? ws.vals0.as<uint2>() : nullptr;
   a.sscr = ws.vals1.as<uint64_t>();
   a.qbuf = ws.lbq.as<uint32_t>();
   a.qscr = a.qbuf + nnz;

@@ -93,6 +93,7 @@ int step_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(ws_reserve(c, rows, nnz));
   DFX_TRY(loc_reserve(c->bws[0], nnz, c->loc_stream));
   DFX_TRY(loc_reserve(c->bws[1], nnz, c->loc_stream));
+  if (c->auc_db) DFX_TRY(auc_reserve(c->aws_alt, rows, c->aux_stream));
   return auc_reserve(c->aws, rows, c->aux_stream);
 }
 
@@ -244,7 +245,12 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   Workspace& bw = c->bws[k];
   DevState* bds = c->bds[k];
   const Lane LL{c->loc_stream, &bw, bds, &c->ds->err};
-  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  // the AUC snapshot's buffers: one, or two alternating (auc_db)
+  const int ap = c->auc_db ? c->auc_par : 0;
+  Workspace& aw = ap ? c->aws_alt : c->aws;
+  hipEvent_t ev_auc_mine = c->auc_db ? c->ev_auc_p[ap] : c->ev_auc;
+  if (c->auc_db) c->auc_par ^= 1;
+  const Lane AL{c->aux_stream, &aw, c->ads, &c->ds->err};
   uint32_t* segstart = bw.segstart.as<uint32_t>();
   uint32_t* col = bw.col.as<uint32_t>();       // per nnz: the rank of its key
   uint64_t* uniq = bw.uniq.as<uint64_t>();     // per rank: the key
@@ -329,9 +335,9 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   // the forward writes the AUC lane's snapshot of (pred, label): the lane's buffers are free
   // once the previous AUC is done.  (A last-block loss reduction inside the forward cost more
   // than the launch it saves: the device-scope fence of each block writes back its XCD's L2.)
-  a.auc_key = c->aws.ak0.as<uint32_t>();
-  a.auc_lab = c->aws.av0.as<uint32_t>();
-  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+  a.auc_key = aw.ak0.as<uint32_t>();
+  a.auc_lab = aw.av0.as<uint32_t>();
+  DFX_HIP(hipStreamWaitEvent(c->stream, ev_auc_mine, 0));
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
   prof_mark(c, 4);
@@ -343,7 +349,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   lane_mark(c, 2, c->aux_stream);
   if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   lane_mark(c, 3, c->aux_stream);
-  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
+  if (c->auc_db) DFX_HIP(hipEventRecord(ev_auc_mine, c->aux_stream));
   prof_mark(c, 5);
 
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
