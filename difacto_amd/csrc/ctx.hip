@@ -95,9 +95,11 @@ struct Kw {
   // lane_after_fwd=1: the fused step's Localizer lane starts after the previous step's forward
   // (A/B of where the lane's traffic lands: beside the backward only)
   int lane_after_fwd = 0;
-  // auc_db=1 (default): the fused step's AUC snapshot alternates between two buffers, so a
-  // forward waits only for the AUC lane of two steps back (0: of the step before)
-  int auc_db = 1;
+  // auc_db=1: the fused step's AUC snapshot alternates between two buffers, so a forward waits
+  // only for the AUC lane of two steps back (0, the default: of the step before).  Same-box A/B:
+  // a tie at C3 (133.5 / 133.5 M ex/s) and C2 (186.6 / 186.4); with it the lane overlaps more of
+  // the backward (0.44 -> 0.49 ms)
+  int auc_db = 0;
   // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
   // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
   int lb_keyfirst = 0;

@@ -242,7 +242,7 @@ struct Context {
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
-  int auc_db = 1;          // kwarg auc_db (step.hip): double-buffered AUC snapshot
+  int auc_db = 0;          // kwarg auc_db (step.hip): double-buffered AUC snapshot
   int lb_wave = 1;        // kwarg lb_wave
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 1;      // kwarg lb_gather (locbucket.hip: valued rows / values by position): one bucket per wave (locbucket.hip k_lb_wbucket)
