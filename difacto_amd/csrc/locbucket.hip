@@ -175,11 +175,12 @@ __device__ inline unsigned long long lb_wave_max(unsigned long long v) {
 
 constexpr int kLbUnr = 8;  // ids in flight per thread
 
-// the histogram and scatter kernels' blocks: 16 waves on a tile, for the loads in flight
-constexpr int kLbHNT = 1024;
-constexpr int kLbHWaves = kLbHNT / kWave;
+// the histogram and scatter kernels' blocks: 16 waves on a tile by default, for the loads in
+// flight (kwarg lb_hnt = 256 | 512 | 1024)
 
-__global__ __launch_bounds__(kLbHNT) void k_lb_hist(LbArgs a) {
+template <int HNT>
+__global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
+  constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
   extern __shared__ uint32_t lb_dyn[];
   uint32_t* hist = lb_dyn;
   __shared__ unsigned long long red[4][kLbHWaves];
@@ -279,8 +280,9 @@ __global__ __launch_bounds__(kLbScanWaves * kWave) void k_lb_colscan(LbArgs a) {
   }
 }
 
-template <bool S>
-__global__ __launch_bounds__(kLbHNT) void k_lb_scatter(LbArgs a) {
+template <bool S, int HNT>
+__global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
+  constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
   extern __shared__ uint64_t lb_dyn64[];
   __shared__ uint32_t lds[kLbHWaves + 1];
   __shared__ uint32_t whist[kLbHWaves][kWave];
@@ -1238,17 +1240,27 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.diag = c->lb_diag;
   a.keyfirst = c->lb_keyfirst;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
-  hipLaunchKernelGGL(k_lb_hist, dim3((unsigned)ntiles), dim3(kLbHNT), nbk * sizeof(uint32_t),
+#define DFX_LB_HIST(NT) \
+  hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT), nbk * sizeof(uint32_t), \
                      L.stream, a);
+  if (c->lb_hnt == 256) { DFX_LB_HIST(256) }
+  else if (c->lb_hnt == 512) { DFX_LB_HIST(512) }
+  else { DFX_LB_HIST(1024) }
+#undef DFX_LB_HIST
   hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
                      L.stream, a);
   const size_t scatter_lds = ((nbk + 1) & ~1u) * sizeof(uint32_t) + (rt + 1) * sizeof(uint64_t);
-  if (valued)
-    hipLaunchKernelGGL(k_lb_scatter<true>, dim3((unsigned)ntiles), dim3(kLbHNT), scatter_lds,
-                       L.stream, a);
-  else
-    hipLaunchKernelGGL(k_lb_scatter<false>, dim3((unsigned)ntiles), dim3(kLbHNT), scatter_lds,
-                       L.stream, a);
+#define DFX_LB_SCAT(NT)                                                                    \
+  if (valued)                                                                              \
+    hipLaunchKernelGGL((k_lb_scatter<true, NT>), dim3((unsigned)ntiles), dim3(NT), scatter_lds, \
+                       L.stream, a);                                                       \
+  else                                                                                     \
+    hipLaunchKernelGGL((k_lb_scatter<false, NT>), dim3((unsigned)ntiles), dim3(NT),         \
+                       scatter_lds, L.stream, a);
+  if (c->lb_hnt == 256) { DFX_LB_SCAT(256) }
+  else if (c->lb_hnt == 512) { DFX_LB_SCAT(512) }
+  else { DFX_LB_SCAT(1024) }
+#undef DFX_LB_SCAT
   // the LDS form of the per-bucket sort follows the last batch's item form (a batch whose items
   // do not pack while the launch expected packed ones sorts through global memory: correct)
   const bool q_lds = hint[2] == 2u;

@@ -325,9 +325,13 @@ def test_bucket_localizer_equals_lsd(H, kind):
     against the onesweep radix sort (loc_bucket=0): predictions, loss and AUC identical every
     step, the model identical at the end, and both equal to the oracle within the usual
     tolerances.  Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one; skewed and moving
-    key ranges exercise the global-memory bucket passes and the radix fallback."""
+    key ranges exercise the global-memory bucket passes and the radix fallback.  A third
+    context runs the histogram / scatter on 256-thread blocks (lb_hnt=256: other row windows
+    per block, another tile split)."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=m, **cfg) for m in (0, 1)]
+    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=0, **cfg),
+          H.Context(0, max_keys=1 << 21, loc_bucket=1, **cfg),
+          H.Context(0, max_keys=1 << 21, loc_bucket=1, lb_hnt=256, **cfg)]
     up = O.Updater(**cfg)
     rng = np.random.default_rng(9)
     for step in range(5):
@@ -350,9 +354,10 @@ def test_bucket_localizer_equals_lsd(H, kind):
             H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pr)
             preds.append(pr.cpu().numpy().view(np.uint32))
             progs.append(H.progress(c))
-        assert np.array_equal(preds[0], preds[1]), step
-        assert progs[0]["loss"] == progs[1]["loss"], step
-        assert progs[0]["auc"] == progs[1]["auc"], step
+        for i in (1, 2):
+            assert np.array_equal(preds[0], preds[i]), (step, i)
+            assert progs[0]["loss"] == progs[i]["loss"], (step, i)
+            assert progs[0]["auc"] == progs[i]["auc"], (step, i)
         assert abs(progs[1]["loss"] - loss) <= 1e-4 * abs(loss), (step, progs[1]["loss"], loss)
         assert abs(progs[1]["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     uniq, _, _ = O.localize(blk.offs, blk.ids)
@@ -361,8 +366,8 @@ def test_bucket_localizer_equals_lsd(H, kind):
         assert np.array_equal(l.cpu().numpy(), vs[0][1].cpu().numpy())
         assert np.array_equal(v.cpu().numpy().view(np.uint32), vs[0][0].cpu().numpy().view(np.uint32))
     st = [H.Store(c).stats() for c in cs]
-    assert st[0]["n_keys"] == st[1]["n_keys"] == up.size()
-    assert st[0]["seed"] == st[1]["seed"] == up.seed
+    assert st[0]["n_keys"] == st[1]["n_keys"] == st[2]["n_keys"] == up.size()
+    assert st[0]["seed"] == st[1]["seed"] == st[2]["seed"] == up.seed
     for c in cs:
         c.close()
 
