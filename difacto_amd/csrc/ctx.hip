@@ -81,6 +81,7 @@ struct Kw {
   // fwd_probe_body IDS; same-box A/B at C3 with fat_nb 8: 127.6 -> 130.0 M ex/s, forward
   // 0.248 -> 0.213 ms in the step); 0: each trip loads its ids
   int fwd_ids = 1;
+  int fwd_pf = 1;  // fwd_pf=1: with fwd_ids, the next row's offsets and ids prefetched
   // lr_lanes=1 (default): the LR forward (V_dim 0) on four lanes per row with a chunk's entry
   // loads in flight together (fm.hip fwd_probe_body, d == 0); 0: one thread per row
   int lr_lanes = 1;
@@ -222,6 +223,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
+    else if (k == "fwd_pf") kw->fwd_pf = atoi(cv) != 0;
     else if (k == "lr_lanes") kw->lr_lanes = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
@@ -448,6 +450,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->main_excl = kw.main_excl;
   c->fwd_lanes = kw.fwd_lanes;
   c->fwd_ids = kw.fwd_ids;
+  c->fwd_pf = kw.fwd_pf;
   c->lr_lanes = kw.lr_lanes;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;

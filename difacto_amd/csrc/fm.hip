@@ -320,13 +320,18 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
 // whole number of trips) in LDS in one trip — G lanes, all loads in flight — and each trip reads
 // its NB ids from LDS: a trip is one memory round trip (the slots) instead of two (ids, then
 // slots).  The same sums in the same order: bit-identical.
+// PF (IDS, kwarg fwd_pf=1): the group's NEXT row's offsets are loaded when a row starts and its
+// first ids beside the row's last trip of slots, so a row costs its slot trips only — not
+// offsets, then ids, then slots.  Still bit-identical.
 constexpr int kFwdIds = 40;
 
-template <int G, bool FAT, int NB = 8, int CPL = 4, bool IDS = false>
+template <int G, bool FAT, int NB = 8, int CPL = 4, bool IDS = false, bool PF = false>
 __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   static_assert(CPL == 4 || (CPL == 8 && !FAT), "fat slots: one float4 per lane");
   constexpr int CHI = (kFwdIds / NB) * NB;  // ids staged per chunk: whole trips
   static_assert(!IDS || (FAT && CHI % G == 0), "staged ids: fat slots");
+  static_assert(!PF || IDS, "prefetch: staged ids");
+  constexpr int PFN = PF ? CHI / G : 1;
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
   constexpr int MA = CH / G;      // lookups per lane per chunk
@@ -337,13 +342,36 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   const int d = a.d;
   __shared__ double red[kFmNT / kWave];
   double loss = 0;
+  const int64_t rstride = (int64_t)gridDim.x * RPB;
+  // PF: the next row's offsets, and (pf_ok) its first ids and values held in registers
+  uint64_t pf_o0 = 0, pf_o1 = 0;
+  uint64_t pf_id[PFN];
+  float pf_x[PFN];
+  bool pf_ok = false;
+  if (PF && (int64_t)blockIdx.x * RPB + g < a.B) {
+    const int64_t r0 = fwd_row(a, (int64_t)blockIdx.x * RPB + g);
+    pf_o0 = a.offs[r0];
+    pf_o1 = a.offs[r0 + 1];
+  }
   // IDS runs on a resident grid (launch_fwd_fused): the block's groups take rows blockIdx.x *
   // RPB + g, then one grid of rows further on, so no half-empty last round of blocks; else one
   // row per group
-  for (int64_t ri = (int64_t)blockIdx.x * RPB + g; ri < a.B;
-       ri = IDS ? ri + (int64_t)gridDim.x * RPB : a.B) {
+  for (int64_t ri = (int64_t)blockIdx.x * RPB + g; ri < a.B; ri = IDS ? ri + rstride : a.B) {
     const int64_t r = fwd_row(a, ri);
-    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
+    uint64_t o0, o1;
+    if constexpr (PF) {
+      o0 = pf_o0;
+      o1 = pf_o1;
+      pf_o0 = pf_o1 = 0;  // no next row: no prefetch
+      if (ri + rstride < a.B) {
+        const int64_t rn = fwd_row(a, ri + rstride);
+        pf_o0 = a.offs[rn];
+        pf_o1 = a.offs[rn + 1];
+      }
+    } else {
+      o0 = a.offs[r];
+      o1 = a.offs[r + 1];
+    }
     float acc = 0.f;
     float xv[CPL], xxvv[CPL];
 #pragma unroll
@@ -354,6 +382,21 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
       __shared__ uint64_t s_id[IDS ? RPB : 1][IDS ? CHI : 1];
       __shared__ float s_x[IDS ? RPB : 1][IDS ? CHI : 1];
       uint64_t c_end = o0;  // the staged chunk of ids ends here
+      if constexpr (PF) {
+        if (pf_ok) {  // this row's first ids, loaded beside the last row's last trip
+          __builtin_amdgcn_wave_barrier();  // the last row's reads are done
+#pragma unroll
+          for (int m = 0; m < PFN; ++m) {
+            if (o0 + l + (uint64_t)G * m < o1) {
+              s_id[g][l + G * m] = pf_id[m];
+              if (valued) s_x[g][l + G * m] = pf_x[m];
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          c_end = o0 + CHI;
+          pf_ok = false;
+        }
+      }
       for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
         const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
         uint64_t key[NB];
@@ -386,6 +429,19 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
           }
           const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
           key[t] = a.keys_ready ? id : reverse_bytes(mm);
+        }
+        if constexpr (PF) {
+          if (j0 + NB >= o1 && pf_o1 > pf_o0) {  // the row's last trip: the next row's ids
+#pragma unroll
+            for (int m = 0; m < PFN; ++m) {
+              const uint64_t j = pf_o0 + l + (uint64_t)G * m;
+              if (j < pf_o1) {
+                pf_id[m] = a.index[j];
+                if (valued) pf_x[m] = a.val[j];
+              }
+            }
+            pf_ok = true;
+          }
         }
         float4 v[NB];
         float2 eh[NB];  // even lanes {w, vrow}, odd lanes the key
@@ -625,9 +681,9 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
 }
 
 // 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
-template <int G, int NB, bool IDS = false>
+template <int G, int NB, bool IDS = false, bool PF = false>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
-  fwd_probe_body<G, true, NB, 4, IDS>(a);
+  fwd_probe_body<G, true, NB, 4, IDS, PF>(a);
 }
 
 // blocks of kernel K resident at once on this device (at most want): a grid whose blocks loop
@@ -888,6 +944,13 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
                          st, a);                                                          \
       DFX_HIP(hipGetLastError());                                                         \
       return DFX_OK;                                                                      \
+    }
+    if (G == 4 && a.fat_nb == 8 && a.fwd_ids && a.fwd_pf) {
+      *nblk = (int)resident_grid<k_fm_fwd_fat<4, 8, true, true>>(*nblk);
+      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true, true>), dim3((unsigned)*nblk), dim3(kFmNT), 0,
+                         st, a);
+      DFX_HIP(hipGetLastError());
+      return DFX_OK;
     }
     DFX_FWDIDS(6) DFX_FWDIDS(8) DFX_FWDIDS(12)
 #undef DFX_FWDIDS

@@ -508,6 +508,7 @@ int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nr
     a.no_fat_fwd = !c->fat_fwd;
     a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
     a.fwd_ids = c->fwd_ids;
+    a.fwd_pf = c->fwd_pf;
     a.part = part_out;
     a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
     if (sliced) {

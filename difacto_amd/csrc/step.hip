@@ -327,6 +327,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
   a.fwd_lanes = c->fwd_lanes;
   a.fwd_ids = c->fwd_ids;
+  a.fwd_pf = c->fwd_pf;
   a.lr_lanes = c->lr_lanes;
   a.nt = c->nt_mask;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();

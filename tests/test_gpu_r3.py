@@ -36,19 +36,25 @@ def _auc_expect(label, opred, oauc):
 
 
 @pytest.mark.parametrize("lanes,nb", [(2, 4), (2, 6), (2, 8), (4, 4), (4, 6), (4, 8),
-                                      (0, 6), (0, 8), (0, 12)])
+                                      (0, 6), (0, 8), (0, 12), (-1, 8)])
 @pytest.mark.parametrize("binary", [True, False])
 def test_prefetch_forward_bit_identical(H, lanes, nb, binary):
     """Two contexts step the same batches: the default forward and the prefetching one
-    (fwd_lanes) or the one staging each row's ids in LDS (lanes 0: fwd_ids=1).  Ragged rows
-    (empty rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips and chunks."""
+    (fwd_lanes) or the one staging each row's ids in LDS (lanes 0: fwd_ids=1 with the next
+    row's offsets and ids prefetched at nb 8, fwd_pf; lanes -1: fwd_pf=0).  Ragged rows (empty
+    rows, rows up to 2k nnz, a row of 700 nnz) exercise partial trips and chunks; at (0, 8) the
+    batches of 80 k rows give each group of the resident grid two or three rows, so the
+    prefetched rows are the ones checked."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    ca = H.Context(0, max_keys=1 << 16, fwd_ids=0, fat_nb=6, **cfg)  # each trip loads its ids
-    kw = dict(fwd_lanes=lanes) if lanes else dict(fwd_ids=1)
-    cb = H.Context(0, max_keys=1 << 16, fat_nb=nb, **kw, **cfg)
+    big = (lanes, nb) == (0, 8)
+    rows, ks, mk = (80001, 1 << 20, 1 << 21) if big else (3001, 1 << 15, 1 << 16)
+    ca = H.Context(0, max_keys=mk, fwd_ids=0, fat_nb=6, **cfg)  # each trip loads its ids
+    kw = (dict(fwd_lanes=lanes) if lanes > 0 else
+          dict(fwd_ids=1, fwd_pf=1 if lanes == 0 else 0))
+    cb = H.Context(0, max_keys=mk, fat_nb=nb, **kw, **cfg)
     up = O.Updater(**cfg)
     for step in range(4):
-        blk = D.synthetic(3001, 39, 1 << 15, binary=binary, ragged=True, seed=40 + step)
+        blk = D.synthetic(rows, 39, ks, binary=binary, ragged=True, seed=40 + step)
         if step == 3:  # one long row
             ids = np.concatenate([blk.ids, np.arange(700, dtype=np.uint64) * 7919])
             offs = np.concatenate([blk.offs, [blk.offs[-1] + 700]]).astype(np.uint64)
