@@ -112,6 +112,7 @@ struct Kw {
   // threads).  Same-box A/B at C3: 256 -> 128 tiles 131.5 -> 132.9 M ex/s (two rounds)
   int lb_tiles = 128;
   int lb_hnt = 1024;  // lb_hnt=256|512|1024: its histogram / scatter blocks' threads
+  int lb_xcd = 0;     // lb_xcd=1: consecutive tiles on one XCD (measured: more scatter writes)
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -221,6 +222,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
+    else if (k == "lb_xcd") kw->lb_xcd = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_pf") kw->fwd_pf = atoi(cv) != 0;
@@ -457,6 +459,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_diag = kw.lb_diag;
   c->lb_tiles = kw.lb_tiles;
   c->lb_hnt = kw.lb_hnt;
+  c->lb_xcd = kw.lb_xcd;
   c->lb_wave = kw.lb_wave;
   c->lane_after_fwd = kw.lane_after_fwd;
   c->auc_db = kw.auc_db;

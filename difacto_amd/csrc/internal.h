@@ -248,7 +248,8 @@ struct Context {
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 1;      // kwarg lb_gather (locbucket.hip: valued rows / values by position): one bucket per wave (locbucket.hip k_lb_wbucket)
   int lb_tiles = 128;     // kwarg lb_tiles
-  int lb_hnt = 1024;      // kwarg lb_hnt: the bucket Localizer's histogram / scatter block: the bucket Localizer's row tiles at most
+  int lb_hnt = 1024;      // kwarg lb_hnt: the bucket Localizer's histogram / scatter block
+  int lb_xcd = 0;         // kwarg lb_xcd: its tiles XCD-contiguous (A/B: more write traffic): the bucket Localizer's row tiles at most
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once

@@ -82,6 +82,7 @@ struct LbArgs {
   unsigned int* hint;    // pinned: Workspace::lb_hint
   int diag;              // Context::lb_diag (measurement only)
   int keyfirst;          // Context::lb_keyfirst: the wave sort's key-first form (lb_wave_sort)
+  int xcd;               // Context::lb_xcd: consecutive tiles on one XCD (lb_tile)
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -178,6 +179,18 @@ constexpr int kLbUnr = 8;  // ids in flight per thread
 // the histogram and scatter kernels' blocks: 16 waves on a tile by default, for the loads in
 // flight (kwarg lb_hnt = 256 | 512 | 1024)
 
+// The tile a histogram / scatter block takes.  Blocks b and b + 8 share an XCD (its L2); with
+// xcd set, XCD x's blocks take a contiguous range of tiles, so the scatter's runs of one bucket
+// from consecutive tiles — adjacent in the bucket's region — are written through one L2 and
+// leave it as whole lines rather than as partial lines from eight L2s.  The map is a bijection
+// on [0, gridDim.x) whatever the grid; which XCD is which does not matter (for speed only).
+__device__ inline int64_t lb_tile(int xcd) {
+  const uint32_t b = blockIdx.x, T = gridDim.x;
+  if (!xcd) return b;
+  const uint32_t q = T >> 3, r = T & 7u, x = b & 7u;
+  return (int64_t)x * q + (x < r ? x : r) + (b >> 3);
+}
+
 template <int HNT>
 __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
@@ -187,7 +200,8 @@ __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   const LbMap m = lb_map(a.ds, a.wbits);
   const int t = threadIdx.x;
   for (uint32_t d = t; d < m.nbk; d += kLbHNT) hist[d] = 0;
-  const int64_t r0 = (int64_t)blockIdx.x * a.rt;
+  const int64_t tile = lb_tile(a.xcd);
+  const int64_t r0 = tile * a.rt;
   const int64_t r1 = r0 + a.rt < a.B ? r0 + a.rt : a.B;
   const uint64_t j0 = a.offset[r0], j1 = a.offset[r1];
   __syncthreads();
@@ -223,7 +237,7 @@ __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
     red[3][w] = vmax;
   }
   __syncthreads();
-  uint32_t* dst = a.tilecnt + (size_t)blockIdx.x * m.nbk;
+  uint32_t* dst = a.tilecnt + (size_t)tile * m.nbk;
   for (uint32_t d = t; d < m.nbk; d += kLbHNT) dst[d] = hist[d];
   if (t == 0 && j1 > j0) {
     for (int i = 1; i < kLbHWaves; ++i) {
@@ -290,7 +304,8 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t* cur = reinterpret_cast<uint32_t*>(lb_dyn64);  // per bucket: this tile's next slot
   uint64_t* offs = lb_dyn64 + (m.nbk + 1u) / 2;
   const int t = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * a.rt;
+  const int64_t tile = lb_tile(a.xcd);
+  const int64_t r0 = tile * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
   // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
   const uint32_t per = (m.nbk + kLbHNT - 1) / kLbHNT;
@@ -305,7 +320,7 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   }
   uint32_t total;
   uint32_t ex = block_excl_scan<kLbHNT>(mine, lds, &total);
-  const uint32_t* pre = a.tilecnt + (size_t)blockIdx.x * m.nbk;
+  const uint32_t* pre = a.tilecnt + (size_t)tile * m.nbk;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < m.nbk) {
@@ -1239,6 +1254,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.hint = ws.lb_hint;
   a.diag = c->lb_diag;
   a.keyfirst = c->lb_keyfirst;
+  a.xcd = c->lb_xcd;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
 #define DFX_LB_HIST(NT) \
   hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT), nbk * sizeof(uint32_t), \

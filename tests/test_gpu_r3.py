@@ -333,11 +333,11 @@ def test_bucket_localizer_equals_lsd(H, kind):
     tolerances.  Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one; skewed and moving
     key ranges exercise the global-memory bucket passes and the radix fallback.  A third
     context runs the histogram / scatter on 256-thread blocks (lb_hnt=256: other row windows
-    per block, another tile split)."""
+    per block, another tile split; lb_xcd=1: XCD-contiguous tiles)."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     cs = [H.Context(0, max_keys=1 << 21, loc_bucket=0, **cfg),
           H.Context(0, max_keys=1 << 21, loc_bucket=1, **cfg),
-          H.Context(0, max_keys=1 << 21, loc_bucket=1, lb_hnt=256, **cfg)]
+          H.Context(0, max_keys=1 << 21, loc_bucket=1, lb_hnt=256, lb_xcd=1, **cfg)]
     up = O.Updater(**cfg)
     rng = np.random.default_rng(9)
     for step in range(5):
