@@ -104,10 +104,12 @@ struct Kw {
   // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
   // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
   int lb_keyfirst = 0;
-  // lb_gather=1 (default): valued batches sort (key | position) items alone, the row and the
-  // value gathered by position at the outputs (A/B at C2: 126 -> 161 M ex/s); 0: {value, row}
-  // carried beside each item
-  int lb_gather = 1;
+  // lb_gather: valued batches sort (key | position) items alone, the row and the value gathered
+  // by position at the outputs (1; A/B at C2: 126 -> 161 M ex/s) or, in the fused step, read by
+  // position in the backward itself (2, the default: no gather launch on the Localizer lane;
+  // C2 187.5-194.5 -> 195.1-195.5 M ex/s, four same-box rounds); 0: {value, row} carried
+  // beside each item
+  int lb_gather = 2;
   // lb_tiles=<n>: the bucket Localizer's row tiles at most (histogram / scatter blocks of 1024
   // threads).  Same-box A/B at C3: 256 -> 128 tiles 131.5 -> 132.9 M ex/s (two rounds)
   int lb_tiles = 128;
@@ -220,7 +222,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lane_after_fwd") kw->lane_after_fwd = atoi(cv) != 0;
     else if (k == "auc_db") kw->auc_db = atoi(cv) != 0;
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
-    else if (k == "lb_gather") kw->lb_gather = atoi(cv) != 0;
+    else if (k == "lb_gather") kw->lb_gather = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
     else if (k == "lb_xcd") kw->lb_xcd = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;

@@ -1098,8 +1098,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
       const uint32_t i = s0 + ((uint32_t)t < len ? (uint32_t)t : 0u);
-      row[t] = ldnt(a.occ_row + i, nto);
-      x[t] = valued ? ldnt(a.occ_x + i, nto) : 1.f;
+      row[t] = occ_get(a, i, valued, nto, &x[t]);
     }
     // ---- level 3: V / Vaux (or grad / W) of the key, p and XV*p of the occurrences' rows
     float gw = 0.f;
@@ -1217,8 +1216,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       const int gb = (int)(threadIdx.x % kWave) - l;
       for (uint32_t i0 = s0; i0 < s1; i0 += G) {
         const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
-        const uint32_t rl = a.occ_row[i];
-        const float xl = valued ? a.occ_x[i] : 1.f;
+        float xl;
+        const uint32_t rl = occ_get(a, i, valued, false, &xl);
         const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
         const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
@@ -1241,8 +1240,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         for (int k = 0; k < CPL; ++k) acc[k] = g0[k] - vcur[k] * xxp;
         for (uint32_t i0 = s0; i0 < s1; i0 += G) {
           const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
-          const uint32_t rl = a.occ_row[i];
-          const float xl = valued ? a.occ_x[i] : 1.f;
+          float xl;
+          const uint32_t rl = occ_get(a, i, valued, false, &xl);
           const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
           for (int t0 = 0; t0 < G; t0 += WU) {
@@ -1287,8 +1286,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
           const uint32_t i = in + t < s1 ? in + t : s1 - 1;
-          rn[t] = in < s1 ? a.occ_row[i] : 0u;
-          xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
+          xn[t] = 1.f;
+          rn[t] = in < s1 ? occ_get(a, i, valued, false, &xn[t]) : 0u;
         }
 #pragma unroll
         for (int t = 0; t < UNR; ++t) {
@@ -1328,8 +1327,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
             const uint32_t i = in + t < s1 ? in + t : s1 - 1;
-            rn[t] = in < s1 ? a.occ_row[i] : 0u;
-            xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
+            xn[t] = 1.f;
+            rn[t] = in < s1 ? occ_get(a, i, valued, false, &xn[t]) : 0u;
           }
 #pragma unroll
           for (int t = 0; t < UNR; ++t) {
@@ -1516,8 +1515,7 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
 #pragma unroll
         for (int t = 0; t < WU; ++t) {
           const uint32_t i = s0 + t < s1 ? s0 + t : s1 - 1;
-          rw[t] = a.occ_row[i];
-          xw[t] = valued ? a.occ_x[i] : 1.f;
+          rw[t] = occ_get(a, i, valued, false, &xw[t]);
         }
         for (uint32_t i0 = s0; i0 < s1; i0 += WU) {
           float pw[WU];
@@ -1530,8 +1528,8 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
 #pragma unroll
           for (int t = 0; t < WU; ++t) {
             const uint32_t i = in + t < s1 ? in + t : s1 - 1;
-            rn[t] = in < s1 ? a.occ_row[i] : 0u;
-            xn[t] = (in < s1 && valued) ? a.occ_x[i] : 1.f;
+            xn[t] = 1.f;
+            rn[t] = in < s1 ? occ_get(a, i, valued, false, &xn[t]) : 0u;
           }
 #pragma unroll
           for (int t = 0; t < WU; ++t) {
@@ -1655,8 +1653,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
       const int gb = (int)(threadIdx.x % kWave) - l;
       for (uint32_t i0 = s0; i0 < s1; i0 += G) {
         const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
-        const uint32_t rl = a.occ_row[i];
-        const float xl = valued ? a.occ_x[i] : 1.f;
+        float xl;
+        const uint32_t rl = occ_get(a, i, valued, false, &xl);
         const uint32_t nt = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
         for (int t0 = 0; t0 < G; t0 += UNR) {
@@ -1714,8 +1712,8 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
     const int gb = (int)(threadIdx.x % kWave) - l;
     for (uint32_t i0 = s0; i0 < s1; i0 += G) {
       const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
-      const uint32_t rl = a.occ_row[i];
-      const float xl = valued ? a.occ_x[i] : 1.f;
+      float xl;
+      const uint32_t rl = occ_get(a, i, valued, false, &xl);
       const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
       const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
@@ -1749,8 +1747,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
       const uint32_t i = i0 + t < s1 ? i0 + t : s1 - 1;
-      rw[t] = a.occ_row[i];
-      xw[t] = valued ? a.occ_x[i] : 1.f;
+      rw[t] = occ_get(a, i, valued, false, &xw[t]);
     }
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {

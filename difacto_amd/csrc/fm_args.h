@@ -107,6 +107,7 @@ struct BwdArgs {
   const uint32_t* segcol;    // column of each segment (NULL: segment index == column)
   const uint32_t* occ_row;   // row of every occurrence, in sorted (key, pos) order
   const float* occ_x;        // its value (NULL: binary data)
+  const uint2* occ_rx;       // (lb_gather=2) occ_row holds input positions: {row, value} here
   const float* zpad;
   const float* p;
   const float* XVp;
@@ -147,6 +148,20 @@ struct BwdArgs {
   uint4* vlist;
   uint32_t* vcount;
 };
+
+// occurrence i's row, and its value into *x: read directly, or (occ_rx: the bucket Localizer's
+// gather left to the backward) through the input position occ_row holds
+__device__ __forceinline__ uint32_t occ_get(const BwdArgs& a, uint64_t i, bool valued, bool nt,
+                                            float* x) {
+  const uint32_t r = ldnt(a.occ_row + i, nt);
+  if (a.occ_rx) {
+    const uint2 rv = a.occ_rx[r];
+    *x = __uint_as_float(rv.y);
+    return rv.x;
+  }
+  *x = valued ? ldnt(a.occ_x + i, nt) : 1.f;
+  return r;
+}
 
 // the XVp row stride the workspace is sized for (step.hip): p rides in each row
 int xvp_stride(const Context* c);

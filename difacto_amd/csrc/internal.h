@@ -244,16 +244,17 @@ struct Context {
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
   int auc_db = 0;          // kwarg auc_db (step.hip): double-buffered AUC snapshot
-  int lb_wave = 1;        // kwarg lb_wave
+  int lb_wave = 1;        // kwarg lb_wave: one bucket per wave (locbucket.hip k_lb_wbucket)
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
-  int lb_gather = 1;      // kwarg lb_gather (locbucket.hip: valued rows / values by position): one bucket per wave (locbucket.hip k_lb_wbucket)
-  int lb_tiles = 128;     // kwarg lb_tiles
+  int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
+  int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_hnt = 1024;      // kwarg lb_hnt: the bucket Localizer's histogram / scatter block
-  int lb_xcd = 0;         // kwarg lb_xcd: its tiles XCD-contiguous (A/B: more write traffic): the bucket Localizer's row tiles at most
+  int lb_xcd = 0;         // kwarg lb_xcd: its tiles XCD-contiguous (A/B: more write traffic)
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
+  const uint2* loc_rowof[2] = {nullptr, nullptr};  // (lb_gather=2) the parity's {row, value} by position
   int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   int auc_sort = 1;  // the AUC lane's sort (kwarg auc_sort): 3 wave buckets, 2 block buckets,
@@ -412,6 +413,9 @@ struct LocOut {
   uint32_t* occ_row = nullptr;
   float* occ_x = nullptr;
   bool keys_ready = false;  // index holds the final keys (the split owner's received keys)
+  // (fused step, lb_gather=2) set by the bucket Localizer when it left each occurrence's input
+  // position in occ_row and its {row, value} here for the backward to read (else nullptr)
+  const uint2** rowof_out = nullptr;
 };
 int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
                  const uint64_t* index, uint64_t max_index, const LocOut& o);

@@ -1302,7 +1302,10 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, false>), bg, bb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_bucket<false, false>), bg, bb, 0, L.stream, a);
   }
-  if (gather && nnz > 0)
+  // (lb_gather=2, the fused step) the backward reads {row, value} by position itself
+  const bool defer = gather && c->lb_gather == 2 && o.rowof_out != nullptr;
+  if (o.rowof_out) *o.rowof_out = defer ? a.rowof : nullptr;
+  if (gather && !defer && nnz > 0)
     hipLaunchKernelGGL(k_lb_gather, dim3((unsigned)((nnz + kLbNT - 1) / kLbNT)), bb, 0, L.stream,
                        a);
   hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);

@@ -279,12 +279,16 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   o.occ_x = occ_x;
   o.col = c->fwd_probe ? nullptr : col;  // probe mode: the forward finds keys itself
   o.uniq = uniq;
+  const uint2* rowof = c->loc_rowof[k];  // (lb_gather=2) kept with the parity's outputs
+  o.rowof_out = &rowof;
   lane_mark(c, 0, c->loc_stream);
   uint32_t* choff = bw.flags.as<uint32_t>();
   uint32_t* chunk_seg = bw.rowtmp.as<uint32_t>();
   uint32_t* nchunks = &bds->totals[1];
   if (!((c->diag & 2) && c->loc_done[k])) {  // (diag: measurement only)
+    rowof = nullptr;
     DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+    c->loc_rowof[k] = rowof;
     // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
     DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
     c->loc_done[k] = true;
@@ -357,7 +361,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
     BwdArgs g{};
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
-    g.occ_row = occ_row; g.occ_x = occ_x; g.zpad = c->zpad; g.p = ws.p.as<float>();
+    g.occ_row = occ_row; g.occ_x = occ_x; g.occ_rx = rowof; g.zpad = c->zpad;
+    g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
     g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from; g.nt = c->nt_mask;
     g.flags = flags; g.dsw = c->ds;

@@ -378,6 +378,45 @@ def test_bucket_localizer_equals_lsd(H, kind):
         c.close()
 
 
+@pytest.mark.parametrize("vdim", [0, 16, 128])
+def test_deferred_gather_bit_identical(H, vdim):
+    """Valued batches through the bucket Localizer with the {row, value} gather left to the
+    backward (lb_gather=2: each occurrence's input position read there) against the gather
+    kernel on the Localizer lane (lb_gather=1): predictions, loss and AUC identical every step,
+    the model identical at the end, both equal to the oracle.  Ragged rows and one key in
+    every row (> 256 occurrences: the chunked sums read occurrences too)."""
+    cfg = dict(V_dim=vdim, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    cs = [H.Context(0, max_keys=1 << 20, lb_gather=g, **cfg) for g in (1, 2)]
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(20000, 39, 1 << 19, binary=False, ragged=(step % 2 == 1),
+                          seed=120 + step)
+        ids = blk.ids.copy()
+        ids[blk.offs[:-1][np.diff(blk.offs) > 0].astype(np.int64)] = 12345  # a hot key
+        blk = D.RowBlock(blk.offs, ids, blk.vals, blk.labels)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        preds, progs = [], []
+        for c in cs:
+            pr = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+            H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pr)
+            preds.append(pr.cpu().numpy())
+            progs.append(H.progress(c))
+        assert np.array_equal(preds[0].view(np.uint32), preds[1].view(np.uint32)), step
+        assert progs[0]["loss"] == progs[1]["loss"] and progs[0]["auc"] == progs[1]["auc"]
+        if step == 0:  # the models still identical: north_star's 1e-5
+            assert close(preds[1], opred, rtol=1e-5)
+        assert abs(progs[1]["loss"] - loss) <= 1e-4 * abs(loss), (step, progs[1]["loss"], loss)
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    vs = [H.Store(c).pull(c.tensor(uniq, torch.int64)) for c in cs]
+    if vs[0][1] is not None:  # (V_dim 0: no V lengths)
+        assert np.array_equal(vs[0][1].cpu().numpy(), vs[1][1].cpu().numpy())
+    assert np.array_equal(vs[0][0].cpu().numpy().view(np.uint32),
+                          vs[1][0].cpu().numpy().view(np.uint32))
+    for c in cs:
+        c.close()
+
+
 @pytest.mark.parametrize("binary", [True, False])
 def test_lr_forward_four_lanes_bit_identical(H, binary):
     """The LR forward (V_dim 0) on four lanes per row (kwarg lr_lanes=1, the default: a 32-nnz
