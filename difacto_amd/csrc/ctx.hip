@@ -97,10 +97,11 @@ struct Kw {
   // (A/B of where the lane's traffic lands: beside the backward only)
   int lane_after_fwd = 0;
   // auc_db=1: the fused step's AUC snapshot alternates between two buffers, so a forward waits
-  // only for the AUC lane of two steps back (0, the default: of the step before).  Same-box A/B:
-  // a tie at C3 (133.5 / 133.5 M ex/s) and C2 (186.6 / 186.4); with it the lane overlaps more of
-  // the backward (0.44 -> 0.49 ms)
-  int auc_db = 0;
+  // only for the AUC lane of two steps back (0: of the step before).  Same-box A/B: a tie at C3
+  // (133.5 / 133.5 M ex/s) and C2 (186.6 / 186.4), the lane overlapping more of the backward
+  // (0.44 -> 0.49 ms); at B = 10^4, where the one-block AUC (~94 us) outlasts the backward,
+  // 58.6 / 61.6 -> 68.0 / 68.8.  2 (the default): double-buffered for B <= kAucBlockMax only
+  int auc_db = 2;
   // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
   // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
   int lb_keyfirst = 0;
@@ -220,7 +221,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
     else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
     else if (k == "lane_after_fwd") kw->lane_after_fwd = atoi(cv) != 0;
-    else if (k == "auc_db") kw->auc_db = atoi(cv) != 0;
+    else if (k == "auc_db") kw->auc_db = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);

@@ -243,7 +243,7 @@ struct Context {
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
-  int auc_db = 0;          // kwarg auc_db (step.hip): double-buffered AUC snapshot
+  int auc_db = 2;          // kwarg auc_db (step.hip): double-buffered AUC snapshot (2: B <= 12288)
   int lb_wave = 1;        // kwarg lb_wave: one bucket per wave (locbucket.hip k_lb_wbucket)
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
@@ -403,6 +403,9 @@ void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* 
 // 31 set on each key's first occurrence in sorted order), and optionally cnt[U] and
 // segstart[U+1].  With occ_row (and occ_x when value != NULL) it also writes every
 // occurrence's row (and value) in sorted order, for the backward walk.  No model access.
+// the one-block LDS AUC's largest snapshot (metric.hip k_auc_block); auc_db=2 double-buffers the
+// fused step's snapshot up to this many rows
+constexpr int64_t kAucBlockMax = 12288;
 struct LocOut {
   uint64_t* uniq = nullptr;
   float* cnt = nullptr;

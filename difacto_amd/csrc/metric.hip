@@ -216,6 +216,7 @@ __global__ __launch_bounds__(kArNT) void k_auc_runs(int64_t n, const uint32_t* _
 // radix lane takes ~14 latency-bound launches (~0.12 ms of lane time at B = 10^4,
 // profiles/r3/kernel_summary_b1e4_pipelined.md).  Same stable order, so the same AUC exactly.
 constexpr int kAbNT = 1024, kAbItems = 12, kAbMax = kAbNT * kAbItems;  // 12288 rows, 152 KiB
+static_assert(kAbMax == kAucBlockMax, "internal.h names the one-block AUC's limit");
 
 __global__ __launch_bounds__(kAbNT) void k_auc_block(int64_t n, const uint32_t* __restrict__ key,
                                                      const uint32_t* __restrict__ lab,

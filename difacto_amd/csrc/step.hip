@@ -88,12 +88,17 @@ int auc_reserve(Workspace& w, int64_t rows, hipStream_t st) {
   return DFX_OK;
 }
 
+// the fused step's AUC snapshot double-buffered at this batch size (kwarg auc_db)
+static bool auc_db_on(const Context* c, int64_t rows) {
+  return c->auc_db == 1 || (c->auc_db == 2 && rows <= kAucBlockMax);
+}
+
 int step_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(pipeline_init(c));
   DFX_TRY(ws_reserve(c, rows, nnz));
   DFX_TRY(loc_reserve(c->bws[0], nnz, c->loc_stream));
   DFX_TRY(loc_reserve(c->bws[1], nnz, c->loc_stream));
-  if (c->auc_db) DFX_TRY(auc_reserve(c->aws_alt, rows, c->aux_stream));
+  if (auc_db_on(c, rows)) DFX_TRY(auc_reserve(c->aws_alt, rows, c->aux_stream));
   return auc_reserve(c->aws, rows, c->aux_stream);
 }
 
@@ -246,10 +251,13 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DevState* bds = c->bds[k];
   const Lane LL{c->loc_stream, &bw, bds, &c->ds->err};
   // the AUC snapshot's buffers: one, or two alternating (auc_db)
-  const int ap = c->auc_db ? c->auc_par : 0;
+  // (auc_db=2 switches with B: a single-buffered step uses buffer 0 and waits for the latest
+  // AUC; every step records which AUC last read its buffer)
+  const bool db = auc_db_on(c, B);
+  const int ap = db ? c->auc_par : 0;
   Workspace& aw = ap ? c->aws_alt : c->aws;
-  hipEvent_t ev_auc_mine = c->auc_db ? c->ev_auc_p[ap] : c->ev_auc;
-  if (c->auc_db) c->auc_par ^= 1;
+  hipEvent_t ev_auc_mine = db ? c->ev_auc_p[ap] : c->ev_auc;
+  if (db) c->auc_par ^= 1;
   const Lane AL{c->aux_stream, &aw, c->ads, &c->ds->err};
   uint32_t* segstart = bw.segstart.as<uint32_t>();
   uint32_t* col = bw.col.as<uint32_t>();       // per nnz: the rank of its key
@@ -355,7 +363,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   lane_mark(c, 3, c->aux_stream);
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
-  if (c->auc_db) DFX_HIP(hipEventRecord(ev_auc_mine, c->aux_stream));
+  DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
   prof_mark(c, 5);
 
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
