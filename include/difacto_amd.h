@@ -85,8 +85,10 @@ typedef struct dfx_progress {
  * entry and V share one 64/128-byte slot when 4 <= V_dim <= 24 and V_dim % 4 == 0); the
  * sharded store's push_agg=sum|ranks and hash=ordered|mixed; and execution choices that do
  * not change results (A/B switches, measured in DESIGN.md): fwd_probe, xvp_row, bwd_lds,
- * sort_pack, sort_items, sort_lookback, auc_sort=radix|merge, fat_fwd, fat_bwd,
- * initv_onepass.  Unknown keys are ignored (InitAllowUnknown). */
+ * sort_pack, sort_items, sort_lookback, auc_sort=radix|merge|bucket|wbucket, fat_fwd, fat_bwd,
+ * initv_onepass, fat_nb, fwd_ids, fwd_pf, lr_lanes, loc_bucket, lb_wave, lb_keyfirst,
+ * lb_gather=0|1|2, lb_tiles, lb_hnt=256|512|1024, lb_xcd, auc_db=0|1|2, lane_after_fwd,
+ * lane_prio.  Unknown keys are ignored (InitAllowUnknown). */
 const char* dfx_last_error(void);
 int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out);
 int dfx_ctx_destroy(dfx_ctx* ctx);
