@@ -114,7 +114,8 @@ struct Kw {
   // lb_tiles=<n>: the bucket Localizer's row tiles at most (histogram / scatter blocks of 1024
   // threads).  Same-box A/B at C3: 256 -> 128 tiles 131.5 -> 132.9 M ex/s (two rounds)
   int lb_tiles = 128;
-  int lb_hnt = 1024;  // lb_hnt=256|512|1024: its histogram / scatter blocks' threads
+  int lb_hnt = 0;  // lb_hnt=256|512|1024: its histogram / scatter blocks' threads (0: auto,
+                   // 512 for valued batches, 1024 for binary ones)
   int lb_xcd = 0;     // lb_xcd=1: consecutive tiles on one XCD (measured: more scatter writes)
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)

@@ -248,7 +248,7 @@ struct Context {
   int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
   int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
   int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
-  int lb_hnt = 1024;      // kwarg lb_hnt: the bucket Localizer's histogram / scatter block
+  int lb_hnt = 0;         // kwarg lb_hnt: the bucket Localizer's histogram / scatter block (0 auto)
   int lb_xcd = 0;         // kwarg lb_xcd: its tiles XCD-contiguous (A/B: more write traffic)
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)

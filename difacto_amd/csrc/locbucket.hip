@@ -1259,8 +1259,11 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
 #define DFX_LB_HIST(NT) \
   hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT), nbk * sizeof(uint32_t), \
                      L.stream, a);
-  if (c->lb_hnt == 256) { DFX_LB_HIST(256) }
-  else if (c->lb_hnt == 512) { DFX_LB_HIST(512) }
+  // lb_hnt (0: auto): 512-thread blocks for valued batches, whose scatter also writes the
+  // {row, value} pairs (C2 +5.6 %), 1024 for binary ones (C3: 1024 best)
+  const int hnt = c->lb_hnt ? c->lb_hnt : (valued ? 512 : 1024);
+  if (hnt == 256) { DFX_LB_HIST(256) }
+  else if (hnt == 512) { DFX_LB_HIST(512) }
   else { DFX_LB_HIST(1024) }
 #undef DFX_LB_HIST
   hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
@@ -1273,8 +1276,8 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   else                                                                                     \
     hipLaunchKernelGGL((k_lb_scatter<false, NT>), dim3((unsigned)ntiles), dim3(NT),         \
                        scatter_lds, L.stream, a);
-  if (c->lb_hnt == 256) { DFX_LB_SCAT(256) }
-  else if (c->lb_hnt == 512) { DFX_LB_SCAT(512) }
+  if (hnt == 256) { DFX_LB_SCAT(256) }
+  else if (hnt == 512) { DFX_LB_SCAT(512) }
   else { DFX_LB_SCAT(1024) }
 #undef DFX_LB_SCAT
   // the LDS form of the per-bucket sort follows the last batch's item form (a batch whose items
