@@ -82,6 +82,9 @@ struct Kw {
   // 0.248 -> 0.213 ms in the step); 0: each trip loads its ids
   int fwd_ids = 1;
   int fwd_pf = 1;  // fwd_pf=1: with fwd_ids, the next row's offsets and ids prefetched
+  // fwd_tile=1: the tiled gather forward at V_dim 16 (fm.hip k_fm_fwd_tile): a tile's nnz
+  // gathered a chunk at a time into LDS, then summed per row in nnz order
+  int fwd_tile = 0;
   // lr_lanes=1 (default): the LR forward (V_dim 0) on four lanes per row with a chunk's entry
   // loads in flight together (fm.hip fwd_probe_body, d == 0); 0: one thread per row
   int lr_lanes = 1;
@@ -230,6 +233,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_pf") kw->fwd_pf = atoi(cv) != 0;
+    else if (k == "fwd_tile") kw->fwd_tile = atoi(cv) != 0;
     else if (k == "lr_lanes") kw->lr_lanes = atoi(cv) != 0;
     else if (k == "fwd_lanes") {
       kw->fwd_lanes = atoi(cv);
@@ -457,6 +461,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fwd_lanes = kw.fwd_lanes;
   c->fwd_ids = kw.fwd_ids;
   c->fwd_pf = kw.fwd_pf;
+  c->fwd_tile = kw.fwd_tile;
   c->lr_lanes = kw.lr_lanes;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;

@@ -297,6 +297,99 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd(FwdArgs a) {
   }
 }
 
+// One row's outputs once its sums are complete (G lanes, CPL coordinates per lane): the split's
+// partial, or FMLoss::Predict's finish — s = sum_l (XV_l^2 - XXVV_l) serially over l, the
+// clip — then CalcGrad's p, XV_ * p, Evaluate's logloss and the AUC lane's snapshot.
+// Loss::Evaluate's term of one row (loss.h:57-66), in double.  Not inlined: a caller that loops
+// over rows would otherwise hold exp's and log's double constants in VGPRs across its loop.
+__device__ __noinline__ double row_logloss(float label, float pr) {
+  const double yy = label > 0 ? 1.0 : -1.0;
+  return log(1.0 + exp(-yy * (double)pr));
+}
+
+template <int G, int CPL, int DK = 0>
+__device__ __forceinline__ void fwd_row_out(const FwdArgs& a, int64_t r, int l, int gbase,
+                                            float acc, const float (&xv)[CPL],
+                                            const float (&xxvv)[CPL], double* loss) {
+  const int d = DK > 0 ? DK : a.d;  // DK: V_dim known to the caller
+  if (a.part) {
+    // owner-computes split: this owner's share of the row (split.hip k_split_combine)
+    float* pr_row = a.part + r * split_part_floats(d, a.part_n);
+    if (a.part_n > 1) {  // [XV | sum w x | sum_l XXVV_l (serial over l) | 0 0]
+      float sx = 0.f;
+      for (int q = 0; q < G; ++q) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const float tk = __shfl(xxvv[k], gbase + q, kWave);
+          if (q * CPL + k < d) sx += tk;
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < CPL / 4; ++m)
+        if (l * CPL + 4 * m < d)
+          *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
+              make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
+      if (l == 0) {
+        pr_row[d] = acc;
+        pr_row[d + 1] = sx;
+        pr_row[d + 2] = pr_row[d + 3] = 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < CPL / 4; ++m) {
+        if (l * CPL + 4 * m < d) {
+          *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
+              make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
+          *reinterpret_cast<float4*>(pr_row + d + l * CPL + 4 * m) =
+              make_float4(xxvv[4 * m], xxvv[4 * m + 1], xxvv[4 * m + 2], xxvv[4 * m + 3]);
+        }
+      }
+      if (l == 0) {
+        pr_row[2 * d] = acc;
+        pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
+      }
+    }
+  }
+  float pr = acc;
+  if (d > 0 && !a.part) {
+    // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
+    float t4[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) t4[k] = xv[k] * xv[k] - xxvv[k];
+    float s = 0.f;
+    for (int q = 0; q < G; ++q) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const float tk = __shfl(t4[k], gbase + q, kWave);
+        if (q * CPL + k < d) s += tk;
+      }
+    }
+    double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
+    pr = (float)y;
+    pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
+  }
+  const float p = a.part ? 0.f : logit_p(a.label[r], pr, a.rw, r);
+  const int64_t xs = a.xs > d ? a.xs : d;
+  if (a.part) {
+    // the partial is all this kernel writes
+  } else if (l == 0) {
+    a.p_out[r] = p;
+    if (xs > d) a.XVp[r * xs + d] = p;
+    a.pred[r] = pr;
+    *loss += row_logloss(a.label[r], pr);  // Loss::Evaluate (loss.h:57-66)
+    if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
+      uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
+      a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < CPL / 4; ++m)  // XV_ *= p (fm_loss.h:196-199)
+    if (d > 0 && l * CPL + 4 * m < d && !a.part)
+      *reinterpret_cast<float4*>(a.XVp + r * xs + l * CPL + 4 * m) =
+          make_float4(xv[4 * m] * p, xv[4 * m + 1] * p, xv[4 * m + 2] * p, xv[4 * m + 3] * p);
+}
+
 // Probe-mode forward with the lookups spread over the row's lanes (CPL = 4: float4 per lane,
 // G lanes per row).  The row is walked in chunks of 32 nnz: first every lane of the group finds
 // the entries of its 32/G of them (id -> key -> home slot -> {w, vrow, key}), all loads issued
@@ -586,83 +679,7 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
         }
       }
     }
-    if (a.part) {
-      // owner-computes split: this owner's share of the row (split.hip k_split_combine)
-      float* pr_row = a.part + r * split_part_floats(d, a.part_n);
-      if (a.part_n > 1) {  // [XV | sum w x | sum_l XXVV_l (serial over l) | 0 0]
-        float sx = 0.f;
-        for (int q = 0; q < G; ++q) {
-#pragma unroll
-          for (int k = 0; k < CPL; ++k) {
-            const float tk = __shfl(xxvv[k], gbase + q, kWave);
-            if (q * CPL + k < d) sx += tk;
-          }
-        }
-#pragma unroll
-        for (int m = 0; m < CPL / 4; ++m)
-          if (l * CPL + 4 * m < d)
-            *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
-                make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
-        if (l == 0) {
-          pr_row[d] = acc;
-          pr_row[d + 1] = sx;
-          pr_row[d + 2] = pr_row[d + 3] = 0.f;
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < CPL / 4; ++m) {
-          if (l * CPL + 4 * m < d) {
-            *reinterpret_cast<float4*>(pr_row + l * CPL + 4 * m) =
-                make_float4(xv[4 * m], xv[4 * m + 1], xv[4 * m + 2], xv[4 * m + 3]);
-            *reinterpret_cast<float4*>(pr_row + d + l * CPL + 4 * m) =
-                make_float4(xxvv[4 * m], xxvv[4 * m + 1], xxvv[4 * m + 2], xxvv[4 * m + 3]);
-          }
-        }
-        if (l == 0) {
-          pr_row[2 * d] = acc;
-          pr_row[2 * d + 1] = pr_row[2 * d + 2] = pr_row[2 * d + 3] = 0.f;
-        }
-      }
-    }
-    float pr = acc;
-    if (d > 0 && !a.part) {
-      // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..d-1 (fm_loss.h:110-113)
-      float t4[CPL];
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) t4[k] = xv[k] * xv[k] - xxvv[k];
-      float s = 0.f;
-      for (int q = 0; q < G; ++q) {
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const float tk = __shfl(t4[k], gbase + q, kWave);
-          if (q * CPL + k < d) s += tk;
-        }
-      }
-      double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
-      pr = (float)y;
-      pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
-    }
-    const float p = a.part ? 0.f : logit_p(a.label[r], pr, a.rw, r);
-    const int64_t xs = a.xs > d ? a.xs : d;
-    if (a.part) {
-      // the partial is all this kernel writes
-    } else if (l == 0) {
-      a.p_out[r] = p;
-      if (xs > d) a.XVp[r * xs + d] = p;
-      a.pred[r] = pr;
-      double yy = a.label[r] > 0 ? 1.0 : -1.0;
-      loss += log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
-      if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
-        uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
-        a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-        a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < CPL / 4; ++m)  // XV_ *= p (fm_loss.h:196-199)
-      if (d > 0 && l * CPL + 4 * m < d && !a.part)
-        *reinterpret_cast<float4*>(a.XVp + r * xs + l * CPL + 4 * m) =
-            make_float4(xv[4 * m] * p, xv[4 * m + 1] * p, xv[4 * m + 2] * p, xv[4 * m + 3] * p);
+    fwd_row_out<G, CPL>(a, r, l, gbase, acc, xv, xxvv, &loss);
   }
   if (a.part) return;  // block-uniform: no loss partial in split mode
   for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
@@ -684,6 +701,174 @@ __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
 template <int G, int NB, bool IDS = false, bool PF = false>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
   fwd_probe_body<G, true, NB, 4, IDS, PF>(a);
+}
+
+// ---- the tiled gather forward (kwarg fwd_tile; fat slots at V_dim 16) -----------------------
+// A block owns a tile of kFtRows consecutive rows (group g = 4 lanes accumulates row g) and
+// walks the tile's nnz — contiguous in CSR — in chunks of kFtChunk.  Per chunk every group
+// gathers kFtPer nnz of it (nnz c0 + g + 64 m): its key's home slot in one trip (even / odd lanes
+// the entry's halves, lane l its float4 of V, as k_fm_fwd_fat), the key checked, and {w, V
+// visible, V} into LDS.  The chunk's ids (and values) were staged in LDS by the whole block, and
+// the NEXT chunk's are in flight beside this chunk's slot loads.  Then each group adds its row's
+// nnz of the chunk from LDS in nnz order — FMLoss::Predict's sums in the reference's order
+// (fm_loss.h:67-119), bit-identical to the row walks.  Every gather of a chunk is independent of
+// the others, so a block keeps kFtChunk slot loads in flight, and a row no longer costs a chain
+// of dependent trips (k_fm_fwd_fat: ~5 per row after its ids, 231 VGPRs at 2 waves / SIMD).
+constexpr int kFtRows = kFmNT / 4;          // 64 rows per tile
+constexpr int kFtChunk = 512;               // nnz gathered per round trip
+constexpr int kFtPer = kFtChunk / kFtRows;  // 8 per group
+constexpr int kFtLd = kFtChunk / kFmNT;     // ids per thread of the block's staging loads
+
+template <bool VALUED>
+__global__ __launch_bounds__(kFmNT, 4) void k_fm_fwd_tile(FwdArgs a) {
+  __shared__ float4 s_v[kFtChunk][4];
+  __shared__ float s_w[kFtChunk];
+  __shared__ uint8_t s_ok[kFtChunk];
+  __shared__ uint64_t s_id[kFtChunk];
+  __shared__ float s_x[VALUED ? 2 : 1][VALUED ? kFtChunk : 1];  // by chunk parity
+  __shared__ uint64_t s_off[kFtRows + 1];
+  __shared__ double red[kFmNT / kWave];
+  constexpr int G = 4;
+  const int t = threadIdx.x;
+  const int g = t / G;
+  const int l = t % G;
+  const int gbase = (t % kWave) - l;
+  const bool ntf = (a.nt & kNtFwdTable) != 0;
+  double loss = 0;
+  const int64_t ntiles = (a.B + kFtRows - 1) / kFtRows;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * kFtRows;
+    const int nr = (int)(a.B - r0 < kFtRows ? a.B - r0 : kFtRows);
+    __syncthreads();  // the last tile's reads of s_off / s_id are done
+    if (t <= nr) s_off[t] = a.offs[r0 + t];
+    __syncthreads();
+    const uint64_t T0 = s_off[0], T1 = s_off[nr];
+    const uint64_t o0 = g < nr ? s_off[g] : T1, o1 = g < nr ? s_off[g + 1] : T1;
+#pragma unroll
+    for (int i = 0; i < kFtLd; ++i) {  // the first chunk's ids, coalesced
+      const uint64_t j = T0 + t + (uint64_t)kFmNT * i;
+      if (j < T1) {
+        s_id[t + kFmNT * i] = a.index[j];
+        if (VALUED) s_x[0][t + kFmNT * i] = a.val[j];
+      }
+    }
+    __syncthreads();
+    float acc = 0.f;
+    float xv[4], xxvv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
+    int par = 0;
+    for (uint64_t c0 = T0; c0 < T1; c0 += kFtChunk, par ^= 1) {  // block-uniform
+      float2 eh[kFtPer];  // even lanes {w, vrow}, odd lanes the key
+      float4 v[kFtPer];
+#pragma unroll
+      for (int m = 0; m < kFtPer; ++m) {
+        const int jl = g + kFtRows * m;
+        if (c0 + jl < T1) {
+          const uint64_t id = s_id[jl];
+          const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+          const uint64_t key = a.keys_ready ? id : reverse_bytes(mm);
+          const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key, a.T)));
+          eh[m] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
+          v[m] = ld4(sl + 8 + 4 * l, ntf);
+        }
+      }
+      // the next chunk's ids (and values), in flight beside the slots
+      const uint64_t c1 = c0 + kFtChunk;
+      uint64_t idn[kFtLd];
+      float xn[kFtLd];
+#pragma unroll
+      for (int i = 0; i < kFtLd; ++i) {
+        const uint64_t j = c1 + t + (uint64_t)kFmNT * i;
+        if (j < T1) {
+          idn[i] = a.index[j];
+          if (VALUED) xn[i] = a.val[j];
+        }
+      }
+      float wm[kFtPer];
+      bool okm[kFtPer];
+#pragma unroll
+      for (int m = 0; m < kFtPer; ++m) {
+        const int jl = g + kFtRows * m;
+        if (c0 + jl >= T1) continue;  // group-uniform
+        const uint64_t id = s_id[jl];
+        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+        const uint64_t key = a.keys_ready ? id : reverse_bytes(mm);
+        const float k0 = __shfl(eh[m].x, gbase + 1, kWave), k1 = __shfl(eh[m].y, gbase + 1, kWave);
+        uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
+        float w = __shfl(eh[m].x, gbase, kWave);
+        int vr = __float_as_int(__shfl(eh[m].y, gbase, kWave));
+        if (ek != key && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
+          uint64_t h = tbl_hash(key, a.T);
+          for (uint64_t probe = 0; ek != key && ek != kEmptyKey && probe < a.T.mask; ++probe) {
+            h = (h + 1) & a.T.mask;
+            ek = ent_at(a.T, h)->key;
+          }
+          if (ek == key) {
+            const Entry* e = ent_at(a.T, h);
+            w = e->w;
+            vr = e->vrow;
+            v[m] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e) + 8 + 4 * l);
+          }
+        }
+        // absent (inserted by this training step's backward): w = 0, no V
+        if (ek != key) { w = 0.f; vr = -1; }
+        wm[m] = w;
+        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
+        okm[m] = vr >= 0 && !(a.l1_shrk && w == 0.f);
+      }
+      __syncthreads();  // the last chunk's sums have read s_v; every group has read s_id
+#pragma unroll
+      for (int m = 0; m < kFtPer; ++m) {
+        const int jl = g + kFtRows * m;
+        if (c0 + jl < T1) {
+          s_v[jl][l] = v[m];
+          if (l == 0) {
+            s_w[jl] = wm[m];
+            s_ok[jl] = okm[m] ? 1 : 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < kFtLd; ++i) {
+        if (c1 + t + (uint64_t)kFmNT * i < T1) {
+          s_id[t + kFmNT * i] = idn[i];
+          if (VALUED) s_x[par ^ 1][t + kFmNT * i] = xn[i];
+        }
+      }
+      __syncthreads();
+      // this group's row inside the chunk, in nnz order
+      const uint64_t lo = o0 > c0 ? o0 : c0, hi = o1 < c1 ? o1 : c1;
+      for (uint64_t j = lo; j < hi; ++j) {
+        const int jl = (int)(j - c0);
+        const float w = s_w[jl];
+        const float x = VALUED ? s_x[par][jl] : 1.f;
+        // SpMV::Times skips w == 0 (spmv.h:124-125)
+        if (w != 0.f) acc = VALUED ? acc + w * x : acc + w;
+        if (s_ok[jl]) {
+          const float4 vv = s_v[jl][l];
+          const float vk[4] = {vv.x, vv.y, vv.z, vv.w};
+          const float xx = x * x;  // XX_ (fm_loss.h:86-92)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            xv[k] = VALUED ? xv[k] + vk[k] * x : xv[k] + vk[k];
+            const float q = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
+            xxvv[k] = VALUED ? xxvv[k] + q * xx : xxvv[k] + q;
+          }
+        }
+      }
+    }
+    if (g < nr) fwd_row_out<4, 4, 16>(a, r0 + g, l, gbase, acc, xv, xxvv, &loss);
+  }
+  if (a.part) return;  // block-uniform: no loss partial in split mode
+  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
+  if (lane_id() == 0) red[t / kWave] = loss;
+  __syncthreads();
+  if (t == 0) {
+    double s = 0;
+    for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
+    a.loss_part[blockIdx.x] = s;
+  }
 }
 
 // blocks of kernel K resident at once on this device (at most want): a grid whose blocks loop
@@ -933,6 +1118,19 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
 #undef DFX_FWDPF
     set_error("fwd_lanes 2 | 4 with fat_nb 4 | 6 | 8");
     return DFX_ERR_ARG;
+  }
+  if (a.index && a.B > 0 && spread && fat && G == 4 && a.fwd_tile && a.slice_len <= 0) {
+    // the tiled gather forward, on a resident grid (its blocks loop over tiles)
+    const int64_t ntiles = (a.B + kFtRows - 1) / kFtRows;
+    if (a.val) {
+      *nblk = (int)resident_grid<k_fm_fwd_tile<true>>(ntiles);
+      hipLaunchKernelGGL(k_fm_fwd_tile<true>, dim3((unsigned)*nblk), dim3(kFmNT), 0, st, a);
+    } else {
+      *nblk = (int)resident_grid<k_fm_fwd_tile<false>>(ntiles);
+      hipLaunchKernelGGL(k_fm_fwd_tile<false>, dim3((unsigned)*nblk), dim3(kFmNT), 0, st, a);
+    }
+    DFX_HIP(hipGetLastError());
+    return DFX_OK;
   }
   if (a.index && a.B > 0 && spread && fat) {
     const dim3 grid((unsigned)*nblk);

@@ -70,6 +70,7 @@ struct FwdArgs {
   int fwd_lanes;   // V_dim 16 fat slots: k_fm_fwd_fat_pf with this many lanes per row (0: off)
   int fwd_ids;     // fat slots: the row's ids staged in LDS first (kwarg fwd_ids)
   int fwd_pf;      // fwd_ids, fat_nb 8: the next row's offsets and ids prefetched (kwarg fwd_pf)
+  int fwd_tile;    // fat slots at V_dim 16: the tiled gather forward (kwarg fwd_tile)
   int lr_lanes;    // V_dim 0: four lanes per row (kwarg lr_lanes)
   float* part;
   int nt;  // kwarg nt: kNtFwdTable = the slots with the streaming policy

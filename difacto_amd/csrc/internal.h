@@ -240,6 +240,7 @@ struct Context {
   int fwd_lanes = 0;      // kwarg fwd_lanes
   int fwd_ids = 1;        // kwarg fwd_ids
   int fwd_pf = 1;         // kwarg fwd_pf
+  int fwd_tile = 0;       // kwarg fwd_tile (fm.hip k_fm_fwd_tile)
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)

@@ -296,7 +296,7 @@ __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
 // ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
-// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments, tile = block;
+// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments, taken by ticket;
 // per segment its chunk count
 // (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
 // (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
@@ -311,7 +311,12 @@ __global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart,
     return;
   }
   unsigned* meta = ds->sortmeta;
-  const int64_t tile = blockIdx.x;  // workgroups start in index order: no ticket needed
+  // tile by ticket (zeroed by k_os_plan / k_lb_init), in block start order: a tile's
+  // predecessors are held by running blocks even beside another look-back kernel
+  __shared__ uint32_t s_tile;
+  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaCpTile], 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
   const int64_t U = (int64_t)ds->u_count;
   if (tile * kLocTile >= U) return;  // no later tile waits on this one
   const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;

@@ -1218,6 +1218,24 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   int wbits = 1;
   while (wbits < kLbMaxBits && ((int64_t)1024 << wbits) < nnz) ++wbits;
   const uint32_t nbk = 1u << wbits;
+  // past ~3/4 of the LDS sort's capacity per bucket on average (beyond ~12.6 M nnz) most buckets
+  // would be oversize: the radix Localizer outright, not a bucket pass that falls back
+  if (nnz > (int64_t)nbk * (kLbCap * 3 / 4)) return DFX_OK;
+  if (hint[2] == 0u) {
+    // no batch seen on this workspace yet: seed the item form from what the host knows, so a
+    // first batch whose items cannot pack (64-bit hashed ids, received keys) takes the LDS form
+    // rather than sending every bucket through k_lb_big.  Varying key bits are at
+    // most the bytes of max_index - 1 (ReverseBytes moves them, localizer.cc:24)
+    int kb = 64;
+    if (!o.keys_ready && max_index != ~0ull) {
+      kb = 0;
+      for (uint64_t m = max_index - 1; m; m >>= 8) kb += 8;
+    }
+    const uint64_t qmax = valued ? (uint64_t)(nnz - 1) : (uint64_t)(B - 1);
+    int rb = 0;
+    for (uint64_t q = qmax; q; q >>= 1) ++rb;
+    hint[2] = kb + rb <= 63 ? 1u : 2u;
+  }
   int64_t ntiles = std::min<int64_t>(c->lb_tiles, std::max<int64_t>(1, nnz / 4096));
   int64_t rt = std::min<int64_t>(kLbMaxRows, std::max<int64_t>(1, (B + ntiles - 1) / ntiles));
   ntiles = (B + rt - 1) / rt;

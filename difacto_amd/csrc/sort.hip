@@ -187,16 +187,16 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   const int w = t / kWave;
   const int l = lane_id();
   const int64_t n = os_count(n0, n_dev);
-  // a grid smaller than the tile count (a pass the host expects to find constant, below) takes
-  // tiles until they run out: tickets are taken in order and a block takes its next one only
-  // after publishing its tile, so every tile a block looks back on is done or held by a
-  // running block
-  // A full grid takes tile = block index: workgroups start in index order, so every tile a block
-  // looks back on is running or done (a ticket counter serialised the ~950 tiles of a pass on one
-  // word: ~88 returning atomics per us, MI355X_MICROARCH.md 'dequeue')
+  // Tiles are taken by ticket (k_os_plan zeroes the counter), in the order blocks actually
+  // start: every tile a block looks back on is then done or held by a running block.  Block
+  // index order is not start order across XCDs, and this pass can run beside another look-back
+  // kernel on another stream (the AUC lane's sort beside the main stream's InitV), so tile =
+  // block index could wait on a block that cannot be placed.  A grid smaller than
+  // the tile count (a pass the host expects to find constant, below) takes tiles until they run
+  // out, its next ticket only after publishing its tile.
   const bool looping = (int64_t)gridDim.x * (kOsNT * IT) < n;
   for (;;) {
-  if (t == 0) s_tile = looping ? (int64_t)atomicAdd(&meta[kMetaTile + q], 1u) : (int64_t)blockIdx.x;
+  if (t == 0) s_tile = (int64_t)atomicAdd(&meta[kMetaTile + q], 1u);
 #pragma unroll
   for (int i = 0; i < kOsWaves; ++i) wcnt[i][t] = 0;
   __syncthreads();

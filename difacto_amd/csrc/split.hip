@@ -509,6 +509,7 @@ int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nr
     a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
     a.fwd_ids = c->fwd_ids;
     a.fwd_pf = c->fwd_pf;
+    a.fwd_tile = c->fwd_tile;
     a.part = part_out;
     a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
     if (sliced) {

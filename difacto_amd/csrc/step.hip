@@ -340,6 +340,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.fwd_lanes = c->fwd_lanes;
   a.fwd_ids = c->fwd_ids;
   a.fwd_pf = c->fwd_pf;
+  a.fwd_tile = c->fwd_tile;
   a.lr_lanes = c->lr_lanes;
   a.nt = c->nt_mask;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();

@@ -105,10 +105,19 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
     if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0u;
     return;
   }
-  // tile = block: workgroups start in index order, so a block only waits on running ones (a
-  // ticket counter serialised ~950 blocks on one word, and a one-word-per-step look-back made
-  // the chain ~40 us of the main stream whenever new keys need V)
-  const int64_t tile = blockIdx.x;
+  // tile by ticket, in the order blocks start: a block only waits on running ones.  Block index
+  // order is not start order across XCDs, and the AUC lane's look-back sort can run beside this
+  // kernel, so tile = block index could wait on a block that cannot be placed.  The
+  // block that draws the last ticket zeroes the counter for the next launch (every block draws
+  // one; k_step_finalize zeroes it too).
+  __shared__ uint32_t s_tile;
+  if (threadIdx.x == 0) {
+    s_tile = atomicAdd(&ds->iv_ticket, 1u);
+    if (s_tile == gridDim.x - 1)
+      __hip_atomic_store(&ds->iv_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int64_t tile = s_tile;
   const int64_t n = (int64_t)nds->u_count;
   const int64_t base = tile * kIvTile;
   if (base >= n) return;  // no later tile waits on this one

@@ -1034,7 +1034,10 @@ class SplitStore:
 
     stale=True (pipelined): the 1-step-stale schedule — step t+1's owner forward runs before
     step t's backward, so each step's partial exchange and row gather travel beside the other
-    step's compute (oracle: dist_oracle.SplitStaleOracle; push_agg=sum).
+    step's compute (oracle: dist_oracle.SplitStaleOracle; push_agg=sum).  EXPERIMENTAL and
+    parity unpinned by the reference, which has no such schedule: the gradient takes the stale
+    forward's p / XV*p but the diag(XXp) V term from the owner's current V.  One slice only
+    (set_slices(k > 1) raises).
 
     Batches must stay alive until the second submit after the one that took them (the store
     keeps them), a pipelined step's predictions / progress are complete after the next submit

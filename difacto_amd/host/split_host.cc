@@ -64,6 +64,7 @@ struct DBuf {
   void* ensure(size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (bytes <= cap) return p;
+    if (p && !grave) throw Error(DFX_ERR_ARG, "split store: DBuf without a graveyard grew");
     if (p) grave->bufs.push_back({c, p});
     p = nullptr;
     cap = std::max(bytes + bytes / 8, 2 * cap);
@@ -944,6 +945,10 @@ void GpuSplitStore::AllReduceSum(std::vector<double>* v) { impl_->t->AllReduceSu
 
 void GpuSplitStore::SetSlices(int K) {
   if (K < 0 || K > 64) throw Error(DFX_ERR_ARG, "split store: 0 <= slices <= 64");
+  // the stale schedule runs each step's owner forward whole (RunStale: one slice); say so
+  // instead of ignoring the request
+  if (impl_->stale && K > 1)
+    throw Error(DFX_ERR_ARG, "split store: slices > 1 are not supported by the stale schedule");
   impl_->slices = K;  // 0: the default
 }
 

@@ -40,9 +40,11 @@ int dfx_dist_rccl_ids(int n, void* out);
  * `nranks`.  force_exchange: exchange through RCCL even at one rank.  pipelined 1: step t+1's
  * partition, key exchange and owner Localizer run beside step t (same results as 0);
  * 2: the 1-step-stale schedule — also step t+1's owner forward before step t's backward, each
- * step's partial exchange and row gather beside the other step's compute (no reference
- * counterpart: one of the schedules KVStoreDist's asynchronous pushes allow, kvstore_dist.h:
- * 137-150) */
+ * step's partial exchange and row gather beside the other step's compute.  EXPERIMENTAL, parity
+ * unpinned by the reference: it has no counterpart there (one of the schedules KVStoreDist's
+ * asynchronous pushes allow, kvstore_dist.h:137-150); its gradient takes the forward's p and
+ * XV*p but the diag(XXp) V term from the owner's current V (the reference would use the pulled
+ * copy).  Pinned only to oracle/dist_oracle.py SplitStaleOracle */
 int dfx_split_store_create_rccl(dfx_ctx* ctx, int rank, int nranks, const void* ids,
                                 int force_exchange, int pipelined, uint64_t max_index,
                                 dfx_split_store** out);
@@ -61,7 +63,8 @@ int dfx_split_store_flush(dfx_split_store* s);
 int dfx_split_store_sync(dfx_split_store* s);
 /* a step's rows in `slices` slices (>= 1; 0: the default, one slice):
  * slice h's partials travel while slice h + 1's owner forward runs, and its [XV*p | p] rows
- * while the next slice combines (streams of the driver's own); results do not change */
+ * while the next slice combines (streams of the driver's own); results do not change.
+ * DFX_ERR_ARG for slices > 1 on a stale (pipelined = 2) store, which runs one slice */
 int dfx_split_store_set_slices(dfx_split_store* s, int slices);
 /* host: v[n] summed over the processes (a collective of every rank, on the split-count
  * communicator; loopback: unchanged) */

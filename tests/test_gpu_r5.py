@@ -1,0 +1,80 @@
+"""Round-5 GPU tests: the kernels added this round against the oracle and the kernels they
+replace.
+
+* k_fm_fwd_tile (context kwarg fwd_tile): the tiled gather forward at V_dim 16 sums each row in
+  the reference's (row, nnz) order (fm_loss.h:67-119) from LDS, so predictions must be
+  BIT-identical to the row-walking forward's and to the oracle's, and the trained model the
+  same.  Ragged rows cover the chunk edges: empty rows, rows longer than a chunk (512 nnz),
+  rows crossing chunk and tile edges, and the last partial tile.
+"""
+import numpy as np
+import pytest
+import torch
+
+from difacto_amd import data as D
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def H():
+    from difacto_amd import hotpath
+    return hotpath
+
+
+def _auc_expect(label, opred, oauc):
+    return O.auc_stable_ties(label, opred) if O.has_ties(opred) else oauc
+
+
+def _long_rows(blk, lens, binary, seed):
+    """blk with rows of the given lengths appended (ids spread over the key space)"""
+    rng = np.random.default_rng(seed)
+    ids, offs, vals, labels = [blk.ids], [blk.offs], [blk.vals], [blk.labels]
+    end = int(blk.offs[-1])
+    for n in lens:
+        ids.append(rng.integers(0, 1 << 40, n, dtype=np.uint64))
+        end += n
+        offs.append(np.array([end], np.uint64))
+        if not binary:
+            vals.append((1.0 - rng.random(n, dtype=np.float32)).astype(np.float32))
+        labels.append(np.array([1.0 if n % 2 else -1.0], np.float32))
+    return D.RowBlock(np.concatenate(offs).astype(np.uint64), np.concatenate(ids),
+                      None if binary else np.concatenate(vals), np.concatenate(labels))
+
+
+@pytest.mark.parametrize("rows", [3001, 80001])
+@pytest.mark.parametrize("binary", [True, False])
+def test_tile_forward_bit_identical(H, rows, binary):
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    ks, mk = (1 << 15, 1 << 16) if rows < 10000 else (1 << 20, 1 << 21)
+    ca = H.Context(0, max_keys=mk, **cfg)              # the row-walking fat forward
+    cb = H.Context(0, max_keys=mk, fwd_tile=1, **cfg)  # the tiled gather forward
+    up = O.Updater(**cfg)
+    for step in range(4):
+        blk = D.synthetic(rows, 39, ks, binary=binary, ragged=True, seed=60 + step)
+        if step >= 2:  # rows longer than a chunk, one exactly a chunk, one crossing two
+            blk = _long_rows(blk, [700, 512, 1300, 0, 3], binary, seed=step)
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=(step < 1), pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=(step < 1), pred=pb)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 1), want_pred=True)
+        qa, qb = H.progress(ca), H.progress(cb)
+        got = pb.cpu().numpy()
+        assert np.array_equal(pa.cpu().numpy().view(np.uint32), got.view(np.uint32)), step
+        # no key reaches a chunked (> 256 occurrences) gradient sum: the model stays the
+        # oracle's, so predictions equal the reference's bit for bit
+        assert np.array_equal(got.view(np.uint32), np.asarray(opred, np.float32).view(np.uint32))
+        # per-block loss partials: the double sums differ in the last bits only
+        assert abs(qa["loss"] - qb["loss"]) <= 1e-12 * abs(qa["loss"]) and qa["auc"] == qb["auc"]
+        assert abs(qb["loss"] - loss) <= 1e-4 * abs(loss)
+        assert abs(qb["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    va, la = H.Store(ca).pull(ca.tensor(uniq, torch.int64))
+    vb, lb = H.Store(cb).pull(cb.tensor(uniq, torch.int64))
+    assert np.array_equal(la.cpu().numpy(), lb.cpu().numpy())
+    assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
+    ca.close()
+    cb.close()
