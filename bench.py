@@ -828,6 +828,42 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         dt = float(t.item())
         colls[cname] = {"ms_per_step": round(dt / nb * 1e3, 4),
                         "value": round(world * B * nb / dt, 1), "steps": nb}
+    used_cpp = store is not None
+    if store is not None and not args.sync and args.push_agg == "sum":
+        # the C++ driver's other pipelined schedule on the same batches, so that one N-GPU run
+        # reports both: the pipelined default (bulk-synchronous results) beside the 1-step-stale
+        # one (each step's exchanges beside the other step's compute; DESIGN.md (e) predicts
+        # ~0.8 of the fused step per GPU at N = 8 against ~0.7) — or the default when --stale
+        # ran the main line.  A store of its own (its own RCCL communicators) on the same shard.
+        other_stale = not args.stale
+        store.flush()
+        store.close()
+        store = None
+        ids2 = torch.zeros(DI.SplitStore.rccl_ids_size(), dtype=torch.uint8)
+        if rank == 0:
+            ids2 = torch.frombuffer(bytearray(DI.SplitStore.rccl_ids()), dtype=torch.uint8)
+        dist.broadcast(ids2, src=0, group=comm.cgroup)
+        st2 = DI.SplitStore([shard], pipelined=True, stale=other_stale,
+                            rccl=(rank, world, ids2.numpy().tobytes(), args.force_collectives))
+        for bt in batches[:2]:
+            st2.submit([bt], H.kTraining)
+        st2.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for bt in batches[:nb]:
+            st2.submit([bt], H.kTraining)
+        st2.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        dt = time.perf_counter() - t1
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=comm.cgroup)
+        dt = float(t.item())
+        colls["split_stale_cpp" if other_stale else "split_pipelined_cpp"] = {
+            "ms_per_step": round(dt / nb * 1e3, 4), "value": round(world * B * nb / dt, 1),
+            "steps": nb}
+        st2.close()
     H.progress(ctx)
     ctx.sync()
     st = H.Store(ctx).stats()
@@ -873,7 +909,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                                   % ("bulk-synchronous" if args.sync else
                                      "1-step-stale (step t+1's owner forward before step t's "
                                      "backward, the exchanges beside the other step's compute)"
-                                     if args.stale and store is not None else
+                                     if args.stale and used_cpp else
                                      "bulk-synchronous results, next step's partition / key "
                                      "exchange / owner Localizer on the Localizer lane")
                                   if split else
@@ -883,7 +919,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
                                   args.push_agg),
                    "rows_per_gpu_step": B, "global_batch": B * world,
                    "parallelism": "dp%d + model sharded by key range" % world,
-                   "driver": "cpp (libdfx_dist.so)" if store is not None else "python"},
+                   "driver": "cpp (libdfx_dist.so)" if used_cpp else "python"},
         "roofline": {"bound": "hbm", "kernel": rkernel,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -58,11 +58,8 @@ struct Kw {
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
   int sort_pack = 1;    // sort_pack=0: the Localizer sorts 12-byte (key, row) pairs
-  // auc_sort=radix (default): the AUC lane's onesweep radix passes; wbucket / bucket: the bucket
-  // sort (locbucket.hip: one wave / one block per bucket); merge: tile sorts + merge rounds.
-  // Same-box A/B: the bucket forms make a shorter lane but a slower
-  // step (120.5 / 121.1 vs 123.4 M ex/s): their high-priority, LDS-holding buckets wait for LDS
-  // the backward's blocks hold, and stall the backward's dispatch meanwhile
+  // auc_sort=radix (default): the AUC lane's onesweep radix passes; merge: tile sorts + merge
+  // rounds (round 4's bucket AUC, a shorter lane but a slower step, is gone: DESIGN.md (d))
   int auc_sort = 1;
   int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
   int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
@@ -92,22 +89,19 @@ struct Kw {
   // bucket sort — histogram, scatter into key-range buckets, one LDS sort per bucket
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
   int loc_bucket = 1;
-  // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_bucket skipped — 1 the LDS
+  // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_wbucket skipped — 1 the LDS
   // sort, 4 the outputs, 8 k_lb_scatter's row search; the Localizer's results are then wrong
   int lb_diag = 0;
-  int lb_wave = 1;  // lb_wave=1: the bucket Localizer sorts one bucket per wave (0: per block)
-  // lane_after_fwd=1: the fused step's Localizer lane starts after the previous step's forward
-  // (A/B of where the lane's traffic lands: beside the backward only)
-  int lane_after_fwd = 0;
   // auc_db=1: the fused step's AUC snapshot alternates between two buffers, so a forward waits
   // only for the AUC lane of two steps back (0: of the step before).  Same-box A/B: a tie at C3
   // (133.5 / 133.5 M ex/s) and C2 (186.6 / 186.4), the lane overlapping more of the backward
   // (0.44 -> 0.49 ms); at B = 10^4, where the one-block AUC (~94 us) outlasts the backward,
   // 58.6 / 61.6 -> 68.0 / 68.8.  2 (the default): double-buffered for B <= kAucBlockMax only
   int auc_db = 2;
-  // lb_keyfirst=1: its wave sort passes over the key bits only, then sorts each run of equal keys
-  // by row / position in a lane (A/B: a tie at C3, C2 slower; 0, the default: full LSD passes)
-  int lb_keyfirst = 0;
+  // auc_lane=after: the AUC lane starts after the step's backward (beside the next step's
+  // forward) instead of beside the backward, on a double-buffered snapshot; auc_lane=bwd: beside
+  // the backward
+  int auc_after = 0;
   // lb_gather: valued batches sort (key | position) items alone, the row and the value gathered
   // by position at the outputs (1; A/B at C2: 126 -> 161 M ex/s) or, in the fused step, read by
   // position in the backward itself (2, the default: no gather launch on the Localizer lane;
@@ -119,7 +113,6 @@ struct Kw {
   int lb_tiles = 128;
   int lb_hnt = 0;  // lb_hnt=256|512|1024: its histogram / scatter blocks' threads (0: auto,
                    // 512 for valued batches, 1024 for binary ones)
-  int lb_xcd = 0;     // lb_xcd=1: consecutive tiles on one XCD (measured: more scatter writes)
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
@@ -142,20 +135,9 @@ struct Kw {
   // same-box A/B: C5 63.5 -> 65.7 M ex/s, forward 0.30 -> 0.23 ms; C4 shard a tie); 4: one
   int fwd_cpl = 8;
   int bwd_cpl_from = 64;  // bwd_cpl_from=<V_dim>: the least V_dim (multiple of 8) bwd_cpl=8 takes
-  // loc_pos=1: valued batches sort packed (key | position) items, the write pass gathering each
-  // position's row (bit-identical; A/B: C2 137.4 -> 131.2 M ex/s, so off by default)
-  int loc_pos = 0;
   // loc_xpay=0: valued 16-byte items carry the position and the write pass gathers the value
   // (A/B; 1: the value's bits ride in the payload, read by the transform in input order)
   int loc_xpay = 1;
-  // sort_hint=1: the Localizer sort's passes beyond the previous sort's active count on a
-  // 64-block looping grid (sort.hip kSortHint; bit-identical).  A/B: C3 lane 0.83 -> 0.63 ms but
-  // the backward 0.50 -> 0.55, 125.8 -> 124.4 M ex/s; C2 a tie — so off by default
-  int sort_hint = 0;
-  // lane_cus=<n>: the Localizer and AUC lanes on n CUs only (a CU-masked stream; lane_cu_stride=1
-  // every (CUs / n)-th CU, else the highest n); main_excl=1: the main stream on the other CUs
-  // (the context's own stream, kept by dfx_ctx_set_stream).  A/B of the lanes' interference.
-  int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;
   // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
   // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
   // auc_high: the AUC lane's short latency-bound chain at high priority, the Localizer lane at
@@ -223,13 +205,16 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
-    else if (k == "lb_wave") kw->lb_wave = atoi(cv) != 0;
-    else if (k == "lane_after_fwd") kw->lane_after_fwd = atoi(cv) != 0;
+    else if (k == "auc_lane") {
+      if (std::string(cv) != "after" && std::string(cv) != "bwd") {
+        set_error("auc_lane must be after or bwd");
+        return DFX_ERR_ARG;
+      }
+      kw->auc_after = std::string(cv) == "after";
+    }
     else if (k == "auc_db") kw->auc_db = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
-    else if (k == "lb_keyfirst") kw->lb_keyfirst = atoi(cv) != 0;
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
-    else if (k == "lb_xcd") kw->lb_xcd = atoi(cv) != 0;
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
     else if (k == "fwd_pf") kw->fwd_pf = atoi(cv) != 0;
@@ -258,12 +243,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
         return DFX_ERR_ARG;
       }
     }
-    else if (k == "loc_pos") kw->loc_pos = atoi(cv) != 0;
     else if (k == "loc_xpay") kw->loc_xpay = atoi(cv) != 0;
-    else if (k == "sort_hint") kw->sort_hint = atoi(cv) != 0;
-    else if (k == "lane_cus") kw->lane_cus = atoi(cv);
-    else if (k == "lane_cu_stride") kw->lane_cu_stride = atoi(cv);
-    else if (k == "main_excl") kw->main_excl = atoi(cv);
     else if (k == "nt") {
       kw->nt = atoi(cv);
       if (kw->nt < 0 || kw->nt > 15) {
@@ -294,11 +274,9 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else { set_error("unknown slot_layout: " + v + " (auto|split|fat)"); return DFX_ERR_ARG; }
     }
     else if (k == "auc_sort") {
-      if (v == "wbucket") kw->auc_sort = 3;
-      else if (v == "bucket") kw->auc_sort = 2;
-      else if (v == "radix") kw->auc_sort = 1;
+      if (v == "radix") kw->auc_sort = 1;
       else if (v == "merge") kw->auc_sort = 0;
-      else { set_error("unknown auc_sort: " + v + " (wbucket|bucket|radix|merge)"); return DFX_ERR_ARG; }
+      else { set_error("unknown auc_sort: " + v + " (radix|merge)"); return DFX_ERR_ARG; }
     }
     else if (k == "push_agg") {
       if (v == "sum") kw->dist_sum = 1;
@@ -338,10 +316,8 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.rowtmp2, &w.lbcnt, &w.lbq};
+                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.lbcnt, &w.lbq};
   for (DevBuf* b : bufs) b->release();
-  if (w.os_hint) (void)hipHostFree(w.os_hint);
-  w.os_hint = nullptr;
   if (w.lb_hint) (void)hipHostFree(w.lb_hint);
   w.lb_hint = nullptr;
 }
@@ -361,31 +337,11 @@ int pipeline_init(Context* c) {
   // Localizer lane at the lowest priority whatever the context stream's
   int main_prio = 0;
   if (hipStreamGetPriority(c->stream, &main_prio) != hipSuccess) main_prio = 0;
-  if (c->lane_cus > 0) {
-    hipDeviceProp_t prop;
-    DFX_HIP(hipGetDeviceProperties(&prop, c->device));
-    const int ncu = prop.multiProcessorCount, n = c->lane_cus < ncu ? c->lane_cus : ncu;
-    std::vector<uint32_t> lane((ncu + 31) / 32, 0u), rest((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) {
-      const bool on = c->lane_cu_stride ? (i % (ncu / n) == 0 && i / (ncu / n) < n)
-                                        : i >= ncu - n;
-      (on ? lane : rest)[i / 32] |= 1u << (i % 32);
-    }
-    DFX_HIP(hipExtStreamCreateWithCUMask(&c->loc_stream, (uint32_t)lane.size(), lane.data()));
-    DFX_HIP(hipExtStreamCreateWithCUMask(&c->aux_stream, (uint32_t)lane.size(), lane.data()));
-    if (c->main_excl) {
-      hipStream_t m = nullptr;
-      DFX_HIP(hipExtStreamCreateWithCUMask(&m, (uint32_t)rest.size(), rest.data()));
-      c->masked_main = m;
-      c->stream = m;
-    }
-  } else {
-    DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
-                                        (c->lane_prio & 1) ? hi
-                                        : (c->lane_prio & 4) ? lo : main_prio));
-    DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
-                                        (c->lane_prio & 2) ? hi : 0));
-  }
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
+                                      (c->lane_prio & 1) ? hi
+                                      : (c->lane_prio & 4) ? lo : main_prio));
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
+                                      (c->lane_prio & 2) ? hi : 0));
   c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
@@ -452,12 +408,7 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->bwd_cpl = kw.bwd_cpl;
   c->bwd_cpl_from = kw.bwd_cpl_from;
   c->fwd_cpl = kw.fwd_cpl;
-  c->loc_pos_payload = kw.loc_pos;
   c->loc_x_payload = kw.loc_xpay;
-  c->sort_hint = kw.sort_hint;
-  c->lane_cus = kw.lane_cus;
-  c->lane_cu_stride = kw.lane_cu_stride;
-  c->main_excl = kw.main_excl;
   c->fwd_lanes = kw.fwd_lanes;
   c->fwd_ids = kw.fwd_ids;
   c->fwd_pf = kw.fwd_pf;
@@ -468,11 +419,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_diag = kw.lb_diag;
   c->lb_tiles = kw.lb_tiles;
   c->lb_hnt = kw.lb_hnt;
-  c->lb_xcd = kw.lb_xcd;
-  c->lb_wave = kw.lb_wave;
-  c->lane_after_fwd = kw.lane_after_fwd;
   c->auc_db = kw.auc_db;
-  c->lb_keyfirst = kw.lb_keyfirst;
+  c->auc_after = kw.auc_after;
   c->lb_gather = kw.lb_gather;
   c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;
@@ -553,10 +501,6 @@ int dfx_ctx_destroy(dfx_ctx* ctx) {
   if (c->zpad) (void)hipFree(c->zpad);
   if (c->ds) (void)hipFree(c->ds);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-  if (c->masked_main) {
-    (void)hipStreamSynchronize(c->masked_main);
-    (void)hipStreamDestroy(c->masked_main);
-  }
   delete ctx;
   return DFX_OK;
 }
@@ -565,7 +509,7 @@ int dfx_ctx_set_stream(dfx_ctx* ctx, void* hip_stream) {
   DFX_CHECK_ARG(ctx, "null ctx");
   // NULL is HIP's null (legacy default) stream, which is also torch's default stream
   // (kwarg main_excl keeps its CU-masked main stream)
-  ctx->c.stream = ctx->c.masked_main ? ctx->c.masked_main : static_cast<hipStream_t>(hip_stream);
+  ctx->c.stream = static_cast<hipStream_t>(hip_stream);
   return DFX_OK;
 }
 

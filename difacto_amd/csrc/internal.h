@@ -107,7 +107,6 @@ struct Workspace {
   DevBuf ivstat;    // the one-launch InitV's look-back words (one per tile, tagged)
   DevBuf live;      // (diagnostic) the fused backward's per-block live-V counts
   DevBuf vlist;     // the two-pass backward's listed keys {segment, V row, XXp, 0} + a counter
-  DevBuf rowtmp2;   // the Localizer's row of each position (valued data, position payloads)
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // the bucket Localizer (locbucket.hip): per (tile, bucket) counts / prefixes, per bucket its
   // total and start; per item its row / position when the items are not packed (and scratch)
@@ -119,10 +118,6 @@ struct Workspace {
   // look-back words [tiles][256] (u64)
   DevBuf os;
   int64_t os_tiles = 0;
-  // per item type (u64/u32, u64/u64, u32/u32) the active pass count of the last sort's plan,
-  // written by the device into pinned memory (kSortHint)
-  unsigned int* os_hint = nullptr;
-  int os_hint_reserve();
   // grows the radix sort's counters / look-back words; fresh ones are zeroed on st, the
   // stream whose sorts use them (stream order, no host wait)
   int os_reserve(int64_t ntiles, hipStream_t st);
@@ -232,25 +227,18 @@ struct Context {
   int bwd_two_pass = 1;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int bwd_cpl = 8;        // kwarg bwd_cpl: coordinates per lane of the fused backward, d >= 64
   int bwd_cpl_from = 64;  // kwarg bwd_cpl_from: the least V_dim bwd_cpl = 8 applies to
-  int loc_pos_payload = 0;  // kwarg loc_pos: valued data sorts packed (key | position) items
   int loc_x_payload = 1;    // kwarg loc_xpay: valued data carries x, not the position
-  int sort_hint = 0;        // kwarg sort_hint: the Localizer sort's kSortHint
-  int lane_cus = 0, lane_cu_stride = 0, main_excl = 0;  // kwargs (ctx.hip)
-  hipStream_t masked_main = nullptr;  // main_excl: the CU-masked main stream (owned)
   int fwd_lanes = 0;      // kwarg fwd_lanes
   int fwd_ids = 1;        // kwarg fwd_ids
   int fwd_pf = 1;         // kwarg fwd_pf
   int fwd_tile = 0;       // kwarg fwd_tile (fm.hip k_fm_fwd_tile)
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
-  int lane_after_fwd = 0;  // kwarg lane_after_fwd (step.hip)
   int auc_db = 2;          // kwarg auc_db (step.hip): double-buffered AUC snapshot (2: B <= 12288)
-  int lb_wave = 1;        // kwarg lb_wave: one bucket per wave (locbucket.hip k_lb_wbucket)
-  int lb_keyfirst = 0;    // kwarg lb_keyfirst (locbucket.hip lb_wave_sort)
+  int auc_after = 0;       // kwarg auc_lane=after (step.hip): the AUC lane after the backward
   int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
   int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_hnt = 0;         // kwarg lb_hnt: the bucket Localizer's histogram / scatter block (0 auto)
-  int lb_xcd = 0;         // kwarg lb_xcd: its tiles XCD-contiguous (A/B: more write traffic)
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
@@ -336,8 +324,6 @@ constexpr int kSortMetaPack = 25;
 constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
 // flags |= kSortNT: the scatter passes load and store their items with the streaming policy
 constexpr int kSortNT = 8;
-// flags |= kSortHint: passes beyond the previous sort's active count run on a small looping grid
-constexpr int kSortHint = 16;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
 // the key and the row of a packed item (and_mask: AND of all keys, their constant bits)
 __device__ inline void sort_unpack(const unsigned* meta, uint64_t and_mask, uint64_t w,
@@ -489,10 +475,6 @@ int auc_run(const Lane& L, int64_t B, const float* label, const float* pred, dou
 int auc_snapshot(const Lane& L, hipStream_t st, int64_t B, const float* label,
                  const float* pred);
 int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, int mode);
-// the bucket sort's AUC*n of a snapshot (locbucket.hip); *used = false when the workspace's
-// hint sent it to the radix sort (nothing enqueued)
-int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
-               double* out_dev, bool accumulate, bool wave, bool* used);
 int evaluate_run(Context* c, int64_t B, const float* label, const float* pred, double* out_dev);
 
 }  // namespace dfx

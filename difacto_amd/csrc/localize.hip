@@ -35,9 +35,6 @@ struct TransformArgs {
   DevState* ds;     // the lane's state: OR / AND of the keys
   int keys_ready;   // index holds the final keys (no ReverseBytes / max_index)
   int nt;           // streaming policy for the ids read and the items written (kwarg nt & 1)
-  // valued data, narrow payload: pay32 carries the position (the value gather needs it) and
-  // row_of[pos] the row
-  uint32_t* row_of;
   // valued data, 8-byte payload, no col: the payload's low word is the value's bits (read here,
   // coalesced) instead of the position, so the write pass gathers nothing
   const float* value;
@@ -81,10 +78,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_transform(TransformArgs a) {
       if (offs[mid] <= j) lo = mid; else hi = mid;
     }
     stnt(a.keys + j, k, a.nt != 0);
-    if (a.pay32 && a.row_of) {
-      stnt(a.pay32 + j, (uint32_t)j, a.nt != 0);
-      stnt(a.row_of + j, (uint32_t)(r0 + lo), a.nt != 0);
-    } else if (a.pay32)
+    if (a.pay32)
       stnt(a.pay32 + j, (uint32_t)(r0 + lo), a.nt != 0);
     else {
       const uint32_t lo32 = a.value ? __float_as_uint(ldnt(a.value + j, a.nt != 0)) : (uint32_t)j;
@@ -140,8 +134,6 @@ struct LocWriteArgs {
   const float* value;
   uint32_t* occ_row;
   float* occ_x;
-  // narrow payload holding positions (valued data): occ_row = row_of[pos], occ_x = value[pos]
-  const uint32_t* row_of;
   int x_in_pay;  // the 8-byte payload's low word is the value's bits (TransformArgs::value)
 };
 
@@ -269,12 +261,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
           const uint32_t q = packed ? (uint32_t)(K[idx] & ((1ull << ((meta[kSortMetaPack] >> 16) &
                                                                       0xFFu)) - 1))
                                     : Q[idx];
-          if (a.row_of) {  // q is the position
-            a.occ_row[idx] = a.row_of[q];
-            if (a.occ_x) a.occ_x[idx] = a.value[q];
-          } else {
-            a.occ_row[idx] = q;
-          }
+          a.occ_row[idx] = q;
         } else {
           const uint64_t p = P[idx];
           a.occ_row[idx] = (uint32_t)(p >> 32);
@@ -406,21 +393,14 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   // nothing but the row travels with a key when there is no col to scatter and no value to
   // gather (the fused step on binary data): a 4-byte payload, 12 instead of 16 bytes per item
   // and sort pass
-  // valued data without col (the fused step, the split owner): the 4-byte payload is the
-  // position (the write pass gathers the value and the row of each occurrence by it), so the
-  // items pack as on binary data instead of sorting 16-byte (key, {pos, row}) pairs
-  const bool narrow_pos = !o.col && o.value && o.occ_row && o.occ_x && c->loc_pos_payload;
-  const bool narrow = (!o.col && !o.value && o.occ_row) || narrow_pos;
+  const bool narrow = !o.col && !o.value && o.occ_row;
   uint32_t* q0 = narrow ? ws.vals0.as<uint32_t>() : nullptr;
   uint32_t* q1 = narrow ? ws.vals1.as<uint32_t>() : nullptr;
-  if (narrow_pos) DFX_TRY(ws.rowtmp2.ensure(nnz * 4));
-  uint32_t* row_of = narrow_pos ? ws.rowtmp2.as<uint32_t>() : nullptr;
   TransformArgs t{};
   t.B = B; t.offset = offset; t.index = index; t.max_index = max_index;
   t.keys = k0; t.pay = p0; t.pay32 = q0; t.parts = ws.os_parts(); t.ds = ds;
   t.keys_ready = o.keys_ready ? 1 : 0;
   t.nt = (c->nt_mask & kNtLane) ? 1 : 0;
-  t.row_of = row_of;
   // valued occurrences without col (the fused step, the split owner): the value rides in the
   // payload in place of the position (kwarg loc_xpay=0: the position, and a gather)
   const bool x_pay = !narrow && !o.col && o.value && o.occ_row && o.occ_x && c->loc_x_payload;
@@ -431,7 +411,7 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   if (narrow) {
     // rows (positions, valued data) travel packed beside the key bits that vary, when they fit
     // (sort.hip)
-    const int64_t qmax = narrow_pos ? nnz - 1 : B - 1;
+    const int64_t qmax = B - 1;
     int rb8 = 8;
     while (rb8 < 32 && qmax >> rb8) rb8 += 8;
     DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, k0, q0, k1, q1, nnz, 0, 64, &ds->or_mask,
@@ -440,16 +420,14 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0) |
-                                                      (c->nt_mask & kNtLane ? kSortNT : 0) |
-                                                      (c->sort_hint ? kSortHint : 0))));
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
                                                       kSortItems(c->sort_items) |
                                                       kSortLookback(c->sort_lookback) |
-                                                      (c->nt_mask & kNtLane ? kSortNT : 0) |
-                                                      (c->sort_hint ? kSortHint : 0))));
+                                                      (c->nt_mask & kNtLane ? kSortNT : 0))));
   }
   // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
   // k_loc_write with look-back
@@ -477,7 +455,6 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
   a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;
-  a.row_of = row_of;
   a.x_in_pay = x_pay ? 1 : 0;
   hipLaunchKernelGGL(k_loc_write, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, a);
   if (o.cnt) {

@@ -23,7 +23,7 @@
 //                 moved) such buckets sorted in place through global memory by a few looping
 //                 blocks, stable 8-bit LSD passes — slower, the same result; the workspace's hint
 //                 then sends the next batches to the radix Localizer and retries every kLbRetry
-//   k_lb_bucket   one block per bucket: the bucket sorted in LDS — LSD radix over the digits
+//   k_lb_wbucket  one wave per bucket: the bucket sorted in LDS — LSD radix over the digits
 //                 that vary inside it, on the whole item: (key, row) resp. (key, position) is a
 //                 total order and equal items are the same occurrence data, so the scatter's
 //                 order inside a bucket never shows — then its heads (CountUniqIndex's run-length
@@ -64,7 +64,7 @@ struct LbArgs {
   uint32_t* tilecnt;     // [ntiles][nbk]: counts, then exclusive prefixes over the tiles
   uint32_t* totals;      // [nbk]
   uint32_t* bstart;      // [nbk + 1]
-  uint32_t* bheads;      // [nbk]: unique keys per bucket (k_lb_bucket)
+  uint32_t* bheads;      // [nbk]: unique keys per bucket (k_lb_wbucket)
   uint32_t* brank;       // [nbk]: the bucket's first rank (k_lb_bscan)
   uint64_t* kbuf;        // items
   uint32_t* qbuf;        // rows / positions of unpacked items
@@ -81,8 +81,6 @@ struct LbArgs {
   float* occ_x;
   unsigned int* hint;    // pinned: Workspace::lb_hint
   int diag;              // Context::lb_diag (measurement only)
-  int keyfirst;          // Context::lb_keyfirst: the wave sort's key-first form (lb_wave_sort)
-  int xcd;               // Context::lb_xcd: consecutive tiles on one XCD (lb_tile)
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -179,18 +177,6 @@ constexpr int kLbUnr = 8;  // ids in flight per thread
 // the histogram and scatter kernels' blocks: 16 waves on a tile by default, for the loads in
 // flight (kwarg lb_hnt = 256 | 512 | 1024)
 
-// The tile a histogram / scatter block takes.  Blocks b and b + 8 share an XCD (its L2); with
-// xcd set, XCD x's blocks take a contiguous range of tiles, so the scatter's runs of one bucket
-// from consecutive tiles — adjacent in the bucket's region — are written through one L2 and
-// leave it as whole lines rather than as partial lines from eight L2s.  The map is a bijection
-// on [0, gridDim.x) whatever the grid; which XCD is which does not matter (for speed only).
-__device__ inline int64_t lb_tile(int xcd) {
-  const uint32_t b = blockIdx.x, T = gridDim.x;
-  if (!xcd) return b;
-  const uint32_t q = T >> 3, r = T & 7u, x = b & 7u;
-  return (int64_t)x * q + (x < r ? x : r) + (b >> 3);
-}
-
 template <int HNT>
 __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
@@ -200,7 +186,7 @@ __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   const LbMap m = lb_map(a.ds, a.wbits);
   const int t = threadIdx.x;
   for (uint32_t d = t; d < m.nbk; d += kLbHNT) hist[d] = 0;
-  const int64_t tile = lb_tile(a.xcd);
+  const int64_t tile = blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int64_t r1 = r0 + a.rt < a.B ? r0 + a.rt : a.B;
   const uint64_t j0 = a.offset[r0], j1 = a.offset[r1];
@@ -304,7 +290,7 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t* cur = reinterpret_cast<uint32_t*>(lb_dyn64);  // per bucket: this tile's next slot
   uint64_t* offs = lb_dyn64 + (m.nbk + 1u) / 2;
   const int t = threadIdx.x;
-  const int64_t tile = lb_tile(a.xcd);
+  const int64_t tile = blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
   // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
@@ -618,10 +604,10 @@ __device__ inline void lb_lds_sort(uint64_t (&k)[kLbRadixIT], uint32_t (&q)[kLbR
 
 // Buckets the LDS sort cannot take — beyond kLbCap items (skewed keys, or a key range that
 // moved), or unpacked items while the launch expected packed ones (q_lds = 0) — sorted in place by
-// a few looping blocks, through global memory, before k_lb_bucket reads them: stable 8-bit LSD
+// a few looping blocks, through global memory, before k_lb_wbucket reads them: stable 8-bit LSD
 // passes over the digits that vary inside the bucket, q's first (the less significant part of an
 // unpacked item), then the key's; the result copied back when it ends in the scratch buffers.
-// Kept out of k_lb_bucket, whose registers would otherwise be sized for it.
+// Kept out of k_lb_wbucket, whose registers would otherwise be sized for it.
 __device__ inline bool lb_needs_global(int64_t n, bool packed, int q_lds) {
   return n > kLbCap || (!packed && !q_lds);
 }
@@ -720,121 +706,7 @@ __global__ __launch_bounds__(kLbNT) void k_lb_big(LbArgs a, int q_lds) {
   }
 }
 
-template <bool Q, bool S>
-__global__ __launch_bounds__(kLbNT) void k_lb_bucket(LbArgs a) {
-  __shared__ uint64_t sk[kLbCap];
-  __shared__ uint32_t sq[Q ? kLbCap : 1];
-  __shared__ uint64_t ss[S ? kLbCap : 1];
-  __shared__ uint32_t wcnt[kLbWaves][256];
-  __shared__ unsigned long long s_red[4][kLbWaves];
-  __shared__ uint32_t lds[kLbWaves + 1];
-  DevState* ds = a.ds;
-  const int t = threadIdx.x;
-  const uint32_t b = blockIdx.x;
-  const int64_t start = a.bstart[b];
-  const int n = (int)((int64_t)a.bstart[b + 1] - start);
-  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
-  const LbPack p = lb_pack(ds, qmax);
-  const bool hasq = !p.packed;
-  // sorted in LDS here, or already in place (k_lb_big)
-  const bool fast = !lb_needs_global(n, p.packed, Q ? 1 : 0);
-  const uint64_t* gk = a.kbuf + start;
-  const uint32_t* gq = a.qbuf + start;
-  const uint64_t* gs = a.sbuf + start;
-  if (fast) {
-    uint64_t kr[kLbRadixIT], sr[kLbRadixIT];
-    uint32_t qr[kLbRadixIT];
-    const int wb = (t / kWave) * kWave * kLbRadixIT + lane_id();
-#pragma unroll
-    for (int c = 0; c < kLbRadixIT; ++c) {  // every load in flight at once
-      const int i = wb + c * kWave;
-      kr[c] = i < n ? ldnt(gk + i, a.nt != 0) : 0ull;
-      qr[c] = (Q && hasq && i < n) ? gq[i] : 0u;
-      sr[c] = (S && i < n) ? gs[i] : 0ull;
-    }
-    if (a.diag & 1) {  // (measurement only) no sort: the items as they came
-#pragma unroll
-      for (int c = 0; c < kLbRadixIT; ++c) {
-        const int i = wb + c * kWave;
-        if (i < n) {
-          sk[i] = kr[c];
-          if (Q && hasq) sq[i] = qr[c];
-          if (S) ss[i] = sr[c];
-        }
-      }
-      __syncthreads();
-    } else {
-      lb_lds_sort<Q, S>(kr, qr, sr, n, hasq, sk, sq, ss, wcnt, lds, s_red);
-    }
-  }
-  // ---- per occurrence its row (and value); per head (an item whose key differs from the one
-  // before it, the bucket's first always) its key and segment start at the bucket's own offset
-  // in the scratch lists (k_lb_out moves them to their ranks); a segment longer than kChunkOcc
-  // raises the chunk plan's gate
-  const uint64_t qmask = p.rb ? (~0ull >> (64 - p.rb)) : 0ull;
-  uint32_t* tseg = a.qscr + start;
-  uint64_t* tkey = a.kscr + start;
-  uint32_t run = 0;
-  bool longseg = false;
-  // instantiated for the LDS and the global-memory copy apart (no flat loads)
-  auto heads = [&](const uint64_t* K, const uint32_t* Qs, const uint64_t* Ss) {
-  auto item = [&](int i) -> uint64_t { return K[i]; };
-  for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
-    const int ib = c0 + t * kLbIT;
-    uint32_t h[kLbIT], s = 0;
-#pragma unroll
-    for (int j = 0; j < kLbIT; ++j) {
-      const int i = ib + j;
-      h[j] = 0u;
-      if (i < n) {
-        const uint64_t kb = lb_keybits(p, item(i));
-        h[j] = (i == 0 || kb != lb_keybits(p, item(i - 1))) ? 1u : 0u;
-        if (i >= kChunkOcc && kb == lb_keybits(p, item(i - kChunkOcc))) longseg = true;
-      }
-      s += h[j];
-    }
-    uint32_t ctot;
-    uint32_t incl = block_excl_scan<kLbNT>(s, lds, &ctot) + run;
-    if (a.diag & 4) {
-      run += ctot;
-      continue;
-    }
-#pragma unroll
-    for (int j = 0; j < kLbIT; ++j) {
-      const int i = ib + j;
-      if (i < n) {
-        incl += h[j];
-        const uint64_t it = item(i);
-        if (h[j]) {
-          tkey[incl - 1] = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
-          tseg[incl - 1] = (uint32_t)(start + i);
-        }
-        uint32_t row;
-        if (S) {
-          const uint64_t sv = Ss[i];
-          row = (uint32_t)(sv >> 32);
-          if (a.occ_x) a.occ_x[start + i] = __uint_as_float((uint32_t)sv);
-        } else if (a.rowof) {  // valued: the position now, its row and value by k_lb_gather
-          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
-        } else {
-          row = p.packed ? (uint32_t)(it & qmask) : Qs[i];
-        }
-        a.occ_row[start + i] = row;
-      }
-    }
-    run += ctot;
-  }
-  };
-  if (fast) heads(sk, sq, ss);
-  else heads(gk, gq, gs);
-  if (__syncthreads_or(longseg) && t == 0 &&
-      __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    atomicOr(&ds->n_init, 1u);
-  if (t == 0) a.bheads[b] = run;
-}
-
-// ---- one wave per bucket (kwarg lb_wave=1, the default): k_lb_bucket's sort and outputs with no
-// block barrier.  The wave holds up to kLbCap items, kLbWIT per lane (lane l's slot c is the
+// ---- the per-bucket sort and outputs, one wave per bucket, no block barrier.  The wave holds up to kLbCap items, kLbWIT per lane (lane l's slot c is the
 // bucket's position c * 64 + l), ranks each pass's digits with ballots against its own 256
 // counters, scans them across its lanes, scatters through LDS and reads back; the heads' ranks
 // are a ballot prefix per slot.  A 64-thread block per bucket: ~17 KiB of LDS and one wave, so
@@ -844,20 +716,11 @@ constexpr int kLbWIT = kLbCap / kWave;  // 32
 // a bucket's n <= kLbCap items (+ rows / positions, side payloads) sorted by one wave into LDS:
 // LSD radix over the digits that vary inside the bucket, q's first when the items are not
 // packed; positions >= n of the last slot hold padding ~0.
-//
-// Key first (packed items, kf): the order wanted is the item's, i.e. (key bits above bit rb,
-// then the row / position below).  Inside a bucket most keys occur once or twice, so only the
-// key bits are sorted by passes (2 of them at C3, where the full item takes 4); then each run of
-// equal keys, in the scatter's order so far, is sorted whole by the lane at its head — runs of
-// up to kLbRun items in registers.  A bucket holding a longer run (hot or few keys) is sorted
-// again from its items in global memory by the full passes.  Either way the LDS holds the
-// bucket in item order.
-constexpr int kLbRun = 8;
 
 template <bool Q, bool S>
 __device__ __attribute__((always_inline)) inline void lb_wave_sort(
     const uint64_t* gk, const uint32_t* gq, const uint64_t* gs, int n, bool hasq, int ntp,
-    int diag, int rb, bool keyfirst, uint64_t* sk, uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
+    int diag, uint64_t* sk, uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
   const int l = threadIdx.x;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
   // the last slot's lanes past n hold padding ~0, which sorts after every item (packed items
@@ -892,17 +755,10 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(
     qand = lb_wave_and(qand);
   }
   const unsigned long long kvary = kor ^ kand, qvary = (Q && hasq) ? (qor ^ qand) : 0ull;
-  // key first only for packed items whose key bits vary (one key: a single run)
-  const bool kf = keyfirst && !hasq && !(diag & 1) && rb < 64 && (kvary >> rb) != 0;
-  // the passes of one schedule (wave-uniform): KEYS — the key's digits from bit rb up; else
-  // q's 4 digits, then the item's 8 (an item's low rb bits are its row / position)
-  auto passes = [&](bool keys_only) {
+  // the passes (wave-uniform): q's 4 digits, then the item's 8 (an item's low rb bits are its
+  // row / position when the items are packed)
+  auto passes = [&]() {
     auto pass_at = [&](int pass, bool* on_q, int* shift) {
-      if (keys_only) {
-        *on_q = false;
-        *shift = rb + 8 * pass;
-        return *shift < 64;
-      }
       *on_q = pass < 4;
       *shift = 8 * (*on_q ? pass : pass - 4);
       return true;
@@ -1002,74 +858,7 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(
     }
     __builtin_amdgcn_wave_barrier();
   };
-  passes(kf);
-  if (!kf) return;
-  // key first: each run of equal keys sorted whole by the lane at its head (only key bits are
-  // compared while runs are found, and a run's own reordering never changes them)
-  bool longrun = false;
-  for (int c = 0; c < nc; ++c) {
-    const int i = c * kWave + l;
-    if (i >= n) continue;
-    const uint64_t kb = sk[i] >> rb;
-    if (i > 0 && (sk[i - 1] >> rb) == kb) continue;  // not a head
-    int len = 1;
-    while (len <= kLbRun && i + len < n && (sk[i + len] >> rb) == kb) ++len;
-    if (len > kLbRun) {
-      longrun = true;
-      continue;
-    }
-    if (len == 1) continue;
-    if (len == 2) {  // the common case: one compare-exchange
-      const uint64_t x0 = sk[i], x1 = sk[i + 1];
-      if (x0 > x1) {
-        sk[i] = x1;
-        sk[i + 1] = x0;
-        if (S) {
-          const uint64_t y0 = ss[i], y1 = ss[i + 1];
-          ss[i] = y1;
-          ss[i + 1] = y0;
-        }
-      }
-      continue;
-    }
-    uint64_t v[kLbRun], w[kLbRun];
-#pragma unroll
-    for (int t = 0; t < kLbRun; ++t) {
-      v[t] = t < len ? sk[i + t] : ~0ull;
-      w[t] = (S && t < len) ? ss[i + t] : 0ull;
-    }
-#pragma unroll
-    for (int r = 0; r < kLbRun; ++r) {  // odd-even transposition: kLbRun rounds sort kLbRun
-#pragma unroll
-      for (int t = r & 1; t + 1 < kLbRun; t += 2) {
-        if (v[t] > v[t + 1]) {
-          const uint64_t x = v[t]; v[t] = v[t + 1]; v[t + 1] = x;
-          if (S) { const uint64_t y = w[t]; w[t] = w[t + 1]; w[t + 1] = y; }
-        }
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < kLbRun; ++t) {
-      if (t < len) {
-        sk[i + t] = v[t];
-        if (S) ss[i + t] = w[t];
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (!__ballot(longrun)) return;
-  // a run too long for one lane: the full passes (row / position digits, then the key's) from
-  // the key-sorted order in LDS — LSD passes do not depend on the order they start from
-#pragma unroll
-  for (int c = 0; c < kLbWIT; ++c) {
-    if (c < nc) {
-      const int i = c * kWave + l;
-      k[c] = sk[i];
-      if (S) sv[c] = ss[i];
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  passes(false);
+  passes();
 }
 
 template <bool Q, bool S>
@@ -1093,7 +882,7 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   const uint64_t* gs = a.sbuf + start;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
   if (fast)
-    lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, p.rb, a.keyfirst != 0, sk, sq, ss, cnt);
+    lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, sk, sq, ss, cnt);
   // ---- per occurrence its row (and value); per head its key and segment start at the
   // bucket's own offset in the scratch lists (k_lb_out moves them to their ranks); a segment
   // longer than kChunkOcc raises the chunk plan's gate.  Instantiated for the LDS and for the
@@ -1271,8 +1060,6 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
   a.diag = c->lb_diag;
-  a.keyfirst = c->lb_keyfirst;
-  a.xcd = c->lb_xcd;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
 #define DFX_LB_HIST(NT) \
   hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT), nbk * sizeof(uint32_t), \
@@ -1307,21 +1094,13 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     hipLaunchKernelGGL(k_lb_big<true>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   else
     hipLaunchKernelGGL(k_lb_big<false>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
-  if (c->lb_wave) {  // one wave per bucket
-    const dim3 wb(kWave);
-    if (carry) {
-      if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, true>), bg, wb, 0, L.stream, a);
-      else hipLaunchKernelGGL((k_lb_wbucket<false, true>), bg, wb, 0, L.stream, a);
-    } else {
-      if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, false>), bg, wb, 0, L.stream, a);
-      else hipLaunchKernelGGL((k_lb_wbucket<false, false>), bg, wb, 0, L.stream, a);
-    }
-  } else if (carry) {
-    if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, true>), bg, bb, 0, L.stream, a);
-    else hipLaunchKernelGGL((k_lb_bucket<false, true>), bg, bb, 0, L.stream, a);
+  const dim3 wb(kWave);  // one wave per bucket
+  if (carry) {
+    if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, true>), bg, wb, 0, L.stream, a);
+    else hipLaunchKernelGGL((k_lb_wbucket<false, true>), bg, wb, 0, L.stream, a);
   } else {
-    if (q_lds) hipLaunchKernelGGL((k_lb_bucket<true, false>), bg, bb, 0, L.stream, a);
-    else hipLaunchKernelGGL((k_lb_bucket<false, false>), bg, bb, 0, L.stream, a);
+    if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, false>), bg, wb, 0, L.stream, a);
+    else hipLaunchKernelGGL((k_lb_wbucket<false, false>), bg, wb, 0, L.stream, a);
   }
   // (lb_gather=2, the fused step) the backward reads {row, value} by position itself
   const bool defer = gather && c->lb_gather == 2 && o.rowof_out != nullptr;
@@ -1331,496 +1110,6 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
                        a);
   hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);
   hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
-  DFX_HIP(hipGetLastError());
-  *used = true;
-  return DFX_OK;
-}
-
-// ---- BinClassMetric::AUC (src/loss/bin_class_metric.h:35-57) by the same bucket sort -------
-// The snapshot's items (orderable pred << 32 | row << 1 | label) go to buckets by a monotone map
-// of the prediction's value, linear over the previous snapshot's range (k_ab_hist,
-// k_lb_colscan, k_ab_scatter); one block per bucket in bucket order sorts its items in LDS —
-// the row in the item makes (pred, row) a total order: the stable tie break of the radix AUC —
-// counts its positives, finds the positives of the buckets before it by decoupled look-back,
-// and adds, per negative, the positives ranked below it (k_ab_bucket).  The area is a sum of
-// integers, exact in double in any order; the last block to finish turns it into AUC * n
-// (k_auc_final's rules) and leaves the lane's state ready for the next snapshot.  Four
-// launches (+ k_ab_big for oversize buckets) where the radix lane takes ~10 latency-bound ones.
-constexpr int kAbTileItems = 4096;
-
-struct AbArgs {
-  int64_t B, ntiles;
-  const uint32_t* key;  // orderable pred (metric.hip k_auc_keys' form)
-  const uint32_t* lab;  // label > 0
-  int wbits;
-  uint32_t* tilecnt;
-  uint32_t* totals;
-  uint32_t* bstart;
-  uint64_t* kbuf;
-  uint64_t* kscr;
-  uint32_t* bpos;   // per bucket: its positives, negatives, and area within it
-  uint32_t* bneg;
-  double* barea;
-  DevState* ds;
-  double* out;
-  int accumulate;
-  unsigned int* hint;
-};
-
-__device__ inline float ab_value(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
-}
-
-// bucket(key): linear in the prediction's value over the previous snapshot's [kmin, kmax]
-// (clamped outside it: NaN and infinities sit at the ends of the key order), or the key's top
-// bits before any snapshot; monotone in the key either way
-struct AbMap {
-  uint32_t kmin, kmax, nbk;
-  int shift;
-  bool linear;
-  double vmin, scale;
-};
-__device__ inline AbMap ab_map(const DevState* ds, int wbits) {
-  AbMap m;
-  m.nbk = 1u << wbits;
-  m.shift = 32 - wbits;
-  m.linear = false;
-  m.kmin = ds->auc_pk_min;
-  m.kmax = ds->auc_pk_max;
-  if (ds->auc_pk_valid && m.kmax > m.kmin) {
-    const double lo = ab_value(m.kmin), hi = ab_value(m.kmax);
-    if (hi > lo && hi - lo < 1e300) {
-      m.linear = true;
-      m.vmin = lo;
-      m.scale = (double)m.nbk / (hi - lo);
-    }
-  }
-  return m;
-}
-__device__ inline uint32_t ab_bucket(uint32_t k, const AbMap& m) {
-  if (!m.linear) return k >> m.shift;
-  if (k <= m.kmin) return 0u;
-  if (k >= m.kmax) return m.nbk - 1u;
-  const double x = ((double)ab_value(k) - m.vmin) * m.scale;
-  const uint32_t b = x > 0.0 ? (uint32_t)x : 0u;
-  return b < m.nbk ? b : m.nbk - 1u;
-}
-
-__global__ __launch_bounds__(kLbNT) void k_ab_hist(AbArgs a) {
-  extern __shared__ uint32_t lb_dyn[];
-  uint32_t* hist = lb_dyn;
-  __shared__ uint32_t red[2][kLbWaves];
-  const AbMap m = ab_map(a.ds, a.wbits);
-  const int t = threadIdx.x;
-  for (uint32_t d = t; d < m.nbk; d += kLbNT) hist[d] = 0;
-  __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * kAbTileItems;
-  const int64_t i1 = i0 + kAbTileItems < a.B ? i0 + kAbTileItems : a.B;
-  uint32_t kmax = 0, kmin_inv = 0;
-  for (int64_t i = i0 + t; i < i1; i += kLbNT) {
-    const uint32_t k = a.key[i];
-    kmax = k > kmax ? k : kmax;
-    kmin_inv = ~k > kmin_inv ? ~k : kmin_inv;
-    atomicAdd(&hist[ab_bucket(k, m)], 1u);
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint32_t x = __shfl_xor(kmax, off, kWave), y = __shfl_xor(kmin_inv, off, kWave);
-    kmax = x > kmax ? x : kmax;
-    kmin_inv = y > kmin_inv ? y : kmin_inv;
-  }
-  if (lane_id() == 0) {
-    red[0][t / kWave] = kmax;
-    red[1][t / kWave] = kmin_inv;
-  }
-  __syncthreads();
-  uint32_t* dst = a.tilecnt + (size_t)blockIdx.x * m.nbk;
-  for (uint32_t d = t; d < m.nbk; d += kLbNT) dst[d] = hist[d];
-  if (t == 0) {
-    for (int w = 1; w < kLbWaves; ++w) {
-      kmax = red[0][w] > kmax ? red[0][w] : kmax;
-      kmin_inv = red[1][w] > kmin_inv ? red[1][w] : kmin_inv;
-    }
-    atomicMax(&a.ds->auc_kmax, kmax);
-    atomicMax(&a.ds->auc_kmin_inv, kmin_inv);
-  }
-}
-
-__global__ __launch_bounds__(kLbNT) void k_ab_scatter(AbArgs a) {
-  extern __shared__ uint32_t lb_dyn[];
-  __shared__ uint32_t lds[kLbWaves + 1];
-  const AbMap m = ab_map(a.ds, a.wbits);
-  uint32_t* cur = lb_dyn;
-  const int t = threadIdx.x;
-  const uint32_t per = (m.nbk + kLbNT - 1) / kLbNT;
-  uint32_t mine = 0, over = 0;
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t d = t * per + i;
-    if (d < m.nbk) {
-      const uint32_t c = a.totals[d];
-      mine += c;
-      over += c > (uint32_t)kLbCap ? 1u : 0u;
-    }
-  }
-  uint32_t total;
-  uint32_t ex = block_excl_scan<kLbNT>(mine, lds, &total);
-  const uint32_t* pre = a.tilecnt + (size_t)blockIdx.x * m.nbk;
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t d = t * per + i;
-    if (d < m.nbk) {
-      cur[d] = ex + pre[d];
-      if (blockIdx.x == 0) a.bstart[d] = ex;
-      ex += a.totals[d];
-    }
-  }
-  if (blockIdx.x == 0) {
-    uint32_t nover;
-    (void)block_excl_scan<kLbNT>(over, lds, &nover);
-    if (t == 0) {
-      a.bstart[m.nbk] = total;
-      a.hint[0] = nover;  // pinned host word, vector store
-    }
-  }
-  __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * kAbTileItems;
-  const int64_t i1 = i0 + kAbTileItems < a.B ? i0 + kAbTileItems : a.B;
-  for (int64_t i = i0 + t; i < i1; i += kLbNT) {
-    const uint32_t k = a.key[i];
-    const uint32_t pos = atomicAdd(&cur[ab_bucket(k, m)], 1u);
-    a.kbuf[pos] = ((uint64_t)k << 32) | ((uint64_t)i << 1) | (uint64_t)(a.lab[i] & 1u);
-  }
-}
-
-// AUC buckets beyond kLbCap (a skewed or shifted snapshot: all predictions equal at epoch 0)
-// sorted in place through global memory before k_ab_bucket (as k_lb_big)
-__global__ __launch_bounds__(kLbNT) void k_ab_big(AbArgs a) {
-  __shared__ uint32_t wcnt[kLbWaves][256];
-  __shared__ uint32_t base[256];
-  __shared__ uint32_t lds[kLbWaves + 1];
-  __shared__ unsigned long long s_red[2][kLbWaves];
-  __shared__ uint32_t s_list[kLbNT];
-  __shared__ uint32_t s_nlist;
-  const int t = threadIdx.x;
-  const uint32_t nbk = 1u << a.wbits;
-  uint32_t listed = 0;
-  for (uint32_t b0 = 0; b0 < nbk; b0 += kLbNT) {
-    const uint32_t bb = b0 + t;
-    const int64_t nb = bb < nbk ? (int64_t)a.bstart[bb + 1] - (int64_t)a.bstart[bb] : 0;
-    const uint32_t need = nb > kLbCap ? 1u : 0u;
-    uint32_t cnt;
-    const uint32_t ex = block_excl_scan<kLbNT>(need, lds, &cnt);
-    if (t == 0) s_nlist = 0;
-    __syncthreads();
-    if (need && (listed + ex) % gridDim.x == blockIdx.x) s_list[atomicAdd(&s_nlist, 1u)] = bb;
-    __syncthreads();
-    listed += cnt;
-    const uint32_t nl = s_nlist;
-    for (uint32_t li = 0; li < nl; ++li) {
-      const uint32_t b = s_list[li];
-      const int64_t start = a.bstart[b];
-      const int64_t n = (int64_t)a.bstart[b + 1] - start;
-      unsigned long long kor = 0, kand = ~0ull;
-      for (int64_t i = t; i < n; i += kLbNT) {
-        kor |= a.kbuf[start + i];
-        kand &= a.kbuf[start + i];
-      }
-      kor = lb_wave_or(kor);
-      kand = lb_wave_and(kand);
-      if (lane_id() == 0) {
-        s_red[0][t / kWave] = kor;
-        s_red[1][t / kWave] = kand;
-      }
-      __syncthreads();
-      for (int i = 0; i < kLbWaves; ++i) {
-        kor |= s_red[0][i];
-        kand &= s_red[1][i];
-      }
-      __syncthreads();
-      uint64_t* X = a.kbuf + start;
-      uint64_t* Y = a.kscr + start;
-      int np = 0;
-      for (int shift = 0; shift < 64; shift += 8) {
-        if ((((kor ^ kand) >> shift) & 255ull) == 0) continue;
-        lb_global_pass<false>(X, nullptr, nullptr, Y, nullptr, nullptr, n, false, shift, wcnt,
-                              base, lds);
-        uint64_t* tk = X;
-        X = Y;
-        Y = tk;
-        ++np;
-      }
-      if (np & 1)
-        for (int64_t i = t; i < n; i += kLbNT) Y[i] = X[i];
-      __syncthreads();
-    }
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(kLbNT) void k_ab_bucket(AbArgs a) {
-  __shared__ uint64_t sk[kLbCap];
-  __shared__ uint32_t wcnt[kLbWaves][256];
-  __shared__ unsigned long long s_red[4][kLbWaves];
-  __shared__ uint32_t lds[kLbWaves + 1];
-  __shared__ double s_area[kLbWaves];
-  __shared__ uint32_t s_neg[kLbWaves];
-  __shared__ uint32_t s_last;
-  DevState* ds = a.ds;
-  const int t = threadIdx.x;
-  const uint32_t b = blockIdx.x;
-  const uint32_t nbk = 1u << a.wbits;
-  const int64_t start = a.bstart[b];
-  const int n = (int)((int64_t)a.bstart[b + 1] - start);
-  const bool fast = n <= kLbCap;  // else sorted in place by k_ab_big
-  const uint64_t* gk = a.kbuf + start;
-  if (fast) {
-    uint64_t kr[kLbRadixIT], sr[kLbRadixIT];
-    uint32_t qr[kLbRadixIT];
-    const int wb = (t / kWave) * kWave * kLbRadixIT + lane_id();
-#pragma unroll
-    for (int c = 0; c < kLbRadixIT; ++c) {
-      const int i = wb + c * kWave;
-      kr[c] = i < n ? gk[i] : 0ull;
-      qr[c] = 0u;
-      sr[c] = 0ull;
-    }
-    lb_lds_sort<false, false>(kr, qr, sr, n, false, sk, nullptr, nullptr, wcnt, lds, s_red);
-  }
-  // within the bucket: every negative adds the positives ranked below it here (exact integers
-  // in double); the positives of the buckets before it are added by the last block
-  double area = 0;
-  uint32_t run = 0, nneg = 0;
-  auto count = [&](const uint64_t* K) {  // LDS or global instantiation (no flat loads)
-  auto item = [&](int i) -> uint64_t { return K[i]; };
-  for (int c0 = 0; c0 < n; c0 += kLbNT * kLbIT) {
-    const int ib = c0 + t * kLbIT;
-    uint32_t lb[kLbIT], s = 0;
-#pragma unroll
-    for (int j = 0; j < kLbIT; ++j) {
-      lb[j] = ib + j < n ? (uint32_t)(item(ib + j) & 1ull) : 2u;
-      s += lb[j] & 1u;
-    }
-    uint32_t ctot;
-    uint32_t cum = block_excl_scan<kLbNT>(s, lds, &ctot) + run;
-#pragma unroll
-    for (int j = 0; j < kLbIT; ++j) {
-      if (lb[j] == 1u) {
-        cum += 1;
-      } else if (lb[j] == 0u) {
-        area += (double)cum;
-        ++nneg;
-      }
-    }
-    run += ctot;
-  }
-  };
-  if (fast) count(sk);
-  else count(gk);
-  for (int off = 32; off > 0; off >>= 1) {
-    area += __shfl_xor(area, off, kWave);
-    nneg += __shfl_xor(nneg, off, kWave);
-  }
-  if (lane_id() == 0) {
-    s_area[t / kWave] = area;
-    s_neg[t / kWave] = nneg;
-  }
-  __syncthreads();
-  if (t == 0) {
-    for (int w = 1; w < kLbWaves; ++w) {
-      area += s_area[w];
-      nneg += s_neg[w];
-    }
-    // write-through (sc1) stores, counted by the agent-scope add; the last adder reads them
-    // with sc1 loads (MI355X_MICROARCH.md, hand-offs without an acquire, first row)
-    __hip_atomic_store(&a.barea[b], area, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.bpos[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.bneg[b], nneg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL,
-                                    __HIP_MEMORY_SCOPE_AGENT) == nbk - 1u ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // the last bucket done: area = sum over buckets of (its own area + its negatives x the
-  // positives of the buckets before it), then AUC * n as k_auc_final computes it, and the lane
-  // reset for the next snapshot (the bucket map fitted to this snapshot's range)
-  const uint32_t per = (nbk + kLbNT - 1) / kLbNT;
-  uint32_t mpos = 0;
-  for (uint32_t i = 0; i < per; ++i)
-    if (t * per + i < nbk) mpos += __hip_atomic_load(&a.bpos[t * per + i], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t P;
-  uint32_t pb = block_excl_scan<kLbNT>(mpos, lds, &P);
-  double tot_area = 0;
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t d = t * per + i;
-    if (d < nbk) {
-      const double ar = __hip_atomic_load(&a.barea[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t ng = __hip_atomic_load(&a.bneg[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tot_area += ar + (double)ng * (double)pb;
-      pb += __hip_atomic_load(&a.bpos[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) tot_area += __shfl_xor(tot_area, off, kWave);
-  if (lane_id() == 0) s_area[t / kWave] = tot_area;
-  __syncthreads();
-  if (t != 0) return;
-  for (int w = 1; w < kLbWaves; ++w) tot_area += s_area[w];
-  const double Pd = (double)P;
-  const double nn = (double)a.B;
-  double r;
-  if (Pd == 0 || Pd == nn) {
-    r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
-  } else {
-    const double ar = tot_area / (Pd * (nn - Pd));
-    r = (ar < 0.5 ? 1 - ar : ar) * nn;
-  }
-  *a.out = a.accumulate ? *a.out + r : r;
-  ds->auc_done = 0;
-  ds->auc_pk_min = ~ds->auc_kmin_inv;
-  ds->auc_pk_max = ds->auc_kmax;
-  ds->auc_pk_valid = 1u;
-  ds->auc_kmin_inv = 0;
-  ds->auc_kmax = 0;
-}
-
-// one wave per AUC bucket (kwarg lb_wave=1): k_ab_bucket's sort, count and hand-off with no
-// block barrier; the last wave to finish adds the buckets' areas and cross terms
-__global__ __launch_bounds__(kWave) void k_ab_wbucket(AbArgs a) {
-  __shared__ uint64_t sk[kLbCap];
-  __shared__ uint32_t cnt[256];
-  DevState* ds = a.ds;
-  const int l = threadIdx.x;
-  const uint32_t b = blockIdx.x;
-  const uint32_t nbk = 1u << a.wbits;
-  const int64_t start = a.bstart[b];
-  const int n = (int)((int64_t)a.bstart[b + 1] - start);
-  const bool fast = n <= kLbCap;  // else sorted in place by k_ab_big
-  const uint64_t* gk = a.kbuf + start;
-  if (fast)
-    lb_wave_sort<false, false>(gk, nullptr, nullptr, n, false, 0, 0, 32, true, sk, nullptr,
-                               nullptr, cnt);
-  // within the bucket: every negative adds the positives ranked below it here (exact integers
-  // in double); the positives of the buckets before it are added by the last wave
-  double area = 0;
-  uint32_t run = 0, nneg = 0;
-  const int nc = (n + kWave - 1) / kWave;
-  auto count = [&](const uint64_t* K) {  // LDS or global instantiation (no flat loads)
-    for (int c = 0; c < nc; ++c) {
-      const int i = c * kWave + l;
-      const bool valid = i < n;
-      const uint32_t lb = valid ? (uint32_t)(K[i] & 1ull) : 0u;
-      const uint64_t pm = __ballot(valid && lb == 1u);
-      if (valid && lb == 0u) {
-        area += (double)(run + (uint32_t)__popcll(pm & lanemask_lt()));
-        ++nneg;
-      }
-      run += (uint32_t)__popcll(pm);
-    }
-  };
-  if (fast) count(sk);
-  else count(gk);
-  for (int off = 32; off > 0; off >>= 1) {
-    area += __shfl_xor(area, off, kWave);
-    nneg += __shfl_xor(nneg, off, kWave);
-  }
-  uint32_t last = 0;
-  if (l == 0) {
-    // write-through (sc1) stores, counted by the agent-scope add; the last adder reads them
-    // with sc1 loads (MI355X_MICROARCH.md, hand-offs without an acquire, first row)
-    __hip_atomic_store(&a.barea[b], area, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.bpos[b], run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.bneg[b], nneg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = __hip_atomic_fetch_add(&ds->auc_done, 1u, __ATOMIC_ACQ_REL,
-                                  __HIP_MEMORY_SCOPE_AGENT) == nbk - 1u ? 1u : 0u;
-  }
-  if (!__shfl(last, 0, kWave)) return;
-  // the last bucket done: area = sum over buckets of (its own area + its negatives x the
-  // positives of the buckets before it), then AUC * n as k_auc_final computes it, and the lane
-  // reset for the next snapshot (the bucket map fitted to this snapshot's range)
-  const uint32_t per = (nbk + kWave - 1) / kWave;
-  uint32_t mpos = 0;
-  for (uint32_t i = 0; i < per; ++i)
-    if (l * per + i < nbk) mpos += __hip_atomic_load(&a.bpos[l * per + i], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t incl = wave_incl_scan(mpos);
-  const uint32_t P = __shfl(incl, kWave - 1, kWave);
-  uint32_t pb = incl - mpos;
-  double tot_area = 0;
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t d = l * per + i;
-    if (d < nbk) {
-      const double ar = __hip_atomic_load(&a.barea[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t ng = __hip_atomic_load(&a.bneg[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tot_area += ar + (double)ng * (double)pb;
-      pb += __hip_atomic_load(&a.bpos[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) tot_area += __shfl_xor(tot_area, off, kWave);
-  if (l != 0) return;
-  const double Pd = (double)P;
-  const double nn = (double)a.B;
-  double r;
-  if (Pd == 0 || Pd == nn) {
-    r = 1.0;  // the reference returns 1 here (bin_class_metric.h:53), not 1*n
-  } else {
-    const double ar = tot_area / (Pd * (nn - Pd));
-    r = (ar < 0.5 ? 1 - ar : ar) * nn;
-  }
-  *a.out = a.accumulate ? *a.out + r : r;
-  ds->auc_done = 0;
-  ds->auc_pk_min = ~ds->auc_kmin_inv;
-  ds->auc_pk_max = ds->auc_kmax;
-  ds->auc_pk_valid = 1u;
-  ds->auc_kmin_inv = 0;
-  ds->auc_kmax = 0;
-}
-
-int auc_bucket(const Lane& L, int64_t B, const uint32_t* key, const uint32_t* lab,
-               double* out_dev, bool accumulate, bool wave, bool* used) {
-  *used = false;
-  Workspace& ws = *L.ws;
-  if (!ws.lb_hint) {
-    DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&ws.lb_hint), 4 * sizeof(unsigned int),
-                          hipHostMallocDefault));
-    for (int i = 0; i < 4; ++i) ws.lb_hint[i] = 0;
-  }
-  volatile unsigned int* hint = ws.lb_hint;
-  if (hint[0] > kLbOverRadix) {  // skewed snapshots lately: the radix lane
-    if (++hint[1] < kLbRetry) return DFX_OK;
-    hint[0] = 0;
-    hint[1] = 0;
-  }
-  int wbits = 1;  // ~256 items a bucket
-  while (wbits < 12 && ((int64_t)256 << wbits) < B) ++wbits;
-  const uint32_t nbk = 1u << wbits;
-  const int64_t ntiles = (B + kAbTileItems - 1) / kAbTileItems;
-  DFX_TRY(ws.keys0.ensure(B * 8));
-  DFX_TRY(ws.keys1.ensure(B * 8));
-  DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 4 * (nbk + 1)) +
-                          sizeof(double) * (nbk + 1)));
-  AbArgs a{};
-  a.B = B; a.ntiles = ntiles; a.key = key; a.lab = lab; a.wbits = wbits;
-  a.barea = ws.lbcnt.as<double>();  // 8-byte aligned first
-  a.tilecnt = reinterpret_cast<uint32_t*>(a.barea + nbk + 1);
-  a.totals = a.tilecnt + (size_t)ntiles * nbk;
-  a.bstart = a.totals + nbk + 1;
-  a.bpos = a.bstart + nbk + 1;
-  a.bneg = a.bpos + nbk + 1;
-  a.kbuf = ws.keys0.as<uint64_t>();
-  a.kscr = ws.keys1.as<uint64_t>();
-  a.ds = L.ds;
-  a.out = out_dev;
-  a.accumulate = accumulate ? 1 : 0;
-  a.hint = ws.lb_hint;
-  LbArgs c{};  // the column scan's view
-  c.tilecnt = a.tilecnt; c.totals = a.totals; c.ntiles = ntiles; c.wbits = wbits;
-  hipLaunchKernelGGL(k_ab_hist, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
-                     L.stream, a);
-  hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
-                     L.stream, c);
-  hipLaunchKernelGGL(k_ab_scatter, dim3((unsigned)ntiles), dim3(kLbNT), nbk * sizeof(uint32_t),
-                     L.stream, a);
-  hipLaunchKernelGGL(k_ab_big, dim3(kLbBigBlocks), dim3(kLbNT), 0, L.stream, a);
-  if (wave) hipLaunchKernelGGL(k_ab_wbucket, dim3(nbk), dim3(kWave), 0, L.stream, a);
-  else hipLaunchKernelGGL(k_ab_bucket, dim3(nbk), dim3(kLbNT), 0, L.stream, a);
   DFX_HIP(hipGetLastError());
   *used = true;
   return DFX_OK;

@@ -338,12 +338,6 @@ int auc_finish(const Lane& L, int64_t B, double* out_dev, bool accumulate, int m
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
-  if (mode >= 2) {  // the bucket sort (locbucket.hip), unless the hint says skewed snapshots
-    bool used = false;
-    DFX_TRY(auc_bucket(L, B, ws.ak0.as<uint32_t>(), ws.av0.as<uint32_t>(), out_dev, accumulate,
-                       mode == 3, &used));
-    if (used) return DFX_OK;
-  }
   const bool radix = mode != 0;
   const int64_t ntiles = (B + kArTile - 1) / kArTile;
   const uint32_t* V0 = nullptr;

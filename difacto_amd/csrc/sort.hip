@@ -6,7 +6,7 @@
 // Launches per sort: [k_os_hist: one read of the keys, the digit counts of EVERY pass — or the
 // producer of the keys accumulates them itself, as the Localizer's transform does] ->
 // k_os_plan (1 block: reduce the counts, pick the digits that vary) -> one k_os_scatter per
-// pass.  A scatter block takes the tile of its index (tiles start in order), ranks its
+// pass.  A scatter block takes a tile by ticket (tiles in block start order), ranks its
 // 4096 items with wave ballots (exact and order preserving), publishes its per-digit counts and
 // finds its global offsets by decoupled look-back over the preceding tiles' published words
 // (several predecessors read per step), then writes the tile through LDS in digit order, so
@@ -35,7 +35,6 @@ static_assert(kOsTile <= 4096, "rank packing below assumes < 2^12 items per wave
 constexpr int kOsMaxPasses = kOsDigits;
 constexpr int kOsLookback = 4;  // predecessor words read per look-back step (default)
 constexpr unsigned kOsNone = 0xFFFFFFFFu;
-constexpr int64_t kOsLoopGrid = 64;  // blocks of a pass expected to be constant (kSortHint)
 // sortmeta layout: [q] digit of active pass q (shift | bits << 16) or kOsNone; [8+q] source
 // buffer of pass q; [16+q] tile counter of pass q; [24] launch epoch; [31] result buffer.
 // The look-back words carry (epoch, pass) as a tag, so stale words never need clearing.
@@ -58,7 +57,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
                                                    int npasses, int begin_bit, int end_bit,
                                                    unsigned int* meta, uint32_t* parts,
                                                    uint32_t* counts, unsigned int* epoch,
-                                                   int pack_rb8, unsigned int* host_nq) {
+                                                   int pack_rb8) {
   __shared__ int s_pos[kOsMaxPasses];
   __shared__ int s_nq;
   const int t = threadIdx.x;
@@ -95,7 +94,6 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
     meta[kMetaPack] = (pack && q > 0) ? (1u | ((unsigned)lo8 << 8) | ((unsigned)pack_rb8 << 16))
                                       : 0u;
     meta[31] = (unsigned)(q & 1);
-    if (host_nq) *host_nq = (unsigned)q;  // the next sort's launch hint (pinned, vector store)
     s_nq = q;
   }
   __syncthreads();
@@ -191,11 +189,7 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
   // start: every tile a block looks back on is then done or held by a running block.  Block
   // index order is not start order across XCDs, and this pass can run beside another look-back
   // kernel on another stream (the AUC lane's sort beside the main stream's InitV), so tile =
-  // block index could wait on a block that cannot be placed.  A grid smaller than
-  // the tile count (a pass the host expects to find constant, below) takes tiles until they run
-  // out, its next ticket only after publishing its tile.
-  const bool looping = (int64_t)gridDim.x * (kOsNT * IT) < n;
-  for (;;) {
+  // block index could wait on a block that cannot be placed.
   if (t == 0) s_tile = (int64_t)atomicAdd(&meta[kMetaTile + q], 1u);
 #pragma unroll
   for (int i = 0; i < kOsWaves; ++i) wcnt[i][t] = 0;
@@ -338,17 +332,6 @@ __global__ __launch_bounds__(kOsNT) void k_os_scatter(K* k0, P* v0, K* k1, P* v1
       }
     }
   }
-  if (!looping) return;
-  __syncthreads();  // the tile's LDS is read out before the next ticket reuses it
-  }
-}
-
-int Workspace::os_hint_reserve() {
-  if (os_hint) return DFX_OK;
-  DFX_HIP(hipHostMalloc(reinterpret_cast<void**>(&os_hint), 4 * sizeof(unsigned int),
-                        hipHostMallocDefault));
-  for (int i = 0; i < 4; ++i) os_hint[i] = kOsNone;  // unknown: every pass on a full grid
-  return DFX_OK;
 }
 
 int Workspace::os_reserve(int64_t ntiles, hipStream_t st) {
@@ -391,7 +374,7 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
   const int pack_rb8 = (sizeof(K) == 8 && sizeof(P) == 4) ? (flags >> 8) & 0xFF : 0;
   if (n <= 0 || end_bit <= begin_bit) {
     hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, 0,
-                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0, nullptr);
+                       begin_bit, end_bit, sortmeta, parts, counts, epoch, 0);
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
@@ -401,24 +384,10 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
     hipLaunchKernelGGL(k_os_hist<K>, dim3((unsigned)((n + kOsTile - 1) / kOsTile)), dim3(kOsNT),
                        0, L.stream, k0, n, n_dev, begin_bit, npasses, parts);
   }
-  // kSortHint: the passes beyond the active count of this workspace's previous sort of the same
-  // item type (k_os_plan writes it to pinned memory; read here without a wait, so it may be a
-  // step old) run on a small looping grid: they are almost always constant digits, whose
-  // full-grid launches only queue for CU slots behind the other streams to find nothing to do.
-  // A wrong hint costs time, never correctness.
-  const int site = sizeof(K) == 8 ? (sizeof(P) == 8 ? 1 : 0) : 2;
-  unsigned int* host_nq = nullptr;
-  int hint = npasses;
-  if (flags & kSortHint) {
-    DFX_TRY(ws.os_hint_reserve());
-    host_nq = ws.os_hint + site;
-    const unsigned h = __atomic_load_n(host_nq, __ATOMIC_RELAXED);
-    if (h <= (unsigned)npasses) hint = (int)h;
-  }
   hipLaunchKernelGGL(k_os_plan, dim3(1), dim3(kOsNT), 0, L.stream, diff_mask, or_and, npasses,
-                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8, host_nq);
+                     begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8);
   for (int q = 0; q < npasses; ++q) {
-    const int64_t grid = q < hint ? ntiles : std::min<int64_t>(ntiles, kOsLoopGrid);
+    const int64_t grid = ntiles;
 #define DFX_OS_SCATTER(IT, LB)                                                               \
     if (it == IT && lb == LB)                                                                \
       hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)grid), dim3(kOsNT), 0,   \

@@ -171,7 +171,8 @@ def test_sharded_sum_equals_one_step_on_concatenated_batches(N):
     FMLoss, sgd_learner.cc:201-317) on the concatenation of the N batches in rank order.  Loss
     is additive over rows; the model keys, V rows, rand_r state and new_w are exact; values
     differ only by the order the gradient sums run in (per worker, then across workers), so
-    they are compared at 1e-4."""
+    they are compared at 1e-4 — and at north_star's 1e-5 for the keys no step ever saw in two
+    workers' batches, whose sums no per-worker pre-summing reorders."""
     from difacto_amd import dist as DI
     from difacto_amd import hotpath as H
     kw = dict(V_dim=8, V_threshold=2, lr=0.1, V_lr=0.05, l1=0.2, seed=13)
@@ -179,10 +180,14 @@ def test_sharded_sum_equals_one_step_on_concatenated_batches(N):
     shards = [DI.Shard(c, N) for c in ctxs]
     comm = DI.LoopbackComm(N)
     one = O.Updater(**kw)
+    multi = set()  # keys some step saw in two or more workers' batches
     for s in range(6):
         step = [D.synthetic(400, 12, 6000, binary=(r % 2 == 0), seed=900 + 37 * s + r)
                 for r in range(N)]
         push = s < 2
+        seen = np.concatenate([np.unique(O.localize(b.offs, b.ids)[0]) for b in step])
+        kk, nk = np.unique(seen, return_counts=True)
+        multi.update(int(k) for k in kk[nk > 1])
         dbs = [H.DeviceRowBlock(ctxs[r], step[r]) for r in range(N)]
         DI.sharded_step(shards, dbs, comm, H.kTraining, push_cnt=push)
         cat = D.concat(step)
@@ -194,7 +199,7 @@ def test_sharded_sum_equals_one_step_on_concatenated_batches(N):
     assert sum(st["new_w"] for st in stats) == one.new_w
     assert all(st["seed"] == one.seed for st in stats)
     cat_keys = np.unique(O.localize(cat.offs, cat.ids)[0])
-    n_v = 0
+    n_v = n_single = 0
     for k in cat_keys:
         g = int(DO.owner_of(np.array([k], np.uint64), N)[0])
         e = one.entry(k)
@@ -202,12 +207,15 @@ def test_sharded_sum_equals_one_step_on_concatenated_batches(N):
         assert (got is None) == (e is None)
         if e is None:
             continue
-        assert close(got[0], e[0], rtol=1e-4), k
+        rt = 1e-4 if int(k) in multi else 1e-5
+        n_single += int(k) not in multi
+        assert close(got[0], e[0], rtol=rt), k
         assert (got[1] is None) == (e[1] is None), k
         if e[1] is not None:
             n_v += 1
-            assert close(got[1], e[1], rtol=1e-4), k
-    assert n_v > 0
+            assert close(got[1], e[1], rtol=rt), k
+    # (at N = 2 about a tenth of the last step's keys never met in two batches)
+    assert n_v > 0 and (n_single > 0 or N > 2), (n_v, n_single, len(cat_keys))
     for c in ctxs:
         c.close()
 

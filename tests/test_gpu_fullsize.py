@@ -63,7 +63,10 @@ def test_localizer_full_c3(H):
     c.close()
 
 
-def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=True):
+def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=True,
+         exact=False):
+    """exact: no key reaches a chunked (> 256 occurrences) gradient sum, so predictions and the
+    model must equal the oracle's bit for bit (sums in the reference's order, glibc expf)"""
     c = H.Context(0, max_keys=max_keys, **cfg)
     up = O.Updater(**cfg)
     for step, blk in enumerate(batches):
@@ -75,6 +78,9 @@ def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=Tr
         p = H.progress(c)
         rt = pred_rtol[step] if isinstance(pred_rtol, (list, tuple)) else pred_rtol
         assert close(pred.cpu().numpy(), opred, rtol=rt), step
+        if exact:
+            assert np.array_equal(pred.cpu().numpy().view(np.uint32),
+                                  np.asarray(opred, np.float32).view(np.uint32)), step
         assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
         assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size, step
         assert p["nrows"] == blk.size
@@ -88,6 +94,9 @@ def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=Tr
         if cfg.get("V_dim", 0) > 0:
             assert np.array_equal(l.cpu().numpy(), ol)
         assert close(v.cpu().numpy(), ov, rtol=model_rtol)
+        if exact:
+            assert np.array_equal(v.cpu().numpy().view(np.uint32),
+                                  np.asarray(ov, np.float32).view(np.uint32))
     c.close()
 
 
@@ -96,7 +105,8 @@ def test_fused_full_c3(H):
     V_threshold = 0), then training steps over fresh batches"""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     batches = [D.synthetic(100_000, 39, 1 << 24, seed=5000 + s) for s in range(3)]
-    _run(H, cfg, batches, n_cnt=1, max_keys=1 << 24, pred_rtol=RTOL, model_rtol=RTOL)
+    _run(H, cfg, batches, n_cnt=1, max_keys=1 << 24, pred_rtol=RTOL, model_rtol=RTOL,
+         exact=True)
 
 
 def test_fused_full_c2(H):
@@ -104,7 +114,8 @@ def test_fused_full_c2(H):
     cfg = dict(V_dim=0, l1=1, l2=0, lr=.1)
     batches = [D.synthetic(10_000, 40, 1 << 20, binary=False, seed=6000 + s)
                for s in range(6)]
-    _run(H, cfg, batches, n_cnt=0, max_keys=1 << 20, pred_rtol=RTOL, model_rtol=RTOL)
+    _run(H, cfg, batches, n_cnt=0, max_keys=1 << 20, pred_rtol=RTOL, model_rtol=RTOL,
+         exact=True)
 
 
 def test_fused_full_c5(H):

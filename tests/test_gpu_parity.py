@@ -85,10 +85,9 @@ def test_localizer_synthetic(H, kind, items, lookback):
         _check_localize(H, c, blk, max_index=1000)
 
 
-def test_localizer_sort_hint_changes(H):
-    """one context sorting narrow keys (3 active digit passes: the next sorts launch the other
-    passes on a small looping grid) then 64-bit ids (every pass active, on that small grid the
-    first time) then narrow keys again: bit-exact every time"""
+def test_localizer_key_width_changes(H):
+    """one context sorting narrow keys (3 active digit passes) then 64-bit ids (every pass
+    active) then narrow keys again: bit-exact every time"""
     c = H.Context(0)
     rng = np.random.default_rng(9)
     for i, wide in enumerate([False, False, True, True, False, True]):
@@ -221,17 +220,16 @@ def test_auc_and_evaluate(H):
 
 @pytest.mark.parametrize("n", [1, 2, 4095, 4097, 10000, 12288, 12289, 100000, 1000003])
 def test_auc_radix_and_merge_sorts_agree(H, n):
-    """the AUC lane's four stable sorts (auc_sort=wbucket | bucket | radix | merge; up to 12288
-    rows all take the one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie
-    break of the oracle, with heavy ties (quantised predictions, one constant digit pattern),
-    with all predictions equal (epoch 0, w = 0: one bucket far beyond the LDS sort) and with
-    signed zeros (-0 == +0).  Each context sees every snapshot twice, so the bucket sort runs
-    with its map fitted to the previous snapshot's range and to a different one"""
+    """the AUC lane's two stable sorts (auc_sort=radix | merge; up to 12288 rows both take the
+    one-block LDS sort, k_auc_block): the same AUC*n, equal to the input-order tie break of the
+    oracle, with heavy ties (quantised predictions, one constant digit pattern), with all
+    predictions equal (epoch 0, w = 0) and with signed zeros (-0 == +0).  Each context sees every
+    snapshot twice"""
     rng = np.random.default_rng(n)
     label = np.where(rng.random(n) < 0.25, 1.0, -1.0).astype(np.float32)
     signed0 = np.where(rng.random(n) < 0.5, np.float32(-0.0), np.float32(0.0)).astype(np.float32)
     signed0[rng.random(n) < 0.3] = -1.5
-    cs = [H.Context(0, auc_sort=mode) for mode in ["bucket", "radix", "merge", "wbucket"]]
+    cs = [H.Context(0, auc_sort=mode) for mode in ["radix", "merge"]]
     for pred in [np.round(rng.standard_normal(n) * 8).astype(np.float32) / 8,
                  np.zeros(n, np.float32), (rng.standard_normal(n) - 0.3 * label).astype(np.float32),
                  signed0]:
@@ -239,7 +237,7 @@ def test_auc_radix_and_merge_sorts_agree(H, n):
         for _ in range(2):
             got = [H.auc(c, c.tensor(label, torch.float32), c.tensor(pred, torch.float32))
                    for c in cs]
-            assert got[0] == got[1] == got[2] == got[3], got
+            assert got[0] == got[1], got
             assert abs(got[0] - want) <= 1e-4 * n, (got, want)
     for c in cs:
         c.close()

@@ -333,11 +333,11 @@ def test_bucket_localizer_equals_lsd(H, kind):
     tolerances.  Batches of 60 k rows (2.3 M nnz) and a ragged 3 k-row one; skewed and moving
     key ranges exercise the global-memory bucket passes and the radix fallback.  A third
     context runs the histogram / scatter on 256-thread blocks (lb_hnt=256: other row windows
-    per block, another tile split; lb_xcd=1: XCD-contiguous tiles)."""
+    per block, another tile split)."""
     cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     cs = [H.Context(0, max_keys=1 << 21, loc_bucket=0, **cfg),
           H.Context(0, max_keys=1 << 21, loc_bucket=1, **cfg),
-          H.Context(0, max_keys=1 << 21, loc_bucket=1, lb_hnt=256, lb_xcd=1, **cfg)]
+          H.Context(0, max_keys=1 << 21, loc_bucket=1, lb_hnt=256, **cfg)]
     up = O.Updater(**cfg)
     rng = np.random.default_rng(9)
     for step in range(5):
@@ -579,42 +579,6 @@ def test_forward_eight_coords_per_lane_bit_identical(H, d, zipf, binary):
     cb.close()
 
 
-@pytest.mark.parametrize("d", [0, 16, 5])
-def test_position_payload_localizer_bit_identical(H, d):
-    """Valued batches: the Localizer sorts packed (key | position) items and gathers each
-    occurrence's row and value by position (loc_pos=1, a measured A/B kwarg) against the
-    16-byte (key, {pos, row}) items (loc_pos=0, the default): the same occurrence order, so predictions, progress
-    and the model are bit-identical; ragged rows, a count-push step, C2's shape at d = 0"""
-    cfg = dict(V_dim=d, lr=.1, V_lr=.02, l1=.5, V_threshold=1) if d else dict(V_dim=0, lr=.1, l1=1)
-    ca = H.Context(0, max_keys=1 << 17, loc_pos=1, **cfg)
-    cb = H.Context(0, max_keys=1 << 17, **cfg)
-    blocks = []
-    for step in range(4):
-        blk = D.synthetic(5000, 40, 1 << 16, binary=False, ragged=(step == 1), seed=90 + step)
-        blocks.append(blk)
-        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
-        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
-        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step == 0, pred=pa)
-        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step == 0, pred=pb)
-        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
-        a, b = H.progress(ca), H.progress(cb)
-        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
-    ca.sync()
-    cb.sync()
-    assert H.Store(ca).stats() == H.Store(cb).stats()
-    keys = np.unique(np.concatenate([O.localize(b.offs, b.ids)[0] for b in blocks]))
-    for k in keys[::5]:
-        ea, eb = H.Store(ca).entry(k), H.Store(cb).entry(k)
-        assert (ea is None) == (eb is None)
-        if ea is not None:
-            assert np.array_equal(ea[0], eb[0]), k
-            assert (ea[1] is None) == (eb[1] is None)
-            if ea[1] is not None:
-                assert np.array_equal(ea[1], eb[1]), k
-    ca.close()
-    cb.close()
-
-
 @pytest.mark.parametrize("d", [0, 5])
 def test_value_payload_localizer_bit_identical(H, d):
     """Valued batches: the Localizer's 16-byte items carry each occurrence's value bits (the
@@ -634,33 +598,6 @@ def test_value_payload_localizer_bit_identical(H, d):
         assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
     ca.sync()
     cb.sync()
-    assert H.Store(ca).stats() == H.Store(cb).stats()
-    ca.close()
-    cb.close()
-
-
-@pytest.mark.parametrize("binary", [True, False])
-def test_sort_hint_wrong_hint_bit_identical(H, binary):
-    """kSortHint runs the Localizer sort's passes beyond the previous sort's active count on a
-    64-block looping grid.  A batch over 2^8 ids (one varying digit) sets the hint to 1; the
-    next batches, over 2^40 ids (five varying digits, 420 k nnz: 103 tiles > 64 blocks), then
-    sort four real passes on the looping grid and back: predictions, progress and the model
-    bit-identical to sort_hint=0 (every pass on a full grid)"""
-    cfg = dict(V_dim=4, lr=.1, V_lr=.02, l1=.5, V_threshold=1)
-    ca = H.Context(0, max_keys=1 << 20, sort_hint=0, **cfg)
-    cb = H.Context(0, max_keys=1 << 20, sort_hint=1, **cfg)
-    spaces = [1 << 8, 1 << 40, 1 << 40, 1 << 8, 1 << 40]
-    for step, ks in enumerate(spaces):
-        blk = D.synthetic(10500, 40, ks, binary=binary, ragged=(step == 2), seed=290 + step)
-        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
-        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
-        H.train_step(ca, H.DeviceRowBlock(ca, blk), H.kTraining, push_cnt=step < 2, pred=pa)
-        H.train_step(cb, H.DeviceRowBlock(cb, blk), H.kTraining, push_cnt=step < 2, pred=pb)
-        ca.sync()
-        cb.sync()  # the hint of the next step is this step's plan
-        assert np.array_equal(pa.cpu().numpy(), pb.cpu().numpy()), step
-        a, b = H.progress(ca), H.progress(cb)
-        assert a["loss"] == b["loss"] and a["auc"] == b["auc"], step
     assert H.Store(ca).stats() == H.Store(cb).stats()
     ca.close()
     cb.close()

@@ -78,3 +78,33 @@ def test_tile_forward_bit_identical(H, rows, binary):
     assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
     ca.close()
     cb.close()
+
+
+@pytest.mark.parametrize("rows", [6000, 40000])
+def test_auc_lane_after_backward(H, rows):
+    """auc_lane=after: the AUC lane of step t starts after step t's backward, on a double-
+    buffered snapshot (step t + 1's forward writes the other buffer).  Progress (loss, AUC) and
+    predictions equal the default schedule's exactly at every step (same kernels, same sums);
+    the one-block AUC (<= 12288 rows) and the radix lane are both covered; a validation step in
+    between reads the same snapshot machinery without a backward."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    ca = H.Context(0, max_keys=1 << 20, **cfg)
+    cb = H.Context(0, max_keys=1 << 20, auc_lane="after", **cfg)
+    up = O.Updater(**cfg)
+    for step in range(6):
+        blk = D.synthetic(rows, 39, 1 << 18, seed=80 + step)
+        job = H.kValidation if step == 3 else H.kTraining
+        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
+        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
+        H.train_step(ca, H.DeviceRowBlock(ca, blk), job, push_cnt=(step == 0), pred=pa)
+        H.train_step(cb, H.DeviceRowBlock(cb, blk), job, push_cnt=(step == 0), pred=pb)
+        if job == H.kTraining:
+            loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                             push_cnt=(step == 0), want_pred=True)
+        qa, qb = H.progress(ca), H.progress(cb)
+        assert np.array_equal(pa.cpu().numpy().view(np.uint32), pb.cpu().numpy().view(np.uint32))
+        assert qa["loss"] == qb["loss"] and qa["auc"] == qb["auc"], (step, qa, qb)
+        if job == H.kTraining:
+            assert abs(qb["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    ca.close()
+    cb.close()

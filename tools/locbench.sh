@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/locbench on the GPU box: the Localizer alone, radix vs bucket and the bucket kernel's
 # measurement switches (lb_diag), then a kernel trace of the default.  B=${LB_B:-100000}.
-# LB_AUC=1: the AUC lane alone instead (bucket / radix / merge), and a trace of the bucket form.
+# LB_AUC=1: the AUC lane alone instead (radix / merge), and a trace of the default.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -15,7 +15,7 @@ if [ -n "$LB_C2" ]; then  # C2's shape: 40 valued nnz per row over 2^20 ids
   exit $?
 fi
 if [ -n "$LB_AUC" ]; then
-  for kw in "auc_sort=bucket" "auc_sort=radix" "auc_sort=merge"; do
+  for kw in "auc_sort=radix" "auc_sort=merge"; do
     timeout -k 10 60 ./build/locbench $B 39 24 20 "$kw" auc || exit $?
   done
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_aucbench -o trace \
