@@ -73,15 +73,6 @@ struct Kw {
   // lane, or each Localizer parity run once and its output reused (results are then wrong
   // unless the batches repeat); never set by the product path
   int diag = 0;
-  int fwd_lanes = 0;  // fwd_lanes=2|4: the prefetching fat forward at V_dim 16 (0: k_fm_fwd_fat)
-  // fwd_ids=1 (default): the fat forward stages each row's ids in LDS in one trip (fm.hip
-  // fwd_probe_body IDS; same-box A/B at C3 with fat_nb 8: 127.6 -> 130.0 M ex/s, forward
-  // 0.248 -> 0.213 ms in the step); 0: each trip loads its ids
-  int fwd_ids = 1;
-  int fwd_pf = 1;  // fwd_pf=1: with fwd_ids, the next row's offsets and ids prefetched
-  // fwd_tile=1: the tiled gather forward at V_dim 16 (fm.hip k_fm_fwd_tile): a tile's nnz
-  // gathered a chunk at a time into LDS, then summed per row in nnz order
-  int fwd_tile = 0;
   // lr_lanes=1 (default): the LR forward (V_dim 0) on four lanes per row with a chunk's entry
   // loads in flight together (fm.hip fwd_probe_body, d == 0); 0: one thread per row
   int lr_lanes = 1;
@@ -98,10 +89,6 @@ struct Kw {
   // (0.44 -> 0.49 ms); at B = 10^4, where the one-block AUC (~94 us) outlasts the backward,
   // 58.6 / 61.6 -> 68.0 / 68.8.  2 (the default): double-buffered for B <= kAucBlockMax only
   int auc_db = 2;
-  // auc_lane=after: the AUC lane starts after the step's backward (beside the next step's
-  // forward) instead of beside the backward, on a double-buffered snapshot; auc_lane=bwd: beside
-  // the backward
-  int auc_after = 0;
   // lb_gather: valued batches sort (key | position) items alone, the row and the value gathered
   // by position at the outputs (1; A/B at C2: 126 -> 161 M ex/s) or, in the fused step, read by
   // position in the backward itself (2, the default: no gather launch on the Localizer lane;
@@ -116,9 +103,6 @@ struct Kw {
   // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
   // heads + scan + write)
   int loc_onepass = 0;
-  // fat_nb=4|6|8|12: the fat forward's nnz per trip (A/B, DESIGN.md (d): 8 with the staged ids,
-  // 6 without)
-  int fat_nb = 8;
   // nt=<mask>: streaming (non-temporal) cache policy for 1 the Localizer lane's sort passes and
   // transform, 2 the backward's model-table lines, 4 the forward's, 8 the backward's
   // per-occurrence arrays (common.h ld4 / st4)
@@ -144,6 +128,7 @@ struct Kw {
   // the context stream's (fused step: it then ends about when the next step needs it, and the
   // backward keeps more of the machine: +1.5 %)
   int lane_prio = 2;  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
+  int strict = 0;     // strict=1: unknown kwargs are an error
 };
 
 static int parse_kwargs(const char* kwargs, Kw* kw) {
@@ -153,7 +138,7 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
   for (char& ch : s)
     if (ch == ',' || ch == ';' || ch == '\n' || ch == '\t') ch = ' ';
   std::istringstream is(s);
-  std::string tok;
+  std::string tok, unknown;
   while (is >> tok) {
     auto eq = tok.find('=');
     if (eq == std::string::npos) continue;
@@ -205,28 +190,11 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
-    else if (k == "auc_lane") {
-      if (std::string(cv) != "after" && std::string(cv) != "bwd") {
-        set_error("auc_lane must be after or bwd");
-        return DFX_ERR_ARG;
-      }
-      kw->auc_after = std::string(cv) == "after";
-    }
     else if (k == "auc_db") kw->auc_db = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
     else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
-    else if (k == "fwd_ids") kw->fwd_ids = atoi(cv) != 0;
-    else if (k == "fwd_pf") kw->fwd_pf = atoi(cv) != 0;
-    else if (k == "fwd_tile") kw->fwd_tile = atoi(cv) != 0;
     else if (k == "lr_lanes") kw->lr_lanes = atoi(cv) != 0;
-    else if (k == "fwd_lanes") {
-      kw->fwd_lanes = atoi(cv);
-      if (kw->fwd_lanes != 0 && kw->fwd_lanes != 2 && kw->fwd_lanes != 4) {
-        set_error("fwd_lanes must be 0, 2 or 4");
-        return DFX_ERR_ARG;
-      }
-    }
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
     else if (k == "bwd_cpl_from") kw->bwd_cpl_from = atoi(cv);
     else if (k == "fwd_cpl") {
@@ -248,14 +216,6 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       kw->nt = atoi(cv);
       if (kw->nt < 0 || kw->nt > 15) {
         set_error("nt must be a mask of 1, 2, 4, 8");
-        return DFX_ERR_ARG;
-      }
-    }
-    else if (k == "fat_nb") {
-      // the fat forward's nnz per trip at V_dim 16 (V_dim 8 always takes 8)
-      kw->fat_nb = atoi(cv);
-      if (kw->fat_nb != 4 && kw->fat_nb != 6 && kw->fat_nb != 8 && kw->fat_nb != 12) {
-        set_error("fat_nb must be 4, 6, 8 or 12");
         return DFX_ERR_ARG;
       }
     }
@@ -293,6 +253,17 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
       else if (v == "logit") kw->loss_fm = 0;
       else { set_error("unknown loss: " + v + " (fm|logit)"); return DFX_ERR_ARG; }
     }
+    else if (k == "strict") kw->strict = atoi(cv) != 0;
+    else {
+      // unknown keys are ignored (dmlc::Parameter::InitAllowUnknown: the C++ adapters pass the
+      // learner's kwargs through) unless strict=1 (the Python mirror sets it): a misspelt or
+      // retired kwarg must not silently run the default there
+      unknown += (unknown.empty() ? "" : ", ") + k;
+    }
+  }
+  if (kw->strict && !unknown.empty()) {
+    set_error("unknown context kwargs: " + unknown);
+    return DFX_ERR_ARG;
   }
   if (kw->P.V_dim < 0 || kw->P.V_dim > 1024) {
     set_error("V_dim must be in [0, 1024]");
@@ -402,17 +373,12 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->fat_fwd = kw.fat_fwd;
   c->fat_bwd = kw.fat_bwd;
   c->initv_onepass = kw.initv_onepass;
-  c->fat_nb = kw.fat_nb;
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
   c->bwd_cpl = kw.bwd_cpl;
   c->bwd_cpl_from = kw.bwd_cpl_from;
   c->fwd_cpl = kw.fwd_cpl;
   c->loc_x_payload = kw.loc_xpay;
-  c->fwd_lanes = kw.fwd_lanes;
-  c->fwd_ids = kw.fwd_ids;
-  c->fwd_pf = kw.fwd_pf;
-  c->fwd_tile = kw.fwd_tile;
   c->lr_lanes = kw.lr_lanes;
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;
@@ -420,7 +386,6 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->lb_tiles = kw.lb_tiles;
   c->lb_hnt = kw.lb_hnt;
   c->auc_db = kw.auc_db;
-  c->auc_after = kw.auc_after;
   c->lb_gather = kw.lb_gather;
   c->loc_onepass = kw.loc_onepass;
   c->lane_prio = kw.lane_prio;

@@ -399,32 +399,12 @@ __device__ __forceinline__ void fwd_row_out(const FwdArgs& a, int64_t r, int l, 
 // dependent trips per 8 nnz.  Sums run in exactly the same (row, nnz) order, so predictions
 // are bit-identical to k_fm_fwd's (and the reference's).
 //
-// FAT (fat slots, common.h Table::es > 0, d == 4*G): a key's entry and V share one slot, so the
-// group reads nnz t's home slot whole in ONE trip — lane l its V coordinates [4l, 4l+4), even
-// lanes {w, vrow}, odd lanes the key — for 8 nnz at a time, and checks the key afterwards (a
-// key away from home, rare at load <= 0.5, walks its chain then).  Reading the slot's two
-// halves together keeps them one DRAM access; read a chain step apart, the entry's line was
-// often evicted before its V was read (the split walk above, applied to fat slots: 185 us).
-//
 // CPL = 8 (kwarg fwd_cpl, V_dim a multiple of 8, not FAT): two float4 of V per lane, half the
 // lanes per row; each coordinate's sums are still one lane's in nnz order and s is summed over
 // l = 0..d-1 in order, so predictions are bit-identical to CPL = 4.
-// IDS (FAT, kwarg fwd_ids=1): the group first stages the row's next ~kFwdIds ids (and values; a
-// whole number of trips) in LDS in one trip — G lanes, all loads in flight — and each trip reads
-// its NB ids from LDS: a trip is one memory round trip (the slots) instead of two (ids, then
-// slots).  The same sums in the same order: bit-identical.
-// PF (IDS, kwarg fwd_pf=1): the group's NEXT row's offsets are loaded when a row starts and its
-// first ids beside the row's last trip of slots, so a row costs its slot trips only — not
-// offsets, then ids, then slots.  Still bit-identical.
-constexpr int kFwdIds = 40;
-
-template <int G, bool FAT, int NB = 8, int CPL = 4, bool IDS = false, bool PF = false>
+template <int G, int CPL = 4>
 __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
-  static_assert(CPL == 4 || (CPL == 8 && !FAT), "fat slots: one float4 per lane");
-  constexpr int CHI = (kFwdIds / NB) * NB;  // ids staged per chunk: whole trips
-  static_assert(!IDS || (FAT && CHI % G == 0), "staged ids: fat slots");
-  static_assert(!PF || IDS, "prefetch: staged ids");
-  constexpr int PFN = PF ? CHI / G : 1;
+  static_assert(CPL == 4 || CPL == 8, "one or two float4 per lane");
   constexpr int RPB = kFmNT / G;  // rows per block
   constexpr int CH = 32;          // nnz per chunk
   constexpr int MA = CH / G;      // lookups per lane per chunk
@@ -435,158 +415,16 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   const int d = a.d;
   __shared__ double red[kFmNT / kWave];
   double loss = 0;
-  const int64_t rstride = (int64_t)gridDim.x * RPB;
-  // PF: the next row's offsets, and (pf_ok) its first ids and values held in registers
-  uint64_t pf_o0 = 0, pf_o1 = 0;
-  uint64_t pf_id[PFN];
-  float pf_x[PFN];
-  bool pf_ok = false;
-  if (PF && (int64_t)blockIdx.x * RPB + g < a.B) {
-    const int64_t r0 = fwd_row(a, (int64_t)blockIdx.x * RPB + g);
-    pf_o0 = a.offs[r0];
-    pf_o1 = a.offs[r0 + 1];
-  }
-  // IDS runs on a resident grid (launch_fwd_fused): the block's groups take rows blockIdx.x *
-  // RPB + g, then one grid of rows further on, so no half-empty last round of blocks; else one
-  // row per group
-  for (int64_t ri = (int64_t)blockIdx.x * RPB + g; ri < a.B; ri = IDS ? ri + rstride : a.B) {
+  const int64_t ri = (int64_t)blockIdx.x * RPB + g;  // one row per group
+  if (ri < a.B) {
     const int64_t r = fwd_row(a, ri);
-    uint64_t o0, o1;
-    if constexpr (PF) {
-      o0 = pf_o0;
-      o1 = pf_o1;
-      pf_o0 = pf_o1 = 0;  // no next row: no prefetch
-      if (ri + rstride < a.B) {
-        const int64_t rn = fwd_row(a, ri + rstride);
-        pf_o0 = a.offs[rn];
-        pf_o1 = a.offs[rn + 1];
-      }
-    } else {
-      o0 = a.offs[r];
-      o1 = a.offs[r + 1];
-    }
+    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = 0.f;
     float xv[CPL], xxvv[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
     const bool valued = a.val != nullptr;
-    const bool ntf = (a.nt & kNtFwdTable) != 0;
-    if constexpr (FAT) {
-      __shared__ uint64_t s_id[IDS ? RPB : 1][IDS ? CHI : 1];
-      __shared__ float s_x[IDS ? RPB : 1][IDS ? CHI : 1];
-      uint64_t c_end = o0;  // the staged chunk of ids ends here
-      if constexpr (PF) {
-        if (pf_ok) {  // this row's first ids, loaded beside the last row's last trip
-          __builtin_amdgcn_wave_barrier();  // the last row's reads are done
-#pragma unroll
-          for (int m = 0; m < PFN; ++m) {
-            if (o0 + l + (uint64_t)G * m < o1) {
-              s_id[g][l + G * m] = pf_id[m];
-              if (valued) s_x[g][l + G * m] = pf_x[m];
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-          c_end = o0 + CHI;
-          pf_ok = false;
-        }
-      }
-      for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
-        const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
-        uint64_t key[NB];
-        float xm[NB];
-        if constexpr (IDS) {
-          if (j0 >= c_end) {  // the next CHI ids of the row, one trip (group-uniform)
-            __builtin_amdgcn_wave_barrier();  // the last chunk's reads are done
-#pragma unroll
-            for (int m = 0; m < CHI / G; ++m) {
-              const uint64_t j = j0 + l + (uint64_t)G * m;
-              if (j < o1) {
-                s_id[g][l + G * m] = a.index[j];
-                if (valued) s_x[g][l + G * m] = a.val[j];
-              }
-            }
-            __builtin_amdgcn_wave_barrier();
-            c_end = j0 + CHI;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const uint64_t jj = j0 + t < o1 ? j0 + t : o1 - 1;
-          uint64_t id;
-          if constexpr (IDS) {
-            id = s_id[g][(int)(jj - (c_end - CHI))];
-            xm[t] = valued ? s_x[g][(int)(jj - (c_end - CHI))] : 1.f;
-          } else {
-            id = a.index[jj];
-            xm[t] = valued ? a.val[jj] : 1.f;
-          }
-          const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-          key[t] = a.keys_ready ? id : reverse_bytes(mm);
-        }
-        if constexpr (PF) {
-          if (j0 + NB >= o1 && pf_o1 > pf_o0) {  // the row's last trip: the next row's ids
-#pragma unroll
-            for (int m = 0; m < PFN; ++m) {
-              const uint64_t j = pf_o0 + l + (uint64_t)G * m;
-              if (j < pf_o1) {
-                pf_id[m] = a.index[j];
-                if (valued) pf_x[m] = a.val[j];
-              }
-            }
-            pf_ok = true;
-          }
-        }
-        float4 v[NB];
-        float2 eh[NB];  // even lanes {w, vrow}, odd lanes the key
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
-          eh[t] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
-          v[t] = ld4(sl + 8 + 4 * l, ntf);
-        }
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
-          uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
-          float w = __shfl(eh[t].x, gbase, kWave);
-          int vr = __float_as_int(__shfl(eh[t].y, gbase, kWave));
-          float4 vv = v[t];
-          if (ek != key[t] && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
-            uint64_t h = tbl_hash(key[t], a.T);
-            for (uint64_t probe = 0; ek != key[t] && ek != kEmptyKey && probe < a.T.mask; ++probe) {
-              h = (h + 1) & a.T.mask;
-              ek = ent_at(a.T, h)->key;
-            }
-            if (ek == key[t]) {
-              const Entry* e = ent_at(a.T, h);
-              w = e->w;
-              vr = e->vrow;
-              vv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e) + 8 + 4 * l);
-            }
-          }
-          // absent (inserted by this training step's backward): w = 0, no V
-          if (ek != key[t]) { w = 0.f; vr = -1; }
-          // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
-          const bool vok = vr >= 0 && !(a.l1_shrk && w == 0.f);
-          if (t < nin) {
-            const float x = xm[t];
-            // SpMV::Times skips w == 0 (spmv.h:124-125)
-            if (w != 0.f) acc = valued ? acc + w * x : acc + w;
-            if (vok) {
-              const float xx = x * x;  // XX_ (fm_loss.h:86-92)
-              const float vk[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                xv[k] = valued ? xv[k] + vk[k] * x : xv[k] + vk[k];
-                const float q = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
-                xxvv[k] = valued ? xxvv[k] + q * xx : xxvv[k] + q;
-              }
-            }
-          }
-        }
-      }
-    }
-    for (uint64_t j0 = o0; !FAT && j0 < o1; j0 += CH) {
+    for (uint64_t j0 = o0; j0 < o1; j0 += CH) {
       // ---- the chunk's lookups, MA per lane: nnz j0 + l + G*m
       uint64_t key[MA], hs[MA];
       float xm[MA];
@@ -694,159 +532,99 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
 
 template <int G, int CPL>
 __global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
-  fwd_probe_body<G, false, 8, CPL>(a);
+  fwd_probe_body<G, CPL>(a);
 }
 
-// 8 nnz in flight per lane (V + entry half each): at most 128 VGPRs keeps 4 waves per SIMD
-template <int G, int NB, bool IDS = false, bool PF = false>
-__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat(FwdArgs a) {
-  fwd_probe_body<G, true, NB, 4, IDS, PF>(a);
-}
+// ---- the fat-slot forward (k_fm_fwd_walk; V_dim 8 or 16) --------------------------------------
+// One group of G = d / 4 lanes per row (lane l: V coordinates 4l..4l+3, a float4), the groups looping
+// over rows on a resident grid.  A row's ids are staged in LDS kWkIds at a time (one coalesced
+// trip); each trip then issues kWkNB home-slot reads at once — even / odd lanes the entry's halves
+// ({w, vrow} / key), lane l its float4 of V, one 128-byte line per nnz — checks the keys (a key
+// away from home walks its probe chain) and adds the trip in nnz order: FMLoss::Predict's sums
+// in the reference's order (fm_loss.h:67-119), so predictions are bit-identical to the oracle.
+// The minimal form of round 4's k_fm_fwd_fat (no next-row prefetch, no runtime value switch):
+// 120 -> ~110 us alone at C3 (tools/membench/fwdreal, cold caches; the random-read floor of
+// its 3.9 M slot lines is 85 us, tools/membench/fwdbench flat).
+constexpr int kWkNB = 8;
+constexpr int kWkIds = (40 / kWkNB) * kWkNB;
 
-// ---- the tiled gather forward (kwarg fwd_tile; fat slots at V_dim 16) -----------------------
-// A block owns a tile of kFtRows consecutive rows (group g = 4 lanes accumulates row g) and
-// walks the tile's nnz — contiguous in CSR — in chunks of kFtChunk.  Per chunk every group
-// gathers kFtPer nnz of it (nnz c0 + g + 64 m): its key's home slot in one trip (even / odd lanes
-// the entry's halves, lane l its float4 of V, as k_fm_fwd_fat), the key checked, and {w, V
-// visible, V} into LDS.  The chunk's ids (and values) were staged in LDS by the whole block, and
-// the NEXT chunk's are in flight beside this chunk's slot loads.  Then each group adds its row's
-// nnz of the chunk from LDS in nnz order — FMLoss::Predict's sums in the reference's order
-// (fm_loss.h:67-119), bit-identical to the row walks.  Every gather of a chunk is independent of
-// the others, so a block keeps kFtChunk slot loads in flight, and a row no longer costs a chain
-// of dependent trips (k_fm_fwd_fat: ~5 per row after its ids, 231 VGPRs at 2 waves / SIMD).
-constexpr int kFtRows = kFmNT / 4;          // 64 rows per tile
-constexpr int kFtChunk = 512;               // nnz gathered per round trip
-constexpr int kFtPer = kFtChunk / kFtRows;  // 8 per group
-constexpr int kFtLd = kFtChunk / kFmNT;     // ids per thread of the block's staging loads
-
-template <bool VALUED>
-__global__ __launch_bounds__(kFmNT, 4) void k_fm_fwd_tile(FwdArgs a) {
-  __shared__ float4 s_v[kFtChunk][4];
-  __shared__ float s_w[kFtChunk];
-  __shared__ uint8_t s_ok[kFtChunk];
-  __shared__ uint64_t s_id[kFtChunk];
-  __shared__ float s_x[VALUED ? 2 : 1][VALUED ? kFtChunk : 1];  // by chunk parity
-  __shared__ uint64_t s_off[kFtRows + 1];
+template <int G, bool VALUED, int MINB = 4>  // MINB blocks per CU: 4 keeps 4 waves per SIMD
+__global__ __launch_bounds__(kFmNT, MINB) void k_fm_fwd_walk(FwdArgs a) {
+  static_assert(G == 2 || G == 4, "fat slots: d = 4 G, even / odd lanes the entry's halves");
+  constexpr int RPB = kFmNT / G;
+  __shared__ uint64_t s_id[RPB][kWkIds];
+  __shared__ float s_x[VALUED ? RPB : 1][VALUED ? kWkIds : 1];
   __shared__ double red[kFmNT / kWave];
-  constexpr int G = 4;
-  const int t = threadIdx.x;
-  const int g = t / G;
-  const int l = t % G;
-  const int gbase = (t % kWave) - l;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int gbase = (threadIdx.x % kWave) - l;
   const bool ntf = (a.nt & kNtFwdTable) != 0;
   double loss = 0;
-  const int64_t ntiles = (a.B + kFtRows - 1) / kFtRows;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * kFtRows;
-    const int nr = (int)(a.B - r0 < kFtRows ? a.B - r0 : kFtRows);
-    __syncthreads();  // the last tile's reads of s_off / s_id are done
-    if (t <= nr) s_off[t] = a.offs[r0 + t];
-    __syncthreads();
-    const uint64_t T0 = s_off[0], T1 = s_off[nr];
-    const uint64_t o0 = g < nr ? s_off[g] : T1, o1 = g < nr ? s_off[g + 1] : T1;
-#pragma unroll
-    for (int i = 0; i < kFtLd; ++i) {  // the first chunk's ids, coalesced
-      const uint64_t j = T0 + t + (uint64_t)kFmNT * i;
-      if (j < T1) {
-        s_id[t + kFmNT * i] = a.index[j];
-        if (VALUED) s_x[0][t + kFmNT * i] = a.val[j];
-      }
-    }
-    __syncthreads();
+  const int64_t rstride = (int64_t)gridDim.x * RPB;
+  for (int64_t ri = (int64_t)blockIdx.x * RPB + g; ri < a.B; ri += rstride) {
+    const int64_t r = fwd_row(a, ri);
+    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
     float acc = 0.f;
     float xv[4], xxvv[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
-    int par = 0;
-    for (uint64_t c0 = T0; c0 < T1; c0 += kFtChunk, par ^= 1) {  // block-uniform
-      float2 eh[kFtPer];  // even lanes {w, vrow}, odd lanes the key
-      float4 v[kFtPer];
+    uint64_t c_end = o0;  // the staged ids end here
+    for (uint64_t j0 = o0; j0 < o1; j0 += kWkNB) {
+      if (j0 >= c_end) {  // the row's next kWkIds ids, one trip (group-uniform)
+        __builtin_amdgcn_wave_barrier();  // the last chunk's reads are done
 #pragma unroll
-      for (int m = 0; m < kFtPer; ++m) {
-        const int jl = g + kFtRows * m;
-        if (c0 + jl < T1) {
-          const uint64_t id = s_id[jl];
-          const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-          const uint64_t key = a.keys_ready ? id : reverse_bytes(mm);
-          const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key, a.T)));
-          eh[m] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
-          v[m] = ld4(sl + 8 + 4 * l, ntf);
+        for (int m = 0; m < (kWkIds + G - 1) / G; ++m) {
+          const uint64_t j = j0 + l + (uint64_t)G * m;
+          if (j < o1 && l + G * m < kWkIds) {
+            s_id[g][l + G * m] = a.index[j];
+            if (VALUED) s_x[g][l + G * m] = a.val[j];
+          }
         }
+        __builtin_amdgcn_wave_barrier();
+        c_end = j0 + kWkIds;
       }
-      // the next chunk's ids (and values), in flight beside the slots
-      const uint64_t c1 = c0 + kFtChunk;
-      uint64_t idn[kFtLd];
-      float xn[kFtLd];
+      const int cb = (int)(j0 - (c_end - kWkIds));  // this trip's first id in the chunk
+      const int nin = (int)((o1 - j0) < (uint64_t)kWkNB ? (o1 - j0) : (uint64_t)kWkNB);
+      uint64_t key[kWkNB];
+      float2 eh[kWkNB];  // even lanes {w, vrow}, odd lanes the key
+      float4 v[kWkNB];
 #pragma unroll
-      for (int i = 0; i < kFtLd; ++i) {
-        const uint64_t j = c1 + t + (uint64_t)kFmNT * i;
-        if (j < T1) {
-          idn[i] = a.index[j];
-          if (VALUED) xn[i] = a.val[j];
-        }
-      }
-      float wm[kFtPer];
-      bool okm[kFtPer];
-#pragma unroll
-      for (int m = 0; m < kFtPer; ++m) {
-        const int jl = g + kFtRows * m;
-        if (c0 + jl >= T1) continue;  // group-uniform
-        const uint64_t id = s_id[jl];
+      for (int t = 0; t < kWkNB; ++t) {
+        const uint64_t id = s_id[g][cb + (t < nin ? t : nin - 1)];
         const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-        const uint64_t key = a.keys_ready ? id : reverse_bytes(mm);
-        const float k0 = __shfl(eh[m].x, gbase + 1, kWave), k1 = __shfl(eh[m].y, gbase + 1, kWave);
+        key[t] = a.keys_ready ? id : reverse_bytes(mm);
+        const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
+        eh[t] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
+        v[t] = ld4(sl + 8 + 4 * l, ntf);
+      }
+#pragma unroll
+      for (int t = 0; t < kWkNB; ++t) {
+        if (t >= nin) break;  // group-uniform
+        const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
         uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
-        float w = __shfl(eh[m].x, gbase, kWave);
-        int vr = __float_as_int(__shfl(eh[m].y, gbase, kWave));
-        if (ek != key && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
-          uint64_t h = tbl_hash(key, a.T);
-          for (uint64_t probe = 0; ek != key && ek != kEmptyKey && probe < a.T.mask; ++probe) {
+        float w = __shfl(eh[t].x, gbase, kWave);
+        int vr = __float_as_int(__shfl(eh[t].y, gbase, kWave));
+        float4 vv = v[t];
+        if (ek != key[t] && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
+          uint64_t h = tbl_hash(key[t], a.T);
+          for (uint64_t probe = 0; ek != key[t] && ek != kEmptyKey && probe < a.T.mask; ++probe) {
             h = (h + 1) & a.T.mask;
             ek = ent_at(a.T, h)->key;
           }
-          if (ek == key) {
+          if (ek == key[t]) {
             const Entry* e = ent_at(a.T, h);
             w = e->w;
             vr = e->vrow;
-            v[m] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e) + 8 + 4 * l);
+            vv = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(e) + 8 + 4 * l);
           }
         }
         // absent (inserted by this training step's backward): w = 0, no V
-        if (ek != key) { w = 0.f; vr = -1; }
-        wm[m] = w;
-        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
-        okm[m] = vr >= 0 && !(a.l1_shrk && w == 0.f);
-      }
-      __syncthreads();  // the last chunk's sums have read s_v; every group has read s_id
-#pragma unroll
-      for (int m = 0; m < kFtPer; ++m) {
-        const int jl = g + kFtRows * m;
-        if (c0 + jl < T1) {
-          s_v[jl][l] = v[m];
-          if (l == 0) {
-            s_w[jl] = wm[m];
-            s_ok[jl] = okm[m] ? 1 : 0;
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < kFtLd; ++i) {
-        if (c1 + t + (uint64_t)kFmNT * i < T1) {
-          s_id[t + kFmNT * i] = idn[i];
-          if (VALUED) s_x[par ^ 1][t + kFmNT * i] = xn[i];
-        }
-      }
-      __syncthreads();
-      // this group's row inside the chunk, in nnz order
-      const uint64_t lo = o0 > c0 ? o0 : c0, hi = o1 < c1 ? o1 : c1;
-      for (uint64_t j = lo; j < hi; ++j) {
-        const int jl = (int)(j - c0);
-        const float w = s_w[jl];
-        const float x = VALUED ? s_x[par][jl] : 1.f;
+        if (ek != key[t]) { w = 0.f; vr = -1; }
+        const float x = VALUED ? s_x[g][cb + t] : 1.f;
         // SpMV::Times skips w == 0 (spmv.h:124-125)
         if (w != 0.f) acc = VALUED ? acc + w * x : acc + w;
-        if (s_ok[jl]) {
-          const float4 vv = s_v[jl][l];
+        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
+        if (vr >= 0 && !(a.l1_shrk && w == 0.f)) {
           const float vk[4] = {vv.x, vv.y, vv.z, vv.w};
           const float xx = x * x;  // XX_ (fm_loss.h:86-92)
 #pragma unroll
@@ -858,13 +636,13 @@ __global__ __launch_bounds__(kFmNT, 4) void k_fm_fwd_tile(FwdArgs a) {
         }
       }
     }
-    if (g < nr) fwd_row_out<4, 4, 16>(a, r0 + g, l, gbase, acc, xv, xxvv, &loss);
+    fwd_row_out<G, 4, 4 * G>(a, r, l, gbase, acc, xv, xxvv, &loss);
   }
   if (a.part) return;  // block-uniform: no loss partial in split mode
   for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
-  if (lane_id() == 0) red[t / kWave] = loss;
+  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
   __syncthreads();
-  if (t == 0) {
+  if (threadIdx.x == 0) {
     double s = 0;
     for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
     a.loss_part[blockIdx.x] = s;
@@ -884,157 +662,6 @@ static int64_t resident_grid(int64_t want) {
       cus <= 0)
     return want;
   return std::min<int64_t>(want, (int64_t)per_cu * cus);
-}
-
-// Fat-slot forward, second form (kwarg fwd_lanes = 2 | 4; V_dim 16, 128-byte slots): G lanes
-// per row, lane l holding V coordinates [CPL*l, CPL*l + CPL) with CPL = 16 / G, NB nnz per
-// trip, and the NEXT trip's ids (and values) loaded while this trip's slots are in flight, so
-// a trip costs one memory round trip instead of two (id, then slot).  At G = 2 a 256-thread
-// block holds 128 rows: B = 100 k rows is 782 blocks, all resident at once on 256 CUs (at G = 4
-// the 1563 blocks ran as 1.5 waves of blocks, the second half-empty).  Sums in the reference's
-// (row, nnz) order exactly as fwd_probe_body's, so predictions are bit-identical to it.
-template <int G, int NB, bool VALUED>
-__global__ __launch_bounds__(kFmNT) void k_fm_fwd_fat_pf(FwdArgs a) {
-  constexpr int RPB = kFmNT / G;  // rows per block
-  constexpr int CPL = 16 / G;     // V coordinates per lane
-  const int g = threadIdx.x / G;
-  const int l = threadIdx.x % G;
-  const int gbase = (threadIdx.x % kWave) - l;
-  const int64_t r = (int64_t)blockIdx.x * RPB + g;
-  __shared__ double red[kFmNT / kWave];
-  double loss = 0;
-  if (r < a.B) {
-    const uint64_t o0 = a.offs[r], o1 = a.offs[r + 1];
-    constexpr bool valued = VALUED;
-    float acc = 0.f;
-    float xv[CPL], xxvv[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) { xv[k] = 0.f; xxvv[k] = 0.f; }
-    uint64_t idn[NB];
-    float xn[NB];
-#pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const uint64_t jj = o0 + t < o1 ? o0 + t : (o1 > o0 ? o1 - 1 : o0);
-      idn[t] = o1 > o0 ? a.index[jj] : 0ull;
-      xn[t] = (valued && o1 > o0) ? a.val[jj] : 1.f;
-    }
-    for (uint64_t j0 = o0; j0 < o1; j0 += NB) {
-      const int nin = (int)((o1 - j0) < (uint64_t)NB ? (o1 - j0) : (uint64_t)NB);
-      uint64_t key[NB];
-      float xm[NB];
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const uint64_t id = idn[t];
-        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-        key[t] = a.keys_ready ? id : reverse_bytes(mm);
-        xm[t] = xn[t];
-      }
-      // this trip's slots: even lanes {w, vrow}, odd lanes the key, every lane its V share
-      float2 eh[NB];
-      float4 v[NB][CPL / 4];
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
-        eh[t] = *reinterpret_cast<const float2*>(sl + ((l & 1) ? 6 : 0));
-#pragma unroll
-        for (int m = 0; m < CPL / 4; ++m)
-          v[t][m] = *reinterpret_cast<const float4*>(sl + 8 + CPL * l + 4 * m);
-      }
-      // the next trip's ids, in flight beside the slots
-      const uint64_t jn = j0 + NB;
-      if (jn < o1) {
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
-          const uint64_t jj = jn + t < o1 ? jn + t : o1 - 1;
-          idn[t] = a.index[jj];
-          if (valued) xn[t] = a.val[jj];
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
-        uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
-        float w = __shfl(eh[t].x, gbase, kWave);
-        int vr = __float_as_int(__shfl(eh[t].y, gbase, kWave));
-        float vk[CPL];
-#pragma unroll
-        for (int m = 0; m < CPL / 4; ++m) {
-          vk[4 * m] = v[t][m].x; vk[4 * m + 1] = v[t][m].y;
-          vk[4 * m + 2] = v[t][m].z; vk[4 * m + 3] = v[t][m].w;
-        }
-        if (ek != key[t] && ek != kEmptyKey) {  // a longer probe chain (group-uniform)
-          uint64_t h = tbl_hash(key[t], a.T);
-          for (uint64_t probe = 0; ek != key[t] && ek != kEmptyKey && probe < a.T.mask; ++probe) {
-            h = (h + 1) & a.T.mask;
-            ek = ent_at(a.T, h)->key;
-          }
-          if (ek == key[t]) {
-            const Entry* e = ent_at(a.T, h);
-            w = e->w;
-            vr = e->vrow;
-            load_coords<CPL, true>(reinterpret_cast<const float*>(e) + 8, l, 16, vk);
-          }
-        }
-        // absent (inserted by this training step's backward): w = 0, no V
-        if (ek != key[t]) { w = 0.f; vr = -1; }
-        // V is visible only if present and not (l1_shrk && w == 0) (sgd_updater.cc:40-43)
-        const bool vok = vr >= 0 && !(a.l1_shrk && w == 0.f);
-        if (t < nin) {
-          const float x = xm[t];
-          // SpMV::Times skips w == 0 (spmv.h:124-125)
-          if (w != 0.f) acc = valued ? acc + w * x : acc + w;
-          if (vok) {
-            const float xx = x * x;  // XX_ (fm_loss.h:86-92)
-#pragma unroll
-            for (int k = 0; k < CPL; ++k) {
-              xv[k] = valued ? xv[k] + vk[k] * x : xv[k] + vk[k];
-              const float q = vk[k] * vk[k];  // VV (fm_loss.h:95-101)
-              xxvv[k] = valued ? xxvv[k] + q * xx : xxvv[k] + q;
-            }
-          }
-        }
-      }
-    }
-    // s = sum_l (XV_l^2 - XXVV_l), serially over l = 0..15 (fm_loss.h:110-113)
-    float tt[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) tt[k] = xv[k] * xv[k] - xxvv[k];
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < G; ++q) {
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) s += __shfl(tt[k], gbase + q, kWave);
-    }
-    double y = (double)acc + .5 * (double)s;  // float += double (fm_loss.h:114)
-    float pr = (float)y;
-    pr = pr > 20.f ? 20.f : (pr < -20.f ? -20.f : pr);  // clip (fm_loss.h:118)
-    const float p = logit_p(a.label[r], pr, a.rw, r);
-    const int64_t xs = a.xs > 16 ? a.xs : 16;
-    if (l == 0) {
-      a.p_out[r] = p;
-      if (xs > 16) a.XVp[r * xs + 16] = p;
-      a.pred[r] = pr;
-      double yy = a.label[r] > 0 ? 1.0 : -1.0;
-      loss = log(1.0 + exp(-yy * (double)pr));  // Loss::Evaluate (loss.h:57-66)
-      if (a.auc_key) {  // the AUC lane's snapshot: orderable key of pred, label > 0
-        uint32_t u = __float_as_uint(pr + 0.0f);  // -0 == +0, as operator< sees them
-        a.auc_key[r] = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-        a.auc_lab[r] = a.label[r] > 0 ? 1u : 0u;
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < CPL / 4; ++m)  // XV_ *= p (fm_loss.h:196-199)
-      *reinterpret_cast<float4*>(a.XVp + r * xs + CPL * l + 4 * m) =
-          make_float4(xv[4 * m] * p, xv[4 * m + 1] * p, xv[4 * m + 2] * p, xv[4 * m + 3] * p);
-  }
-  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off, kWave);
-  if (lane_id() == 0) red[threadIdx.x / kWave] = loss;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double s = 0;
-    for (int i = 0; i < kFmNT / kWave; ++i) s += red[i];
-    a.loss_part[blockIdx.x] = s;
-  }
 }
 
 // Lane layout for V_dim d.  vec: float4 chunks (the fused path's 16-byte aligned rows, d a
@@ -1099,69 +726,24 @@ int launch_fwd_fused(const FwdArgs& a, hipStream_t st, int* nblk, bool spread) {
   // fat slots: one trip per nnz (G lanes x float4 = d exactly; even / odd lanes hold the
   // entry's halves, so G >= 2: d = 8 and 16 — other fat V_dims take the probe walk below)
   const bool fat = a.T.es != 0 && !a.no_fat_fwd && vec && CPL == 4 && 4 * G == a.d && G >= 2;
-  if (a.index && a.B > 0 && spread && fat && G == 4 && !a.part && a.fwd_lanes) {
-    // the prefetching form (kwarg fwd_lanes): G' lanes per row
-    const int G2 = a.fwd_lanes;
-    *nblk = (int)((a.B + kFmNT / G2 - 1) / (kFmNT / G2));
-    const dim3 grid((unsigned)*nblk);
-#define DFX_FWDPF(GG, NN)                                                              \
-    if (G2 == GG && a.fat_nb == NN) {                                                  \
-      if (a.val)                                                                       \
-        hipLaunchKernelGGL((k_fm_fwd_fat_pf<GG, NN, true>), grid, dim3(kFmNT), 0, st, a); \
-      else                                                                             \
-        hipLaunchKernelGGL((k_fm_fwd_fat_pf<GG, NN, false>), grid, dim3(kFmNT), 0, st, a); \
-      DFX_HIP(hipGetLastError());                                                      \
-      return DFX_OK;                                                                   \
-    }
-    DFX_FWDPF(2, 4) DFX_FWDPF(2, 6) DFX_FWDPF(2, 8) DFX_FWDPF(4, 4) DFX_FWDPF(4, 6)
-    DFX_FWDPF(4, 8)
-#undef DFX_FWDPF
-    set_error("fwd_lanes 2 | 4 with fat_nb 4 | 6 | 8");
-    return DFX_ERR_ARG;
-  }
-  if (a.index && a.B > 0 && spread && fat && G == 4 && a.fwd_tile && a.slice_len <= 0) {
-    // the tiled gather forward, on a resident grid (its blocks loop over tiles)
-    const int64_t ntiles = (a.B + kFtRows - 1) / kFtRows;
-    if (a.val) {
-      *nblk = (int)resident_grid<k_fm_fwd_tile<true>>(ntiles);
-      hipLaunchKernelGGL(k_fm_fwd_tile<true>, dim3((unsigned)*nblk), dim3(kFmNT), 0, st, a);
-    } else {
-      *nblk = (int)resident_grid<k_fm_fwd_tile<false>>(ntiles);
-      hipLaunchKernelGGL(k_fm_fwd_tile<false>, dim3((unsigned)*nblk), dim3(kFmNT), 0, st, a);
-    }
-    DFX_HIP(hipGetLastError());
-    return DFX_OK;
-  }
   if (a.index && a.B > 0 && spread && fat) {
-    const dim3 grid((unsigned)*nblk);
-    // the staged-ids forms on a resident grid (their groups loop over rows): *nblk loss partials
-#define DFX_FWDIDS(NN)                                                                    \
-    if (G == 4 && a.fat_nb == NN && a.fwd_ids) {                                          \
-      *nblk = (int)resident_grid<k_fm_fwd_fat<4, NN, true>>(*nblk);                       \
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, NN, true>), dim3((unsigned)*nblk), dim3(kFmNT), 0, \
-                         st, a);                                                          \
+    // the fat forward (k_fm_fwd_walk), on a resident grid (its groups loop over rows)
+#define DFX_FWDWALK(GG)                                                                   \
+    if (G == GG) {                                                                        \
+      if (a.val) {                                                                        \
+        *nblk = (int)resident_grid<k_fm_fwd_walk<GG, true>>(*nblk);                       \
+        hipLaunchKernelGGL((k_fm_fwd_walk<GG, true>), dim3((unsigned)*nblk), dim3(kFmNT), 0, \
+                           st, a);                                                        \
+      } else {                                                                            \
+        *nblk = (int)resident_grid<k_fm_fwd_walk<GG, false>>(*nblk);                      \
+        hipLaunchKernelGGL((k_fm_fwd_walk<GG, false>), dim3((unsigned)*nblk), dim3(kFmNT), \
+                           0, st, a);                                                     \
+      }                                                                                   \
       DFX_HIP(hipGetLastError());                                                         \
       return DFX_OK;                                                                      \
     }
-    if (G == 4 && a.fat_nb == 8 && a.fwd_ids && a.fwd_pf) {
-      *nblk = (int)resident_grid<k_fm_fwd_fat<4, 8, true, true>>(*nblk);
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true, true>), dim3((unsigned)*nblk), dim3(kFmNT), 0,
-                         st, a);
-      DFX_HIP(hipGetLastError());
-      return DFX_OK;
-    }
-    DFX_FWDIDS(6) DFX_FWDIDS(8) DFX_FWDIDS(12)
-#undef DFX_FWDIDS
-    if (G == 2) hipLaunchKernelGGL((k_fm_fwd_fat<2, 8>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 4)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 4>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 6)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 6>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4 && a.fat_nb == 12)
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 12>), grid, dim3(kFmNT), 0, st, a);
-    else if (G == 4) hipLaunchKernelGGL((k_fm_fwd_fat<4, 8>), grid, dim3(kFmNT), 0, st, a);
-    DFX_HIP(hipGetLastError());
-    if (G == 2 || G == 4) return DFX_OK;
+    DFX_FWDWALK(2) DFX_FWDWALK(4)
+#undef DFX_FWDWALK
   }
   if (a.index && spread && a.d == 0 && a.lr_lanes && a.B > 0 && !a.part) {
     // LR (V_dim 0): four lanes per row, each finding a quarter of a 32-nnz chunk's entries with

@@ -65,12 +65,7 @@ struct FwdArgs {
   int keys_ready;
   int part_n;      // owners of the split step (the partial's layout, split_part_floats)
   int no_fat_fwd;  // fat slots: the split forward walk instead of the one-trip read (A/B)
-  int fat_nb;      // fat forward: nnz per trip at V_dim 16 (kwarg fat_nb = 4 | 6 | 8 | 12)
   int cpl;         // kwarg fwd_cpl: V coordinates per lane of the probe forward (0 / 4, or 8)
-  int fwd_lanes;   // V_dim 16 fat slots: k_fm_fwd_fat_pf with this many lanes per row (0: off)
-  int fwd_ids;     // fat slots: the row's ids staged in LDS first (kwarg fwd_ids)
-  int fwd_pf;      // fwd_ids, fat_nb 8: the next row's offsets and ids prefetched (kwarg fwd_pf)
-  int fwd_tile;    // fat slots at V_dim 16: the tiled gather forward (kwarg fwd_tile)
   int lr_lanes;    // V_dim 0: four lanes per row (kwarg lr_lanes)
   float* part;
   int nt;  // kwarg nt: kNtFwdTable = the slots with the streaming policy

@@ -221,21 +221,15 @@ struct Context {
   int fat_fwd = 1;    // kwarg fat_fwd
   int fat_bwd = 1;    // kwarg fat_bwd
   int initv_onepass = 1;  // kwarg initv_onepass
-  int fat_nb = 8;         // kwarg fat_nb
   int fwd_cpl = 8;        // kwarg fwd_cpl: V coordinates per lane of the probe forward
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 1;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
   int bwd_cpl = 8;        // kwarg bwd_cpl: coordinates per lane of the fused backward, d >= 64
   int bwd_cpl_from = 64;  // kwarg bwd_cpl_from: the least V_dim bwd_cpl = 8 applies to
   int loc_x_payload = 1;    // kwarg loc_xpay: valued data carries x, not the position
-  int fwd_lanes = 0;      // kwarg fwd_lanes
-  int fwd_ids = 1;        // kwarg fwd_ids
-  int fwd_pf = 1;         // kwarg fwd_pf
-  int fwd_tile = 0;       // kwarg fwd_tile (fm.hip k_fm_fwd_tile)
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
   int auc_db = 2;          // kwarg auc_db (step.hip): double-buffered AUC snapshot (2: B <= 12288)
-  int auc_after = 0;       // kwarg auc_lane=after (step.hip): the AUC lane after the backward
   int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
   int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_hnt = 0;         // kwarg lb_hnt: the bucket Localizer's histogram / scatter block (0 auto)

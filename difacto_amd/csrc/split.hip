@@ -506,10 +506,7 @@ int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nr
     a.index = c->split_keys[slot]; a.max_index = ~0ull; a.keys_ready = 1;
     a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad; a.d = c->P.V_dim;
     a.no_fat_fwd = !c->fat_fwd;
-    a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
-    a.fwd_ids = c->fwd_ids;
-    a.fwd_pf = c->fwd_pf;
-    a.fwd_tile = c->fwd_tile;
+    a.cpl = c->fwd_cpl;
     a.part = part_out;
     a.part_n = (int)c->T.range_mul;  // the owners (dfx_split_owner_begin's table_set_ranges)
     if (sliced) {

@@ -90,9 +90,7 @@ int auc_reserve(Workspace& w, int64_t rows, hipStream_t st) {
 
 // the fused step's AUC snapshot double-buffered at this batch size (kwarg auc_db)
 static bool auc_db_on(const Context* c, int64_t rows) {
-  // (auc_lane=after: the lane of step t runs beside step t + 1's forward, whose snapshot must
-  // go to the other buffer)
-  return c->auc_after || c->auc_db == 1 || (c->auc_db == 2 && rows <= kAucBlockMax);
+  return c->auc_db == 1 || (c->auc_db == 2 && rows <= kAucBlockMax);
 }
 
 int step_reserve(Context* c, int64_t rows, int64_t nnz) {
@@ -335,11 +333,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   }
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.no_fat_fwd = !c->fat_fwd;
-  a.fat_nb = c->fat_nb; a.cpl = c->fwd_cpl;
-  a.fwd_lanes = c->fwd_lanes;
-  a.fwd_ids = c->fwd_ids;
-  a.fwd_pf = c->fwd_pf;
-  a.fwd_tile = c->fwd_tile;
+  a.cpl = c->fwd_cpl;
   a.lr_lanes = c->lr_lanes;
   a.nt = c->nt_mask;
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
@@ -356,19 +350,14 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   prof_mark(c, 4);
   // (the forward's loss partials are summed by k_step_finalize, the step's last kernel)
 
-  // ---- aux lane: AUC of this batch's predictions, beside the backward (or, auc_lane=after,
-  // once the backward is done: beside the next step's forward)
-  auto aux_lane = [&]() -> int {
-    DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
-    DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
-    lane_mark(c, 2, c->aux_stream);
-    if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
-    lane_mark(c, 3, c->aux_stream);
-    DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
-    DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
-    return DFX_OK;
-  };
-  if (!c->auc_after) DFX_TRY(aux_lane());
+  // ---- aux lane: AUC of this batch's predictions, beside the backward
+  DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
+  DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
+  lane_mark(c, 2, c->aux_stream);
+  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
+  lane_mark(c, 3, c->aux_stream);
+  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
+  DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
   prof_mark(c, 5);
 
   if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
@@ -397,7 +386,6 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   } else {
     prof_mark(c, 6);
   }
-  if (c->auc_after) DFX_TRY(aux_lane());
   const bool initv = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 && d > 0;
   unsigned long long* cap_host = nullptr;
   DFX_TRY(cap_record_slot(c, &cap_host));

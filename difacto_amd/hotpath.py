@@ -47,7 +47,8 @@ class Context:
         self.device = torch.device("cuda", device)
         self.kwargs = dict(kwargs)
         h = ctypes.c_void_p()
-        check(_lib.lib().dfx_ctx_create(device, _kwstr(kwargs), ctypes.byref(h)))
+        # strict: a misspelt or retired kwarg raises instead of running the default
+        check(_lib.lib().dfx_ctx_create(device, _kwstr(dict(kwargs, strict=1)), ctypes.byref(h)))
         self.h = h
         self.V_dim = _lib.lib().dfx_ctx_vdim(h)
         self.use_current_stream()

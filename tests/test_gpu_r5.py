@@ -1,11 +1,12 @@
 """Round-5 GPU tests: the kernels added this round against the oracle and the kernels they
 replace.
 
-* k_fm_fwd_tile (context kwarg fwd_tile): the tiled gather forward at V_dim 16 sums each row in
-  the reference's (row, nnz) order (fm_loss.h:67-119) from LDS, so predictions must be
-  BIT-identical to the row-walking forward's and to the oracle's, and the trained model the
-  same.  Ragged rows cover the chunk edges: empty rows, rows longer than a chunk (512 nnz),
-  rows crossing chunk and tile edges, and the last partial tile.
+* k_fm_fwd_walk (the fat-slot forward at V_dim 8 / 16): each row's slots read kWkNB per trip
+  from ids staged in LDS, summed in the reference's (row, nnz) order (fm_loss.h:67-119), so
+  predictions must be BIT-identical to the oracle's and to the probe walk's (fat_fwd=0: the
+  entry, then V, per nnz), and the trained model the same.  Ragged rows cover the staging
+  edges: empty rows, rows longer than a staged chunk (40 ids), a row of 1300 nnz, and rows
+  the resident grid's groups reach on their second and third pass (80 k rows).
 """
 import numpy as np
 import pytest
@@ -43,13 +44,13 @@ def _long_rows(blk, lens, binary, seed):
                       None if binary else np.concatenate(vals), np.concatenate(labels))
 
 
-@pytest.mark.parametrize("rows", [3001, 80001])
+@pytest.mark.parametrize("rows,d", [(3001, 16), (80001, 16), (3001, 8)])
 @pytest.mark.parametrize("binary", [True, False])
-def test_tile_forward_bit_identical(H, rows, binary):
-    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+def test_walk_forward_bit_identical(H, rows, d, binary):
+    cfg = dict(V_dim=d, V_threshold=0, l1=0, lr=.1, V_lr=.01)
     ks, mk = (1 << 15, 1 << 16) if rows < 10000 else (1 << 20, 1 << 21)
-    ca = H.Context(0, max_keys=mk, **cfg)              # the row-walking fat forward
-    cb = H.Context(0, max_keys=mk, fwd_tile=1, **cfg)  # the tiled gather forward
+    ca = H.Context(0, max_keys=mk, fat_fwd=0, **cfg)  # the probe walk: entry, then V
+    cb = H.Context(0, max_keys=mk, **cfg)             # the fat walk (k_fm_fwd_walk)
     up = O.Updater(**cfg)
     for step in range(4):
         blk = D.synthetic(rows, 39, ks, binary=binary, ragged=True, seed=60 + step)
@@ -76,35 +77,5 @@ def test_tile_forward_bit_identical(H, rows, binary):
     vb, lb = H.Store(cb).pull(cb.tensor(uniq, torch.int64))
     assert np.array_equal(la.cpu().numpy(), lb.cpu().numpy())
     assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
-    ca.close()
-    cb.close()
-
-
-@pytest.mark.parametrize("rows", [6000, 40000])
-def test_auc_lane_after_backward(H, rows):
-    """auc_lane=after: the AUC lane of step t starts after step t's backward, on a double-
-    buffered snapshot (step t + 1's forward writes the other buffer).  Progress (loss, AUC) and
-    predictions equal the default schedule's exactly at every step (same kernels, same sums);
-    the one-block AUC (<= 12288 rows) and the radix lane are both covered; a validation step in
-    between reads the same snapshot machinery without a backward."""
-    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
-    ca = H.Context(0, max_keys=1 << 20, **cfg)
-    cb = H.Context(0, max_keys=1 << 20, auc_lane="after", **cfg)
-    up = O.Updater(**cfg)
-    for step in range(6):
-        blk = D.synthetic(rows, 39, 1 << 18, seed=80 + step)
-        job = H.kValidation if step == 3 else H.kTraining
-        pa = torch.zeros(blk.size, dtype=torch.float32, device=ca.device)
-        pb = torch.zeros(blk.size, dtype=torch.float32, device=cb.device)
-        H.train_step(ca, H.DeviceRowBlock(ca, blk), job, push_cnt=(step == 0), pred=pa)
-        H.train_step(cb, H.DeviceRowBlock(cb, blk), job, push_cnt=(step == 0), pred=pb)
-        if job == H.kTraining:
-            loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
-                                             push_cnt=(step == 0), want_pred=True)
-        qa, qb = H.progress(ca), H.progress(cb)
-        assert np.array_equal(pa.cpu().numpy().view(np.uint32), pb.cpu().numpy().view(np.uint32))
-        assert qa["loss"] == qb["loss"] and qa["auc"] == qb["auc"], (step, qa, qb)
-        if job == H.kTraining:
-            assert abs(qb["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
     ca.close()
     cb.close()
