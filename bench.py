@@ -193,12 +193,15 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
 
 PMC_ROUND = "r4"
 
-# Random 128-byte chunks per second on MI355X, measured in isolation (tools/membench/pmccal,
-# DESIGN.md (d)): reads of distinct random rows, and read-modify-writes of them
-CHUNK_READS_PER_S = 45.5e9
-CHUNK_RMW_PER_S = 17.9e9
-STREAM_BYTES_PER_S = 5.0e12  # the Localizer lane's sequential passes (~0.4 GB per C3 step)
-LOC_BYTES_PER_NNZ = 104.0    # its traffic per nnz (profiles/r2c: transform, 3 sort passes, write)
+# Random 128-byte lines per second on MI355X in the step's own access patterns, measured alone
+# with cold caches (tools/membench/spanbench, profiles/r5/spanbench_cold.txt): the forward's
+# read of 3.9 M random fat slots (84.3 us), the backward's read-modify-write of 3.48 M sorted
+# keys' slot + Vaux row (329.3 us: 2 lines per key; in one 256-B span the same 331 us, so two
+# lines per key is this layout's floor)
+CHUNK_READS_PER_S = 46.2e9
+CHUNK_RMW_PER_S = 21.1e9
+STREAM_BYTES_PER_S = 5.0e12  # the Localizer lane's streaming passes
+LOC_BYTES_PER_NNZ = 70.0     # the bucket Localizer's traffic per nnz (profiles/r4 PMC: ~273 MB)
 
 
 def chunk_model(nnz, U, ms_per_step):
@@ -208,23 +211,27 @@ def chunk_model(nnz, U, ms_per_step):
     floor_ms = (nnz / CHUNK_READS_PER_S + 2 * U / CHUNK_RMW_PER_S
                 + nnz * LOC_BYTES_PER_NNZ / STREAM_BYTES_PER_S) * 1e3
     return {"floor_ms": round(floor_ms, 4), "frac": round(floor_ms / ms_per_step, 3),
-            "source": "tools/membench/pmccal rates; DESIGN.md (d)"}  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
+            "source": "tools/membench/spanbench cold-cache line rates; DESIGN.md (d)"}  # the profiles/<round>/ the traffic figures come from (tools/profile.sh)
 
 
-def pmc_traffic(kernel_prefix, fname="pmc_hbm.json"):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/<PMC_ROUND>/<fname>: FETCH_SIZE + WRITE_SIZE, separate --pmc runs of this bench,
-    tools/profile.sh).  None when absent."""
+def pmc_traffic(prefixes, fname="pmc_hbm.json"):
+    """HBM bytes per step of a phase's kernels (every kernel whose name starts with one of
+    prefixes, e.g. the backward phase's k_fm_bwd* and k_chunk_hotsum) from the committed
+    rocprofv3 PMC passes (profiles/<PMC_ROUND>/<fname>: FETCH_SIZE + WRITE_SIZE per dispatch,
+    separate --pmc runs of this bench, tools/profile.sh).  None when absent."""
     path = os.path.join(ROOT, "profiles", PMC_ROUND, fname)
     try:
         with open(path) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    for name, v in ks.items():
-        if name.startswith(kernel_prefix):
-            return int((v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]) * 1024)
-    return None
+    if isinstance(prefixes, str):
+        prefixes = (prefixes,)
+    hit = [v for name, v in ks.items() if name.startswith(prefixes)]
+    if not hit:
+        return None
+    return int(sum(v["fetch_size_kb_per_dispatch"] + v["write_size_kb_per_dispatch"]
+                   for v in hit) * 1024)
 
 
 def pmc_requests(kernel_prefix, fname="pmc_requests.json"):
@@ -519,8 +526,8 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("k_fm_bwd" if dom == "backward_update"
-                                            else "k_fm_fwd",
+                     "traffic": pmc_traffic(("k_fm_bwd", "k_chunk_hotsum")
+                                            if dom == "backward_update" else "k_fm_fwd",
                                             "pmc_hbm.json" if args.config == "c3"
                                             else "pmc_hbm_%s.json" % args.config),
                      "traffic_source": "profiles/%s/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
@@ -550,6 +557,18 @@ def main():
         "train_auc": round(prog["auc"] / max(prog["nrows"], 1), 6),
         "model_keys": st["n_keys"], "model_vrows": st["n_vrows"],
     }
+    if dom == "backward_update" and args.config == "c3":
+        # the ceiling of this kernel is the random-line rate, not the byte peak: a key's 144 B
+        # of hot state (entry 16, V 64, Vaux 64) is 2 random 128-B line read-modify-writes,
+        # and two lines in one 256-B span cost the same as two unrelated ones
+        # (tools/membench/spanbench, profiles/r5/spanbench_cold.txt)
+        lines = 2 * mean_u / (max(per_launch_ms[dom], 1e-9) * 1e-3)
+        out["roofline"]["line_roofline"] = {
+            "bound": "random 128-B line read-modify-writes", "achieved": round(lines / 1e9, 2),
+            "peak": round(CHUNK_RMW_PER_S / 1e9, 2), "unit": "G lines/s",
+            "frac": round(lines / CHUNK_RMW_PER_S, 4),
+            "source": "tools/membench/spanbench (cold caches): 3.48 M sorted keys x 2 lines in "
+                      "329 us alone; a 256-B-span layout 331 us"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
@@ -874,7 +893,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         # backward formula over the owner's rows, keys and unique keys)
         ab = algorithmic_bytes(o_rows, o_nnz, o_uniq, d)["backward_update"]
         rkernel = "owner_backward (split: fused backward + FTRL/AdaGrad + InitV, rank 0)"
-        traffic, tsrc = (pmc_traffic("k_fm_bwd", "pmc_hbm_split.json"),
+        traffic, tsrc = (pmc_traffic(("k_fm_bwd", "k_chunk_hotsum"), "pmc_hbm_split.json"),
                          "profiles/%s/pmc_hbm_split.json (rocprofv3 FETCH_SIZE + WRITE_SIZE "
                          "per launch of the owner's backward, bench.py --sharded)" % PMC_ROUND)
     else:
