@@ -962,7 +962,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
       // chunk order, all in double and rounded once — the sums differ from the reference's
       // sequential float sums only by that float rounding (reordering error)
       const uint32_t c0 = a.choff[u];
-      const uint32_t nc = hot_chunks_read(seg_chunks(len, a.ntiles));
+      const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
       const int P = d + 2;
       double gwd = 0, xxpd = 0, accp[CPL];
 #pragma unroll
@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
       float gw = 0.f, xxp = 0.f;
       if (a.choff && len > (uint32_t)kChunkOcc) {
         const uint32_t c0 = a.choff[u];
-        const uint32_t nc = hot_chunks_read(seg_chunks(len, a.ntiles));
+        const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
         double gwd = 0, xxpd = 0;
         for (uint32_t c = 0; c < nc; ++c) {
           const double* pc = a.part + (int64_t)(c0 + c) * (d + 2);
@@ -1410,7 +1410,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
     // grad_u = (g0 - V*XXp) + sum (XV_ p) x, g0 = 0 (fm_loss.h:185-202, spmm.h:127-159)
     if (a.choff && len > (uint32_t)kChunkOcc) {
       const uint32_t c0 = a.choff[u];
-      const uint32_t nc = hot_chunks_read(seg_chunks(len, a.ntiles));
+      const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
       double accp[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) accp[k] = 0;
@@ -1464,12 +1464,20 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
   }
 }
 
-// a chunk's partial {g_w, XXp, sum (XV p) x} over its occurrences [s0, s1) in order (the same
-// terms as k_fm_bwd's walk), by one group of G lanes, written to chunk ch's slot
-template <int G, int CPL, bool VEC>
-__device__ __forceinline__ void chunk_partial(const BwdArgs& a, uint32_t s0, uint32_t s1, int l,
-                                              int64_t ch) {
+// one group per chunk of a long segment: partial {g_w, XXp, sum (XV p) x} over its
+// kChunkOcc occurrences in order (the same terms as k_fm_bwd's walk)
+template <int G, int CPL, bool VEC = false>
+__global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
+  constexpr int CPB = kFmNT / G;
   constexpr int UNR = 4;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t ch = (int64_t)blockIdx.x * CPB + g;
+  if (ch >= (int64_t)*a.nchunks) return;
+  const uint32_t u = a.chunk_seg[ch];
+  const uint32_t s0 = a.segstart[u] + (uint32_t)(ch - a.choff[u]) * kChunkOcc;
+  const uint32_t send = a.segstart[u + 1];
+  const uint32_t s1 = s0 + kChunkOcc < send ? s0 + kChunkOcc : send;
   const bool valued = a.occ_x != nullptr;
   const int d = a.d;
   const int64_t xs = a.xs > d ? a.xs : d;
@@ -1551,49 +1559,6 @@ __device__ __forceinline__ void chunk_partial(const BwdArgs& a, uint32_t s0, uin
   }
 }
 
-// one group per occurrence chunk of a long segment: kChunkOcc consecutive occurrences (tile
-// chunks are k_fm_bwd_tchunks')
-template <int G, int CPL, bool VEC = false>
-__global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
-  constexpr int CPB = kFmNT / G;
-  const int g = threadIdx.x / G;
-  const int l = threadIdx.x % G;
-  const int64_t ch = (int64_t)blockIdx.x * CPB + g;
-  if (ch >= (int64_t)*a.nchunks) return;
-  const uint32_t u = a.chunk_seg[ch];
-  const uint32_t seg0 = a.segstart[u], send = a.segstart[u + 1];
-  if (seg_tiled(send - seg0, a.ntiles)) return;  // group-uniform
-  const uint32_t s0 = seg0 + (uint32_t)(ch - a.choff[u]) * kChunkOcc;
-  const uint32_t s1 = s0 + kChunkOcc < send ? s0 + kChunkOcc : send;
-  chunk_partial<G, CPL, VEC>(a, s0, s1, l, ch);
-}
-
-// The tile chunks (internal.h kTileRows): row tile T goes to XCD T % 8 (a block's XCD is its
-// index mod 8), and an XCD's groups take its (tile, tile-chunked key) pairs tile-major, so the
-// groups working at once share a few tiles' [XV*p | p] rows in that XCD's L2.  Each pair's
-// occurrences are the key's in rows [T kTileRows, (T + 1) kTileRows), summed in order.
-constexpr int kTcBlocksPerXcd = 64;
-template <int G, int CPL, bool VEC = false>
-__global__ __launch_bounds__(kFmNT) void k_fm_bwd_tchunks(BwdArgs a) {
-  constexpr int CPB = kFmNT / G;
-  const uint32_t H = *a.ntkeys;
-  if (H == 0u) return;
-  const int g = threadIdx.x / G;
-  const int l = threadIdx.x % G;
-  const uint32_t x = blockIdx.x % 8u, i = blockIdx.x / 8u;
-  const uint32_t nbx = gridDim.x / 8u;
-  const uint32_t tiles_x = a.ntiles > x ? (a.ntiles - x + 7u) / 8u : 0u;  // this XCD's tiles
-  const uint64_t pairs = (uint64_t)tiles_x * H;
-  for (uint64_t q = (uint64_t)i * CPB + g; q < pairs; q += (uint64_t)nbx * CPB) {
-    const uint32_t T = x + 8u * (uint32_t)(q / H);
-    const uint32_t u = a.tkeys[q % H];
-    const uint32_t c = a.choff[u] + T;
-    const uint32_t s0 = a.tstart[c];
-    const uint32_t s1 = T + 1u < a.ntiles ? a.tstart[c + 1] : a.segstart[u + 1];
-    chunk_partial<G, CPL, VEC>(a, s0, s1, l, (int64_t)c);
-  }
-}
-
 // A key of >= kHotChunks chunks (the hottest keys of a skewed batch: C5's top key has ~1750)
 // gets its chunk partials summed by a block of its own, one thread per partial value, in chunk
 // order in double — exactly the sequence the backward's per-key combine would add — and the
@@ -1601,14 +1566,14 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_tchunks(BwdArgs a) {
 // (0 + total = total: bit-identical).  Without it one group walked all of a hot key's chunks
 // serially, a memory round trip per chunk, the backward's longest chain.
 __global__ __launch_bounds__(256) void k_chunk_hotsum(BwdArgs a) {
-  const int64_t nch = (int64_t)*a.nchunks;
-  for (int64_t ch = blockIdx.x; ch < nch; ch += gridDim.x) {  // block-uniform
+  const int64_t ch = blockIdx.x;
+  if (ch >= (int64_t)*a.nchunks) return;
   const uint32_t u = a.chunk_seg[ch];
   const uint32_t c0 = a.choff[u];
-  if ((uint32_t)ch != c0) continue;
+  if ((uint32_t)ch != c0) return;
   const uint32_t len = a.segstart[u + 1] - a.segstart[u];
-  const uint32_t nc = seg_chunks(len, a.ntiles);
-  if (nc < kHotChunks) continue;
+  const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+  if (nc < kHotChunks) return;
   const int P = a.d + 2;
   constexpr int U = 16;
   for (int j = threadIdx.x; j < P; j += blockDim.x) {
@@ -1625,7 +1590,6 @@ __global__ __launch_bounds__(256) void k_chunk_hotsum(BwdArgs a) {
     for (; c < nc; ++c) s += pj[(int64_t)c * P];
     a.part[(int64_t)c0 * P + j] = s;
   }
-  }
 }
 
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, bool aligned) {
@@ -1637,17 +1601,12 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, boo
   lanes_for(a.d, aligned && a.d >= 64, &G, &CPL, &vec);
   const int64_t cpb = kFmNT / G;
   dim3 grid((unsigned)((chunk_bound + cpb - 1) / cpb));
-  // the hot-key sums: a block per chunk slot, looping (most slots are not a hot key's first)
-  const unsigned hot_grid = (unsigned)std::min<int64_t>(chunk_bound, 4096);
 #define DFX_BWDC(GG, CC, VV)                                                              \
   if (G == GG && CPL == CC && vec == VV) {                                                \
     hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC, VV>), grid, dim3(kFmNT), 0, st, a);      \
-    if (a.ntiles >= 2 && a.tkeys)                                                         \
-      hipLaunchKernelGGL((k_fm_bwd_tchunks<GG, CC, VV>), dim3(8 * kTcBlocksPerXcd),       \
-                         dim3(kFmNT), 0, st, a);                                          \
     DFX_HIP(hipGetLastError());                                                           \
     if (chunk_bound >= (int64_t)kHotChunks) {                                             \
-      hipLaunchKernelGGL(k_chunk_hotsum, dim3(hot_grid), dim3(256), 0, st, a);            \
+      hipLaunchKernelGGL(k_chunk_hotsum, dim3((unsigned)chunk_bound), dim3(256), 0, st, a); \
       DFX_HIP(hipGetLastError());                                                         \
     }                                                                                     \
     return DFX_OK;                                                                        \
@@ -1949,9 +1908,7 @@ extern "C" int dfx_fm_calcgrad(dfx_ctx* ctx, int64_t B, int64_t nnz, const uint6
   uint32_t* choff = ws.col.as<uint32_t>();
   uint32_t* chunk_seg = ws.vpos.as<uint32_t>();
   uint32_t* nchunks = total + 1;
-  // (no row tiles here: dfx_fm_calcgrad's chunks are all occurrence chunks)
-  DFX_TRY(chunk_plan(main_lane(c), nnz, 0, ws.segstart.as<uint32_t>(), nullptr, nullptr, choff,
-                     chunk_seg, nchunks, nullptr, nullptr));
+  DFX_TRY(chunk_plan(main_lane(c), nnz, ws.segstart.as<uint32_t>(), choff, chunk_seg, nchunks));
   // 4) segmented reduction into grad
   BwdArgs b{};
   b.segstart = ws.segstart.as<uint32_t>();

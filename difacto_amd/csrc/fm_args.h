@@ -138,12 +138,6 @@ struct BwdArgs {
   const uint32_t* chunk_seg;
   const uint32_t* nchunks;
   double* part;
-  // tile chunks (internal.h kTileRows; ntiles 0: none): row tiles of the batch, the first
-  // occurrence of each tile chunk, the tile-chunked segments and their count (device)
-  uint32_t ntiles;
-  const uint32_t* tstart;
-  const uint32_t* tkeys;
-  const uint32_t* ntkeys;
   // wide V_dim, two passes (launch_bwd_fused with wsplit): a pass with one lane per key (entry,
   // g_w, FTRL) lists the keys whose V it must update {segment, V row, XXp}; a pass with G lanes
   // per listed key does the V sums and AdaGrad

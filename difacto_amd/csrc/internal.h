@@ -75,7 +75,6 @@ struct DevState {
   unsigned long long kmin, kmax, pk_min, pk_max;
   unsigned int pk_valid;
   unsigned int lb_over;  // buckets of this batch beyond the LDS sort's capacity (k_lb_colscan)
-  unsigned int n_tkeys;  // tile-chunked keys of this batch (chunk_plan; reset by the Localizer)
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
@@ -107,8 +106,6 @@ struct Workspace {
   // the bucket Localizer (locbucket.hip): per (tile, bucket) counts / prefixes, per bucket its
   // total and start; per item its row / position when the items are not packed (and scratch)
   DevBuf lbcnt, lbq;
-  // tile chunks (chunk_plan): each tile chunk's first occurrence, the tile-chunked segments
-  DevBuf tstart, tkeys;
   // pinned, written by the device: [0] buckets over the LDS capacity in the last bucket
   // Localizer of this workspace, [1] radix Localizers run since, [2] 1 packed / 2 not
   unsigned int* lb_hint = nullptr;
@@ -366,39 +363,12 @@ constexpr uint32_t kHotChunks = 8;
 __host__ __device__ inline uint32_t hot_chunks_read(uint32_t nc) {
   return nc >= kHotChunks ? 1u : nc;
 }
-// Tile chunks (the hottest keys of a skewed batch: more than kTileMinOcc occurrences per row
-// tile on average).  Such a key's chunk T covers its occurrences in rows [T kTileRows, (T + 1)
-// kTileRows) instead of kChunkOcc consecutive occurrences, and the tile chunks are walked tile
-// by tile, each tile on one XCD (fm.hip k_fm_bwd_tchunks): a tile's [XV*p | p] rows come from
-// the Infinity Cache / HBM once and then from that XCD's L2 for every hot key of the tile, where
-// occurrence chunks read a row per occurrence.  Still partials of consecutive occurrences in
-// row order, combined in order: deterministic.  ntiles = chunk_tiles(rows) (0: off).
-constexpr int kTileRows = 1024;
-constexpr uint32_t kTileMinOcc = 128;
-__host__ __device__ inline uint32_t chunk_tiles(int64_t rows) {
-  return rows > kTileRows ? (uint32_t)((rows + kTileRows - 1) / kTileRows) : 0u;
-}
-__host__ __device__ inline bool seg_tiled(uint32_t len, uint32_t ntiles) {
-  return ntiles >= 2 && len > (uint32_t)kChunkOcc && len > ntiles * kTileMinOcc;
-}
-// chunks of a segment of len occurrences (0: a short segment, summed by its own group)
-__host__ __device__ inline uint32_t seg_chunks(uint32_t len, uint32_t ntiles) {
-  if (len <= (uint32_t)kChunkOcc) return 0u;
-  return seg_tiled(len, ntiles) ? ntiles : (len + kChunkOcc - 1) / kChunkOcc;
-}
 // chunks of a batch, at most: a long segment of len > kChunkOcc occurrences has
-// ceil(len / kChunkOcc) <= len / kChunkOcc + 1 occurrence chunks or, tiled, ntiles < len /
-// kTileMinOcc, and there are at most nnz / (kChunkOcc + 1) long segments (the chunk partials,
-// the chunk -> segment table, the tile starts)
-inline int64_t max_chunks(int64_t nnz) {
-  return nnz / kTileMinOcc + nnz / (kChunkOcc + 1) + 2;
-}
-// rows: the batch's rows (the row tiles); occ_row / occ_rx: each occurrence's row, or (occ_rx
-// set) its input position whose row is occ_rx[position].x; tstart[c]: the first occurrence of
-// tile chunk c; tkeys[0 .. ds->n_tkeys): the tile-chunked segments (in no particular order)
-int chunk_plan(const Lane& L, int64_t nnz, int64_t rows, const uint32_t* segstart,
-               const uint32_t* occ_row, const uint2* occ_rx, uint32_t* choff, uint32_t* chunk_seg,
-               uint32_t* nchunks_dev, uint32_t* tstart, uint32_t* tkeys);
+// ceil(len / kChunkOcc) <= len / kChunkOcc + 1 of them, and there are at most
+// nnz / (kChunkOcc + 1) long segments (the chunk partials and the chunk -> segment table)
+inline int64_t max_chunks(int64_t nnz) { return nnz / kChunkOcc + nnz / (kChunkOcc + 1) + 2; }
+int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
+               uint32_t* chunk_seg, uint32_t* nchunks_dev);
 
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
 void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);

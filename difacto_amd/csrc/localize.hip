@@ -114,7 +114,6 @@ __global__ void k_loc_init(DevState* ds) {
   ds->or_mask = 0;
   ds->and_mask = ~0ull;
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
-  ds->n_tkeys = 0;
 }
 
 struct LocWriteArgs {
@@ -283,16 +282,15 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
-// ds->n_init is nonzero when the batch has long segments (reset by k_loc_init / k_lb_init,
-// raised by the heads / bucket kernels).  One launch: tiles of 2048 segments, taken by ticket;
-// per segment its chunk count (seg_chunks: occurrence chunks of kChunkOcc, or one per row tile
-// for the hottest keys, which are also listed in tkeys), their exclusive scan by decoupled
-// look-back (choff), the chunk -> segment table, the total.  With no long segment (uniform
-// keys) it writes the total 0 and exits.
+// ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
+// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments, taken by ticket;
+// per segment its chunk count
+// (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
+// (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
+// writes the total 0 and exits.
 __global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart, DevState* ds,
                                                        unsigned long long* stat, uint32_t* choff,
-                                                       uint32_t* chunk_seg, uint32_t* nchunks,
-                                                       uint32_t ntiles, uint32_t* tkeys) {
+                                                       uint32_t* chunk_seg, uint32_t* nchunks) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
   __shared__ uint32_t s_pre;
   if (ds->n_init == 0u) {
@@ -316,8 +314,7 @@ __global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart,
     cnt[i] = 0;
     if (base + i < U) {
       const uint32_t len = segstart[base + i + 1] - segstart[base + i];
-      cnt[i] = seg_chunks(len, ntiles);
-      if (seg_tiled(len, ntiles)) tkeys[atomicAdd(&ds->n_tkeys, 1u)] = (uint32_t)(base + i);
+      cnt[i] = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
     }
     s += cnt[i];
   }
@@ -335,38 +332,10 @@ __global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart,
   }
 }
 
-// the row of occurrence i (occ_rx: occ_row holds the input position, its row in occ_rx)
-__device__ inline uint32_t occ_row_of(const uint32_t* occ_row, const uint2* occ_rx, uint32_t i) {
-  const uint32_t r = occ_row[i];
-  return occ_rx ? occ_rx[r].x : r;
-}
-
-// tile chunk c of a tile-chunked segment: its first occurrence, the first one of the segment
-// (rows ascending) in row tile T or later — a binary search, one thread per chunk
-__global__ void k_tile_starts(const uint32_t* segstart, const uint32_t* choff,
-                              const uint32_t* chunk_seg, const uint32_t* nchunks,
-                              const uint32_t* occ_row, const uint2* occ_rx, uint32_t ntiles,
-                              uint32_t* tstart) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= (int64_t)*nchunks) return;
-  const uint32_t u = chunk_seg[c];
-  const uint32_t s0 = segstart[u], s1 = segstart[u + 1];
-  if (!seg_tiled(s1 - s0, ntiles)) return;
-  const uint32_t rlo = (uint32_t)(c - choff[u]) * (uint32_t)kTileRows;
-  uint32_t lo = s0, hi = s1;  // the first occurrence with row >= rlo in [s0, s1)
-  while (lo < hi) {
-    const uint32_t mid = lo + (hi - lo) / 2;
-    if (occ_row_of(occ_row, occ_rx, mid) < rlo) lo = mid + 1; else hi = mid;
-  }
-  tstart[c] = lo;
-}
-
-int chunk_plan(const Lane& L, int64_t nnz, int64_t rows, const uint32_t* segstart,
-               const uint32_t* occ_row, const uint2* occ_rx, uint32_t* choff, uint32_t* chunk_seg,
-               uint32_t* nchunks_dev, uint32_t* tstart, uint32_t* tkeys) {
+int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
+               uint32_t* chunk_seg, uint32_t* nchunks_dev) {
   if (nnz <= 0) {
     DFX_HIP(hipMemsetAsync(nchunks_dev, 0, sizeof(uint32_t), L.stream));
-    DFX_HIP(hipMemsetAsync(&L.ds->n_tkeys, 0, sizeof(uint32_t), L.stream));
     return DFX_OK;
   }
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
@@ -375,15 +344,8 @@ int chunk_plan(const Lane& L, int64_t nnz, int64_t rows, const uint32_t* segstar
   DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * ntiles));
   if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
     DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  const uint32_t rt = tstart && tkeys ? chunk_tiles(rows) : 0u;
   hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, segstart,
-                     L.ds, ws.hstat.as<unsigned long long>(), choff, chunk_seg, nchunks_dev, rt,
-                     tkeys);
-  if (rt >= 2) {
-    const int64_t cb = max_chunks(nnz);
-    hipLaunchKernelGGL(k_tile_starts, dim3((unsigned)((cb + 255) / 256)), dim3(256), 0, L.stream,
-                       segstart, choff, chunk_seg, nchunks_dev, occ_row, occ_rx, rt, tstart);
-  }
+                     L.ds, ws.hstat.as<unsigned long long>(), choff, chunk_seg, nchunks_dev);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -143,7 +143,6 @@ __global__ void k_lb_init(DevState* ds) {
   ds->kmin = ~0ull;
   ds->kmax = 0;
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
-  ds->n_tkeys = 0;
   ds->lb_over = 0;
   unsigned* meta = ds->sortmeta;
   meta[kSortMetaEpoch] = ++ds->sort_epoch;  // tags this Localizer's look-back words

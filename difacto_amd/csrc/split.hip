@@ -452,11 +452,8 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   o.keys_ready = true;
   DFX_TRY(localize_run(c, OL, R, nnz, offs, keys, ~0ull, o));
   // long segments (hot keys): their chunk plan, as the fused step's Localizer lane makes it
-  DFX_TRY(ows.tstart.ensure(max_chunks(nnz) * 4));
-  DFX_TRY(ows.tkeys.ensure((nnz / (kChunkOcc + 1) + 2) * 4));
-  DFX_TRY(chunk_plan(OL, nnz, R, o.segstart, o.occ_row, nullptr, ows.flags.as<uint32_t>(),
-                     ows.rowtmp.as<uint32_t>(), &OL.ds->totals[1], ows.tstart.as<uint32_t>(),
-                     ows.tkeys.as<uint32_t>()));
+  DFX_TRY(chunk_plan(OL, nnz, o.segstart, ows.flags.as<uint32_t>(), ows.rowtmp.as<uint32_t>(),
+                     &OL.ds->totals[1]));
   c->split_rows[slot] = R;
   c->split_nnz[slot] = nnz;
   c->split_keys[slot] = keys;
@@ -631,8 +628,6 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
     g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();
     g.nchunks = &ods->totals[1];
-    g.ntiles = chunk_tiles(c->split_rows[slot]); g.tstart = ows.tstart.as<uint32_t>();
-    g.tkeys = ows.tkeys.as<uint32_t>(); g.ntkeys = &ods->n_tkeys;
     DFX_TRY(ows.Vb.ensure((size_t)max_chunks(nnz) * (d + 2) * 8));
     g.part = ows.Vb.as<double>();
     DFX_TRY(bwd_two_pass_reserve(c, ows, nnz, &g));

@@ -65,8 +65,6 @@ int loc_reserve(Workspace& w, int64_t nnz, hipStream_t st) {
   DFX_TRY(w.uniq.ensure(nnz * 8));
   DFX_TRY(w.flags.ensure((nnz + 1) * 4));                   // chunk plan: choff
   DFX_TRY(w.rowtmp.ensure(max_chunks(nnz) * 4));      // chunk plan: chunk_seg
-  DFX_TRY(w.tstart.ensure(max_chunks(nnz) * 4));      // chunk plan: tile chunks' starts
-  DFX_TRY(w.tkeys.ensure((nnz / (kChunkOcc + 1) + 2) * 4));  // ... and their segments
   DFX_TRY(w.slot.ensure((nnz + 1) * 4));
   DFX_TRY(w.occ_row.ensure(nnz * 4));
   DFX_TRY(w.occ_x.ensure(nnz * 4));
@@ -297,8 +295,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
     c->loc_rowof[k] = rowof;
     // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
-    DFX_TRY(chunk_plan(LL, nnz, B, segstart, occ_row, rowof, choff, chunk_seg, nchunks,
-                       bw.tstart.as<uint32_t>(), bw.tkeys.as<uint32_t>()));
+    DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
     c->loc_done[k] = true;
   }
   lane_mark(c, 1, c->loc_stream);
@@ -373,8 +370,6 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.flags = flags; g.dsw = c->ds;
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
-    g.ntiles = chunk_tiles(B); g.tstart = bw.tstart.as<uint32_t>();
-    g.tkeys = bw.tkeys.as<uint32_t>(); g.ntkeys = &bds->n_tkeys;
     // (diagnostic, dfx_prof_enable_marks bit 9) the live-V key / occurrence counts
     const bool count_live = c->prof_n < c->prof_max && (c->prof_mask >> 9 & 1u);
     DFX_TRY(bwd_two_pass_reserve(c, ws, nnz, &g));
