@@ -1559,36 +1559,106 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
   }
 }
 
-// A key of >= kHotChunks chunks (the hottest keys of a skewed batch: C5's top key has ~1750)
-// gets its chunk partials summed by a block of its own, one thread per partial value, in chunk
-// order in double — exactly the sequence the backward's per-key combine would add — and the
-// total written over its first chunk's partial; the backward then reads that one partial
-// (0 + total = total: bit-identical).  Without it one group walked all of a hot key's chunks
-// serially, a memory round trip per chunk, the backward's longest chain.
-__global__ __launch_bounds__(256) void k_chunk_hotsum(BwdArgs a) {
-  const int64_t ch = blockIdx.x;
+// A key of >= kHotChunks chunks (the hottest keys of a skewed batch: C5's top key has ~3500
+// chunks of 128 occurrences) gets its chunk partials pre-summed in two fixed-shape levels, and
+// the total written over its first chunk's partial; the backward then reads that one partial.
+// Level 1 (k_chunk_hotgroup): a thread per (chunk, value) sums the kHotGroup chunks of its
+// group in chunk order into the group's first chunk.  Level 2 (k_chunk_hotsum): a wave per hot
+// key sums the group totals in R = 64 / (d + 2) interleaved slices, then the slices in order.
+// Both orders are fixed by the batch, in double: deterministic.  Round 4 walked all of a hot
+// key's partials serially (~110 round trips of 16 loads for the top key), C5's longest chain
+// after the chunks.
+constexpr int kHotGroup = 32, kHotNT = 1024, kHotGrid = 256;
+__global__ __launch_bounds__(256) void k_chunk_hotgroup(BwdArgs a) {
+  const int P = a.d + 2;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t ch = i / P;
+  const int j = (int)(i - ch * P);
   if (ch >= (int64_t)*a.nchunks) return;
   const uint32_t u = a.chunk_seg[ch];
   const uint32_t c0 = a.choff[u];
-  if ((uint32_t)ch != c0) return;
+  const uint32_t k = (uint32_t)ch - c0;
+  if (k % kHotGroup) return;
   const uint32_t len = a.segstart[u + 1] - a.segstart[u];
   const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
   if (nc < kHotChunks) return;
+  const uint32_t n = nc - k < (uint32_t)kHotGroup ? nc - k : (uint32_t)kHotGroup;
+  const double* pj = a.part + ch * P + j;
+  double v[kHotGroup];
+#pragma unroll
+  for (int q = 0; q < kHotGroup; ++q) v[q] = (uint32_t)q < n ? pj[(int64_t)q * P] : 0.0;
+  double s = 0;
+#pragma unroll
+  for (int q = 0; q < kHotGroup; ++q)
+    if ((uint32_t)q < n) s += v[q];
+  a.part[ch * P + j] = s;
+}
+__device__ inline void hotsum_key(const BwdArgs& a, uint32_t c0, uint32_t nc, double* part_w) {
   const int P = a.d + 2;
-  constexpr int U = 16;
-  for (int j = threadIdx.x; j < P; j += blockDim.x) {
-    const double* pj = a.part + (int64_t)c0 * P + j;
+  const uint32_t ng = (nc + kHotGroup - 1) / kHotGroup;  // group totals, kHotGroup apart
+  const int R = P <= 64 ? 64 / P : 1;                   // slices
+  constexpr int U = 8;
+  const int l = threadIdx.x & 63;
+  for (int j0 = 0; j0 < P; j0 += 64) {  // P > 64: value blocks of 64, one slice
+    const int r = R > 1 ? l / P : 0, j = R > 1 ? l % P : j0 + l;
     double s = 0;
-    uint32_t c = 0;
-    for (; c + U <= nc; c += U) {
-      double v[U];
+    if (r < R && j < P) {
+      const double* pj = a.part + (int64_t)c0 * P + j;
+      const int64_t gs = (int64_t)kHotGroup * P;
+      uint32_t g = (uint32_t)r;
+      for (; g + (uint32_t)(U - 1) * R < ng; g += (uint32_t)U * R) {
+        double v[U];
 #pragma unroll
-      for (int t = 0; t < U; ++t) v[t] = pj[(int64_t)(c + t) * P];
+        for (int q = 0; q < U; ++q) v[q] = pj[(int64_t)(g + (uint32_t)q * R) * gs];
 #pragma unroll
-      for (int t = 0; t < U; ++t) s += v[t];
+        for (int q = 0; q < U; ++q) s += v[q];
+      }
+      for (; g < ng; g += (uint32_t)R) s += pj[(int64_t)g * gs];
     }
-    for (; c < nc; ++c) s += pj[(int64_t)c * P];
-    a.part[(int64_t)c0 * P + j] = s;
+    if (R > 1) {
+      part_w[l] = s;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (l < P) {
+        double tot = 0;
+        for (int q = 0; q < R; ++q) tot += part_w[q * P + l];
+        a.part[(int64_t)c0 * P + l] = tot;
+      }
+      return;
+    }
+    if (j < P) a.part[(int64_t)c0 * P + j] = s;
+  }
+}
+// kHotGrid blocks scan the chunk table kHotNT chunks at a time (a block per tile, tiles strided
+// over the grid), list the tile's hot keys (first chunks of segments of >= kHotChunks chunks)
+// in LDS, then sum the listed keys a wave per key.
+__global__ __launch_bounds__(kHotNT) void k_chunk_hotsum(BwdArgs a) {
+  __shared__ double part_w[kHotNT];
+  __shared__ uint32_t s_c0[kHotNT], s_nc[kHotNT];
+  __shared__ int s_n;
+  const uint32_t nch = *a.nchunks;
+  const int w = threadIdx.x >> 6;
+  for (uint32_t base = blockIdx.x * (uint32_t)kHotNT; base < nch; base += gridDim.x * (uint32_t)kHotNT) {
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const uint32_t ch = base + threadIdx.x;
+    if (ch < nch) {
+      const uint32_t u = a.chunk_seg[ch];
+      if (ch == a.choff[u]) {
+        const uint32_t len = a.segstart[u + 1] - a.segstart[u];
+        const uint32_t nc = (len + kChunkOcc - 1) / kChunkOcc;
+        if (nc >= kHotChunks) {
+          const int i = atomicAdd(&s_n, 1);
+          s_c0[i] = ch;
+          s_nc[i] = nc;
+        }
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    for (int i = w; i < n; i += kHotNT / 64) hotsum_key(a, s_c0[i], s_nc[i], part_w + w * 64);
+    __syncthreads();
   }
 }
 
@@ -1606,7 +1676,11 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, boo
     hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC, VV>), grid, dim3(kFmNT), 0, st, a);      \
     DFX_HIP(hipGetLastError());                                                           \
     if (chunk_bound >= (int64_t)kHotChunks) {                                             \
-      hipLaunchKernelGGL(k_chunk_hotsum, dim3((unsigned)chunk_bound), dim3(256), 0, st, a); \
+      hipLaunchKernelGGL(k_chunk_hotgroup, dim3((unsigned)((chunk_bound * (a.d + 2) + 255) / 256)), \
+                         dim3(256), 0, st, a);                                              \
+      hipLaunchKernelGGL(k_chunk_hotsum,                                                    \
+                         dim3((unsigned)std::min<int64_t>(kHotGrid, (chunk_bound + kHotNT - 1) / kHotNT)), \
+                         dim3(kHotNT), 0, st, a);                                           \
       DFX_HIP(hipGetLastError());                                                         \
     }                                                                                     \
     return DFX_OK;                                                                        \

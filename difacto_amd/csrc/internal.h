@@ -356,7 +356,7 @@ int scan_u32(const Lane& L, uint32_t* data, int64_t n, uint32_t* total_dev,
 // chunk_plan (localize.hip, on lane L): choff[u] = first chunk of segment u (exclusive scan
 // of its chunk count, 0 for short segments), chunk_seg[c] = segment of chunk c, total in
 // *nchunks_dev.  Arrays sized for nnz + 1 (choff) and nnz / kChunkOcc + 1 (chunk_seg).
-constexpr int kChunkOcc = 256;
+constexpr int kChunkOcc = 128;
 // keys of at least this many chunks have their chunk partials pre-summed (fm.hip
 // k_chunk_hotsum): the per-key combines read one partial for them
 constexpr uint32_t kHotChunks = 8;

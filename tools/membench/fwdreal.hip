@@ -1,4 +1,4 @@
-// The library's own fat forward (fm.hip k_fm_fwd_fat, compiled into this harness) on the bench's
+// The library's own fat forward (fm.hip k_fm_fwd_walk, compiled into this harness) on the bench's
 // table shape, alone: 2^25 fat slots of 128 B, every key of a 2^24 id space at its ordered-hash
 // home slot (ids ~ U[0, 2^24): distinct home slots, no probe chains — the bench's table), B
 // rows of 39 binary ids.  Against tools/membench/fwdbench's stripped-down walks it tells what
@@ -120,45 +120,18 @@ int main(int argc, char** argv) {
   };
   const int nb = (B + 63) / 64;
   {
-    const int g = resident<k_fm_fwd_fat<4, 8, true, true>>(nb);
-    timeit("k_fm_fwd_fat<4,8,ids,pf> (default)", [&] {
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true, true>), dim3(g), dim3(kFmNT), 0, 0, a);
-    });
-    float h0[4];
-    CK(hipMemcpy(h0, XVp, 16, hipMemcpyDeviceToHost));
-    printf("fat XVp[0..3] %g %g %g %g\n", h0[0], h0[1], h0[2], h0[3]);
-  }
-  {
-    const int g = resident<k_fm_fwd_fat<4, 8, true, false>>(nb);
-    timeit("k_fm_fwd_fat<4,8,ids>", [&] {
-      hipLaunchKernelGGL((k_fm_fwd_fat<4, 8, true, false>), dim3(g), dim3(kFmNT), 0, 0, a);
-    });
-  }
-  timeit("k_fm_fwd_fat<4,8> (ids per trip)", [&] {
-    hipLaunchKernelGGL((k_fm_fwd_fat<4, 8>), dim3(nb), dim3(kFmNT), 0, 0, a);
-  });
-  timeit("k_fm_fwd_fat<4,6> (ids per trip)", [&] {
-    hipLaunchKernelGGL((k_fm_fwd_fat<4, 6>), dim3(nb), dim3(kFmNT), 0, 0, a);
-  });
-  {
-    const int g = resident<k_fm_fwd_walk<false>>(nb);
+    const int g = resident<k_fm_fwd_walk<4, false>>(nb);
     timeit("k_fm_fwd_walk", [&] {
-      hipLaunchKernelGGL(k_fm_fwd_walk<false>, dim3(g), dim3(kFmNT), 0, 0, a);
+      hipLaunchKernelGGL((k_fm_fwd_walk<4, false>), dim3(g), dim3(kFmNT), 0, 0, a);
     });
     float h0[4];
     CK(hipMemcpy(h0, XVp, 16, hipMemcpyDeviceToHost));
     printf("walk XVp[0..3] %g %g %g %g\n", h0[0], h0[1], h0[2], h0[3]);
   }
   {
-    const int g = resident<k_fm_fwd_walk<false, 2>>(nb);
+    const int g = resident<k_fm_fwd_walk<4, false, 2>>(nb);
     timeit("k_fm_fwd_walk (MINB 2)", [&] {
-      hipLaunchKernelGGL((k_fm_fwd_walk<false, 2>), dim3(g), dim3(kFmNT), 0, 0, a);
-    });
-  }
-  {
-    const int g = resident<k_fm_fwd_tile<false>>(nb);
-    timeit("k_fm_fwd_tile", [&] {
-      hipLaunchKernelGGL(k_fm_fwd_tile<false>, dim3(g), dim3(kFmNT), 0, 0, a);
+      hipLaunchKernelGGL((k_fm_fwd_walk<4, false, 2>), dim3(g), dim3(kFmNT), 0, 0, a);
     });
   }
   float h[4];
