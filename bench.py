@@ -191,7 +191,7 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r4"
+PMC_ROUND = "r5"
 
 # Random 128-byte lines per second on MI355X in the step's own access patterns, measured alone
 # with cold caches (tools/membench/spanbench, profiles/r5/spanbench_cold.txt): the forward's
@@ -505,6 +505,7 @@ def main():
     ab = algorithmic_bytes(B, B * k, mean_u, d, cf["valued"], counts["U_V"], counts["occ_V"])
     dom = max(ab, key=lambda p: per_launch_ms[p])
     achieved = ab[dom] / (max(per_launch_ms[dom], 1e-9) * 1e-3) / 1e9
+    pmc_file = "pmc_hbm.json" if args.config == "c3" else "pmc_hbm_%s.json" % args.config
     out = {
         "metric": "train examples/sec (FM V_dim=16) at 1/8 GPU + achieved HBM GB/s",
         "value": round(value, 1),
@@ -526,16 +527,17 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic(("k_fm_bwd", "k_chunk_hotsum")
+                     "traffic": pmc_traffic(("k_fm_bwd", "k_chunk_hot")
                                             if dom == "backward_update" else "k_fm_fwd",
-                                            "pmc_hbm.json" if args.config == "c3"
-                                            else "pmc_hbm_%s.json" % args.config),
-                     "traffic_source": "profiles/%s/pmc_hbm.json (rocprofv3 FETCH_SIZE + "
-                                       "WRITE_SIZE per launch; request counts per key / nnz "
+                                            pmc_file),
+                     "traffic_source": "profiles/%s/" % PMC_ROUND + pmc_file +
+                                       " (rocprofv3 FETCH_SIZE + "
+                                       "WRITE_SIZE per launch, summed over the phase's "
+                                       "kernels; request counts per key / nnz "
                                        "in profiles/%s/pmc_requests.json); counters "
                                        "calibrated for these access shapes in "
                                        "profiles/r1/pmc_calibration.json (64-B requests "
-                                       "counted exactly, factor 1.00)" % (PMC_ROUND, PMC_ROUND),
+                                       "counted exactly, factor 1.00)" % PMC_ROUND,
                      "algorithmic_bytes_per_launch": int(ab[dom]),
                      "launch_ms": round(per_launch_ms[dom], 4)},
         "roofline_forward": forward_roofline(ab["forward"], per_launch_ms["forward"],
@@ -893,7 +895,7 @@ def run_sharded(args, torch, dist, dev, rank, world, local):
         # backward formula over the owner's rows, keys and unique keys)
         ab = algorithmic_bytes(o_rows, o_nnz, o_uniq, d)["backward_update"]
         rkernel = "owner_backward (split: fused backward + FTRL/AdaGrad + InitV, rank 0)"
-        traffic, tsrc = (pmc_traffic(("k_fm_bwd", "k_chunk_hotsum"), "pmc_hbm_split.json"),
+        traffic, tsrc = (pmc_traffic(("k_fm_bwd", "k_chunk_hot"), "pmc_hbm_split.json"),
                          "profiles/%s/pmc_hbm_split.json (rocprofv3 FETCH_SIZE + WRITE_SIZE "
                          "per launch of the owner's backward, bench.py --sharded)" % PMC_ROUND)
     else:

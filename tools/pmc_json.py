@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-KERNELS = ("k_probe_keys", "k_fm_fwd", "k_fm_bwd", "k_chunk_hotsum", "k_loc_", "k_lb_",
+KERNELS = ("k_probe_keys", "k_fm_fwd", "k_fm_bwd", "k_chunk_hot", "k_loc_", "k_lb_",
            "k_os_scatter<", "k_initv", "k_dist_", "k_split_", "k_auc")
 
 

@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-KERNELS = ("k_probe_keys", "k_fm_fwd", "k_fm_bwd", "k_chunk_hotsum", "k_loc_write", "k_loc_transform",
+KERNELS = ("k_probe_keys", "k_fm_fwd", "k_fm_bwd", "k_chunk_hot", "k_loc_write", "k_loc_transform",
            "k_initv", "k_os_scatter<")
 
 
