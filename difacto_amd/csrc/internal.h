@@ -75,6 +75,12 @@ struct DevState {
   unsigned long long kmin, kmax, pk_min, pk_max;
   unsigned int pk_valid;
   unsigned int lb_over;  // buckets of this batch beyond the LDS sort's capacity (k_lb_colscan)
+  // the bucket Localizer's hot-key map (skewed binary batches, locbucket.hip): Workspace::lbsplit
+  // holds it, built by the previous batch on this lane for 2^lb_sp_wbits buckets; lb_sp_use: the
+  // map is valid (the previous batch had hot keys); lb_hot: this batch's flag (k_lb_wbucket)
+  unsigned int lb_sp_wbits, lb_sp_use, lb_hot;
+  unsigned int lb_nhot, lb_hm_n, lb_hm_s;  // the hot list's length; the map's keys, coarse shift
+  unsigned long long lb_hm_base;           // ... and coarse base
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
@@ -105,7 +111,7 @@ struct Workspace {
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // the bucket Localizer (locbucket.hip): per (tile, bucket) counts / prefixes, per bucket its
   // total and start; per item its row / position when the items are not packed (and scratch)
-  DevBuf lbcnt, lbq;
+  DevBuf lbcnt, lbq, lbsplit;
   // pinned, written by the device: [0] buckets over the LDS capacity in the last bucket
   // Localizer of this workspace, [1] radix Localizers run since, [2] 1 packed / 2 not
   unsigned int* lb_hint = nullptr;

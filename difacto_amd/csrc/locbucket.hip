@@ -36,6 +36,8 @@
 // with rows, and a binary row's repeats of one key are identical items.  So the outputs are
 // bit-identical to localize.hip's (test_gpu_r3.py test_bucket_localizer_equals_lsd).
 #include <algorithm>
+#include <mutex>
+#include <set>
 
 #include "lookback.h"
 
@@ -81,6 +83,21 @@ struct LbArgs {
   float* occ_x;
   unsigned int* hint;    // pinned: Workspace::lb_hint
   int diag;              // Context::lb_diag (measurement only)
+  // the hot-key map (Workspace::lbsplit): the previous batch's hot keys (runs of >= hot_th),
+  // listed, then laid out over the buckets; per bucket its first and last key and whether its
+  // first key continues the previous non-empty bucket's last (a hot key's run over buckets)
+  uint64_t* hl_key;      // [kLbHotMax] the list (k_lb_hotlist, unordered)
+  uint32_t* hl_len;
+  uint64_t* hm_key;      // [kLbHotMax] the map (k_lb_hotmap): hot keys in order,
+  uint32_t* hm_p;        // [kLbHotMax + 1] exclusive prefix of (W + 1),
+  uint32_t* hm_w;        // [kLbHotMax] buckets per hot key,
+  uint32_t* hm_ic;       // [nbk / 2 + 1] per coarse bucket its first hot key
+  uint64_t* bfk;
+  uint64_t* blk;
+  uint32_t* bcont;
+  int hm_lds;            // the histogram / scatter launches hold LDS for the map
+  int wbits_hot;         // the bucket bits a map is built for (one more than the key map's)
+  uint32_t hot_th;       // a hot key's occurrences, at least
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -116,6 +133,76 @@ __device__ inline uint32_t lb_bucket(uint64_t k, const LbMap& m) {
   return x < m.nbk ? (uint32_t)x : m.nbk - 1u;
 }
 
+// The hot-key map, for binary batches after one with hot keys (Zipf keys: C5's top key holds
+// ~11 % of a batch's nnz, ~600 buckets' worth, which no map of the key alone can split).  The
+// previous batch's keys of >= hot_th occurrences, in key order, each get W_h = ceil(len_h /
+// target) buckets of their own; a coarse key map (half the buckets, the key map's form) places
+// every other key.  In key order, coarse bucket c holds [cold keys below its first hot key]
+// [hot key 1: W_1 buckets] [cold keys between] ... [cold keys above its last hot key]: with
+// P_i = sum over the hot keys before i of (W + 1), a cold key of coarse bucket c above q of its
+// hot keys (the first being i_c) goes to c + P[i_c + q], and occurrence j of hot key i to
+// c + P[i] + 1 + min(W_i - 1, floor(j * W_i / nnz)) — by position, so by row: the map is
+// monotone in (key, row) and the buckets still concatenate in sorted order.  Per item a coarse
+// bucket, its hot-key range and a compare or two, from LDS.
+constexpr int kLbHotMax = 1024;
+struct LbHot {
+  const uint64_t* hk;
+  const uint32_t* hp;
+  const uint32_t* hw;
+  const uint32_t* ic;
+  LbMap cm;
+  double inv_nnz;
+};
+__device__ inline bool lb_hot_on(const LbArgs& a) {
+  return a.hm_lds && a.value == nullptr && a.ds->lb_sp_use &&
+         a.ds->lb_sp_wbits == (unsigned)a.wbits;
+}
+__host__ __device__ constexpr size_t lb_hot_lds(uint32_t nbk) {
+  return (size_t)kLbHotMax * 8 + ((size_t)kLbHotMax + 1) * 4 + (size_t)kLbHotMax * 4 +
+         ((size_t)nbk / 2 + 1) * 4;
+}
+__device__ inline LbHot lb_stage_hot(const LbArgs& a, void* lds, int t, int nt) {
+  LbHot h;
+  uint64_t* hk = reinterpret_cast<uint64_t*>(lds);
+  uint32_t* hp = reinterpret_cast<uint32_t*>(hk + kLbHotMax);
+  uint32_t* hw = hp + kLbHotMax + 1;
+  uint32_t* ic = hw + kLbHotMax;
+  const uint32_t n = a.ds->lb_hm_n, C = (1u << a.wbits) / 2;
+  for (uint32_t i = t; i < n; i += nt) {
+    hk[i] = a.hm_key[i];
+    hw[i] = a.hm_w[i];
+  }
+  for (uint32_t i = t; i <= n; i += nt) hp[i] = a.hm_p[i];
+  for (uint32_t c = t; c <= C; c += nt) ic[c] = a.hm_ic[c];
+  h.hk = hk;
+  h.hp = hp;
+  h.hw = hw;
+  h.ic = ic;
+  h.cm.nbk = C;
+  h.cm.base = a.ds->lb_hm_base;
+  h.cm.s = (int)a.ds->lb_hm_s;
+  h.inv_nnz = 1.0 / (double)a.nnz;
+  return h;
+}
+__device__ inline uint32_t lb_hot_bucket(uint64_t k, uint64_t j, const LbHot& h) {
+  const uint32_t c = lb_bucket(k, h.cm);
+  uint32_t i = h.ic[c];
+  const uint32_t i1 = h.ic[c + 1];
+  for (; i < i1; ++i) {
+    const uint64_t hkey = h.hk[i];
+    if (hkey >= k) {
+      if (hkey == k) {
+        const uint32_t W = h.hw[i];
+        uint32_t sub = (uint32_t)((double)j * (double)W * h.inv_nnz);
+        sub = sub < W - 1 ? sub : W - 1;
+        return c + h.hp[i] + 1 + sub;
+      }
+      break;
+    }
+  }
+  return c + h.hp[i];
+}
+
 // the item form of this batch: ((key - kmin) >> lo) << rb | q when the key's varying bits and q's
 // rb bits fit 63 bits (the top bit stays clear, so no item equals the sort's padding ~0);
 // else the raw key (never ~0: common.h kEmptyKey) with q apart
@@ -144,6 +231,8 @@ __global__ void k_lb_init(DevState* ds) {
   ds->kmax = 0;
   ds->n_init = 0;  // long segments of the batch (chunk_plan's gate)
   ds->lb_over = 0;
+  ds->lb_hot = 0;
+  ds->lb_nhot = 0;
   unsigned* meta = ds->sortmeta;
   meta[kSortMetaEpoch] = ++ds->sort_epoch;  // tags this Localizer's look-back words
   meta[kSortMetaCpTile] = 0;                // the chunk plan's tile tickets
@@ -180,12 +269,15 @@ constexpr int kLbUnr = 8;  // ids in flight per thread
 template <int HNT>
 __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
-  extern __shared__ uint32_t lb_dyn[];
-  uint32_t* hist = lb_dyn;
+  extern __shared__ uint64_t lb_dyn64[];  // 8-byte aligned: the splitter keys follow hist
+  uint32_t* hist = reinterpret_cast<uint32_t*>(lb_dyn64);
   __shared__ unsigned long long red[4][kLbHWaves];
   const LbMap m = lb_map(a.ds, a.wbits);
   const int t = threadIdx.x;
   for (uint32_t d = t; d < m.nbk; d += kLbHNT) hist[d] = 0;
+  const bool qs = lb_hot_on(a);
+  LbHot hm{};
+  if (qs) hm = lb_stage_hot(a, hist + m.nbk, t, kLbHNT);
   const int64_t tile = blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int64_t r1 = r0 + a.rt < a.B ? r0 + a.rt : a.B;
@@ -201,13 +293,14 @@ __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < kLbUnr; ++u) {
-      if (jb + (uint64_t)u * kLbHNT + t < j1) {
+      const uint64_t j = jb + (uint64_t)u * kLbHNT + t;
+      if (j < j1) {
         const uint64_t k = lb_key(id[u], a.max_index, a.keys_ready);
         vor |= k;
         vand &= k;
         vmin = k < vmin ? k : vmin;
         vmax = k > vmax ? k : vmax;
-        atomicAdd(&hist[lb_bucket(k, m)], 1u);
+        atomicAdd(&hist[qs ? lb_hot_bucket(k, j, hm) : lb_bucket(k, m)], 1u);
       }
     }
   }
@@ -290,6 +383,9 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t* cur = reinterpret_cast<uint32_t*>(lb_dyn64);  // per bucket: this tile's next slot
   uint64_t* offs = lb_dyn64 + (m.nbk + 1u) / 2;
   const int t = threadIdx.x;
+  const bool qs = lb_hot_on(a);
+  LbHot hm{};
+  if (qs) hm = lb_stage_hot(a, offs + a.rt + 1, t, kLbHNT);
   const int64_t tile = blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
@@ -380,7 +476,7 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
       const uint64_t k = lb_key(id[u], a.max_index, a.keys_ready);
       const uint32_t row = (uint32_t)(r0 + lo);
       const uint64_t q = S ? j : (uint64_t)row;
-      const uint32_t pos = atomicAdd(&cur[lb_bucket(k, m)], 1u);
+      const uint32_t pos = atomicAdd(&cur[qs ? lb_hot_bucket(k, j, hm) : lb_bucket(k, m)], 1u);
       stnt(a.kbuf + pos, p.packed ? ((((k - p.kmin) >> p.lo) << p.rb) | (q & qmask)) : k,
            a.nt != 0);
       if (!p.packed) a.qbuf[pos] = (uint32_t)q;
@@ -891,7 +987,9 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   uint32_t* tseg = a.qscr + start;
   uint64_t* tkey = a.kscr + start;
   uint32_t run = 0;
-  bool longseg = false;
+  bool longseg = false, hot = false;
+  const int th = (int)a.hot_th;  // a run this long inside the bucket: the batch has a hot key
+  auto fullkey = [&](uint64_t it) { return p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it; };
   auto heads = [&](const uint64_t* K, const uint32_t* Qs, const uint64_t* Ss) {
     uint64_t prev = 0;  // the key bits of the item before this slot's first
     for (int c = 0; c < nc; ++c) {
@@ -902,12 +1000,13 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
       const uint64_t up = __shfl_up(kb, 1, kWave);
       const bool h = valid && (i == 0 || kb != (l == 0 ? prev : up));
       if (valid && i >= kChunkOcc && kb == lb_keybits(p, K[i - kChunkOcc])) longseg = true;
+      if (valid && i >= th && kb == lb_keybits(p, K[i - th])) hot = true;
       prev = __shfl(kb, kWave - 1, kWave);
       const uint64_t hb = __ballot(h);
       if (!(a.diag & 4) && valid) {
         if (h) {
           const uint32_t r = run + (uint32_t)__popcll(hb & lanemask_lt());
-          tkey[r] = p.packed ? (((it >> p.rb) << p.lo) + p.kmin) : it;
+          tkey[r] = fullkey(it);
           tseg[r] = (uint32_t)(start + i);
         }
         uint32_t row;
@@ -927,6 +1026,12 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   };
   if (fast) heads(sk, sq, ss);
   else heads(gk, gq, gs);
+  // the bucket's first and last key (k_lb_bscan's continuations)
+  if (n > 0 && l == 0) {
+    a.bfk[b] = fullkey(fast ? sk[0] : gk[0]);
+    a.blk[b] = fullkey(fast ? sk[n - 1] : gk[n - 1]);
+  }
+  if (__ballot(hot) && l == 0) atomicOr(&ds->lb_hot, 1u);
   if (__ballot(longseg) && l == 0 &&
       __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     atomicOr(&ds->n_init, 1u);
@@ -938,22 +1043,53 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
 constexpr int kLbScanNT = 1024;
 __global__ __launch_bounds__(kLbScanNT) void k_lb_bscan(LbArgs a) {
   __shared__ uint32_t lds[kLbScanNT / kWave + 1];
+  __shared__ int s_last[kLbScanNT];
   const int t = threadIdx.x;
   const uint32_t nbk = 1u << a.wbits;
   const uint32_t per = (nbk + kLbScanNT - 1) / kLbScanNT;
-  uint32_t mine = 0;
-  for (uint32_t i = 0; i < per; ++i)
-    if (t * per + i < nbk) mine += a.bheads[t * per + i];
+  // a bucket whose first key is the previous non-empty bucket's last continues that key's run
+  // (the hot-key map spreads a hot key over buckets): its first head is no new rank
+  int lastne = -1;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < nbk && a.bstart[d + 1] > a.bstart[d]) lastne = (int)d;
+  }
+  s_last[t] = lastne;
+  __syncthreads();
+  for (int off = 1; off < kLbScanNT; off <<= 1) {  // inclusive max scan
+    const int v = t >= off ? s_last[t - off] : -1;
+    __syncthreads();
+    if (v > s_last[t]) s_last[t] = v;
+    __syncthreads();
+  }
+  int prev = t > 0 ? s_last[t - 1] : -1;
+  uint32_t mine = 0, anycont = 0;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t d = t * per + i;
+    if (d < nbk) {
+      uint32_t c = 0;
+      if (a.bstart[d + 1] > a.bstart[d]) {
+        if (prev >= 0 && a.bfk[d] == a.blk[prev]) c = 1;
+        prev = (int)d;
+      }
+      a.bcont[d] = c;
+      anycont |= c;
+      mine += a.bheads[d] - c;
+    }
+  }
   uint32_t U;
   uint32_t ex = block_excl_scan<kLbScanNT>(mine, lds, &U);
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < nbk) {
-      const uint32_t h = a.bheads[d];
       a.brank[d] = ex;
-      ex += h;
+      ex += a.bheads[d] - a.bcont[d];
     }
   }
+  // a continued run may be long although no bucket's part is: the chunk plan's gate opens (an
+  // open gate with no long segment plans no chunk — the same result)
+  if (anycont && __hip_atomic_load(&a.ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&a.ds->n_init, 1u);
   if (t == 0) {
     DevState* ds = a.ds;
     ds->u_count = U;
@@ -969,10 +1105,115 @@ __global__ __launch_bounds__(kLbScanNT) void k_lb_bscan(LbArgs a) {
 __global__ __launch_bounds__(kLbNT) void k_lb_out(LbArgs a) {
   const uint32_t b = blockIdx.x;
   const int64_t start = a.bstart[b];
-  const uint32_t h = a.bheads[b], r0 = a.brank[b];
-  for (uint32_t j = threadIdx.x; j < h; j += kLbNT) {
-    if (a.uniq) a.uniq[r0 + j] = a.kscr[start + j];
-    if (a.segstart) a.segstart[r0 + j] = a.qscr[start + j];
+  const uint32_t h = a.bheads[b], r0 = a.brank[b], c = a.bcont[b];
+  for (uint32_t j = threadIdx.x + c; j < h; j += kLbNT) {
+    if (a.uniq) a.uniq[r0 + j - c] = a.kscr[start + j];
+    if (a.segstart) a.segstart[r0 + j - c] = a.qscr[start + j];
+  }
+}
+
+// binary batches with a hot key (k_lb_wbucket's flag): every segment of >= hot_th occurrences
+// listed (key, length), for the next batch's hot-key map; a grid-stride pass over the U segments
+constexpr int kLbHotGrid = 512;
+__global__ __launch_bounds__(kLbNT) void k_lb_hotlist(LbArgs a) {
+  DevState* ds = a.ds;
+  if (ds->lb_hot == 0u) return;
+  const int64_t U = ds->u_count;
+  for (int64_t i = (int64_t)blockIdx.x * kLbNT + threadIdx.x; i < U;
+       i += (int64_t)gridDim.x * kLbNT) {
+    const uint32_t len = a.segstart[i + 1] - a.segstart[i];
+    if (len >= a.hot_th) {
+      const uint32_t x = atomicAdd(&ds->lb_nhot, 1u);
+      if (x < (uint32_t)kLbHotMax) {
+        a.hl_key[x] = a.uniq[i];
+        a.hl_len[x] = len;
+      }
+    }
+  }
+}
+
+// the next batch's hot-key map from the list (one block): the hot keys sorted (bitonic, LDS),
+// W_h = ceil(len_h / target) with target sized so the buckets needed, nbk / 2 coarse plus
+// sum (W_h + 1), fit 2^wbits_hot; P (the exclusive prefix of W + 1); per coarse bucket its first
+// hot key.  No list, a list past kLbHotMax, or no room: the key map next.  A batch that was
+// skewed under the key map sends the next one to the bucket Localizer again (hint[0]).
+__global__ __launch_bounds__(kLbHotMax) void k_lb_hotmap(LbArgs a) {
+  __shared__ uint64_t sk[kLbHotMax];
+  __shared__ uint32_t sl[kLbHotMax];
+  __shared__ uint32_t lds[kLbHotMax / kWave + 1];
+  DevState* ds = a.ds;
+  const int t = threadIdx.x;
+  const bool was = lb_hot_on(a);
+  const uint32_t nh = ds->lb_hot ? ds->lb_nhot : 0u;
+  const int wb = a.wbits_hot;
+  const uint32_t nbk = 1u << wb, C = nbk / 2;
+  if (nh == 0u || nh > (uint32_t)kLbHotMax || wb < 2 || 2 * nh >= nbk - C) {
+    if (t == 0) {
+      ds->lb_sp_use = 0u;
+      a.hint[3] = 0u;
+    }
+    return;
+  }
+  sk[t] = (uint32_t)t < nh ? a.hl_key[t] : ~0ull;
+  sl[t] = (uint32_t)t < nh ? a.hl_len[t] : 0u;
+  __syncthreads();
+  for (int k = 2; k <= kLbHotMax; k <<= 1) {  // bitonic sort by key (keys are distinct)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int p = t ^ j;
+      if (p > t) {
+        const bool up = (t & k) == 0;
+        const uint64_t x = sk[t], y = sk[p];
+        if ((x > y) == up) {
+          sk[t] = y;
+          sk[p] = x;
+          const uint32_t lx = sl[t];
+          sl[t] = sl[p];
+          sl[p] = lx;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint32_t len = sl[t];
+  uint32_t mass;
+  (void)block_excl_scan<kLbHotMax>(len, lds, &mass);
+  const uint32_t room = nbk - C - 2 * nh;  // sum W_h <= mass / target + nh <= nbk - C - nh
+  const uint32_t target = (mass + room - 1) / room;
+  const uint32_t W = (uint32_t)t < nh ? (len + target - 1) / target : 0u;
+  uint32_t tot;
+  const uint32_t P = block_excl_scan<kLbHotMax>((uint32_t)t < nh ? W + 1 : 0u, lds, &tot);
+  if ((uint32_t)t < nh) {
+    a.hm_key[t] = sk[t];
+    a.hm_w[t] = W;
+    a.hm_p[t] = P;
+  }
+  if (t == 0) a.hm_p[nh] = tot;
+  // the coarse map: the key map's form over C buckets, fitted to this batch's key range (the
+  // parameters travel with the map: the next batch's own fit may move)
+  LbMap cm;
+  cm.nbk = C;
+  cm.base = ds->kmin;
+  {
+    const int bl = lb_bitlen(ds->kmax - ds->kmin), cb = wb - 1;
+    cm.s = bl > cb ? bl - cb : 0;
+  }
+  for (uint32_t c = t; c <= C; c += kLbHotMax) {  // the first hot key of coarse bucket >= c
+    uint32_t lo = 0, hi = nh;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (lb_bucket(sk[mid], cm) < c) lo = mid + 1;
+      else hi = mid;
+    }
+    a.hm_ic[c] = lo;
+  }
+  if (t == 0) {
+    ds->lb_hm_n = nh;
+    ds->lb_hm_base = cm.base;
+    ds->lb_hm_s = (unsigned)cm.s;
+    ds->lb_sp_wbits = (unsigned)wb;
+    ds->lb_sp_use = 1u;
+    a.hint[3] = 1u;
+    if (!was) a.hint[0] = 0u;
   }
 }
 
@@ -986,6 +1227,26 @@ __global__ __launch_bounds__(kLbNT) void k_lb_gather(LbArgs a) {
   const uint2 rv = a.rowof[a.occ_row[i]];  // one 8-byte read per occurrence
   a.occ_row[i] = rv.x;
   if (a.occ_x) a.occ_x[i] = __uint_as_float(rv.y);
+}
+
+// Workspace::lbsplit: the hot list and map, the buckets' first / last keys and continuations
+static size_t lb_split_bytes() {
+  constexpr size_t kNb = (size_t)1 << kLbMaxBits;
+  return (size_t)kLbHotMax * 8 * 2 + kNb * 8 * 2 + (size_t)kLbHotMax * 4 * 3 + 4 + (kNb / 2 + 1) * 4 +
+         kNb * 4;
+}
+
+// dynamic LDS past 64 KiB (the splitters at 8192 buckets): allowed once per kernel
+static void lb_lds_attr(const void* f) {
+  static std::mutex mu;
+  static std::set<const void*> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (!done.insert(f).second) return;
+  hipFuncAttributes at{};
+  if (hipFuncGetAttributes(&at, f) == hipSuccess)
+    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - (int)at.sharedSizeBytes);
+  (void)hipGetLastError();  // a refusal leaves the default (64 KiB): no sticky error
 }
 
 int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64_t* offset,
@@ -1006,7 +1267,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   const bool valued = o.value != nullptr && o.occ_x != nullptr;
   int wbits = 1;
   while (wbits < kLbMaxBits && ((int64_t)1024 << wbits) < nnz) ++wbits;
-  const uint32_t nbk = 1u << wbits;
+  uint32_t nbk = 1u << wbits;
   // past ~3/4 of the LDS sort's capacity per bucket on average (beyond ~12.6 M nnz) most buckets
   // would be oversize: the radix Localizer outright, not a bucket pass that falls back
   if (nnz > (int64_t)nbk * (kLbCap * 3 / 4)) return DFX_OK;
@@ -1025,6 +1286,16 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     for (uint64_t q = qmax; q; q >>= 1) ++rb;
     hint[2] = kb + rb <= 63 ? 1u : 2u;
   }
+  // the hot-key map (binary batches, after one that built it here): one more bucket bit, and
+  // LDS for the map in the histogram / scatter launches (the device decides whether to use it;
+  // without the LDS it keeps the key map).  Hot keys: runs of at least half a bucket's average
+  // under the key map (and >= 64)
+  const int hm_lds = (!valued && hint[3]) ? 1 : 0;
+  const int wbits_key = wbits, wbits_hot = wbits + 1 < kLbMaxBits ? wbits + 1 : kLbMaxBits;
+  if (hm_lds) {
+    wbits = wbits_hot;
+    nbk = 1u << wbits;
+  }
   int64_t ntiles = std::min<int64_t>(c->lb_tiles, std::max<int64_t>(1, nnz / 4096));
   int64_t rt = std::min<int64_t>(kLbMaxRows, std::max<int64_t>(1, (B + ntiles - 1) / ntiles));
   ntiles = (B + rt - 1) / rt;
@@ -1034,6 +1305,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   DFX_TRY(ws.vals1.ensure(nnz * 8));
   DFX_TRY(ws.lbq.ensure(nnz * 8));
   DFX_TRY(ws.lbcnt.ensure(sizeof(uint32_t) * ((size_t)ntiles * nbk + 4 * (nbk + 1))));
+  DFX_TRY(ws.lbsplit.ensure(lb_split_bytes()));  // the hot-key map persists across batches
   LbArgs a{};
   a.B = B; a.nnz = nnz; a.offset = offset; a.index = index; a.max_index = max_index;
   a.keys_ready = o.keys_ready ? 1 : 0;
@@ -1060,10 +1332,29 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
   a.diag = c->lb_diag;
+  {
+    constexpr size_t kNb = (size_t)1 << kLbMaxBits;
+    char* q = ws.lbsplit.as<char>();
+    a.hl_key = reinterpret_cast<uint64_t*>(q);
+    a.hm_key = a.hl_key + kLbHotMax;
+    a.bfk = a.hm_key + kLbHotMax;
+    a.blk = a.bfk + kNb;
+    a.hl_len = reinterpret_cast<uint32_t*>(a.blk + kNb);
+    a.hm_p = a.hl_len + kLbHotMax;
+    a.hm_w = a.hm_p + kLbHotMax + 1;
+    a.hm_ic = a.hm_w + kLbHotMax;
+    a.bcont = a.hm_ic + kNb / 2 + 1;
+  }
+  a.hm_lds = hm_lds;
+  a.wbits_hot = wbits_hot;
+  a.hot_th = (uint32_t)std::max<int64_t>(
+      kWave, std::min<int64_t>(nnz / ((int64_t)1 << wbits_key) / 2, kLbCap));
+  const size_t sp_bytes = a.hm_lds ? lb_hot_lds(nbk) : 0;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
 #define DFX_LB_HIST(NT) \
-  hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT), nbk * sizeof(uint32_t), \
-                     L.stream, a);
+  lb_lds_attr((const void*)k_lb_hist<NT>);                                                   \
+  hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT),                         \
+                     nbk * sizeof(uint32_t) + sp_bytes, L.stream, a);
   // lb_hnt (0: auto): 512-thread blocks for valued batches, whose scatter also writes the
   // {row, value} pairs (C2 +5.6 %), 1024 for binary ones (C3: 1024 best)
   const int hnt = c->lb_hnt ? c->lb_hnt : (valued ? 512 : 1024);
@@ -1073,8 +1364,11 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
 #undef DFX_LB_HIST
   hipLaunchKernelGGL(k_lb_colscan, dim3((nbk + kWave - 1) / kWave), dim3(kLbScanWaves * kWave), 0,
                      L.stream, a);
-  const size_t scatter_lds = ((nbk + 1) & ~1u) * sizeof(uint32_t) + (rt + 1) * sizeof(uint64_t);
+  const size_t scatter_lds =
+      ((nbk + 1) & ~1u) * sizeof(uint32_t) + (rt + 1) * sizeof(uint64_t) + sp_bytes;
 #define DFX_LB_SCAT(NT)                                                                    \
+  lb_lds_attr((const void*)k_lb_scatter<true, NT>);                                        \
+  lb_lds_attr((const void*)k_lb_scatter<false, NT>);                                       \
   if (valued)                                                                              \
     hipLaunchKernelGGL((k_lb_scatter<true, NT>), dim3((unsigned)ntiles), dim3(NT), scatter_lds, \
                        L.stream, a);                                                       \
@@ -1110,6 +1404,10 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
                        a);
   hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);
   hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
+  if (!valued && a.uniq && a.segstart) {  // the next batch's hot-key map
+    hipLaunchKernelGGL(k_lb_hotlist, dim3(kLbHotGrid), bb, 0, L.stream, a);
+    hipLaunchKernelGGL(k_lb_hotmap, dim3(1), dim3(kLbHotMax), 0, L.stream, a);
+  }
   DFX_HIP(hipGetLastError());
   *used = true;
   return DFX_OK;

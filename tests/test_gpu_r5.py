@@ -79,3 +79,58 @@ def test_walk_forward_bit_identical(H, rows, d, binary):
     assert np.array_equal(va.cpu().numpy().view(np.uint32), vb.cpu().numpy().view(np.uint32))
     ca.close()
     cb.close()
+
+
+# ---------------------------------------------------------------- the splitter map
+def _hot_ids(kind, rng, n, step):
+    if kind == "zipf":      # C5's keys: Zipf(1.1) over 2^24, the top key ~11 % of the nnz
+        return D.zipf_keys(rng, n, 1.1, 1 << 24)
+    if kind == "one_hot":   # one key in 40 % of the nnz, the rest uniform
+        ids = rng.integers(0, 1 << 22, n, dtype=np.uint64)
+        ids[rng.random(n) < 0.4] = 12345
+        return ids
+    if kind == "drift":     # the hot keys change every step: yesterday's splitters misplace them
+        return (D.zipf_keys(rng, n, 1.1, 1 << 20) + np.uint64(7919 * step)) % np.uint64(1 << 20)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["zipf", "one_hot", "drift"])
+@pytest.mark.parametrize("rows", [60000, 100])
+def test_bucket_splitter_map_equals_lsd(H, kind, rows):
+    """The bucket Localizer on skewed binary batches (locbucket.hip's splitter map: after a
+    batch with a hot key, the next batch's buckets follow that batch's (key, row) quantiles, and
+    a hot key's occurrences spread over buckets of their own, its run continued across them)
+    against the onesweep radix Localizer (loc_bucket=0): predictions, loss and AUC identical
+    every step, the model identical at the end, and within the usual tolerances of the oracle.
+    Equal-sized batches so the map engages from the second step; 100-row batches give 4
+    buckets, so runs continue over buckets with parts shorter than a chunk; 'drift' moves the
+    hot keys under stale splitters (oversize buckets: the global-memory passes)."""
+    cfg = dict(V_dim=16, V_threshold=0, l1=0, lr=.1, V_lr=.01)
+    cs = [H.Context(0, max_keys=1 << 21, loc_bucket=0, **cfg),
+          H.Context(0, max_keys=1 << 21, loc_bucket=1, **cfg)]
+    up = O.Updater(**cfg)
+    rng = np.random.default_rng(17)
+    for step in range(5):
+        blk = D.synthetic(rows, 39, 2, binary=True, seed=90 + step)
+        blk = D.RowBlock(blk.offs, _hot_ids(kind, rng, blk.nnz, step), None, blk.labels)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, None, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        preds, progs = [], []
+        for c in cs:
+            pr = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+            H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pr)
+            preds.append(pr.cpu().numpy().view(np.uint32))
+            progs.append(H.progress(c))
+        assert np.array_equal(preds[0], preds[1]), step
+        assert progs[0]["loss"] == progs[1]["loss"] and progs[0]["auc"] == progs[1]["auc"], step
+        assert abs(progs[1]["loss"] - loss) <= 1e-4 * abs(loss), (step, progs[1]["loss"], loss)
+        assert abs(progs[1]["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size
+    uniq, _, _ = O.localize(blk.offs, blk.ids)
+    vs = [H.Store(c).pull(c.tensor(uniq, torch.int64)) for c in cs]
+    assert np.array_equal(vs[0][1].cpu().numpy(), vs[1][1].cpu().numpy())
+    assert np.array_equal(vs[0][0].cpu().numpy().view(np.uint32),
+                          vs[1][0].cpu().numpy().view(np.uint32))
+    st = [H.Store(c).stats() for c in cs]
+    assert st[0]["n_keys"] == st[1]["n_keys"] == up.size()
+    for c in cs:
+        c.close()

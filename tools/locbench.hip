@@ -5,7 +5,9 @@
 // times.  With a sixth argument "auc": the AUC lane's sort + area of a B-row (pred, label)
 // snapshot instead (auc_sort from the kwargs).  Measurement tool (links the library's
 // internals), not a test.
-//   build/locbench [B] [k] [kbits] [iters] [context kwargs] [auc | valued]
+//   build/locbench [B] [k] [kbits] [iters] [context kwargs] [auc | valued | zipf]
+// zipf: Zipf(1.1) keys, a fresh batch every iteration (untimed), the chunk plan timed with the
+// Localizer as the fused step's lane runs it
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -22,6 +24,23 @@ __global__ void k_gen(int64_t B, int k, int kbits, uint64_t* offs, uint64_t* ids
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   x ^= x >> 31;
   ids[i] = x >> (64 - kbits);
+}
+
+// Zipf(s) ranks over [1, 2^kbits] by the continuous inverse CDF (C5's keys, approximately)
+__global__ void k_gen_zipf(int64_t B, int k, int kbits, double zs, uint64_t* offs, uint64_t* ids,
+                           uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= B) offs[i] = (uint64_t)i * k;
+  if (i >= B * k) return;
+  uint64_t x = seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;  // splitmix64
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  const double u = (double)(x >> 11) * (1.0 / 9007199254740992.0);
+  const double N = (double)(1ull << kbits), a = 1.0 - zs;
+  double r = pow((pow(N + 1.0, a) - 1.0) * u + 1.0, 1.0 / a);
+  uint64_t rk = (uint64_t)r;
+  ids[i] = rk < 1 ? 1 : (rk > (1ull << kbits) ? (1ull << kbits) : rk);
 }
 
 __global__ void k_gen_pred(int64_t B, float* pred, float* lab, uint64_t seed) {
@@ -87,6 +106,13 @@ int main(int argc, char** argv) {
     return rc;
   }
   const bool valued = argc > 6 && std::string(argv[6]) == "valued";
+  const bool zipf = argc > 6 && std::string(argv[6]) == "zipf";
+  uint32_t *choff = nullptr, *chseg = nullptr, *nch = nullptr;
+  if (zipf) {
+    hipMalloc(&choff, (nnz + 1) * 4);
+    hipMalloc(&chseg, dfx::max_chunks(nnz) * 4);
+    hipMalloc(&nch, 4);
+  }
   uint64_t *offs, *ids, *uniq;
   uint32_t *seg, *occ;
   float *val = nullptr, *occx = nullptr;
@@ -114,9 +140,16 @@ int main(int argc, char** argv) {
   hipEventCreate(&e1);
   double tot = 0;
   for (int it = 0; it < iters + 2; ++it) {
+    if (zipf)
+      hipLaunchKernelGGL(k_gen_zipf, dim3((unsigned)((nnz + 256) / 256)), dim3(256), 0, c->stream,
+                         B, k, kbits, 1.1, offs, ids, 42ull + 7919ull * it);
     hipEventRecord(e0, c->stream);
     if (dfx::localize_run(c, L, B, nnz, offs, ids, ~0ull, o) != DFX_OK) {
       fprintf(stderr, "localize: %s\n", dfx_last_error());
+      return 1;
+    }
+    if (zipf && dfx::chunk_plan(L, nnz, seg, choff, chseg, nch) != DFX_OK) {
+      fprintf(stderr, "chunk plan: %s\n", dfx_last_error());
       return 1;
     }
     hipEventRecord(e1, c->stream);
@@ -130,7 +163,8 @@ int main(int argc, char** argv) {
   int err = 0;
   hipMemcpy(&err, &c->ds->err, 4, hipMemcpyDeviceToHost);
   printf("locbench B=%lld k=%d kbits=%d kwargs='%s'%s: %.4f ms per Localizer, U=%u, err=%d\n",
-         (long long)B, k, kbits, kw, valued ? " valued" : "", tot / iters, u, err);
+         (long long)B, k, kbits, kw, valued ? " valued" : zipf ? " zipf (+ chunk plan)" : "",
+         tot / iters, u, err);
   dfx_ctx_destroy(ctx);
   return 0;
 }
