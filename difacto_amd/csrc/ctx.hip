@@ -287,7 +287,7 @@ static void release_ws(Workspace& w) {
                     &w.vpos, &w.p, &w.pred, &w.XVp, &w.rowtmp, &w.dscratch, &w.os, &w.wv,
                     &w.occ_row, &w.occ_x, &w.ak0, &w.ak1, &w.av0, &w.av1,
                     &w.oflags, &w.ofrank, &w.osegstart, &w.osegslot, &w.oseg_of, &w.osorted,
-                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.lbcnt, &w.lbq, &w.lbsplit};
+                    &w.ivstat, &w.live, &w.hstat, &w.vlist, &w.lbcnt, &w.lbq, &w.lbsplit, &w.cptiles};
   for (DevBuf* b : bufs) b->release();
   if (w.lb_hint) (void)hipHostFree(w.lb_hint);
   w.lb_hint = nullptr;

@@ -1466,14 +1466,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
 
 // one group per chunk of a long segment: partial {g_w, XXp, sum (XV p) x} over its
 // kChunkOcc occurrences in order (the same terms as k_fm_bwd's walk)
-template <int G, int CPL, bool VEC = false>
-__global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
-  constexpr int CPB = kFmNT / G;
+template <int G, int CPL, bool VEC>
+__device__ __attribute__((always_inline)) inline void chunk_one(const BwdArgs& a, int64_t ch,
+                                                                int l) {
   constexpr int UNR = 4;
-  const int g = threadIdx.x / G;
-  const int l = threadIdx.x % G;
-  const int64_t ch = (int64_t)blockIdx.x * CPB + g;
-  if (ch >= (int64_t)*a.nchunks) return;
   const uint32_t u = a.chunk_seg[ch];
   const uint32_t s0 = a.segstart[u] + (uint32_t)(ch - a.choff[u]) * kChunkOcc;
   const uint32_t send = a.segstart[u + 1];
@@ -1558,6 +1554,18 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
     if (cd < d) pc[2 + cd] = acc[k];
   }
 }
+// a bounded grid strides over the chunks: a batch with none (uniform keys) pays for a few
+// thousand blocks that exit at once on every step otherwise
+constexpr int kChunkGrid = 2048;
+template <int G, int CPL, bool VEC = false>
+__global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
+  constexpr int CPB = kFmNT / G;
+  const int g = threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const int64_t nch = (int64_t)*a.nchunks;
+  for (int64_t ch = (int64_t)blockIdx.x * CPB + g; ch < nch; ch += (int64_t)gridDim.x * CPB)
+    chunk_one<G, CPL, VEC>(a, ch, l);
+}
 
 // A key of >= kHotChunks chunks (the hottest keys of a skewed batch: C5's top key has ~3500
 // chunks of 128 occurrences) gets its chunk partials pre-summed in two fixed-shape levels, and
@@ -1569,12 +1577,10 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_chunks(BwdArgs a) {
 // key's partials serially (~110 round trips of 16 loads for the top key), C5's longest chain
 // after the chunks.
 constexpr int kHotGroup = 32, kHotNT = 1024, kHotGrid = 256;
-__global__ __launch_bounds__(256) void k_chunk_hotgroup(BwdArgs a) {
+__device__ inline void hotgroup_one(const BwdArgs& a, int64_t i) {
   const int P = a.d + 2;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t ch = i / P;
   const int j = (int)(i - ch * P);
-  if (ch >= (int64_t)*a.nchunks) return;
   const uint32_t u = a.chunk_seg[ch];
   const uint32_t c0 = a.choff[u];
   const uint32_t k = (uint32_t)ch - c0;
@@ -1592,6 +1598,12 @@ __global__ __launch_bounds__(256) void k_chunk_hotgroup(BwdArgs a) {
   for (int q = 0; q < kHotGroup; ++q)
     if ((uint32_t)q < n) s += v[q];
   a.part[ch * P + j] = s;
+}
+__global__ __launch_bounds__(256) void k_chunk_hotgroup(BwdArgs a) {
+  const int64_t n = (int64_t)*a.nchunks * (a.d + 2);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    hotgroup_one(a, i);
 }
 __device__ inline void hotsum_key(const BwdArgs& a, uint32_t c0, uint32_t nc, double* part_w) {
   const int P = a.d + 2;
@@ -1670,13 +1682,14 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, boo
   // chunk on d / 4 lanes (same per-coordinate sums: the partials are bit-identical)
   lanes_for(a.d, aligned && a.d >= 64, &G, &CPL, &vec);
   const int64_t cpb = kFmNT / G;
-  dim3 grid((unsigned)((chunk_bound + cpb - 1) / cpb));
+  dim3 grid((unsigned)std::min<int64_t>(kChunkGrid, (chunk_bound + cpb - 1) / cpb));
 #define DFX_BWDC(GG, CC, VV)                                                              \
   if (G == GG && CPL == CC && vec == VV) {                                                \
     hipLaunchKernelGGL((k_fm_bwd_chunks<GG, CC, VV>), grid, dim3(kFmNT), 0, st, a);      \
     DFX_HIP(hipGetLastError());                                                           \
     if (chunk_bound >= (int64_t)kHotChunks) {                                             \
-      hipLaunchKernelGGL(k_chunk_hotgroup, dim3((unsigned)((chunk_bound * (a.d + 2) + 255) / 256)), \
+      hipLaunchKernelGGL(k_chunk_hotgroup,                                                  \
+                         dim3((unsigned)std::min<int64_t>(kChunkGrid, (chunk_bound * (a.d + 2) + 255) / 256)), \
                          dim3(256), 0, st, a);                                              \
       hipLaunchKernelGGL(k_chunk_hotsum,                                                    \
                          dim3((unsigned)std::min<int64_t>(kHotGrid, (chunk_bound + kHotNT - 1) / kHotNT)), \

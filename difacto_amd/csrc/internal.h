@@ -111,7 +111,7 @@ struct Workspace {
   DevBuf hstat;     // the Localizer's heads / write pass: per tile its tagged look-back word
   // the bucket Localizer (locbucket.hip): per (tile, bucket) counts / prefixes, per bucket its
   // total and start; per item its row / position when the items are not packed (and scratch)
-  DevBuf lbcnt, lbq, lbsplit;
+  DevBuf lbcnt, lbq, lbsplit, cptiles;
   // pinned, written by the device: [0] buckets over the LDS capacity in the last bucket
   // Localizer of this workspace, [1] radix Localizers run since, [2] 1 packed / 2 not
   unsigned int* lb_hint = nullptr;
@@ -313,10 +313,9 @@ inline constexpr int kSortItems(int it) { return it << 16; }
 // flags |= kSortLookback(lb): predecessor words a look-back step reads (4 = default, 16, 32)
 inline constexpr int kSortLookback(int lb) { return lb << 24; }
 constexpr int kSortMetaPack = 25;
-// sortmeta[24]: the sort's launch epoch (tags its look-back words); [26] / [27]: the tile
-// tickets of the Localizer's one-pass write and of the chunk plan (localize.hip k_loc_write,
-// k_chunk_plan), reset by each sort's plan
-constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26, kSortMetaCpTile = 27;
+// sortmeta[24]: the sort's launch epoch (tags its look-back words); [26]: the tile tickets of
+// the Localizer's one-pass write (localize.hip k_loc_write), reset by each sort's plan
+constexpr int kSortMetaEpoch = 24, kSortMetaHwTile = 26;
 // flags |= kSortNT: the scatter passes load and store their items with the streaming policy
 constexpr int kSortNT = 8;
 __device__ inline bool sort_packed(const unsigned* meta) { return meta[kSortMetaPack] != 0u; }
@@ -378,6 +377,9 @@ int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* c
 
 // exclusive scan of ntiles tile sums in place (one block); grand total -> *total_dev
 void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev);
+// the same, skipped (total 0) while *gate == 0
+void scan_tiles_top_gated(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev,
+                          const uint32_t* gate);
 
 // Localizer::Compact on the device (localize.hip), on lane L.  Leaves in L's workspace the
 // sorted (key, {pos, row}) pairs (buffer selected by L.ds->sortmeta[31]) and U in

@@ -282,54 +282,75 @@ __global__ void k_loc_cnt(const DevState* ds, const uint32_t* segstart, float* c
 __global__ void k_set_u(DevState* ds, unsigned v) { ds->u_count = v; }
 
 // ---- chunk plan of long segments ------------------------------------------------------
-// ds->n_init is nonzero when the batch has long segments (reset by k_loc_init, raised by
-// k_loc_heads or the one-pass k_loc_write).  One launch: tiles of 2048 segments, taken by ticket;
-// per segment its chunk count
-// (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan by decoupled look-back
-// (choff), the chunk -> segment table, the total.  With no long segment (uniform keys) it
-// writes the total 0 and exits.
-__global__ __launch_bounds__(kLocNT) void k_chunk_plan(const uint32_t* segstart, DevState* ds,
-                                                       unsigned long long* stat, uint32_t* choff,
-                                                       uint32_t* chunk_seg, uint32_t* nchunks) {
+// ds->n_init is nonzero when the batch has long segments (reset by k_loc_init / k_lb_init,
+// raised by k_loc_heads, the one-pass k_loc_write or the bucket Localizer).  Per segment its
+// chunk count (ceil(len / kChunkOcc) when len > kChunkOcc), their exclusive scan (choff), the
+// chunk -> segment table and the total, as reduce, top scan, apply over tiles of 2048 segments:
+// three short launches with no chain between tiles (a look-back pass over C5's ~300 tiles took
+// ~60 µs, each tile waiting on its predecessor's flag).  With no long segment (uniform keys)
+// every launch exits at once and the total is 0.
+__device__ inline uint32_t seg_chunks(const uint32_t* segstart, int64_t u) {
+  const uint32_t len = segstart[u + 1] - segstart[u];
+  return len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
+}
+
+__global__ __launch_bounds__(kLocNT) void k_chunk_count(const uint32_t* segstart,
+                                                        const DevState* ds, uint32_t* tsum) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
-  __shared__ uint32_t s_pre;
-  if (ds->n_init == 0u) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *nchunks = 0u;
-    return;
-  }
-  unsigned* meta = ds->sortmeta;
-  // tile by ticket (zeroed by k_os_plan / k_lb_init), in block start order: a tile's
-  // predecessors are held by running blocks even beside another look-back kernel
-  __shared__ uint32_t s_tile;
-  if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaCpTile], 1u);
-  __syncthreads();
-  const int64_t tile = s_tile;
-  const int64_t U = (int64_t)ds->u_count;
-  if (tile * kLocTile >= U) return;  // no later tile waits on this one
+  if (ds->n_init == 0u) return;
+  const int64_t U = (int64_t)ds->u_count, tile = blockIdx.x;
+  const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kLocItems; ++i)
+    if (base + i < U) s += seg_chunks(segstart, base + i);
+  uint32_t tot;
+  (void)block_excl_scan<kLocNT>(s, lds, &tot);
+  if (threadIdx.x == 0) tsum[tile] = tot;  // tiles past U: 0
+}
+
+__global__ __launch_bounds__(kLocNT) void k_chunk_write(const uint32_t* segstart,
+                                                        const DevState* ds, const uint32_t* tsum,
+                                                        uint32_t* choff, uint32_t* chunk_seg) {
+  __shared__ uint32_t lds[kLocNT / kWave + 1];
+  constexpr int kList = 256;  // segments of many chunks: their table entries written block-wide
+  __shared__ uint32_t s_u[kList], s_b[kList], s_c[kList];
+  __shared__ int s_n;
+  if (ds->n_init == 0u) return;
+  const int64_t U = (int64_t)ds->u_count, tile = blockIdx.x;
+  if (tile * kLocTile >= U) return;
+  if (threadIdx.x == 0) s_n = 0;
   const int64_t base = tile * kLocTile + (int64_t)threadIdx.x * kLocItems;
   uint32_t cnt[kLocItems];
   uint32_t s = 0;
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
-    cnt[i] = 0;
-    if (base + i < U) {
-      const uint32_t len = segstart[base + i + 1] - segstart[base + i];
-      cnt[i] = len > (uint32_t)kChunkOcc ? (len + kChunkOcc - 1) / kChunkOcc : 0u;
-    }
+    cnt[i] = base + i < U ? seg_chunks(segstart, base + i) : 0u;
     s += cnt[i];
   }
-  uint32_t tot;
-  const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
-  uint32_t incl = ex + tile_lookback(stat, tile, cp_tag(meta), tot, &ds->err, &s_pre);
+  uint32_t incl = block_excl_scan<kLocNT>(s, lds, nullptr) + tsum[tile];
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     const int64_t u = base + i;
     if (u >= U) break;
     choff[u] = incl;
-    for (uint32_t c = 0; c < cnt[i]; ++c) chunk_seg[incl + c] = (uint32_t)u;
+    int at = -1;
+    if (cnt[i] > 16u) {
+      at = atomicAdd(&s_n, 1);
+      if (at < kList) {
+        s_u[at] = (uint32_t)u;
+        s_b[at] = incl;
+        s_c[at] = cnt[i];
+      }
+    }
+    if (at < 0 || at >= kList)
+      for (uint32_t c = 0; c < cnt[i]; ++c) chunk_seg[incl + c] = (uint32_t)u;
     incl += cnt[i];
-    if (u == U - 1) *nchunks = incl;
   }
+  __syncthreads();
+  const int n = s_n < kList ? s_n : kList;
+  for (int e = 0; e < n; ++e)  // (a hot key's thousands of chunks: one lane would walk them)
+    for (uint32_t c = threadIdx.x; c < s_c[e]; c += kLocNT) chunk_seg[s_b[e] + c] = s_u[e];
 }
 
 int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* choff,
@@ -338,14 +359,16 @@ int chunk_plan(const Lane& L, int64_t nnz, const uint32_t* segstart, uint32_t* c
     DFX_HIP(hipMemsetAsync(nchunks_dev, 0, sizeof(uint32_t), L.stream));
     return DFX_OK;
   }
-  const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
+  const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;  // U <= nnz
   Workspace& ws = *L.ws;
-  void* before = ws.hstat.p;
-  DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * ntiles));
-  if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
-    DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, segstart,
-                     L.ds, ws.hstat.as<unsigned long long>(), choff, chunk_seg, nchunks_dev);
+  DFX_TRY(ws.cptiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+  uint32_t* ts = ws.cptiles.as<uint32_t>();
+  const uint32_t* gate = &L.ds->n_init;
+  hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, segstart,
+                     L.ds, ts);
+  scan_tiles_top_gated(L, ts, ntiles, nchunks_dev, gate);
+  hipLaunchKernelGGL(k_chunk_write, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, segstart,
+                     L.ds, ts, choff, chunk_seg);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

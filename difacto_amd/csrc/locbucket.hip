@@ -235,7 +235,6 @@ __global__ void k_lb_init(DevState* ds) {
   ds->lb_nhot = 0;
   unsigned* meta = ds->sortmeta;
   meta[kSortMetaEpoch] = ++ds->sort_epoch;  // tags this Localizer's look-back words
-  meta[kSortMetaCpTile] = 0;                // the chunk plan's tile tickets
 }
 
 __device__ inline unsigned long long lb_wave_or(unsigned long long v) {
@@ -266,7 +265,8 @@ constexpr int kLbUnr = 8;  // ids in flight per thread
 // the histogram and scatter kernels' blocks: 16 waves on a tile by default, for the loads in
 // flight (kwarg lb_hnt = 256 | 512 | 1024)
 
-template <int HNT>
+// HOT: instantiated with the hot-key map's lookup (the key map's launches keep their registers)
+template <int HNT, bool HOT>
 __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
   extern __shared__ uint64_t lb_dyn64[];  // 8-byte aligned: the splitter keys follow hist
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(HNT) void k_lb_hist(LbArgs a) {
   const LbMap m = lb_map(a.ds, a.wbits);
   const int t = threadIdx.x;
   for (uint32_t d = t; d < m.nbk; d += kLbHNT) hist[d] = 0;
-  const bool qs = lb_hot_on(a);
+  const bool qs = HOT && lb_hot_on(a);
   LbHot hm{};
   if (qs) hm = lb_stage_hot(a, hist + m.nbk, t, kLbHNT);
   const int64_t tile = blockIdx.x;
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kLbScanWaves * kWave) void k_lb_colscan(LbArgs a) {
   }
 }
 
-template <bool S, int HNT>
+template <bool S, int HNT, bool HOT>
 __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   constexpr int kLbHNT = HNT, kLbHWaves = HNT / kWave;
   extern __shared__ uint64_t lb_dyn64[];
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t* cur = reinterpret_cast<uint32_t*>(lb_dyn64);  // per bucket: this tile's next slot
   uint64_t* offs = lb_dyn64 + (m.nbk + 1u) / 2;
   const int t = threadIdx.x;
-  const bool qs = lb_hot_on(a);
+  const bool qs = HOT && lb_hot_on(a);
   LbHot hm{};
   if (qs) hm = lb_stage_hot(a, offs + a.rt + 1, t, kLbHNT);
   const int64_t tile = blockIdx.x;
@@ -1000,7 +1000,8 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
       const uint64_t up = __shfl_up(kb, 1, kWave);
       const bool h = valid && (i == 0 || kb != (l == 0 ? prev : up));
       if (valid && i >= kChunkOcc && kb == lb_keybits(p, K[i - kChunkOcc])) longseg = true;
-      if (valid && i >= th && kb == lb_keybits(p, K[i - th])) hot = true;
+      // (a run of >= th is a long one first: uniform batches never read the extra item)
+      if (longseg && valid && i >= th && kb == lb_keybits(p, K[i - th])) hot = true;
       prev = __shfl(kb, kWave - 1, kWave);
       const uint64_t hb = __ballot(h);
       if (!(a.diag & 4) && valid) {
@@ -1048,27 +1049,29 @@ __global__ __launch_bounds__(kLbScanNT) void k_lb_bscan(LbArgs a) {
   const uint32_t nbk = 1u << a.wbits;
   const uint32_t per = (nbk + kLbScanNT - 1) / kLbScanNT;
   // a bucket whose first key is the previous non-empty bucket's last continues that key's run
-  // (the hot-key map spreads a hot key over buckets): its first head is no new rank
+  // (the hot-key map spreads a hot key over buckets): its first head is no new rank.  Only
+  // under the hot-key map (a key map keeps a key in one bucket)
+  const bool hm = lb_hot_on(a);
   int lastne = -1;
-  for (uint32_t i = 0; i < per; ++i) {
+  for (uint32_t i = 0; hm && i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < nbk && a.bstart[d + 1] > a.bstart[d]) lastne = (int)d;
   }
   s_last[t] = lastne;
   __syncthreads();
-  for (int off = 1; off < kLbScanNT; off <<= 1) {  // inclusive max scan
+  for (int off = 1; hm && off < kLbScanNT; off <<= 1) {  // inclusive max scan
     const int v = t >= off ? s_last[t - off] : -1;
     __syncthreads();
     if (v > s_last[t]) s_last[t] = v;
     __syncthreads();
   }
-  int prev = t > 0 ? s_last[t - 1] : -1;
+  int prev = t > 0 && hm ? s_last[t - 1] : -1;
   uint32_t mine = 0, anycont = 0;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < nbk) {
       uint32_t c = 0;
-      if (a.bstart[d + 1] > a.bstart[d]) {
+      if (hm && a.bstart[d + 1] > a.bstart[d]) {
         if (prev >= 0 && a.bfk[d] == a.blk[prev]) c = 1;
         prev = (int)d;
       }
@@ -1157,22 +1160,19 @@ __global__ __launch_bounds__(kLbHotMax) void k_lb_hotmap(LbArgs a) {
   sk[t] = (uint32_t)t < nh ? a.hl_key[t] : ~0ull;
   sl[t] = (uint32_t)t < nh ? a.hl_len[t] : 0u;
   __syncthreads();
-  for (int k = 2; k <= kLbHotMax; k <<= 1) {  // bitonic sort by key (keys are distinct)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const int p = t ^ j;
-      if (p > t) {
-        const bool up = (t & k) == 0;
-        const uint64_t x = sk[t], y = sk[p];
-        if ((x > y) == up) {
-          sk[t] = y;
-          sk[p] = x;
-          const uint32_t lx = sl[t];
-          sl[t] = sl[p];
-          sl[p] = lx;
-        }
-      }
-      __syncthreads();
+  {  // sorted by key: a key's place is the count of smaller keys (keys are distinct; every
+     // thread reads the same key at a time, an LDS broadcast)
+    const uint64_t mk = sk[t];
+    const uint32_t ml = sl[t];
+    uint32_t r = 0;
+    if ((uint32_t)t < nh)
+      for (uint32_t i = 0; i < nh; ++i) r += sk[i] < mk ? 1u : 0u;
+    __syncthreads();
+    if ((uint32_t)t < nh) {
+      sk[r] = mk;
+      sl[r] = ml;
     }
+    __syncthreads();
   }
   const uint32_t len = sl[t];
   uint32_t mass;
@@ -1351,10 +1351,15 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
       kWave, std::min<int64_t>(nnz / ((int64_t)1 << wbits_key) / 2, kLbCap));
   const size_t sp_bytes = a.hm_lds ? lb_hot_lds(nbk) : 0;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
-#define DFX_LB_HIST(NT) \
-  lb_lds_attr((const void*)k_lb_hist<NT>);                                                   \
-  hipLaunchKernelGGL(k_lb_hist<NT>, dim3((unsigned)ntiles), dim3(NT),                         \
-                     nbk * sizeof(uint32_t) + sp_bytes, L.stream, a);
+#define DFX_LB_HIST(NT)                                                                     \
+  if (a.hm_lds) {                                                                           \
+    lb_lds_attr((const void*)k_lb_hist<NT, true>);                                          \
+    hipLaunchKernelGGL((k_lb_hist<NT, true>), dim3((unsigned)ntiles), dim3(NT),             \
+                       nbk * sizeof(uint32_t) + sp_bytes, L.stream, a);                     \
+  } else {                                                                                  \
+    hipLaunchKernelGGL((k_lb_hist<NT, false>), dim3((unsigned)ntiles), dim3(NT),            \
+                       nbk * sizeof(uint32_t), L.stream, a);                                \
+  }
   // lb_hnt (0: auto): 512-thread blocks for valued batches, whose scatter also writes the
   // {row, value} pairs (C2 +5.6 %), 1024 for binary ones (C3: 1024 best)
   const int hnt = c->lb_hnt ? c->lb_hnt : (valued ? 512 : 1024);
@@ -1367,13 +1372,17 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   const size_t scatter_lds =
       ((nbk + 1) & ~1u) * sizeof(uint32_t) + (rt + 1) * sizeof(uint64_t) + sp_bytes;
 #define DFX_LB_SCAT(NT)                                                                    \
-  lb_lds_attr((const void*)k_lb_scatter<true, NT>);                                        \
-  lb_lds_attr((const void*)k_lb_scatter<false, NT>);                                       \
+  lb_lds_attr((const void*)k_lb_scatter<true, NT, false>);                                 \
+  lb_lds_attr((const void*)k_lb_scatter<false, NT, false>);                                \
+  lb_lds_attr((const void*)k_lb_scatter<false, NT, true>);                                 \
   if (valued)                                                                              \
-    hipLaunchKernelGGL((k_lb_scatter<true, NT>), dim3((unsigned)ntiles), dim3(NT), scatter_lds, \
-                       L.stream, a);                                                       \
+    hipLaunchKernelGGL((k_lb_scatter<true, NT, false>), dim3((unsigned)ntiles), dim3(NT),   \
+                       scatter_lds, L.stream, a);                                          \
+  else if (a.hm_lds)                                                                       \
+    hipLaunchKernelGGL((k_lb_scatter<false, NT, true>), dim3((unsigned)ntiles), dim3(NT),   \
+                       scatter_lds, L.stream, a);                                          \
   else                                                                                     \
-    hipLaunchKernelGGL((k_lb_scatter<false, NT>), dim3((unsigned)ntiles), dim3(NT),         \
+    hipLaunchKernelGGL((k_lb_scatter<false, NT, false>), dim3((unsigned)ntiles), dim3(NT),  \
                        scatter_lds, L.stream, a);
   if (hnt == 256) { DFX_LB_SCAT(256) }
   else if (hnt == 512) { DFX_LB_SCAT(512) }

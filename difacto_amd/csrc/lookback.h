@@ -137,11 +137,8 @@ __device__ inline uint32_t block_lookback(unsigned long long* stat, int64_t tile
                        __HIP_MEMORY_SCOPE_AGENT);
   return pre;
 }
-// tag spaces of the two users of Workspace::hstat on a lane (the same sort epoch)
+// the tag of the Localizer's one-pass write's look-back words in Workspace::hstat (its sort epoch)
 __device__ inline uint32_t hw_tag(const unsigned* meta) { return meta[kSortMetaEpoch] & 0x1FFFFFFFu; }
-__device__ inline uint32_t cp_tag(const unsigned* meta) {
-  return (meta[kSortMetaEpoch] & 0x1FFFFFFFu) | 0x20000000u;
-}
 
 
 }  // namespace dfx

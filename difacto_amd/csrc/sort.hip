@@ -90,7 +90,6 @@ __global__ __launch_bounds__(kOsNT) void k_os_plan(const unsigned long long* dif
       meta[kMetaTile + r] = 0;
     }
     meta[kSortMetaHwTile] = 0;
-    meta[kSortMetaCpTile] = 0;
     meta[kMetaPack] = (pack && q > 0) ? (1u | ((unsigned)lo8 << 8) | ((unsigned)pack_rb8 << 16))
                                       : 0u;
     meta[31] = (unsigned)(q & 1);
@@ -621,6 +620,12 @@ __global__ __launch_bounds__(kScanNT) void k_scan_apply(uint32_t* data, int64_t 
     }
     __syncthreads();  // lds is reused by the next tile
   }
+}
+
+void scan_tiles_top_gated(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev,
+                          const uint32_t* gate) {
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, L.stream, tilesum, ntiles, total_dev,
+                     gate);
 }
 
 void scan_tiles_top(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint32_t* total_dev) {
