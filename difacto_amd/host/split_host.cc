@@ -369,7 +369,10 @@ struct GpuSplitStore::Impl {
   uint64_t max_index;
   int N, L, d, PS, PX;
   int next_slot = 0;
-  // step slots: two (pipelined), three (stale: a step's owner state is held until its
+  // step slots: three when pipelined — step s + 1's partition and owner Localizer then wait
+  // only for step s - 2, and run beside step s's forward and backward (with two they waited for
+  // step s - 1's backward and sat in front of step s + 1's forward: ~0.2 ms of the split's N = 1
+  // step); the stale schedule needs three anyway (a step's owner state is held until its
   // deferred backward while the step after next is localized); the library holds three
   static constexpr int kSlotsMax = 3;
   int nslots = 2;
@@ -400,7 +403,7 @@ struct GpuSplitStore::Impl {
 
   Impl(SplitTransport* tr, int pipe, uint64_t mi)
       : t(tr), pipelined(pipe != 0), stale(pipe == 2), max_index(mi) {
-    nslots = stale ? 3 : 2;
+    nslots = pipelined ? 3 : 2;
     N = t->nranks();
     L = t->nlocal();
     d = dfx_ctx_vdim(t->ctx(0));
