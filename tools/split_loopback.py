@@ -23,12 +23,19 @@ def main():
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 12
     rows = int(sys.argv[4]) if len(sys.argv) > 4 else 12500
     kw = dict(V_dim=16, V_threshold=0, l1=0.0, lr=0.1, V_lr=0.01)
-    ctxs = [H.Context(0, max_keys=1 << 22, push_agg="sum", **kw) for _ in range(N)]
+    # one stream per shard, as each rank has its own (a Context takes the current torch
+    # stream: on the default one all N shards' compute would queue on one stream)
+    streams = [torch.cuda.Stream() for _ in range(N)]
+    ctxs = []
+    for r in range(N):
+        with torch.cuda.stream(streams[r]):
+            ctxs.append(H.Context(0, max_keys=1 << 22, push_agg="sum", **kw))
     shards = [DI.Shard(c, N) for c in ctxs]
     store = DI.SplitStore(shards, stale=stale)
     blocks = [[D.synthetic(rows, 39, 1 << 22, seed=1000 * s + r) for r in range(N)]
               for s in range(steps)]
     dev = [[H.DeviceRowBlock(ctxs[r], b[r]) for r in range(N)] for b in blocks]
+    torch.cuda.synchronize()
     store.submit(dev[0], H.kTraining, push_cnt=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
