@@ -789,6 +789,14 @@ int launch_fwd_records(const FwdArgs& a, hipStream_t st, int* nblk) {
 }
 
 // ---- backward: sorted-key segmented reduction --------------------------------------------
+// p of row r for a backward that also reads the row's XV*p: from the XV*p row when p shares
+// its last line (4d % 128 != 0: d = 16's 68 bytes in one 128-byte line), else from the
+// compact per-row array (d = 64 / 128: p would be a line of its own in a 384 / 640-byte row,
+// where the 400-KB array stays in the L2); the split owner has only the rows (p == nullptr)
+__device__ inline float row_p(const BwdArgs& a, uint32_t r, int d, int64_t xs) {
+  if (a.p && (xs <= d || (4 * d) % 128 == 0)) return a.p[r];
+  return a.XVp[(int64_t)r * xs + d];
+}
 template <int G, int CPL, bool FUSED, bool VEC>
 __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
   constexpr int SPB = kFmNT / G;
@@ -998,7 +1006,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
         float xl;
         const uint32_t rl = occ_get(a, i, valued, false, &xl);
-        const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
+        const float pl = row_p(a, rl, d, xs);
         const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
         for (int t = 0; t < G; ++t) {
@@ -1059,7 +1067,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         float pw[UNR];
 #pragma unroll
         for (int t = 0; t < UNR; ++t)
-          pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+          pw[t] = row_p(a, rw[t], d, xs);
         const uint32_t in = i0 + UNR;
         uint32_t rn[UNR];
         float xn[UNR];
@@ -1301,7 +1309,8 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
           float pw[WU];
 #pragma unroll
           for (int t = 0; t < WU; ++t)
-            pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+            // (this pass reads no XV*p: the compact array whenever there is one)
+            pw[t] = a.p ? a.p[rw[t]] : a.XVp[(int64_t)rw[t] * xs + d];
           const uint32_t in = i0 + WU;
           uint32_t rn[WU];
           float xn[WU];
@@ -1490,7 +1499,7 @@ __device__ __attribute__((always_inline)) inline void chunk_one(const BwdArgs& a
       const uint32_t i = i0 + (uint32_t)l < s1 ? i0 + (uint32_t)l : s1 - 1;
       float xl;
       const uint32_t rl = occ_get(a, i, valued, false, &xl);
-      const float pl = xs > d ? a.XVp[(int64_t)rl * xs + d] : a.p[rl];
+      const float pl = row_p(a, rl, d, xs);
       const uint32_t n = s1 - i0 < (uint32_t)G ? s1 - i0 : (uint32_t)G;
 #pragma unroll
       for (int t0 = 0; t0 < G; t0 += WU) {
@@ -1527,7 +1536,7 @@ __device__ __attribute__((always_inline)) inline void chunk_one(const BwdArgs& a
     }
 #pragma unroll
     for (int t = 0; t < UNR; ++t) {
-      pw[t] = xs > d ? a.XVp[(int64_t)rw[t] * xs + d] : a.p[rw[t]];
+      pw[t] = row_p(a, rw[t], d, xs);
       load_coords<CPL, false>(d > 0 ? a.XVp + (int64_t)rw[t] * xs : a.zpad, l, d, xr[t]);
     }
 #pragma unroll
