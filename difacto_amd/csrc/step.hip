@@ -26,10 +26,12 @@ namespace dfx {
 
 // Row stride of the fused step's XV_*p rows: a multiple of 32 floats (128 B) carrying p after
 // XV_*p, so the backward's per-occurrence p and XV_*p sit in one 128-byte line (+3 % of the
-// step at d = 16, same-box A/B).  Context kwarg xvp_row=0: rows of d floats, p apart.
+// step at d = 16, same-box A/B).  Context kwarg xvp_row=0: rows of d floats, p apart.  At d a
+// multiple of 32 p would fill a 128-byte line of its own: the rows are d floats and the
+// backward reads p from the per-row array (fm.hip row_p), which stays in the L2
 int xvp_stride(const Context* c) {
   const int d = c->P.V_dim;
-  return (c->xvp_row && d > 0) ? (d + 1 + 31) / 32 * 32 : d;
+  return (c->xvp_row && d > 0 && d % 32 != 0) ? (d + 1 + 31) / 32 * 32 : d;
 }
 
 // main lane: per-row arrays of the forward / backward and the InitV scan
