@@ -92,6 +92,7 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 // exactly as k_initv.
 // The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
 constexpr int kIvItems = 16, kIvTile = kStNT * kIvItems;
+constexpr int kIvMaxD = 256;  // V rows drawn a coordinate per thread up to this V_dim
 
 __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, uint32_t* total,
                                                          const uint32_t* slot, Table T,
@@ -134,27 +135,65 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
   const uint32_t pre = block_lookback<kStNT>(status, tile, tag, tot, &ds->err, s_lb);
   if (threadIdx.x == 0 && base + kIvTile >= n) *total = pre + tot;  // the last tile
-  if (cnt == 0) return;
-  uint32_t e = pre + ex;
+  if (tot == 0) return;  // block-uniform
   const int d = T.d;
+  uint32_t e = pre + ex;
+  if (d > kIvMaxD) {  // (wide V: each thread draws its keys' rows in turn)
+#pragma unroll 1
+    for (int k = 0; k < kIvItems; ++k) {
+      if (!f[k]) continue;
+      const int64_t u = i0 + k;
+      uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+      const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
+      ++e;
+      if (vr >= T.vcap) {
+        atomicOr(&ds->err, kErrPoolFull);
+        continue;
+      }
+      float* V = row_V(T, vr);
+      float* C = row_C(T, vr);
+      for (int q = 0; q < d; ++q) {
+        V[q] = initv_value(rand_r_dev(&s), scale);
+        C[q] = 0.f;
+      }
+      ent_at(T, slot[u])->vrow = (int32_t)vr;
+    }
+    return;
+  }
+  // the block's requested keys, each with its V row and the LCG state at its first draw
+  // (3·d·rank steps past the seed, sgd_updater.cc:118-121), then every (key, coordinate) drawn
+  // by its own thread: coordinate j's state is 3·j steps on (A_j·state + C_j), the same rand_r
+  // values as one thread walking the row — a row's d draws were one lane's d · 3 dependent LCG
+  // steps (C5: ~0.1 ms of the step with ~1.5 k requests per 4096-key tile)
+  __shared__ uint32_t s_st[kIvTile], s_vr[kIvTile];
+  __shared__ uint32_t s_A[kIvMaxD], s_C[kIvMaxD];
+  uint32_t idx = ex;
 #pragma unroll 1
   for (int k = 0; k < kIvItems; ++k) {
     if (!f[k]) continue;
     const int64_t u = i0 + k;
-    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
     const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
-    ++e;
+    s_st[idx] = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
     if (vr >= T.vcap) {
       atomicOr(&ds->err, kErrPoolFull);
-      continue;
+      s_vr[idx] = 0xFFFFFFFFu;
+    } else {
+      s_vr[idx] = (uint32_t)vr;
+      ent_at(T, slot[u])->vrow = (int32_t)vr;
     }
-    float* V = row_V(T, vr);
-    float* C = row_C(T, vr);
-    for (int q = 0; q < d; ++q) {
-      V[q] = initv_value(rand_r_dev(&s), scale);
-      C[q] = 0.f;
-    }
-    ent_at(T, slot[u])->vrow = (int32_t)vr;
+    ++e;
+    ++idx;
+  }
+  for (int j = threadIdx.x; j < d; j += kStNT) lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
+  __syncthreads();
+  const uint32_t npairs = tot * (uint32_t)d;
+  for (uint32_t q = threadIdx.x; q < npairs; q += kStNT) {
+    const uint32_t i = q / (uint32_t)d, j = q - i * (uint32_t)d;
+    const uint32_t vr = s_vr[i];
+    if (vr == 0xFFFFFFFFu) continue;
+    uint32_t st = s_A[j] * s_st[i] + s_C[j];
+    row_V(T, vr)[j] = initv_value(rand_r_dev(&st), scale);
+    row_C(T, vr)[j] = 0.f;
   }
 }
 
