@@ -139,6 +139,27 @@ __host__ __device__ inline float initv_value(int r, float scale) {
   return (float)(((double)q - 0.5) * (double)scale);
 }
 
+// InitV's rows a coordinate per thread: row i of a block's list starts at LCG state st[i]
+// (3·d·rank steps past the seed) and its coordinate j is the rand_r draw 3·j steps further,
+// (A[j], C[j]) = lcg_jump(3·j) — the values one thread walking the row would draw.  vrow
+// 0xFFFFFFFF: skipped (pool full).  Callers: store.hip k_initv / k_initv_onepass, dist.hip
+// k_dist_initv_sum.
+constexpr int kIvMaxD = 256;  // up to this V_dim; wider rows are drawn a row per thread
+template <int NT, class RowV, class RowC>
+__device__ inline void initv_draw_list(uint32_t n, const uint32_t* st, const uint32_t* vrow,
+                                       int d, float scale, const uint32_t* A, const uint32_t* C,
+                                       RowV row_v, RowC row_c) {
+  const uint32_t npairs = n * (uint32_t)d;
+  for (uint32_t q = threadIdx.x; q < npairs; q += NT) {
+    const uint32_t i = q / (uint32_t)d, j = q - i * (uint32_t)d;
+    const uint32_t vr = vrow[i];
+    if (vr == 0xFFFFFFFFu) continue;
+    uint32_t s = A[j] * st[i] + C[j];
+    row_v(vr)[j] = initv_value(rand_r_dev(&s), scale);
+    row_c(vr)[j] = 0.f;
+  }
+}
+
 // ---- device hash table (open addressing, linear probing) -----------------------------
 // One 32-byte entry per key (SGDEntry, sgd_updater.h:20-34): the probe that finds the key
 // brings the FTRL state and the V-pool row in the same cache line.

@@ -590,31 +590,66 @@ __global__ void k_dist_initv_count(const uint32_t* ftotal, int64_t* out) {
 
 // InitV draws of this owner's flagged keys (key order), ranked after every lower owner's
 // draws of this step: the q-th of them jumps the shared seed by 3*d*(sum_{h<rank} F_h + q)
-__global__ void k_dist_initv_sum(const uint32_t* excl, const uint32_t* ftotal,
-                                 const uint32_t* nuniq, int64_t bound,
-                                 const uint32_t* segslot, const int64_t* Fall, int rank,
-                                 Table T, float scale, const DevState* ds) {
+__global__ __launch_bounds__(kDNT) void k_dist_initv_sum(const uint32_t* excl,
+                                                         const uint32_t* ftotal,
+                                                         const uint32_t* nuniq, int64_t bound,
+                                                         const uint32_t* segslot,
+                                                         const int64_t* Fall, int rank, Table T,
+                                                         float scale, const DevState* ds) {
   const uint32_t F = *ftotal;
   if (F == 0) return;
   int64_t off = 0;
   for (int h = 0; h < rank; ++h) off += Fall[h];
   const int64_t n = std::min<int64_t>(*nuniq, bound);
   const int d = T.d;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
-       u += (int64_t)gridDim.x * blockDim.x) {
-    const uint32_t e = excl[u];
-    const uint32_t nx = (u + 1 < n) ? excl[u + 1] : F;
-    if (nx == e) continue;
-    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
-    const int64_t vr = initv_row(T, ds->n_vrows, e, segslot[u]);
-    if (vr >= T.vcap) continue;  // kErrPoolFull is set by the finalize
-    float* V = row_V(T, vr);
-    float* C = row_C(T, vr);
-    for (int k = 0; k < d; ++k) {
-      V[k] = initv_value(rand_r_dev(&s), scale);
-      C[k] = 0.f;
+  if (d > kIvMaxD) {  // (wide V: a row per thread)
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * blockDim.x) {
+      const uint32_t e = excl[u];
+      const uint32_t nx = (u + 1 < n) ? excl[u + 1] : F;
+      if (nx == e) continue;
+      uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
+      const int64_t vr = initv_row(T, ds->n_vrows, e, segslot[u]);
+      if (vr >= T.vcap) continue;  // kErrPoolFull is set by the finalize
+      float* V = row_V(T, vr);
+      float* C = row_C(T, vr);
+      for (int k = 0; k < d; ++k) {
+        V[k] = initv_value(rand_r_dev(&s), scale);
+        C[k] = 0.f;
+      }
+      ent_at(T, segslot[u])->vrow = (int32_t)vr;
     }
-    ent_at(T, segslot[u])->vrow = (int32_t)vr;
+    return;
+  }
+  // per kDNT keys: the flagged ones listed (a block scan), then drawn a coordinate per thread
+  __shared__ uint32_t s_st[kDNT], s_vr[kDNT], s_A[kIvMaxD], s_C[kIvMaxD];
+  __shared__ uint32_t lds[kDNT / kWave + 1];
+  for (int j = threadIdx.x; j < d; j += kDNT) lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
+  for (int64_t b0 = (int64_t)blockIdx.x * kDNT; b0 < n; b0 += (int64_t)gridDim.x * kDNT) {
+    const int64_t u = b0 + threadIdx.x;
+    uint32_t e = 0;
+    bool f = false;
+    if (u < n) {
+      e = excl[u];
+      f = ((u + 1 < n) ? excl[u + 1] : F) != e;
+    }
+    uint32_t cnt;
+    const uint32_t at = block_excl_scan<kDNT>(f ? 1u : 0u, lds, &cnt);
+    if (f) {
+      const int64_t vr = initv_row(T, ds->n_vrows, e, segslot[u]);
+      s_st[at] = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
+      if (vr >= T.vcap) {
+        s_vr[at] = 0xFFFFFFFFu;  // kErrPoolFull is set by the finalize
+      } else {
+        s_vr[at] = (uint32_t)vr;
+        ent_at(T, segslot[u])->vrow = (int32_t)vr;
+      }
+    }
+    __syncthreads();
+    initv_draw_list<kDNT>(cnt, s_st, s_vr, d, scale, s_A, s_C,
+                          [&](uint32_t r) { return row_V(T, r); },
+                          [&](uint32_t r) { return row_C(T, r); });
+    __syncthreads();
   }
 }
 

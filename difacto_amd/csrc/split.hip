@@ -300,6 +300,13 @@ __global__ __launch_bounds__(kSpNT) void k_split_combine_vec(int64_t row0, int64
   }
 }
 
+// the received rows' p as a compact array (V_dim a multiple of 32: p would be a 128-byte line of
+// its own per occurrence in the backward; fm.hip row_p)
+__global__ void k_split_p_compact(const float* pxv, int64_t R, int xs, int d, float* p) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) p[r] = pxv[r * xs + d];
+}
+
 __global__ void k_split_worker_finalize(DevState* ds, int64_t B) {
   ds->prog[0] += (double)B;       // sgd::Progress of this worker (sgd_learner.cc:213-229)
   ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
@@ -623,6 +630,12 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.occ_row = ows.occ_row.as<uint32_t>();
     g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
     g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d, c->xvp_row); g.d = d;
+    if (d >= 64 && d % 32 == 0 && R > 0) {  // p a line of its own in the rows: compact (row_p)
+      DFX_TRY(ows.p.ensure((size_t)R * 4));
+      hipLaunchKernelGGL(k_split_p_compact, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,
+                         c->stream, pxv, R, g.xs, d, ows.p.as<float>());
+      g.p = ows.p.as<float>();
+    }
     g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from;
     g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
@@ -634,7 +647,6 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream, true));
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
   }
-  (void)R;
   // every owner takes part in the InitV ranking, with or without keys this step
   if (d > 0) {
     c->split_initv_pending[slot] = true;

@@ -55,26 +55,60 @@ __global__ __launch_bounds__(kStNT) void k_initv(int64_t n_host, const uint32_t*
                                                  const DevState* nds, const uint32_t* gate) {
   if (gate && *gate == 0u) return;
   const int64_t n = count_of(n_host, nds);
-  // strided over a grid capped like a gated scan's (run_initv)
-  for (int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x; u < n;
-       u += (int64_t)gridDim.x * kStNT) {
-    const uint32_t e = excl[u];
-    const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
-    if (nx == e) continue;
-    const int d = T.d;
-    uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
-    const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
-    if (vr >= T.vcap) {
-      atomicOr(&ds->err, kErrPoolFull);
-      continue;
+  const int d = T.d;
+  if (d > kIvMaxD) {  // (wide V: a row per thread)
+    // strided over a grid capped like a gated scan's (run_initv)
+    for (int64_t u = (int64_t)blockIdx.x * kStNT + threadIdx.x; u < n;
+         u += (int64_t)gridDim.x * kStNT) {
+      const uint32_t e = excl[u];
+      const uint32_t nx = (u + 1 < n) ? excl[u + 1] : *total;
+      if (nx == e) continue;
+      uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+      const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
+      if (vr >= T.vcap) {
+        atomicOr(&ds->err, kErrPoolFull);
+        continue;
+      }
+      float* V = row_V(T, vr);
+      float* C = row_C(T, vr);
+      for (int k = 0; k < d; ++k) {
+        V[k] = initv_value(rand_r_dev(&s), scale);
+        C[k] = 0.f;
+      }
+      ent_at(T, slot[u])->vrow = (int32_t)vr;
     }
-    float* V = row_V(T, vr);
-    float* C = row_C(T, vr);
-    for (int k = 0; k < d; ++k) {
-      V[k] = initv_value(rand_r_dev(&s), scale);
-      C[k] = 0.f;
+    return;
+  }
+  // per kStNT keys: the flagged ones listed (a block scan), then drawn a coordinate per thread
+  __shared__ uint32_t s_st[kStNT], s_vr[kStNT], s_A[kIvMaxD], s_C[kIvMaxD];
+  __shared__ uint32_t lds[kStNT / kWave + 1];
+  for (int j = threadIdx.x; j < d; j += kStNT) lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
+  for (int64_t b0 = (int64_t)blockIdx.x * kStNT; b0 < n; b0 += (int64_t)gridDim.x * kStNT) {
+    const int64_t u = b0 + threadIdx.x;
+    uint32_t e = 0;
+    bool f = false;
+    if (u < n) {
+      e = excl[u];
+      f = ((u + 1 < n) ? excl[u + 1] : *total) != e;
     }
-    ent_at(T, slot[u])->vrow = (int32_t)vr;
+    uint32_t cnt;
+    const uint32_t at = block_excl_scan<kStNT>(f ? 1u : 0u, lds, &cnt);
+    if (f) {
+      const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
+      s_st[at] = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+      if (vr >= T.vcap) {
+        atomicOr(&ds->err, kErrPoolFull);
+        s_vr[at] = 0xFFFFFFFFu;
+      } else {
+        s_vr[at] = (uint32_t)vr;
+        ent_at(T, slot[u])->vrow = (int32_t)vr;
+      }
+    }
+    __syncthreads();
+    initv_draw_list<kStNT>(cnt, s_st, s_vr, d, scale, s_A, s_C,
+                           [&](uint32_t r) { return row_V(T, r); },
+                           [&](uint32_t r) { return row_C(T, r); });
+    __syncthreads();
   }
 }
 
@@ -92,7 +126,6 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 // exactly as k_initv.
 // The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
 constexpr int kIvItems = 16, kIvTile = kStNT * kIvItems;
-constexpr int kIvMaxD = 256;  // V rows drawn a coordinate per thread up to this V_dim
 
 __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, uint32_t* total,
                                                          const uint32_t* slot, Table T,
@@ -186,15 +219,9 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   }
   for (int j = threadIdx.x; j < d; j += kStNT) lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
   __syncthreads();
-  const uint32_t npairs = tot * (uint32_t)d;
-  for (uint32_t q = threadIdx.x; q < npairs; q += kStNT) {
-    const uint32_t i = q / (uint32_t)d, j = q - i * (uint32_t)d;
-    const uint32_t vr = s_vr[i];
-    if (vr == 0xFFFFFFFFu) continue;
-    uint32_t st = s_A[j] * s_st[i] + s_C[j];
-    row_V(T, vr)[j] = initv_value(rand_r_dev(&st), scale);
-    row_C(T, vr)[j] = 0.f;
-  }
+  initv_draw_list<kStNT>(tot, s_st, s_vr, d, scale, s_A, s_C,
+                         [&](uint32_t r) { return row_V(T, r); },
+                         [&](uint32_t r) { return row_C(T, r); });
 }
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
