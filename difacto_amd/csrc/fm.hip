@@ -1217,7 +1217,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
 // — the entry's find-or-insert, g_w and XXp over the key's occurrences in order, FTRL, the InitV
 // flag — and lists each key whose V was pulled with its XXp; pass V takes G lanes per listed key
 // for the sum of (XV*p) x in occurrence order and AdaGrad.  Every term and its order are
-// k_fm_bwd's, so the model is bit-identical; the list's order (wave-aggregated appends) changes
+// k_fm_bwd's, so the model is bit-identical; the list's order (block-aggregated appends) changes
 // only which group updates which key.  Both passes loop over a resident grid.  Measured on C5
 // (same box, kwarg bwd_two_pass): first 1.53 -> 1.85 ms — a wave of pass W ran as long as its
 // longest key's serial walk, a hot key's ~1750 chunk partials one round trip each; with those
@@ -1228,6 +1228,7 @@ constexpr int kBwdWNT = 256;
 __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
   __shared__ int red[kBwdWNT / kWave], redn[kBwdWNT / kWave], redi[kBwdWNT / kWave];
   __shared__ unsigned redl[kBwdWNT / kWave], redo[kBwdWNT / kWave];
+  __shared__ uint32_t wcnt[kBwdWNT / kWave], wbase;
   const int64_t nseg = a.nseg_host >= 0 ? a.nseg_host : (int64_t)a.ds->u_count;
   const int d = a.d;
   const int64_t xs = a.xs > d ? a.xs : d;
@@ -1235,7 +1236,7 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
   int dnew = 0, ninit = 0, nins = 0;
   unsigned nlive = 0, nlocc = 0;
   const int64_t stride = (int64_t)gridDim.x * kBwdWNT;
-  // every lane runs the same number of rounds (the list append is wave-aggregated)
+  // every lane runs the same number of rounds (the list append is block-aggregated)
   const int64_t rounds = (nseg + stride - 1) / stride;
   for (int64_t rd = 0; rd < rounds; ++rd) {
     const int64_t u = rd * stride + (int64_t)blockIdx.x * kBwdWNT + threadIdx.x;
@@ -1355,14 +1356,24 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
         nlocc += len;
       }
     }
-    // the listed keys of this wave: one append
+    // the listed keys of this block: one append (returning atomics on one word serialise,
+    // DESIGN.md (d); a wave each was 9.3 k of them at C5)
     const uint64_t m = __ballot(listed);
-    if (m) {
-      uint32_t base = 0;
-      if (lane_id() == 0) base = atomicAdd(a.vcount, (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, 0, kWave);
-      if (listed) a.vlist[base + (uint32_t)__popcll(m & lanemask_lt())] = item;
+    const int wv = threadIdx.x / kWave;
+    if (lane_id() == 0) wcnt[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int i = 0; i < kBwdWNT / kWave; ++i) {
+        const uint32_t c = wcnt[i];
+        wcnt[i] = t;
+        t += c;
+      }
+      wbase = t ? atomicAdd(a.vcount, t) : 0u;
     }
+    __syncthreads();
+    if (listed) a.vlist[wbase + wcnt[wv] + (uint32_t)__popcll(m & lanemask_lt())] = item;
+    __syncthreads();
   }
   for (int off = 32; off > 0; off >>= 1) {
     dnew += __shfl_xor(dnew, off, kWave);
@@ -1389,10 +1400,46 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
       lv += redl[i];
       lo += redo[i];
     }
-    if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
-    if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
-    if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
+    a.wstat[blockIdx.x] = make_int4(s, q, i2, 0);
     if (a.live_part) a.live_part[blockIdx.x] = make_uint2((unsigned)lv, (unsigned)lo);
+  }
+}
+
+// pass W's per-block counts into the step's counters (by pass V's first block: pass W's blocks
+// each adding theirs serialised on the three words)
+__device__ inline void bwd_fold_wstat(const BwdArgs& a) {
+  __shared__ long long rs[kFmNT / kWave];
+  __shared__ unsigned rq[kFmNT / kWave];
+  __shared__ unsigned long long ri[kFmNT / kWave];
+  long long s = 0;
+  unsigned q = 0;
+  unsigned long long i2 = 0;
+  for (int i = threadIdx.x; i < a.nwstat; i += kFmNT) {
+    const int4 w = a.wstat[i];
+    s += w.x;
+    q += (unsigned)w.y;
+    i2 += (unsigned long long)w.z;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off, kWave);
+    q += __shfl_xor(q, off, kWave);
+    i2 += __shfl_xor(i2, off, kWave);
+  }
+  if (lane_id() == 0) {
+    rs[threadIdx.x / kWave] = s;
+    rq[threadIdx.x / kWave] = q;
+    ri[threadIdx.x / kWave] = i2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kFmNT / kWave; ++i) {
+      s += rs[i];
+      q += rq[i];
+      i2 += ri[i];
+    }
+    if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)s);
+    if (q) atomicAdd(&a.dsw->n_init, q);
+    if (i2) atomicAdd(&a.dsw->n_keys, i2);
   }
 }
 
@@ -1402,6 +1449,7 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
   constexpr int UNR = CPL <= 4 ? 8 : 2;
   const int g = threadIdx.x / G;
   const int l = threadIdx.x % G;
+  if (blockIdx.x == 0) bwd_fold_wstat(a);
   const int64_t n = (int64_t)*a.vcount;
   const int d = a.d;
   const int64_t xs = a.xs > d ? a.xs : d;
@@ -1799,16 +1847,22 @@ int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long 
   const size_t lds_bytes = lds >= 0 ? (size_t)lds : kBwdLdsCap;
   DFX_HIP(hipMemsetAsync(a.vcount, 0, sizeof(uint32_t), st));
   const int64_t gw = std::min<int64_t>((nseg_bound + kBwdWNT - 1) / kBwdWNT, kBwdPassBlocks);
-  hipLaunchKernelGGL(k_fm_bwd_w, dim3((unsigned)gw), dim3(kBwdWNT), 0, st, a);
+  if (!a.wstat || gw > a.nwstat) {
+    set_error("two-pass backward: block counts reserved for fewer blocks than launched");
+    return DFX_ERR_ARG;
+  }
+  BwdArgs b = a;
+  b.nwstat = (int32_t)gw;
+  hipLaunchKernelGGL(k_fm_bwd_w, dim3((unsigned)gw), dim3(kBwdWNT), 0, st, b);
   const int64_t epb = kFmNT / G;
   // pass V: enough blocks that a group takes about one listed key (blocks past the list exit
   // at once) — the list's keys differ widely in walk length, and a resident grid's stride
   // loop stacked several long walks on one group
   const int64_t gv = std::min<int64_t>((nseg_bound + epb - 1) / epb, kBwdPassVBlocks);
   if (G == 32)
-    hipLaunchKernelGGL((k_fm_bwd_v<32, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, a);
+    hipLaunchKernelGGL((k_fm_bwd_v<32, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, b);
   else
-    hipLaunchKernelGGL((k_fm_bwd_v<64, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, a);
+    hipLaunchKernelGGL((k_fm_bwd_v<64, 4>), dim3((unsigned)gv), dim3(kFmNT), lds_bytes, st, b);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -1817,9 +1871,12 @@ int bwd_two_pass_reserve(Context* c, Workspace& ws, int64_t nseg_bound, BwdArgs*
   g->vlist = nullptr;
   g->vcount = nullptr;
   if (c->bwd_two_pass == 0 || !bwd_two_pass(c->P.V_dim) || nseg_bound <= 0) return DFX_OK;
-  DFX_TRY(ws.vlist.ensure((size_t)(nseg_bound + 1) * sizeof(uint4)));
+  const int64_t nw = bwd_fused_blocks(c->P.V_dim, nseg_bound, true, 0);
+  DFX_TRY(ws.vlist.ensure((size_t)(nseg_bound + 1 + nw) * sizeof(uint4)));
   g->vlist = ws.vlist.as<uint4>();
   g->vcount = reinterpret_cast<uint32_t*>(g->vlist + nseg_bound);
+  g->wstat = reinterpret_cast<int4*>(g->vlist + nseg_bound + 1);
+  g->nwstat = (int32_t)nw;
   return DFX_OK;
 }
 

@@ -143,6 +143,10 @@ struct BwdArgs {
   // per listed key does the V sums and AdaGrad
   uint4* vlist;
   uint32_t* vcount;
+  // the pass with one lane per key leaves its blocks' {new_w, n_init, n_keys} counts here and
+  // the V pass's first block adds them to dsw (one atomic per counter instead of one per block)
+  int4* wstat;
+  int32_t nwstat;
 };
 
 // occurrence i's row, and its value into *x: read directly, or (occ_rx: the bucket Localizer's
