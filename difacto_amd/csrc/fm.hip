@@ -450,7 +450,7 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
       int vm[MA];
 #pragma unroll
       for (int m = 0; m < MA; ++m) {
-        uint64_t h = hs[m];
+        uint64_t h = ek[m] != key[m] ? tbl_hash(key[m], a.T) : 0ull;  // (hs[m] not kept live)
         for (uint64_t probe = 0; ek[m] != key[m] && ek[m] != kEmptyKey && probe < a.T.mask;
              ++probe) {  // the (rare) longer probe chains
           h = (h + 1) & a.T.mask;
@@ -530,8 +530,12 @@ __device__ __forceinline__ void fwd_probe_body(const FwdArgs& a) {
   }
 }
 
+// two float4 per lane at V_dim 128 (G = 16, CPL = 8): 4 blocks per CU asked for, 128 VGPRs at
+// 4 waves / SIMD instead of 143 at 3 (a few spilled).  Same box: C5 forward 0.336 -> 0.268 ms,
+// 116.0 -> 118.6 M ex/s; at V_dim 64 (G = 8) the bound cut the forward 0.41 -> 0.37 ms but the
+// backward, beside more of the Localizer lane, rose 1.06 -> 1.11 (C4 shard 65.6 -> 64.2): not there
 template <int G, int CPL>
-__global__ __launch_bounds__(kFmNT) void k_fm_fwd_probe(FwdArgs a) {
+__global__ __launch_bounds__(kFmNT, (CPL == 8 && G >= 16) ? 4 : 1) void k_fm_fwd_probe(FwdArgs a) {
   fwd_probe_body<G, CPL>(a);
 }
 
