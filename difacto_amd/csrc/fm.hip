@@ -1355,7 +1355,10 @@ __global__ __launch_bounds__(kBwdWNT) void k_fm_bwd_w(BwdArgs a) {
       ninit += need ? 1 : 0;
       if (vq >= 0) {
         listed = true;
-        item = make_uint4((uint32_t)u, (uint32_t)vq, __float_as_uint(xxp), 0u);
+        // {first occurrence, or first chunk partial of a chunked key; V row; XXp; length}: pass
+        // V starts on the key's walk without reading segstart / choff again
+        const uint32_t first = (a.choff && len > (uint32_t)kChunkOcc) ? a.choff[u] : s0;
+        item = make_uint4(first, (uint32_t)vq, __float_as_uint(xxp), len);
         nlive += 1u;
         nlocc += len;
       }
@@ -1460,17 +1463,16 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd_v(BwdArgs a) {
   const bool valued = a.occ_x != nullptr;
   for (int64_t j = (int64_t)blockIdx.x * EPB + g; j < n; j += (int64_t)gridDim.x * EPB) {
     const uint4 it = a.vlist[j];
-    const uint32_t u = it.x;
     const int vq = (int)it.y;
     const float xxp = __uint_as_float(it.z);
-    const uint32_t s0 = a.segstart[u], s1 = a.segstart[u + 1];
-    const uint32_t len = s1 - s0;
+    const uint32_t len = it.w;
+    const uint32_t s0 = it.x, s1 = s0 + len;  // (it.x is the first chunk of a chunked key)
     float vcur[CPL], ccur[CPL], acc[CPL];
     load_coords<CPL, true>(row_V(a.T, vq), l, d, vcur);
     load_coords<CPL, true>(row_C(a.T, vq), l, d, ccur);
     // grad_u = (g0 - V*XXp) + sum (XV_ p) x, g0 = 0 (fm_loss.h:185-202, spmm.h:127-159)
     if (a.choff && len > (uint32_t)kChunkOcc) {
-      const uint32_t c0 = a.choff[u];
+      const uint32_t c0 = it.x;
       const uint32_t nc = hot_chunks_read((len + kChunkOcc - 1) / kChunkOcc);
       double accp[CPL];
 #pragma unroll
