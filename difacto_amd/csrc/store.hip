@@ -125,7 +125,9 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 // decoupled look-back over the lower tiles' tagged words (lookback.h), then draws its keys' V
 // exactly as k_initv.
 // The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
-constexpr int kIvItems = 16, kIvTile = kStNT * kIvItems;
+// 8192-key tiles (a thread's 32 flags as one bit mask), the requested keys listed kIvList at a
+// time: 4096-key tiles took 850 tickets at C3, ~9 us of serialised atomics.
+constexpr int kIvItems = 32, kIvTile = kStNT * kIvItems, kIvList = 4096;
 
 __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, uint32_t* total,
                                                          const uint32_t* slot, Table T,
@@ -142,40 +144,50 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   // tile by ticket, in the order blocks start: a block only waits on running ones.  Block index
   // order is not start order across XCDs, and the AUC lane's look-back sort can run beside this
   // kernel, so tile = block index could wait on a block that cannot be placed.  The
-  // block that draws the last ticket zeroes the counter for the next launch (every block draws
-  // one; k_step_finalize zeroes it too).
+  // block that draws the last ticket zeroes the counter for the next launch (k_step_finalize
+  // zeroes it too).  Only as many blocks as the batch has tiles draw one: the grid is sized for
+  // the nnz bound, and each ticket is a returning atomic on one word, ~11 ns apiece serialised
+  // (DESIGN.md (d)); the blocks past the count leave at once, and the tickets still go to running
+  // blocks in start order.
+  const int64_t n = (int64_t)nds->u_count;
+  const uint32_t need = (uint32_t)((n + kIvTile - 1) / kIvTile);
+  if (blockIdx.x >= need) return;
   __shared__ uint32_t s_tile;
   if (threadIdx.x == 0) {
     s_tile = atomicAdd(&ds->iv_ticket, 1u);
-    if (s_tile == gridDim.x - 1)
+    if (s_tile == need - 1)
       __hip_atomic_store(&ds->iv_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   const int64_t tile = s_tile;
-  const int64_t n = (int64_t)nds->u_count;
   const int64_t base = tile * kIvTile;
-  if (base >= n) return;  // no later tile waits on this one
   const uint32_t tag = ds->iv_epoch & 0x3FFFFFFFu;
-  // this thread's kIvItems consecutive flags
+  // this thread's kIvItems consecutive flags (0 / 1) as bits
   const int64_t i0 = base + (int64_t)threadIdx.x * kIvItems;
-  uint32_t f[kIvItems], cnt = 0;
+  uint32_t mask = 0;
+  if (i0 + kIvItems <= n && ((uintptr_t)flags & 15u) == 0) {
+    const uint4* f4 = reinterpret_cast<const uint4*>(flags + i0);
 #pragma unroll
-  for (int k = 0; k < kIvItems; ++k) {
-    f[k] = i0 + k < n ? flags[i0 + k] : 0u;
-    cnt += f[k];
+    for (int q = 0; q < kIvItems / 4; ++q) {
+      const uint4 v = f4[q];
+      mask |= ((v.x ? 1u : 0u) | (v.y ? 2u : 0u) | (v.z ? 4u : 0u) | (v.w ? 8u : 0u)) << (4 * q);
+    }
+  } else {
+#pragma unroll 4
+    for (int k = 0; k < kIvItems; ++k)
+      if (i0 + k < n && flags[i0 + k]) mask |= 1u << k;
   }
+  const uint32_t cnt = (uint32_t)__popc(mask);
   uint32_t tot;
-  uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
+  const uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
   const uint32_t pre = block_lookback<kStNT>(status, tile, tag, tot, &ds->err, s_lb);
   if (threadIdx.x == 0 && base + kIvTile >= n) *total = pre + tot;  // the last tile
   if (tot == 0) return;  // block-uniform
   const int d = T.d;
-  uint32_t e = pre + ex;
   if (d > kIvMaxD) {  // (wide V: each thread draws its keys' rows in turn)
-#pragma unroll 1
-    for (int k = 0; k < kIvItems; ++k) {
-      if (!f[k]) continue;
-      const int64_t u = i0 + k;
+    uint32_t e = pre + ex;
+    for (uint32_t m = mask; m; m &= m - 1) {
+      const int64_t u = i0 + (__ffs(m) - 1);
       uint32_t s = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
       const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
       ++e;
@@ -193,35 +205,39 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
     }
     return;
   }
-  // the block's requested keys, each with its V row and the LCG state at its first draw
-  // (3·d·rank steps past the seed, sgd_updater.cc:118-121), then every (key, coordinate) drawn
-  // by its own thread: coordinate j's state is 3·j steps on (A_j·state + C_j), the same rand_r
-  // values as one thread walking the row — a row's d draws were one lane's d · 3 dependent LCG
-  // steps (C5: ~0.1 ms of the step with ~1.5 k requests per 4096-key tile)
-  __shared__ uint32_t s_st[kIvTile], s_vr[kIvTile];
+  // the block's requested keys, kIvList at a time, each with its V row and the LCG state at its
+  // first draw (3·d·rank steps past the seed, sgd_updater.cc:118-121), then every (key,
+  // coordinate) drawn by its own thread: coordinate j's state is 3·j steps on (A_j·state + C_j),
+  // the same rand_r values as one thread walking the row — a row's d draws were one lane's d · 3
+  // dependent LCG steps (C5: ~0.1 ms of the step with ~1.5 k requests per 4096-key tile)
+  __shared__ uint32_t s_st[kIvList], s_vr[kIvList];
   __shared__ uint32_t s_A[kIvMaxD], s_C[kIvMaxD];
-  uint32_t idx = ex;
-#pragma unroll 1
-  for (int k = 0; k < kIvItems; ++k) {
-    if (!f[k]) continue;
-    const int64_t u = i0 + k;
-    const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
-    s_st[idx] = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
-    if (vr >= T.vcap) {
-      atomicOr(&ds->err, kErrPoolFull);
-      s_vr[idx] = 0xFFFFFFFFu;
-    } else {
-      s_vr[idx] = (uint32_t)vr;
-      ent_at(T, slot[u])->vrow = (int32_t)vr;
-    }
-    ++e;
-    ++idx;
-  }
   for (int j = threadIdx.x; j < d; j += kStNT) lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
-  __syncthreads();
-  initv_draw_list<kStNT>(tot, s_st, s_vr, d, scale, s_A, s_C,
-                         [&](uint32_t r) { return row_V(T, r); },
-                         [&](uint32_t r) { return row_C(T, r); });
+  for (uint32_t q0 = 0; q0 < tot; q0 += kIvList) {
+    if (ex < q0 + kIvList && ex + cnt > q0) {
+      uint32_t idx = ex;
+      for (uint32_t m = mask; m; m &= m - 1, ++idx) {
+        if (idx < q0) continue;
+        if (idx >= q0 + kIvList) break;
+        const int64_t u = i0 + (__ffs(m) - 1);
+        const uint32_t e = pre + idx;
+        const int64_t vr = initv_row(T, ds->n_vrows, e, slot[u]);
+        s_st[idx - q0] = lcg_advance(ds->seed, 3ull * (uint64_t)d * e);
+        if (vr >= T.vcap) {
+          atomicOr(&ds->err, kErrPoolFull);
+          s_vr[idx - q0] = 0xFFFFFFFFu;
+        } else {
+          s_vr[idx - q0] = (uint32_t)vr;
+          ent_at(T, slot[u])->vrow = (int32_t)vr;
+        }
+      }
+    }
+    __syncthreads();
+    initv_draw_list<kStNT>(tot - q0 < (uint32_t)kIvList ? tot - q0 : (uint32_t)kIvList, s_st, s_vr,
+                           d, scale, s_A, s_C, [&](uint32_t r) { return row_V(T, r); },
+                           [&](uint32_t r) { return row_C(T, r); });
+    __syncthreads();
+  }
 }
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
