@@ -432,11 +432,16 @@ def main():
     # untimed epoch 0: touch the key space with count pushes (all keys end up with V)
     n_warm_epoch = max(1, math.ceil(4.6 * keyspace / (B * k)))
     live = []
-    for i in range(n_warm_epoch):
-        live.append(make(1_000_000 * (rank + 1) + i))
+    warm = [make(1_000_000 * (rank + 1) + i) for i in range(n_warm_epoch)]
+    torch.cuda.synchronize()
+    tw = time.perf_counter()  # (the cold model's epoch: every key new, reported, not timed)
+    for bt in warm:
+        live.append(bt)
         step(live[-1], True)
     torch.cuda.synchronize()
+    t_warm = time.perf_counter() - tw
     live.clear()
+    warm.clear()
     H.progress(ctx)
     for i in range(args.warmup):
         live.append(make(2_000_000 * (rank + 1) + i))
@@ -543,6 +548,7 @@ def main():
         "roofline_forward": forward_roofline(ab["forward"], per_launch_ms["forward"],
                                              args.config),
         "phases_ms_per_step": {p: round(v, 4) for p, v in per_launch_ms.items()},
+        "cold_epoch_ms_per_step": round(t_warm / n_warm_epoch * 1e3, 4),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
         # the host's own work per step: the calls' time less their waits on the capacity guard
         # (which lets the host run a few steps ahead of the device, then blocks it)

@@ -1206,9 +1206,18 @@ __global__ __launch_bounds__(kFmNT) void k_fm_bwd(BwdArgs a) {
         lv += redl[i];
         lo += redo[i];
       }
-      if (s) atomicAdd((unsigned long long*)&a.dsw->new_w, (unsigned long long)(long long)s);
-      if (q) atomicAdd(&a.dsw->n_init, (unsigned int)q);
-      if (i2) atomicAdd(&a.dsw->n_keys, (unsigned long long)i2);
+      // one-word atomics serialise (~88 per us) and a cold model has a new w in
+      // nearly every block: the counts go to a stripe of their own line; n_init is a gate only
+      unsigned long long* nw = (unsigned long long*)&a.dsw->new_w;
+      unsigned long long* nk = &a.dsw->n_keys;
+      if (a.stripes) {
+        nw = a.stripes + (blockIdx.x % kBwStripes) * 16;
+        nk = nw + 1;
+      }
+      if (s) atomicAdd(nw, (unsigned long long)(long long)s);
+      if (q && __hip_atomic_load(&a.dsw->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicOr(&a.dsw->n_init, 1u);
+      if (i2) atomicAdd(nk, (unsigned long long)i2);
       if (a.live_part) a.live_part[blockIdx.x] = make_uint2((unsigned)lv, (unsigned)lo);
     }
   }

@@ -147,6 +147,8 @@ struct BwdArgs {
   // the V pass's first block adds them to dsw (one atomic per counter instead of one per block)
   int4* wstat;
   int32_t nwstat;
+  // the fused step's striped counters (DevState::bw_stripe; NULL: add to dsw directly)
+  unsigned long long* stripes;
 };
 
 // occurrence i's row, and its value into *x: read directly, or (occ_rx: the bucket Localizer's

@@ -45,6 +45,10 @@ struct DevBuf {
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// stripes of the fused backward's counters (one 128-byte line each): its ~10^5 blocks adding to
+// one word serialised at ~88 per us; k_step_finalize adds them in
+constexpr int kBwStripes = 32;
+
 // Device counters and progress, one small allocation.
 struct DevState {
   unsigned long long n_keys;   // occupied table slots
@@ -81,6 +85,9 @@ struct DevState {
   unsigned int lb_sp_wbits, lb_sp_use, lb_hot;
   unsigned int lb_nhot, lb_hm_n, lb_hm_s;  // the hot list's length; the map's keys, coarse shift
   unsigned long long lb_hm_base;           // ... and coarse base
+  // the fused backward's {new_w, n_keys} increments by block (blockIdx % kBwStripes), summed
+  // into new_w / n_keys and zeroed by k_step_finalize
+  alignas(128) unsigned long long bw_stripe[kBwStripes][16];
 };
 
 constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)

@@ -1032,7 +1032,10 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
     a.bfk[b] = fullkey(fast ? sk[0] : gk[0]);
     a.blk[b] = fullkey(fast ? sk[n - 1] : gk[n - 1]);
   }
-  if (__ballot(hot) && l == 0) atomicOr(&ds->lb_hot, 1u);
+  // (each flag raised once or so: one-word atomics serialise)
+  if (__ballot(hot) && l == 0 &&
+      __hip_atomic_load(&ds->lb_hot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    atomicOr(&ds->lb_hot, 1u);
   if (__ballot(longseg) && l == 0 &&
       __hip_atomic_load(&ds->n_init, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     atomicOr(&ds->n_init, 1u);

@@ -196,6 +196,21 @@ __global__ __launch_bounds__(kFinNT) void k_step_finalize(DevState* ds, const De
                                                           const double* loss_part, int64_t nparts,
                                                           unsigned long long* cap_host) {
   __shared__ double red[kFinNT / kWave];
+  // the fused backward's striped {new_w, n_keys}: summed by wave 0, zeroed for the next step
+  unsigned long long snw = 0, snk = 0;
+  if (threadIdx.x < kBwStripes) {
+    unsigned long long* st = ds->bw_stripe[threadIdx.x];
+    snw = st[0];
+    snk = st[1];
+    st[0] = 0ull;
+    st[1] = 0ull;
+  }
+  if (threadIdx.x < kWave) {
+    for (int off = 32; off > 0; off >>= 1) {
+      snw += __shfl_xor(snw, off, kWave);
+      snk += __shfl_xor(snk, off, kWave);
+    }
+  }
   double a = 0;
   for (int64_t i = threadIdx.x; i < nparts; i += kFinNT) a += loss_part[i];
   for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, kWave);
@@ -219,6 +234,9 @@ __global__ __launch_bounds__(kFinNT) void k_step_finalize(DevState* ds, const De
     const unsigned long long nv = ds->n_vrows + n;
     ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
   }
+  // (atomics: the Localizer lane's probe for the next batch may be inserting beside this)
+  if (snw) atomicAdd((unsigned long long*)&ds->new_w, snw);
+  if (snk) atomicAdd(&ds->n_keys, snk);
   if (cap_host) {
     cap_host[0] = ds->n_keys;
     cap_host[1] = ds->n_vrows;
@@ -369,7 +387,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
     g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from; g.nt = c->nt_mask;
-    g.flags = flags; g.dsw = c->ds;
+    g.flags = flags; g.dsw = c->ds; g.stripes = &c->ds->bw_stripe[0][0];
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();
     // (diagnostic, dfx_prof_enable_marks bit 9) the live-V key / occurrence counts

@@ -15,7 +15,7 @@ for i in $(seq 1 ${ROUNDS:-2}); do
     python3 - "$log" "$lib" <<'PY'
 import json, sys
 j = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-print(sys.argv[2], round(j["value"] / 1e6, 2), "M", j.get("phases_ms_per_step"))
+print(sys.argv[2], round(j["value"] / 1e6, 2), "M", j.get("phases_ms_per_step"), "cold", j.get("cold_epoch_ms_per_step"))
 PY
   done
 done
