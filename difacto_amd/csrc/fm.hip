@@ -589,21 +589,27 @@ __global__ __launch_bounds__(kFmNT, MINB) void k_fm_fwd_walk(FwdArgs a) {
       }
       const int cb = (int)(j0 - (c_end - kWkIds));  // this trip's first id in the chunk
       const int nin = (int)((o1 - j0) < (uint64_t)kWkNB ? (o1 - j0) : (uint64_t)kWkNB);
-      uint64_t key[kWkNB];
+      // the id -> key transform, run twice (for the loads, then for the check) rather than
+      // holding 8 keys (16 VGPRs) across the loads: the kernel then fits 4 waves / SIMD unspilled
+      auto key_of = [&](int i) {
+        const uint64_t id = s_id[g][i];
+        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
+        return a.keys_ready ? id : reverse_bytes(mm);
+      };
       float2 eh[kWkNB];  // even lanes {w, vrow}, odd lanes the key
       float4 v[kWkNB];
 #pragma unroll
       for (int t = 0; t < kWkNB; ++t) {
-        const uint64_t id = s_id[g][cb + (t < nin ? t : nin - 1)];
-        const uint64_t mm = a.max_index == ~0ull ? (id == ~0ull ? 0ull : id) : id % a.max_index;
-        key[t] = a.keys_ready ? id : reverse_bytes(mm);
-        const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key[t], a.T)));
+        const uint64_t key = key_of(cb + (t < nin ? t : nin - 1));
+        const float* sl = reinterpret_cast<const float*>(ent_at(a.T, tbl_hash(key, a.T)));
         eh[t] = ld2(sl + ((l & 1) ? 6 : 0), ntf);
         v[t] = ld4(sl + 8 + 4 * l, ntf);
       }
+      uint64_t key[kWkNB];
 #pragma unroll
       for (int t = 0; t < kWkNB; ++t) {
         if (t >= nin) break;  // group-uniform
+        key[t] = key_of(cb + t);
         const float k0 = __shfl(eh[t].x, gbase + 1, kWave), k1 = __shfl(eh[t].y, gbase + 1, kWave);
         uint64_t ek = ((uint64_t)__float_as_uint(k1) << 32) | (uint64_t)__float_as_uint(k0);
         float w = __shfl(eh[t].x, gbase, kWave);
