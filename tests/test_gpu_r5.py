@@ -134,3 +134,29 @@ def test_bucket_splitter_map_equals_lsd(H, kind, rows):
     assert st[0]["n_keys"] == st[1]["n_keys"] == up.size()
     for c in cs:
         c.close()
+
+
+@pytest.mark.parametrize("d", [16, 128])
+def test_cold_model_counters_vs_oracle(H, d):
+    """A cold model: nearly every backward block has new w's and InitV requests.  The fused
+    backward adds its {new_w, n_keys} counts to 32 striped lines (summed by k_step_finalize) and
+    raises the InitV gate once; at V_dim 128 pass W leaves its blocks' counts for pass V to add
+    (one-word atomics serialise).  The step's statistics must still equal
+    SGDUpdater's: n_keys, new_w (sgd_updater.cc: w leaving / returning to zero under l1) and the
+    rand_r seed after every InitV draw — over enough keys that every stripe is used."""
+    cfg = dict(V_dim=d, V_threshold=0, l1=0.5, lr=.1, V_lr=.02)
+    c = H.Context(0, max_keys=1 << 20, **cfg)
+    up = O.Updater(**cfg)
+    for step in range(3):
+        blk = D.synthetic(6000, 39, 1 << 20, binary=True, seed=400 + step)
+        loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
+                                         push_cnt=(step < 2), want_pred=True)
+        pred = torch.zeros(blk.size, dtype=torch.float32, device=c.device)
+        H.train_step(c, H.DeviceRowBlock(c, blk), H.kTraining, push_cnt=(step < 2), pred=pred)
+        H.progress(c)
+        s = H.Store(c).stats()
+        assert s["n_keys"] == up.size(), step
+        assert s["new_w"] == int(up.new_w), (step, s["new_w"], up.new_w)
+        assert s["seed"] == up.seed, step
+        assert np.allclose(pred.cpu().numpy(), opred, rtol=1e-4, atol=1e-6), step
+    c.close()
