@@ -1,0 +1,9 @@
+#!/bin/bash
+# the probe forward at 4 waves / SIMD for two float4 per lane: its tests, then C5 / C4 shard A/B
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && mkdir -p gpurun_out/r5
+export TMPDIR=/tmp
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  -k "c5 or probe or fwd or c4 or parity" > gpurun_out/r5/t_r5z.log 2>&1 || { tail -40 gpurun_out/r5/t_r5z.log; exit 1; }
+tail -1 gpurun_out/r5/t_r5z.log
+LIBS="build/ab/libdifacto_amd.so tree" BENCH_ARGS="--config c5 --steps 20 --warmup 5" tools/ab_libs.sh || exit 1
+LIBS="build/ab/libdifacto_amd.so tree" BENCH_ARGS="--config c4shard --steps 20 --warmup 5" tools/ab_libs.sh

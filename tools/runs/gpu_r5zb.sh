@@ -1,0 +1,9 @@
+#!/bin/bash
+# InitV in 8192-key tiles (fewer tickets): the whole GPU suite, then C3 / C5 A/B against build/ab
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && mkdir -p gpurun_out/r5
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/r5/t_r5zb.log 2>&1 || { tail -40 gpurun_out/r5/t_r5zb.log; exit 1; }
+tail -1 gpurun_out/r5/t_r5zb.log
+LIBS="build/ab/libdifacto_amd.so tree" BENCH_ARGS="--steps 20 --warmup 5" tools/ab_libs.sh || exit 1
+LIBS="build/ab/libdifacto_amd.so tree" BENCH_ARGS="--config c5 --steps 20 --warmup 5" tools/ab_libs.sh
