@@ -1791,8 +1791,9 @@ int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, boo
 constexpr size_t kBwdLdsCap = 32768;
 // The one-kernel fused backward (V_dim < 128) since round 4's lighter lanes (bucket Localizer,
 // radix AUC): 16 KiB, i.e. up to 10 blocks by LDS (8 by wave slots).  Same-box A/B at C3:
-// 32 KiB 123.4, 20 KiB 126.9, 16 KiB 127.7 M ex/s (backward 0.53 -> 0.42 ms).
-constexpr size_t kBwdLdsCapFused = 16384;
+// 32 KiB 123.4, 20 KiB 126.9, 16 KiB 127.7 M ex/s (backward 0.53 -> 0.42 ms).  Round 5's close:
+// 12 KiB, C3 +0.25 to +0.5 % over eight same-box rounds, C2 and the C4 shard a tie.
+constexpr size_t kBwdLdsCapFused = 12288;
 
 // Lane layout of a fused backward.  kwarg bwd_cpl = 8 at V_dim >= 64 (float4-aligned rows):
 // two float4 per lane, half the lanes per key — a key's walk (entry, rows, update) is latency
