@@ -330,6 +330,35 @@ def cpu_baseline(args):
                       % (nb * args.cpu_batch, nb, args.cpu_batch)}
 
 
+def step_window(torch, dev, world, batches, run):
+    """The timed window's shape (untimed replay of the same K steps, same barrier + sync
+    bracket): one event on the main stream after each step's enqueue, so the K intervals are
+    the main stream's time per step — the first holds the Localizer of its batch that no
+    earlier step overlapped (the pipeline's fill); the wall time past the last event is the
+    drain of the side lanes (the last AUC).  Only the first/last/median are reported."""
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(batches) + 1)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i, bt in enumerate(batches):
+        run(bt)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3
+    ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(len(batches))]
+    mid = sorted(ms[1:-1] or ms)
+    med = mid[len(mid) // 2]
+    span = evs[0].elapsed_time(evs[-1])
+    return {"steps": len(ms), "first_ms": round(ms[0], 4), "second_ms": round(ms[1], 4)
+            if len(ms) > 1 else None, "median_ms": round(med, 4), "last_ms": round(ms[-1], 4),
+            "main_span_ms": round(span, 4), "wall_ms": round(wall, 4),
+            "fill_ms": round(sum(ms[:2]) - 2 * med, 4) if len(ms) > 1 else None,
+            "launch_and_drain_ms": round(wall - span, 4),
+            "ms": [round(x, 3) for x in ms]}
+
+
 def spawn_ranks(args):
     """`--gpus N` without a launcher: run this script as N ranks, one process per GPU, with the
     environment torch.distributed.run gives them (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*), and
@@ -479,6 +508,7 @@ def main():
     phases, nrec, mean_u = H.prof_read(ctx)
     bwd_ms = phases["backward_update"]
     prog = H.progress(ctx)
+    window = step_window(torch, dev, world, batches, lambda bt: step(bt, False))
     # diagnostic pass (untimed): every phase and the lanes, over the same batches again
     H.prof_enable(ctx, len(batches))
     for bt in batches:
@@ -556,6 +586,7 @@ def main():
         "host_waits": host_wait["waits"],
         "host_call_ms_idle_device": round(host_idle[len(host_idle) // 2] * 1e3, 4),
         "lanes_ms": {k_: round(v, 4) for k_, v in lanes.items()},
+        "step_window": window,
         "mean_unique_keys": round(mean_u, 1),
         "mean_live_v_keys": counts["U_V"] and round(counts["U_V"], 1),
         "mean_live_v_occurrences": counts["occ_V"] and round(counts["occ_V"], 1),

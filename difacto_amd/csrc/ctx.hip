@@ -81,7 +81,11 @@ struct Kw {
   // (locbucket.hip); 0: the onesweep radix sort's LSD passes (localize.hip, sort.hip)
   int loc_bucket = 1;
   // lb_diag=<bits>: MEASUREMENT ONLY (tools/locbench): parts of k_lb_wbucket skipped — 1 the LDS
-  // sort, 4 the outputs, 8 k_lb_scatter's row search; the Localizer's results are then wrong
+  // sort, 4 the outputs, 8 k_lb_scatter's row search; launches skipped on a workspace that holds
+  // an earlier batch of the same shape — 16 k_lb_scatter, 32 k_lb_wbucket, 64 k_lb_out; 128
+  // k_lb_scatter's items written by input position to a scratch buffer, 256 to the scratch buffer
+  // at tile-local positions (the tile's items grouped by bucket; binary batches); the
+  // Localizer's results are then wrong
   int lb_diag = 0;
   // auc_db=1: the fused step's AUC snapshot alternates between two buffers, so a forward waits
   // only for the AUC lane of two steps back (0: of the step before).  Same-box A/B: a tie at C3

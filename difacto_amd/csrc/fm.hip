@@ -1752,8 +1752,17 @@ __global__ __launch_bounds__(kHotNT) void k_chunk_hotsum(BwdArgs a) {
   }
 }
 
+// row_p reads p from the [XV*p | p] row only when the row holds it (xs > d): rows of d floats
+// need the per-row array (a null p there would read the next row's first XV*p)
+static int check_row_p(const BwdArgs& a) {
+  DFX_CHECK_ARG(!(a.d > 0 && a.xs <= a.d && !a.p),
+                "backward: XV*p rows without p need the per-row p array");
+  return DFX_OK;
+}
+
 int launch_bwd_chunks(const BwdArgs& a, int64_t chunk_bound, hipStream_t st, bool aligned) {
   if (chunk_bound <= 0 || !a.choff) return DFX_OK;
+  DFX_TRY(check_row_p(a));
   int G, CPL;
   bool vec;
   // aligned (the fused steps' 16-byte XV*p rows, V_dim a multiple of 4): float4 per lane, a
@@ -1855,6 +1864,7 @@ bool bwd_two_pass(int d) {
 }
 
 int launch_bwd_fused(const BwdArgs& a, int64_t nseg_bound, hipStream_t st, long lds) {
+  DFX_TRY(check_row_p(a));
   if (!a.vlist) return launch_bwd<true>(a, nseg_bound, st, true, lds);
   if (nseg_bound <= 0) return DFX_OK;
   int G, CPL;

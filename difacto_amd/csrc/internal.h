@@ -84,6 +84,7 @@ struct DevState {
   // map is valid (the previous batch had hot keys); lb_hot: this batch's flag (k_lb_wbucket)
   unsigned int lb_sp_wbits, lb_sp_use, lb_hot;
   unsigned int lb_nhot, lb_hm_n, lb_hm_s;  // the hot list's length; the map's keys, coarse shift
+  unsigned int lb_map_steps;  // batches placed by the hot-key map (dfx_prof_counts out[3])
   unsigned long long lb_hm_base;           // ... and coarse base
   // the fused backward's {new_w, n_keys} increments by block (blockIdx % kBwStripes), summed
   // into new_w / n_keys and zeroed by k_step_finalize
@@ -242,6 +243,7 @@ struct Context {
   int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_hnt = 0;         // kwarg lb_hnt: the bucket Localizer's histogram / scatter block (0 auto)
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
+  int lb_skip = 0;        // lb_diag's launch-skip bits, armed once a workspace holds a batch
   int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists

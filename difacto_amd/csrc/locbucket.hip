@@ -386,7 +386,10 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   const bool qs = HOT && lb_hot_on(a);
   LbHot hm{};
   if (qs) hm = lb_stage_hot(a, offs + a.rt + 1, t, kLbHNT);
-  const int64_t tile = blockIdx.x;
+  // (lb_diag 512, measurement only) each XCD a contiguous range of tiles
+  const int64_t tile = ((a.diag & 512) && a.ntiles % 8 == 0)
+                           ? (int64_t)(blockIdx.x % 8) * (a.ntiles / 8) + blockIdx.x / 8
+                           : (int64_t)blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
   // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
@@ -403,12 +406,39 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t total;
   uint32_t ex = block_excl_scan<kLbHNT>(mine, lds, &total);
   const uint32_t* pre = a.tilecnt + (size_t)tile * m.nbk;
+  const bool mid4 = (a.diag & 512) && per == 4;  // (measurement only) 4 buckets per cursor
+  uint32_t msum = 0;
+  const uint32_t mex = ex;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < m.nbk) {
-      cur[d] = ex + pre[d];
+      if (!mid4) cur[d] = ex + pre[d];
+      msum += pre[d];
       if (blockIdx.x == 0) a.bstart[d] = ex;
       ex += a.totals[d];
+    }
+  }
+  if (mid4) {
+    __syncthreads();
+    cur[t] = mex + msum;
+  }
+  if (a.diag & 256) {  // (measurement only) tile-local positions: the tile's items by bucket
+    auto tcnt = [&](uint32_t d) {
+      const uint32_t nx = tile + 1 < a.ntiles ? a.tilecnt[(size_t)(tile + 1) * m.nbk + d]
+                                              : a.totals[d];
+      return nx - pre[d];
+    };
+    uint32_t lm = 0;
+    for (uint32_t i = 0; i < per; ++i)
+      if (t * per + i < m.nbk) lm += tcnt(t * per + i);
+    uint32_t lex = block_excl_scan<kLbHNT>(lm, lds, nullptr);
+    for (uint32_t i = 0; i < per; ++i) {
+      const uint32_t d = t * per + i;
+      if (d < m.nbk) {
+        const uint32_t cd = tcnt(d);
+        cur[d] = lex;
+        lex += cd;
+      }
     }
   }
   const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
@@ -476,9 +506,12 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
       const uint64_t k = lb_key(id[u], a.max_index, a.keys_ready);
       const uint32_t row = (uint32_t)(r0 + lo);
       const uint64_t q = S ? j : (uint64_t)row;
-      const uint32_t pos = atomicAdd(&cur[qs ? lb_hot_bucket(k, j, hm) : lb_bucket(k, m)], 1u);
-      stnt(a.kbuf + pos, p.packed ? ((((k - p.kmin) >> p.lo) << p.rb) | (q & qmask)) : k,
-           a.nt != 0);
+      const uint32_t bk = qs ? lb_hot_bucket(k, j, hm) : lb_bucket(k, m);
+      const uint32_t pos = atomicAdd(&cur[mid4 ? bk >> 2 : bk], 1u);
+      // (lb_diag 128, measurement only: the same items written contiguously, by input
+      // position, to a scratch buffer — the scatter's work without its scattered writes)
+      stnt((a.diag & 128) ? a.sscr + j : (a.diag & (256 | 512)) ? a.sscr + (a.diag & 256 ? j0 : 0) + pos : a.kbuf + pos,
+           p.packed ? ((((k - p.kmin) >> p.lo) << p.rb) | (q & qmask)) : k, a.nt != 0);
       if (!p.packed) a.qbuf[pos] = (uint32_t)q;
       if (S && a.rowof) a.rowof[j] = make_uint2(row, __float_as_uint(x[u]));  // input order
       else if (S) a.sbuf[pos] = (uint64_t)__float_as_uint(x[u]) | ((uint64_t)row << 32);
@@ -1123,7 +1156,10 @@ __global__ __launch_bounds__(kLbNT) void k_lb_out(LbArgs a) {
 constexpr int kLbHotGrid = 512;
 __global__ __launch_bounds__(kLbNT) void k_lb_hotlist(LbArgs a) {
   DevState* ds = a.ds;
-  if (ds->lb_hot == 0u) return;
+  // under the hot-key map a hot key's run is split over buckets in parts of <= target, which may
+  // be below hot_th, so no bucket raises lb_hot: a batch placed by the map lists its hot keys
+  // whatever the flag says (else the map would switch off every other batch)
+  if (ds->lb_hot == 0u && !lb_hot_on(a)) return;
   const int64_t U = ds->u_count;
   for (int64_t i = (int64_t)blockIdx.x * kLbNT + threadIdx.x; i < U;
        i += (int64_t)gridDim.x * kLbNT) {
@@ -1150,7 +1186,8 @@ __global__ __launch_bounds__(kLbHotMax) void k_lb_hotmap(LbArgs a) {
   DevState* ds = a.ds;
   const int t = threadIdx.x;
   const bool was = lb_hot_on(a);
-  const uint32_t nh = ds->lb_hot ? ds->lb_nhot : 0u;
+  const uint32_t nh = (ds->lb_hot || was) ? ds->lb_nhot : 0u;  // (k_lb_hotlist's condition)
+  if (t == 0 && was) ds->lb_map_steps += 1u;  // diagnostic: batches placed by the map
   const int wb = a.wbits_hot;
   const uint32_t nbk = 1u << wb, C = nbk / 2;
   if (nh == 0u || nh > (uint32_t)kLbHotMax || wb < 2 || 2 * nh >= nbk - C) {
@@ -1334,7 +1371,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.uniq = o.uniq; a.segstart = o.segstart; a.occ_row = o.occ_row;
   a.occ_x = valued ? o.occ_x : nullptr;
   a.hint = ws.lb_hint;
-  a.diag = c->lb_diag;
+  a.diag = (c->lb_diag & ~(16 | 32 | 64 | 128 | 256 | 512)) | c->lb_skip;
   {
     constexpr size_t kNb = (size_t)1 << kLbMaxBits;
     char* q = ws.lbsplit.as<char>();
@@ -1387,7 +1424,8 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   else                                                                                     \
     hipLaunchKernelGGL((k_lb_scatter<false, NT, false>), dim3((unsigned)ntiles), dim3(NT),  \
                        scatter_lds, L.stream, a);
-  if (hnt == 256) { DFX_LB_SCAT(256) }
+  if (c->lb_skip & 16) {}  // (measurement only)
+  else if (hnt == 256) { DFX_LB_SCAT(256) }
   else if (hnt == 512) { DFX_LB_SCAT(512) }
   else { DFX_LB_SCAT(1024) }
 #undef DFX_LB_SCAT
@@ -1401,7 +1439,8 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   else
     hipLaunchKernelGGL(k_lb_big<false>, dim3(kLbBigBlocks), bb, 0, L.stream, a, q_lds ? 1 : 0);
   const dim3 wb(kWave);  // one wave per bucket
-  if (carry) {
+  if (c->lb_skip & 32) {}  // (measurement only)
+  else if (carry) {
     if (q_lds) hipLaunchKernelGGL((k_lb_wbucket<true, true>), bg, wb, 0, L.stream, a);
     else hipLaunchKernelGGL((k_lb_wbucket<false, true>), bg, wb, 0, L.stream, a);
   } else {
@@ -1415,7 +1454,7 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     hipLaunchKernelGGL(k_lb_gather, dim3((unsigned)((nnz + kLbNT - 1) / kLbNT)), bb, 0, L.stream,
                        a);
   hipLaunchKernelGGL(k_lb_bscan, dim3(1), dim3(kLbScanNT), 0, L.stream, a);
-  hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
+  if (!(c->lb_skip & 64)) hipLaunchKernelGGL(k_lb_out, bg, bb, 0, L.stream, a);
   if (!valued && a.uniq && a.segstart) {  // the next batch's hot-key map
     hipLaunchKernelGGL(k_lb_hotlist, dim3(kLbHotGrid), bb, 0, L.stream, a);
     hipLaunchKernelGGL(k_lb_hotmap, dim3(1), dim3(kLbHotMax), 0, L.stream, a);

@@ -243,6 +243,34 @@ __global__ __launch_bounds__(kFinNT) void k_step_finalize(DevState* ds, const De
   }
 }
 
+// the fused backward's striped {new_w, n_keys} folded into the state (k_step_finalize's first
+// part) when a step ends on an error after its backward was enqueued: the counts then reach
+// dfx_store_stats and the capacity guard at once, not in a later step's finalize
+__global__ __launch_bounds__(kWave) void k_fold_stripes(DevState* ds) {
+  unsigned long long nw = 0, nk = 0;
+  if (threadIdx.x < kBwStripes) {
+    unsigned long long* st = ds->bw_stripe[threadIdx.x];
+    nw = st[0];
+    nk = st[1];
+    st[0] = 0ull;
+    st[1] = 0ull;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    nw += __shfl_xor(nw, off, kWave);
+    nk += __shfl_xor(nk, off, kWave);
+  }
+  if (threadIdx.x == 0) {
+    if (nw) atomicAdd((unsigned long long*)&ds->new_w, nw);
+    if (nk) atomicAdd(&ds->n_keys, nk);
+  }
+}
+
+static int fold_stripes_on_error(Context* c, int rc) {
+  hipLaunchKernelGGL(k_fold_stripes, dim3(1), dim3(kWave), 0, c->stream, c->ds);
+  (void)hipGetLastError();
+  return rc;
+}
+
 // One minibatch, pipelined over three streams:
 //   loc lane   Localizer (transform + find-or-insert, sort, segments) of this batch.  It needs
 //              only the batch and the key -> slot map, which the backward never changes
@@ -312,7 +340,9 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   uint32_t* nchunks = &bds->totals[1];
   if (!((c->diag & 2) && c->loc_done[k])) {  // (diag: measurement only)
     rowof = nullptr;
+    c->lb_skip = c->loc_done[k] ? (c->lb_diag & (16 | 32 | 64 | 128 | 256 | 512)) : 0;  // (measurement only)
     DFX_TRY(localize_run(c, LL, B, nnz, b->offset, b->index, max_index, o));
+    c->lb_skip = 0;
     c->loc_rowof[k] = rowof;
     // long segments (skewed keys) get reduced in chunks: plan them here, off the main stream
     DFX_TRY(chunk_plan(LL, nnz, segstart, choff, chunk_seg, nchunks));
@@ -321,16 +351,20 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   lane_mark(c, 1, c->loc_stream);
   DFX_HIP(hipEventRecord(c->ev_loc[k], c->loc_stream));
 
-  // ---- main: wait for this batch's Localizer (the exposed part of it is the "localize" phase)
-  prof_mark(c, 0);
-  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_loc[k], 0));
-  prof_mark(c, 1);
   // Get over the sorted unique keys (find-or-insert + pull); a count push goes in between
   const bool cnt_first = push_cnt && d > 0;
   // a training step whose forward finds keys itself needs no Get pass: absent keys read as
   // the empty entry and the backward inserts them (its find-or-insert is Get's)
   const bool bwd_inserts = c->fwd_probe && !cnt_first && job_type == DFX_JOB_TRAINING &&
                            B > 0 && nnz > 0;
+  // ---- main: wait for this batch's Localizer (the exposed part of it is the "localize" phase).
+  // (The probe forward needs only the batch, but a forward that waits for the batch alone and
+  // the backward for the Localizer measured worse: same box, driver command, 139.0 / 138.3 /
+  // 130.7 -> 133.6 / 125.5 / 126.3 M ex/s — the fill shrinks 0.26 -> 0.05 ms, but the lane then
+  // runs beside the backward instead of the forward and ends 0.04-0.16 ms before it is needed)
+  prof_mark(c, 0);
+  DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_loc[k], 0));
+  prof_mark(c, 1);
   const dim3 ug((unsigned)((nnz + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
   if (nnz > 0 && !bwd_inserts)
     hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, c->stream, uniq, bds, c->T,
@@ -402,13 +436,18 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);
-    DFX_TRY(run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false));
+    const int rc = run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false);
+    if (rc != DFX_OK) return fold_stripes_on_error(c, rc);
   } else {
     prof_mark(c, 6);
   }
   const bool initv = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 && d > 0;
   unsigned long long* cap_host = nullptr;
-  DFX_TRY(cap_record_slot(c, &cap_host));
+  {
+    const int rc = cap_record_slot(c, &cap_host);
+    if (rc != DFX_OK)
+      return job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 ? fold_stripes_on_error(c, rc) : rc;
+  }
   hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(kFinNT), 0, c->stream, c->ds, bds, B,
                      initv ? total : nullptr, d, c->T.vcap, a.loss_part, (int64_t)nblk, cap_host);
   DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
@@ -462,8 +501,9 @@ extern "C" int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask)
 // after dfx_prof_read: out[4] = mean ms of the Localizer lane per batch, of its start after
 // the context stream reached that batch (negative: it ran ahead), of its end after that point
 // (positive: the exposed wait), and of the AUC lane
-// out[3]: per dfx_train_step since the last call, the mean number of unique keys, of keys with
-// live V (their V is read and updated) and of those keys' occurrences; resets the counters
+// out[4]: per dfx_train_step since the last call, the mean number of unique keys, of keys with
+// live V (their V is read and updated) and of those keys' occurrences; then the number of
+// batches the bucket Localizer placed by its hot-key map; resets the counters
 extern "C" int dfx_prof_counts(dfx_ctx* ctx, double* out) {
   DFX_CHECK_ARG(ctx && out, "bad argument");
   Context* c = &ctx->c;
@@ -478,6 +518,16 @@ extern "C" int dfx_prof_counts(dfx_ctx* ctx, double* out) {
   out[2] = (double)lv[1] / n;
   DFX_HIP(hipMemsetAsync(&c->ds->sum_u, 0, sizeof(h), c->stream));
   DFX_HIP(hipMemsetAsync(&c->ds->live_keys, 0, sizeof(lv), c->stream));
+  // the Localizer lanes' hot-key map use (their own states; the lane is drained first)
+  if (c->loc_stream) DFX_HIP(hipStreamSynchronize(c->loc_stream));
+  out[3] = 0;
+  for (DevState* s : c->bds) {
+    if (!s) continue;
+    unsigned m = 0;
+    DFX_HIP(hipMemcpy(&m, &s->lb_map_steps, sizeof(unsigned), hipMemcpyDeviceToHost));
+    DFX_HIP(hipMemset(&s->lb_map_steps, 0, sizeof(unsigned)));
+    out[3] += (double)m;
+  }
   DFX_HIP(hipStreamSynchronize(c->stream));
   return DFX_OK;
 }

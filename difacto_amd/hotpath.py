@@ -286,12 +286,12 @@ def prof_read(ctx):
 
 def prof_counts(ctx):
     """per step since the last call (or prof_read): mean unique keys, keys with live V and
-    their occurrences; resets"""
-    out = (ctypes.c_double * 3)()
-    if not hasattr(_lib.lib(), "dfx_prof_counts"):  # an older library under A/B (DFX_LIB_PATH)
-        return {"U": 0.0, "U_V": None, "occ_V": None}
+    their occurrences; and the batches the bucket Localizer placed by its hot-key map; resets"""
+    out = (ctypes.c_double * 4)()
     check(_lib.lib().dfx_prof_counts(ctx.h, out))
-    return dict(zip(("U", "U_V", "occ_V"), list(out)))
+    r = dict(zip(("U", "U_V", "occ_V"), list(out)))
+    r["lb_map_steps"] = int(out[3])
+    return r
 
 
 def prof_host(ctx):

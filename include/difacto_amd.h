@@ -236,9 +236,10 @@ int dfx_prof_read(dfx_ctx* ctx, double* ms, int* n_steps, double* mean_u);
  * end relative to the context stream reaching that batch (start < 0: it ran ahead; end > 0:
  * the exposed wait), and of the AUC lane */
 int dfx_prof_lanes(dfx_ctx* ctx, double* out);
-/* out[3] = per dfx_train_step since the last call (or dfx_prof_read): the mean number of
+/* out[4] = per dfx_train_step since the last call (or dfx_prof_read): the mean number of
  * unique keys, of keys with live V and of their occurrences (the roofline's bytes; the live-V
- * counts are taken only in steps recorded with mark bit 9, dfx_prof_enable_marks); resets */
+ * counts are taken only in steps recorded with mark bit 9, dfx_prof_enable_marks); out[3] = the
+ * number of batches the bucket Localizer placed by its hot-key map (skewed keys); resets */
 int dfx_prof_counts(dfx_ctx* ctx, double* out);
 /* out[2] = host seconds dfx_train_step calls spent blocked (the capacity guard waiting for
  * earlier steps' counts) since the last call, and the number of such waits; resets */

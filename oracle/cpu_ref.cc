@@ -475,7 +475,9 @@ void cref_step(void* h, int nt, int64_t B, const uint64_t* offs, const uint64_t*
   Updater* up = static_cast<Updater*>(h);
   Block D;
   const bool cnt = push_cnt && up->P.V_dim > 0;
+  const double tc = Now();
   Compact(offs, ids, val, label, (size_t)B, nt, cnt, &D);
+  g_phase[0] += Now() - tc;
   if (cnt) up->PushCnt(D.uniq, D.cnt);
   Result r;
   Execute(up, D, nt, train != 0, &r, pred_out);

@@ -132,6 +132,12 @@ def test_bucket_splitter_map_equals_lsd(H, kind, rows):
                           vs[1][0].cpu().numpy().view(np.uint32))
     st = [H.Store(c).stats() for c in cs]
     assert st[0]["n_keys"] == st[1]["n_keys"] == up.size()
+    # the hot-key map actually placed batches (else the map's paths — lb_hot_bucket, the
+    # continued runs, k_lb_out's skipped heads — would go untested).  Batch t takes
+    # the map batch t - 2 built on the same lane workspace: batches 2, 3, 4 of five
+    maps = H.prof_counts(cs[1])["lb_map_steps"]
+    if kind == "one_hot" or (kind == "zipf" and rows >= 60000):
+        assert maps == 3, maps
     for c in cs:
         c.close()
 
