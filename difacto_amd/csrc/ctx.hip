@@ -49,11 +49,6 @@ struct Kw {
   int loss_fm = 1;
   int ordered = 1;
   // execution choices (context kwargs, not behaviour switches of the process environment)
-  // fwd_probe=1 (default): the forward finds its keys, lookups spread over the row's lanes;
-  // 2: the same with each lane walking all of its row's nnz (k_fm_fwd); 0: Localizer col +
-  // pulled {w, vrow} instead of probing
-  int fwd_probe = 1;
-  int xvp_row = 1;      // xvp_row=0: XV*p rows of d floats, p in its own array
   long bwd_lds = -1;    // bwd_lds=<bytes>: LDS reserved per backward block (-1: default cap)
   int autogrow = 1;     // autogrow=0: never grow the table / V pool on its own
   int dist_sum = 1;     // push_agg=sum|ranks (sharded store, dist.hip)
@@ -61,14 +56,10 @@ struct Kw {
   // auc_sort=radix (default): the AUC lane's onesweep radix passes; merge: tile sorts + merge
   // rounds (round 4's bucket AUC, a shorter lane but a slower step, is gone: DESIGN.md (d))
   int auc_sort = 1;
-  int sort_items = 16;  // sort_items=8|16|32: the Localizer sort's tile (256 x items)
-  int sort_lookback = 4;  // sort_lookback=4|16|32: predecessor words per look-back step
   // slot_layout=auto (default): fat slots (entry + V in one 64/128-byte slot, common.h Table)
   // when V_dim allows them (4 <= d <= 24, d % 4 == 0), else the split layout; split | fat force
   int slot_layout = -1;
   int fat_fwd = 1;  // fat_fwd=0: with fat slots, the split forward walk (A/B of the one-trip read)
-  int fat_bwd = 1;  // fat_bwd=0: the backward reads V / Vaux after the entry (A/B)
-  int initv_onepass = 1;
   // diag=noauc|noloc|noauc_noloc: MEASUREMENT ONLY (the headroom of the side lanes): no AUC
   // lane, or each Localizer parity run once and its output reused (results are then wrong
   // unless the batches repeat); never set by the product path
@@ -87,26 +78,14 @@ struct Kw {
   // at tile-local positions (the tile's items grouped by bucket; binary batches); the
   // Localizer's results are then wrong
   int lb_diag = 0;
-  // auc_db=1: the fused step's AUC snapshot alternates between two buffers, so a forward waits
-  // only for the AUC lane of two steps back (0: of the step before).  Same-box A/B: a tie at C3
-  // (133.5 / 133.5 M ex/s) and C2 (186.6 / 186.4), the lane overlapping more of the backward
-  // (0.44 -> 0.49 ms); at B = 10^4, where the one-block AUC (~94 us) outlasts the backward,
-  // 58.6 / 61.6 -> 68.0 / 68.8.  2 (the default): double-buffered for B <= kAucBlockMax only
-  int auc_db = 2;
   // lb_gather: valued batches sort (key | position) items alone, the row and the value gathered
   // by position at the outputs (1; A/B at C2: 126 -> 161 M ex/s) or, in the fused step, read by
   // position in the backward itself (2, the default: no gather launch on the Localizer lane;
   // C2 187.5-194.5 -> 195.1-195.5 M ex/s, four same-box rounds); 0: {value, row} carried
   // beside each item
   int lb_gather = 2;
-  // lb_tiles=<n>: the bucket Localizer's row tiles at most (histogram / scatter blocks of 1024
-  // threads).  Same-box A/B at C3: 256 -> 128 tiles 131.5 -> 132.9 M ex/s (two rounds)
-  int lb_tiles = 128;
   int lb_hnt = 0;  // lb_hnt=256|512|1024: its histogram / scatter blocks' threads (0: auto,
                    // 512 for valued batches, 1024 for binary ones)
-  // loc_onepass=1: the Localizer's heads -> ranks -> outputs in one look-back pass (A/B; 0:
-  // heads + scan + write)
-  int loc_onepass = 0;
   // nt=<mask>: streaming (non-temporal) cache policy for 1 the Localizer lane's sort passes and
   // transform, 2 the backward's model-table lines, 4 the forward's, 8 the backward's
   // per-occurrence arrays (common.h ld4 / st4)
@@ -126,12 +105,6 @@ struct Kw {
   // loc_xpay=0: valued 16-byte items carry the position and the write pass gathers the value
   // (A/B; 1: the value's bits ride in the payload, read by the transform in input order)
   int loc_xpay = 1;
-  // lane_prio=auc_high|high|normal|loc_high: the Localizer / AUC lanes' priorities (A/B;
-  // "normal" = the context stream's for the Localizer lane, 0 for the AUC lane).  Default
-  // auc_high: the AUC lane's short latency-bound chain at high priority, the Localizer lane at
-  // the context stream's (fused step: it then ends about when the next step needs it, and the
-  // backward keeps more of the machine: +1.5 %)
-  int lane_prio = 2;  // initv_onepass=0: the fused step's InitV as scan + k_initv (A/B)
   int strict = 0;     // strict=1: unknown kwargs are an error
 };
 
@@ -163,41 +136,20 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
     else if (k == "seed") kw->seed = (unsigned)strtoul(cv, nullptr, 10);
     else if (k == "max_keys") kw->max_keys = atoll(cv);
     else if (k == "max_vrows") kw->max_vrows = atoll(cv);
-    else if (k == "fwd_probe") kw->fwd_probe = atoi(cv);
-    else if (k == "xvp_row") kw->xvp_row = atoi(cv) != 0;
     else if (k == "bwd_lds") kw->bwd_lds = atol(cv);
     else if (k == "autogrow") kw->autogrow = atoi(cv) != 0;
     else if (k == "sort_pack") kw->sort_pack = atoi(cv) != 0;
-    else if (k == "sort_items") {
-      kw->sort_items = atoi(cv);
-      if (kw->sort_items != 8 && kw->sort_items != 16 && kw->sort_items != 32) {
-        set_error("sort_items must be 8, 16 or 32");
-        return DFX_ERR_ARG;
-      }
-    }
-    else if (k == "sort_lookback") {
-      kw->sort_lookback = atoi(cv);
-      if (kw->sort_lookback != 4 && kw->sort_lookback != 16 && kw->sort_lookback != 32) {
-        set_error("sort_lookback must be 4, 16 or 32");
-        return DFX_ERR_ARG;
-      }
-    }
     else if (k == "fat_fwd") kw->fat_fwd = atoi(cv) != 0;
-    else if (k == "fat_bwd") kw->fat_bwd = atoi(cv) != 0;
-    else if (k == "initv_onepass") kw->initv_onepass = atoi(cv) != 0;
     else if (k == "diag") {
       if (v == "noauc") kw->diag = 1;
       else if (v == "noloc") kw->diag = 2;
       else if (v == "noauc_noloc") kw->diag = 3;
       else { set_error("unknown diag: " + v + " (noauc|noloc|noauc_noloc)"); return DFX_ERR_ARG; }
     }
-    else if (k == "loc_onepass") kw->loc_onepass = atoi(cv) != 0;
     else if (k == "loc_bucket") kw->loc_bucket = atoi(cv) != 0;
     else if (k == "lb_diag") kw->lb_diag = atoi(cv);
-    else if (k == "auc_db") kw->auc_db = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_gather") kw->lb_gather = atoi(cv) < 0 ? 0 : (atoi(cv) > 2 ? 2 : atoi(cv));
     else if (k == "lb_hnt") kw->lb_hnt = atoi(cv);
-    else if (k == "lb_tiles") kw->lb_tiles = atoi(cv) > 0 ? atoi(cv) : 128;
     else if (k == "lr_lanes") kw->lr_lanes = atoi(cv) != 0;
     else if (k == "bwd_two_pass") kw->bwd_two_pass = atoi(cv);
     else if (k == "bwd_cpl_from") kw->bwd_cpl_from = atoi(cv);
@@ -222,14 +174,6 @@ static int parse_kwargs(const char* kwargs, Kw* kw) {
         set_error("nt must be a mask of 1, 2, 4, 8");
         return DFX_ERR_ARG;
       }
-    }
-    else if (k == "lane_prio") {
-      if (v == "high") kw->lane_prio = 3;
-      else if (v == "normal") kw->lane_prio = 0;
-      else if (v == "loc_high") kw->lane_prio = 1;
-      else if (v == "auc_high") kw->lane_prio = 2;
-      else if (v == "loc_low") kw->lane_prio = 6;
-      else { set_error("unknown lane_prio: " + v + " (high|normal|loc_high|auc_high|loc_low)"); return DFX_ERR_ARG; }
     }
     else if (k == "slot_layout") {
       if (v == "auto") kw->slot_layout = -1;
@@ -302,21 +246,17 @@ int pipeline_init(Context* c) {
   if (c->loc_stream) return DFX_OK;
   // the side lanes run latency-bound chains of small launches beside a full-occupancy
   // backward: the AUC lane gets priority so its workgroups are not queued behind its tail;
-  // the Localizer lane, which has a step of slack, runs at the main stream's priority by default
-  // (kwarg lane_prio; DESIGN.md (d) has the sweep)
+  // the Localizer lane, which has a step of slack, runs at the context stream's priority (the
+  // sharded bench runs its compute on a high-priority stream: a Localizer lane below it
+  // starved, 108 -> 70 M ex/s).  The other assignments were measured in rounds 2-4 (DESIGN.md
+  // (d)) and pruned as kwargs in round 6
   int lo = 0, hi = 0;
   DFX_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  // kwarg lane_prio: bit 0 the Localizer lane high, else at the context stream's priority (the
-  // sharded bench runs its compute on a high-priority stream: a Localizer lane below it
-  // starved, 108 -> 70 M ex/s); bit 1 the AUC lane high, else priority 0; bit 2 (loc_low) the
-  // Localizer lane at the lowest priority whatever the context stream's
+  (void)lo;
   int main_prio = 0;
   if (hipStreamGetPriority(c->stream, &main_prio) != hipSuccess) main_prio = 0;
-  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking,
-                                      (c->lane_prio & 1) ? hi
-                                      : (c->lane_prio & 4) ? lo : main_prio));
-  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking,
-                                      (c->lane_prio & 2) ? hi : 0));
+  DFX_HIP(hipStreamCreateWithPriority(&c->loc_stream, hipStreamNonBlocking, main_prio));
+  DFX_HIP(hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, hi));
   c->own_loc_stream = c->loc_stream;
   DFX_HIP(hipStreamCreateWithPriority(&c->part_stream, hipStreamNonBlocking, hi));
   c->own_part_stream = c->part_stream;
@@ -364,19 +304,13 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->device = device;
   c->P = kw.P;
   c->loss_fm = kw.loss_fm;
-  c->fwd_probe = kw.fwd_probe;
-  c->xvp_row = kw.xvp_row;
   c->bwd_lds = kw.bwd_lds;
   c->autogrow = kw.autogrow;
   c->dist_sum = kw.dist_sum;
   c->sort_pack = kw.sort_pack;
   c->auc_sort = kw.auc_sort;
-  c->sort_items = kw.sort_items;
-  c->sort_lookback = kw.sort_lookback;
   c->slot_es = kw.slot_layout == 0 ? 0 : fat_es(c->P.V_dim);
   c->fat_fwd = kw.fat_fwd;
-  c->fat_bwd = kw.fat_bwd;
-  c->initv_onepass = kw.initv_onepass;
   c->nt_mask = kw.nt;
   c->bwd_two_pass = kw.bwd_two_pass;
   c->bwd_cpl = kw.bwd_cpl;
@@ -387,12 +321,8 @@ int dfx_ctx_create(int device, const char* kwargs, dfx_ctx** out) {
   c->diag = kw.diag;
   c->loc_bucket = kw.loc_bucket;
   c->lb_diag = kw.lb_diag;
-  c->lb_tiles = kw.lb_tiles;
   c->lb_hnt = kw.lb_hnt;
-  c->auc_db = kw.auc_db;
   c->lb_gather = kw.lb_gather;
-  c->loc_onepass = kw.loc_onepass;
-  c->lane_prio = kw.lane_prio;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     set_error("hipStreamCreate failed");

@@ -666,24 +666,171 @@ __global__ void k_dist_initv_sum_finalize(const uint32_t* ftotal, const int64_t*
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
 }
 
+// ---- the split owner's ranked InitV in two launches (round 6; was a three-launch scan, a count
+// kernel, the draws and a finalize: six launches on the critical path of every step, even in
+// the steady state where the backward flagged nothing and every launch exits at once).
+//   count: per tile of kIvrTile flags its count (ts[tile]); the last block (a ticket per block)
+//          sums them into this owner's F — the request count the owners all-gather
+//   draw:  per tile its exclusive prefix from ts, per chunk of kIvrNT flags a block scan, then the
+//          listed keys drawn a coordinate per thread at their rank over all owners (off + e);
+//          the last block advances the shared seed by every owner's draws and the V pool by F
+// The draws equal k_dist_initv_sum's (the same rank per key, the same rand_r jump); the tiles'
+// counts cross blocks through agent-scope atomics, as the look-back words do (lookback.h)
+constexpr int kIvrTile = 4096, kIvrNT = 256, kIvrGrid = 256;
+
+__device__ inline int64_t ivr_n(const uint32_t* nuniq, int64_t bound) {
+  const int64_t n = (int64_t)*nuniq;
+  return n < bound ? n : bound;
+}
+
+// the block's last-block ticket: true in every thread of the block that took the last ticket
+__device__ inline bool ivr_last_block(unsigned* ticket, bool* s_last) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) *s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  return *s_last;
+}
+
+__global__ __launch_bounds__(kIvrNT) void k_initv_rank_count(const uint32_t* flags, int64_t bound,
+                                                             const uint32_t* nuniq,
+                                                             const uint32_t* gate, uint32_t* ts,
+                                                             uint32_t* ftotal, int64_t* count_out,
+                                                             unsigned* ticket) {
+  __shared__ uint32_t lds[kIvrNT / kWave + 1];
+  __shared__ bool s_last;
+  if (gate && *gate == 0u) {  // no key flagged this step (the steady state): F = 0
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      *ftotal = 0u;
+      *count_out = 0;
+    }
+    return;
+  }
+  const int64_t n = ivr_n(nuniq, bound);
+  const int64_t ntiles = (n + kIvrTile - 1) / kIvrTile;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * kIvrTile;
+    uint32_t f = 0;
+    for (int i = threadIdx.x; i < kIvrTile; i += kIvrNT) {
+      const int64_t u = b0 + i;
+      f += (u < n && flags[u]) ? 1u : 0u;
+    }
+    uint32_t tot;
+    (void)block_excl_scan<kIvrNT>(f, lds, &tot);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(ts + tile, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (!ivr_last_block(ticket, &s_last)) return;
+  uint32_t f = 0;
+  for (int64_t i = threadIdx.x; i < ntiles; i += kIvrNT)
+    f += __hip_atomic_load(ts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t F;
+  (void)block_excl_scan<kIvrNT>(f, lds, &F);
+  if (threadIdx.x == 0) {
+    *ftotal = F;
+    *count_out = (int64_t)F;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(kIvrNT) void k_initv_rank_draw(
+    const uint32_t* flags, int64_t bound, const uint32_t* nuniq, const uint32_t* ftotal,
+    const uint32_t* ts, const uint32_t* segslot, const int64_t* Fall, int rank, int nranks,
+    Table T, float scale, DevState* ds, int64_t vcap, uint32_t* fcount, unsigned* ticket) {
+  __shared__ uint32_t lds[kIvrNT / kWave + 1];
+  __shared__ uint32_t s_st[kIvrNT], s_vr[kIvrNT], s_A[kIvMaxD], s_C[kIvMaxD];
+  __shared__ bool s_last;
+  int64_t tot = 0, off = 0;
+  for (int h = 0; h < nranks; ++h) {
+    tot += Fall[h];
+    if (h < rank) off += Fall[h];
+  }
+  if (tot == 0) {  // no owner draws: nothing advances (the gate's reset only)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *fcount = 0u;
+    return;
+  }
+  const uint32_t F = *ftotal;
+  const int d = T.d;
+  if (F > 0) {
+    for (int j = threadIdx.x; j < d && j < kIvMaxD; j += kIvrNT)
+      lcg_jump(3ull * (uint64_t)j, &s_A[j], &s_C[j]);
+    const int64_t n = ivr_n(nuniq, bound);
+    const int64_t ntiles = (n + kIvrTile - 1) / kIvrTile;
+    const uint32_t seed = ds->seed;
+    const uint64_t nv0 = ds->n_vrows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      uint32_t pre = 0;  // the tile's exclusive prefix: the counts of the tiles before it
+      for (int64_t i = threadIdx.x; i < tile; i += kIvrNT)
+        pre += __hip_atomic_load(ts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t base;
+      (void)block_excl_scan<kIvrNT>(pre, lds, &base);
+      if (__hip_atomic_load(ts + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) continue;
+      const int64_t b0 = tile * kIvrTile;
+      for (int c0 = 0; c0 < kIvrTile; c0 += kIvrNT) {
+        const int64_t u = b0 + c0 + threadIdx.x;
+        const bool f = u < n && flags[u] != 0u;
+        uint32_t cnt;
+        const uint32_t at = block_excl_scan<kIvrNT>(f ? 1u : 0u, lds, &cnt);
+        if (f) {
+          const uint32_t e = base + at;
+          uint32_t st = lcg_advance(seed, 3ull * (uint64_t)d * (uint64_t)(off + e));
+          const int64_t vr = initv_row(T, nv0, e, segslot[u]);
+          if (vr >= T.vcap) {
+            s_vr[at] = 0xFFFFFFFFu;  // kErrPoolFull: set by the last block
+          } else {
+            s_vr[at] = (uint32_t)vr;
+            ent_at(T, segslot[u])->vrow = (int32_t)vr;
+            if (d > kIvMaxD) {  // (wide V: the row by its own thread)
+              float* V = row_V(T, vr);
+              float* C = row_C(T, vr);
+              for (int k = 0; k < d; ++k) {
+                V[k] = initv_value(rand_r_dev(&st), scale);
+                C[k] = 0.f;
+              }
+            }
+          }
+          s_st[at] = st;
+        }
+        __syncthreads();
+        if (d <= kIvMaxD)
+          initv_draw_list<kIvrNT>(cnt, s_st, s_vr, d, scale, s_A, s_C,
+                                  [&](uint32_t r) { return row_V(T, r); },
+                                  [&](uint32_t r) { return row_C(T, r); });
+        base += cnt;
+        __syncthreads();
+      }
+    }
+  }
+  // the last block: every owner's draws advance the shared seed, this owner's F the pool
+  if (!ivr_last_block(ticket, &s_last) || threadIdx.x != 0) return;
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *fcount = 0u;
+  ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * (uint64_t)tot);
+  const unsigned long long nv = ds->n_vrows + F;
+  if (nv > (unsigned long long)vcap) atomicOr(&ds->err, kErrPoolFull);
+  ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+}
+
 int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32_t* nuniq,
                      uint32_t* ftotal, const uint32_t* gate, int64_t* count_dev) {
-  DFX_TRY(scan_u32(L, flags, bound, ftotal, nuniq, gate));
-  hipLaunchKernelGGL(k_dist_initv_count, dim3(1), dim3(1), 0, L.stream, ftotal, count_dev);
+  const int64_t ntiles = std::max<int64_t>(1, (bound + kIvrTile - 1) / kIvrTile);
+  DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+  const dim3 g((unsigned)std::min<int64_t>(ntiles, kIvrGrid));
+  hipLaunchKernelGGL(k_initv_rank_count, g, dim3(kIvrNT), 0, L.stream, flags, bound, nuniq, gate,
+                     L.ws->tiles.as<uint32_t>(), ftotal, count_dev, &L.ds->ivr_ticket[0]);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
 
-int initv_rank_draw(Context* c, const Lane& L, const uint32_t* excl, const uint32_t* ftotal,
+int initv_rank_draw(Context* c, const Lane& L, const uint32_t* flags, const uint32_t* ftotal,
                     const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
                     const int64_t* counts_all, int rank, int nranks, uint32_t* fcount) {
-  if (bound > 0) {
-    const dim3 igrid((unsigned)std::min<int64_t>((bound + kDNT - 1) / kDNT, 1024));
-    hipLaunchKernelGGL(k_dist_initv_sum, igrid, dim3(kDNT), 0, L.stream, excl, ftotal, nuniq,
-                       bound, segslot, counts_all, rank, c->T, c->P.V_init_scale, c->ds);
-  }
-  hipLaunchKernelGGL(k_dist_initv_sum_finalize, dim3(1), dim3(1), 0, L.stream, ftotal,
-                     counts_all, nranks, c->P.V_dim, c->T.vcap, c->ds, fcount);
+  const int64_t ntiles = std::max<int64_t>(1, (bound + kIvrTile - 1) / kIvrTile);
+  DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+  const dim3 g((unsigned)std::min<int64_t>(ntiles, kIvrGrid));
+  hipLaunchKernelGGL(k_initv_rank_draw, g, dim3(kIvrNT), 0, L.stream, flags, bound, nuniq, ftotal,
+                     L.ws->tiles.as<uint32_t>(), segslot, counts_all, rank, nranks, c->T,
+                     c->P.V_init_scale, c->ds, c->T.vcap, fcount, &L.ds->ivr_ticket[1]);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

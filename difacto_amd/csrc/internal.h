@@ -74,6 +74,7 @@ struct DevState {
   double scratch[8];
   unsigned int iv_ticket;      // the one-launch InitV's tile tickets (reset by k_step_finalize)
   unsigned int iv_epoch;       // its look-back words' tag (advanced by k_step_finalize)
+  unsigned int ivr_ticket[2];  // the ranked InitV's two launches: block tickets (self-resetting)
   // the bucket Localizer (locbucket.hip): min / max of the batch's keys, and the key range its
   // bucket map was fitted to (the previous batch on this lane; pk_valid == 0: none yet)
   unsigned long long kmin, kmax, pk_min, pk_max;
@@ -213,23 +214,17 @@ struct Context {
   Workspace bws[kSlots];  // [0], [1]: also the fused step's Localizer parities
   DevState* bds[kSlots] = {};
   Workspace aws;
-  Workspace aws_alt;  // auc_db: the other parity's AUC snapshot (fused step)
+  Workspace aws_alt;  // the other parity's AUC snapshot (fused step, B <= kAucBlockMax)
   int auc_par = 0;
-  hipEvent_t ev_auc_p[2] = {};  // auc_db: the AUC that last read each parity's snapshot
+  hipEvent_t ev_auc_p[2] = {};  // the AUC that last read each parity's snapshot
   DevState* ads = nullptr;
   hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
   hipEvent_t ev_loc[kSlots] = {}, ev_free[kSlots] = {};
   int parity = 0;
-  // the fused forward finds every nnz's key in the table (no Localizer col scatter, no pulled
-  // {w, vrow} per key); 0: col + pulled (kwarg fwd_probe=0)
-  int fwd_probe = 1;
-  int xvp_row = 1;    // p rides in the XV*p rows (kwarg xvp_row)
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
   int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
   int slot_es = 0;    // Table::es of this context's store (kwarg slot_layout)
   int fat_fwd = 1;    // kwarg fat_fwd
-  int fat_bwd = 1;    // kwarg fat_bwd
-  int initv_onepass = 1;  // kwarg initv_onepass
   int fwd_cpl = 8;        // kwarg fwd_cpl: V coordinates per lane of the probe forward
   int nt_mask = 0;        // kwarg nt (common.h kNt*)
   int bwd_two_pass = 1;   // kwarg bwd_two_pass: 1 = two passes at >= 32 lanes per key
@@ -238,22 +233,16 @@ struct Context {
   int loc_x_payload = 1;    // kwarg loc_xpay: valued data carries x, not the position
   int lr_lanes = 1;       // kwarg lr_lanes (fm.hip launch_fwd_fused, V_dim 0) (fm.hip fwd_probe_body IDS)
   int loc_bucket = 1;     // kwarg loc_bucket: the bucket Localizer (locbucket.hip); 0: radix
-  int auc_db = 2;          // kwarg auc_db (step.hip): double-buffered AUC snapshot (2: B <= 12288)
   int lb_gather = 2;      // kwarg lb_gather (valued rows / values by position; 2: in the backward)
-  int lb_tiles = 128;     // kwarg lb_tiles: the bucket Localizer's row tiles at most
   int lb_hnt = 0;         // kwarg lb_hnt: the bucket Localizer's histogram / scatter block (0 auto)
   int lb_diag = 0;        // kwarg lb_diag (MEASUREMENT ONLY, wrong results): bucket kernel parts off
   int lb_skip = 0;        // lb_diag's launch-skip bits, armed once a workspace holds a batch
-  int loc_onepass = 0;    // kwarg loc_onepass (localize.hip k_loc_write)
   int diag = 0;           // kwarg diag (measurement only): bit 0 no AUC lane, bit 1 Localizer once
   bool loc_done[2] = {false, false};  // diag bit 1: the parity's Localizer output exists
   const uint2* loc_rowof[2] = {nullptr, nullptr};  // (lb_gather=2) the parity's {row, value} by position
-  int lane_prio = 2;      // kwarg lane_prio (bit 0 Localizer lane high, bit 1 AUC lane high)
   int sort_pack = 1;  // the Localizer's sort carries (key bits, row) as one u64 (kwarg)
   int auc_sort = 1;  // the AUC lane's sort (kwarg auc_sort): 3 wave buckets, 2 block buckets,
                      // 1 onesweep radix, 0 merge
-  int sort_items = 16;    // the Localizer sort's items per thread (tile = 256 x this; kwarg)
-  int sort_lookback = 4;  // the Localizer sort's look-back step width (kwarg)
   // capacity guard (store.hip cap_check / cap_record): the model's key and V-row counts as of
   // recent steps, read back asynchronously into pinned memory, and the inserts enqueued since
   CapGuard capg;
@@ -396,7 +385,7 @@ void scan_tiles_top_gated(const Lane& L, uint32_t* tilesum, int64_t ntiles, uint
 // 31 set on each key's first occurrence in sorted order), and optionally cnt[U] and
 // segstart[U+1].  With occ_row (and occ_x when value != NULL) it also writes every
 // occurrence's row (and value) in sorted order, for the backward walk.  No model access.
-// the one-block LDS AUC's largest snapshot (metric.hip k_auc_block); auc_db=2 double-buffers the
+// the one-block LDS AUC's largest snapshot (metric.hip k_auc_block); step.hip double-buffers the
 // fused step's snapshot up to this many rows
 constexpr int64_t kAucBlockMax = 12288;
 struct LocOut {
@@ -459,12 +448,12 @@ int store_maybe_grow(Context* c);
 
 // metrics (metric.hip): AUC*n and sum of log(1+exp(-y pred)) into device doubles
 // push_agg=sum InitV ranked over all owners (dist.hip), for the flags of any owner step: count
-// scans the flags (per unique key, key order) in place and writes their number to count_dev;
+// counts the flags (per unique key, key order) by tile and writes their number to count_dev;
 // draw draws this owner's flagged keys after every lower owner's and advances the shared seed
-// by the total of counts_all[nranks]
+// by the total of counts_all[nranks] — one launch each
 int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32_t* nuniq,
                      uint32_t* ftotal, const uint32_t* gate, int64_t* count_dev);
-int initv_rank_draw(Context* c, const Lane& L, const uint32_t* excl, const uint32_t* ftotal,
+int initv_rank_draw(Context* c, const Lane& L, const uint32_t* flags, const uint32_t* ftotal,
                     const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
                     const int64_t* counts_all, int rank, int nranks, uint32_t* fcount);
 // Update(kFeaCount) of a localized batch's segments (count = segment length), InitV requests

@@ -126,7 +126,6 @@ struct LocWriteArgs {
   int64_t n;
   DevState* ds;
   const uint32_t* tilebase;   // two-pass mode: per tile the heads before it (k_loc_heads + scan)
-  unsigned long long* hstat;  // one-pass mode: per tile its tagged look-back word
   uint64_t* uniq;
   uint32_t* col;
   int col_heads;     // col[pos] = rank | (pos is its segment's head) << 31
@@ -176,24 +175,16 @@ __global__ __launch_bounds__(kLocNT) void k_loc_heads(const uint64_t* k0, const 
 
 // Ranks -> outputs (RemapIndex, localizer.cc:62-107) over tiles of 2048 sorted items: per
 // unique key (rank) uniq and segment start; per nnz col[pos] = rank; per occurrence in sorted
-// order its row (and value).  A tile's base rank comes from the two-pass scan (a.tilebase), or
-// — one-pass mode (kwarg loc_onepass), no heads launch — tiles are taken in order by a ticket,
-// count their own heads and find the heads before them by decoupled look-back (a wave reads 64
-// predecessors' words at a time).  The one-pass form reads the keys once, but its blocks sit
-// spinning on the look-back beside the backward (measured: 100 us against 60 us for heads +
-// scan + write, and a slower backward), so two passes are the default.
+// order its row (and value).  A tile's base rank comes from the two-pass scan (a.tilebase).
+// (A one-pass form — tiles by ticket, their heads' base by decoupled look-back — read the keys
+// once, but its blocks sat spinning on the look-back beside the backward: 100 us against 60 us
+// for heads + scan + write, and a slower backward; pruned in round 6.)
 __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   __shared__ uint32_t lds[kLocNT / kWave + 1];
-  __shared__ uint32_t s_tile, s_pre;
   unsigned* meta = a.ds->sortmeta;
-  const bool onepass = a.tilebase == nullptr;
-  if (onepass) {
-    if (threadIdx.x == 0) s_tile = atomicAdd(&meta[kSortMetaHwTile], 1u);
-    __syncthreads();
-  }
-  const int64_t tile = onepass ? (int64_t)s_tile : (int64_t)blockIdx.x;
+  const int64_t tile = blockIdx.x;
   const int64_t n = a.n;
-  if (tile * kLocTile >= n) return;  // every later ticket exits too: no waiter is left behind
+  if (tile * kLocTile >= n) return;
   const bool s1 = meta[31] != 0;
   const uint64_t* K = s1 ? a.k1 : a.k0;
   const uint64_t* P = s1 ? a.p1 : a.p0;
@@ -205,7 +196,6 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
   uint64_t k[kLocItems];
   uint32_t h[kLocItems];
   uint32_t s = 0;
-  bool longseg = false;
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
@@ -214,8 +204,6 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
       k[i] = K[idx];
       const uint64_t kb = sort_key_bits(meta, k[i]);
       h[i] = (idx == 0 || kb != sort_key_bits(meta, K[idx - 1])) ? 1u : 0u;
-      if (onepass && idx >= kChunkOcc && kb == sort_key_bits(meta, K[idx - kChunkOcc]))
-        longseg = true;
       if (packed) {
         uint32_t row;
         sort_unpack(meta, andm, k[i], &k[i], &row);
@@ -223,16 +211,7 @@ __global__ __launch_bounds__(kLocNT) void k_loc_write(LocWriteArgs a) {
     }
     s += h[i];
   }
-  uint32_t incl;
-  if (onepass) {
-    flag_longseg(longseg, a.ds);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kLocNT>(s, lds, &tot);
-    // decoupled look-back over the tiles before this one: their heads
-    incl = ex + tile_lookback(a.hstat, tile, hw_tag(meta), tot, &a.ds->err, &s_pre);
-  } else {
-    incl = block_excl_scan<kLocNT>(s, lds, nullptr) + a.tilebase[tile];
-  }
+  uint32_t incl = block_excl_scan<kLocNT>(s, lds, nullptr) + a.tilebase[tile];
 #pragma unroll
   for (int i = 0; i < kLocItems; ++i) {
     int64_t idx = base + i;
@@ -440,41 +419,24 @@ int localize_run(Context* c, const Lane& L, int64_t B, int64_t nnz, const uint64
     DFX_TRY((radix_sort_pairs<uint64_t, uint32_t>(L, k0, q0, k1, q1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
-                                                      kSortItems(c->sort_items) |
-                                                      kSortLookback(c->sort_lookback) |
                                                       (c->sort_pack ? kSortPackRows(rb8) : 0) |
                                                       (c->nt_mask & kNtLane ? kSortNT : 0))));
   } else {
     DFX_TRY((radix_sort_pairs<uint64_t, uint64_t>(L, k0, p0, k1, p1, nnz, 0, 64, &ds->or_mask,
                                                   ds->sortmeta, nullptr,
                                                   kSortDiffIsOrAnd | kSortCountsReady |
-                                                      kSortItems(c->sort_items) |
-                                                      kSortLookback(c->sort_lookback) |
                                                       (c->nt_mask & kNtLane ? kSortNT : 0))));
   }
-  // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write, or (loc_onepass) one
-  // k_loc_write with look-back
+  // heads -> ranks -> outputs: k_loc_heads + k_scan_top + k_loc_write
   const int64_t ntiles = (nnz + kLocTile - 1) / kLocTile;
-  uint32_t* ts = nullptr;
-  if (!c->loc_onepass) {
-    DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
-    ts = ws.tiles.as<uint32_t>();
-  }
-  if (c->loc_onepass) {
-    void* before = ws.hstat.p;
-    DFX_TRY(ws.hstat.ensure(sizeof(unsigned long long) * (ntiles > 256 ? ntiles : 256)));
-    if (ws.hstat.p != before)  // fresh words read as unpublished (tag 0, flag 0)
-      DFX_HIP(hipMemsetAsync(ws.hstat.p, 0, ws.hstat.bytes, L.stream));
-  }
-  if (ts) {
-    hipLaunchKernelGGL(k_loc_heads, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, k0, k1,
-                       nnz, ds, ts);
-    scan_tiles_top(L, ts, ntiles, nullptr);
-  }
+  DFX_TRY(ws.tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
+  uint32_t* ts = ws.tiles.as<uint32_t>();
+  hipLaunchKernelGGL(k_loc_heads, dim3((unsigned)ntiles), dim3(kLocNT), 0, L.stream, k0, k1, nnz,
+                     ds, ts);
+  scan_tiles_top(L, ts, ntiles, nullptr);
   LocWriteArgs a{};
   a.k0 = k0; a.k1 = k1; a.p0 = p0; a.p1 = p1; a.q0 = q0; a.q1 = q1;
   a.n = nnz; a.ds = ds; a.tilebase = ts;
-  a.hstat = ts ? nullptr : ws.hstat.as<unsigned long long>();
   a.uniq = o.uniq; a.col = o.col; a.col_heads = o.col_heads ? 1 : 0; a.segstart = segs;
   a.value = o.value; a.occ_row = o.occ_row;
   a.occ_x = (o.occ_row && o.value) ? o.occ_x : nullptr;

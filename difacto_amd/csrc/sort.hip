@@ -353,16 +353,9 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                      int end_bit, const unsigned long long* diff_mask, unsigned int* sortmeta,
                      const uint32_t* n_dev, int flags) {
   Workspace& ws = *L.ws;
-  const int it = (flags >> 16) & 0xFF ? (flags >> 16) & 0xFF : kOsItems;
-  const int lb = (flags >> 24) & 0x7F ? (flags >> 24) & 0x7F : kOsLookback;
-  if ((lb != 4 && lb != 16 && lb != 32) || (lb != 4 && it != 16)) {
-    set_error("radix_sort_pairs: look-back width 4, or 16 / 32 with 16 items per thread");
-    return DFX_ERR_ARG;
-  }
-  if (it != 8 && it != 16 && it != 32) {
-    set_error("radix_sort_pairs: items per thread must be 8, 16 or 32");
-    return DFX_ERR_ARG;
-  }
+  // (round 6: the tile / look-back variants — 8 or 32 items per thread, 16 or 32 look-back
+  // words — measured slower in rounds 2-3 and pruned: one instantiation per key / payload type)
+  constexpr int it = kOsItems;
   const int64_t tile = (int64_t)kOsNT * it;
   const int64_t ntiles = n > 0 ? (n + tile - 1) / tile : 1;
   DFX_TRY(ws.os_reserve(n > 0 ? (n + 2047) / 2048 : 1, L.stream));  // look-back words for tiles >= 2048
@@ -387,17 +380,9 @@ int radix_sort_pairs(const Lane& L, K* k0, P* v0, K* k1, P* v1, int64_t n, int b
                      begin_bit, end_bit, sortmeta, parts, counts, epoch, pack_rb8);
   for (int q = 0; q < npasses; ++q) {
     const int64_t grid = ntiles;
-#define DFX_OS_SCATTER(IT, LB)                                                               \
-    if (it == IT && lb == LB)                                                                \
-      hipLaunchKernelGGL((k_os_scatter<K, P, IT, LB>), dim3((unsigned)grid), dim3(kOsNT), 0,   \
-                         L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts, status,     \
-                         L.err, (flags & kSortNT) ? 1 : 0);
-    DFX_OS_SCATTER(8, 4)
-    DFX_OS_SCATTER(16, 4)
-    DFX_OS_SCATTER(32, 4)
-    DFX_OS_SCATTER(16, 16)
-    DFX_OS_SCATTER(16, 32)
-#undef DFX_OS_SCATTER
+    hipLaunchKernelGGL((k_os_scatter<K, P, kOsItems, kOsLookback>), dim3((unsigned)grid),
+                       dim3(kOsNT), 0, L.stream, k0, v0, k1, v1, n, n_dev, sortmeta, q, counts,
+                       status, L.err, (flags & kSortNT) ? 1 : 0);
   }
   DFX_HIP(hipGetLastError());
   return DFX_OK;

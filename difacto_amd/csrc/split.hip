@@ -334,7 +334,7 @@ int dfx_split_part_floats(dfx_ctx* ctx, int nranks) {
 }
 
 int dfx_split_pxv_floats(dfx_ctx* ctx) {
-  return ctx ? split_pxv_floats(ctx->c.P.V_dim, ctx->c.xvp_row) : -1;
+  return ctx ? split_pxv_floats(ctx->c.P.V_dim, 1) : -1;
 }
 
 int dfx_split_partition(dfx_ctx* ctx, int slot, const dfx_batch* b, uint64_t max_index,
@@ -522,7 +522,7 @@ int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nr
       a.slice_len = len;
     }
     int nblk = 0;
-    DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+    DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, true));
   }
   if (!last) return DFX_OK;
   // a step without a backward is done with the slot (and the table) here
@@ -561,7 +561,7 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   }
   const int64_t rpb = G ? kSpNT / G : kSpNT;
   const int64_t nb = (B + rpb - 1) / rpb;
-  const int PX = split_pxv_floats(d, c->xvp_row);
+  const int PX = split_pxv_floats(d, 1);
   const bool first = lo == 0, last = lo + len >= part_rows;
   // one loss partial per block (the blocks of every call tile the batch), after the 8 doubles
   // the scratch keeps in front
@@ -629,14 +629,14 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     g.segstart = ows.segstart.as<uint32_t>(); g.ds = ods; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = ows.occ_row.as<uint32_t>();
     g.occ_x = c->split_x[slot] ? ows.occ_x.as<float>() : nullptr;
-    g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d, c->xvp_row); g.d = d;
+    g.zpad = c->zpad; g.p = nullptr; g.XVp = pxv; g.xs = split_pxv_floats(d, 1); g.d = d;
     if (d >= 64 && d % 32 == 0 && R > 0) {  // p a line of its own in the rows: compact (row_p)
       DFX_TRY(ows.p.ensure((size_t)R * 4));
       hipLaunchKernelGGL(k_split_p_compact, dim3((unsigned)((R + 255) / 256)), dim3(256), 0,
                          c->stream, pxv, R, g.xs, d, ows.p.as<float>());
       g.p = ows.p.as<float>();
     }
-    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from;
+    g.slot = ows.slot.as<uint32_t>(); g.T = c->T; g.Pm = c->P; g.no_fat_spec = false; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from;
     g.flags = ows.oflags.as<uint32_t>(); g.dsw = c->ds;
     g.uniq = ows.uniq.as<uint64_t>(); g.insert_keys = c->split_resolved[slot] ? 0 : 1;
     g.choff = ows.flags.as<uint32_t>(); g.chunk_seg = ows.rowtmp.as<uint32_t>();

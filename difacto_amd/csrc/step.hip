@@ -26,12 +26,12 @@ namespace dfx {
 
 // Row stride of the fused step's XV_*p rows: a multiple of 32 floats (128 B) carrying p after
 // XV_*p, so the backward's per-occurrence p and XV_*p sit in one 128-byte line (+3 % of the
-// step at d = 16, same-box A/B).  Context kwarg xvp_row=0: rows of d floats, p apart.  At d a
-// multiple of 32 p would fill a 128-byte line of its own: the rows are d floats and the
-// backward reads p from the per-row array (fm.hip row_p), which stays in the L2
+// step at d = 16, same-box A/B against rows of d floats with p apart).  At d a multiple of 32 p
+// would fill a 128-byte line of its own: the rows are d floats and the backward reads p from
+// the per-row array (fm.hip row_p), which stays in the L2
 int xvp_stride(const Context* c) {
   const int d = c->P.V_dim;
-  return (c->xvp_row && d > 0 && d % 32 != 0) ? (d + 1 + 31) / 32 * 32 : d;
+  return (d > 0 && d % 32 != 0) ? (d + 1 + 31) / 32 * 32 : d;
 }
 
 // main lane: per-row arrays of the forward / backward and the InitV scan
@@ -90,10 +90,11 @@ int auc_reserve(Workspace& w, int64_t rows, hipStream_t st) {
   return DFX_OK;
 }
 
-// the fused step's AUC snapshot double-buffered at this batch size (kwarg auc_db)
-static bool auc_db_on(const Context* c, int64_t rows) {
-  return c->auc_db == 1 || (c->auc_db == 2 && rows <= kAucBlockMax);
-}
+// the fused step's AUC snapshot double-buffered at this batch size: at B <= kAucBlockMax the
+// one-block AUC (~94 us beside the backward) outlasts the rest of a small step, and a forward
+// then waits only for the AUC of two steps back (B = 10^4: 58.6 / 61.6 -> 68.0 / 68.8 M ex/s);
+// at B = 10^5 always-on was a tie (measured in round 4; the kwarg auc_db pruned in round 6)
+static bool auc_db_on(const Context*, int64_t rows) { return rows <= kAucBlockMax; }
 
 int step_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(pipeline_init(c));
@@ -174,16 +175,6 @@ int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uni
                      segslot, c->ds);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
-}
-
-// the pull after a count push: {w, vrow} of each unique key by slot
-__global__ __launch_bounds__(256) void k_pull_keys(const uint32_t* __restrict__ segslot,
-                                                   const DevState* nds, Table T,
-                                                   int2* __restrict__ pulled) {
-  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (u >= (int64_t)nds->u_count) return;
-  const uint32_t s = segslot[u];
-  pulled[u] = s == kNoSlot ? make_int2(0, -1) : *reinterpret_cast<const int2*>(ent_at(T, s));
 }
 
 // the step's last kernel: the forward's loss partials summed (k_sum_parts' order exactly),
@@ -299,7 +290,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DevState* bds = c->bds[k];
   const Lane LL{c->loc_stream, &bw, bds, &c->ds->err};
   // the AUC snapshot's buffers: one, or two alternating (auc_db)
-  // (auc_db=2 switches with B: a single-buffered step uses buffer 0 and waits for the latest
+  // (the form switches with B: a single-buffered step uses buffer 0 and waits for the latest
   // AUC; every step records which AUC last read its buffer)
   const bool db = auc_db_on(c, B);
   const int ap = db ? c->auc_par : 0;
@@ -308,10 +299,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   if (db) c->auc_par ^= 1;
   const Lane AL{c->aux_stream, &aw, c->ads, &c->ds->err};
   uint32_t* segstart = bw.segstart.as<uint32_t>();
-  uint32_t* col = bw.col.as<uint32_t>();       // per nnz: the rank of its key
   uint64_t* uniq = bw.uniq.as<uint64_t>();     // per rank: the key
   uint32_t* segslot = bw.slot.as<uint32_t>();  // per rank: its model-table slot
-  int2* pulled = ws.wv.as<int2>();             // per rank: {w, vrow} (the Pull)
   uint32_t* occ_row = bw.occ_row.as<uint32_t>();
   float* occ_x = b->value ? bw.occ_x.as<float>() : nullptr;
   uint32_t* flags = ws.flags.as<uint32_t>();
@@ -330,7 +319,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   o.value = b->value;
   o.occ_row = occ_row;
   o.occ_x = occ_x;
-  o.col = c->fwd_probe ? nullptr : col;  // probe mode: the forward finds keys itself
+  o.col = nullptr;  // probe mode: the forward finds keys itself
   o.uniq = uniq;
   const uint2* rowof = c->loc_rowof[k];  // (lb_gather=2) kept with the parity's outputs
   o.rowof_out = &rowof;
@@ -355,7 +344,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   const bool cnt_first = push_cnt && d > 0;
   // a training step whose forward finds keys itself needs no Get pass: absent keys read as
   // the empty entry and the backward inserts them (its find-or-insert is Get's)
-  const bool bwd_inserts = c->fwd_probe && !cnt_first && job_type == DFX_JOB_TRAINING &&
+  const bool bwd_inserts = !cnt_first && job_type == DFX_JOB_TRAINING &&
                            B > 0 && nnz > 0;
   // ---- main: wait for this batch's Localizer (the exposed part of it is the "localize" phase).
   // (The probe forward needs only the batch, but a forward that waits for the batch alone and
@@ -368,23 +357,16 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   const dim3 ug((unsigned)((nnz + kProbeNT * kProbeUnr - 1) / (kProbeNT * kProbeUnr)));
   if (nnz > 0 && !bwd_inserts)
     hipLaunchKernelGGL(k_probe_keys, ug, dim3(kProbeNT), 0, c->stream, uniq, bds, c->T,
-                       cnt_first || c->fwd_probe ? nullptr : pulled, segslot, c->ds);
+                       nullptr, segslot, c->ds);
   prof_mark(c, 2);
   if (cnt_first) {
     DFX_TRY(push_cnt_seg_run(c, nnz, segstart, segslot, flags, total, bds));
-    if (!c->fwd_probe)
-      hipLaunchKernelGGL(k_pull_keys, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
-                         c->stream, segslot, bds, c->T, pulled);
   }
   prof_mark(c, 3);
 
   FwdArgs a{};
   a.B = B; a.offs = b->offset; a.val = b->value;
-  if (c->fwd_probe) {
-    a.index = b->index; a.max_index = max_index;
-  } else {
-    a.col = col; a.wv_rank = pulled;
-  }
+  a.index = b->index; a.max_index = max_index;  // probe mode: the forward finds its keys
   a.T = c->T; a.l1_shrk = c->P.l1_shrk; a.Vbase = c->T.V; a.zpad = c->zpad;
   a.no_fat_fwd = !c->fat_fwd;
   a.cpl = c->fwd_cpl;
@@ -400,7 +382,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.auc_lab = aw.av0.as<uint32_t>();
   DFX_HIP(hipStreamWaitEvent(c->stream, ev_auc_mine, 0));
   int nblk = 0;
-  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, c->fwd_probe == 1));
+  DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, true));
   prof_mark(c, 4);
   // (the forward's loss partials are summed by k_step_finalize, the step's last kernel)
 
@@ -420,7 +402,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     g.occ_row = occ_row; g.occ_x = occ_x; g.occ_rx = rowof; g.zpad = c->zpad;
     g.p = ws.p.as<float>();
     g.XVp = ws.XVp.as<float>(); g.xs = xvp_stride(c); g.d = d; g.slot = segslot;
-    g.T = c->T; g.Pm = c->P; g.no_fat_spec = !c->fat_bwd; g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from; g.nt = c->nt_mask;
+    g.T = c->T; g.Pm = c->P;  g.cpl = c->bwd_cpl; g.cpl_from = c->bwd_cpl_from; g.nt = c->nt_mask;
     g.flags = flags; g.dsw = c->ds; g.stripes = &c->ds->bw_stripe[0][0];
     g.uniq = uniq; g.insert_keys = bwd_inserts ? 1 : 0;
     g.choff = choff; g.chunk_seg = chunk_seg; g.nchunks = nchunks; g.part = ws.Vb.as<double>();

@@ -245,7 +245,7 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
               const uint32_t* slot, const DevState* nds, const uint32_t* gate, bool finalize) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
-  if (gate && n_host < 0 && !finalize && c->initv_onepass) {  // the fused step
+  if (gate && n_host < 0 && !finalize) {  // the fused step
     const int64_t ntiles = (n_bound + kIvTile - 1) / kIvTile;
     Workspace& ws = c->ws;
     void* before = ws.ivstat.p;

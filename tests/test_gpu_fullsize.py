@@ -16,6 +16,8 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
+K_CHUNK_OCC = 128  # csrc/internal.h kChunkOcc: longer segments are summed in chunks
+
 RTOL = 1e-5  # north_star: per-minibatch predictions within 1e-5 relative (fp32)
 
 
@@ -65,11 +67,16 @@ def test_localizer_full_c3(H):
 
 def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=True,
          exact=False):
-    """exact: no key reaches a chunked (> 256 occurrences) gradient sum, so predictions and the
-    model must equal the oracle's bit for bit (sums in the reference's order, glibc expf)"""
+    """exact: no key reaches a chunked (> kChunkOcc = 128 occurrences, csrc/internal.h) gradient
+    sum, so predictions and the model must equal the oracle's bit for bit (sums in the
+    reference's order, glibc expf); asserted per batch, so a change of the chunk threshold fails
+    here by name rather than as an unexplained bit mismatch"""
     c = H.Context(0, max_keys=max_keys, **cfg)
     up = O.Updater(**cfg)
     for step, blk in enumerate(batches):
+        if exact:
+            _, cnt = np.unique(blk.ids, return_counts=True)
+            assert int(cnt.max()) <= K_CHUNK_OCC, (step, int(cnt.max()))
         push = step < n_cnt
         loss, auc, opred = up.train_step(blk.offs, blk.ids, blk.vals, blk.labels,
                                          push_cnt=push, want_pred=True)

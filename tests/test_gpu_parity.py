@@ -58,12 +58,10 @@ def test_localizer_rcv1_known_answers(H, rcv1, known):
     assert int(_rev(ou).sum()) == known["localizer_hash1000"]["sum_uidx"]
 
 
-@pytest.mark.parametrize("items,lookback", [(16, 4), (8, 4), (32, 4), (16, 16), (16, 32)])
 @pytest.mark.parametrize("kind", ["criteo", "ragged", "zipf", "u64", "dups", "big"])
-def test_localizer_synthetic(H, kind, items, lookback):
-    """bit-exact Localizer; items: the radix sort's items per thread (tiles of 2048 / 4096 /
-    8192 items, context kwarg sort_items), lookback: predecessor words per look-back step"""
-    c = H.Context(0, sort_items=items, sort_lookback=lookback)
+def test_localizer_synthetic(H, kind):
+    """bit-exact Localizer (the radix sort's tile / look-back variants were pruned in round 6)"""
+    c = H.Context(0)
     if kind == "criteo":
         blk = D.synthetic(4000, 39, 1 << 24, seed=1)
     elif kind == "ragged":
