@@ -98,7 +98,6 @@ struct LbArgs {
   int hm_lds;            // the histogram / scatter launches hold LDS for the map
   int wbits_hot;         // the bucket bits a map is built for (one more than the key map's)
   uint32_t hot_th;       // a hot key's occurrences, at least
-  int mid;               // the mid-grouped item layout may be used (lb_mid_on decides per batch)
 };
 
 __device__ inline uint64_t lb_key(uint64_t id, uint64_t max_index, int keys_ready) {
@@ -223,28 +222,6 @@ __device__ inline LbPack lb_pack(const DevState* ds, uint64_t qmax) {
 }
 __device__ inline uint64_t lb_keybits(const LbPack& p, uint64_t it) {
   return p.packed ? it >> p.rb : it;
-}
-
-// The mid-grouped item layout (round 6).  Buckets go in groups of 4 (a "mid"); inside a mid's
-// region the items are ordered by row tile, then by bucket: tile t's items of the mid's 4
-// buckets form one span of ~30 items (C3) that only tile t's block writes, in 4 sub-runs.  The
-// per-bucket layout had each (tile, bucket) run of ~7 items share its 128-B lines with the
-// runs of the neighbouring tiles — blocks on other XCDs, whose L2s each wrote the line back
-// partially: 105 MB of WRITE_SIZE for 31 MB of items.  With the spans, and each XCD given a
-// contiguous range of tiles (so neighbouring spans meet in one L2), a line is completed in one
-// L2.  The sort wave of bucket b then gathers b's 128 sub-runs (one per tile) into LDS — the 4
-// waves of a mid run on one XCD, so the mid's region is read into its L2 once.
-// Packed binary items only, and no oversize bucket (those sort in place through global memory,
-// k_lb_big, which needs a bucket's items contiguous): else the per-bucket layout.
-__device__ inline bool lb_mid_on(const LbArgs& a, const LbPack& p) {
-  return a.mid && p.packed &&
-         __hip_atomic_load(&a.ds->lb_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
-}
-// the sort wave's bucket: block i runs on XCD i % 8; each XCD takes a contiguous range of
-// mids, and a mid's 4 buckets go to 4 consecutive blocks of one XCD (nbk % 32 == 0)
-__device__ inline uint32_t lb_mid_bucket(uint32_t i, uint32_t nbk) {
-  const uint32_t x = i % 8u, r = i / 8u;
-  return 4u * (x * (nbk / 32u) + r / 4u) + r % 4u;
 }
 
 __global__ void k_lb_init(DevState* ds) {
@@ -409,18 +386,14 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   const bool qs = HOT && lb_hot_on(a);
   LbHot hm{};
   if (qs) hm = lb_stage_hot(a, offs + a.rt + 1, t, kLbHNT);
-  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
-  const LbPack p = lb_pack(a.ds, qmax);
-  // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
-  const uint32_t per = (m.nbk + kLbHNT - 1) / kLbHNT;
-  const bool midl = !S && per % 4 == 0 && lb_mid_on(a, p);  // (block-uniform)
-  // the mid-grouped layout (or lb_diag 512, measurement only): each XCD a contiguous range of
-  // tiles (block i runs on XCD i % 8)
-  const int64_t tile = ((midl || (a.diag & 512)) && a.ntiles % 8 == 0)
+  // (lb_diag 512, measurement only) each XCD a contiguous range of tiles
+  const int64_t tile = ((a.diag & 512) && a.ntiles % 8 == 0)
                            ? (int64_t)(blockIdx.x % 8) * (a.ntiles / 8) + blockIdx.x / 8
                            : (int64_t)blockIdx.x;
   const int64_t r0 = tile * a.rt;
   const int nr = (int)(a.B - r0 < a.rt ? a.B - r0 : a.rt);
+  // the buckets' starts: thread t holds buckets [t * per, (t + 1) * per)
+  const uint32_t per = (m.nbk + kLbHNT - 1) / kLbHNT;
   uint32_t mine = 0, over = 0;
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
@@ -433,24 +406,13 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
   uint32_t total;
   uint32_t ex = block_excl_scan<kLbHNT>(mine, lds, &total);
   const uint32_t* pre = a.tilecnt + (size_t)tile * m.nbk;
-  const bool mid4 = !midl && (a.diag & 512) && per == 4;  // (measurement only) 4 per cursor
+  const bool mid4 = (a.diag & 512) && per == 4;  // (measurement only) 4 buckets per cursor
   uint32_t msum = 0;
   const uint32_t mex = ex;
-  const uint32_t* nxt = a.tilecnt + (size_t)(tile + 1) * m.nbk;  // (row ntiles: the totals)
   for (uint32_t i = 0; i < per; ++i) {
     const uint32_t d = t * per + i;
     if (d < m.nbk) {
-      if (midl && i % 4 == 0) {
-        // this tile's span of mid d / 4: after the mid's spans of the tiles before it, its
-        // buckets' sub-runs in bucket order
-        uint32_t base = ex + pre[d] + pre[d + 1] + pre[d + 2] + pre[d + 3];
-        for (uint32_t j = 0; j < 4; ++j) {
-          cur[d + j] = base;
-          base += nxt[d + j] - pre[d + j];
-        }
-      } else if (!midl && !mid4) {
-        cur[d] = ex + pre[d];
-      }
+      if (!mid4) cur[d] = ex + pre[d];
       msum += pre[d];
       if (blockIdx.x == 0) a.bstart[d] = ex;
       ex += a.totals[d];
@@ -479,6 +441,8 @@ __global__ __launch_bounds__(HNT) void k_lb_scatter(LbArgs a) {
       }
     }
   }
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const LbPack p = lb_pack(a.ds, qmax);
   if (blockIdx.x == 0) {
     uint32_t nover;
     (void)block_excl_scan<kLbHNT>(over, lds, &nover);
@@ -882,11 +846,10 @@ constexpr int kLbWIT = kLbCap / kWave;  // 32
 // LSD radix over the digits that vary inside the bucket, q's first when the items are not
 // packed; positions >= n of the last slot hold padding ~0.
 
-template <bool Q, bool S, bool LDSIN = false>
+template <bool Q, bool S>
 __device__ __attribute__((always_inline)) inline void lb_wave_sort(
     const uint64_t* gk, const uint32_t* gq, const uint64_t* gs, int n, bool hasq, int ntp,
     int diag, uint64_t* sk, uint32_t* sq, uint64_t* ss, uint32_t* cnt) {
-  // LDSIN: the items were gathered into sk (the mid-grouped layout, lb_mid_gather)
   const int l = threadIdx.x;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
   // the last slot's lanes past n hold padding ~0, which sorts after every item (packed items
@@ -898,8 +861,7 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(
   for (int c = 0; c < kLbWIT; ++c) {  // every load in flight at once
     const int i = c * kWave + l;
     const bool v = c < nc && i < n;
-    if (LDSIN) k[c] = v ? sk[i] : ~0ull;
-    else k[c] = v ? ldnt(gk + i, ntp != 0) : ~0ull;
+    k[c] = v ? ldnt(gk + i, ntp != 0) : ~0ull;
     q[c] = (Q && hasq) ? (v ? gq[i] : ~0u) : 0u;
     sv[c] = (S && v) ? gs[i] : 0ull;
   }
@@ -1028,50 +990,6 @@ __device__ __attribute__((always_inline)) inline void lb_wave_sort(
   passes();
 }
 
-// the mid-grouped layout: bucket b's sub-run in each row tile (tile t's span of the mid after the
-// spans of the tiles before it, then the sub-runs of the mid's buckets before b), gathered into
-// sk in tile order; lane l takes tiles l and l + 64 (ntiles <= kLbTiles = 128)
-__device__ inline void lb_mid_gather(const LbArgs& a, uint32_t b, uint32_t nbk, uint64_t* sk) {
-  const int l = threadIdx.x;
-  const uint32_t m4 = b & ~3u, j = b & 3u;
-  const int64_t T = a.ntiles;
-  const uint32_t bs = a.bstart[m4];
-  uint32_t st[2], ct[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int64_t t = l + 64 * h;
-    st[h] = 0;
-    ct[h] = 0;
-    if (t < T) {  // prefixes over the tiles before t (row t) and t + 1 (row T: the totals)
-      const uint4 pr = *reinterpret_cast<const uint4*>(a.tilecnt + (size_t)t * nbk + m4);
-      const uint4 nx = *reinterpret_cast<const uint4*>(a.tilecnt + (size_t)(t + 1) * nbk + m4);
-      const uint32_t c[4] = {nx.x - pr.x, nx.y - pr.y, nx.z - pr.z, nx.w - pr.w};
-      uint32_t s = bs + pr.x + pr.y + pr.z + pr.w;
-      for (uint32_t i = 0; i < j; ++i) s += c[i];
-      st[h] = s;
-      ct[h] = c[j];
-    }
-  }
-  const uint32_t i0 = wave_incl_scan(ct[0]);
-  const uint32_t half = __shfl(i0, kWave - 1, kWave);
-  const uint32_t d0 = i0 - ct[0], d1 = half + wave_incl_scan(ct[1]) - ct[1];
-  // every lane's loads in flight together, 4 at a time per sub-run
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t n = ct[h], dst = h ? d1 : d0;
-    const uint64_t* src = a.kbuf + st[h];
-    for (uint32_t k0 = 0; k0 < n; k0 += 4) {
-      uint64_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = k0 + u < n ? src[k0 + u] : 0ull;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (k0 + u < n) sk[dst + k0 + u] = v[u];
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
 template <bool Q, bool S>
 __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   __shared__ uint64_t sk[kLbCap];
@@ -1080,12 +998,11 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   __shared__ uint32_t cnt[256];
   DevState* ds = a.ds;
   const int l = threadIdx.x;
-  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
-  const LbPack p = lb_pack(ds, qmax);
-  const bool midl = !S && lb_mid_on(a, p);  // (grid-uniform)
-  const uint32_t b = midl ? lb_mid_bucket(blockIdx.x, 1u << a.wbits) : blockIdx.x;
+  const uint32_t b = blockIdx.x;
   const int64_t start = a.bstart[b];
   const int n = (int)((int64_t)a.bstart[b + 1] - start);
+  const uint64_t qmax = (S || a.rowof) ? (uint64_t)(a.nnz - 1) : (uint64_t)(a.B - 1);
+  const LbPack p = lb_pack(ds, qmax);
   const bool hasq = !p.packed;
   // sorted in LDS here, or already in place (k_lb_big)
   const bool fast = !lb_needs_global(n, p.packed, Q ? 1 : 0);
@@ -1093,12 +1010,8 @@ __global__ __launch_bounds__(kWave) void k_lb_wbucket(LbArgs a) {
   const uint32_t* gq = a.qbuf + start;
   const uint64_t* gs = a.sbuf + start;
   const int nc = (n + kWave - 1) / kWave;  // slots in use (wave-uniform)
-  if (midl) {  // (n <= kLbCap: no bucket is oversize in this layout)
-    lb_mid_gather(a, b, 1u << a.wbits, sk);
-    lb_wave_sort<Q, S, true>(gk, gq, gs, n, false, a.nt, a.diag, sk, sq, ss, cnt);
-  } else if (fast) {
+  if (fast)
     lb_wave_sort<Q, S>(gk, gq, gs, n, hasq, a.nt, a.diag, sk, sq, ss, cnt);
-  }
   // ---- per occurrence its row (and value); per head its key and segment start at the
   // bucket's own offset in the scratch lists (k_lb_out moves them to their ranks); a segment
   // longer than kChunkOcc raises the chunk plan's gate.  Instantiated for the LDS and for the
@@ -1480,14 +1393,6 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
   a.hot_th = (uint32_t)std::max<int64_t>(
       kWave, std::min<int64_t>(nnz / ((int64_t)1 << wbits_key) / 2, kLbCap));
   const size_t sp_bytes = a.hm_lds ? lb_hot_lds(nbk) : 0;
-  // lb_hnt (0: auto): 512-thread blocks for valued batches, whose scatter also writes the
-  // {row, value} pairs (C2 +5.6 %), 1024 for binary ones (C3: 1024 best)
-  const int hnt = c->lb_hnt ? c->lb_hnt : (valued ? 512 : 1024);
-  // the mid-grouped item layout where its index arithmetic holds (binary batches; the device
-  // takes it per batch when the items pack and no bucket is oversize: lb_mid_on)
-  a.mid = (!valued && nbk % 32 == 0 && (nbk / (uint32_t)hnt) % 4 == 0 && ntiles <= kLbTiles &&
-           !(c->lb_diag & (16 | 32 | 64 | 128 | 256 | 512)))
-              ? 1 : 0;
   hipLaunchKernelGGL(k_lb_init, dim3(1), dim3(1), 0, L.stream, L.ds);
 #define DFX_LB_HIST(NT)                                                                     \
   if (a.hm_lds) {                                                                           \
@@ -1498,6 +1403,9 @@ int localize_bucket(Context* c, const Lane& L, int64_t B, int64_t nnz, const uin
     hipLaunchKernelGGL((k_lb_hist<NT, false>), dim3((unsigned)ntiles), dim3(NT),            \
                        nbk * sizeof(uint32_t), L.stream, a);                                \
   }
+  // lb_hnt (0: auto): 512-thread blocks for valued batches, whose scatter also writes the
+  // {row, value} pairs (C2 +5.6 %), 1024 for binary ones (C3: 1024 best)
+  const int hnt = c->lb_hnt ? c->lb_hnt : (valued ? 512 : 1024);
   if (hnt == 256) { DFX_LB_HIST(256) }
   else if (hnt == 512) { DFX_LB_HIST(512) }
   else { DFX_LB_HIST(1024) }
