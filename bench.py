@@ -318,7 +318,20 @@ def cpu_baseline(args):
     # the best thread count is the baseline (on a shared host, all cores is not always the
     # fastest: the single-threaded updater competes with the OpenMP threads)
     best = max(by_threads, key=lambda k: by_threads[k])
+    cal = None  # the port against the survey's reference number, in the survey's own container
+    try:
+        cj = json.load(open(os.path.join(ROOT, "profiles", "r6", "cpu_calibration.json")))
+        al = cj["all_V (bench settings)"]["by_threads"]
+        cal = {"in_container_vs_survey_2thr_sequential": al["2"]["sequential"]["vs_survey"],
+               "in_container_vs_survey_1thr_sequential": al["1"]["sequential"]["vs_survey"],
+               "in_container_vs_survey_2thr_pipelined": al["2"]["pipelined"]["vs_survey"],
+               "source": "profiles/r6/cpu_calibration.json (tools/cpu_calibrate.py: B=10^4, "
+                         "k=39, d=16, 2^24 keys, the bench's updater settings, in the build "
+                         "container the survey measured 35.8 k ex/s in)"}
+    except (OSError, ValueError, KeyError):
+        pass
     return {"value": by_threads[best], "unit": "train examples/sec", "cores": int(best),
+            "calibration": cal,
             "cores_available": cores, "kind": "port",
             "by_threads": by_threads,
             "us_per_row_by_phase": phases,

@@ -683,9 +683,10 @@ __device__ inline int64_t ivr_n(const uint32_t* nuniq, int64_t bound) {
   return n < bound ? n : bound;
 }
 
-// the block's last-block ticket: true in every thread of the block that took the last ticket
+// the block's last-block ticket: true in every thread of the block that took the last ticket.
+// No fence: what crosses blocks goes through agent-scope atomics (a device-scope fence per
+// block would write back its XCD's L2, store.hip k_initv_onepass)
 __device__ inline bool ivr_last_block(unsigned* ticket, bool* s_last) {
-  __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) *s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   __syncthreads();

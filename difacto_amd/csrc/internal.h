@@ -75,6 +75,7 @@ struct DevState {
   unsigned int iv_ticket;      // the one-launch InitV's tile tickets (reset by k_step_finalize)
   unsigned int iv_epoch;       // its look-back words' tag (advanced by k_step_finalize)
   unsigned int ivr_ticket[2];  // the ranked InitV's two launches: block tickets (self-resetting)
+  unsigned int iv_done;        // the fused InitV's blocks done (its last block finalizes the step)
   // the bucket Localizer (locbucket.hip): min / max of the batch's keys, and the key range its
   // bucket map was fitted to (the previous batch on this lane; pk_valid == 0: none yet)
   unsigned long long kmin, kmax, pk_min, pk_max;
@@ -425,9 +426,82 @@ int auc_reserve(Workspace& w, int64_t rows, hipStream_t st);
 // nds: the device state whose u_count holds the count when n_host < 0
 // gate (optional, device): the number of set flags, or any nonzero; zero skips the pass
 // finalize = false: the caller advances the seed and the V-row count itself (by *total_dev)
+// the fused step's last work (step.hip step_finalize_body): the forward's loss partials summed,
+// the progress counters, the InitV pass's seed advance, the capacity guard's counts
+struct FinArgs {
+  DevState* ds = nullptr;
+  const DevState* bds = nullptr;
+  int64_t B = 0;
+  const uint32_t* initv_total = nullptr;
+  int d = 0;
+  int64_t vcap = 0;
+  const double* loss_part = nullptr;
+  int64_t nparts = 0;
+  unsigned long long* cap_host = nullptr;
+};
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
               const uint32_t* slot, const DevState* nds = nullptr,
-              const uint32_t* gate = nullptr, bool finalize = true);
+              const uint32_t* gate = nullptr, bool finalize = true,
+              const FinArgs* fin = nullptr);
+
+// the threads that run it (k_step_finalize; the fused InitV's blocks, store.hip kStNT)
+constexpr int kFinNT = 256;
+// the step's last work: the forward's loss partials summed (a fixed order: NT-strided, then the
+// waves in order), the progress counters, the InitV pass's seed advance, and the capacity
+// guard's counts into its pinned ring entry (cap_host, or NULL).  Run by k_step_finalize, or by
+// the last block of the fused InitV (store.hip k_initv_onepass: one launch less per step); both
+// with kFinNT threads, so a step's loss is the same sum either way.  initv_total is read with
+// an agent-scope load: the InitV kernel's last tile wrote it from another block
+template <int NT>
+__device__ inline void step_finalize_body(const FinArgs& f, double* red) {
+  DevState* ds = f.ds;
+  // the fused backward's striped {new_w, n_keys}: summed by wave 0, zeroed for the next step
+  unsigned long long snw = 0, snk = 0;
+  if (threadIdx.x < kBwStripes) {
+    unsigned long long* st = ds->bw_stripe[threadIdx.x];
+    snw = st[0];
+    snk = st[1];
+    st[0] = 0ull;
+    st[1] = 0ull;
+  }
+  if (threadIdx.x < kWave) {
+    for (int off = 32; off > 0; off >>= 1) {
+      snw += __shfl_xor(snw, off, kWave);
+      snk += __shfl_xor(snk, off, kWave);
+    }
+  }
+  double a = 0;
+  for (int64_t i = threadIdx.x; i < f.nparts; i += NT) a += f.loss_part[i];
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double loss = 0;
+  for (int k = 0; k < NT / kWave; ++k) loss += red[k];
+  ds->scratch[3] = loss;
+  // sgd::Progress: nrows, loss (sgd_learner.cc:213-229); the AUC lane adds its own
+  ds->prog[0] += (double)f.B;
+  ds->prog[1] += loss;
+  ds->sum_u += (double)f.bds->u_count;
+  ds->n_steps += 1;
+  ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
+  ds->iv_ticket = 0u;  // the next step's one-launch InitV takes its tiles from 0 again
+  ds->iv_epoch += 1u;
+  if (f.initv_total) {  // the InitV pass's rand_r advance and V rows (k_initv_finalize's work)
+    const uint32_t n = __hip_atomic_load(f.initv_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)f.d * n);
+    const unsigned long long nv = ds->n_vrows + n;
+    ds->n_vrows = nv > (unsigned long long)f.vcap ? (unsigned long long)f.vcap : nv;
+  }
+  // (atomics: the Localizer lane's probe for the next batch may be inserting beside this)
+  if (snw) atomicAdd((unsigned long long*)&ds->new_w, snw);
+  if (snk) atomicAdd(&ds->n_keys, snk);
+  if (f.cap_host) {
+    f.cap_host[0] = ds->n_keys;
+    f.cap_host[1] = ds->n_vrows;
+  }
+}
+
 // fused Update(kFeaCount): one segment per unique key (count = segment length = nds->u_count)
 int push_cnt_seg_run(Context* c, int64_t n_bound, const uint32_t* segstart,
                      const uint32_t* segslot, uint32_t* flags, uint32_t* total_dev,

@@ -307,9 +307,23 @@ __global__ void k_split_p_compact(const float* pxv, int64_t R, int xs, int d, fl
   if (r < R) p[r] = pxv[r * xs + d];
 }
 
-__global__ void k_split_worker_finalize(DevState* ds, int64_t B) {
-  ds->prog[0] += (double)B;       // sgd::Progress of this worker (sgd_learner.cc:213-229)
-  ds->prog[1] += ds->scratch[3];  // the AUC lane adds prog[2] itself
+// the combine's loss partials summed (k_sum_parts' order: 1024-strided, then the waves in
+// order) and the worker's progress — one launch (round 6; was k_sum_parts + a one-thread
+// finalize)
+__global__ __launch_bounds__(1024) void k_split_worker_finalize(const double* part, int64_t n,
+                                                                DevState* ds, int64_t B) {
+  __shared__ double red[1024 / kWave];
+  double a = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) a += part[i];
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, kWave);
+  if (lane_id() == 0) red[threadIdx.x / kWave] = a;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double s = 0;
+  for (int k = 0; k < 1024 / kWave; ++k) s += red[k];
+  ds->scratch[3] = s;
+  ds->prog[0] += (double)B;  // sgd::Progress of this worker (sgd_learner.cc:213-229)
+  ds->prog[1] += s;          // the AUC lane adds prog[2] itself
 }
 
 __global__ void k_split_zero_count(uint32_t* ftotal, int64_t* out) {
@@ -596,12 +610,12 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }
-  sum_parts(c, loss_part, nb, &c->ds->scratch[3], false);
   DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
-  hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
+  hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1024), 0, c->stream, loss_part, nb,
+                     c->ds, B);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -177,61 +177,10 @@ int probe_keys_run(Context* c, const Lane& L, int64_t bound, const uint64_t* uni
   return DFX_OK;
 }
 
-// the step's last kernel: the forward's loss partials summed (k_sum_parts' order exactly),
-// the progress counters, the InitV pass's seed advance, and the capacity guard's counts into
-// its pinned ring entry (cap_host, or NULL)
-constexpr int kFinNT = 1024;
-__global__ __launch_bounds__(kFinNT) void k_step_finalize(DevState* ds, const DevState* bds,
-                                                          int64_t B, const uint32_t* initv_total,
-                                                          int d, int64_t vcap,
-                                                          const double* loss_part, int64_t nparts,
-                                                          unsigned long long* cap_host) {
+
+__global__ __launch_bounds__(kFinNT) void k_step_finalize(FinArgs f) {
   __shared__ double red[kFinNT / kWave];
-  // the fused backward's striped {new_w, n_keys}: summed by wave 0, zeroed for the next step
-  unsigned long long snw = 0, snk = 0;
-  if (threadIdx.x < kBwStripes) {
-    unsigned long long* st = ds->bw_stripe[threadIdx.x];
-    snw = st[0];
-    snk = st[1];
-    st[0] = 0ull;
-    st[1] = 0ull;
-  }
-  if (threadIdx.x < kWave) {
-    for (int off = 32; off > 0; off >>= 1) {
-      snw += __shfl_xor(snw, off, kWave);
-      snk += __shfl_xor(snk, off, kWave);
-    }
-  }
-  double a = 0;
-  for (int64_t i = threadIdx.x; i < nparts; i += kFinNT) a += loss_part[i];
-  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, kWave);
-  if (lane_id() == 0) red[threadIdx.x / kWave] = a;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  double loss = 0;
-  for (int k = 0; k < kFinNT / kWave; ++k) loss += red[k];
-  ds->scratch[3] = loss;
-  // sgd::Progress: nrows, loss (sgd_learner.cc:213-229); the AUC lane adds its own
-  ds->prog[0] += (double)B;
-  ds->prog[1] += loss;
-  ds->sum_u += (double)bds->u_count;
-  ds->n_steps += 1;
-  ds->n_init = 0;  // the backward's InitV request count (gates the next step's InitV pass)
-  ds->iv_ticket = 0u;  // the next step's one-launch InitV takes its tiles from 0 again
-  ds->iv_epoch += 1u;
-  if (initv_total) {  // the InitV pass's rand_r advance and V rows (k_initv_finalize's work)
-    const uint32_t n = *initv_total;
-    ds->seed = lcg_advance(ds->seed, 3ull * (uint64_t)d * n);
-    const unsigned long long nv = ds->n_vrows + n;
-    ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
-  }
-  // (atomics: the Localizer lane's probe for the next batch may be inserting beside this)
-  if (snw) atomicAdd((unsigned long long*)&ds->new_w, snw);
-  if (snk) atomicAdd(&ds->n_keys, snk);
-  if (cap_host) {
-    cap_host[0] = ds->n_keys;
-    cap_host[1] = ds->n_vrows;
-  }
+  step_finalize_body<kFinNT>(f, red);
 }
 
 // the fused backward's striped {new_w, n_keys} folded into the state (k_step_finalize's first
@@ -396,7 +345,14 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
   prof_mark(c, 5);
 
-  if (job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0) {
+  const bool bwd_runs = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0;
+  const bool initv = bwd_runs && d > 0;
+  // the step's last work: folded into the InitV launch when one runs (its last block), else a
+  // kernel of its own
+  FinArgs fin;
+  fin.ds = c->ds; fin.bds = bds; fin.B = B; fin.initv_total = initv ? total : nullptr;
+  fin.d = d; fin.vcap = c->T.vcap; fin.loss_part = a.loss_part; fin.nparts = nblk;
+  if (bwd_runs) {
     BwdArgs g{};
     g.segstart = segstart; g.ds = bds; g.nseg_host = -1; g.segcol = nullptr;
     g.occ_row = occ_row; g.occ_x = occ_x; g.occ_rx = rowof; g.zpad = c->zpad;
@@ -418,20 +374,19 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);
-    const int rc = run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false);
-    if (rc != DFX_OK) return fold_stripes_on_error(c, rc);
   } else {
     prof_mark(c, 6);
   }
-  const bool initv = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 && d > 0;
-  unsigned long long* cap_host = nullptr;
   {
-    const int rc = cap_record_slot(c, &cap_host);
-    if (rc != DFX_OK)
-      return job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0 ? fold_stripes_on_error(c, rc) : rc;
+    const int rc = cap_record_slot(c, &fin.cap_host);
+    if (rc != DFX_OK) return bwd_runs ? fold_stripes_on_error(c, rc) : rc;
   }
-  hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(kFinNT), 0, c->stream, c->ds, bds, B,
-                     initv ? total : nullptr, d, c->T.vcap, a.loss_part, (int64_t)nblk, cap_host);
+  if (initv) {
+    const int rc = run_initv(c, -1, nnz, flags, total, segslot, bds, &c->ds->n_init, false, &fin);
+    if (rc != DFX_OK) return fold_stripes_on_error(c, rc);
+  } else {
+    hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(kFinNT), 0, c->stream, fin);
+  }
   DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
   DFX_TRY(cap_record_commit(c));
   prof_mark(c, 7);

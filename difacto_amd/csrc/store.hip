@@ -124,23 +124,61 @@ __global__ void k_initv_finalize(const uint32_t* total, int d, int64_t vcap, Dev
 // counts tile b's kIvTile flags, publishes the count and finds its prefix by the block-wide
 // decoupled look-back over the lower tiles' tagged words (lookback.h), then draws its keys' V
 // exactly as k_initv.
-// The last tile writes the total (k_step_finalize advances the seed and n_vrows by it).
+// The last tile writes the total; with fin.ds set the step's last work follows in this launch
+// (step_finalize_body: the seed and n_vrows advanced by the total, the progress, the capacity
+// guard's counts) — by block 0 when the gate is closed, else by the last block to finish, one
+// launch less per step (round 6).
 // 8192-key tiles (a thread's 32 flags as one bit mask), the requested keys listed kIvList at a
 // time: 4096-key tiles took 850 tickets at C3, ~9 us of serialised atomics.
 constexpr int kIvItems = 32, kIvTile = kStNT * kIvItems, kIvList = 4096;
+
+static_assert(kStNT == kFinNT, "the fused InitV's blocks run the step's finalize");
+
+__device__ void initv_onepass_body(const uint32_t* flags, uint32_t* total, const uint32_t* slot,
+                                   const Table& T, float scale, DevState* ds, const DevState* nds,
+                                   unsigned long long* status, int64_t n, uint32_t need);
 
 __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, uint32_t* total,
                                                          const uint32_t* slot, Table T,
                                                          float scale, DevState* ds,
                                                          const DevState* nds,
                                                          const uint32_t* gate,
-                                                         unsigned long long* status) {
-  __shared__ uint32_t lds[kStNT / kWave + 1];
-  __shared__ uint32_t s_lb[3 * kStNT / kWave];
-  if (*gate == 0u) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0u;
+                                                         unsigned long long* status, FinArgs fin) {
+  __shared__ double s_red[kFinNT / kWave];
+  __shared__ bool s_last;
+  const int64_t n = (int64_t)nds->u_count;
+  const uint32_t need = (uint32_t)((n + kIvTile - 1) / kIvTile);
+  if (*gate == 0u || need == 0) {  // nothing to draw: block 0 finalizes
+    if (blockIdx.x != 0) return;
+    if (threadIdx.x == 0)
+      __hip_atomic_store(total, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (fin.ds) {
+      __syncthreads();
+      step_finalize_body<kFinNT>(fin, s_red);
+    }
     return;
   }
+  if (blockIdx.x >= need) return;
+  initv_onepass_body(flags, total, slot, T, scale, ds, nds, status, n, need);
+  if (!fin.ds) return;
+  // every block that took a tile counts itself done; the last one finalizes the step (its
+  // draws read ds->seed / n_vrows, which the finalize advances).  No fence: the finalize reads
+  // nothing this launch wrote but the total (an agent-scope store and load), and a device-scope
+  // fence per block writes its XCD's L2 back — here full of the backward's dirty model lines
+  // (measured: with the fences C3 lost 2.7 % in every step that drew a V row)
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&ds->iv_done, 1u) == need - 1;
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(&ds->iv_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  step_finalize_body<kFinNT>(fin, s_red);
+}
+
+__device__ void initv_onepass_body(const uint32_t* flags, uint32_t* total, const uint32_t* slot,
+                                   const Table& T, float scale, DevState* ds, const DevState* nds,
+                                   unsigned long long* status, int64_t n, uint32_t need) {
+  __shared__ uint32_t lds[kStNT / kWave + 1];
+  __shared__ uint32_t s_lb[3 * kStNT / kWave];
   // tile by ticket, in the order blocks start: a block only waits on running ones.  Block index
   // order is not start order across XCDs, and the AUC lane's look-back sort can run beside this
   // kernel, so tile = block index could wait on a block that cannot be placed.  The
@@ -149,9 +187,6 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   // the nnz bound, and each ticket is a returning atomic on one word, ~11 ns apiece serialised
   // (DESIGN.md (d)); the blocks past the count leave at once, and the tickets still go to running
   // blocks in start order.
-  const int64_t n = (int64_t)nds->u_count;
-  const uint32_t need = (uint32_t)((n + kIvTile - 1) / kIvTile);
-  if (blockIdx.x >= need) return;
   __shared__ uint32_t s_tile;
   if (threadIdx.x == 0) {
     s_tile = atomicAdd(&ds->iv_ticket, 1u);
@@ -181,7 +216,8 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
   uint32_t tot;
   const uint32_t ex = block_excl_scan<kStNT>(cnt, lds, &tot);
   const uint32_t pre = block_lookback<kStNT>(status, tile, tag, tot, &ds->err, s_lb);
-  if (threadIdx.x == 0 && base + kIvTile >= n) *total = pre + tot;  // the last tile
+  if (threadIdx.x == 0 && base + kIvTile >= n)  // the last tile
+    __hip_atomic_store(total, pre + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tot == 0) return;  // block-uniform
   const int d = T.d;
   if (d > kIvMaxD) {  // (wide V: each thread draws its keys' rows in turn)
@@ -242,7 +278,8 @@ __global__ __launch_bounds__(kStNT) void k_initv_onepass(const uint32_t* flags, 
 
 // flags[0..n) -> InitV.  flags is scanned in place; total_dev receives the count.
 int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint32_t* total_dev,
-              const uint32_t* slot, const DevState* nds, const uint32_t* gate, bool finalize) {
+              const uint32_t* slot, const DevState* nds, const uint32_t* gate, bool finalize,
+              const FinArgs* fin) {
   if (c->P.V_dim <= 0 || n_bound <= 0) return DFX_OK;
   if (!nds) nds = c->ds;
   if (gate && n_host < 0 && !finalize) {  // the fused step
@@ -254,7 +291,7 @@ int run_initv(Context* c, int64_t n_host, int64_t n_bound, uint32_t* flags, uint
       DFX_HIP(hipMemsetAsync(ws.ivstat.p, 0, ws.ivstat.bytes, c->stream));
     hipLaunchKernelGGL(k_initv_onepass, dim3((unsigned)ntiles), dim3(kStNT), 0, c->stream, flags,
                        total_dev, slot, c->T, c->P.V_init_scale, c->ds, nds, gate,
-                       ws.ivstat.as<unsigned long long>());
+                       ws.ivstat.as<unsigned long long>(), fin ? *fin : FinArgs{});
     DFX_HIP(hipGetLastError());
     return DFX_OK;
   }

@@ -66,13 +66,20 @@ def test_localizer_full_c3(H):
 
 
 def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=True,
-         exact=False):
+         exact=False, drift=None):
     """exact: no key reaches a chunked (> kChunkOcc = 128 occurrences, csrc/internal.h) gradient
     sum, so predictions and the model must equal the oracle's bit for bit (sums in the
     reference's order, glibc expf); asserted per batch, so a change of the chunk threshold fails
-    here by name rather than as an unexplained bit mismatch"""
+    here by name rather than as an unexplained bit mismatch.
+    drift: after every step the model over the batch's keys is compared as a vector with the
+    reference's and with the exact trajectory's (the oracle with every gradient column summed in
+    double, sum64): ||device - ref|| / ||ref|| <= drift, and the device no farther from the exact
+    trajectory than the reference is (test_gpu_r3.py test_c5_model_drift_bound's form)"""
     c = H.Context(0, max_keys=max_keys, **cfg)
     up = O.Updater(**cfg)
+    ex = O.Updater(**cfg, sum64=1) if drift is not None else None
+    nrel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    rows = []
     for step, blk in enumerate(batches):
         if exact:
             _, cnt = np.unique(blk.ids, return_counts=True)
@@ -91,6 +98,20 @@ def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=Tr
         assert abs(p["loss"] - loss) <= 1e-4 * abs(loss), (step, p["loss"], loss)
         assert abs(p["auc"] - _auc_expect(blk.labels, opred, auc)) <= 1e-4 * blk.size, step
         assert p["nrows"] == blk.size
+        if ex is not None:
+            ex.train_step(blk.offs, blk.ids, blk.vals, blk.labels, push_cnt=push)
+            uniq, _, _ = O.localize(blk.offs, blk.ids)
+            v, l = H.Store(c).pull(c.tensor(uniq, torch.int64))
+            ov, ol = up.get(uniq)
+            xv, xl = ex.get(uniq)
+            assert np.array_equal(l.cpu().numpy(), ol) and np.array_equal(xl, ol), step
+            a, b, x = (t.astype(np.float64) for t in (v.cpu().numpy(), ov, xv))
+            rows.append((nrel(a, b), nrel(a, x), nrel(b, x)))
+    if ex is not None:
+        print("full-size model drift ||.||/||.|| (device-ref, device-exact, ref-exact):",
+              ["%.2e/%.2e/%.2e" % r for r in rows])
+        assert max(r[0] for r in rows) <= drift, rows
+        assert all(r[1] <= r[2] + 1e-8 for r in rows), rows
     s = H.Store(c).stats()
     assert s["n_keys"] == up.size() and s["seed"] == up.seed
     if check_model:
@@ -100,7 +121,8 @@ def _run(H, cfg, batches, n_cnt, max_keys, pred_rtol, model_rtol, check_model=Tr
         ov, ol = up.get(uniq)
         if cfg.get("V_dim", 0) > 0:
             assert np.array_equal(l.cpu().numpy(), ol)
-        assert close(v.cpu().numpy(), ov, rtol=model_rtol)
+        if model_rtol is not None:
+            assert close(v.cpu().numpy(), ov, rtol=model_rtol)
         if exact:
             assert np.array_equal(v.cpu().numpy().view(np.uint32),
                                   np.asarray(ov, np.float32).view(np.uint32))
@@ -130,14 +152,16 @@ def test_fused_full_c5(H):
     l1 = 1, l1_shrk): V is created lazily for the hot keys.  Hot keys' Xᵀ sums run in
     256-occurrence chunks combined in chunk order (reordered sums), so predictions after the
     first update and the model are compared within tolerance (Determinism).  The
-    drift itself is bounded against the exact (f64-sum) trajectory in test_gpu_r3.py
-    test_c5_model_drift_bound; this full-size run keeps close()'s elementwise 1e-3."""
+    model is held to the drift bound every step (the device within 1e-5 of the reference as a
+    vector, and no farther from the exact f64-sum trajectory than the reference is), not to an
+    elementwise tolerance: FTRL's L1 threshold turns a last-bit difference of z into w = 0 (round
+    6; was close()'s elementwise 1e-3)."""
     cfg = dict(V_dim=128, lr=.05, V_lr=.01)
     batches = [D.synthetic(10_000, 39, 1 << 24, zipf=1.1, seed=7000 + s) for s in range(4)]
     # step 0 reads the oracle's own (empty) model: north_star's 1e-5; after the first chunked
     # update the models differ by the reference's float rounding of hot keys' sums
     _run(H, cfg, batches, n_cnt=2, max_keys=1 << 20, pred_rtol=[RTOL, 1e-4, 1e-4, 1e-4],
-         model_rtol=1e-3)
+         model_rtol=None, drift=1e-5)
 
 
 def test_calcgrad_c5_chunked(H):

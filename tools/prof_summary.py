@@ -5,8 +5,10 @@ The timed window is the last N steps: it starts where the (N+1)-th-from-last ste
 `k_step_finalize` ended and stops where the last one ended.  Per kernel: dispatches per step,
 average duration, microseconds per step, and the busy fraction of the window.
 usage: prof_summary.py trace.csv N [fetch_pmc.csv write_pmc.csv]
-DFX_STEP_MARKER (default k_step_finalize; the sharded store: k_dist_worker_finalize, the split:
-k_split_worker_finalize) names the once-per-step kernel the window is anchored on;
+DFX_STEP_MARKER (default: k_step_finalize or k_initv_onepass — since round 6 a V_dim > 0 training
+step finalizes in its InitV launch; the sharded store: k_dist_worker_finalize, the split:
+k_split_worker_finalize; comma-separated alternatives) names the once-per-step kernel the window
+is anchored on;
 DFX_STEP_SKIP skips that many trailing steps (the bench's secondary schedule runs).
 """
 import collections
@@ -34,8 +36,8 @@ def main():
     rows = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
             for r in csv.DictReader(open(trace))]
     rows.sort()
-    marker = os.environ.get("DFX_STEP_MARKER", "k_step_finalize")
-    fin = [e for s, e, k in rows if marker in k]
+    markers = os.environ.get("DFX_STEP_MARKER", "k_step_finalize,k_initv_onepass").split(",")
+    fin = [e for s, e, k in rows if any(m in k for m in markers)]
     skip = int(os.environ.get("DFX_STEP_SKIP", "0"))
     if len(fin) < nsteps + 1 + skip:
         raise SystemExit("trace holds %d steps, need %d" % (len(fin), nsteps + 1 + skip))

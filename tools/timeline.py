@@ -10,14 +10,14 @@ def main():
     path = sys.argv[1]
     s0 = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 2
-    marker = sys.argv[4] if len(sys.argv) > 4 else "k_step_finalize"
+    marker = sys.argv[4] if len(sys.argv) > 4 else "k_step_finalize,k_initv_onepass"
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"],
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"],
                          r["Kernel_Name"].split("(")[0]))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if marker in r[3]]
+    ends = [i for i, r in enumerate(rows) if any(m in r[3] for m in marker.split(","))]
     lo = ends[s0 - 1] + 1 if s0 > 0 else 0
     hi = ends[s0 + n - 1] + 1
     t0 = rows[lo][0]
