@@ -191,7 +191,7 @@ def algorithmic_bytes_sharded(B, nnz, U, d):
     return fwd + bwd
 
 
-PMC_ROUND = "r5"
+PMC_ROUND = "r6"
 
 # Random 128-byte lines per second on MI355X in the step's own access patterns, measured alone
 # with cold caches (tools/membench/spanbench, profiles/r5/spanbench_cold.txt): the forward's
