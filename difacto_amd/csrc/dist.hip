@@ -958,7 +958,7 @@ extern "C" {
 
 int dfx_dist_record_floats(dfx_ctx* ctx) { return ctx ? rec_floats(ctx->c.P.V_dim) : -1; }
 
-#define DFX_CHECK_SLOT(slot) DFX_CHECK_ARG((slot) >= 0 && (slot) < kSlots, "dist: slot must be 0, 1 or 2")
+#define DFX_CHECK_SLOT(slot) DFX_CHECK_ARG((slot) >= 0 && (slot) < kSlots, "dist: slot must be 0 .. 3")
 
 // Localizer lane: Compact of the batch into the slot's buffers, then the owner splits, copied
 // to pinned memory; dfx_dist_localize_wait joins it on the host
@@ -1086,8 +1086,7 @@ int dfx_dist_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* recv_keys,
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks, "dist: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_TRY(pipeline_init(c));
-  DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1] &&
-                    !c->dist_initv_pending[2],
+  DFX_CHECK_ARG(!any_pending(c->dist_initv_pending),
                 "dist_owner_begin: finish the pending InitV first (dfx_dist_initv_local / _draw)");
   // this table serves one of nranks key ranges: hash keys by their position in the range
   DFX_TRY(table_set_ranges(c, nranks));
@@ -1201,8 +1200,7 @@ int dfx_dist_owner_push(dfx_ctx* ctx, int slot, const float* recv_grads) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_CHECK_SLOT(slot);
   Context* c = &ctx->c;
-  DFX_CHECK_ARG(!c->dist_initv_pending[0] && !c->dist_initv_pending[1] &&
-                    !c->dist_initv_pending[2],
+  DFX_CHECK_ARG(!any_pending(c->dist_initv_pending),
                 "dist_owner_push: finish the pending InitV first (dfx_dist_initv_local / _draw)");
   const int64_t R = c->dist_R[slot];
   if (R == 0 && !c->dist_sum) {

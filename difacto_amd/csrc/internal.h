@@ -97,7 +97,12 @@ constexpr int kMaxDistRanks = 64;  // sharded store (dist.hip)
 // step slots of the sharded stores (dist.hip, split.hip): two steps in flight when pipelined,
 // three in the split's 1-step-stale schedule (a step's owner state lives until its backward,
 // after the next step's forward, while the step after that localizes)
-constexpr int kSlots = 3;
+constexpr int kSlots = 4;  // per-step buffer sets of the sharded schedules (split_host.cc)
+inline bool any_pending(const bool (&v)[kSlots]) {
+  for (bool b : v)
+    if (b) return true;
+  return false;
+}
 constexpr int kOsSortTile = 4096;  // radix sort tile (sort.hip)
 constexpr int kOsDigits = 8;       // 8-bit digit positions of a u64 key
 constexpr int kOsParts = 16;       // partial digit-count copies (spread the atomics)
@@ -196,7 +201,7 @@ struct Context {
   Workspace ows[kSlots];
   DevState* ods[kSlots] = {};
   Workspace uws;  // the union of the workers' keys (dfx_dist_union)
-  int64_t dist_R[kSlots] = {}, dist_rows[kSlots] = {}, dist_U[kSlots] = {-1, -1, -1};
+  int64_t dist_R[kSlots] = {}, dist_rows[kSlots] = {}, dist_U[kSlots] = {-1, -1, -1, -1};
   std::vector<int64_t> dist_offs[kSlots];
   // owner segments of a slot not yet built: owner_begin leaves them to the pull, which
   // builds them and answers the pull in one pass (k_dist_segs_pull)

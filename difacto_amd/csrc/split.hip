@@ -341,7 +341,7 @@ using namespace dfx;
 
 extern "C" {
 
-#define DFX_SPLIT_SLOT(slot) DFX_CHECK_ARG((slot) >= 0 && (slot) < kSlots, "split: slot must be 0, 1 or 2")
+#define DFX_SPLIT_SLOT(slot) DFX_CHECK_ARG((slot) >= 0 && (slot) < kSlots, "split: slot must be 0 .. 3")
 
 int dfx_split_part_floats(dfx_ctx* ctx, int nranks) {
   return ctx && nranks >= 1 ? split_part_floats(ctx->c.P.V_dim, nranks) : -1;
@@ -421,8 +421,7 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   DFX_CHECK_ARG(nranks >= 1 && nranks <= kMaxDistRanks, "split: 1 <= nranks <= 64");
   Context* c = &ctx->c;
   DFX_CHECK_ARG(c->dist_sum, "split: needs push_agg=sum (one Update per key per step)");
-  DFX_CHECK_ARG(!c->split_initv_pending[0] && !c->split_initv_pending[1] &&
-                    !c->split_initv_pending[2],
+  DFX_CHECK_ARG(!any_pending(c->split_initv_pending),
                 "split_owner_begin: finish the pending InitV first (dfx_split_initv_*)");
   DFX_TRY(pipeline_init(c));
   int64_t R = 0, nnz = 0;
@@ -630,8 +629,7 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
   DFX_CHECK_ARG(ctx, "null ctx");
   DFX_SPLIT_SLOT(slot);
   Context* c = &ctx->c;
-  DFX_CHECK_ARG(!c->split_initv_pending[0] && !c->split_initv_pending[1] &&
-                    !c->split_initv_pending[2],
+  DFX_CHECK_ARG(!any_pending(c->split_initv_pending),
                 "split_owner_backward: finish the pending InitV first (dfx_split_initv_*)");
   const int64_t R = c->split_rows[slot], nnz = c->split_nnz[slot];
   const int d = c->P.V_dim;

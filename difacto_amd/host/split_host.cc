@@ -369,12 +369,14 @@ struct GpuSplitStore::Impl {
   uint64_t max_index;
   int N, L, d, PS, PX;
   int next_slot = 0;
-  // step slots: three when pipelined — step s + 1's partition and owner Localizer then wait
-  // only for step s - 2, and run beside step s's forward and backward (with two they waited for
-  // step s - 1's backward and sat in front of step s + 1's forward: ~0.2 ms of the split's N = 1
-  // step); the stale schedule needs three anyway (a step's owner state is held until its
-  // deferred backward while the step after next is localized); the library holds three
-  static constexpr int kSlotsMax = 3;
+  // step slots: four when pipelined.  Step t + 1's partition waits only for step t - 3 (its
+  // slot), so it is done when the host comes to issue t + 1's owner Localizer; the Localizer lane
+  // waits on the device for step t - 2 — it starts with step t - 1's forward, as the fused step's
+  // Localizer does, instead of when the host got the partition counts (~0.1-0.25 ms into step
+  // t - 1, behind the backward's blocks).  With two slots the partition waited for step t - 1's
+  // backward and sat in front of step t + 1's forward; the stale schedule needs three (a step's
+  // owner state is held until its deferred backward while the step after next is localized)
+  static constexpr int kSlotsMax = 4;
   int nslots = 2;
   std::vector<Buf> buf[kSlotsMax];  // [slot][local]
   std::vector<DBuf> icnt, iall;
@@ -403,7 +405,7 @@ struct GpuSplitStore::Impl {
 
   Impl(SplitTransport* tr, int pipe, uint64_t mi)
       : t(tr), pipelined(pipe != 0), stale(pipe == 2), max_index(mi) {
-    nslots = pipelined ? 3 : 2;
+    nslots = pipelined ? kSlotsMax : 2;
     N = t->nranks();
     L = t->nlocal();
     d = dfx_ctx_vdim(t->ctx(0));
@@ -555,8 +557,13 @@ struct GpuSplitStore::Impl {
       const dfx_batch& x = b[l];
       hipStream_t sl = lane ? Stream(l, 0) : Main(l);
       st[l] = sl;
-      // this slot's receive buffers are read by its previous step's main-stream work
-      if (lane) HipCheck(hipStreamWaitEvent(sl, slot_done[s][l], 0), "wait");
+      // this slot's receive buffers are read by its previous step's main-stream work; the lane
+      // starts with the forward of the step after the one three back (kSlotsMax above)
+      if (lane) {
+        HipCheck(hipStreamWaitEvent(sl, slot_done[s][l], 0), "wait");
+        if (nslots > 3) HipCheck(hipStreamWaitEvent(sl, slot_done[(s + nslots - 3) % nslots][l], 0),
+                                 "wait");
+      }
       // nnz per (owner, row), padded to M rows per owner
       void* rc = u.rc.p;
       if (x.size < M) {
@@ -871,6 +878,10 @@ struct GpuSplitStore::Impl {
     }
     for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(done[l], Main(l)), "record");
     inflight.push_back(done);
+  }
+
+  // the run-ahead bound: the host waits until at most kAhead issued steps are unfinished
+  void Throttle() {
     const auto t0 = std::chrono::steady_clock::now();
     while ((int)inflight.size() > kAhead) {
       for (auto e : inflight.front()) HipCheck(hipEventSynchronize(e), "sync");
@@ -896,8 +907,11 @@ struct GpuSplitStore::Impl {
       return;
     }
     if (have_pending) Run(pending);
+    // the next step's partition counts and owner Localizer before the wait on the run-ahead
+    // bound, so that its lane is queued behind its device-side gate (kSlotsMax above)
     pending = Begin(s, b, job, want_cnt, preds, true);
     have_pending = true;
+    Throttle();
   }
 
   void Flush() {
