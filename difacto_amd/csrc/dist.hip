@@ -737,7 +737,8 @@ __global__ __launch_bounds__(kIvrNT) void k_initv_rank_count(const uint32_t* fla
 __global__ __launch_bounds__(kIvrNT) void k_initv_rank_draw(
     const uint32_t* flags, int64_t bound, const uint32_t* nuniq, const uint32_t* ftotal,
     const uint32_t* ts, const uint32_t* segslot, const int64_t* Fall, int rank, int nranks,
-    Table T, float scale, DevState* ds, int64_t vcap, uint32_t* fcount, unsigned* ticket) {
+    Table T, float scale, DevState* ds, int64_t vcap, uint32_t* fcount, unsigned* ticket,
+    unsigned long long* cap_host) {
   __shared__ uint32_t lds[kIvrNT / kWave + 1];
   __shared__ uint32_t s_st[kIvrNT], s_vr[kIvrNT], s_A[kIvMaxD], s_C[kIvMaxD];
   __shared__ bool s_last;
@@ -747,7 +748,13 @@ __global__ __launch_bounds__(kIvrNT) void k_initv_rank_draw(
     if (h < rank) off += Fall[h];
   }
   if (tot == 0) {  // no owner draws: nothing advances (the gate's reset only)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *fcount = 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      *fcount = 0u;
+      if (cap_host) {  // the capacity guard's counts (pinned host words)
+        cap_host[0] = ds->n_keys;
+        cap_host[1] = ds->n_vrows;
+      }
+    }
     return;
   }
   const uint32_t F = *ftotal;
@@ -810,6 +817,10 @@ __global__ __launch_bounds__(kIvrNT) void k_initv_rank_draw(
   const unsigned long long nv = ds->n_vrows + F;
   if (nv > (unsigned long long)vcap) atomicOr(&ds->err, kErrPoolFull);
   ds->n_vrows = nv > (unsigned long long)vcap ? (unsigned long long)vcap : nv;
+  if (cap_host) {
+    cap_host[0] = ds->n_keys;
+    cap_host[1] = ds->n_vrows;
+  }
 }
 
 int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32_t* nuniq,
@@ -825,13 +836,14 @@ int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32
 
 int initv_rank_draw(Context* c, const Lane& L, const uint32_t* flags, const uint32_t* ftotal,
                     const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
-                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount) {
+                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount,
+                    unsigned long long* cap_host) {
   const int64_t ntiles = std::max<int64_t>(1, (bound + kIvrTile - 1) / kIvrTile);
   DFX_TRY(L.ws->tiles.ensure(sizeof(uint32_t) * (ntiles + 1)));
   const dim3 g((unsigned)std::min<int64_t>(ntiles, kIvrGrid));
   hipLaunchKernelGGL(k_initv_rank_draw, g, dim3(kIvrNT), 0, L.stream, flags, bound, nuniq, ftotal,
                      L.ws->tiles.as<uint32_t>(), segslot, counts_all, rank, nranks, c->T,
-                     c->P.V_init_scale, c->ds, c->T.vcap, fcount, &L.ds->ivr_ticket[1]);
+                     c->P.V_init_scale, c->ds, c->T.vcap, fcount, &L.ds->ivr_ticket[1], cap_host);
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -1060,6 +1072,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  ++c->auc_seq;
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {
     // every gradient record is written whole, the live slot carrying whether this worker
@@ -1075,6 +1088,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   }
   // the slot's Localizer buffers may be refilled once the main stream is past this point
   DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
+  c->slot_free[slot] = nullptr;
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }

@@ -226,6 +226,14 @@ struct Context {
   DevState* ads = nullptr;
   hipEvent_t ev_in = nullptr, ev_fwd = nullptr, ev_auc = nullptr;
   hipEvent_t ev_loc[kSlots] = {}, ev_free[kSlots] = {};
+  // per fused-step parity / split slot: the event after which its buffers are free (the
+  // capacity guard's step event when that is recorded at the same point: one record, not two);
+  // null: ev_free
+  hipEvent_t slot_free[kSlots] = {};
+  // AUC lane records (ev_auc), counted; a split slot's Localizer lane that joined the AUC lane
+  // notes the count, and its combine skips its own wait when no AUC was issued since
+  uint64_t auc_seq = 0;
+  uint64_t split_auc_joined[kSlots] = {};
   int parity = 0;
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)
   int autogrow = 1;   // grow the table / V pool before a step could overflow them (kwarg)
@@ -296,6 +304,15 @@ inline void lane_mark(Context* c, int m, hipStream_t st) {
 inline void prof_mark(Context* c, int m) {
   if (c->prof_n < c->prof_max && (c->prof_mask >> m & 1u))
     (void)hipEventRecord(c->prof_ev[(size_t)c->prof_n * kProfMarks + m], c->stream);
+}
+// an event record between two kernels costs the stream ~5 us (tools/membench/waitbench.hip):
+// phase mark m when it is recorded, else `other`, as one record; -> the event recorded
+inline hipEvent_t prof_mark_or(Context* c, int m, hipEvent_t other) {
+  hipEvent_t e = other;
+  if (c->prof_n < c->prof_max && (c->prof_mask >> m & 1u))
+    e = c->prof_ev[(size_t)c->prof_n * kProfMarks + m];
+  (void)hipEventRecord(e, c->stream);
+  return e;
 }
 
 // ---- cross-file launchers --------------------------------------------------------------
@@ -520,7 +537,7 @@ int cap_record(Context* c);
 // cap_record in two halves: the pinned ring entry for {n_keys, n_vrows} (NULL: no guard), to be
 // written by the caller's last kernel on the context stream, then the entry's event
 int cap_record_slot(Context* c, unsigned long long** slot);
-int cap_record_commit(Context* c);
+int cap_record_commit(Context* c, hipEvent_t* recorded = nullptr);
 void cap_release(Context* c);
 // at a sync point (the stream is idle): grow the table once its load passes 0.5
 int store_maybe_grow(Context* c);
@@ -534,7 +551,8 @@ int initv_rank_count(const Lane& L, uint32_t* flags, int64_t bound, const uint32
                      uint32_t* ftotal, const uint32_t* gate, int64_t* count_dev);
 int initv_rank_draw(Context* c, const Lane& L, const uint32_t* flags, const uint32_t* ftotal,
                     const uint32_t* nuniq, int64_t bound, const uint32_t* segslot,
-                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount);
+                    const int64_t* counts_all, int rank, int nranks, uint32_t* fcount,
+                    unsigned long long* cap_host = nullptr);  // (the capacity guard's counts)
 // Update(kFeaCount) of a localized batch's segments (count = segment length), InitV requests
 // into flags; no draws (store.hip)
 int push_cnt_seg_flags(Context* c, const Lane& L, int64_t n_bound, const uint32_t* segstart,

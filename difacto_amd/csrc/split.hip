@@ -452,7 +452,8 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
     // library's lane, which the caller made wait for the exchange); the slot's buffers are free
     // once the main stream finished the step that used them before
     OL.stream = c->loc_stream;
-    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[slot], 0));
+    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->slot_free[slot] ? c->slot_free[slot]
+                                                                  : c->ev_free[slot], 0));
   }
   Workspace& ows = c->ows[slot];
   DFX_TRY(loc_reserve(ows, nnz, OL.stream));
@@ -497,7 +498,14 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   }
   c->split_lane[slot] = lane != 0;
   c->split_job[slot] = job_type;
-  if (lane) DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
+  if (lane) {
+    // the combine writes the AUC lane's snapshot once the AUC issued before it is done: the
+    // lane joins that AUC before it hands the slot over (the owner forward waits for the lane),
+    // so the main stream waits on one event less per step (~4 us, tools/membench/waitbench.hip)
+    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_auc, 0));
+    c->split_auc_joined[slot] = c->auc_seq;
+    DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
+  }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -538,9 +546,13 @@ int dfx_split_owner_forward_rows(dfx_ctx* ctx, int slot, float* part_out, int nr
     DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, true));
   }
   if (!last) return DFX_OK;
-  // a step without a backward is done with the slot (and the table) here
-  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
-  if (c->split_job[slot] != DFX_JOB_TRAINING) DFX_TRY(cap_record(c));
+  // a step without a backward is done with the slot (and the table) here (a training step's
+  // InitV draw, or its backward at V_dim 0, frees it: an event record costs the stream ~5 us)
+  if (c->split_job[slot] != DFX_JOB_TRAINING) {
+    DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
+    c->slot_free[slot] = nullptr;
+    DFX_TRY(cap_record(c));
+  }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -584,7 +596,10 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
   if (first) {
     DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
-    DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+    // (joined already when this slot's Localizer lane waited for the latest AUC: the owner
+    // forward before this combine waited for that lane)
+    if (!(c->split_lane[slot] && c->split_auc_joined[slot] == c->auc_seq))
+      DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
   }
   const int64_t r1 = lo + len < B ? lo + len : B;
   if (r1 > lo) {
@@ -613,6 +628,7 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  ++c->auc_seq;
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1024), 0, c->stream, loss_part, nb,
                      c->ds, B);
   DFX_HIP(hipGetLastError());
@@ -664,10 +680,13 @@ int dfx_split_owner_backward(dfx_ctx* ctx, int slot, const float* pxv) {
     c->split_initv_pending[slot] = true;
     c->split_initv_gated[slot] = true;
   }
-  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
-  // the store's counts after this step (capacity guard, cap_check), once its updates are in:
-  // here at V_dim 0, after the ranked InitV draws otherwise
-  if (d == 0) DFX_TRY(cap_record(c));
+  // the slot is free and the store's counts final (capacity guard, cap_check) here at V_dim 0,
+  // after the ranked InitV draws otherwise
+  if (d == 0) {
+    DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));
+    c->slot_free[slot] = nullptr;
+    DFX_TRY(cap_record(c));
+  }
   DFX_HIP(hipGetLastError());
   return DFX_OK;
 }
@@ -715,14 +734,23 @@ int dfx_split_initv_draw(dfx_ctx* ctx, int slot, const int64_t* counts_all_dev, 
   Context* c = &ctx->c;
   const Lane OL = split_owner_lane(c, slot);
   const bool pend = c->split_initv_pending[slot] && c->split_nnz[slot] > 0;
+  const bool after_backward = c->split_initv_gated[slot];
+  // after a backward: the draw's last block writes the store's counts for the capacity guard
+  // (no copy on the stream), and the guard's event frees the slot too (one record)
+  unsigned long long* cap = nullptr;
+  if (after_backward) DFX_TRY(cap_record_slot(c, &cap));
   DFX_TRY(initv_rank_draw(c, OL, c->ows[slot].oflags.as<uint32_t>(), &OL.ds->totals[2],
                           &OL.ds->u_count, pend ? c->split_nnz[slot] : 0,
                           c->ows[slot].slot.as<uint32_t>(), counts_all_dev, rank, nranks,
-                          &c->ds->n_init));
-  const bool after_backward = c->split_initv_gated[slot];
+                          &c->ds->n_init, cap));
   c->split_initv_pending[slot] = false;
-  DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));  // the slot's last reader
-  if (after_backward) DFX_TRY(cap_record(c));
+  hipEvent_t fe = nullptr;
+  if (cap) DFX_TRY(cap_record_commit(c, &fe));
+  if (!fe) {
+    DFX_HIP(hipEventRecord(c->ev_free[slot], c->stream));  // the slot's last reader
+    fe = c->ev_free[slot];
+  }
+  c->slot_free[slot] = fe;
   return DFX_OK;
 }
 

@@ -260,7 +260,7 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   // once the main stream finished the batch that used them before
   DFX_HIP(hipEventRecord(c->ev_in, c->has_in_stream ? c->in_stream : c->stream));
   DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_in, 0));
-  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_free[k], 0));
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->slot_free[k] ? c->slot_free[k] : c->ev_free[k], 0));
   // Localizer::Compact: sorted unique keys (segments in key order, the order Update walks
   // keys in — InitV draws — and, per key, the (row, nnz) order of its gradient sums)
   LocOut o;
@@ -287,6 +287,11 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     c->loc_done[k] = true;
   }
   lane_mark(c, 1, c->loc_stream);
+  // the forward writes the AUC lane's snapshot of (pred, label), whose buffers are free once the
+  // AUC that last read them is done: the lane joins that AUC before it hands its batch over, so
+  // the main stream waits on one event instead of two (a cross-stream wait costs the stream that
+  // waits ~4 us, tools/membench/waitbench.hip; the AUC ends long before this lane does)
+  DFX_HIP(hipStreamWaitEvent(c->loc_stream, ev_auc_mine, 0));
   DFX_HIP(hipEventRecord(c->ev_loc[k], c->loc_stream));
 
   // Get over the sorted unique keys (find-or-insert + pull); a count push goes in between
@@ -324,26 +329,30 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   a.d = d; a.label = b->label; a.rw = b->weight; a.pred = pred; a.p_out = ws.p.as<float>();
   a.XVp = ws.XVp.as<float>(); a.xs = xvp_stride(c);
   a.loss_part = ws.dscratch.as<double>() + 8;
-  // the forward writes the AUC lane's snapshot of (pred, label): the lane's buffers are free
-  // once the previous AUC is done.  (A last-block loss reduction inside the forward cost more
-  // than the launch it saves: the device-scope fence of each block writes back its XCD's L2.)
+  // the forward writes the AUC lane's snapshot of (pred, label) (free: ev_loc joined the AUC
+  // that last read it).  (A last-block loss reduction inside the forward cost more than the
+  // launch it saves: the device-scope fence of each block writes back its XCD's L2.)
   a.auc_key = aw.ak0.as<uint32_t>();
   a.auc_lab = aw.av0.as<uint32_t>();
-  DFX_HIP(hipStreamWaitEvent(c->stream, ev_auc_mine, 0));
   int nblk = 0;
   DFX_TRY(launch_fwd_fused(a, c->stream, &nblk, true));
   prof_mark(c, 4);
   // (the forward's loss partials are summed by k_step_finalize, the step's last kernel)
 
-  // ---- aux lane: AUC of this batch's predictions, beside the backward
-  DFX_HIP(hipEventRecord(c->ev_fwd, c->stream));
-  DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
-  lane_mark(c, 2, c->aux_stream);
-  if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
-  lane_mark(c, 3, c->aux_stream);
-  DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
-  DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
-  prof_mark(c, 5);
+  // ---- aux lane: AUC of this batch's predictions, beside the backward.  Started from the
+  // event of phase mark 5 (the backward's start, after the chunk kernels): one record where a
+  // separate ev_fwd and mark cost ~5 us of the main stream each (tools/membench/waitbench.hip)
+  auto auc_lane = [&]() -> int {
+    const hipEvent_t e = prof_mark_or(c, 5, c->ev_fwd);
+    DFX_HIP(hipStreamWaitEvent(c->aux_stream, e, 0));
+    lane_mark(c, 2, c->aux_stream);
+    if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
+    lane_mark(c, 3, c->aux_stream);
+    DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
+    ++c->auc_seq;
+    DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
+    return DFX_OK;
+  };
 
   const bool bwd_runs = job_type == DFX_JOB_TRAINING && B > 0 && nnz > 0;
   const bool initv = bwd_runs && d > 0;
@@ -371,10 +380,12 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
       g.live_part = ws.live.as<uint2>();
     }
     DFX_TRY(launch_bwd_chunks(g, max_chunks(nnz), c->stream, true));
+    DFX_TRY(auc_lane());
     DFX_TRY(launch_bwd_fused(g, nnz, c->stream, c->bwd_lds));
     if (count_live) DFX_TRY(sum_live(g.live_part, nbb, c->ds, c->stream));
     prof_mark(c, 6);
   } else {
+    DFX_TRY(auc_lane());
     prof_mark(c, 6);
   }
   {
@@ -387,8 +398,15 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
   } else {
     hipLaunchKernelGGL(k_step_finalize, dim3(1), dim3(kFinNT), 0, c->stream, fin);
   }
-  DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
-  DFX_TRY(cap_record_commit(c));
+  // this parity's buffers are free past here: the capacity guard's step event when it records
+  // one, else ev_free (one record, not two)
+  hipEvent_t fe = nullptr;
+  DFX_TRY(cap_record_commit(c, &fe));
+  if (!fe) {
+    DFX_HIP(hipEventRecord(c->ev_free[k], c->stream));
+    fe = c->ev_free[k];
+  }
+  c->slot_free[k] = fe;
   prof_mark(c, 7);
   if (c->prof_n < c->prof_max) ++c->prof_n;
   DFX_HIP(hipGetLastError());
@@ -432,9 +450,10 @@ extern "C" int dfx_prof_enable_marks(dfx_ctx* ctx, int max_steps, unsigned mask)
   return DFX_OK;
 }
 
-// ms[7]: summed milliseconds of localize (wait), probe+pull, feacnt, forward, eval + AUC
-// snapshot, backward+update, initv+finalize over the recorded steps; *n_steps their count; *mean_u the mean U per step
-// over all dfx_train_step calls since the last read.  Resets the recording.
+// ms[7]: summed milliseconds of localize (wait), probe+pull, feacnt, forward, eval (the AUC
+// lane's launch and, in a training step, the chunk kernels), backward+update, initv+finalize
+// over the recorded steps; *n_steps their count; *mean_u the mean U per step over all
+// dfx_train_step calls since the last read.  Resets the recording.
 // after dfx_prof_read: out[4] = mean ms of the Localizer lane per batch, of its start after
 // the context stream reached that batch (negative: it ran ahead), of its end after that point
 // (positive: the exposed wait), and of the AUC lane

@@ -713,11 +713,13 @@ int cap_record_slot(Context* c, unsigned long long** slot) {
 }
 
 // the counts of the slot cap_record_slot returned are written by work already on the stream
-int cap_record_commit(Context* c) {
+int cap_record_commit(Context* c, hipEvent_t* recorded) {
+  if (recorded) *recorded = nullptr;
   if (!c->autogrow) return DFX_OK;
   CapGuard& g = c->capg;
   const int i = g.head;
   DFX_HIP(hipEventRecord(g.ev[i], c->stream));
+  if (recorded) *recorded = g.ev[i];  // (re-recorded kCapRing steps later)
   g.enq_at[i] = g.enq_total;
   g.head = (g.head + 1) % kCapRing;
   ++g.count;

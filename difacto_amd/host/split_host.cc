@@ -382,7 +382,9 @@ struct GpuSplitStore::Impl {
   std::vector<DBuf> icnt, iall;
   std::vector<hipEvent_t> slot_done[kSlotsMax];  // [slot][local]: the main streams are done
   Graveyard grave;  // outgrown step buffers, freed after the device is idle
-  std::deque<std::vector<hipEvent_t>> inflight;
+  // the issued, unfinished steps' events: the slot's own slot_done (not owned), or events of
+  // their own (the stale schedule records slot_done later)
+  std::deque<std::pair<std::vector<hipEvent_t>, bool>> inflight;
   std::vector<std::vector<hipEvent_t>> spare;
   bool have_pending = false;
   Step pending;
@@ -451,7 +453,8 @@ struct GpuSplitStore::Impl {
       for (auto& v : *ev)
         for (auto e : v) (void)hipEventDestroy(e);
     for (auto& v : inflight)
-      for (auto e : v) (void)hipEventDestroy(e);
+      if (v.second)
+        for (auto e : v.first) (void)hipEventDestroy(e);
     for (auto& v : spare)
       for (auto e : v) (void)hipEventDestroy(e);
     for (auto& s : slot_done)
@@ -868,6 +871,10 @@ struct GpuSplitStore::Impl {
     if (!stale)
       for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(slot_done[s][l], Main(l)), "record");
     if (!pipelined) return;
+    if (!stale) {  // the slot's event is the step's (an event record costs the stream ~5 us)
+      inflight.emplace_back(slot_done[s], false);
+      return;
+    }
     std::vector<hipEvent_t> done;
     if (!spare.empty()) {
       done = spare.back();
@@ -877,15 +884,15 @@ struct GpuSplitStore::Impl {
       for (auto& e : done) HipCheck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
     }
     for (int l = 0; l < L; ++l) HipCheck(hipEventRecord(done[l], Main(l)), "record");
-    inflight.push_back(done);
+    inflight.emplace_back(done, true);
   }
 
   // the run-ahead bound: the host waits until at most kAhead issued steps are unfinished
   void Throttle() {
     const auto t0 = std::chrono::steady_clock::now();
     while ((int)inflight.size() > kAhead) {
-      for (auto e : inflight.front()) HipCheck(hipEventSynchronize(e), "sync");
-      spare.push_back(inflight.front());
+      for (auto e : inflight.front().first) HipCheck(hipEventSynchronize(e), "sync");
+      if (inflight.front().second) spare.push_back(inflight.front().first);
       inflight.pop_front();
     }
     throttle_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
