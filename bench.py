@@ -522,6 +522,10 @@ def main():
     bwd_ms = phases["backward_update"]
     prog = H.progress(ctx)
     window = step_window(torch, dev, world, batches, lambda bt: step(bt, False))
+    # the per-step counters restart here: the live-V counts below are the diagnostic pass's
+    # alone, and so must be the step count they are divided by (the window's steps counted
+    # none of them: a mean over both halved them, and with them the roofline's bytes)
+    H.prof_counts(ctx)
     # diagnostic pass (untimed): every phase and the lanes, over the same batches again
     H.prof_enable(ctx, len(batches))
     for bt in batches:
