@@ -465,16 +465,13 @@ def test_bench_two_ranks_gloo(collective, sync):
     the test box's GPU): one JSON line from rank 0, whole-job throughput over both ranks"""
     import json
     import os
-    import socket
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    # (--standalone: the launcher binds its rendezvous port itself — a port picked here and
+    # closed again can be taken before the launcher binds it: EADDRINUSE)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--standalone", "--local-addr", "127.0.0.1", "bench.py", "--gpus", "2",
            "--steps", "3", "--warmup", "1", "--batch", "20000", "--key-bits", "20",
            "--backend", "gloo", "--no-cpu-baseline", "--collective", collective] + (
                ["--sync"] if sync else [])
@@ -597,7 +594,6 @@ def test_bench_rccl_collectives_at_world_one(collective):
     Python) train identically."""
     import json
     import os
-    import socket
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -605,13 +601,11 @@ def test_bench_rccl_collectives_at_world_one(collective):
     drivers = ("cpp", "py") if collective == "split" else ("py",)
     for driver in drivers:
         for force in (False, True):
-            s = socket.socket()
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-            s.close()
+            # (--standalone: the launcher binds its rendezvous port itself; a port picked here
+            # and closed again was once taken first: EADDRINUSE)
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                   "--nproc-per-node", "1", "--master-addr", "127.0.0.1", "--master-port",
-                   str(port), "bench.py", "--sharded", "--steps", "4", "--warmup", "1",
+                   "--nproc-per-node", "1", "--standalone", "--local-addr", "127.0.0.1",
+                   "bench.py", "--sharded", "--steps", "4", "--warmup", "1",
                    "--batch", "20000", "--key-bits", "20", "--no-cpu-baseline", "--collective",
                    collective, "--driver", driver] + (["--force-collectives"] if force else [])
             r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6: the fused step's chunk plan and chunk kernels only when the batch two back on the
+# same parity had a long segment (host-visible pinned flag, read after that batch's Localizer):
+# the GPU tests from test_gpu_r6 on (the ones before passed on the r6t box), then ABBA against
+# build/ab (HEAD before) at the driver command for C3, B = 10^4,
+# C2 and C5
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" && mkdir -p gpurun_out/r6u
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_r6.py tests/test_gpu_split.py tests/test_gpu_store_layout.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r6u/tests.log 2>&1 || { tail -30 gpurun_out/r6u/tests.log; exit 1; }
+tail -2 gpurun_out/r6u/tests.log
+TAG=r6u_c3 BENCH_ARGS="--steps 20 --warmup 5" bash tools/abba.sh || exit 1
+TAG=r6u_b1e4 BENCH_ARGS="--steps 20 --warmup 5 --batch 10000" bash tools/abba.sh || exit 1
+TAG=r6u_c2 ROUNDS=1 BENCH_ARGS="--config c2 --steps 20 --warmup 5" bash tools/abba.sh || exit 1
+TAG=r6u_c5 ROUNDS=1 BENCH_ARGS="--config c5 --steps 20 --warmup 5" bash tools/abba.sh || exit 1
