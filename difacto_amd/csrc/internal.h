@@ -220,7 +220,7 @@ struct Context {
   Workspace bws[kSlots];  // [0], [1]: also the fused step's Localizer parities
   DevState* bds[kSlots] = {};
   Workspace aws;
-  Workspace aws_alt;  // the other parity's AUC snapshot (fused step, B <= kAucBlockMax)
+  Workspace aws_alt;  // the other parity's AUC snapshot (fused step)
   int auc_par = 0;
   hipEvent_t ev_auc_p[2] = {};  // the AUC that last read each parity's snapshot
   DevState* ads = nullptr;

@@ -90,11 +90,13 @@ int auc_reserve(Workspace& w, int64_t rows, hipStream_t st) {
   return DFX_OK;
 }
 
-// the fused step's AUC snapshot double-buffered at this batch size: at B <= kAucBlockMax the
-// one-block AUC (~94 us beside the backward) outlasts the rest of a small step, and a forward
-// then waits only for the AUC of two steps back (B = 10^4: 58.6 / 61.6 -> 68.0 / 68.8 M ex/s);
-// at B = 10^5 always-on was a tie (measured in round 4; the kwarg auc_db pruned in round 6)
-static bool auc_db_on(const Context*, int64_t rows) { return rows <= kAucBlockMax; }
+// the fused step's AUC snapshot double-buffered: a forward waits (through the Localizer lane's
+// join) only for the AUC of two steps back.  At B <= kAucBlockMax the one-block AUC (~94 us
+// beside the backward) outlasts the rest of a small step (B = 10^4: 58.6 / 61.6 -> 68.0 / 68.8
+// M ex/s, round 4); since round 6 at every size (two boxes, ABBA, driver command: C2 200.6 ->
+// 206.1 and 202.0 -> 207.4, C3 132.0 -> 130.7 (one outlier) and 140.2 -> 142.0, C5 a tie;
+// round 4 had measured B = 10^5 a tie with the wait on the main stream)
+static bool auc_db_on(const Context*, int64_t) { return true; }
 
 int step_reserve(Context* c, int64_t rows, int64_t nnz) {
   DFX_TRY(pipeline_init(c));
