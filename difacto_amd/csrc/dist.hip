@@ -1072,6 +1072,8 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  // (snapshot buffer 0's last reader, for a fused step of this context that writes it next)
+  DFX_HIP(hipEventRecord(c->ev_auc_p[0], c->aux_stream));
   ++c->auc_seq;
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {

@@ -628,6 +628,8 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
+  // (snapshot buffer 0's last reader, for a fused step of this context that writes it next)
+  DFX_HIP(hipEventRecord(c->ev_auc_p[0], c->aux_stream));
   ++c->auc_seq;
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1024), 0, c->stream, loss_part, nb,
                      c->ds, B);
