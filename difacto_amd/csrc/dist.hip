@@ -1074,7 +1074,7 @@ int dfx_dist_fwd_bwd(dfx_ctx* ctx, int slot, const dfx_batch* b, const float* pu
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
   // (snapshot buffer 0's last reader, for a fused step of this context that writes it next)
   DFX_HIP(hipEventRecord(c->ev_auc_p[0], c->aux_stream));
-  ++c->auc_seq;
+  ++c->auc_seq_p[0];
   hipLaunchKernelGGL(k_dist_worker_finalize, dim3(1), dim3(1), 0, c->stream, c->ds, B);
   if (train) {
     // every gradient record is written whole, the live slot carrying whether this worker

@@ -230,9 +230,13 @@ struct Context {
   // capacity guard's step event when that is recorded at the same point: one record, not two);
   // null: ev_free
   hipEvent_t slot_free[kSlots] = {};
-  // AUC lane records (ev_auc), counted; a split slot's Localizer lane that joined the AUC lane
-  // notes the count, and its combine skips its own wait when no AUC was issued since
-  uint64_t auc_seq = 0;
+  // the AUC snapshot's two buffers (aws, aws_alt): records of each one's last reader (ev_auc_p),
+  // counted; the split combine's alternation (the next step's buffer, this step's); the buffer
+  // a split slot's Localizer lane joined and its count then (the combine skips its own wait when
+  // no AUC read that buffer since)
+  uint64_t auc_seq_p[2] = {};
+  int split_auc_par = 0, split_auc_cur = 0;
+  int split_auc_joined_par[kSlots] = {};
   uint64_t split_auc_joined[kSlots] = {};
   int parity = 0;
   long bwd_lds = -1;  // LDS bytes reserved per fused-backward block (kwarg bwd_lds; -1 default)

@@ -499,11 +499,15 @@ int dfx_split_owner_begin(dfx_ctx* ctx, int slot, const uint64_t* keys, const fl
   c->split_lane[slot] = lane != 0;
   c->split_job[slot] = job_type;
   if (lane) {
-    // the combine writes the AUC lane's snapshot once the AUC issued before it is done: the
-    // lane joins that AUC before it hands the slot over (the owner forward waits for the lane),
-    // so the main stream waits on one event less per step (~4 us, tools/membench/waitbench.hip)
-    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_auc, 0));
-    c->split_auc_joined[slot] = c->auc_seq;
+    // the combine writes the AUC lane's snapshot buffer (two, alternating) once the AUC that last
+    // read it is done: the lane joins that AUC before it hands the slot over (the owner forward
+    // waits for the lane), so the main stream waits on one event less per step (~4 us,
+    // tools/membench/waitbench.hip).  The buffer is the next combine's when the driver begins a
+    // step after the previous step's combine (split_host.cc); else the combine waits itself
+    const int p = c->split_auc_par;
+    DFX_HIP(hipStreamWaitEvent(c->loc_stream, c->ev_auc_p[p], 0));
+    c->split_auc_joined_par[slot] = p;
+    c->split_auc_joined[slot] = c->auc_seq_p[p];
     DFX_HIP(hipEventRecord(c->ev_loc[slot], c->loc_stream));
   }
   DFX_HIP(hipGetLastError());
@@ -592,19 +596,27 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   // the scratch keeps in front
   if (first) DFX_TRY(ws.dscratch.ensure((size_t)(nb + 16) * 8));
   double* loss_part = ws.dscratch.as<double>() + 8;
-  // the AUC lane's snapshot buffers are free once its previous AUC is done
-  const Lane AL{c->aux_stream, &c->aws, c->ads, &c->ds->err};
+  // the AUC lane's snapshot: two buffers, alternating by step, each free once the AUC that last
+  // read it is done — the AUC of two steps back (as the fused step's, step.hip auc_db_on)
   if (first) {
-    DFX_TRY(auc_reserve(c->aws, B, c->aux_stream));
-    // (joined already when this slot's Localizer lane waited for the latest AUC: the owner
-    // forward before this combine waited for that lane)
-    if (!(c->split_lane[slot] && c->split_auc_joined[slot] == c->auc_seq))
-      DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc, 0));
+    c->split_auc_cur = c->split_auc_par;
+    c->split_auc_par ^= 1;
+  }
+  const int ap = c->split_auc_cur;
+  Workspace& aw = ap ? c->aws_alt : c->aws;
+  const Lane AL{c->aux_stream, &aw, c->ads, &c->ds->err};
+  if (first) {
+    DFX_TRY(auc_reserve(aw, B, c->aux_stream));
+    // (joined already when this slot's Localizer lane waited for that buffer's last reader and
+    // no AUC read the buffer since: the owner forward before this combine waited for the lane)
+    if (!(c->split_lane[slot] && c->split_auc_joined_par[slot] == ap &&
+          c->split_auc_joined[slot] == c->auc_seq_p[ap]))
+      DFX_HIP(hipStreamWaitEvent(c->stream, c->ev_auc_p[ap], 0));
   }
   const int64_t r1 = lo + len < B ? lo + len : B;
   if (r1 > lo) {
-    uint32_t* ak = c->aws.ak0.as<uint32_t>();
-    uint32_t* al = c->aws.av0.as<uint32_t>();
+    uint32_t* ak = aw.ak0.as<uint32_t>();
+    uint32_t* al = aw.av0.as<uint32_t>();
     const dim3 grid((unsigned)((r1 - lo + rpb - 1) / rpb));
     double* lp = loss_part + lo / rpb;
 #define DFX_COMBINE(GG)                                                                        \
@@ -628,9 +640,8 @@ int dfx_split_combine_rows(dfx_ctx* ctx, int slot, const dfx_batch* b, const flo
   DFX_HIP(hipStreamWaitEvent(c->aux_stream, c->ev_fwd, 0));
   DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
   DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));
-  // (snapshot buffer 0's last reader, for a fused step of this context that writes it next)
-  DFX_HIP(hipEventRecord(c->ev_auc_p[0], c->aux_stream));
-  ++c->auc_seq;
+  DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
+  ++c->auc_seq_p[ap];
   hipLaunchKernelGGL(k_split_worker_finalize, dim3(1), dim3(1024), 0, c->stream, loss_part, nb,
                      c->ds, B);
   DFX_HIP(hipGetLastError());

@@ -351,8 +351,8 @@ int train_step(Context* c, const dfx_batch* b, int job_type, int push_cnt, uint6
     if (!(c->diag & 1)) DFX_TRY(auc_finish(AL, B, &c->ds->prog[2], true, c->auc_sort));
     lane_mark(c, 3, c->aux_stream);
     DFX_HIP(hipEventRecord(c->ev_auc, c->aux_stream));  // the lane's latest (syncs join it)
-    ++c->auc_seq;
     DFX_HIP(hipEventRecord(c->ev_auc_p[ap], c->aux_stream));  // this buffer's last reader
+    ++c->auc_seq_p[ap];
     return DFX_OK;
   };
 
